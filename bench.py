@@ -1,0 +1,215 @@
+"""bench.py -- predicted edges/s of the link-prediction hot path on MI355X.
+
+BASELINE.json metric: "predicted edges/sec + F1, LHub Jaccard, 0.1|E| removed,
+1/2/4/8 MI355X".  Workload (N=1): configs[1], the soc-LiveJournal1-shaped
+Chung-Lu stand-in (n = 4,847,571, m = 68,993,773, alpha 0.6, seed 12; SURVEY
+§8(d) C2), symmetrized, 0.1|E| undirected edges deleted, then
+predictLinksJaccardCoefficient<4> with maxEdges = |deletions| / 2
+(main.cxx:50).  A step = one full prediction (score + top-k select + order)
+with the graph resident in HBM; for N > 1 it also includes the RCCL exchange
+and merge.  Scaling is weak: at N GPUs the graph is N x configs[1] (n and m
+scaled) and each rank owns 1/N of the source vertices.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import nlp_loader  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def f1_on_device(out, n, du, dw, span):
+    """main.cxx:48-57,199-206: P = |ins1 ∩ del0| / |ins1|, R = ... / |del0|."""
+    e = out[:n].long()
+    u, v = e[:, 0] & 0xffffffff, e[:, 1] & 0xffffffff
+    ins = torch.unique(torch.cat([u * span + v, v * span + u]))
+    dels = torch.unique(du.long() * span + dw.long())
+    common = int(torch.isin(ins, dels).sum())
+    p = common / max(ins.numel(), 1)
+    r = common / max(dels.numel(), 1)
+    return p, r, (0.0 if p + r == 0 else 2 * p * r / (p + r))
+
+
+def cpu_baseline(off, keys, metric, hub, k, ncand):
+    """The reference's own OpenMP path (oracle/_ref/ref_driver, compiled from
+    /root/reference/inc by oracle/Makefile) on this host's cores, same graph.
+    maxEdges is capped at the candidate count: above it the reference's
+    OpenMP merge reads past its per-thread lists."""
+    drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    metric_id = ["CN", "JAC", "SOR", "SAL", "HPI", "HDI", "LHN", "AA", "RA"].index(metric)
+    me = min(k, ncand) if ncand else k
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "g.csr")
+        with open(path, "wb") as f:
+            np.array([len(off) - 1, len(keys)], np.uint64).tofile(f)
+            off.astype(np.uint64).tofile(f)
+            keys.astype(np.uint32).tofile(f)
+        if os.path.exists(drv):
+            env = dict(os.environ, OMP_NUM_THREADS=str(cores))
+            r = subprocess.run([drv, "time", path, str(metric_id), str(hub), str(me), str(cores), "3"],
+                               capture_output=True, text=True, env=env, timeout=900)
+            if r.returncode == 0:
+                t_ms, ts_ms, n = r.stdout.split()
+                t_ms = float(t_ms)
+                return dict(value=int(n) / (t_ms / 1e3) if t_ms > 0 else None, unit="predicted edges/s",
+                            cores=cores, kind="reference", time_ms=t_ms, scoring_ms=float(ts_ms),
+                            sample="full workload, predictLinks%sOmp<%d> repeat=3, maxEdges=%d"
+                                   % (metric, hub, me))
+    # fallback: the single-threaded C restatement (port)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    t0 = time.perf_counter()
+    u, _, _, _ = pyoracle.predict(off, keys, metric, hub, max_edges=k)
+    dt = time.perf_counter() - t0
+    return dict(value=len(u) / dt, unit="predicted edges/s", cores=1, kind="port", time_ms=dt * 1e3,
+                sample="full workload, oracle/nlp_oracle.c single thread")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2-soc-LiveJournal1")
+    ap.add_argument("--metric", default=None)
+    ap.add_argument("--hub", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    nlp = nlp_loader.load()
+    gg = nlp_loader.load_sub("graphgen")
+    dmod = nlp_loader.load_sub("dist")
+    nlp.lib()
+
+    n, m, alpha, seed, d, metric, hub = gg.CONFIGS[args.config]
+    metric = args.metric or metric
+    hub = hub if args.hub is None else args.hub
+    spec = (n * world, m * world, alpha, seed, d, metric, hub)
+    t0 = time.time()
+    off, keys, du, dw, info = gg.make_workload(spec, "cuda")
+    torch.cuda.synchronize()
+    gen_s = time.time() - t0
+    t0 = time.time()
+    G = nlp.Graph.from_device(off, keys)
+    torch.cuda.synchronize()
+    create_s = time.time() - t0
+    ginfo = G.info()
+    span = ginfo["span"]
+    k = info["k"]
+    stream = torch.cuda.current_stream()
+    out_local = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+    out = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+    mid = nlp.METRICS.index(metric)
+    last = {}
+
+    def step():
+        if world == 1:
+            cnt, t = G.predict_device(mid, hub, k, out, stream=stream)
+            last.update(t)
+            return cnt
+        res, cnt, inf = dmod.predict_sharded(dmod.hip_local_predict(G, mid, hub, k, out_local, stream),
+                                             dmod.hip_merge(G, out, stream), span, k)
+        last.update(inf)
+        return cnt
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # per-phase device time of the library's own events, averaged over the timed steps
+    score_ms = select_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt = step()
+        score_ms += last.get("score_ms", 0.0)
+        select_ms += last.get("select_ms", 0.0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = cnt / (elapsed / args.steps)
+
+    if rank == 0:
+        p, r, f1 = f1_on_device(out, cnt, du, dw, span)
+        score_ms /= args.steps
+        select_ms /= args.steps
+        # Roofline of the scoring phase (path 1), DESIGN.md §4: algorithmic bytes
+        # = degree scan 4*S + transposed offsets 8*(S+1) + in-lists, wedge keys and
+        # candidates; filled from the per-call counters.
+        wedges = int(last.get("wedges", 0))
+        cands = int(last.get("candidates", 0))
+        b_alg = 4 * span + 8 * (span + 1) + 12 * wedges + 16 * cands
+        achieved = b_alg / (score_ms * 1e-3) / 1e9 if score_ms > 0 else None
+        line = {
+            "metric": "predicted edges/sec + F1, LHub Jaccard, 0.1|E| removed",
+            "value": value,
+            "unit": "predicted edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32/f32",
+            "data": "synthetic (Chung-Lu stand-in of %s, generated on device)" % args.config,
+            "config": {"workload": "%s x%d: predictLinks%sOmp<%d>, k=|del|/2" % (args.config, world, metric, hub),
+                       "n": spec[0], "m": spec[1], "alpha": alpha, "M": ginfo["nnz"], "k": k,
+                       "deletion_fraction": d, "parallelism": "source-range shards x%d" % world},
+            "predicted": cnt,
+            "f1": f1, "precision": p, "recall": r,
+            "score_ms": score_ms, "select_ms": select_ms,
+            "wedges": wedges, "candidates": cands, "path": last.get("path"),
+            "graph_gen_s": gen_s, "graph_create_s": create_s,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "kernel": "scoring phase (path 1)"},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(off.cpu().numpy(), keys.cpu().numpy().view(np.uint32), metric,
+                                                    hub, k, cands)
+            except Exception as e:  # report, never hide
+                line["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(line), flush=True)
+    G.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

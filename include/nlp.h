@@ -1,0 +1,151 @@
+/*
+ * nlp.h -- C-ABI of the MI355X (gfx950) neighborhood link-prediction engine
+ * (libnlp.so).  Plain pointers and sizes only; no HIP or torch types.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (/root/reference/inc/predict.hxx).  The reference's entry points are C++
+ * templates called from main.cxx:50:
+ *
+ *   template <int MINDEGREE1=4, int MAXFACTOR2=0, bool FORCEHEAP=false, class G, class W=float>
+ *   auto predictLinks<Metric>Omp(const G& x, const PredictLinkOptions<W>& o={})
+ *       -> PredictLinkResult<typename G::key_type, W>          (predict.hxx:519-831)
+ *
+ * Templates and lambdas cannot cross a C ABI, so the metric becomes an enum
+ * (the nine built-in metrics, predict.hxx:502-831), MINDEGREE1 becomes the
+ * runtime `hub_max_degree` (0 = IHub), PredictLinkOptions{repeat, maxEdges,
+ * minScore} (predict.hxx:33-55) become arguments, and PredictLinkResult
+ * {edges, time, scoringTime} (predict.hxx:65-102) becomes the caller-owned
+ * `out` array plus nlp_timing.  The C++ header include/nlp/predict.hxx
+ * rebuilds the reference's template API on top of these functions.
+ *
+ * Graph input = CSR of the reference's graph concept (Graph.hxx span /
+ * forEachEdgeKey / degree, csr.hxx csrCreateOffsetsW / csrCreateEdgeKeysW):
+ * offsets[span+1] (u64, like DiGraphCsr<..., O=size_t>), keys[nnz] (u32 vertex
+ * ids, each adjacency list sorted ascending; duplicate entries are allowed and
+ * counted, exactly like LazyBitset lists, _bitset.hxx:53,114).  Vertices with no
+ * edges (including the reference's absent vertex 0) simply have empty rows.
+ *
+ * Output order is canonical: score descending, then u ascending, then v
+ * ascending.  The reference's own tie order is thread-schedule dependent
+ * (SURVEY.md Appendix A.1); its score multiset and above-boundary set are
+ * reproduced bit-exactly.  Every output pair has u < v.
+ *
+ * Errors: the reference has none (everything noexcept, bad input is UB).  Every
+ * function here returns an nlp_status and never throws or aborts.
+ */
+#ifndef NLP_H
+#define NLP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  NLP_OK = 0,
+  NLP_ERR_INVALID = 1,    /* bad argument or malformed CSR */
+  NLP_ERR_DEVICE = 2,     /* HIP runtime / kernel failure */
+  NLP_ERR_NOMEM = 3,      /* device or host allocation failed */
+  NLP_ERR_NODEVICE = 4,   /* no usable gfx950 device */
+  NLP_ERR_CAPACITY = 5    /* caller buffer too small (see out_count) */
+} nlp_status;
+
+/* The nine similarity metrics of predict.hxx (enum order = main.cxx:212-220). */
+typedef enum {
+  NLP_CN = 0,   /* predictLinksCommonNeighbors[Omp]           predict.hxx:502,519 */
+  NLP_JAC = 1,  /* predictLinksJaccardCoefficient[Omp]        predict.hxx:540,557 */
+  NLP_SOR = 2,  /* predictLinksSorensenIndex[Omp]             predict.hxx:578,595 */
+  NLP_SAL = 3,  /* predictLinksSaltonCosineSimilarity[Omp]    predict.hxx:616,633 */
+  NLP_HPI = 4,  /* predictLinksHubPromoted[Omp]               predict.hxx:654,671 */
+  NLP_HDI = 5,  /* predictLinksHubDepressed[Omp]              predict.hxx:692,709 */
+  NLP_LHN = 6,  /* predictLinksLeichtHolmeNermanScore[Omp]    predict.hxx:730,747 */
+  NLP_AA = 7,   /* predictLinksAdamicAdarCoefficient[Omp]     predict.hxx:768,786 */
+  NLP_RA = 8    /* predictLinksResourceAllocationScore[Omp]   predict.hxx:808,826 */
+} nlp_metric;
+
+/* One predicted link: PredictLinkResult::edges element tuple<K,K,W>
+ * (predict.hxx:69) with K = uint32_t, W = float. */
+typedef struct {
+  uint32_t u;
+  uint32_t v;
+  float score;
+} nlp_edge;
+
+/* Timing and counters of one predict call.  score_ms / total_ms correspond to
+ * PredictLinkResult::scoringTime / time (predict.hxx:71-73, 466): score_ms is
+ * averaged over `repeat` like measureDuration (_utility.hxx:345-352); select_ms
+ * is the top-k selection + ordering (the reference's merge, predict.hxx:431-460);
+ * copy_ms is the device->host copy of the result (not part of total_ms).  All
+ * from HIP events on the device stream. */
+typedef struct {
+  float score_ms;
+  float select_ms;
+  float total_ms;
+  float copy_ms;
+  uint64_t wedges;          /* (u, v, w) wedges scanned, w > u  (SURVEY §8(d) W_H) */
+  uint64_t candidates;      /* candidates with score > min_score (NaN included) */
+  uint64_t nan_candidates;  /* of which NaN */
+  uint32_t path;            /* 1 = intermediate-centric, 2 = source-centric */
+  uint32_t chunks;          /* source-range chunks used by path 2 */
+} nlp_timing;
+
+typedef struct nlp_graph nlp_graph;
+
+/* Upload a host CSR to `device` (HIP ordinal) and build the graph handle.
+ * Inputs are borrowed for the duration of the call only.  The handle keeps the
+ * CSR, degrees, the transposed adjacency (shared when the graph is symmetric)
+ * and the Adamic-Adar / Resource-Allocation contribution tables resident in
+ * HBM for its lifetime (main.cxx runs 99 predictions per graph). */
+nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint64_t span,
+                            int device, nlp_graph** out);
+
+/* Same, from CSR arrays already resident on `device` (device pointers).  The
+ * arrays are copied; `stream` (hipStream_t or NULL) orders the copy. */
+nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_keys, uint64_t span,
+                                   uint64_t nnz, int device, void* stream, nlp_graph** out);
+
+void nlp_graph_destroy(nlp_graph* g);
+
+/* Graph properties: span (S), nnz (M), maximum degree, symmetric flag. */
+nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uint32_t* max_degree,
+                          int* symmetric);
+
+/* predictLinks<Metric>Omp<hub_max_degree>(G, {repeat, max_edges, min_score}).
+ * `out` is a caller-owned HOST array of at least max_edges entries (it may be
+ * NULL when max_edges == 0).  *out_count receives the number of predicted
+ * links (< max_edges when there are fewer candidates; the reference's
+ * OpenMP merge reads out of bounds in that case).
+ * max_edges = UINT64_MAX means "all candidates" (then `out` must hold them:
+ * query the count first with max_edges = 0 -> t->candidates). */
+nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
+                       uint64_t max_edges, int repeat, nlp_edge* out, uint64_t* out_count,
+                       nlp_timing* t);
+
+/* Device-resident variant for a source-vertex range [u_begin, u_end) (the
+ * multi-GPU shard; pass 0, UINT64_MAX for all).  `d_out` is a DEVICE array of
+ * at least max_edges entries; `stream` is a hipStream_t (NULL = the graph's
+ * own stream).  The call is synchronous with respect to the host: on return
+ * d_out and *out_count are valid. */
+nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
+                              uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
+                              uint64_t* out_count, nlp_timing* t, void* stream);
+
+/* Merge step of the multi-GPU path: given `n` device-resident edges that are the
+ * concatenation, in ascending source-range order, of per-shard canonical
+ * results, write the canonical global top max_edges into d_out (device).
+ * Stable: equal scores keep input order, which is (u asc, v asc) across shards. */
+nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,
+                                   nlp_edge* d_out, uint64_t* out_count, void* stream);
+
+const char* nlp_status_string(nlp_status s);
+const char* nlp_metric_name(nlp_metric m);
+
+/* Library version (major*10000 + minor*100 + patch). */
+int nlp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NLP_H */

@@ -1,0 +1,247 @@
+"""nlp_amd -- MI355X-native neighborhood link prediction (host binding).
+
+Python mirror of the reference's predict.hxx API over the C-ABI of
+include/nlp.h (libnlp.so, HIP/gfx950).  The C++ mirror for main.cxx-style
+callers is include/nlp/predict.hxx; this module serves the tests, bench.py and
+the multi-GPU driver (dist.py).
+
+Reference names (/root/reference/inc/predict.hxx):
+    PredictLinkOptions{repeat, maxEdges, minScore}          predict.hxx:33-55
+    PredictLinkResult{edges, time, scoringTime}             predict.hxx:65-102
+    predictLinks<Metric>Omp<MINDEGREE1>(x, o)               predict.hxx:519-831
+Here: predictLinks<Metric>Hip(graph, o, mindegree1=4) with the same meaning.
+
+There is no CPU fallback: without libnlp.so or a gfx950 device every call
+raises NlpError (the oracle under oracle/ is test infrastructure only).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import build as _build
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnlp.so")
+
+CN, JAC, SOR, SAL, HPI, HDI, LHN, AA, RA = range(9)
+METRICS = ["CN", "JAC", "SOR", "SAL", "HPI", "HDI", "LHN", "AA", "RA"]
+METRIC_FUNCS = [
+    "CommonNeighbors", "JaccardCoefficient", "SorensenIndex", "SaltonCosineSimilarity",
+    "HubPromoted", "HubDepressed", "LeichtHolmeNermanScore", "AdamicAdarCoefficient",
+    "ResourceAllocationScore",
+]
+STATUS = {0: "ok", 1: "invalid argument", 2: "HIP device error", 3: "out of memory",
+          4: "no gfx950 device", 5: "output buffer too small"}
+UINT64_MAX = (1 << 64) - 1
+
+EDGE_DTYPE = np.dtype([("u", "<u4"), ("v", "<u4"), ("score", "<f4")])
+
+
+class NlpError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__("%s: %s" % (what or "libnlp", STATUS.get(status, "status %d" % status)))
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("score_ms", ctypes.c_float), ("select_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+                ("copy_ms", ctypes.c_float), ("wedges", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
+                ("nan_candidates", ctypes.c_uint64), ("path", ctypes.c_uint32), ("chunks", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+EXPORTS = [
+    "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
+    "nlp_predict_device", "nlp_select_edges_device", "nlp_status_string", "nlp_metric_name", "nlp_version",
+]
+
+_lib = None
+
+
+def lib(build_if_missing=True):
+    """Load libnlp.so (building it first when it is missing and hipcc exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH) and build_if_missing:
+        _build.build()
+    if not os.path.exists(LIB_PATH):
+        raise NlpError(4, "libnlp.so missing (run neighborhood-link-prediction-openmp_amd/build.py)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, f32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_int
+    P = ctypes.POINTER
+    L.nlp_graph_create.argtypes = [vp, vp, u64, i32, P(vp)]
+    L.nlp_graph_create_device.argtypes = [vp, vp, u64, u64, i32, vp, P(vp)]
+    L.nlp_graph_destroy.argtypes = [vp]
+    L.nlp_graph_destroy.restype = None
+    L.nlp_graph_info.argtypes = [vp, P(u64), P(u64), P(u32), P(i32)]
+    L.nlp_predict.argtypes = [vp, i32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
+    L.nlp_predict_device.argtypes = [vp, i32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
+    L.nlp_select_edges_device.argtypes = [vp, vp, u64, u64, vp, P(u64), vp]
+    L.nlp_status_string.argtypes = [i32]
+    L.nlp_status_string.restype = ctypes.c_char_p
+    L.nlp_metric_name.argtypes = [i32]
+    L.nlp_metric_name.restype = ctypes.c_char_p
+    L.nlp_version.restype = i32
+    for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict",
+              "nlp_predict_device", "nlp_select_edges_device"):
+        getattr(L, f).restype = i32
+    _lib = L
+    return L
+
+
+def _check(status, what):
+    if status != 0:
+        raise NlpError(status, what)
+
+
+def _metric(m):
+    if isinstance(m, str):
+        return METRICS.index(m)
+    if not 0 <= int(m) <= 8:
+        raise ValueError("metric out of range")
+    return int(m)
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return getattr(stream, "cuda_stream", stream)
+
+
+class PredictLinkOptions:
+    """predict.hxx:33-55: repeat [1], maxEdges [-1 = all], minScore [0]."""
+
+    def __init__(self, repeat=1, maxEdges=-1, minScore=0.0):
+        self.repeat = int(repeat)
+        self.maxEdges = int(maxEdges)
+        self.minScore = float(minScore)
+
+
+class PredictLinkResult:
+    """predict.hxx:65-102: edges [(u, v, score)] by score desc, time / scoringTime in ms."""
+
+    def __init__(self, edges, time=0.0, scoringTime=0.0, timing=None):
+        self.edges = edges
+        self.time = time
+        self.scoringTime = scoringTime
+        self.timing = timing or {}
+
+
+class Graph:
+    """A CSR graph resident in HBM (nlp_graph handle).
+
+    offsets: u64[span+1], keys: u32[nnz]; rows sorted ascending, duplicates
+    allowed (the reference's LazyBitset multiset semantics)."""
+
+    def __init__(self, offsets, keys, device=0):
+        L = lib()
+        self._off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self._keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        span = len(self._off) - 1
+        h = ctypes.c_void_p()
+        _check(L.nlp_graph_create(self._off.ctypes.data, self._keys.ctypes.data if len(self._keys) else None,
+                                  span, int(device), ctypes.byref(h)), "nlp_graph_create")
+        self._h = h
+        self.device = int(device)
+        del self._off, self._keys
+
+    @classmethod
+    def from_device(cls, offsets, keys, device=None, stream=None):
+        """From torch tensors already on the GPU (int64 offsets, int32 keys)."""
+        L = lib()
+        g = cls.__new__(cls)
+        dev = offsets.device.index if device is None else device
+        span = offsets.numel() - 1
+        h = ctypes.c_void_p()
+        _check(L.nlp_graph_create_device(offsets.data_ptr(), keys.data_ptr() if keys.numel() else None, span,
+                                         keys.numel(), int(dev or 0), _stream_ptr(stream), ctypes.byref(h)),
+               "nlp_graph_create_device")
+        g._h = h
+        g.device = int(dev or 0)
+        return g
+
+    def info(self):
+        s, m, d, y = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_int()
+        _check(lib().nlp_graph_info(self._h, ctypes.byref(s), ctypes.byref(m), ctypes.byref(d), ctypes.byref(y)),
+               "nlp_graph_info")
+        return dict(span=s.value, nnz=m.value, max_degree=d.value, symmetric=bool(y.value))
+
+    def predict(self, metric, hub, max_edges=None, min_score=0.0, repeat=1):
+        """Host-output predict: returns (u, v, score) numpy arrays and the timing dict."""
+        L = lib()
+        m = _metric(metric)
+        me = UINT64_MAX if max_edges is None or max_edges < 0 else int(max_edges)
+        t = Timing()
+        cnt = ctypes.c_uint64()
+        if me == UINT64_MAX:
+            # count first (out = NULL), then fetch
+            _check(L.nlp_predict(self._h, m, int(hub), float(min_score), me, int(repeat), None,
+                                 ctypes.byref(cnt), ctypes.byref(t)), "nlp_predict")
+            me = cnt.value
+        out = np.zeros(max(me, 1), dtype=EDGE_DTYPE)
+        _check(L.nlp_predict(self._h, m, int(hub), float(min_score), me, int(repeat), out.ctypes.data if me else None,
+                             ctypes.byref(cnt), ctypes.byref(t)), "nlp_predict")
+        n = cnt.value
+        out = out[:n]
+        return out["u"].copy(), out["v"].copy(), out["score"].copy(), t.as_dict()
+
+    def predict_device(self, metric, hub, max_edges, out, u_begin=0, u_end=UINT64_MAX, min_score=0.0, stream=None):
+        """Device-output predict into `out` (torch int32 [>= max_edges, 3]).  Returns (count, timing)."""
+        if out.numel() < 3 * max_edges or out.element_size() * out.numel() < 12 * max_edges:
+            raise ValueError("output tensor too small")
+        t = Timing()
+        cnt = ctypes.c_uint64()
+        _check(lib().nlp_predict_device(self._h, _metric(metric), int(hub), float(min_score), int(max_edges),
+                                        int(u_begin), int(u_end), out.data_ptr(), ctypes.byref(cnt),
+                                        ctypes.byref(t), _stream_ptr(stream)), "nlp_predict_device")
+        return cnt.value, t.as_dict()
+
+    def select_edges_device(self, edges_in, n, max_edges, out, stream=None):
+        cnt = ctypes.c_uint64()
+        _check(lib().nlp_select_edges_device(self._h, edges_in.data_ptr(), int(n), int(max_edges), out.data_ptr(),
+                                             ctypes.byref(cnt), _stream_ptr(stream)), "nlp_select_edges_device")
+        return cnt.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nlp_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def _make_predictor(metric):
+    def fn(x, o=None, mindegree1=4):
+        o = o or PredictLinkOptions()
+        u, v, s, t = x.predict(metric, mindegree1, None if o.maxEdges < 0 else o.maxEdges, o.minScore, o.repeat)
+        edges = list(zip(u.tolist(), v.tolist(), s.tolist()))
+        return PredictLinkResult(edges, t["total_ms"], t["score_ms"], t)
+    fn.__name__ = "predictLinks%sHip" % METRIC_FUNCS[metric]
+    fn.__doc__ = ("predictLinks%sOmp<MINDEGREE1>(x, o) of predict.hxx on the GPU (mindegree1=0 -> IHub)."
+                  % METRIC_FUNCS[metric])
+    return fn
+
+
+for _m, _name in enumerate(METRIC_FUNCS):
+    globals()["predictLinks%sHip" % _name] = _make_predictor(_m)
+del _m, _name
+
+
+def edges_from_tensor(t, n):
+    """Split a device edge tensor (int32 [cap, 3]) into numpy u, v, score."""
+    a = t[:n].cpu().numpy()
+    return a[:, 0].view(np.uint32).copy(), a[:, 1].view(np.uint32).copy(), a[:, 2].view(np.float32).copy()

@@ -1,0 +1,53 @@
+"""Build libnlp.so (gfx950) in-tree.
+
+    python neighborhood-link-prediction-openmp_amd/build.py
+
+hipcc cross-compiles for gfx950 without a GPU.  Floating-point flags matter for
+parity: no fast-math, no FP contraction, correctly rounded fp32 division (the
+reference's scores are IEEE float divisions on x86-64, predict.hxx:542-749).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libnlp.so")
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("nlp.hip",)]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("prims.hpp", "kernels.hpp")] + \
+    [os.path.join(ROOT, "include", "nlp.h")]
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math",
+    "-Wall", "-Wno-unused-function",
+]
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    return "hipcc"
+
+
+def needs_build():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+
+
+def build(force=False, verbose=True):
+    if not force and not needs_build():
+        return LIB
+    cmd = [hipcc()] + HIPCC_FLAGS + SOURCES + ["-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

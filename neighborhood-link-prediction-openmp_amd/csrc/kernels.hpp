@@ -1,0 +1,339 @@
+// kernels.hpp -- the link-prediction hot path on gfx950.
+//
+// Reference: /root/reference/inc/predict.hxx.  The reference scans, per source
+// vertex u (predict.hxx:287-288), every first-hop neighbour v (hub filter
+// deg(v) > MINDEGREE1 skips, predict.hxx:298-301), every second-hop w > u
+// (predict.hxx:153-179, ft 292-296), accumulating a per-thread dense counter,
+// zeroes u and N(u) (306-307) and scores each touched w (309-311).
+//
+// Here the same multiset of wedges (u, v, w) is materialised as 64-bit keys
+// (u << 32 | w) in an order in which, for every (u, w), the wedges appear with
+// v ascending (= the reference's position order in the sorted list N(u)); a
+// STABLE radix sort groups them by (u, w) and a segmented pass produces the
+// count (basic metrics) or the sequential float accumulation (AA/RA) exactly
+// as the reference computes it.  Two generators:
+//   path 1 (intermediate-centric, LHub): for v with 0 < deg(v) <= H, for u in
+//          the transposed list I(v), the w in N(v) with w > u;
+//   path 2 (source-centric, any H, chunked by source range): for u, for v in
+//          N(u) surviving the hub filter, the w in N(v) with w > u.
+#pragma once
+#include "prims.hpp"
+
+namespace nlp {
+
+enum { M_CN = 0, M_JAC, M_SOR, M_SAL, M_HPI, M_HDI, M_LHN, M_AA, M_RA };
+
+__device__ __forceinline__ uint32_t score_key(float s) {
+  if (s != s) return 0u;            // NaN ranks last (nlp_oracle.c nlpo_score_key)
+  if (s == 0.0f) s = 0.0f;          // -0 == +0
+  uint32_t b = __float_as_uint(s);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// Basic-metric scores, predict.hxx:504-749.  Degrees are size_t in the
+// reference (Graph.hxx:167) -> u64 here, counts are K = uint32_t.
+__device__ __forceinline__ float score_basic(int m, uint32_t c, uint64_t du, uint64_t dw) {
+  const float fc = (float)c;
+  switch (m) {
+    case M_CN: return fc;
+    case M_JAC: return fc / (float)(du + dw - (uint64_t)c);   // size_t wrap kept
+    case M_SOR: return fc / (float)(du + dw);
+    case M_SAL: return (float)((double)fc / sqrt((double)(du * dw)));
+    case M_HPI: return fc / (float)(du < dw ? du : dw);
+    case M_HDI: return fc / (float)(du < dw ? dw : du);
+    case M_LHN: return fc / (float)(du * dw);
+  }
+  return 0.0f;
+}
+
+// number of entries <= x in the sorted list a[0..n)
+__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ bool contains_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo < n && a[lo] == x;
+}
+
+// ---------------------------------------------------------------- graph build
+__global__ void k_degrees(const uint64_t* __restrict__ off, uint64_t span, uint32_t* __restrict__ deg,
+                          uint32_t* __restrict__ maxdeg, uint32_t* __restrict__ bad) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < span; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t a = off[u], b = off[u + 1];
+    if (b < a) { atomicOr(bad, 1u); deg[u] = 0; continue; }
+    uint64_t d = b - a;
+    if (d > 0xffffffffull) { atomicOr(bad, 2u); d = 0xffffffffull; }
+    deg[u] = (uint32_t)d;
+    atomicMax(maxdeg, (uint32_t)d);
+  }
+}
+
+// keys must be < span and sorted ascending inside each row
+__global__ void k_check_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
+                             uint64_t nnz, uint32_t* __restrict__ bad) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t k = keys[e];
+    if (k >= span) atomicOr(bad, 4u);
+    if (e + 1 < nnz && keys[e + 1] < k) {
+      // a descent is only legal at a row boundary
+      uint64_t u = lbs_find(off, span + 1, e);
+      if (off[u + 1] != e + 1) atomicOr(bad, 8u);
+    }
+  }
+}
+
+__global__ void k_count_cols(const uint32_t* __restrict__ keys, uint64_t nnz, uint32_t* __restrict__ tdeg) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&tdeg[keys[e]], 1u);
+}
+
+// (v << 32 | u) for every edge u -> v; row u found by binary search on offsets
+__global__ void k_transpose_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
+                                 uint64_t nnz, uint64_t* __restrict__ out) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t u = lbs_find(off, span + 1, e);
+    out[e] = ((uint64_t)keys[e] << 32) | u;
+  }
+}
+
+__global__ void k_low32(const uint64_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ out) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x)
+    out[e] = (uint32_t)in[e];
+}
+
+__global__ void k_diff_u64(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint64_t n, uint32_t* __restrict__ flag) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x)
+    if (a[e] != b[e]) { *flag = 1u; return; }
+}
+
+__global__ void k_diff_u32(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint64_t n, uint32_t* __restrict__ flag) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x)
+    if (a[e] != b[e]) { *flag = 1u; return; }
+}
+
+// ---------------------------------------------------------------- path 1: intermediate-centric
+// c[v] = |I(v)| if v survives the hub filter (0 < deg v <= H), else 0.
+__global__ void k_p1_vcount(const uint32_t* __restrict__ deg, const uint64_t* __restrict__ toff, uint64_t span,
+                            uint32_t H, uint32_t* __restrict__ c) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < span; v += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t d = deg[v];
+    c[v] = (d > 0 && d <= H) ? (uint32_t)(toff[v + 1] - toff[v]) : 0u;
+  }
+}
+
+// One thread per in-edge slot e (v from the scanned per-v counts).
+// ewc[e] = #{w in N(v) : w > u} if u in [ua, ub) else 0; efirst[e] = index in N(v)
+// of the first such w.
+__global__ void k_p1_inedges(const uint64_t* __restrict__ ioff, uint64_t span, const uint64_t* __restrict__ d_E,
+                             const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tkeys,
+                             const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                             const uint32_t* __restrict__ deg, uint64_t ua, uint64_t ub,
+                             uint32_t* __restrict__ ev, uint32_t* __restrict__ eu, uint32_t* __restrict__ ewc,
+                             uint32_t* __restrict__ efirst) {
+  const uint64_t E = *d_E;
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t v = lbs_find(ioff, span, e);
+    uint32_t u = tkeys[toff[v] + (e - ioff[v])];
+    uint32_t d = deg[v];
+    uint32_t first = upper_bound_u32(keys + off[v], d, u);
+    ev[e] = (uint32_t)v;
+    eu[e] = u;
+    efirst[e] = first;
+    ewc[e] = (u >= ua && u < ub) ? d - first : 0u;
+  }
+}
+
+// ---------------------------------------------------------------- path 2: source-centric
+// One thread per edge e in [e0, e1) (relative index e - e0).
+__global__ void k_p2_edges(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                           const uint32_t* __restrict__ deg, uint64_t span, uint64_t e0, uint64_t e1, uint32_t H,
+                           uint32_t* __restrict__ ev, uint32_t* __restrict__ eu, uint32_t* __restrict__ ewc,
+                           uint32_t* __restrict__ efirst) {
+  const uint64_t n = e1 - e0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t e = e0 + i;
+    uint32_t u = (uint32_t)lbs_find(off, span + 1, e);
+    uint32_t v = keys[e];
+    uint32_t d = deg[v];
+    bool surv = (H == 0) || (d <= H);                     // predict.hxx:301
+    uint32_t first = surv ? upper_bound_u32(keys + off[v], d, u) : d;
+    ev[i] = v;
+    eu[i] = u;
+    efirst[i] = first;
+    ewc[i] = d - first;
+  }
+}
+
+// Running maximum edge index whose wedge offset is <= target (for chunking).
+__global__ void k_find_chunk_end(const uint64_t* __restrict__ woff, uint64_t E, uint64_t target,
+                                 uint64_t* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t lo = 0, hi = E;  // first e with woff[e] > target
+    while (lo < hi) {
+      uint64_t mid = (lo + hi) >> 1;
+      if (woff[mid] <= target) lo = mid + 1; else hi = mid;
+    }
+    *out = lo;
+  }
+}
+
+// ---------------------------------------------------------------- common: wedge materialisation
+// One thread per wedge slot i < W; slot order = (edge slot, w index) so the
+// generator's order is preserved.  val = deg(v) for AA/RA (contribution table).
+template <bool VAL>
+__global__ void k_wedges(const uint64_t* __restrict__ woff, uint64_t E, const uint64_t* __restrict__ d_W,
+                         uint64_t wbase, const uint32_t* __restrict__ ev, const uint32_t* __restrict__ eu,
+                         const uint32_t* __restrict__ efirst, const uint64_t* __restrict__ off,
+                         const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg,
+                         uint64_t* __restrict__ wkey, uint32_t* __restrict__ wval) {
+  const uint64_t W = *d_W - wbase;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < W; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s = wbase + i;
+    uint64_t e = lbs_find(woff, E, s);
+    uint32_t v = ev[e];
+    uint32_t w = keys[off[v] + efirst[e] + (s - woff[e])];
+    wkey[i] = ((uint64_t)eu[e] << 32) | w;
+    if (VAL) wval[i] = deg[v];
+  }
+}
+
+__global__ void k_run_flags(const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ flag) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    flag[i] = (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_run_starts(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ rid, uint64_t n,
+                             uint64_t* __restrict__ rstart, const uint64_t* __restrict__ d_R) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[i]) rstart[rid[i]] = i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) rstart[*d_R] = n;
+}
+
+// One thread per candidate run: count / ordered accumulation, first-order
+// exclusion (predict.hxx:306-307), score (fs), score <= minScore filter (311).
+template <bool CUSTOM>
+__global__ void k_score(const uint64_t* __restrict__ rstart, const uint64_t* __restrict__ d_R,
+                        const uint64_t* __restrict__ wkey, const uint32_t* __restrict__ wval,
+                        const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                        const uint32_t* __restrict__ deg, const double* __restrict__ ctab, int metric,
+                        float min_score, uint32_t* __restrict__ ckey, uint32_t* __restrict__ cu,
+                        uint32_t* __restrict__ cw, float* __restrict__ cs, uint32_t* __restrict__ cflag) {
+  const uint64_t R = *d_R;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s = rstart[r], e = rstart[r + 1];
+    uint64_t k = wkey[s];
+    uint32_t u = (uint32_t)(k >> 32), w = (uint32_t)k;
+    bool excl = contains_u32(keys + off[u], deg[u], w);
+    float sc;
+    if (CUSTOM) {
+      float acc = 0.0f;  // entry += 1.0/log(deg v) | 1.0/deg v, in v order
+      if (!excl)
+        for (uint64_t i = s; i < e; ++i) acc = (float)((double)acc + ctab[wval[i]]);
+      sc = acc;
+    } else {
+      uint32_t c = excl ? 0u : (uint32_t)(e - s);
+      sc = score_basic(metric, c, deg[u], deg[w]);
+    }
+    bool keep = !(sc <= min_score);
+    ckey[r] = score_key(sc);
+    cu[r] = u;
+    cw[r] = w;
+    cs[r] = sc;
+    cflag[r] = keep ? 1u : 0u;
+  }
+}
+
+// Compact flagged candidates to base + pos.
+__global__ void k_compact_cands(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ pos,
+                                const uint64_t* __restrict__ d_n, const uint32_t* __restrict__ ikey,
+                                const uint32_t* __restrict__ iu, const uint32_t* __restrict__ iw,
+                                const float* __restrict__ is, uint64_t base, uint32_t* __restrict__ okey,
+                                uint32_t* __restrict__ ou, uint32_t* __restrict__ ow, float* __restrict__ os) {
+  const uint64_t n = *d_n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (flag[i]) {
+      uint64_t p = base + pos[i];
+      okey[p] = ikey[i];
+      ou[p] = iu[i];
+      ow[p] = iw[i];
+      os[p] = is[i];
+    }
+  }
+}
+
+__global__ void k_count_key0(const uint32_t* __restrict__ key, uint64_t n, unsigned long long* __restrict__ cnt) {
+  uint32_t c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    c += key[i] == 0u;
+  if (c) atomicAdd(cnt, (unsigned long long)c);
+}
+
+// ---------------------------------------------------------------- selection
+// tie[i] = key == kth
+__global__ void k_tie_flags(const uint32_t* __restrict__ key, uint64_t n, const uint64_t* __restrict__ sel,
+                            uint32_t* __restrict__ tie) {
+  const uint32_t kth = (uint32_t)sel[3];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    tie[i] = key[i] == kth ? 1u : 0u;
+}
+
+// keep = key > kth, or a tie whose rank (in input order) is < quota.
+__global__ void k_keep_flags(const uint32_t* __restrict__ key, uint64_t n, const uint64_t* __restrict__ sel,
+                             const uint64_t* __restrict__ trank, uint32_t* __restrict__ keep) {
+  const uint32_t kth = (uint32_t)sel[3];
+  const uint64_t quota = sel[1];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t k = key[i];
+    keep[i] = (k > kth || (k == kth && trank[i] < quota)) ? 1u : 0u;
+  }
+}
+
+// 64-bit sort keys for a descending stable sort of u32 keys: ~key.
+__global__ void k_desc_keys(const uint32_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ k64,
+                            uint32_t* __restrict__ idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    k64[i] = (uint64_t)(~key[i]);
+    idx[i] = (uint32_t)i;
+  }
+}
+
+struct EdgeOut {
+  uint32_t u, v;
+  float score;
+};
+
+__global__ void k_gather_edges(const uint32_t* __restrict__ idx, uint64_t n, const uint32_t* __restrict__ cu,
+                               const uint32_t* __restrict__ cw, const float* __restrict__ cs,
+                               EdgeOut* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t j = idx[i];
+    EdgeOut o;
+    o.u = cu[j];
+    o.v = cw[j];
+    o.score = cs[j];
+    out[i] = o;
+  }
+}
+
+__global__ void k_split_edges(const EdgeOut* __restrict__ in, uint64_t n, uint32_t* __restrict__ ckey,
+                              uint32_t* __restrict__ cu, uint32_t* __restrict__ cw, float* __restrict__ cs) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    EdgeOut e = in[i];
+    ckey[i] = score_key(e.score);
+    cu[i] = e.u;
+    cw[i] = e.v;
+    cs[i] = e.score;
+  }
+}
+
+}  // namespace nlp

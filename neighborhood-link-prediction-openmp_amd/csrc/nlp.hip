@@ -1,0 +1,837 @@
+// nlp.hip -- libnlp.so: graph handle, predict pipeline and the C-ABI of include/nlp.h.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -fPIC -shared (see build.py).  The
+// product path is HIP only: there is no CPU fallback; without a gfx950 device
+// every entry point returns NLP_ERR_NODEVICE.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <math.h>
+#include <new>
+#include <vector>
+#include <algorithm>
+
+#include "../../include/nlp.h"
+#include "prims.hpp"
+#include "kernels.hpp"
+
+using namespace nlp;
+
+namespace {
+
+constexpr int GRID_CAP = 4096;  // grid-stride kernels: at most 4096 x 256 threads
+
+inline unsigned grid_for(uint64_t n) {
+  uint64_t g = (n + NT - 1) / NT;
+  if (g < 1) g = 1;
+  if (g > GRID_CAP) g = GRID_CAP;
+  return (unsigned)g;
+}
+
+#define LAUNCH(kern, n, st, ...) hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(NT), 0, st, __VA_ARGS__)
+
+// Buffer ids of the per-graph workspace.
+enum Buf {
+  B_C32, B_IOFF, B_EV, B_EU, B_EWC, B_EFIRST, B_WOFF,
+  B_WKEY0, B_WKEY1, B_WVAL0, B_WVAL1, B_RFLAG, B_RID, B_RSTART,
+  B_RKEY, B_RU, B_RW, B_RS, B_RFL, B_RPOS,
+  B_CKEY, B_CU, B_CW, B_CS,           // candidate buffer (appended per chunk)
+  B_TKEY, B_TU, B_TW, B_TS,           // compaction target
+  B_TIE, B_TRANK, B_KEEP, B_KPOS,
+  B_SK0, B_SK1, B_SV0, B_SV1,         // final sort
+  B_HIST, B_HOFF, B_SCAN, B_SCAN2, B_SELHIST, B_SEL, B_CNT, B_EDGES,
+  NBUF
+};
+
+struct Workspace {
+  void* p[NBUF] = {};
+  size_t bytes[NBUF] = {};
+  hipError_t get(int id, size_t need, void** out) {
+    if (need == 0) need = 16;
+    if (bytes[id] < need) {
+      if (p[id]) {
+        hipError_t e = hipFree(p[id]);
+        if (e != hipSuccess) return e;
+        p[id] = nullptr;
+        bytes[id] = 0;
+      }
+      size_t nb = std::max(need, bytes[id] + bytes[id] / 2);
+      nb = (nb + 255) & ~(size_t)255;
+      hipError_t e = hipMalloc(&p[id], nb);
+      if (e != hipSuccess) { p[id] = nullptr; return e; }
+      bytes[id] = nb;
+    }
+    *out = p[id];
+    return hipSuccess;
+  }
+  void release() {
+    for (int i = 0; i < NBUF; ++i) {
+      if (p[i]) (void)hipFree(p[i]);
+      p[i] = nullptr;
+      bytes[i] = 0;
+    }
+  }
+};
+
+template <typename T>
+hipError_t wsget(Workspace& ws, int id, uint64_t count, T** out) {
+  void* p;
+  hipError_t e = ws.get(id, (size_t)count * sizeof(T), &p);
+  *out = (T*)p;
+  return e;
+}
+
+}  // namespace
+
+struct nlp_graph {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t span = 0, nnz = 0;
+  uint64_t* off = nullptr;
+  uint32_t* keys = nullptr;
+  uint32_t* deg = nullptr;
+  uint64_t* toff = nullptr;   // transposed CSR (== off/keys when symmetric)
+  uint32_t* tkeys = nullptr;
+  bool symmetric = true;
+  uint32_t maxdeg = 0;
+  double* ctab_aa = nullptr;  // 1.0 / log((double)d), d = 0..maxdeg  (predict.hxx:788)
+  double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
+  uint64_t* host_small = nullptr;  // pinned counters
+  hipEvent_t ev[4] = {};
+  Workspace ws;
+  uint64_t wedge_budget = 0;
+};
+
+namespace {
+
+nlp_status from_hip(hipError_t e) {
+  if (e == hipSuccess) return NLP_OK;
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return NLP_ERR_NOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return NLP_ERR_NODEVICE;
+  return NLP_ERR_DEVICE;
+}
+
+#define TRY(x)                                   \
+  do {                                           \
+    hipError_t e__ = (x);                        \
+    if (e__ != hipSuccess) return from_hip(e__); \
+  } while (0)
+
+nlp_status check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return NLP_ERR_NODEVICE;
+  if (device < 0 || device >= n) return NLP_ERR_INVALID;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return NLP_ERR_NODEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NLP_ERR_NODEVICE;
+  return NLP_OK;
+}
+
+// read `n` u64 device words into pinned host memory and wait
+hipError_t read_small(nlp_graph* g, const uint64_t* d, int n, hipStream_t st) {
+  hipError_t e = hipMemcpyAsync(g->host_small, d, 8 * n, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(st);
+}
+
+void destroy_graph(nlp_graph* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  g->ws.release();
+  if (!g->symmetric) {
+    if (g->toff) (void)hipFree(g->toff);
+    if (g->tkeys) (void)hipFree(g->tkeys);
+  }
+  if (g->off) (void)hipFree(g->off);
+  if (g->keys) (void)hipFree(g->keys);
+  if (g->deg) (void)hipFree(g->deg);
+  if (g->ctab_aa) (void)hipFree(g->ctab_aa);
+  if (g->ctab_ra) (void)hipFree(g->ctab_ra);
+  for (int i = 0; i < 4; ++i)
+    if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
+  if (g->host_small) (void)hipHostFree(g->host_small);
+  if (g->stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+}
+
+int bits_for(uint64_t maxval) {  // bits needed to represent values <= maxval
+  int b = 0;
+  while (b < 64 && (maxval >> b)) ++b;
+  return b;
+}
+
+// Build everything derived from off/keys (already on the device).
+nlp_status finish_graph(nlp_graph* g) {
+  hipStream_t st = g->stream;
+  const uint64_t S = g->span, M = g->nnz;
+  uint32_t* flags;  // [0] bad, [1] maxdeg, [2] asym
+  TRY(wsget(g->ws, B_CNT, 8, &flags));
+  TRY(hipMemsetAsync(flags, 0, 32, st));
+  TRY(hipMalloc(&g->deg, std::max<uint64_t>(S, 1) * 4));
+  LAUNCH(k_degrees, S, st, g->off, S, g->deg, flags + 1, flags);
+  TRY(hipGetLastError());
+  if (M) {
+    LAUNCH(k_check_keys, M, st, g->off, g->keys, S, M, flags);
+    TRY(hipGetLastError());
+  }
+  TRY(hipMemcpyAsync(g->host_small, flags, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  uint32_t hf[2];
+  memcpy(hf, g->host_small, 8);
+  if (hf[0]) return NLP_ERR_INVALID;
+  g->maxdeg = hf[1];
+  // the offsets must also start at 0 and end at nnz
+  uint64_t ends[2];
+  TRY(hipMemcpy(&ends[0], g->off, 8, hipMemcpyDeviceToHost));
+  TRY(hipMemcpy(&ends[1], g->off + S, 8, hipMemcpyDeviceToHost));
+  if (ends[0] != 0 || ends[1] != M) return NLP_ERR_INVALID;
+
+  // Transposed adjacency I(v): stable radix sort of (v << 32 | u).
+  g->symmetric = true;
+  g->toff = g->off;
+  g->tkeys = g->keys;
+  if (M) {
+    uint64_t *k0, *k1, *scan, *hoff;
+    uint32_t *tdeg, *hist;
+    TRY(wsget(g->ws, B_WKEY0, M, &k0));
+    TRY(wsget(g->ws, B_WKEY1, M, &k1));
+    uint64_t nb = rs_blocks(M);
+    TRY(wsget(g->ws, B_HIST, RS_BINS * nb, &hist));
+    TRY(wsget(g->ws, B_HOFF, RS_BINS * nb, &hoff));
+    TRY(wsget(g->ws, B_SCAN, scan_scratch_words(std::max<uint64_t>(RS_BINS * nb, S + 1)) + 16, &scan));
+    TRY(wsget(g->ws, B_C32, S + 1, &tdeg));
+    uint64_t* toff;
+    uint32_t* tkeys;
+    TRY(hipMalloc(&toff, (S + 1) * 8));
+    TRY(hipMalloc(&tkeys, M * 4));
+    TRY(hipMemsetAsync(tdeg, 0, (S + 1) * 4, st));
+    LAUNCH(k_count_cols, M, st, g->keys, M, tdeg);
+    TRY(hipGetLastError());
+    TRY(scan_excl_u64<uint32_t>(tdeg, S + 1, toff, nullptr, scan, st));
+    LAUNCH(k_transpose_keys, M, st, g->off, g->keys, S, M, k0);
+    TRY(hipGetLastError());
+    int vb = bits_for(S - 1);
+    int shifts[8], np = 0;
+    for (int b = 0; b < vb; b += 8) shifts[np++] = b;            // u bytes (low word)
+    for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;       // v bytes (high word)
+    SortScratch sc{hist, hoff, scan, nb};
+    int which = 0;
+    TRY(sort_pairs_u64(k0, nullptr, k1, nullptr, M, shifts, np, sc, &which, st));
+    LAUNCH(k_low32, M, st, which ? k1 : k0, M, tkeys);
+    TRY(hipGetLastError());
+    LAUNCH(k_diff_u64, S + 1, st, toff, g->off, S + 1, flags + 2);
+    LAUNCH(k_diff_u32, M, st, tkeys, g->keys, M, flags + 2);
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(g->host_small, flags + 2, 4, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    uint32_t asym;
+    memcpy(&asym, g->host_small, 4);
+    if (asym) {
+      g->symmetric = false;
+      g->toff = toff;
+      g->tkeys = tkeys;
+    } else {
+      TRY(hipFree(toff));
+      TRY(hipFree(tkeys));
+    }
+  }
+  // AA / RA contribution tables, computed on the host with the same libm the
+  // reference uses (glibc log), indexed by degree.
+  std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
+  for (uint64_t d = 0; d <= g->maxdeg; ++d) {
+    aa[d] = 1.0 / log((double)d);
+    ra[d] = 1.0 / (double)d;
+  }
+  TRY(hipMalloc(&g->ctab_aa, aa.size() * 8));
+  TRY(hipMalloc(&g->ctab_ra, ra.size() * 8));
+  TRY(hipMemcpyAsync(g->ctab_aa, aa.data(), aa.size() * 8, hipMemcpyHostToDevice, st));
+  TRY(hipMemcpyAsync(g->ctab_ra, ra.data(), ra.size() * 8, hipMemcpyHostToDevice, st));
+  TRY(hipStreamSynchronize(st));
+  // Wedge budget per chunk of path 2 / limit of path 1: ~1/8 of free HBM at
+  // ~44 B per wedge of working set.
+  size_t fr = 0, tot = 0;
+  TRY(hipMemGetInfo(&fr, &tot));
+  uint64_t b = (uint64_t)(fr / 8 / 44);
+  g->wedge_budget = std::max<uint64_t>(1u << 20, std::min<uint64_t>(b, 1ull << 30));
+  // test hook: NLP_WEDGE_BUDGET forces path-2 chunking on small graphs
+  if (const char* ev = getenv("NLP_WEDGE_BUDGET")) {
+    unsigned long long v = strtoull(ev, nullptr, 10);
+    if (v > 0) g->wedge_budget = v;
+  }
+  g->ws.release();  // drop build scratch; predict grows its own
+  return NLP_OK;
+}
+
+nlp_status new_graph(int device, nlp_graph** out) {
+  nlp_status s = check_device(device);
+  if (s != NLP_OK) return s;
+  nlp_graph* g = new (std::nothrow) nlp_graph();
+  if (!g) return NLP_ERR_NOMEM;
+  g->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(&g->host_small, 64 * 8) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  for (int i = 0; i < 4; ++i)
+    if (hipEventCreate(&g->ev[i]) != hipSuccess) { destroy_graph(g); return NLP_ERR_DEVICE; }
+  *out = g;
+  return NLP_OK;
+}
+
+// ---------------------------------------------------------------- predict pipeline
+
+struct Params {
+  int metric;
+  uint32_t H;
+  float min_score;
+  uint64_t max_edges;
+  uint64_t ua, ub;
+};
+
+struct Cands {
+  uint64_t n = 0;     // candidates currently held in B_CKEY..B_CS
+  uint64_t nan = 0;
+  uint64_t total = 0; // candidates produced (before pruning)
+  uint64_t wedges = 0;
+};
+
+// Group the W wedges of one generator pass, score them and append the
+// surviving candidates to the candidate buffer.
+nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* wk, uint32_t* wv, Cands& C,
+                           hipStream_t st) {
+  Workspace& ws = g->ws;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  if (W == 0) return NLP_OK;
+  uint64_t *wk1, *hoff, *scan, *rid, *rstart, *rpos, *cnt;
+  uint32_t *wv1 = nullptr, *hist, *rflag, *rkey, *ru, *rw, *rfl;
+  float* rs;
+  TRY(wsget(ws, B_WKEY1, W, &wk1));
+  if (custom) TRY(wsget(ws, B_WVAL1, W, &wv1));
+  uint64_t nb = rs_blocks(W);
+  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(W, RS_BINS * nb)) + 16, &scan));
+  TRY(wsget(ws, B_CNT, 8, &cnt));
+  // 1. stable sort by (u, w): bytes of w then bytes of u
+  int vb = bits_for(g->span - 1);
+  int shifts[8], np = 0;
+  for (int b = 0; b < vb; b += 8) shifts[np++] = b;
+  for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
+  SortScratch sc{hist, hoff, scan, nb};
+  int which = 0;
+  TRY(sort_pairs_u64(wk, custom ? wv : nullptr, wk1, custom ? wv1 : nullptr, W, shifts, np, sc, &which, st));
+  uint64_t* sk = which ? wk1 : wk;
+  uint32_t* sv = which ? wv1 : wv;
+  // 2. runs of equal (u, w)
+  TRY(wsget(ws, B_RFLAG, W, &rflag));
+  TRY(wsget(ws, B_RID, W, &rid));
+  LAUNCH(k_run_flags, W, st, sk, W, rflag);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(rflag, W, rid, cnt, scan, st));
+  TRY(read_small(g, cnt, 1, st));
+  const uint64_t R = g->host_small[0];
+  TRY(wsget(ws, B_RSTART, R + 1, &rstart));
+  LAUNCH(k_run_starts, W, st, rflag, rid, W, rstart, cnt);
+  TRY(hipGetLastError());
+  // 3. score every run
+  TRY(wsget(ws, B_RKEY, R, &rkey));
+  TRY(wsget(ws, B_RU, R, &ru));
+  TRY(wsget(ws, B_RW, R, &rw));
+  TRY(wsget(ws, B_RS, R, &rs));
+  TRY(wsget(ws, B_RFL, R, &rfl));
+  TRY(wsget(ws, B_RPOS, R, &rpos));
+  const double* ctab = p.metric == M_AA ? g->ctab_aa : g->ctab_ra;
+  if (custom)
+    LAUNCH(k_score<true>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru, rw,
+           rs, rfl);
+  else
+    LAUNCH(k_score<false>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru,
+           rw, rs, rfl);
+  TRY(hipGetLastError());
+  // 4. append flagged candidates
+  TRY(scan_excl_u64<uint32_t>(rfl, R, rpos, cnt + 1, scan, st));
+  TRY(read_small(g, cnt + 1, 1, st));
+  const uint64_t add = g->host_small[0];
+  uint32_t *ckey, *cu, *cw;
+  float* cs;
+  uint64_t need = C.n + add;
+  // grow the candidate buffer preserving contents
+  if (need * 4 > ws.bytes[B_CKEY]) {
+    uint32_t *ok = (uint32_t*)ws.p[B_CKEY], *ou = (uint32_t*)ws.p[B_CU], *ow = (uint32_t*)ws.p[B_CW];
+    float* os = (float*)ws.p[B_CS];
+    uint64_t cap = std::max<uint64_t>(need, 2 * C.n);
+    uint32_t *nk, *nu, *nw;
+    float* ns;
+    TRY(wsget(ws, B_TKEY, cap, &nk));
+    TRY(wsget(ws, B_TU, cap, &nu));
+    TRY(wsget(ws, B_TW, cap, &nw));
+    TRY(wsget(ws, B_TS, cap, &ns));
+    if (C.n) {
+      TRY(hipMemcpyAsync(nk, ok, C.n * 4, hipMemcpyDeviceToDevice, st));
+      TRY(hipMemcpyAsync(nu, ou, C.n * 4, hipMemcpyDeviceToDevice, st));
+      TRY(hipMemcpyAsync(nw, ow, C.n * 4, hipMemcpyDeviceToDevice, st));
+      TRY(hipMemcpyAsync(ns, os, C.n * 4, hipMemcpyDeviceToDevice, st));
+    }
+    std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
+    std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
+    std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
+    std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  }
+  TRY(wsget(ws, B_CKEY, need, &ckey));
+  TRY(wsget(ws, B_CU, need, &cu));
+  TRY(wsget(ws, B_CW, need, &cw));
+  TRY(wsget(ws, B_CS, need, &cs));
+  LAUNCH(k_compact_cands, R, st, rfl, rpos, cnt, rkey, ru, rw, rs, C.n, ckey, cu, cw, cs);
+  TRY(hipGetLastError());
+  C.n += add;
+  C.total += add;
+  return NLP_OK;
+}
+
+// Radix-select the canonical top `k` of the candidate buffer (in place).  The
+// buffer is in (u, w) order, so "first `quota` ties in buffer order" is the
+// canonical (u asc, w asc) tie fill.
+nlp_status prune_to(nlp_graph* g, Cands& C, uint64_t k, hipStream_t st) {
+  if (C.n <= k) return NLP_OK;
+  Workspace& ws = g->ws;
+  uint32_t *ckey = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
+  float* cs = (float*)ws.p[B_CS];
+  uint32_t *selhist, *tie, *keep;
+  uint64_t *sel, *trank, *kpos, *scan, *cnt;
+  TRY(wsget(ws, B_SELHIST, SEL_BINS, &selhist));
+  TRY(wsget(ws, B_SEL, 8, &sel));
+  TRY(wsget(ws, B_TIE, C.n, &tie));
+  TRY(wsget(ws, B_TRANK, C.n, &trank));
+  TRY(wsget(ws, B_KEEP, C.n, &keep));
+  TRY(wsget(ws, B_KPOS, C.n, &kpos));
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(C.n) + 16, &scan));
+  TRY(wsget(ws, B_CNT, 8, &cnt));
+  // candidate count lives on the device for the select kernels
+  g->host_small[8] = C.n;
+  g->host_small[9] = 0;  // sel[0] prefix
+  g->host_small[10] = k; // sel[1] rank
+  g->host_small[11] = 0; // sel[2] above
+  g->host_small[12] = 0;
+  TRY(hipMemcpyAsync(cnt + 4, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
+  TRY(hipMemcpyAsync(sel, &g->host_small[9], 32, hipMemcpyHostToDevice, st));
+  TRY(hipMemsetAsync(selhist, 0, SEL_BINS * 4, st));
+  for (int pass = 0; pass < 3; ++pass) {
+    LAUNCH(k_sel_hist, C.n, st, ckey, cnt + 4, pass, sel, selhist);
+    hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(NT), 0, st, selhist, pass, sel);
+    TRY(hipGetLastError());
+  }
+  LAUNCH(k_tie_flags, C.n, st, ckey, C.n, sel, tie);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(tie, C.n, trank, nullptr, scan, st));
+  LAUNCH(k_keep_flags, C.n, st, ckey, C.n, sel, trank, keep);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(keep, C.n, kpos, cnt + 5, scan, st));
+  uint32_t *nk, *nu, *nw;
+  float* ns;
+  TRY(wsget(ws, B_TKEY, k, &nk));
+  TRY(wsget(ws, B_TU, k, &nu));
+  TRY(wsget(ws, B_TW, k, &nw));
+  TRY(wsget(ws, B_TS, k, &ns));
+  LAUNCH(k_compact_cands, C.n, st, keep, kpos, cnt + 4, ckey, cu, cw, cs, (uint64_t)0, nk, nu, nw, ns);
+  TRY(hipGetLastError());
+  std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
+  std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
+  std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
+  std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  C.n = k;
+  return NLP_OK;
+}
+
+// Stable sort of the candidate buffer by score key descending -> edges.
+nlp_status order_into(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
+  if (C.n == 0) return NLP_OK;
+  Workspace& ws = g->ws;
+  uint64_t *k0, *k1, *hoff, *scan;
+  uint32_t *v0, *v1, *hist;
+  TRY(wsget(ws, B_SK0, C.n, &k0));
+  TRY(wsget(ws, B_SK1, C.n, &k1));
+  TRY(wsget(ws, B_SV0, C.n, &v0));
+  TRY(wsget(ws, B_SV1, C.n, &v1));
+  uint64_t nb = rs_blocks(C.n);
+  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(C.n, RS_BINS * nb)) + 16, &scan));
+  LAUNCH(k_desc_keys, C.n, st, (const uint32_t*)ws.p[B_CKEY], C.n, k0, v0);
+  TRY(hipGetLastError());
+  int shifts[4] = {0, 8, 16, 24};
+  SortScratch sc{hist, hoff, scan, nb};
+  int which = 0;
+  TRY(sort_pairs_u64(k0, v0, k1, v1, C.n, shifts, 4, sc, &which, st));
+  LAUNCH(k_gather_edges, C.n, st, which ? v1 : v0, C.n, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW],
+         (const float*)ws.p[B_CS], d_out);
+  TRY(hipGetLastError());
+  return NLP_OK;
+}
+
+nlp_status count_nan(nlp_graph* g, Cands& C, hipStream_t st) {
+  uint64_t* cnt;
+  TRY(wsget(g->ws, B_CNT, 8, &cnt));
+  TRY(hipMemsetAsync(cnt + 6, 0, 8, st));
+  if (C.n) LAUNCH(k_count_key0, C.n, st, (const uint32_t*)g->ws.p[B_CKEY], C.n, (unsigned long long*)(cnt + 6));
+  TRY(hipGetLastError());
+  TRY(read_small(g, cnt + 6, 1, st));
+  C.nan = g->host_small[0];
+  return NLP_OK;
+}
+
+// Path 1 generator: returns NLP_ERR_CAPACITY through *fits = false when the
+// wedge count exceeds the budget (then path 2 runs instead).
+nlp_status run_path1(nlp_graph* g, const Params& p, Cands& C, bool* fits, hipStream_t st) {
+  Workspace& ws = g->ws;
+  const uint64_t S = g->span;
+  uint32_t *c32, *ev, *eu, *ewc, *efirst, *wv = nullptr;
+  uint64_t *ioff, *woff, *scan, *cnt, *wk;
+  TRY(wsget(ws, B_C32, S, &c32));
+  TRY(wsget(ws, B_IOFF, S, &ioff));
+  TRY(wsget(ws, B_SCAN, scan_scratch_words(S) + 16, &scan));
+  TRY(wsget(ws, B_CNT, 8, &cnt));
+  LAUNCH(k_p1_vcount, S, st, g->deg, g->toff, S, p.H, c32);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(c32, S, ioff, cnt, scan, st));
+  TRY(read_small(g, cnt, 1, st));
+  const uint64_t E = g->host_small[0];
+  *fits = true;
+  if (E == 0) return NLP_OK;
+  TRY(wsget(ws, B_EV, E, &ev));
+  TRY(wsget(ws, B_EU, E, &eu));
+  TRY(wsget(ws, B_EWC, E, &ewc));
+  TRY(wsget(ws, B_EFIRST, E, &efirst));
+  TRY(wsget(ws, B_WOFF, E, &woff));
+  LAUNCH(k_p1_inedges, E, st, ioff, S, cnt, g->toff, g->tkeys, g->off, g->keys, g->deg, p.ua, p.ub, ev, eu, ewc, efirst);
+  TRY(hipGetLastError());
+  TRY(wsget(ws, B_SCAN, scan_scratch_words(std::max(S, E)) + 16, &scan));
+  TRY(scan_excl_u64<uint32_t>(ewc, E, woff, cnt + 1, scan, st));
+  TRY(read_small(g, cnt + 1, 1, st));
+  const uint64_t W = g->host_small[0];
+  if (W > g->wedge_budget) { *fits = false; return NLP_OK; }
+  C.wedges += W;
+  if (W == 0) return NLP_OK;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  TRY(wsget(ws, B_WKEY0, W, &wk));
+  if (custom) TRY(wsget(ws, B_WVAL0, W, &wv));
+  if (custom)
+    LAUNCH(k_wedges<true>, W, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+  else
+    LAUNCH(k_wedges<false>, W, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+  TRY(hipGetLastError());
+  return group_and_score(g, p, W, wk, wv, C, st);
+}
+
+// Path 2 generator: source range [ua, ub) in chunks of <= wedge_budget wedges
+// (a single source vertex larger than the budget forms its own chunk).
+nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks, hipStream_t st) {
+  Workspace& ws = g->ws;
+  const uint64_t S = g->span;
+  uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
+  uint64_t hb[2];
+  TRY(hipMemcpyAsync(&g->host_small[16], g->off + ua, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(&g->host_small[17], g->off + ub, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  hb[0] = g->host_small[16];
+  hb[1] = g->host_small[17];
+  const uint64_t e0 = hb[0], e1 = hb[1];
+  const uint64_t E = e1 - e0;
+  *nchunks = 0;
+  if (E == 0) return NLP_OK;
+  uint32_t *ev, *eu, *ewc, *efirst, *wv = nullptr;
+  uint64_t *woff, *scan, *cnt, *wk;
+  TRY(wsget(ws, B_EV, E, &ev));
+  TRY(wsget(ws, B_EU, E, &eu));
+  TRY(wsget(ws, B_EWC, E, &ewc));
+  TRY(wsget(ws, B_EFIRST, E, &efirst));
+  TRY(wsget(ws, B_WOFF, E + 1, &woff));
+  TRY(wsget(ws, B_SCAN, scan_scratch_words(E + 1) + 16, &scan));
+  TRY(wsget(ws, B_CNT, 8, &cnt));
+  LAUNCH(k_p2_edges, E, st, g->off, g->keys, g->deg, S, e0, e1, p.H, ev, eu, ewc, efirst);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(ewc, E, woff, cnt + 1, scan, st));
+  TRY(hipMemcpyAsync(woff + E, cnt + 1, 8, hipMemcpyDeviceToDevice, st));  // woff[E] = W
+  TRY(read_small(g, cnt + 1, 1, st));
+  const uint64_t Wall = g->host_small[0];
+  C.wedges += Wall;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  // chunk loop over edge slots [a, b) aligned to source rows
+  uint64_t a = 0;
+  std::vector<uint64_t> row_starts;
+  while (a < E && Wall > 0) {
+    uint64_t wa = 0, bnd = E;
+    TRY(hipMemcpyAsync(&g->host_small[18], woff + a, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    wa = g->host_small[18];
+    if (Wall - wa > g->wedge_budget) {
+      // first edge slot whose offset exceeds wa + budget, then back to its row start
+      hipLaunchKernelGGL(k_find_chunk_end, dim3(1), dim3(64), 0, st, woff, E + 1, wa + g->wedge_budget, cnt + 2);
+      TRY(hipGetLastError());
+      TRY(read_small(g, cnt + 2, 1, st));
+      uint64_t e = g->host_small[0];  // first slot with woff > target (1..E+1)
+      uint64_t slot = e - 1;          // last slot with woff <= target
+      if (slot > E) slot = E;
+      // row containing edge e0 + slot: find via offsets on the host side copy
+      uint64_t eg = e0 + slot;
+      // binary search offsets on the device would need another kernel; use a
+      // small host bisection over device reads
+      uint64_t lo = ua, hi = ub;  // largest u with off[u] <= eg
+      while (hi - lo > 1) {
+        uint64_t mid = (lo + hi) / 2;
+        TRY(hipMemcpy(&g->host_small[19], g->off + mid, 8, hipMemcpyDeviceToHost));
+        if (g->host_small[19] <= eg) lo = mid; else hi = mid;
+      }
+      TRY(hipMemcpy(&g->host_small[19], g->off + lo, 8, hipMemcpyDeviceToHost));
+      uint64_t rs = g->host_small[19] - e0;
+      if (rs <= a) {  // a single row larger than the budget: take the whole row
+        TRY(hipMemcpy(&g->host_small[19], g->off + lo + 1, 8, hipMemcpyDeviceToHost));
+        rs = g->host_small[19] - e0;
+      }
+      bnd = std::min(rs, E);
+    }
+    TRY(hipMemcpyAsync(&g->host_small[20], woff + bnd, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t wb = g->host_small[20];
+    const uint64_t W = wb - wa;
+    if (W) {
+      TRY(wsget(ws, B_WKEY0, W, &wk));
+      if (custom) TRY(wsget(ws, B_WVAL0, W, &wv));
+      // cnt[3] = wb for the grid-stride bound
+      g->host_small[21] = wb;
+      TRY(hipMemcpyAsync(cnt + 3, &g->host_small[21], 8, hipMemcpyHostToDevice, st));
+      if (custom)
+        LAUNCH(k_wedges<true>, W, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+      else
+        LAUNCH(k_wedges<false>, W, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+      TRY(hipGetLastError());
+      nlp_status s = group_and_score(g, p, W, wk, wv, C, st);
+      if (s != NLP_OK) return s;
+      if (C.n > 2 * p.max_edges + (1u << 20)) {
+        s = prune_to(g, C, p.max_edges, st);
+        if (s != NLP_OK) return s;
+      }
+    }
+    ++*nchunks;
+    a = bnd;
+  }
+  return NLP_OK;
+}
+
+nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
+                        hipStream_t st, EdgeOut** result) {
+  Cands C;
+  uint32_t path = 0, chunks = 0;
+  TRY(hipEventRecord(g->ev[0], st));
+  if (p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
+    bool fits = false;
+    if (p.H > 0) {
+      nlp_status s = run_path1(g, p, C, &fits, st);
+      if (s != NLP_OK) return s;
+      if (fits) path = 1;
+    }
+    if (!fits) {
+      C = Cands();
+      nlp_status s = run_path2(g, p, C, &chunks, st);
+      if (s != NLP_OK) return s;
+      path = 2;
+    }
+  }
+  TRY(hipEventRecord(g->ev[1], st));
+  nlp_status s = count_nan(g, C, st);
+  if (s != NLP_OK) return s;
+  uint64_t total = C.total, nan = C.nan;
+  s = prune_to(g, C, p.max_edges, st);
+  if (s != NLP_OK) return s;
+  if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.n, 1), &d_out));
+  s = order_into(g, C, d_out, st);
+  if (s != NLP_OK) return s;
+  TRY(hipEventRecord(g->ev[2], st));
+  TRY(hipEventSynchronize(g->ev[2]));
+  *out_count = C.n;
+  if (result) *result = d_out;
+  if (t) {
+    float a = 0, b = 0;
+    TRY(hipEventElapsedTime(&a, g->ev[0], g->ev[1]));
+    TRY(hipEventElapsedTime(&b, g->ev[1], g->ev[2]));
+    t->score_ms = a;
+    t->select_ms = b;
+    t->total_ms = a + b;
+    t->wedges = C.wedges;
+    t->candidates = total;
+    t->nan_candidates = nan;
+    t->path = path;
+    t->chunks = chunks;
+  }
+  return NLP_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C-ABI
+
+extern "C" {
+
+nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint64_t span, int device,
+                            nlp_graph** out) {
+  if (!out || !offsets || span == 0 || span > 0xffffffffull) return NLP_ERR_INVALID;
+  *out = nullptr;
+  const uint64_t M = offsets[span];
+  if (offsets[0] != 0 || (M && !keys)) return NLP_ERR_INVALID;
+  nlp_graph* g;
+  nlp_status s = new_graph(device, &g);
+  if (s != NLP_OK) return s;
+  g->span = span;
+  g->nnz = M;
+  if (hipMalloc(&g->off, (span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(M, 1) * 4) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_NOMEM;
+  }
+  if (hipMemcpyAsync(g->off, offsets, (span + 1) * 8, hipMemcpyHostToDevice, g->stream) != hipSuccess ||
+      (M && hipMemcpyAsync(g->keys, keys, M * 4, hipMemcpyHostToDevice, g->stream) != hipSuccess)) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g);
+  if (s != NLP_OK) { destroy_graph(g); return s; }
+  *out = g;
+  return NLP_OK;
+}
+
+nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_keys, uint64_t span, uint64_t nnz,
+                                   int device, void* stream, nlp_graph** out) {
+  if (!out || !d_offsets || span == 0 || span > 0xffffffffull || (nnz && !d_keys)) return NLP_ERR_INVALID;
+  *out = nullptr;
+  nlp_graph* g;
+  nlp_status s = new_graph(device, &g);
+  if (s != NLP_OK) return s;
+  g->span = span;
+  g->nnz = nnz;
+  hipStream_t ust = (hipStream_t)stream;
+  if (hipMalloc(&g->off, (span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(nnz, 1) * 4) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_NOMEM;
+  }
+  if (ust && hipStreamSynchronize(ust) != hipSuccess) { destroy_graph(g); return NLP_ERR_DEVICE; }
+  if (hipMemcpyAsync(g->off, d_offsets, (span + 1) * 8, hipMemcpyDeviceToDevice, g->stream) != hipSuccess ||
+      (nnz && hipMemcpyAsync(g->keys, d_keys, nnz * 4, hipMemcpyDeviceToDevice, g->stream) != hipSuccess)) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g);
+  if (s != NLP_OK) { destroy_graph(g); return s; }
+  *out = g;
+  return NLP_OK;
+}
+
+void nlp_graph_destroy(nlp_graph* g) { destroy_graph(g); }
+
+nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uint32_t* max_degree, int* symmetric) {
+  if (!g) return NLP_ERR_INVALID;
+  if (span) *span = g->span;
+  if (nnz) *nnz = g->nnz;
+  if (max_degree) *max_degree = g->maxdeg;
+  if (symmetric) *symmetric = g->symmetric ? 1 : 0;
+  return NLP_OK;
+}
+
+nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
+                              uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
+                              uint64_t* out_count, nlp_timing* t, void* stream) {
+  if (!g || !out_count || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span)};
+  nlp_timing tt;
+  memset(&tt, 0, sizeof(tt));
+  nlp_status s = predict_impl(g, p, (EdgeOut*)d_out, out_count, &tt, st, nullptr);
+  if (t) *t = tt;
+  return s;
+}
+
+nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score, uint64_t max_edges,
+                       int repeat, nlp_edge* out, uint64_t* out_count, nlp_timing* t) {
+  if (!g || !out_count || (int)metric < 0 || (int)metric > 8) return NLP_ERR_INVALID;
+  if (repeat < 1) repeat = 1;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  hipStream_t st = g->stream;
+  Params p{(int)metric, hub_max_degree, min_score, max_edges, 0, g->span};
+  // measureDuration(fn, repeat) semantics (_utility.hxx:345-352): the timed
+  // work runs `repeat` times and the reported times are averages.
+  float score_sum = 0, select_sum = 0;
+  nlp_timing last;
+  memset(&last, 0, sizeof(last));
+  EdgeOut* d_res = nullptr;
+  uint64_t n = 0;
+  for (int r = 0; r < repeat; ++r) {
+    nlp_status s = predict_impl(g, p, nullptr, &n, &last, st, &d_res);
+    if (s != NLP_OK) return s;
+    score_sum += last.score_ms;
+    select_sum += last.select_ms;
+  }
+  last.score_ms = score_sum / repeat;
+  last.select_ms = select_sum / repeat;
+  last.total_ms = last.score_ms + last.select_ms;
+  if (out && n) {
+    TRY(hipEventRecord(g->ev[0], st));
+    TRY(hipMemcpyAsync(out, d_res, n * sizeof(EdgeOut), hipMemcpyDeviceToHost, st));
+    TRY(hipEventRecord(g->ev[1], st));
+    TRY(hipEventSynchronize(g->ev[1]));
+    TRY(hipEventElapsedTime(&last.copy_ms, g->ev[0], g->ev[1]));
+  }
+  *out_count = n;
+  if (t) *t = last;
+  return NLP_OK;
+}
+
+nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,
+                                   nlp_edge* d_out, uint64_t* out_count, void* stream) {
+  if (!g || !out_count || (n && !d_in) || (max_edges && !d_out)) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  Cands C;
+  if (n) {
+    uint32_t *ck, *cu, *cw;
+    float* cs;
+    TRY(wsget(g->ws, B_CKEY, n, &ck));
+    TRY(wsget(g->ws, B_CU, n, &cu));
+    TRY(wsget(g->ws, B_CW, n, &cw));
+    TRY(wsget(g->ws, B_CS, n, &cs));
+    LAUNCH(k_split_edges, n, st, (const EdgeOut*)d_in, n, ck, cu, cw, cs);
+    TRY(hipGetLastError());
+    C.n = n;
+  }
+  nlp_status s = prune_to(g, C, max_edges, st);
+  if (s != NLP_OK) return s;
+  s = order_into(g, C, (EdgeOut*)d_out, st);
+  if (s != NLP_OK) return s;
+  TRY(hipStreamSynchronize(st));
+  *out_count = C.n;
+  return NLP_OK;
+}
+
+const char* nlp_status_string(nlp_status s) {
+  switch (s) {
+    case NLP_OK: return "ok";
+    case NLP_ERR_INVALID: return "invalid argument";
+    case NLP_ERR_DEVICE: return "HIP device error";
+    case NLP_ERR_NOMEM: return "out of memory";
+    case NLP_ERR_NODEVICE: return "no gfx950 device";
+    case NLP_ERR_CAPACITY: return "output buffer too small";
+  }
+  return "unknown status";
+}
+
+const char* nlp_metric_name(nlp_metric m) {
+  static const char* names[] = {"CommonNeighbors", "JaccardCoefficient", "SorensenIndex",
+                                "SaltonCosineSimilarity", "HubPromoted", "HubDepressed",
+                                "LeichtHolmeNermanScore", "AdamicAdarCoefficient",
+                                "ResourceAllocationScore"};
+  return ((int)m >= 0 && (int)m <= 8) ? names[(int)m] : "unknown";
+}
+
+int nlp_version(void) { return 100; }
+
+}  // extern "C"

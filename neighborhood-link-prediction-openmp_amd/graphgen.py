@@ -1,0 +1,158 @@
+"""Synthetic inputs for the link-prediction path (host/device plumbing, not the
+hot path).
+
+The reference experiment (main.cxx:157-179, 241-245) reads a SuiteSparse graph,
+symmetrizes it, removes self-loops and then deletes a random fraction of its
+undirected edges.  The SuiteSparse graphs are not available offline, so the
+bench and the large parity tests use deterministic Chung-Lu stand-ins with the
+shape of each BASELINE.json config:
+
+    endpoints i.i.d. with P(i) ~ (i+1)^-alpha, ids randomly permuted,
+    self-loops dropped, (u, v) deduped, then symmetrized.
+
+Vertex ids are 1..n and row 0 is empty, as in the reference's DiGraph
+(mtx.hxx reads 1-based ids; Graph.hxx span() = n+1).
+
+Deletions follow the reference's sampling shape (batch.hxx:29-58, 99-112):
+a uniformly random vertex u in [1, n] (retried up to 5 times when deg(u)=0,
+_utility.hxx:432), then a uniformly random entry of N(u); both directions are
+deleted; duplicates are removed by tidy (batch.hxx:200-208).  Random numbers come
+from torch's generator, so the draws are not the reference's minstd_rand0
+sequence -- bit-exact replay of the reference's ingest is done by the oracle's
+ref_driver for the golden fixtures instead.
+
+Everything is vectorised torch so it runs on the GPU (bench) or the CPU (tests).
+"""
+import math
+
+import torch
+
+# SURVEY.md §8(d) stand-ins: name -> (n, m, alpha, graph_seed, deletion fraction, metric, hub)
+CONFIGS = {
+    "C1-web-Google": (916_428, 5_105_039, 0.7, 11, 0.01, "JAC", 4),
+    "C2-soc-LiveJournal1": (4_847_571, 68_993_773, 0.6, 12, 0.1, "JAC", 4),
+    "C3-uk-2005": (39_459_925, 936_364_282, 0.7, 13, 0.1, "AA", 4),
+    "C4-sk-2005": (50_636_154, 1_949_412_601, 0.7, 14, 0.1, "JAC", 4),
+    "C5-sk-2005-ihub": (50_636_154, 1_949_412_601, 0.7, 14, 0.01, "CN", 0),
+}
+
+
+def _gen(seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    return g
+
+
+def chung_lu_edges(n, m, alpha, seed, device="cpu"):
+    """Return (src, dst) int64 tensors of m distinct directed edges, ids in 1..n."""
+    g = _gen(seed, device)
+    w = torch.arange(1, n + 1, dtype=torch.float64, device=device).pow_(-alpha)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    del w
+    perm = torch.randperm(n, generator=g, device=device) + 1
+    draws = int(m * 1.15) + 1024
+    keys = []
+    have = 0
+    # draw in chunks to bound peak memory
+    chunk = 1 << 26
+    while True:
+        todo = min(chunk, draws)
+        r = torch.rand(todo, generator=g, dtype=torch.float64, device=device)
+        u = torch.searchsorted(cdf, r).clamp_(max=n - 1)
+        r = torch.rand(todo, generator=g, dtype=torch.float64, device=device)
+        v = torch.searchsorted(cdf, r).clamp_(max=n - 1)
+        del r
+        u = perm[u]
+        v = perm[v]
+        ok = u != v
+        keys.append((u[ok] * (n + 1) + v[ok]))
+        del u, v, ok
+        have += todo
+        if have >= draws:
+            allk = torch.unique(torch.cat(keys))
+            keys = [allk]
+            if allk.numel() >= m:
+                break
+            draws = int((m - allk.numel()) * 1.3) + 1024
+            have = 0
+    allk = keys[0]
+    if allk.numel() > m:
+        sel = torch.randperm(allk.numel(), generator=g, device=device)[:m]
+        allk = torch.sort(allk[sel]).values
+    return allk // (n + 1), allk % (n + 1)
+
+
+def symmetric_csr(n, src, dst):
+    """CSR (offsets int64 [n+2], keys int32 [M]) of the symmetrized, self-loop-free,
+    deduplicated graph, span = n+1 (row 0 empty)."""
+    span = n + 1
+    a = torch.cat([src * span + dst, dst * span + src])
+    a = torch.unique(a)  # sorted
+    rows = a // span
+    keys = (a % span).to(torch.int32)
+    del a
+    counts = torch.bincount(rows, minlength=span)
+    offsets = torch.zeros(span + 1, dtype=torch.int64, device=src.device)
+    offsets[1:] = torch.cumsum(counts, 0)
+    return offsets, keys
+
+
+def csr_rows(offsets, M):
+    span = offsets.numel() - 1
+    deg = offsets[1:] - offsets[:-1]
+    return torch.repeat_interleave(torch.arange(span, device=offsets.device), deg, output_size=M)
+
+
+def delete_edges(offsets, keys, frac, seed, n=None):
+    """Reference-shaped random undirected deletions (see module docstring).
+
+    Returns (offsets', keys', del_u, del_w) where (del_u, del_w) are the sorted,
+    unique directed deletions (both directions), i.e. main.cxx's `deletions0`;
+    the reference predicts maxEdges = len(deletions0) // 2 links (main.cxx:50)."""
+    dev = offsets.device
+    span = offsets.numel() - 1
+    n = span - 1 if n is None else n
+    M = keys.numel()
+    D = int(frac * M / 2)
+    g = _gen(seed, dev)
+    deg = offsets[1:] - offsets[:-1]
+    # 5 tries per draw (retry(fn, 5), batch.hxx:110 / _utility.hxx:432)
+    tries = 5
+    u = (1 + torch.floor(n * torch.rand(D, tries, generator=g, dtype=torch.float64, device=dev))).long()
+    u.clamp_(max=span - 1)
+    has = deg[u] > 0
+    first = torch.argmax(has.to(torch.int8), dim=1)
+    okrow = has.any(dim=1)
+    u = u.gather(1, first[:, None])[:, 0][okrow]
+    r = torch.rand(u.numel(), generator=g, dtype=torch.float64, device=dev)
+    vi = torch.floor(r * deg[u].double()).long()
+    v = keys[offsets[u] + vi].long()
+    pairs = torch.unique(torch.cat([u * span + v, v * span + u]))
+    rows = csr_rows(offsets, M)
+    ek = rows * span + keys.long()
+    pos = torch.searchsorted(pairs, ek).clamp_(max=pairs.numel() - 1)
+    drop = pairs[pos] == ek
+    keep = ~drop
+    keys2 = keys[keep]
+    counts = torch.bincount(rows[keep], minlength=span)
+    off2 = torch.zeros(span + 1, dtype=torch.int64, device=dev)
+    off2[1:] = torch.cumsum(counts, 0)
+    return off2, keys2, (pairs // span).to(torch.int32), (pairs % span).to(torch.int32)
+
+
+def make_workload(name_or_spec, device="cpu", scale=1.0):
+    """Build (offsets, keys, del_u, del_w, spec) for a CONFIGS entry.
+
+    `scale` shrinks n and m proportionally (tests use small scales)."""
+    spec = CONFIGS[name_or_spec] if isinstance(name_or_spec, str) else name_or_spec
+    n, m, alpha, seed, d, metric, hub = spec
+    n = max(16, int(math.ceil(n * scale)))
+    m = max(16, int(math.ceil(m * scale)))
+    src, dst = chung_lu_edges(n, m, alpha, seed, device)
+    off, keys = symmetric_csr(n, src, dst)
+    del src, dst
+    off2, keys2, du, dw = delete_edges(off, keys, d, seed + 1000, n=n)
+    return off2, keys2, du, dw, dict(n=n, m=m, alpha=alpha, seed=seed, d=d, metric=metric, hub=hub,
+                                     M_before=int(keys.numel()), M=int(keys2.numel()),
+                                     k=int(du.numel()) // 2)

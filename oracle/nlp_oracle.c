@@ -1,0 +1,257 @@
+/*
+ * nlp_oracle.c -- CPU restatement of the reference's link-prediction hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the *checker*: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product path (libnlp.so, HIP) never links or calls it.
+ *
+ * Parity status: PINNED.  tests/golden/ holds fixtures produced by the real
+ * reference (oracle/ref_driver.cxx compiled against /root/reference/inc by
+ * oracle/Makefile, see tests/golden/make_golden.py); tests/test_oracle_golden.py
+ * checks this restatement against them (candidate multisets bit-exact, top-k
+ * above-boundary sets bit-exact, ties inside the reference's tie set).
+ *
+ * What it restates (all citations are /root/reference paths):
+ *   - predictLinksWithIntersectionLoopU        inc/predict.hxx:214-265
+ *       dense per-u counter table + touched list, hub filter deg(v) > H skip
+ *       (predict.hxx:227), second-hop filter w > u (predict.hxx:221),
+ *       first-order exclusion (predict.hxx:232-233), score <= minScore skip
+ *       (predict.hxx:237)
+ *   - predictScanEdgesBasicU / predictScanEdgesU inc/predict.hxx:153-179
+ *   - predictClearScanW                         inc/predict.hxx:187-192
+ *   - the nine metric score/update lambdas      inc/predict.hxx:502-831
+ *   - degree() counts duplicate adjacency entries (Graph.hxx:167-169,
+ *     _bitset.hxx:53), so every list is treated as a sorted multiset.
+ *
+ * Where the reference is nondeterministic (ties at the k-th score, SURVEY
+ * Appendix A.1) or undefined (OpenMP dummy-heap read when candidates < k,
+ * A.2; NaN scores, A.4), this restatement uses the canonical contract that the
+ * GPU path also implements:
+ *     order = (score key descending, u ascending, w ascending)
+ *     NaN scores are kept (they pass `score <= minScore`, predict.hxx:237) and
+ *     rank below every non-NaN score; -0.0 ranks equal to +0.0.
+ *     fewer than maxEdges candidates -> return all of them (sequential
+ *     reference behaviour, predict.hxx:358-374).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+enum {
+  NLPO_CN = 0,   /* predictLinksCommonNeighbors          predict.hxx:502 */
+  NLPO_JAC = 1,  /* predictLinksJaccardCoefficient       predict.hxx:540 */
+  NLPO_SOR = 2,  /* predictLinksSorensenIndex            predict.hxx:578 */
+  NLPO_SAL = 3,  /* predictLinksSaltonCosineSimilarity   predict.hxx:616 */
+  NLPO_HPI = 4,  /* predictLinksHubPromoted              predict.hxx:654 */
+  NLPO_HDI = 5,  /* predictLinksHubDepressed             predict.hxx:692 */
+  NLPO_LHN = 6,  /* predictLinksLeichtHolmeNermanScore   predict.hxx:730 */
+  NLPO_AA = 7,   /* predictLinksAdamicAdarCoefficient    predict.hxx:768 */
+  NLPO_RA = 8    /* predictLinksResourceAllocationScore  predict.hxx:808 */
+};
+
+/* Order-preserving map float -> uint32 (larger score -> larger key).
+ * NaN -> 0 (ranks last); -0.0 -> key of +0.0. */
+uint32_t nlpo_score_key(float s) {
+  uint32_t b;
+  if (s != s) return 0u;
+  if (s == 0.0f) s = 0.0f;
+  memcpy(&b, &s, 4);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+/* Score of a basic (count) metric, predict.hxx:504-749.  du, dw are size_t
+ * degrees (Graph.hxx:167), c is the uint32 wedge count (VT = K). */
+static float score_basic(int metric, uint32_t c, uint64_t du, uint64_t dw) {
+  float fc = (float)c;
+  switch (metric) {
+    case NLPO_CN:  return fc;                                   /* W(Nuv) */
+    case NLPO_JAC: return fc / (float)(du + dw - (uint64_t)c);  /* size_t wrap kept */
+    case NLPO_SOR: return fc / (float)(du + dw);
+    case NLPO_SAL: return (float)((double)fc / sqrt((double)(du * dw)));
+    case NLPO_HPI: return fc / (float)(du < dw ? du : dw);
+    case NLPO_HDI: return fc / (float)(du < dw ? dw : du);
+    case NLPO_LHN: return fc / (float)(du * dw);
+    default: return 0.0f;
+  }
+}
+
+/* Per-intermediate contribution of AA / RA (predict.hxx:770, 810), where the
+ * lambda's `u` argument is the intermediate vertex v. */
+static double contrib(int metric, uint64_t dv) {
+  return metric == NLPO_AA ? 1.0 / log((double)dv) : 1.0 / (double)dv;
+}
+
+typedef struct {
+  uint32_t u, w;
+  float score;
+  uint32_t key;
+} cand_t;
+
+typedef struct {
+  cand_t *a;
+  size_t n, cap;
+} cvec_t;
+
+static int cvec_push(cvec_t *v, cand_t c) {
+  if (v->n == v->cap) {
+    size_t nc = v->cap ? v->cap * 2 : 1024;
+    cand_t *na = (cand_t *)realloc(v->a, nc * sizeof(cand_t));
+    if (!na) return -1;
+    v->a = na; v->cap = nc;
+  }
+  v->a[v->n++] = c;
+  return 0;
+}
+
+static int cmp_u32(const void *x, const void *y) {
+  uint32_t a = *(const uint32_t *)x, b = *(const uint32_t *)y;
+  return (a > b) - (a < b);
+}
+
+/* Canonical order: key desc, u asc, w asc. */
+static int cmp_cand(const void *x, const void *y) {
+  const cand_t *a = (const cand_t *)x, *b = (const cand_t *)y;
+  if (a->key != b->key) return a->key < b->key ? 1 : -1;
+  if (a->u != b->u) return a->u < b->u ? -1 : 1;
+  if (a->w != b->w) return a->w < b->w ? -1 : 1;
+  return 0;
+}
+
+/*
+ * Enumerate every candidate (u, w, score) with score > min_score (or NaN) for
+ * u in [u_begin, u_end), in (u asc, w asc) order.  Returns 0 on success.
+ * Also reports the wedge count the reference scans (SURVEY §8(d) W_H).
+ */
+static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                     int metric, uint32_t hub, float min_score,
+                     uint64_t u_begin, uint64_t u_end, cvec_t *out,
+                     uint64_t *wedges_out) {
+  int custom = (metric == NLPO_AA || metric == NLPO_RA);
+  uint32_t *cnt = (uint32_t *)calloc(span ? span : 1, sizeof(uint32_t));
+  float *acc = custom ? (float *)calloc(span ? span : 1, sizeof(float)) : NULL;
+  uint32_t *touched = (uint32_t *)malloc((span ? span : 1) * sizeof(uint32_t));
+  uint64_t wedges = 0;
+  if (!cnt || !touched || (custom && !acc)) { free(cnt); free(acc); free(touched); return -1; }
+  for (uint64_t u = u_begin; u < u_end && u < span; ++u) {
+    size_t nt = 0;
+    uint64_t du = off[u + 1] - off[u];
+    /* wedge scan: predict.hxx:224-230 -> 153-179 */
+    for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
+      uint32_t v = keys[i];
+      uint64_t dv = v < span ? off[v + 1] - off[v] : 0;
+      if (hub && dv > hub) continue;                /* predict.hxx:227 */
+      double c = custom ? contrib(metric, dv) : 0.0;
+      for (uint64_t j = off[v]; j < off[v + 1]; ++j) {
+        uint32_t w = keys[j];
+        ++wedges;
+        if (!(w > u)) continue;                      /* ft: predict.hxx:221 */
+        if (custom) {
+          if (!acc[w]) touched[nt++] = w;            /* predict.hxx:176 */
+          acc[w] = (float)((double)acc[w] + c);      /* fu: entry += 1.0/..  */
+        } else {
+          if (!cnt[w]) touched[nt++] = w;            /* predict.hxx:157 */
+          ++cnt[w];
+        }
+      }
+    }
+    /* first-order exclusion, predict.hxx:232-233 */
+    if (custom) acc[u] = 0.0f; else cnt[u] = 0;
+    for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
+      if (custom) acc[keys[i]] = 0.0f; else cnt[keys[i]] = 0;
+    }
+    /* canonical w order inside u (the reference scores in first-touch order,
+       which only matters for ties, A.1) */
+    qsort(touched, nt, sizeof(uint32_t), cmp_u32);
+    for (size_t t = 0; t < nt; ++t) {
+      uint32_t w = touched[t];
+      float s;
+      if (custom) s = acc[w];                        /* fs = W(Nuv) */
+      else {
+        uint64_t dw = w < span ? off[w + 1] - off[w] : 0;
+        s = score_basic(metric, cnt[w], du, dw);
+      }
+      if (custom) acc[w] = 0.0f; else cnt[w] = 0;    /* predictClearScanW 187-192 */
+      if (s <= min_score) continue;                  /* predict.hxx:237 (NaN passes) */
+      cand_t cd = {(uint32_t)u, w, s, nlpo_score_key(s)};
+      if (cvec_push(out, cd)) { free(cnt); free(acc); free(touched); return -1; }
+    }
+  }
+  free(cnt); free(acc); free(touched);
+  if (wedges_out) *wedges_out = wedges;
+  return 0;
+}
+
+/*
+ * Canonical top-k.  Writes at most max_edges tuples (score desc, u asc, w asc)
+ * into out_u/out_w/out_score (caller-owned, may be NULL when max_edges == 0)
+ * and the number written into *out_count.  *n_candidates gets the number of
+ * candidates that passed the score filter, *n_nan those with NaN score,
+ * *n_wedges the wedges scanned.  Returns 0 on success, -1 on allocation failure.
+ */
+int nlpo_predict_range(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                       int metric, uint32_t hub, float min_score, uint64_t max_edges,
+                       uint64_t u_begin, uint64_t u_end,
+                       uint32_t *out_u, uint32_t *out_w, float *out_score,
+                       uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
+                       uint64_t *n_wedges) {
+  cvec_t c = {0, 0, 0};
+  if (enumerate(off, keys, span, metric, hub, min_score, u_begin, u_end, &c, n_wedges)) {
+    free(c.a); return -1;
+  }
+  uint64_t nn = 0;
+  for (size_t i = 0; i < c.n; ++i) nn += (c.a[i].key == 0);
+  if (n_candidates) *n_candidates = c.n;
+  if (n_nan) *n_nan = nn;
+  uint64_t take = c.n < max_edges ? c.n : max_edges;
+  if (take == 0) c.n = 0;
+  if (take < c.n) {
+    /* threshold = take-th largest key; candidates are in (u,w) order, so the
+       first `quota` ties in that order are the canonical tie fill. */
+    uint32_t *hi = (uint32_t *)calloc(65536, sizeof(uint32_t));
+    uint32_t *lo = (uint32_t *)calloc(65536, sizeof(uint32_t));
+    if (!hi || !lo) { free(hi); free(lo); free(c.a); return -1; }
+    for (size_t i = 0; i < c.n; ++i) hi[c.a[i].key >> 16]++;
+    uint64_t acc = 0; int b = 65535;
+    for (; b >= 0; --b) { if (acc + hi[b] >= take) break; acc += hi[b]; }
+    for (size_t i = 0; i < c.n; ++i) if ((c.a[i].key >> 16) == (uint32_t)b) lo[c.a[i].key & 0xffff]++;
+    int l = 65535;
+    for (; l >= 0; --l) { if (acc + lo[l] >= take) break; acc += lo[l]; }
+    uint32_t kth = ((uint32_t)b << 16) | (uint32_t)l;
+    uint64_t quota = take - acc;  /* ties to keep */
+    size_t j = 0;
+    for (size_t i = 0; i < c.n; ++i) {
+      if (c.a[i].key > kth) c.a[j++] = c.a[i];
+      else if (c.a[i].key == kth && quota) { c.a[j++] = c.a[i]; --quota; }
+    }
+    c.n = j;
+    free(hi); free(lo);
+  }
+  qsort(c.a, c.n, sizeof(cand_t), cmp_cand);
+  if (c.n > take) c.n = take;
+  for (size_t i = 0; i < c.n; ++i) {
+    if (out_u) out_u[i] = c.a[i].u;
+    if (out_w) out_w[i] = c.a[i].w;
+    if (out_score) out_score[i] = c.a[i].score;
+  }
+  if (out_count) *out_count = c.n;
+  free(c.a);
+  return 0;
+}
+
+int nlpo_predict(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                 int metric, uint32_t hub, float min_score, uint64_t max_edges,
+                 uint32_t *out_u, uint32_t *out_w, float *out_score,
+                 uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
+                 uint64_t *n_wedges) {
+  return nlpo_predict_range(off, keys, span, metric, hub, min_score, max_edges, 0, span,
+                            out_u, out_w, out_score, out_count, n_candidates, n_nan, n_wedges);
+}
+
+/* Number of candidates (score > min_score or NaN) -- sizing helper for tests. */
+int nlpo_count_candidates(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                          int metric, uint32_t hub, float min_score,
+                          uint64_t *n_candidates, uint64_t *n_wedges) {
+  return nlpo_predict(off, keys, span, metric, hub, min_score, 0, NULL, NULL, NULL,
+                      NULL, n_candidates, NULL, n_wedges);
+}
