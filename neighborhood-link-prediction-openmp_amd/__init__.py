@@ -106,7 +106,13 @@ def _metric(m):
     return int(m)
 
 
-def _stream_ptr(stream):
+def _stream_ptr(stream, tensor=None):
+    """hipStream_t for the library: the given stream, else torch's current
+    stream when the operands are torch device tensors (so that library kernels
+    are ordered after the kernels that produced them)."""
+    if stream is None and tensor is not None and getattr(tensor, "is_cuda", False):
+        import torch
+        stream = torch.cuda.current_stream(tensor.device)
     if stream is None:
         return None
     return getattr(stream, "cuda_stream", stream)
@@ -158,7 +164,7 @@ class Graph:
         span = offsets.numel() - 1
         h = ctypes.c_void_p()
         _check(L.nlp_graph_create_device(offsets.data_ptr(), keys.data_ptr() if keys.numel() else None, span,
-                                         keys.numel(), int(dev or 0), _stream_ptr(stream), ctypes.byref(h)),
+                                         keys.numel(), int(dev or 0), _stream_ptr(stream, offsets), ctypes.byref(h)),
                "nlp_graph_create_device")
         g._h = h
         g.device = int(dev or 0)
@@ -197,13 +203,13 @@ class Graph:
         cnt = ctypes.c_uint64()
         _check(lib().nlp_predict_device(self._h, _metric(metric), int(hub), float(min_score), int(max_edges),
                                         int(u_begin), int(u_end), out.data_ptr(), ctypes.byref(cnt),
-                                        ctypes.byref(t), _stream_ptr(stream)), "nlp_predict_device")
+                                        ctypes.byref(t), _stream_ptr(stream, out)), "nlp_predict_device")
         return cnt.value, t.as_dict()
 
     def select_edges_device(self, edges_in, n, max_edges, out, stream=None):
         cnt = ctypes.c_uint64()
         _check(lib().nlp_select_edges_device(self._h, edges_in.data_ptr(), int(n), int(max_edges), out.data_ptr(),
-                                             ctypes.byref(cnt), _stream_ptr(stream)), "nlp_select_edges_device")
+                                             ctypes.byref(cnt), _stream_ptr(stream, out)), "nlp_select_edges_device")
         return cnt.value
 
     def close(self):

@@ -714,7 +714,11 @@ nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_
     destroy_graph(g);
     return NLP_ERR_NOMEM;
   }
-  if (ust && hipStreamSynchronize(ust) != hipSuccess) { destroy_graph(g); return NLP_ERR_DEVICE; }
+  // inputs may come from any stream: order after `stream`, or after everything
+  if ((ust ? hipStreamSynchronize(ust) : hipDeviceSynchronize()) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
   if (hipMemcpyAsync(g->off, d_offsets, (span + 1) * 8, hipMemcpyDeviceToDevice, g->stream) != hipSuccess ||
       (nnz && hipMemcpyAsync(g->keys, d_keys, nnz * 4, hipMemcpyDeviceToDevice, g->stream) != hipSuccess)) {
     destroy_graph(g);
@@ -743,6 +747,9 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  // the graph's own stream does not order after other streams: with no caller
+  // stream, wait for all prior device work (inputs/outputs may come from it)
+  if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
   Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span)};
   nlp_timing tt;
   memset(&tt, 0, sizeof(tt));
@@ -791,6 +798,7 @@ nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t 
   if (!g || !out_count || (n && !d_in) || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
   Cands C;
   if (n) {
     uint32_t *ck, *cu, *cw;

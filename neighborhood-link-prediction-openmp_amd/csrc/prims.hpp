@@ -106,14 +106,12 @@ __global__ __launch_bounds__(NT) void k_scan_down(const T* __restrict__ in, uint
     *total = (boff ? boff[blockIdx.x] : 0) + tot;
 }
 
-// Scratch needed by scan_excl_u64 for n items (in u64 words).
+// Scratch needed by scan_excl_u64 for n items (in u64 words): per level
+// nb block sums + nb block offsets + 1, then the level above.
 inline uint64_t scan_scratch_words(uint64_t n) {
-  uint64_t w = 0;
-  while (n > (uint64_t)SCAN_TILE) {
-    n = (n + SCAN_TILE - 1) / SCAN_TILE;
-    w += n + 1;
-  }
-  return w + 1;
+  uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (nb <= 1) return 1;
+  return 2 * nb + 1 + scan_scratch_words(nb);
 }
 
 // Exclusive scan of n items into out (u64).  *d_total (device) receives the sum.

@@ -121,17 +121,18 @@ static int cmp_cand(const void *x, const void *y) {
 /*
  * Enumerate every candidate (u, w, score) with score > min_score (or NaN) for
  * u in [u_begin, u_end), in (u asc, w asc) order.  Returns 0 on success.
- * Also reports the wedge count the reference scans (SURVEY §8(d) W_H).
+ * Also reports the wedge count the reference scans (SURVEY §8(d) W_H) and
+ * the number of those with w > u (the wedges that reach the counter table).
  */
 static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
                      int metric, uint32_t hub, float min_score,
                      uint64_t u_begin, uint64_t u_end, cvec_t *out,
-                     uint64_t *wedges_out) {
+                     uint64_t *wedges_out, uint64_t *wedges_gt_out) {
   int custom = (metric == NLPO_AA || metric == NLPO_RA);
   uint32_t *cnt = (uint32_t *)calloc(span ? span : 1, sizeof(uint32_t));
   float *acc = custom ? (float *)calloc(span ? span : 1, sizeof(float)) : NULL;
   uint32_t *touched = (uint32_t *)malloc((span ? span : 1) * sizeof(uint32_t));
-  uint64_t wedges = 0;
+  uint64_t wedges = 0, wedges_gt = 0;
   if (!cnt || !touched || (custom && !acc)) { free(cnt); free(acc); free(touched); return -1; }
   for (uint64_t u = u_begin; u < u_end && u < span; ++u) {
     size_t nt = 0;
@@ -146,6 +147,7 @@ static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
         uint32_t w = keys[j];
         ++wedges;
         if (!(w > u)) continue;                      /* ft: predict.hxx:221 */
+        ++wedges_gt;
         if (custom) {
           if (!acc[w]) touched[nt++] = w;            /* predict.hxx:176 */
           acc[w] = (float)((double)acc[w] + c);      /* fu: entry += 1.0/..  */
@@ -179,6 +181,7 @@ static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
   }
   free(cnt); free(acc); free(touched);
   if (wedges_out) *wedges_out = wedges;
+  if (wedges_gt_out) *wedges_gt_out = wedges_gt;
   return 0;
 }
 
@@ -194,9 +197,9 @@ int nlpo_predict_range(const uint64_t *off, const uint32_t *keys, uint64_t span,
                        uint64_t u_begin, uint64_t u_end,
                        uint32_t *out_u, uint32_t *out_w, float *out_score,
                        uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
-                       uint64_t *n_wedges) {
+                       uint64_t *n_wedges, uint64_t *n_wedges_gt) {
   cvec_t c = {0, 0, 0};
-  if (enumerate(off, keys, span, metric, hub, min_score, u_begin, u_end, &c, n_wedges)) {
+  if (enumerate(off, keys, span, metric, hub, min_score, u_begin, u_end, &c, n_wedges, n_wedges_gt)) {
     free(c.a); return -1;
   }
   uint64_t nn = 0;
@@ -245,7 +248,7 @@ int nlpo_predict(const uint64_t *off, const uint32_t *keys, uint64_t span,
                  uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
                  uint64_t *n_wedges) {
   return nlpo_predict_range(off, keys, span, metric, hub, min_score, max_edges, 0, span,
-                            out_u, out_w, out_score, out_count, n_candidates, n_nan, n_wedges);
+                            out_u, out_w, out_score, out_count, n_candidates, n_nan, n_wedges, NULL);
 }
 
 /* Number of candidates (score > min_score or NaN) -- sizing helper for tests. */

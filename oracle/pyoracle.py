@@ -34,7 +34,7 @@ def lib():
         L.nlpo_predict_range.argtypes = [
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
             ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
-            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p, u64p, u64p, u64p]
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p, u64p, u64p, u64p, u64p]
         L.nlpo_predict_range.restype = ctypes.c_int
         L.nlpo_score_key.argtypes = [ctypes.c_float]
         L.nlpo_score_key.restype = ctypes.c_uint32
@@ -45,7 +45,8 @@ def lib():
 def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0, u_end=None):
     """Canonical top-k from the C restatement.
 
-    Returns (u, w, score, info) with info = dict(candidates, nan, wedges)."""
+    Returns (u, w, score, info) with info = dict(candidates, nan, wedges, wedges_gt):
+    wedges = all (u, v, w) the reference scans, wedges_gt = those with w > u."""
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     keys = np.ascontiguousarray(keys, dtype=np.uint32)
     span = len(offsets) - 1
@@ -54,13 +55,13 @@ def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0
     if isinstance(metric, str):
         metric = METRICS.index(metric)
     L = lib()
-    ncand, nnan, nw, cnt = (ctypes.c_uint64() for _ in range(4))
+    ncand, nnan, nw, nwg, cnt = (ctypes.c_uint64() for _ in range(5))
     if max_edges is None:
         # first pass: count, so the output buffer can be sized exactly
         rc = L.nlpo_predict_range(offsets.ctypes.data, keys.ctypes.data, span, metric, hub,
                                   min_score, 0, u_begin, u_end, None, None, None,
                                   ctypes.byref(cnt), ctypes.byref(ncand), ctypes.byref(nnan),
-                                  ctypes.byref(nw))
+                                  ctypes.byref(nw), ctypes.byref(nwg))
         if rc:
             raise MemoryError("oracle allocation failed")
         max_edges = ncand.value
@@ -71,11 +72,11 @@ def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0
     rc = L.nlpo_predict_range(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, min_score,
                               int(max_edges), u_begin, u_end, ou.ctypes.data, ow.ctypes.data,
                               os_.ctypes.data, ctypes.byref(cnt), ctypes.byref(ncand),
-                              ctypes.byref(nnan), ctypes.byref(nw))
+                              ctypes.byref(nnan), ctypes.byref(nw), ctypes.byref(nwg))
     if rc:
         raise MemoryError("oracle allocation failed")
     n = cnt.value
-    info = dict(candidates=ncand.value, nan=nnan.value, wedges=nw.value)
+    info = dict(candidates=ncand.value, nan=nnan.value, wedges=nw.value, wedges_gt=nwg.value)
     return ou[:n].copy(), ow[:n].copy(), os_[:n].copy(), info
 
 
