@@ -15,6 +15,9 @@
 #include "../../include/nlp.h"
 #include "prims.hpp"
 #include "kernels.hpp"
+#include "lookback.hpp"
+#include "group.hpp"
+#include "select.hpp"
 
 using namespace nlp;
 
@@ -30,6 +33,16 @@ inline unsigned grid_for(uint64_t n) {
 }
 
 #define LAUNCH(kern, n, st, ...) hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(NT), 0, st, __VA_ARGS__)
+// one thread per item: for sparse latency-bound passes, where a grid-stride
+// loop would chain several items' dependent loads in one wave
+inline unsigned grid_full(uint64_t n) {
+  uint64_t g = (n + NT - 1) / NT;
+  return (unsigned)std::min<uint64_t>(std::max<uint64_t>(g, 1), 0x7fffffffull);
+}
+inline unsigned p1_grid(uint64_t S) {
+  return (unsigned)std::min<uint64_t>(std::max<uint64_t>((S + P1_TILE - 1) / P1_TILE, 1), 65535);
+}
+#define LAUNCH_FULL(kern, n, st, ...) hipLaunchKernelGGL(kern, dim3(grid_full(n)), dim3(NT), 0, st, __VA_ARGS__)
 
 // Buffer ids of the per-graph workspace.
 enum Buf {
@@ -41,6 +54,10 @@ enum Buf {
   B_TIE, B_TRANK, B_KEEP, B_KPOS,
   B_SK0, B_SK1, B_SV0, B_SV1,         // final sort
   B_HIST, B_HOFF, B_SCAN, B_SCAN2, B_SELHIST, B_SEL, B_CNT, B_EDGES,
+  // v1 pipeline
+  B_ARENA, B_ARENA2, B_VLIST, B_VIOFF, B_UCNT, B_UOFF, B_IEU, B_IEV, B_IEF, B_IEP, B_BUCKET,
+  B_SKEY, B_SU, B_SW, B_SS, B_SFLAG, B_BIG, B_OK0, B_OK1, B_OV0, B_OV1, B_NSORT,
+  B_FARENA, B_FAGG,
   NBUF
 };
 
@@ -101,6 +118,8 @@ struct nlp_graph {
   hipEvent_t ev[4] = {};
   Workspace ws;
   uint64_t wedge_budget = 0;
+  uint64_t capE = 1u << 20, capW = 1u << 20;  // path-1 capacities (grown on overflow)
+  bool force_radix = false;                    // test hook: NLP_FORCE_RADIX=1
 };
 
 namespace {
@@ -255,6 +274,7 @@ nlp_status finish_graph(nlp_graph* g) {
   TRY(hipMemGetInfo(&fr, &tot));
   uint64_t b = (uint64_t)(fr / 8 / 44);
   g->wedge_budget = std::max<uint64_t>(1u << 20, std::min<uint64_t>(b, 1ull << 30));
+  if (const char* fr = getenv("NLP_FORCE_RADIX")) g->force_radix = fr[0] == '1';
   // test hook: NLP_WEDGE_BUDGET forces path-2 chunking on small graphs
   if (const char* ev = getenv("NLP_WEDGE_BUDGET")) {
     unsigned long long v = strtoull(ev, nullptr, 10);
@@ -482,6 +502,218 @@ nlp_status count_nan(nlp_graph* g, Cands& C, hipStream_t st) {
   return NLP_OK;
 }
 
+
+// ================================================================ v1 pipeline
+// Arena layout (u64 words): [0,16) counters, [16,32) tickets (u32 pairs),
+// then look-back descriptors of the scans, each region tiles(n) words.
+struct Arena {
+  uint64_t* base = nullptr;
+  uint64_t words = 0;
+  uint64_t* ctr() const { return base; }
+  uint32_t* ticket(int i) const { return (uint32_t*)(base + 16) + i; }
+};
+
+inline uint64_t tiles_of(uint64_t n) { return (n + LB_TILE - 1) / LB_TILE + 1; }
+
+// zero the arena and set the initial counters (one kernel)
+nlp_status arena_init(nlp_graph* g, int id, uint64_t desc_words, Arena& A, const uint64_t* init, hipStream_t st) {
+  A.words = 32 + desc_words;
+  TRY(wsget(g->ws, id, A.words, &A.base));
+  CtrInit ci;
+  for (int i = 0; i < NCTR; ++i) ci.v[i] = init ? init[i] : 0;
+  hipLaunchKernelGGL(k_arena_init, dim3(std::min<uint64_t>(1024, (A.words + NT - 1) / NT)), dim3(NT), 0, st, A.base,
+                     A.words, ci);
+  TRY(hipGetLastError());
+  return NLP_OK;
+}
+
+GraphView view_of(nlp_graph* g, int metric) {
+  return GraphView{g->off, g->keys, g->deg, g->toff, g->tkeys, metric == M_AA ? g->ctab_aa : g->ctab_ra};
+}
+
+template <class F>
+hipError_t launch_scan(const F& f, const uint64_t* d_n, uint64_t n_upper, uint32_t* ticket, uint64_t* desc,
+                       uint32_t* err, uint64_t* total, hipStream_t st) {
+  LbState ls{ticket, desc, err};
+  hipLaunchKernelGGL(k_lb_scan<F>, dim3(lb_grid(n_upper)), dim3(NT), 0, st, f, d_n, ls, total);
+  return hipGetLastError();
+}
+
+struct StageBufs {
+  Stage st;
+  uint64_t* bucket;
+  uint32_t* big;
+};
+
+nlp_status stage_bufs(nlp_graph* g, uint64_t capW, uint64_t nbig, StageBufs& b) {
+  Workspace& ws = g->ws;
+  TRY(wsget(ws, B_BUCKET, capW, &b.bucket));
+  TRY(wsget(ws, B_SKEY, capW, &b.st.key));
+  TRY(wsget(ws, B_SU, capW, &b.st.u));
+  TRY(wsget(ws, B_SW, capW, &b.st.w));
+  TRY(wsget(ws, B_SS, capW, &b.st.s));
+  TRY(wsget(ws, B_SFLAG, capW, &b.st.flag));
+  TRY(wsget(ws, B_BIG, nbig, &b.big));
+  return NLP_OK;
+}
+
+// Make sure the candidate buffer holds `need` entries, preserving `keep`.
+nlp_status cand_reserve(nlp_graph* g, uint64_t need, uint64_t keep, hipStream_t st) {
+  Workspace& ws = g->ws;
+  if (need * 4 <= ws.bytes[B_CKEY] && need * 4 <= ws.bytes[B_CU] && need * 4 <= ws.bytes[B_CW] &&
+      need * 4 <= ws.bytes[B_CS])
+    return NLP_OK;
+  uint32_t *nk, *nu, *nw;
+  float* ns;
+  uint64_t cap = std::max<uint64_t>(need, 2 * keep);
+  TRY(wsget(ws, B_TKEY, cap, &nk));
+  TRY(wsget(ws, B_TU, cap, &nu));
+  TRY(wsget(ws, B_TW, cap, &nw));
+  TRY(wsget(ws, B_TS, cap, &ns));
+  if (keep) {
+    TRY(hipMemcpyAsync(nk, ws.p[B_CKEY], keep * 4, hipMemcpyDeviceToDevice, st));
+    TRY(hipMemcpyAsync(nu, ws.p[B_CU], keep * 4, hipMemcpyDeviceToDevice, st));
+    TRY(hipMemcpyAsync(nw, ws.p[B_CW], keep * 4, hipMemcpyDeviceToDevice, st));
+    TRY(hipMemcpyAsync(ns, ws.p[B_CS], keep * 4, hipMemcpyDeviceToDevice, st));
+  }
+  std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
+  std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
+  std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
+  std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  return NLP_OK;
+}
+
+// Path 1 (intermediate-centric) with per-source buckets.  F_OVERFLOW is
+// handled here by growing and re-running; F_TOOBIG is returned to the caller,
+// which then uses the radix path.  ucnt/cursor are kept all-zero between calls.
+nlp_status run_path1_v1(nlp_graph* g, const Params& p, Cands& C, uint64_t* flags_out, bool* over_budget,
+                        hipStream_t st) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  const GraphView gv = view_of(g, p.metric);
+  Workspace& ws = g->ws;
+  *over_budget = false;
+  // zero-invariant counters: allocate (and zero) once
+  if (ws.bytes[B_UCNT] < S * 4 || ws.bytes[B_IEP] < S * 4) {
+    uint32_t *a, *b;
+    TRY(wsget(ws, B_UCNT, S, &a));
+    TRY(wsget(ws, B_IEP, S, &b));
+    TRY(hipMemsetAsync(a, 0, S * 4, st));
+    TRY(hipMemsetAsync(b, 0, S * 4, st));
+  }
+  uint32_t* ucnt = (uint32_t*)ws.p[B_UCNT];
+  uint32_t* cursor = (uint32_t*)ws.p[B_IEP];
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    const uint64_t capW = g->capW;
+    uint64_t* uoff;
+    TRY(wsget(ws, B_UOFF, S, &uoff));
+    StageBufs sb;
+    nlp_status s = stage_bufs(g, capW, 0, sb);
+    if (s != NLP_OK) return s;
+    BigItem* big;
+    TRY(wsget(ws, B_BIG, std::max<uint64_t>(nU, 1), &big));
+    s = cand_reserve(g, capW, 0, st);
+    if (s != NLP_OK) return s;
+    uint32_t *ck = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
+    float* cs = (float*)ws.p[B_CS];
+    constexpr int IPT_S = 16, IPT_W = 4;
+    const uint64_t aU = (nU + NT * IPT_S - 1) / (NT * IPT_S) + 1, aW = (capW + NT * IPT_W - 1) / (NT * IPT_W) + 1;
+    Arena A;
+    uint64_t init[NCTR] = {};
+    init[C_N_URANGE] = nU;
+    init[10] = S;
+    s = arena_init(g, B_ARENA, 0, A, init, st);
+    if (s != NLP_OK) return s;
+    uint64_t* ctr = A.ctr();
+    uint64_t* aggs;
+    TRY(wsget(ws, B_ARENA2, aU + aW, &aggs));
+    uint64_t* gU = aggs;
+    uint64_t* gW = gU + aU;
+    hipLaunchKernelGGL(k_p1_pass<false>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, ucnt, (const uint64_t*)nullptr, capW, sb.bucket, ctr);
+    TRY(hipGetLastError());
+    TRY((rts_scan<F_UOff, IPT_S>(F_UOff{ucnt, uoff, ua}, &ctr[C_N_URANGE], nU, gU, &ctr[C_W], st)));
+    hipLaunchKernelGGL(k_p1_pass<true>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, cursor, (const uint64_t*)uoff, capW, sb.bucket, ctr);
+    TRY(hipGetLastError());
+    BucketsP1 bk{uoff, ucnt};
+    const unsigned gtiles = (unsigned)std::min<uint64_t>(std::max<uint64_t>((nU + GT_TILE - 1) / GT_TILE, 1), 65535);
+    if (custom) {
+      hipLaunchKernelGGL((k_group_tiles<BucketsP1, true>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                         p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
+      hipLaunchKernelGGL((k_group_big<true>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                         (const BigItem*)big, ctr);
+      LAUNCH_FULL(k_score_runs<true>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+    } else {
+      hipLaunchKernelGGL((k_group_tiles<BucketsP1, false>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                         p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
+      hipLaunchKernelGGL((k_group_big<false>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                         (const BigItem*)big, ctr);
+      LAUNCH_FULL(k_score_runs<false>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+    }
+    TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_clamp_n, dim3(1), dim3(64), 0, st, ctr, (uint64_t)C_W, capW, (uint64_t)11);
+    TRY((rts_scan<F_Compact, IPT_W>(F_Compact{sb.st, ck, cu, cw, cs, ctr, &ctr[C_NAN]}, &ctr[11], capW, gW,
+                                    &ctr[C_C], st)));
+    TRY(hipMemcpyAsync(g->host_small, ctr, NCTR * 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t* h = g->host_small;
+    if (h[C_FLAGS] & F_OVERFLOW) {
+      // the grouping did not run: counters are dirty
+      TRY(hipMemsetAsync(ucnt, 0, S * 4, st));
+      TRY(hipMemsetAsync(cursor, 0, S * 4, st));
+      uint64_t W = h[C_W];
+      if (W > g->wedge_budget) { *over_budget = true; return NLP_OK; }
+      if (W > g->capW) g->capW = W + W / 4 + 1024;
+      continue;
+    }
+    if (h[C_W] > g->wedge_budget) { *over_budget = true; return NLP_OK; }
+    *flags_out = h[C_FLAGS];
+    C.n = h[C_C];
+    C.total = h[C_C];
+    C.nan = h[C_NAN];
+    C.wedges += h[C_W];
+    return NLP_OK;
+  }
+  return NLP_ERR_DEVICE;
+}
+
+// Stable descending order of the candidate buffer by score key -> edges (onesweep).
+nlp_status order_v1(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
+  if (C.n == 0) return NLP_OK;
+  Workspace& ws = g->ws;
+  uint32_t *k0, *k1, *v0, *v1;
+  TRY(wsget(ws, B_OK0, C.n, &k0));
+  TRY(wsget(ws, B_OK1, C.n, &k1));
+  TRY(wsget(ws, B_OV0, C.n, &v0));
+  TRY(wsget(ws, B_OV1, C.n, &v1));
+  const uint64_t nt = (C.n + OS_TILE - 1) / OS_TILE;
+  Arena A;
+  uint64_t init[NCTR] = {};
+  init[0] = C.n;
+  nlp_status s = arena_init(g, B_ARENA2, 512 + 4 * nt * RS_BINS, A, init, st);
+  if (s != NLP_OK) return s;
+  uint64_t* ctr = A.ctr();
+  uint32_t* ghist = (uint32_t*)(A.base + 32);  // 4 x 256 u32 = 512 words... (uses 512 u64 of space)
+  uint64_t* desc = A.base + 32 + 512;
+  uint32_t* err = (uint32_t*)&ctr[1];
+  LAUNCH(k_desc_keys32, C.n, st, (const uint32_t*)ws.p[B_CKEY], C.n, k0, v0);
+  TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_os_hist, dim3(std::min<uint64_t>(64, grid_for(C.n))), dim3(NT), 0, st, k0, ctr, ghist);
+  TRY(hipGetLastError());
+  uint32_t *ka = k0, *va = v0, *kb = k1, *vb = v1;
+  for (int pass = 0; pass < 4; ++pass) {
+    hipLaunchKernelGGL(k_os_pass, dim3((unsigned)nt), dim3(NT), 0, st, ka, va, kb, vb, ctr, 8 * pass,
+                       ghist + pass * RS_BINS, A.ticket(pass), desc + (uint64_t)pass * nt * RS_BINS, err);
+    TRY(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  LAUNCH(k_gather_edges, C.n, st, va, C.n, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW],
+         (const float*)ws.p[B_CS], d_out);
+  TRY(hipGetLastError());
+  return NLP_OK;
+}
+
 // Path 1 generator: returns NLP_ERR_CAPACITY through *fits = false when the
 // wedge count exceeds the budget (then path 2 runs instead).
 nlp_status run_path1(nlp_graph* g, const Params& p, Cands& C, bool* fits, hipStream_t st) {
@@ -620,33 +852,220 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   return NLP_OK;
 }
 
+// ================================================================ fast path
+// Path 1 + selection + ordering enqueued with no host synchronisation: every
+// kernel reads its sizes from device counters and buffers are sized by the
+// wedge capacity.  The caller synchronises once and checks the flags.
+nlp_status enqueue_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, hipStream_t st, uint64_t** ctr_out) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  const GraphView gv = view_of(g, p.metric);
+  Workspace& ws = g->ws;
+  if (ws.bytes[B_UCNT] < S * 4 || ws.bytes[B_IEP] < S * 4) {
+    uint32_t *a, *b;
+    TRY(wsget(ws, B_UCNT, S, &a));
+    TRY(wsget(ws, B_IEP, S, &b));
+    TRY(hipMemsetAsync(a, 0, S * 4, st));
+    TRY(hipMemsetAsync(b, 0, S * 4, st));
+  }
+  uint32_t* ucnt = (uint32_t*)ws.p[B_UCNT];
+  uint32_t* cursor = (uint32_t*)ws.p[B_IEP];
+  const uint64_t capW = g->capW;
+  uint64_t* uoff;
+  TRY(wsget(ws, B_UOFF, S, &uoff));
+  StageBufs sb;
+  nlp_status s = stage_bufs(g, capW, 0, sb);
+  if (s != NLP_OK) return s;
+  BigItem* big;
+  TRY(wsget(ws, B_BIG, std::max<uint64_t>(nU, 1), &big));
+  s = cand_reserve(g, capW, 0, st);
+  if (s != NLP_OK) return s;
+  uint32_t *ck = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
+  float* cs = (float*)ws.p[B_CS];
+  uint32_t *tk, *tu, *tw, *k0, *k1, *v0, *v1;
+  float* ts;
+  uint64_t* trank;
+  TRY(wsget(ws, B_TKEY, capW, &tk));
+  TRY(wsget(ws, B_TU, capW, &tu));
+  TRY(wsget(ws, B_TW, capW, &tw));
+  TRY(wsget(ws, B_TS, capW, &ts));
+  TRY(wsget(ws, B_TRANK, capW, &trank));
+  TRY(wsget(ws, B_OK0, capW, &k0));
+  TRY(wsget(ws, B_OK1, capW, &k1));
+  TRY(wsget(ws, B_OV0, capW, &v0));
+  TRY(wsget(ws, B_OV1, capW, &v1));
+  constexpr int IPT_S = 16, IPT_W = 4;
+  const uint64_t aU = (nU + NT * IPT_S - 1) / (NT * IPT_S) + 1, aW = (capW + NT * IPT_W - 1) / (NT * IPT_W) + 1;
+  uint64_t* aggs;
+  TRY(wsget(ws, B_FAGG, aU + 3 * aW, &aggs));
+  uint64_t *gU = aggs, *gW = aggs + aU, *gT = gW + aW, *gK = gT + aW;
+  const uint64_t ntW = (capW + OS_TILE - 1) / OS_TILE + 1;
+  Arena A;
+  uint64_t init[NCTR] = {};
+  init[C_N_URANGE] = nU;
+  init[10] = S;
+  s = arena_init(g, B_FARENA, AR_DESC - 32 + 4 * ntW * RS_BINS, A, init, st);
+  if (s != NLP_OK) return s;
+  uint64_t* ctr = A.ctr();
+  uint64_t* sel = A.base + AR_SEL;
+  uint32_t* tickets = (uint32_t*)(A.base + AR_TICKETS);
+  uint32_t* selhist = (uint32_t*)(A.base + AR_SELHIST);
+  uint32_t* oshist = (uint32_t*)(A.base + AR_OSHIST);
+  uint64_t* desc = A.base + AR_DESC;
+  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+
+  TRY(hipEventRecord(g->ev[0], st));
+  // ---- candidates (path 1)
+  hipLaunchKernelGGL(k_p1_pass<false>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, ucnt, (const uint64_t*)nullptr, capW, sb.bucket, ctr);
+  TRY(hipGetLastError());
+  TRY((rts_scan<F_UOff, IPT_S>(F_UOff{ucnt, uoff, ua}, &ctr[C_N_URANGE], nU, gU, &ctr[C_W], st)));
+  hipLaunchKernelGGL(k_p1_pass<true>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, cursor, (const uint64_t*)uoff, capW, sb.bucket, ctr);
+  TRY(hipGetLastError());
+  BucketsP1 bk{uoff, ucnt};
+  const unsigned gtiles = (unsigned)std::min<uint64_t>(std::max<uint64_t>((nU + GT_TILE - 1) / GT_TILE, 1), 65535);
+  if (custom) {
+    hipLaunchKernelGGL((k_group_tiles<BucketsP1, true>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                       p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
+    hipLaunchKernelGGL((k_group_big<true>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                       (const BigItem*)big, ctr);
+    LAUNCH_FULL(k_score_runs<true>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+  } else {
+    hipLaunchKernelGGL((k_group_tiles<BucketsP1, false>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                       p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
+    hipLaunchKernelGGL((k_group_big<false>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                       (const BigItem*)big, ctr);
+    LAUNCH_FULL(k_score_runs<false>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+  }
+  TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_clamp_n, dim3(1), dim3(64), 0, st, ctr, (uint64_t)C_W, capW, (uint64_t)11);
+  TRY((rts_scan<F_Compact, IPT_W>(F_Compact{sb.st, ck, cu, cw, cs, ctr, &ctr[C_NAN]}, &ctr[11], capW, gW, &ctr[C_C],
+                                  st)));
+  TRY(hipEventRecord(g->ev[1], st));
+  // ---- top-k selection (only when candidates > max_edges; kernels no-op otherwise)
+  hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, st, ctr, sel, p.max_edges);
+  for (int pass = 0; pass < 3; ++pass) {
+    LAUNCH(k_sel_hist, capW, st, (const uint32_t*)ck, &ctr[C_SEL_N], pass, (const uint64_t*)sel, selhist);
+    hipLaunchKernelGGL(k_sel_pick2, dim3(1), dim3(NT), 0, st, selhist, pass, sel, (const uint64_t*)ctr);
+  }
+  TRY(hipGetLastError());
+  TRY((rts_scan<F_Sel, IPT_W>(F_Sel{ck, cu, cw, cs, sel, tk, tu, tw, ts}, &ctr[C_SEL_N], capW, gT, nullptr, st)));
+  (void)gK;
+  (void)trank;
+  // ---- canonical order: stable sort by score key descending
+  CandBufs ca{ck, cu, cw, cs}, cb{tk, tu, tw, ts};
+  LAUNCH(k_desc_keys_sel, capW, st, ca, cb, (const uint64_t*)ctr, k0, v0);
+  hipLaunchKernelGGL(k_os_hist, dim3(64), dim3(NT), 0, st, (const uint32_t*)k0, (const uint64_t*)&ctr[C_OUT_N], oshist);
+  TRY(hipGetLastError());
+  uint32_t *ka = k0, *va = v0, *kb = k1, *vb = v1;
+  for (int pass = 0; pass < 4; ++pass) {
+    hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntW), dim3(NT), 0, st, ka, va, kb, vb, (const uint64_t*)&ctr[C_OUT_N],
+                       8 * pass, oshist + pass * RS_BINS, tickets + pass, desc + (uint64_t)pass * ntW * RS_BINS, err);
+    TRY(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  LAUNCH(k_gather_sel, capW, st, (const uint32_t*)va, ca, cb, (const uint64_t*)ctr, d_out);
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(g->host_small, ctr, NCTR * 8, hipMemcpyDeviceToHost, st));
+  TRY(hipEventRecord(g->ev[2], st));
+  *ctr_out = ctr;
+  return NLP_OK;
+}
+
+// Run the fast path; *handled = false when the caller must use the general
+// flow (wedges beyond the budget, or a bucket beyond the LDS cap).
+nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
+                        hipStream_t st, EdgeOut** result, bool* handled) {
+  *handled = false;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    EdgeOut* out = d_out;
+    if (!out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(std::min(p.max_edges, g->capW), 1), &out));
+    uint64_t* ctr = nullptr;
+    nlp_status s = enqueue_fast(g, p, out, st, &ctr);
+    if (s != NLP_OK) return s;
+    TRY(hipEventSynchronize(g->ev[2]));
+    const uint64_t* h = g->host_small;
+    if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
+    if (h[C_FLAGS] & F_OVERFLOW) {
+      // the grouping did not run: its counters are dirty
+      TRY(hipMemsetAsync(g->ws.p[B_UCNT], 0, g->span * 4, st));
+      TRY(hipMemsetAsync(g->ws.p[B_IEP], 0, g->span * 4, st));
+      const uint64_t W = h[C_W];
+      if (W > g->wedge_budget) return NLP_OK;
+      g->capW = std::max(g->capW, W + W / 4 + 1024);
+      continue;
+    }
+    if ((h[C_FLAGS] & F_TOOBIG) || h[C_W] > g->wedge_budget) return NLP_OK;
+    *out_count = h[C_OUT_N];
+    if (result) *result = out;
+    if (t) {
+      float a = 0, b = 0;
+      TRY(hipEventElapsedTime(&a, g->ev[0], g->ev[1]));
+      TRY(hipEventElapsedTime(&b, g->ev[1], g->ev[2]));
+      t->score_ms = a;
+      t->select_ms = b;
+      t->total_ms = a + b;
+      t->wedges = h[C_W];
+      t->candidates = h[C_C];
+      t->nan_candidates = h[C_NAN];
+      t->path = 1;
+      t->chunks = 0;
+    }
+    *handled = true;
+    return NLP_OK;
+  }
+  return NLP_OK;
+}
+
 nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result) {
+  if (p.H > 0 && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
+    bool handled = false;
+    nlp_status s = predict_fast(g, p, d_out, out_count, t, st, result, &handled);
+    if (s != NLP_OK || handled) return s;
+  }
   Cands C;
   uint32_t path = 0, chunks = 0;
+  bool have_nan = false;
   TRY(hipEventRecord(g->ev[0], st));
   if (p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
-    bool fits = false;
-    if (p.H > 0) {
+    bool done = false;
+    if (p.H > 0 && !g->force_radix) {
+      uint64_t fl = 0;
+      bool over = false;
+      nlp_status s = run_path1_v1(g, p, C, &fl, &over, st);
+      if (s != NLP_OK) return s;
+      if (!over && !(fl & F_TOOBIG)) {
+        done = true;
+        path = 1;
+        have_nan = true;
+      } else {
+        C = Cands();
+      }
+    }
+    if (!done && p.H > 0) {  // intermediate-centric with the radix grouping (any bucket size)
+      bool fits = false;
       nlp_status s = run_path1(g, p, C, &fits, st);
       if (s != NLP_OK) return s;
-      if (fits) path = 1;
+      if (fits) { done = true; path = 3; } else C = Cands();
     }
-    if (!fits) {
-      C = Cands();
+    if (!done) {
       nlp_status s = run_path2(g, p, C, &chunks, st);
       if (s != NLP_OK) return s;
       path = 2;
     }
   }
   TRY(hipEventRecord(g->ev[1], st));
-  nlp_status s = count_nan(g, C, st);
-  if (s != NLP_OK) return s;
+  if (!have_nan) {
+    nlp_status s = count_nan(g, C, st);
+    if (s != NLP_OK) return s;
+  }
   uint64_t total = C.total, nan = C.nan;
-  s = prune_to(g, C, p.max_edges, st);
+  nlp_status s = prune_to(g, C, p.max_edges, st);
   if (s != NLP_OK) return s;
   if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.n, 1), &d_out));
-  s = order_into(g, C, d_out, st);
+  s = order_v1(g, C, d_out, st);
   if (s != NLP_OK) return s;
   TRY(hipEventRecord(g->ev[2], st));
   TRY(hipEventSynchronize(g->ev[2]));
@@ -813,7 +1232,7 @@ nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t 
   }
   nlp_status s = prune_to(g, C, max_edges, st);
   if (s != NLP_OK) return s;
-  s = order_into(g, C, (EdgeOut*)d_out, st);
+  s = order_v1(g, C, (EdgeOut*)d_out, st);
   if (s != NLP_OK) return s;
   TRY(hipStreamSynchronize(st));
   *out_count = C.n;

@@ -210,3 +210,47 @@ def test_gpu_full_size_c2_vs_oracle(gpu, oracle, nlp):
             assert n2 == n
             u2, w2, s2 = gpu.edges_from_tensor(out, n2)
             assert np.array_equal(u, u2) and np.array_equal(w, w2)
+
+
+def star_csr(leaves=12000):
+    """Hub 1 joined to `leaves` vertices of degree 2 (each also joined to its own
+    private vertex): vertex 1's bucket holds > 8192 wedges (LDS bucket cap)."""
+    n = 1 + 2 * leaves
+    rows = {1: list(range(2, 2 + leaves))}
+    for i in range(leaves):
+        a, b = 2 + i, 2 + leaves + i
+        rows.setdefault(a, []).extend([1, b])
+        rows.setdefault(b, []).append(a)
+    off = [0]
+    keys = []
+    for u in range(n + 1):
+        keys += sorted(rows.get(u, []))
+        off.append(len(keys))
+    return np.array(off, np.uint64), np.array(keys, np.uint32)
+
+
+def test_gpu_oversized_bucket_falls_back(gpu, oracle):
+    off, keys = star_csr()
+    with gpu.Graph(off, keys) as G:
+        for m, H, k in ((0, 2, 500), (7, 4, 20000), (1, 2, 10 ** 6)):
+            u, w, s, t = G.predict(m, H, k)
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+            assert t["path"] == 3
+
+
+def test_gpu_radix_path_equals_bucket_path(gpu, oracle):
+    off, keys = random_csr(6000, 16, 6)
+    k = 4000
+    with gpu.Graph(off, keys) as G1:
+        res1 = {(m, H): G1.predict(m, H, k) for m in range(9) for H in (1, 4, 32)}
+    try:
+        os.environ["NLP_FORCE_RADIX"] = "1"
+        with gpu.Graph(off, keys) as G3:
+            for (m, H), (u, w, s, t) in res1.items():
+                u3, w3, s3, t3 = G3.predict(m, H, k)
+                assert t["path"] in (1, 3) and t3["path"] == 3  # 3 also when a bucket exceeds the LDS cap
+                assert_canonical_equal(u3, w3, s3, u, w, s)
+                assert t["wedges"] == t3["wedges"] and t["candidates"] == t3["candidates"]
+    finally:
+        del os.environ["NLP_FORCE_RADIX"]
