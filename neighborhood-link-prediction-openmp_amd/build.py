@@ -38,14 +38,33 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
 
 
+CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "predict_main.cxx")
+CPP_TEST_BIN = os.path.join(HERE, "predict_main")
+
+
+def build_cpp_test(verbose=True):
+    """The C++ drop-in check (tests/cpp/predict_main.cxx) linked against libnlp.so."""
+    deps = [CPP_TEST_SRC, LIB, os.path.join(ROOT, "include", "nlp", "predict.hxx")]
+    if os.path.exists(CPP_TEST_BIN) and all(os.path.getmtime(d) <= os.path.getmtime(CPP_TEST_BIN) for d in deps):
+        return CPP_TEST_BIN
+    cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), CPP_TEST_SRC, "-L", HERE, "-lnlp",
+           "-Wl,-rpath," + HERE, "-o", CPP_TEST_BIN]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return CPP_TEST_BIN
+
+
 def build(force=False, verbose=True):
     if not force and not needs_build():
+        build_cpp_test(verbose)
         return LIB
     cmd = [hipcc()] + HIPCC_FLAGS + SOURCES + ["-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    build_cpp_test(verbose)
     return LIB
 
 

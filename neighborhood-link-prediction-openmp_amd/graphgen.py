@@ -17,14 +17,16 @@ Deletions follow the reference's sampling shape (batch.hxx:29-58, 99-112):
 a uniformly random vertex u in [1, n] (retried up to 5 times when deg(u)=0,
 _utility.hxx:432), then a uniformly random entry of N(u); both directions are
 deleted; duplicates are removed by tidy (batch.hxx:200-208).  Random numbers come
-from torch's generator, so the draws are not the reference's minstd_rand0
-sequence -- bit-exact replay of the reference's ingest is done by the oracle's
-ref_driver for the golden fixtures instead.
+from a counter-based splitmix64 stream, so the workload is bit-identical on the
+CPU and on any GPU (the draws are not the reference's minstd_rand0 sequence --
+bit-exact replay of the reference's ingest is done by the oracle's ref_driver
+for the golden fixtures instead).
 
 Everything is vectorised torch so it runs on the GPU (bench) or the CPU (tests).
 """
 import math
 
+import numpy as np
 import torch
 
 # SURVEY.md §8(d) stand-ins: name -> (n, m, alpha, graph_seed, deletion fraction, metric, hub)
@@ -37,32 +39,65 @@ CONFIGS = {
 }
 
 
-def _gen(seed, device):
-    g = torch.Generator(device=device)
-    g.manual_seed(int(seed))
-    return g
+_M64 = (1 << 64) - 1
+
+
+def _s64(c):
+    """uint64 constant as a signed int64 Python int (torch has no uint64 arithmetic)."""
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _srl(x, s):
+    """Logical right shift of int64 tensor values."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def splitmix64(x):
+    """splitmix64 finaliser on int64 tensors (wrapping arithmetic): a
+    counter-based generator, identical on CPU and GPU and independent of
+    launch geometry (torch's Philox offsets are not)."""
+    z = x + _s64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(z, 27)) * _s64(0x94D049BB133111EB)
+    return z ^ _srl(z, 31)
+
+
+def uniform(seed, stream, start, count, device):
+    """count doubles in [0, 1) for counter indices [start, start+count) of (seed, stream)."""
+    base = _s64(((seed * 0x100000001B3) ^ (stream * 0xC2B2AE3D27D4EB4F)) & _M64)
+    idx = torch.arange(start, start + count, dtype=torch.int64, device=device)
+    z = splitmix64(splitmix64(idx + base))
+    return _srl(z, 11).to(torch.float64) * (1.0 / (1 << 53))
+
+
+def permutation(n, seed, stream, device):
+    """Deterministic random permutation of 0..n-1 (argsort of random 64-bit keys)."""
+    base = _s64(((seed * 0x100000001B3) ^ (stream * 0xC2B2AE3D27D4EB4F)) & _M64)
+    k = splitmix64(torch.arange(n, dtype=torch.int64, device=device) + base)
+    return torch.sort(k, stable=True).indices
 
 
 def chung_lu_edges(n, m, alpha, seed, device="cpu"):
-    """Return (src, dst) int64 tensors of m distinct directed edges, ids in 1..n."""
-    g = _gen(seed, device)
-    w = torch.arange(1, n + 1, dtype=torch.float64, device=device).pow_(-alpha)
-    cdf = torch.cumsum(w, 0)
-    cdf /= cdf[-1].clone()
+    """Return (src, dst) int64 tensors of m distinct directed edges, ids in 1..n.
+
+    The CDF is computed on the host in float64 (sequential cumsum) so that every
+    device sees the same values; all random draws come from splitmix64."""
+    w = np.arange(1, n + 1, dtype=np.float64) ** (-alpha)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    cdf = torch.from_numpy(cdf).to(device)
     del w
-    perm = torch.randperm(n, generator=g, device=device) + 1
+    perm = permutation(n, seed, 1, device) + 1
     draws = int(m * 1.15) + 1024
     keys = []
     have = 0
-    # draw in chunks to bound peak memory
+    pos = 0  # counter position in the endpoint streams
     chunk = 1 << 26
     while True:
         todo = min(chunk, draws)
-        r = torch.rand(todo, generator=g, dtype=torch.float64, device=device)
-        u = torch.searchsorted(cdf, r).clamp_(max=n - 1)
-        r = torch.rand(todo, generator=g, dtype=torch.float64, device=device)
-        v = torch.searchsorted(cdf, r).clamp_(max=n - 1)
-        del r
+        u = torch.searchsorted(cdf, uniform(seed, 2, pos, todo, device)).clamp_(max=n - 1)
+        v = torch.searchsorted(cdf, uniform(seed, 3, pos, todo, device)).clamp_(max=n - 1)
+        pos += todo
         u = perm[u]
         v = perm[v]
         ok = u != v
@@ -78,7 +113,7 @@ def chung_lu_edges(n, m, alpha, seed, device="cpu"):
             have = 0
     allk = keys[0]
     if allk.numel() > m:
-        sel = torch.randperm(allk.numel(), generator=g, device=device)[:m]
+        sel = permutation(allk.numel(), seed, 4, device)[:m]
         allk = torch.sort(allk[sel]).values
     return allk // (n + 1), allk % (n + 1)
 
@@ -115,17 +150,16 @@ def delete_edges(offsets, keys, frac, seed, n=None):
     n = span - 1 if n is None else n
     M = keys.numel()
     D = int(frac * M / 2)
-    g = _gen(seed, dev)
     deg = offsets[1:] - offsets[:-1]
     # 5 tries per draw (retry(fn, 5), batch.hxx:110 / _utility.hxx:432)
     tries = 5
-    u = (1 + torch.floor(n * torch.rand(D, tries, generator=g, dtype=torch.float64, device=dev))).long()
+    u = (1 + torch.floor(n * uniform(seed, 5, 0, D * tries, dev).view(D, tries))).long()
     u.clamp_(max=span - 1)
     has = deg[u] > 0
     first = torch.argmax(has.to(torch.int8), dim=1)
     okrow = has.any(dim=1)
     u = u.gather(1, first[:, None])[:, 0][okrow]
-    r = torch.rand(u.numel(), generator=g, dtype=torch.float64, device=dev)
+    r = uniform(seed, 6, 0, u.numel(), dev)
     vi = torch.floor(r * deg[u].double()).long()
     v = keys[offsets[u] + vi].long()
     pairs = torch.unique(torch.cat([u * span + v, v * span + u]))

@@ -1,0 +1,91 @@
+"""The multi-GPU orchestration (dist.py) with world_size 2 over gloo on the
+CPU.  The per-rank device predictor is replaced by the oracle here (there is no
+GPU in this container); the shard ranges, the padded all_gather, the rank-order
+concatenation and the stable merge are the production code.  The result must
+equal the single-process canonical top-k exactly."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _edges_tensor(u, w, s):
+    a = np.zeros((len(u), 3), np.int32)
+    a[:, 0] = u.view(np.int32)
+    a[:, 1] = w.view(np.int32)
+    a[:, 2] = s.view(np.int32)
+    return torch.from_numpy(a)
+
+
+def _canonical_merge(allv, n, k):
+    """Reference merge rule: stable sort of the rank-ordered concatenation by
+    score key descending, first k (what nlp_select_edges_device computes)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from parity import keys_of
+    a = allv[:n].numpy()
+    s = a[:, 2].view(np.float32)
+    kk = keys_of(s).astype(np.int64)
+    order = np.lexsort((np.arange(len(kk)), -kk))[:k]
+    return torch.from_numpy(a[order].copy()), len(order)
+
+
+def _worker(rank, world, port, name, metric, hub, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import nlp_loader
+        import pyoracle
+        dmod = nlp_loader.load_sub("dist")
+        g = dict(np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"), allow_pickle=False))
+        off, keys, k = g["offsets"], g["keys"], int(g["k"][0])
+
+        def local(ub, ue):
+            u, w, s, info = pyoracle.predict(off, keys, metric, hub, max_edges=k, u_begin=ub, u_end=ue)
+            return _edges_tensor(u, w, s), len(u), info
+
+        out, n, info = dmod.predict_sharded(local, _canonical_merge, len(off) - 1, k)
+        q.put((rank, out[:n].numpy().copy(), info["shard"], info["counts"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,metric,hub", [("g3k", 1, 4), ("g3k", 7, 8), ("g300", 0, 0)])
+def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, metric, hub, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda x: x[0])
+    g = golden[name]
+    k = int(g["k"][0])
+    eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], metric, hub, max_edges=k)
+    for rank, a, shard, counts in res:
+        assert np.array_equal(a[:, 0].view(np.uint32), eu)
+        assert np.array_equal(a[:, 1].view(np.uint32), ew)
+        assert np.array_equal(a[:, 2].view(np.uint32), es.view(np.uint32))
+    assert res[0][2][1] == res[1][2][0]  # contiguous shards
+    assert sum(res[0][3]) >= len(eu)

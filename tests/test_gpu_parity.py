@@ -254,3 +254,23 @@ def test_gpu_radix_path_equals_bucket_path(gpu, oracle):
                 assert t["wedges"] == t3["wedges"] and t["candidates"] == t3["candidates"]
     finally:
         del os.environ["NLP_FORCE_RADIX"]
+
+
+def test_gpu_cpp_dropin_header(gpu, golden, oracle, tmp_path):
+    """main.cxx-style C++ caller of include/nlp/predict.hxx (tests/cpp/predict_main.cxx):
+    the reference's template names on a graph-concept type and on a resident
+    nlp::HipGraph agree, and equal the oracle for all nine metrics."""
+    import subprocess
+    from nlp_amd import build as b
+    exe = b.build_cpp_test(verbose=False)
+    g = golden["g3k"]
+    k = int(g["k"][0])
+    csr = str(tmp_path / "g.csr")
+    oracle.write_csr(csr, g["offsets"], g["keys"])
+    for H in (0, 4, 8):
+        pre = str(tmp_path / ("out%d" % H))
+        subprocess.run([exe, csr, str(H), str(k), pre], check=True, timeout=300)
+        for m in range(9):
+            u, w, s = oracle.read_edges(pre + "." + str(m))
+            eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
