@@ -87,6 +87,23 @@ def cpu_baseline(off, keys, metric, hub, k, ncand):
                 sample="full workload, oracle/nlp_oracle.c single thread")
 
 
+def pmc_traffic(config, world, metric, hub):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (tools/pmc_summary.py over tools/gpu_pmc.sh's separate FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command, corrected as
+    MI355X_MICROARCH.md's HBM section prescribes).  None when absent or for
+    another workload."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config or d.get("n_gpus") != world or d.get("metric") != metric or d.get("hub") != hub:
+        return None
+    return {"bytes_per_launch": d["kernels"]["k_group_tiles"]["traffic_bytes"], "source": d.get("source")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,12 +163,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     # per-phase device time of the library's own events, averaged over the timed steps
-    score_ms = select_ms = 0.0
+    score_ms = select_ms = hot_ms = 0.0
+    hot_bytes = replays = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         cnt = step()
         score_ms += last.get("score_ms", 0.0)
         select_ms += last.get("select_ms", 0.0)
+        hot_ms += last.get("hot_ms", 0.0)
+        hot_bytes += int(last.get("hot_bytes", 0))
+        replays += int(last.get("graph_replay", 0))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -166,13 +187,17 @@ def main():
         p, r, f1 = f1_on_device(out, cnt, du, dw, span)
         score_ms /= args.steps
         select_ms /= args.steps
-        # Roofline of the scoring phase (path 1), DESIGN.md §4: algorithmic bytes
-        # = degree scan 4*S + transposed offsets 8*(S+1) + in-lists, wedge keys and
-        # candidates; filled from the per-call counters.
+        # Roofline of the dominant kernel, k_group_tiles: its
+        # algorithmic bytes per launch (4*nU bucket counts + 8*W records + 4*W
+        # run flags + 12*C runs, from the call's own counters) over its device
+        # time, from the HIP events the library records around that launch on
+        # the stream it runs on, averaged over the timed steps.
         wedges = int(last.get("wedges", 0))
         cands = int(last.get("candidates", 0))
-        b_alg = 4 * span + 8 * (span + 1) + 12 * wedges + 16 * cands
-        achieved = b_alg / (score_ms * 1e-3) / 1e9 if score_ms > 0 else None
+        hot_ms /= args.steps
+        hot_bytes //= args.steps
+        achieved = hot_bytes / (hot_ms * 1e-3) / 1e9 if hot_ms > 0 else None
+        traffic = pmc_traffic(args.config, world, metric, hub)
         line = {
             "metric": "predicted edges/sec + F1, LHub Jaccard, 0.1|E| removed",
             "value": value,
@@ -195,8 +220,11 @@ def main():
             "wedges": wedges, "candidates": cands, "path": last.get("path"),
             "graph_gen_s": gen_s, "graph_create_s": create_s,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                         "kernel": "scoring phase (path 1)"},
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "kernel": "k_group_tiles", "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
+                         "traffic_source": traffic["source"] if traffic else None},
+            "graph_replay": replays == args.steps,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -88,6 +88,9 @@ typedef struct {
   uint64_t nan_candidates;  /* of which NaN */
   uint32_t path;            /* 1 = intermediate-centric, 2 = source-centric */
   uint32_t chunks;          /* source-range chunks used by path 2 */
+  float hot_ms;             /* device time of the dominant kernel (HIP events around its launch) */
+  uint32_t graph_replay;    /* 1 when the call replayed a captured hipGraph */
+  uint64_t hot_bytes;       /* algorithmic bytes of that launch */
 } nlp_timing;
 
 typedef struct nlp_graph nlp_graph;

@@ -115,11 +115,24 @@ struct nlp_graph {
   double* ctab_aa = nullptr;  // 1.0 / log((double)d), d = 0..maxdeg  (predict.hxx:788)
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
   uint64_t* host_small = nullptr;  // pinned counters
-  hipEvent_t ev[4] = {};
+  hipEvent_t ev[8] = {};
   Workspace ws;
   uint64_t wedge_budget = 0;
   uint64_t capE = 1u << 20, capW = 1u << 20;  // path-1 capacities (grown on overflow)
   bool force_radix = false;                    // test hook: NLP_FORCE_RADIX=1
+  bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
+  uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
+  struct Cached {
+    int metric;
+    uint32_t H;
+    float min_score;
+    uint64_t max_edges, ua, ub, capW, gen;
+    void* out;
+    hipGraphExec_t exec[4];
+    uint64_t last_use;
+  };
+  std::vector<Cached> graphs;
+  uint64_t use_clock = 0;
 };
 
 namespace {
@@ -158,6 +171,9 @@ void destroy_graph(nlp_graph* g) {
   if (!g) return;
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (auto& c : g->graphs)
+    for (auto& x : c.exec) (void)hipGraphExecDestroy(x);
+  g->graphs.clear();
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -168,7 +184,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->deg) (void)hipFree(g->deg);
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
     if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
   if (g->host_small) (void)hipHostFree(g->host_small);
   if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -275,6 +291,7 @@ nlp_status finish_graph(nlp_graph* g) {
   uint64_t b = (uint64_t)(fr / 8 / 44);
   g->wedge_budget = std::max<uint64_t>(1u << 20, std::min<uint64_t>(b, 1ull << 30));
   if (const char* fr = getenv("NLP_FORCE_RADIX")) g->force_radix = fr[0] == '1';
+  if (const char* ng = getenv("NLP_NO_GRAPH")) g->use_graphs = ng[0] != '1';
   // test hook: NLP_WEDGE_BUDGET forces path-2 chunking on small graphs
   if (const char* ev = getenv("NLP_WEDGE_BUDGET")) {
     unsigned long long v = strtoull(ev, nullptr, 10);
@@ -295,7 +312,7 @@ nlp_status new_graph(int device, nlp_graph** out) {
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
     if (hipEventCreate(&g->ev[i]) != hipSuccess) { destroy_graph(g); return NLP_ERR_DEVICE; }
   *out = g;
   return NLP_OK;
@@ -853,14 +870,33 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
 }
 
 // ================================================================ fast path
-// Path 1 + selection + ordering enqueued with no host synchronisation: every
-// kernel reads its sizes from device counters and buffers are sized by the
-// wedge capacity.  The caller synchronises once and checks the flags.
-nlp_status enqueue_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, hipStream_t st, uint64_t** ctr_out) {
+// Path 1 + selection + ordering with no host synchronisation: every kernel
+// reads its sizes from device counters and buffers are sized by the wedge
+// capacity.  prepare_fast allocates (never inside a capture); launch_fast only
+// launches, so it can be captured into a hipGraph and replayed.
+struct FastBufs {
+  uint32_t *ucnt, *cursor;
+  uint64_t* uoff;
+  StageBufs sb;
+  BigItem* big;
+  uint32_t *ck, *cu, *cw, *tk, *tu, *tw, *k0, *k1, *v0, *v1;
+  float *cs, *ts;
+  uint64_t *aggs, *arena;
+  uint64_t aU, aW, ntW, arena_words;
+};
+
+uint64_t ws_fingerprint(const Workspace& ws) {
+  uint64_t h = 1469598103934665603ull;
+  for (int i = 0; i < NBUF; ++i) {
+    h = (h ^ (uint64_t)(uintptr_t)ws.p[i]) * 1099511628211ull;
+    h = (h ^ (uint64_t)ws.bytes[i]) * 1099511628211ull;
+  }
+  return h;
+}
+
+nlp_status prepare_fast(nlp_graph* g, const Params& p, FastBufs& f, hipStream_t st) {
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
-  const bool custom = p.metric == M_AA || p.metric == M_RA;
-  const GraphView gv = view_of(g, p.metric);
   Workspace& ws = g->ws;
   if (ws.bytes[B_UCNT] < S * 4 || ws.bytes[B_IEP] < S * 4) {
     uint32_t *a, *b;
@@ -869,98 +905,119 @@ nlp_status enqueue_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, hipStream
     TRY(hipMemsetAsync(a, 0, S * 4, st));
     TRY(hipMemsetAsync(b, 0, S * 4, st));
   }
-  uint32_t* ucnt = (uint32_t*)ws.p[B_UCNT];
-  uint32_t* cursor = (uint32_t*)ws.p[B_IEP];
+  f.ucnt = (uint32_t*)ws.p[B_UCNT];
+  f.cursor = (uint32_t*)ws.p[B_IEP];
   const uint64_t capW = g->capW;
-  uint64_t* uoff;
-  TRY(wsget(ws, B_UOFF, S, &uoff));
-  StageBufs sb;
-  nlp_status s = stage_bufs(g, capW, 0, sb);
+  TRY(wsget(ws, B_UOFF, S, &f.uoff));
+  nlp_status s = stage_bufs(g, capW, 0, f.sb);
   if (s != NLP_OK) return s;
-  BigItem* big;
-  TRY(wsget(ws, B_BIG, std::max<uint64_t>(nU, 1), &big));
+  TRY(wsget(ws, B_BIG, std::max<uint64_t>(nU, 1), &f.big));
   s = cand_reserve(g, capW, 0, st);
   if (s != NLP_OK) return s;
-  uint32_t *ck = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
-  float* cs = (float*)ws.p[B_CS];
-  uint32_t *tk, *tu, *tw, *k0, *k1, *v0, *v1;
-  float* ts;
-  uint64_t* trank;
-  TRY(wsget(ws, B_TKEY, capW, &tk));
-  TRY(wsget(ws, B_TU, capW, &tu));
-  TRY(wsget(ws, B_TW, capW, &tw));
-  TRY(wsget(ws, B_TS, capW, &ts));
-  TRY(wsget(ws, B_TRANK, capW, &trank));
-  TRY(wsget(ws, B_OK0, capW, &k0));
-  TRY(wsget(ws, B_OK1, capW, &k1));
-  TRY(wsget(ws, B_OV0, capW, &v0));
-  TRY(wsget(ws, B_OV1, capW, &v1));
+  f.ck = (uint32_t*)ws.p[B_CKEY]; f.cu = (uint32_t*)ws.p[B_CU]; f.cw = (uint32_t*)ws.p[B_CW]; f.cs = (float*)ws.p[B_CS];
+  TRY(wsget(ws, B_TKEY, capW, &f.tk));
+  TRY(wsget(ws, B_TU, capW, &f.tu));
+  TRY(wsget(ws, B_TW, capW, &f.tw));
+  TRY(wsget(ws, B_TS, capW, &f.ts));
+  TRY(wsget(ws, B_OK0, capW, &f.k0));
+  TRY(wsget(ws, B_OK1, capW, &f.k1));
+  TRY(wsget(ws, B_OV0, capW, &f.v0));
+  TRY(wsget(ws, B_OV1, capW, &f.v1));
   constexpr int IPT_S = 16, IPT_W = 4;
-  const uint64_t aU = (nU + NT * IPT_S - 1) / (NT * IPT_S) + 1, aW = (capW + NT * IPT_W - 1) / (NT * IPT_W) + 1;
-  uint64_t* aggs;
-  TRY(wsget(ws, B_FAGG, aU + 3 * aW, &aggs));
-  uint64_t *gU = aggs, *gW = aggs + aU, *gT = gW + aW, *gK = gT + aW;
-  const uint64_t ntW = (capW + OS_TILE - 1) / OS_TILE + 1;
-  Arena A;
-  uint64_t init[NCTR] = {};
-  init[C_N_URANGE] = nU;
-  init[10] = S;
-  s = arena_init(g, B_FARENA, AR_DESC - 32 + 4 * ntW * RS_BINS, A, init, st);
-  if (s != NLP_OK) return s;
-  uint64_t* ctr = A.ctr();
-  uint64_t* sel = A.base + AR_SEL;
-  uint32_t* tickets = (uint32_t*)(A.base + AR_TICKETS);
-  uint32_t* selhist = (uint32_t*)(A.base + AR_SELHIST);
-  uint32_t* oshist = (uint32_t*)(A.base + AR_OSHIST);
-  uint64_t* desc = A.base + AR_DESC;
-  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  f.aU = (nU + NT * IPT_S - 1) / (NT * IPT_S) + 1;
+  f.aW = (capW + NT * IPT_W - 1) / (NT * IPT_W) + 1;
+  TRY(wsget(ws, B_FAGG, f.aU + 2 * f.aW, &f.aggs));
+  f.ntW = (capW + OS_TILE - 1) / OS_TILE + 1;
+  f.arena_words = AR_DESC + 4 * f.ntW * RS_BINS;
+  TRY(wsget(ws, B_FARENA, f.arena_words, &f.arena));
+  return NLP_OK;
+}
 
-  TRY(hipEventRecord(g->ev[0], st));
-  // ---- candidates (path 1)
-  hipLaunchKernelGGL(k_p1_pass<false>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, ucnt, (const uint64_t*)nullptr, capW, sb.bucket, ctr);
-  TRY(hipGetLastError());
-  TRY((rts_scan<F_UOff, IPT_S>(F_UOff{ucnt, uoff, ua}, &ctr[C_N_URANGE], nU, gU, &ctr[C_W], st)));
-  hipLaunchKernelGGL(k_p1_pass<true>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, cursor, (const uint64_t*)uoff, capW, sb.bucket, ctr);
-  TRY(hipGetLastError());
-  BucketsP1 bk{uoff, ucnt};
+// seg < 0 launches everything and records the timing events; seg = 0..3
+// launches one segment only (the hipGraph pieces; events go between them).
+nlp_status launch_fast(nlp_graph* g, const Params& p, const FastBufs& f, EdgeOut* d_out, hipStream_t st, int seg) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  const GraphView gv = view_of(g, p.metric);
+  const uint64_t capW = g->capW;
+  constexpr int IPT_S = 16, IPT_W = 4;
+  uint64_t *gU = f.aggs, *gW = f.aggs + f.aU, *gT = gW + f.aW;
+  uint64_t* ctr = f.arena;
+  uint64_t* sel = f.arena + AR_SEL;
+  uint32_t* tickets = (uint32_t*)(f.arena + AR_TICKETS);
+  uint32_t* selhist = (uint32_t*)(f.arena + AR_SELHIST);
+  uint32_t* oshist = (uint32_t*)(f.arena + AR_OSHIST);
+  uint64_t* desc = f.arena + AR_DESC;
+  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  const StageBufs& sb = f.sb;
+  CtrInit ci;
+  for (int i = 0; i < NCTR; ++i) ci.v[i] = 0;
+  ci.v[C_N_URANGE] = nU;
+  ci.v[10] = S;
+  BucketsP1 bk{f.uoff, f.ucnt};
   const unsigned gtiles = (unsigned)std::min<uint64_t>(std::max<uint64_t>((nU + GT_TILE - 1) / GT_TILE, 1), 65535);
-  if (custom) {
-    hipLaunchKernelGGL((k_group_tiles<BucketsP1, true>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
-                       p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
-    hipLaunchKernelGGL((k_group_big<true>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
-                       (const BigItem*)big, ctr);
-    LAUNCH_FULL(k_score_runs<true>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
-  } else {
-    hipLaunchKernelGGL((k_group_tiles<BucketsP1, false>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
-                       p.min_score, sb.bucket, capW, sb.st, big, ctr, ucnt, cursor);
-    hipLaunchKernelGGL((k_group_big<false>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
-                       (const BigItem*)big, ctr);
-    LAUNCH_FULL(k_score_runs<false>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+  if (seg < 0) TRY(hipEventRecord(g->ev[0], st));
+  if (seg < 0 || seg == 0) {
+    hipLaunchKernelGGL(k_arena_init, dim3(std::min<uint64_t>(1024, (f.arena_words + NT - 1) / NT)), dim3(NT), 0, st,
+                       f.arena, f.arena_words, ci);
+    // ---- candidates (path 1)
+    hipLaunchKernelGGL(k_p1_pass<false>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, f.ucnt,
+                       (const uint64_t*)nullptr, capW, sb.bucket, ctr);
+    TRY(hipGetLastError());
+    TRY((rts_scan<F_UOff, IPT_S>(F_UOff{f.ucnt, f.uoff, ua}, &ctr[C_N_URANGE], nU, gU, &ctr[C_W], st)));
+    hipLaunchKernelGGL(k_p1_pass<true>, dim3(p1_grid(S)), dim3(NT), 0, st, gv, S, p.H, ua, ub, f.cursor,
+                       (const uint64_t*)f.uoff, capW, sb.bucket, ctr);
+    TRY(hipGetLastError());
+  }
+  if (seg < 0) TRY(hipEventRecord(g->ev[3], st));
+  if (seg < 0 || seg == 1) {
+    if (custom)
+      hipLaunchKernelGGL((k_group_tiles<BucketsP1, true>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                         p.min_score, sb.bucket, capW, sb.st, f.big, ctr, f.ucnt, f.cursor);
+    else
+      hipLaunchKernelGGL((k_group_tiles<BucketsP1, false>), dim3(gtiles), dim3(NT), 0, st, gv, bk, ua, ub, p.metric,
+                         p.min_score, sb.bucket, capW, sb.st, f.big, ctr, f.ucnt, f.cursor);
+    TRY(hipGetLastError());
+  }
+  if (seg < 0) TRY(hipEventRecord(g->ev[4], st));
+  if (seg < 0 || seg == 2) {
+    if (custom) {
+      hipLaunchKernelGGL((k_group_big<true>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                         (const BigItem*)f.big, ctr);
+      LAUNCH_FULL(k_score_runs<true>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
+    } else {
+      hipLaunchKernelGGL((k_group_big<false>), dim3(256), dim3(NT), 0, st, gv, p.metric, p.min_score, sb.bucket, sb.st,
+                         (const BigItem*)f.big, ctr);
+      LAUNCH_FULL(k_score_runs<false>, capW, st, gv, p.metric, p.min_score, ctr, capW, sb.st);
   }
   TRY(hipGetLastError());
   hipLaunchKernelGGL(k_clamp_n, dim3(1), dim3(64), 0, st, ctr, (uint64_t)C_W, capW, (uint64_t)11);
-  TRY((rts_scan<F_Compact, IPT_W>(F_Compact{sb.st, ck, cu, cw, cs, ctr, &ctr[C_NAN]}, &ctr[11], capW, gW, &ctr[C_C],
-                                  st)));
-  TRY(hipEventRecord(g->ev[1], st));
-  // ---- top-k selection (only when candidates > max_edges; kernels no-op otherwise)
-  hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, st, ctr, sel, p.max_edges);
-  for (int pass = 0; pass < 3; ++pass) {
-    LAUNCH(k_sel_hist, capW, st, (const uint32_t*)ck, &ctr[C_SEL_N], pass, (const uint64_t*)sel, selhist);
-    hipLaunchKernelGGL(k_sel_pick2, dim3(1), dim3(NT), 0, st, selhist, pass, sel, (const uint64_t*)ctr);
+  TRY((rts_scan<F_Compact, IPT_W>(F_Compact{sb.st, f.ck, f.cu, f.cw, f.cs, ctr, &ctr[C_NAN]}, &ctr[11], capW, gW,
+                                  &ctr[C_C], st)));
+  }
+  if (seg < 0) TRY(hipEventRecord(g->ev[1], st));
+  if (seg < 0 || seg == 3) {
+    // ---- top-k selection (only when candidates > max_edges; kernels no-op otherwise)
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(64), 0, st, ctr, sel, p.max_edges);
+    for (int pass = 0; pass < 3; ++pass) {
+      LAUNCH(k_sel_hist, capW, st, (const uint32_t*)f.ck, &ctr[C_SEL_N], pass, (const uint64_t*)sel, selhist);
+      hipLaunchKernelGGL(k_sel_pick2, dim3(1), dim3(NT), 0, st, selhist, pass, sel, (const uint64_t*)ctr);
   }
   TRY(hipGetLastError());
-  TRY((rts_scan<F_Sel, IPT_W>(F_Sel{ck, cu, cw, cs, sel, tk, tu, tw, ts}, &ctr[C_SEL_N], capW, gT, nullptr, st)));
-  (void)gK;
-  (void)trank;
+  TRY((rts_scan<F_Sel, IPT_W>(F_Sel{f.ck, f.cu, f.cw, f.cs, sel, f.tk, f.tu, f.tw, f.ts}, &ctr[C_SEL_N], capW, gT,
+                              nullptr, st)));
   // ---- canonical order: stable sort by score key descending
-  CandBufs ca{ck, cu, cw, cs}, cb{tk, tu, tw, ts};
-  LAUNCH(k_desc_keys_sel, capW, st, ca, cb, (const uint64_t*)ctr, k0, v0);
-  hipLaunchKernelGGL(k_os_hist, dim3(64), dim3(NT), 0, st, (const uint32_t*)k0, (const uint64_t*)&ctr[C_OUT_N], oshist);
+  CandBufs ca{f.ck, f.cu, f.cw, f.cs}, cb{f.tk, f.tu, f.tw, f.ts};
+  LAUNCH(k_desc_keys_sel, capW, st, ca, cb, (const uint64_t*)ctr, f.k0, f.v0);
+  hipLaunchKernelGGL(k_os_hist, dim3(64), dim3(NT), 0, st, (const uint32_t*)f.k0, (const uint64_t*)&ctr[C_OUT_N],
+                     oshist);
   TRY(hipGetLastError());
-  uint32_t *ka = k0, *va = v0, *kb = k1, *vb = v1;
+  uint32_t *ka = f.k0, *va = f.v0, *kb = f.k1, *vb = f.v1;
   for (int pass = 0; pass < 4; ++pass) {
-    hipLaunchKernelGGL(k_os_pass, dim3((unsigned)ntW), dim3(NT), 0, st, ka, va, kb, vb, (const uint64_t*)&ctr[C_OUT_N],
-                       8 * pass, oshist + pass * RS_BINS, tickets + pass, desc + (uint64_t)pass * ntW * RS_BINS, err);
+    hipLaunchKernelGGL(k_os_pass, dim3((unsigned)f.ntW), dim3(NT), 0, st, ka, va, kb, vb,
+                       (const uint64_t*)&ctr[C_OUT_N], 8 * pass, oshist + pass * RS_BINS, tickets + pass,
+                       desc + (uint64_t)pass * f.ntW * RS_BINS, err);
     TRY(hipGetLastError());
     std::swap(ka, kb);
     std::swap(va, vb);
@@ -968,8 +1025,66 @@ nlp_status enqueue_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, hipStream
   LAUNCH(k_gather_sel, capW, st, (const uint32_t*)va, ca, cb, (const uint64_t*)ctr, d_out);
   TRY(hipGetLastError());
   TRY(hipMemcpyAsync(g->host_small, ctr, NCTR * 8, hipMemcpyDeviceToHost, st));
+  }
+  if (seg < 0) TRY(hipEventRecord(g->ev[2], st));
+  return NLP_OK;
+}
+
+// Replay (or capture, then replay) the fast path as hipGraphs.  The pipeline
+// is captured as four segments on the graph's own stream and replayed on the
+// caller's stream with the timing events recorded between them (events inside
+// a graph cannot be timed), so hot_ms stays a live measurement.  *replayed =
+// false when graphs are disabled or capture failed (the caller then launches
+// directly).
+nlp_status run_fast_graph(nlp_graph* g, const Params& p, const FastBufs& f, EdgeOut* out, hipStream_t st,
+                          bool* replayed) {
+  *replayed = false;
+  if (!g->use_graphs) return NLP_OK;
+  const uint64_t gen = ws_fingerprint(g->ws);
+  nlp_graph::Cached* hit = nullptr;
+  for (auto& c : g->graphs)
+    if (c.metric == p.metric && c.H == p.H && c.min_score == p.min_score && c.max_edges == p.max_edges &&
+        c.ua == p.ua && c.ub == p.ub && c.capW == g->capW && c.gen == gen && c.out == (void*)out)
+      hit = &c;
+  if (!hit) {
+    nlp_graph::Cached c{p.metric, p.H, p.min_score, p.max_edges, p.ua, p.ub, g->capW, gen, (void*)out, {}, 0};
+    hipStream_t gs = g->stream;
+    bool ok = true;
+    for (int seg = 0; seg < 4 && ok; ++seg) {
+      hipGraph_t graph = nullptr;
+      c.exec[seg] = nullptr;
+      if (hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal) != hipSuccess) { ok = false; break; }
+      nlp_status s = launch_fast(g, p, f, out, gs, seg);
+      hipError_t e = hipStreamEndCapture(gs, &graph);
+      ok = s == NLP_OK && e == hipSuccess && graph;
+      if (ok) ok = hipGraphInstantiate(&c.exec[seg], graph, nullptr, nullptr, 0) == hipSuccess;
+      if (graph) (void)hipGraphDestroy(graph);
+    }
+    if (!ok) {
+      for (auto& x : c.exec)
+        if (x) (void)hipGraphExecDestroy(x);
+      (void)hipGetLastError();
+      g->use_graphs = false;
+      return NLP_OK;
+    }
+    if (g->graphs.size() >= 32) {  // evict the least recently used
+      size_t lru = 0;
+      for (size_t i = 1; i < g->graphs.size(); ++i)
+        if (g->graphs[i].last_use < g->graphs[lru].last_use) lru = i;
+      for (auto& x : g->graphs[lru].exec) (void)hipGraphExecDestroy(x);
+      g->graphs.erase(g->graphs.begin() + lru);
+    }
+    g->graphs.push_back(c);
+    hit = &g->graphs.back();
+  }
+  hit->last_use = ++g->use_clock;
+  static const int ev_before[4] = {0, 3, 4, 1};
+  for (int seg = 0; seg < 4; ++seg) {
+    TRY(hipEventRecord(g->ev[ev_before[seg]], st));
+    TRY(hipGraphLaunch(hit->exec[seg], st));
+  }
   TRY(hipEventRecord(g->ev[2], st));
-  *ctr_out = ctr;
+  *replayed = true;
   return NLP_OK;
 }
 
@@ -981,9 +1096,16 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   for (int attempt = 0; attempt < 3; ++attempt) {
     EdgeOut* out = d_out;
     if (!out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(std::min(p.max_edges, g->capW), 1), &out));
-    uint64_t* ctr = nullptr;
-    nlp_status s = enqueue_fast(g, p, out, st, &ctr);
+    FastBufs f;
+    nlp_status s = prepare_fast(g, p, f, st);
     if (s != NLP_OK) return s;
+    bool replayed = false;
+    s = run_fast_graph(g, p, f, out, st, &replayed);
+    if (s != NLP_OK) return s;
+    if (!replayed) {
+      s = launch_fast(g, p, f, out, st, -1);
+      if (s != NLP_OK) return s;
+    }
     TRY(hipEventSynchronize(g->ev[2]));
     const uint64_t* h = g->host_small;
     if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
@@ -1000,9 +1122,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     *out_count = h[C_OUT_N];
     if (result) *result = out;
     if (t) {
-      float a = 0, b = 0;
+      float a = 0, b = 0, hot = 0;
       TRY(hipEventElapsedTime(&a, g->ev[0], g->ev[1]));
       TRY(hipEventElapsedTime(&b, g->ev[1], g->ev[2]));
+      TRY(hipEventElapsedTime(&hot, g->ev[3], g->ev[4]));
+      const uint64_t nU = std::min(p.ub, g->span) - std::min(p.ua, g->span);
       t->score_ms = a;
       t->select_ms = b;
       t->total_ms = a + b;
@@ -1011,6 +1135,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->nan_candidates = h[C_NAN];
       t->path = 1;
       t->chunks = 0;
+      t->hot_ms = hot;
+      t->graph_replay = replayed ? 1u : 0u;
+      // k_group_tiles: bucket counts, records, flags, runs
+      t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
     }
     *handled = true;
     return NLP_OK;

@@ -274,3 +274,31 @@ def test_gpu_cpp_dropin_header(gpu, golden, oracle, tmp_path):
             u, w, s = oracle.read_edges(pre + "." + str(m))
             eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], m, H, max_edges=k)
             assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_graph_replay_equals_direct_launch(gpu, oracle):
+    """The sync-free path is captured once per (metric, H, k, range, buffers)
+    and replayed as hipGraphs; replays must equal the directly launched run and
+    the oracle, across interleaved cache entries and a capacity regrow."""
+    off, keys = random_csr(6000, 14, 5)
+    runs = [(1, 4, 400), (7, 4, 400), (1, 4, 400), (0, 8, 50), (7, 4, 400), (1, 4, 400)]
+    with gpu.Graph(off, keys) as G:
+        seen = {}
+        for m, H, k in runs:
+            u, w, s, t = G.predict(m, H, k)
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+            if t["path"] == 1 and (m, H, k) in seen:
+                assert t["graph_replay"] == 1
+            seen[(m, H, k)] = True
+            assert t["hot_ms"] > 0 and t["hot_bytes"] > 0
+    try:
+        os.environ["NLP_NO_GRAPH"] = "1"
+        with gpu.Graph(off, keys) as G:
+            for m, H, k in runs[:3]:
+                u, w, s, t = G.predict(m, H, k)
+                assert t["graph_replay"] == 0
+                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                assert_canonical_equal(eu, ew, es, u, w, s)
+    finally:
+        del os.environ["NLP_NO_GRAPH"]
