@@ -18,6 +18,7 @@
 #include "lookback.hpp"
 #include "group.hpp"
 #include "select.hpp"
+#include "sortpath.hpp"
 
 using namespace nlp;
 
@@ -58,6 +59,9 @@ enum Buf {
   B_ARENA, B_ARENA2, B_VLIST, B_VIOFF, B_UCNT, B_UOFF, B_IEU, B_IEV, B_IEF, B_IEP, B_BUCKET,
   B_SKEY, B_SU, B_SW, B_SS, B_SFLAG, B_BIG, B_OK0, B_OK1, B_OV0, B_OV1, B_NSORT,
   B_FARENA, B_FAGG,
+  // sort-grouped fast path (sortpath.hpp)
+  B_SP_SURV, B_SP_RK0, B_SP_RK1, B_SP_RV0, B_SP_RV1, B_SP_STASH, B_SP_CU, B_SP_CW, B_SP_CS,
+  B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
   NBUF
 };
 
@@ -120,6 +124,10 @@ struct nlp_graph {
   uint64_t wedge_budget = 0;
   uint64_t capE = 1u << 20, capW = 1u << 20;  // path-1 capacities (grown on overflow)
   bool force_radix = false;                    // test hook: NLP_FORCE_RADIX=1
+  bool sort_grouping = true;                   // NLP_GROUPING=bucket selects the per-source bucket grouping
+  int hot_stage = 2;                           // sort path: stage timed as the dominant kernel (k_sp_expand)
+  // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
+  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256;
   bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
   struct Cached {
@@ -296,6 +304,26 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ev = getenv("NLP_WEDGE_BUDGET")) {
     unsigned long long v = strtoull(ev, nullptr, 10);
     if (v > 0) g->wedge_budget = v;
+  }
+  if (const char* gr = getenv("NLP_GROUPING")) g->sort_grouping = strcmp(gr, "bucket") != 0;
+  {
+    hipDeviceProp_t prop;
+    TRY(hipGetDeviceProperties(&prop, g->device));
+    const unsigned cus = (unsigned)std::max(prop.multiProcessorCount, 1);
+    auto occ = [&](const void* k, unsigned* out) -> hipError_t {
+      int nb = 0;
+      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, NT, 0);
+      if (e == hipSuccess) *out = cus * (unsigned)std::max(nb, 1);
+      return e;
+    };
+    TRY(occ((const void*)k_sp_survivors, &g->occ_surv));
+    TRY(occ((const void*)k_sp_expand, &g->occ_exp));
+    TRY(occ((const void*)k_sp_pass<uint64_t>, &g->occ_p64));
+    TRY(occ((const void*)k_sp_pass<uint32_t>, &g->occ_p32));
+    unsigned a = 0, b = 0;
+    TRY(occ((const void*)k_sp_scan<F_Runs<true>, RN_IPT>, &a));
+    TRY(occ((const void*)k_sp_scan<F_Runs<false>, RN_IPT>, &b));
+    g->occ_run = std::min(a, b);
   }
   g->ws.release();  // drop build scratch; predict grows its own
   return NLP_OK;
@@ -1030,14 +1058,173 @@ nlp_status launch_fast(nlp_graph* g, const Params& p, const FastBufs& f, EdgeOut
   return NLP_OK;
 }
 
-// Replay (or capture, then replay) the fast path as hipGraphs.  The pipeline
-// is captured as four segments on the graph's own stream and replayed on the
+// ---------------------------------------------------------------- sort-grouped fast path
+struct SpBufs {
+  uint32_t* surv;
+  uint64_t *rk0, *rk1;
+  uint32_t *rv0, *rv1, *cu, *cw, *ok0, *ok1, *ov0, *ov1;
+  float *stash, *cs;
+  uint64_t* arena;
+  uint64_t arena_words;
+  uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
+  uint64_t ostride;                             // u32 onesweep descriptors per pass
+  int wbits, passes;
+};
+
+inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 1)
+  int b = 1;
+  while (b < 64 && (x >> b)) ++b;
+  return b;
+}
+
+nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
+  const uint64_t capW = g->capW;
+  Workspace& ws = g->ws;
+  TRY(wsget(ws, B_SP_SURV, S, &f.surv));
+  TRY(wsget(ws, B_SP_RK0, capW, &f.rk0));
+  TRY(wsget(ws, B_SP_RK1, capW, &f.rk1));
+  TRY(wsget(ws, B_SP_RV0, capW, &f.rv0));
+  TRY(wsget(ws, B_SP_RV1, capW, &f.rv1));
+  TRY(wsget(ws, B_SP_STASH, capW, &f.stash));
+  TRY(wsget(ws, B_SP_CU, capW, &f.cu));
+  TRY(wsget(ws, B_SP_CW, capW, &f.cw));
+  TRY(wsget(ws, B_SP_CS, capW, &f.cs));
+  TRY(wsget(ws, B_SP_OK0, capW, &f.ok0));
+  TRY(wsget(ws, B_SP_OK1, capW, &f.ok1));
+  TRY(wsget(ws, B_SP_OV0, capW, &f.ov0));
+  TRY(wsget(ws, B_SP_OV1, capW, &f.ov1));
+  f.wbits = key_bits(S ? S - 1 : 0);
+  const int ubits = key_bits(ub > ua ? ub - ua - 1 : 0);
+  f.passes = (f.wbits + ubits + 7) / 8;
+  const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + EX_TILE - 1) / EX_TILE;
+  const uint64_t tR = (capW + RN_TILE - 1) / RN_TILE, tO = (capW + OS2_TILE - 1) / OS2_TILE;
+  f.ostride = tO * RS_BINS;
+  f.d_surv = SP_DESC;
+  f.d_exp = f.d_surv + tS + 1;
+  f.d_run = f.d_exp + tE + 1;
+  f.d_rec = f.d_run + tR + 1;
+  f.d_ord = f.d_rec + ((uint64_t)f.passes * f.ostride + 1) / 2;
+  f.arena_words = f.d_ord + (4 * f.ostride + 1) / 2;
+  TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
+  return NLP_OK;
+}
+
+// Algorithmic bytes of one launch of sort-path stage `s`,
+// from the call's own counters (host copy of the arena counters).
+uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64_t* h) {
+  const uint64_t S = g->span, V = h[C_NV], W = h[C_W], C = h[C_C];
+  if (s == 1) return 4 * S + 4 * V;             // deg read, survivor ids written
+  if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
+  if (s >= 4 && s < 4 + f.passes) return 24 * W;  // records in + out
+  if (s == 4 + f.passes) return 12 * W + 4 * W + 20 * C;  // records (+stash), candidates
+  return 0;
+}
+
+// The sort path as an ordered list of stages; seg < 0 launches all stages and
+// records the events, seg = 0..3 launches one capture segment:
+// [0, hot) | hot | (hot, runs] | (runs, end].
+nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* out, hipStream_t st, int seg) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
+  const uint64_t capW = g->capW;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  const GraphView gv = view_of(g, p.metric);
+  uint64_t* ctr = f.arena;
+  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  uint32_t* hrec = (uint32_t*)(f.arena + SP_HREC);
+  uint32_t* hord = (uint32_t*)(f.arena + SP_HORD);
+  uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
+  uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
+  const int P = f.passes;
+  const int s_runs = 4 + P, n_st = s_runs + 7;
+  const int hot = std::min(std::max(g->hot_stage, 1), s_runs);
+  auto grid = [](uint64_t tiles, unsigned occ) {
+    return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, occ)));
+  };
+  const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
+  // sorted records / candidate order end up in buffer 0 after an even number of passes
+  uint64_t* rks = (P & 1) ? f.rk1 : f.rk0;
+  uint32_t* rvs = (P & 1) ? f.rv1 : f.rv0;
+  auto stage = [&](int s) -> nlp_status {
+    if (s == 0) {
+      CtrInit ci;
+      for (int i = 0; i < NCTR; ++i) ci.v[i] = 0;
+      hipLaunchKernelGGL(k_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (f.arena_words + NT - 1) / NT)),
+                         dim3(NT), 0, st, f.arena, f.arena_words, ci);
+    } else if (s == 1) {
+      hipLaunchKernelGGL(k_sp_survivors, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
+                         (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, ctr);
+    } else if (s == 2) {
+      hipLaunchKernelGGL(k_sp_expand, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua, ub,
+                         f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr);
+    } else if (s == 3) {
+      hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, st, (const uint64_t*)f.rk0,
+                         (const uint64_t*)&ctr[C_W], capW, P, hrec, &ctr[C_WSORT], &ctr[C_FLAGS]);
+    } else if (s < s_runs) {
+      const int ps = s - 4;
+      const bool odd = ps & 1;
+      hipLaunchKernelGGL(k_sp_pass<uint64_t>, grid(tO, g->occ_p64), dim3(NT), 0, st,
+                         (const uint64_t*)(odd ? f.rk1 : f.rk0), (const uint32_t*)(odd ? f.rv1 : f.rv0),
+                         odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT], 8 * ps,
+                         (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err);
+    } else if (s == s_runs) {
+      const dim3 gr = grid((capW + RN_TILE - 1) / RN_TILE, g->occ_run);
+      if (custom) {
+        F_Runs<true> fr{gv, p.metric, p.min_score, ua, f.wbits, rks, rvs, f.stash, f.cu, f.cw, f.cs, f.ok0, f.ov0,
+                        &ctr[C_NAN]};
+        hipLaunchKernelGGL((k_sp_scan<F_Runs<true>, RN_IPT>), gr, dim3(NT), 0, st, fr, (const uint64_t*)&ctr[C_WSORT],
+                           f.arena + f.d_run, err, &ctr[C_C]);
+      } else {
+        F_Runs<false> fr{gv, p.metric, p.min_score, ua, f.wbits, rks, rvs, f.stash, f.cu, f.cw, f.cs, f.ok0, f.ov0,
+                         &ctr[C_NAN]};
+        hipLaunchKernelGGL((k_sp_scan<F_Runs<false>, RN_IPT>), gr, dim3(NT), 0, st, fr,
+                           (const uint64_t*)&ctr[C_WSORT], f.arena + f.d_run, err, &ctr[C_C]);
+      }
+    } else if (s == s_runs + 1) {
+      hipLaunchKernelGGL(k_sp_hist<uint32_t>, dim3(128), dim3(NT), 0, st, (const uint32_t*)f.ok0,
+                         (const uint64_t*)&ctr[C_C], capW, 4, hord, (uint64_t*)nullptr, (uint64_t*)nullptr);
+    } else if (s < s_runs + 6) {
+      const int ps = s - (s_runs + 2);
+      const bool odd = ps & 1;
+      hipLaunchKernelGGL(k_sp_pass<uint32_t>, grid(tO, g->occ_p32), dim3(NT), 0, st,
+                         (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
+                         odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
+                         (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, err);
+    } else {
+      const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
+      hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
+                         dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
+                         (const float*)f.cs, p.max_edges, out, ctr);
+      TRY(hipGetLastError());
+      TRY(hipMemcpyAsync(g->host_small, ctr, NCTR * 8, hipMemcpyDeviceToHost, st));
+    }
+    TRY(hipGetLastError());
+    return NLP_OK;
+  };
+  const int lo[4] = {0, hot, hot + 1, s_runs + 1}, hi[4] = {hot, hot + 1, s_runs + 1, n_st};
+  static const int ev_at[4] = {0, 3, 4, 1};
+  for (int sg = 0; sg < 4; ++sg) {
+    if (seg >= 0 && seg != sg) continue;
+    if (seg < 0) TRY(hipEventRecord(g->ev[ev_at[sg]], st));
+    for (int s = lo[sg]; s < hi[sg]; ++s) {
+      nlp_status r = stage(s);
+      if (r != NLP_OK) return r;
+    }
+  }
+  if (seg < 0) TRY(hipEventRecord(g->ev[2], st));
+  return NLP_OK;
+}
+
+// Replay (or capture, then replay) a fast path as hipGraphs.  The pipeline is
+// captured as four segments on the graph's own stream and replayed on the
 // caller's stream with the timing events recorded between them (events inside
 // a graph cannot be timed), so hot_ms stays a live measurement.  *replayed =
 // false when graphs are disabled or capture failed (the caller then launches
-// directly).
-nlp_status run_fast_graph(nlp_graph* g, const Params& p, const FastBufs& f, EdgeOut* out, hipStream_t st,
-                          bool* replayed) {
+// directly).  launch(stream, seg) enqueues one segment.
+template <class L>
+nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, bool* replayed, L&& launch) {
   *replayed = false;
   if (!g->use_graphs) return NLP_OK;
   const uint64_t gen = ws_fingerprint(g->ws);
@@ -1054,7 +1241,7 @@ nlp_status run_fast_graph(nlp_graph* g, const Params& p, const FastBufs& f, Edge
       hipGraph_t graph = nullptr;
       c.exec[seg] = nullptr;
       if (hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal) != hipSuccess) { ok = false; break; }
-      nlp_status s = launch_fast(g, p, f, out, gs, seg);
+      nlp_status s = launch(gs, seg);
       hipError_t e = hipStreamEndCapture(gs, &graph);
       ok = s == NLP_OK && e == hipSuccess && graph;
       if (ok) ok = hipGraphInstantiate(&c.exec[seg], graph, nullptr, nullptr, 0) == hipSuccess;
@@ -1089,31 +1276,40 @@ nlp_status run_fast_graph(nlp_graph* g, const Params& p, const FastBufs& f, Edge
 }
 
 // Run the fast path; *handled = false when the caller must use the general
-// flow (wedges beyond the budget, or a bucket beyond the LDS cap).
+// flow (wedges beyond the budget, or -- bucket grouping -- a bucket beyond the
+// LDS cap).
 nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result, bool* handled) {
   *handled = false;
+  const bool sorted = g->sort_grouping;
   for (int attempt = 0; attempt < 3; ++attempt) {
+    if (sorted && g->capW > SP_MAX_N) return NLP_OK;
     EdgeOut* out = d_out;
     if (!out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(std::min(p.max_edges, g->capW), 1), &out));
     FastBufs f;
-    nlp_status s = prepare_fast(g, p, f, st);
+    SpBufs sp;
+    nlp_status s = sorted ? prepare_sp(g, p, sp) : prepare_fast(g, p, f, st);
     if (s != NLP_OK) return s;
     bool replayed = false;
-    s = run_fast_graph(g, p, f, out, st, &replayed);
+    if (sorted)
+      s = run_graph(g, p, out, st, &replayed, [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
+    else
+      s = run_graph(g, p, out, st, &replayed,
+                    [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
     if (s != NLP_OK) return s;
     if (!replayed) {
-      s = launch_fast(g, p, f, out, st, -1);
+      s = sorted ? launch_sp(g, p, sp, out, st, -1) : launch_fast(g, p, f, out, st, -1);
       if (s != NLP_OK) return s;
     }
     TRY(hipEventSynchronize(g->ev[2]));
     const uint64_t* h = g->host_small;
     if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
     if (h[C_FLAGS] & F_OVERFLOW) {
-      // the grouping did not run: its counters are dirty
-      TRY(hipMemsetAsync(g->ws.p[B_UCNT], 0, g->span * 4, st));
-      TRY(hipMemsetAsync(g->ws.p[B_IEP], 0, g->span * 4, st));
       const uint64_t W = h[C_W];
+      if (!sorted) {  // the grouping did not run: its counters are dirty
+        TRY(hipMemsetAsync(g->ws.p[B_UCNT], 0, g->span * 4, st));
+        TRY(hipMemsetAsync(g->ws.p[B_IEP], 0, g->span * 4, st));
+      }
       if (W > g->wedge_budget) return NLP_OK;
       g->capW = std::max(g->capW, W + W / 4 + 1024);
       continue;
@@ -1137,8 +1333,13 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->chunks = 0;
       t->hot_ms = hot;
       t->graph_replay = replayed ? 1u : 0u;
-      // k_group_tiles: bucket counts, records, flags, runs
-      t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
+      if (sorted) {
+        const int s_runs = 4 + sp.passes;
+        t->hot_bytes = sp_stage_bytes(g, sp, std::min(std::max(g->hot_stage, 1), s_runs), h);
+      } else {
+        // k_group_tiles: bucket counts, records, flags, runs
+        t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
+      }
     }
     *handled = true;
     return NLP_OK;
@@ -1148,7 +1349,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
 
 nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result) {
-  if (p.H > 0 && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
+  if ((p.H > 0 || g->sort_grouping) && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
     bool handled = false;
     nlp_status s = predict_fast(g, p, d_out, out_count, t, st, result, &handled);
     if (s != NLP_OK || handled) return s;

@@ -229,14 +229,41 @@ def star_csr(leaves=12000):
     return np.array(off, np.uint64), np.array(keys, np.uint32)
 
 
-def test_gpu_oversized_bucket_falls_back(gpu, oracle):
+@pytest.mark.parametrize("grouping", ["sort", "bucket"])
+def test_gpu_oversized_bucket_falls_back(gpu, oracle, grouping):
+    """A source with a huge wedge bucket: the sort grouping has no size limit
+    (path 1); the bucket grouping exceeds its LDS cap and falls back (path 3)."""
     off, keys = star_csr()
-    with gpu.Graph(off, keys) as G:
-        for m, H, k in ((0, 2, 500), (7, 4, 20000), (1, 2, 10 ** 6)):
-            u, w, s, t = G.predict(m, H, k)
-            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
-            assert_canonical_equal(eu, ew, es, u, w, s)
-            assert t["path"] == 3
+    try:
+        os.environ["NLP_GROUPING"] = grouping
+        with gpu.Graph(off, keys) as G:
+            for m, H, k in ((0, 2, 500), (7, 4, 20000), (1, 2, 10 ** 6)):
+                u, w, s, t = G.predict(m, H, k)
+                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                assert_canonical_equal(eu, ew, es, u, w, s)
+                assert t["path"] == (1 if grouping == "sort" else 3)
+    finally:
+        del os.environ["NLP_GROUPING"]
+
+
+def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle):
+    """The two sync-free groupings (wedge-record sort / per-source buckets)
+    give identical results and counters, IHub included (sort grouping only)."""
+    off, keys = random_csr(8000, 14, 7)
+    k = 3000
+    with gpu.Graph(off, keys) as Gs:
+        res = {(m, H): Gs.predict(m, H, k) for m in range(9) for H in (0, 1, 2, 4, 16)}
+    try:
+        os.environ["NLP_GROUPING"] = "bucket"
+        with gpu.Graph(off, keys) as Gb:
+            for (m, H), (u, w, s, t) in res.items():
+                assert t["path"] == 1
+                ub, wb, sb, tb = Gb.predict(m, H, k)
+                assert_canonical_equal(ub, wb, sb, u, w, s)
+                assert t["wedges"] == tb["wedges"] and t["candidates"] == tb["candidates"]
+                assert t["nan_candidates"] == tb["nan_candidates"]
+    finally:
+        del os.environ["NLP_GROUPING"]
 
 
 def test_gpu_radix_path_equals_bucket_path(gpu, oracle):
