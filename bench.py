@@ -29,6 +29,8 @@ sys.path.insert(0, ROOT)
 import nlp_loader  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
+HOT_KERNELS = {1: "k_sp_bucket", 2: "k_sp_scan<F_Runs>", 3: "k_group_tiles", 4: "k_sp_survivors",
+               5: "k_sp_expand", 6: "k_sp_pass"}
 
 
 def log(*a):
@@ -101,7 +103,10 @@ def pmc_traffic(config, world, metric, hub):
         return None
     if d.get("config") != config or d.get("n_gpus") != world or d.get("metric") != metric or d.get("hub") != hub:
         return None
-    return {"bytes_per_launch": d["kernels"]["k_group_tiles"]["traffic_bytes"], "source": d.get("source")}
+    k = d.get("hot_kernel", "k_sp_bucket")
+    if k not in d.get("kernels", {}):
+        return None
+    return {"bytes_per_launch": d["kernels"][k]["traffic_bytes"], "source": d.get("source"), "kernel": k}
 
 
 def main():
@@ -217,12 +222,14 @@ def main():
             "predicted": cnt,
             "f1": f1, "precision": p, "recall": r,
             "score_ms": score_ms, "select_ms": select_ms,
+            "host_overhead_ms": ms_per_step - score_ms - select_ms,
             "wedges": wedges, "candidates": cands, "path": last.get("path"),
             "graph_gen_s": gen_s, "graph_create_s": create_s,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
-                         "kernel": "k_group_tiles", "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
+                         "kernel": HOT_KERNELS.get(int(last.get("hot_kernel", 0)), "?"),
+                         "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
                          "traffic_source": traffic["source"] if traffic else None},
             "graph_replay": replays == args.steps,
             "cpu_baseline": None,

@@ -91,6 +91,8 @@ typedef struct {
   float hot_ms;             /* device time of the dominant kernel (HIP events around its launch) */
   uint32_t graph_replay;    /* 1 when the call replayed a captured hipGraph */
   uint64_t hot_bytes;       /* algorithmic bytes of that launch */
+  uint32_t hot_kernel;      /* which kernel hot_ms times: 1 k_sp_bucket, 2 k_sp_scan<F_Runs>,
+                               3 k_group_tiles, 4 k_sp_survivors, 5 k_sp_expand, 6 k_sp_pass; 0 none */
 } nlp_timing;
 
 typedef struct nlp_graph nlp_graph;

@@ -48,7 +48,8 @@ class Timing(ctypes.Structure):
     _fields_ = [("score_ms", ctypes.c_float), ("select_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("copy_ms", ctypes.c_float), ("wedges", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
                 ("nan_candidates", ctypes.c_uint64), ("path", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
-                ("hot_ms", ctypes.c_float), ("graph_replay", ctypes.c_uint32), ("hot_bytes", ctypes.c_uint64)]
+                ("hot_ms", ctypes.c_float), ("graph_replay", ctypes.c_uint32), ("hot_bytes", ctypes.c_uint64),
+                ("hot_kernel", ctypes.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

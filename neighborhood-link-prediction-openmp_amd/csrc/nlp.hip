@@ -5,11 +5,13 @@
 // every entry point returns NLP_ERR_NODEVICE.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 #include <stdlib.h>
 #include <math.h>
 #include <new>
 #include <vector>
+#include <string>
 #include <algorithm>
 
 #include "../../include/nlp.h"
@@ -120,23 +122,34 @@ struct nlp_graph {
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
   uint64_t* host_small = nullptr;  // pinned counters
   hipEvent_t ev[8] = {};
+  hipEvent_t gev[5] = {};  // recorded only as event nodes of captured graphs
+  bool last_single = false; // the last fast call replayed a single graph (timing in gev)
   Workspace ws;
   uint64_t wedge_budget = 0;
   uint64_t capE = 1u << 20, capW = 1u << 20;  // path-1 capacities (grown on overflow)
   bool force_radix = false;                    // test hook: NLP_FORCE_RADIX=1
   bool sort_grouping = true;                   // NLP_GROUPING=bucket selects the per-source bucket grouping
-  int hot_stage = 2;                           // sort path: stage timed as the dominant kernel (k_sp_expand)
+  bool sort_lsd = false;                       // NLP_GROUPING=lsd: full LSD record sort (no MSD buckets)
+  // NLP_STAMP=<file>: per-workgroup phase stamps of the timed stage appended to <file> (diagnostics)
+  uint64_t* d_stamp = nullptr;
+  uint32_t stamp_blocks = 0;
+  std::string stamp_path;
+  int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
+                                               // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
   unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256;
   bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
+  bool graph_single = true;                    // NLP_GRAPH_SEGMENTS=1: four graph segments with host events
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
   struct Cached {
     int metric;
     uint32_t H;
     float min_score;
     uint64_t max_edges, ua, ub, capW, gen;
+    int mode;  // fast-path variant (graph shapes differ)
     void* out;
     hipGraphExec_t exec[4];
+    bool single;  // one graph with event-record nodes (else four segments)
     uint64_t last_use;
   };
   std::vector<Cached> graphs;
@@ -152,11 +165,28 @@ nlp_status from_hip(hipError_t e) {
   return NLP_ERR_DEVICE;
 }
 
-#define TRY(x)                                   \
-  do {                                           \
-    hipError_t e__ = (x);                        \
-    if (e__ != hipSuccess) return from_hip(e__); \
+// NLP_DEBUG=1 reports the failing runtime call on stderr
+inline bool debug_on() {
+  static const bool on = getenv("NLP_DEBUG") != nullptr;
+  return on;
+}
+#define TRY(x)                                                                                     \
+  do {                                                                                             \
+    hipError_t e__ = (x);                                                                          \
+    if (e__ != hipSuccess) {                                                                       \
+      if (debug_on()) fprintf(stderr, "nlp: %s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e__)); \
+      return from_hip(e__);                                                                        \
+    }                                                                                              \
   } while (0)
+
+// Wait for an event by polling: a blocking wait can add tens of microseconds
+// of wake-up latency to every call, which is a large share of a fast prediction.
+hipError_t wait_event(hipEvent_t e) {
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q != hipErrorNotReady) return q;
+  }
+}
 
 nlp_status check_device(int device) {
   int n = 0;
@@ -180,8 +210,10 @@ void destroy_graph(nlp_graph* g) {
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& c : g->graphs)
-    for (auto& x : c.exec) (void)hipGraphExecDestroy(x);
+    for (auto& x : c.exec)
+      if (x) (void)hipGraphExecDestroy(x);
   g->graphs.clear();
+  if (g->d_stamp) (void)hipFree(g->d_stamp);
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -194,6 +226,8 @@ void destroy_graph(nlp_graph* g) {
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   for (int i = 0; i < 8; ++i)
     if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
+  for (int i = 0; i < 5; ++i)
+    if (g->gev[i]) (void)hipEventDestroy(g->gev[i]);
   if (g->host_small) (void)hipHostFree(g->host_small);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
@@ -305,7 +339,17 @@ nlp_status finish_graph(nlp_graph* g) {
     unsigned long long v = strtoull(ev, nullptr, 10);
     if (v > 0) g->wedge_budget = v;
   }
-  if (const char* gr = getenv("NLP_GROUPING")) g->sort_grouping = strcmp(gr, "bucket") != 0;
+  if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
+  if (const char* gs = getenv("NLP_GRAPH_SEGMENTS")) g->graph_single = gs[0] != '1';
+  if (const char* sp = getenv("NLP_STAMP")) {
+    g->stamp_path = sp;
+    TRY(hipMalloc(&g->d_stamp, 8 * 65536 * 8));
+    TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
+  }
+  if (const char* gr = getenv("NLP_GROUPING")) {
+    g->sort_grouping = strcmp(gr, "bucket") != 0;
+    g->sort_lsd = strcmp(gr, "lsd") == 0;
+  }
   {
     hipDeviceProp_t prop;
     TRY(hipGetDeviceProperties(&prop, g->device));
@@ -316,10 +360,10 @@ nlp_status finish_graph(nlp_graph* g) {
       if (e == hipSuccess) *out = cus * (unsigned)std::max(nb, 1);
       return e;
     };
-    TRY(occ((const void*)k_sp_survivors, &g->occ_surv));
-    TRY(occ((const void*)k_sp_expand, &g->occ_exp));
-    TRY(occ((const void*)k_sp_pass<uint64_t>, &g->occ_p64));
-    TRY(occ((const void*)k_sp_pass<uint32_t>, &g->occ_p32));
+    TRY(occ((const void*)k_sp_survivors<>, &g->occ_surv));
+    TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
+    TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64));
+    TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32));
     unsigned a = 0, b = 0;
     TRY(occ((const void*)k_sp_scan<F_Runs<true>, RN_IPT>, &a));
     TRY(occ((const void*)k_sp_scan<F_Runs<false>, RN_IPT>, &b));
@@ -342,6 +386,14 @@ nlp_status new_graph(int device, nlp_graph** out) {
   }
   for (int i = 0; i < 8; ++i)
     if (hipEventCreate(&g->ev[i]) != hipSuccess) { destroy_graph(g); return NLP_ERR_DEVICE; }
+  // timing-only events skip the system-scope fence (cache writeback) of a
+  // default event record; gev[2] ends the call and keeps it (the host reads
+  // the counters after it)
+  for (int i = 0; i < 5; ++i)
+    if (hipEventCreateWithFlags(&g->gev[i], i == 2 ? hipEventDefault : hipEventDisableSystemFence) != hipSuccess) {
+      destroy_graph(g);
+      return NLP_ERR_DEVICE;
+    }
   *out = g;
   return NLP_OK;
 }
@@ -1069,6 +1121,8 @@ struct SpBufs {
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
+  bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
+  int msd_shift;  // shift of that digit
 };
 
 inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 1)
@@ -1077,7 +1131,7 @@ inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 
   return b;
 }
 
-nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f) {
+nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd) {
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
   const uint64_t capW = g->capW;
@@ -1098,8 +1152,11 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f) {
   f.wbits = key_bits(S ? S - 1 : 0);
   const int ubits = key_bits(ub > ua ? ub - ua - 1 : 0);
   f.passes = (f.wbits + ubits + 7) / 8;
+  f.msd = msd;
+  f.msd_shift = std::max(0, f.wbits + ubits - 8);
   const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + EX_TILE - 1) / EX_TILE;
-  const uint64_t tR = (capW + RN_TILE - 1) / RN_TILE, tO = (capW + OS2_TILE - 1) / OS2_TILE;
+  const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, RS_BINS);
+  const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
   f.d_surv = SP_DESC;
   f.d_exp = f.d_surv + tS + 1;
@@ -1117,8 +1174,9 @@ uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64
   const uint64_t S = g->span, V = h[C_NV], W = h[C_W], C = h[C_C];
   if (s == 1) return 4 * S + 4 * V;             // deg read, survivor ids written
   if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
-  if (s >= 4 && s < 4 + f.passes) return 24 * W;  // records in + out
-  if (s == 4 + f.passes) return 12 * W + 4 * W + 20 * C;  // records (+stash), candidates
+  const int P = f.msd ? 1 : f.passes;
+  if (s >= 4 && s < 4 + P) return 24 * W;  // records in + out
+  if (s == 4 + P) return f.msd ? 8 * W + 20 * C : 12 * W + 4 * W + 20 * C;  // records (+stash), candidates
   return 0;
 }
 
@@ -1137,9 +1195,9 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint32_t* hord = (uint32_t*)(f.arena + SP_HORD);
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
-  const int P = f.passes;
+  const int P = f.msd ? 1 : f.passes;
   const int s_runs = 4 + P, n_st = s_runs + 7;
-  const int hot = std::min(std::max(g->hot_stage, 1), s_runs);
+  const int hot = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
   auto grid = [](uint64_t tiles, unsigned occ) {
     return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, occ)));
   };
@@ -1154,21 +1212,42 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       hipLaunchKernelGGL(k_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (f.arena_words + NT - 1) / NT)),
                          dim3(NT), 0, st, f.arena, f.arena_words, ci);
     } else if (s == 1) {
-      hipLaunchKernelGGL(k_sp_survivors, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
-                         (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, ctr);
+      hipLaunchKernelGGL(k_sp_survivors<>, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
+                         (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, ctr, hot == 1 ? g->d_stamp : nullptr);
     } else if (s == 2) {
-      hipLaunchKernelGGL(k_sp_expand, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua, ub,
-                         f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr);
+      if (f.msd)  // the MSD digit histogram is fused into the expansion
+        hipLaunchKernelGGL(k_sp_expand<true>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua,
+                           ub, f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr,
+                           f.msd_shift, hrec);
+      else
+        hipLaunchKernelGGL(k_sp_expand<false>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv,
+                           ua, ub, f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, 0,
+                           (uint32_t*)nullptr);
     } else if (s == 3) {
+      if (f.msd) return NLP_OK;
       hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, st, (const uint64_t*)f.rk0,
-                         (const uint64_t*)&ctr[C_W], capW, P, hrec, &ctr[C_WSORT], &ctr[C_FLAGS]);
+                         (const uint64_t*)&ctr[C_W], capW, f.msd ? f.msd_shift : 0, P, hrec, &ctr[C_WSORT],
+                         &ctr[C_FLAGS]);
     } else if (s < s_runs) {
       const int ps = s - 4;
       const bool odd = ps & 1;
-      hipLaunchKernelGGL(k_sp_pass<uint64_t>, grid(tO, g->occ_p64), dim3(NT), 0, st,
+      hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(NT), 0, st,
                          (const uint64_t*)(odd ? f.rk1 : f.rk0), (const uint32_t*)(odd ? f.rv1 : f.rv0),
-                         odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT], 8 * ps,
-                         (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err);
+                         odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT],
+                         f.msd ? f.msd_shift : 8 * ps,
+                         (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err,
+                         hot == s ? g->d_stamp : nullptr, GatherOut{});
+    } else if (s == s_runs && f.msd) {
+      if (custom)
+        hipLaunchKernelGGL(k_sp_bucket<true>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
+                           f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
+                           f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr);
+      else
+        hipLaunchKernelGGL(k_sp_bucket<false>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
+                           f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
+                           f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr);
     } else if (s == s_runs) {
       const dim3 gr = grid((capW + RN_TILE - 1) / RN_TILE, g->occ_run);
       if (custom) {
@@ -1183,15 +1262,17 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint64_t*)&ctr[C_WSORT], f.arena + f.d_run, err, &ctr[C_C]);
       }
     } else if (s == s_runs + 1) {
+      if (f.msd) return NLP_OK;  // fused into k_sp_bucket
       hipLaunchKernelGGL(k_sp_hist<uint32_t>, dim3(128), dim3(NT), 0, st, (const uint32_t*)f.ok0,
-                         (const uint64_t*)&ctr[C_C], capW, 4, hord, (uint64_t*)nullptr, (uint64_t*)nullptr);
+                         (const uint64_t*)&ctr[C_C], capW, 0, 4, hord, (uint64_t*)nullptr, (uint64_t*)nullptr);
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      hipLaunchKernelGGL(k_sp_pass<uint32_t>, grid(tO, g->occ_p32), dim3(NT), 0, st,
-                         (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
-                         odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
-                         (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, err);
+      hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(NT), 0, st,
+                           (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
+                           odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
+                           (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, err,
+                           (uint64_t*)nullptr, GatherOut{});
     } else {
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
@@ -1203,17 +1284,22 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     TRY(hipGetLastError());
     return NLP_OK;
   };
-  const int lo[4] = {0, hot, hot + 1, s_runs + 1}, hi[4] = {hot, hot + 1, s_runs + 1, n_st};
-  static const int ev_at[4] = {0, 3, 4, 1};
-  for (int sg = 0; sg < 4; ++sg) {
+  // three segments [0, hot) | hot | (hot, end) with events 0, 3, 4 before them
+  // and 2 at the end; with the default hot stage (the scoring kernel) event 4
+  // also splits scoring from selection
+  const int lo[3] = {0, hot, hot + 1}, hi[3] = {hot, hot + 1, n_st};
+  static const int ev_at[3] = {0, 3, 4};
+  // seg -1: direct launch with event records (captured segments carry none)
+  auto mark = [&](int e) -> hipError_t { return seg == -1 ? hipEventRecord(g->ev[e], st) : hipSuccess; };
+  for (int sg = 0; sg < 3; ++sg) {
     if (seg >= 0 && seg != sg) continue;
-    if (seg < 0) TRY(hipEventRecord(g->ev[ev_at[sg]], st));
+    TRY(mark(ev_at[sg]));
     for (int s = lo[sg]; s < hi[sg]; ++s) {
       nlp_status r = stage(s);
       if (r != NLP_OK) return r;
     }
   }
-  if (seg < 0) TRY(hipEventRecord(g->ev[2], st));
+  TRY(mark(2));
   return NLP_OK;
 }
 
@@ -1223,30 +1309,74 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
 // a graph cannot be timed), so hot_ms stays a live measurement.  *replayed =
 // false when graphs are disabled or capture failed (the caller then launches
 // directly).  launch(stream, seg) enqueues one segment.
+// events recorded before each capture segment (event 2 ends the call)
+static const int EV_SEG4[4] = {0, 3, 4, 1};  // bucket grouping: pre | hot | rest of scoring | selection
+static const int EV_SEG3[3] = {0, 3, 4};     // sort grouping: pre | hot (scoring) | selection
+
 template <class L>
-nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, bool* replayed, L&& launch) {
+nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, int mode, bool* replayed,
+                     L&& launch) {
   *replayed = false;
   if (!g->use_graphs) return NLP_OK;
+  const bool single = g->graph_single && mode != 0;  // the bucket grouping is captured in segments
   const uint64_t gen = ws_fingerprint(g->ws);
   nlp_graph::Cached* hit = nullptr;
   for (auto& c : g->graphs)
     if (c.metric == p.metric && c.H == p.H && c.min_score == p.min_score && c.max_edges == p.max_edges &&
-        c.ua == p.ua && c.ub == p.ub && c.capW == g->capW && c.gen == gen && c.out == (void*)out)
+        c.ua == p.ua && c.ub == p.ub && c.capW == g->capW && c.gen == gen && c.mode == mode && c.out == (void*)out)
       hit = &c;
   if (!hit) {
-    nlp_graph::Cached c{p.metric, p.H, p.min_score, p.max_edges, p.ua, p.ub, g->capW, gen, (void*)out, {}, 0};
+    nlp_graph::Cached c{p.metric, p.H, p.min_score, p.max_edges, p.ua, p.ub, g->capW, gen, mode, (void*)out, {}, false, 0};
     hipStream_t gs = g->stream;
     bool ok = true;
-    for (int seg = 0; seg < 4 && ok; ++seg) {
-      hipGraph_t graph = nullptr;
-      c.exec[seg] = nullptr;
+    c.single = false;
+    hipGraph_t seg_graph[4] = {};
+    const int nseg = mode == 0 ? 4 : 3;
+    const int* ev_before = mode == 0 ? EV_SEG4 : EV_SEG3;
+    for (int seg = 0; seg < nseg && ok; ++seg) {
       if (hipStreamBeginCapture(gs, hipStreamCaptureModeThreadLocal) != hipSuccess) { ok = false; break; }
       nlp_status s = launch(gs, seg);
-      hipError_t e = hipStreamEndCapture(gs, &graph);
-      ok = s == NLP_OK && e == hipSuccess && graph;
-      if (ok) ok = hipGraphInstantiate(&c.exec[seg], graph, nullptr, nullptr, 0) == hipSuccess;
-      if (graph) (void)hipGraphDestroy(graph);
+      hipError_t e = hipStreamEndCapture(gs, &seg_graph[seg]);
+      ok = s == NLP_OK && e == hipSuccess && seg_graph[seg];
+      if (!ok && debug_on())
+        fprintf(stderr, "nlp: graph capture failed (seg=%d launch=%d end=%s)\n", seg, (int)s, hipGetErrorString(e));
     }
+    if (ok && single) {
+      // one graph: event-record nodes around the four segments as child graphs,
+      // so a call is a single launch and the events still time the hot kernel
+      hipGraph_t top = nullptr;
+      bool ok1 = hipGraphCreate(&top, 0) == hipSuccess;
+      hipGraphNode_t prev = nullptr;
+      auto chain_ev = [&](int e) {
+        hipGraphNode_t n = nullptr;
+        ok1 = ok1 && hipGraphAddEventRecordNode(&n, top, prev ? &prev : nullptr, prev ? 1 : 0, g->gev[e]) == hipSuccess;
+        prev = n;
+      };
+      for (int seg = 0; seg < nseg && ok1; ++seg) {
+        chain_ev(ev_before[seg]);
+        hipGraphNode_t n = nullptr;
+        ok1 = ok1 && hipGraphAddChildGraphNode(&n, top, &prev, 1, seg_graph[seg]) == hipSuccess;
+        prev = n;
+      }
+      if (ok1) chain_ev(2);
+      if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
+      if (top) (void)hipGraphDestroy(top);
+      if (ok1) {
+        c.single = true;
+      } else {
+        if (c.exec[0]) (void)hipGraphExecDestroy(c.exec[0]);
+        c.exec[0] = nullptr;
+        (void)hipGetLastError();
+        g->graph_single = false;
+        if (debug_on()) fprintf(stderr, "nlp: single-graph composition failed, using segments\n");
+      }
+    }
+    for (int seg = 0; seg < nseg && ok && !c.single; ++seg) {
+      hipError_t ei = hipGraphInstantiate(&c.exec[seg], seg_graph[seg], nullptr, nullptr, 0);
+      ok = ei == hipSuccess;
+    }
+    for (auto& x : seg_graph)
+      if (x) (void)hipGraphDestroy(x);
     if (!ok) {
       for (auto& x : c.exec)
         if (x) (void)hipGraphExecDestroy(x);
@@ -1258,19 +1388,26 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
       size_t lru = 0;
       for (size_t i = 1; i < g->graphs.size(); ++i)
         if (g->graphs[i].last_use < g->graphs[lru].last_use) lru = i;
-      for (auto& x : g->graphs[lru].exec) (void)hipGraphExecDestroy(x);
+      for (auto& x : g->graphs[lru].exec)
+        if (x) (void)hipGraphExecDestroy(x);
       g->graphs.erase(g->graphs.begin() + lru);
     }
     g->graphs.push_back(c);
     hit = &g->graphs.back();
   }
   hit->last_use = ++g->use_clock;
-  static const int ev_before[4] = {0, 3, 4, 1};
-  for (int seg = 0; seg < 4; ++seg) {
-    TRY(hipEventRecord(g->ev[ev_before[seg]], st));
-    TRY(hipGraphLaunch(hit->exec[seg], st));
+  g->last_single = hit->single;
+  if (hit->single) {
+    TRY(hipGraphLaunch(hit->exec[0], st));
+  } else {
+    const int nseg = mode == 0 ? 4 : 3;
+    const int* ev_before = mode == 0 ? EV_SEG4 : EV_SEG3;
+    for (int seg = 0; seg < nseg; ++seg) {
+      TRY(hipEventRecord(g->ev[ev_before[seg]], st));
+      TRY(hipGraphLaunch(hit->exec[seg], st));
+    }
+    TRY(hipEventRecord(g->ev[2], st));
   }
-  TRY(hipEventRecord(g->ev[2], st));
   *replayed = true;
   return NLP_OK;
 }
@@ -1282,26 +1419,30 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
                         hipStream_t st, EdgeOut** result, bool* handled) {
   *handled = false;
   const bool sorted = g->sort_grouping;
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  bool msd = !g->sort_lsd;  // sort grouping: MSD bucket kernel first, full LSD sort when a bucket is too big
+  for (int attempt = 0; attempt < 4; ++attempt) {
     if (sorted && g->capW > SP_MAX_N) return NLP_OK;
     EdgeOut* out = d_out;
     if (!out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(std::min(p.max_edges, g->capW), 1), &out));
     FastBufs f;
     SpBufs sp;
-    nlp_status s = sorted ? prepare_sp(g, p, sp) : prepare_fast(g, p, f, st);
+    nlp_status s = sorted ? prepare_sp(g, p, sp, msd) : prepare_fast(g, p, f, st);
     if (s != NLP_OK) return s;
     bool replayed = false;
+    g->last_single = false;
     if (sorted)
-      s = run_graph(g, p, out, st, &replayed, [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
+      s = run_graph(g, p, out, st, msd ? 2 : 1, &replayed,
+                    [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
     else
-      s = run_graph(g, p, out, st, &replayed,
+      s = run_graph(g, p, out, st, 0, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
     if (s != NLP_OK) return s;
     if (!replayed) {
       s = sorted ? launch_sp(g, p, sp, out, st, -1) : launch_fast(g, p, f, out, st, -1);
       if (s != NLP_OK) return s;
     }
-    TRY(hipEventSynchronize(g->ev[2]));
+    hipEvent_t* E = (replayed && g->last_single) ? g->gev : g->ev;
+    TRY(wait_event(E[2]));
     const uint64_t* h = g->host_small;
     if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
     if (h[C_FLAGS] & F_OVERFLOW) {
@@ -1314,14 +1455,19 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       g->capW = std::max(g->capW, W + W / 4 + 1024);
       continue;
     }
+    if (sorted && msd && (h[C_FLAGS] & F_TOOBIG) && h[C_W] <= g->wedge_budget) {
+      msd = false;
+      continue;
+    }
     if ((h[C_FLAGS] & F_TOOBIG) || h[C_W] > g->wedge_budget) return NLP_OK;
     *out_count = h[C_OUT_N];
     if (result) *result = out;
     if (t) {
       float a = 0, b = 0, hot = 0;
-      TRY(hipEventElapsedTime(&a, g->ev[0], g->ev[1]));
-      TRY(hipEventElapsedTime(&b, g->ev[1], g->ev[2]));
-      TRY(hipEventElapsedTime(&hot, g->ev[3], g->ev[4]));
+      const hipEvent_t split = sorted ? E[4] : E[1];  // sort grouping: event 4 ends the scoring kernel
+      TRY(hipEventElapsedTime(&a, E[0], split));
+      TRY(hipEventElapsedTime(&b, split, E[2]));
+      TRY(hipEventElapsedTime(&hot, E[3], E[4]));
       const uint64_t nU = std::min(p.ub, g->span) - std::min(p.ua, g->span);
       t->score_ms = a;
       t->select_ms = b;
@@ -1334,11 +1480,22 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->hot_ms = hot;
       t->graph_replay = replayed ? 1u : 0u;
       if (sorted) {
-        const int s_runs = 4 + sp.passes;
-        t->hot_bytes = sp_stage_bytes(g, sp, std::min(std::max(g->hot_stage, 1), s_runs), h);
+        const int s_runs = 4 + (sp.msd ? 1 : sp.passes);
+        const int hs = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
+        t->hot_bytes = sp_stage_bytes(g, sp, hs, h);
+        t->hot_kernel = hs == s_runs ? (sp.msd ? 1u : 2u) : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
       } else {
         // k_group_tiles: bucket counts, records, flags, runs
         t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
+        t->hot_kernel = 3;
+      }
+    }
+    if (g->d_stamp && !g->stamp_path.empty()) {  // diagnostics: append this call's stamps
+      std::vector<uint64_t> hs(8 * 65536);
+      TRY(hipMemcpy(hs.data(), g->d_stamp, hs.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* fp = fopen(g->stamp_path.c_str(), "ab")) {
+        fwrite(hs.data(), 8, hs.size(), fp);
+        fclose(fp);
       }
     }
     *handled = true;

@@ -45,8 +45,8 @@ constexpr uint64_t SP_HREC = 16;               // 8 x 256 u32: record-key digits
 constexpr uint64_t SP_HORD = SP_HREC + 1024;   // 4 x 256 u32: score-key digits
 constexpr uint64_t SP_DESC = SP_HORD + 512;    // descriptors follow
 
-constexpr int SV_STEPS = 32;                   // survivor scan: 64-vertex steps per wave
-constexpr int SV_TILE = NT * SV_STEPS;         // 8192 vertices per tile
+constexpr int SV_STEPS = 8;                    // survivor scan: 256-vertex steps per wave
+constexpr int SV_TILE = NT * 4 * SV_STEPS;     // 8192 vertices per tile
 constexpr int EX_TILE = NT;                    // expansion: one survivor per thread
 constexpr int RN_IPT = 4;
 constexpr int RN_TILE = NT * RN_IPT;           // run scoring: 1024 records per tile
@@ -109,40 +109,65 @@ __device__ __forceinline__ uint64_t lb_lookback_r(uint64_t* desc, uint64_t tile,
   return excl;
 }
 
+// Optional phase stamps for tools/ubench (nullptr in the product): workgroup b
+// writes s_memrealtime (100 MHz) of phase i of its first tile to stamp[8 b + i].
+__device__ __forceinline__ void sp_stamp(uint64_t* stamp, bool first, int i) {
+  if (stamp && first && threadIdx.x == 0) stamp[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ uint64_t lane_mask_lt() {
   const int lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
 // ---------------------------------------------------------------- survivors
-// Tile = 4 waves x 32 steps x 64 consecutive vertices; a vertex survives when
+// Tile = 4 waves x STEPS steps x 256 consecutive vertices (16-byte loads, lane l
+// of step i holds vertices base + 256 i + 4 l .. +3); a vertex survives when
 // 1 <= deg v <= H (H = 0: IHub, every vertex with edges).  Output ascending v.
+template <int STEPS = SV_STEPS>
 __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict__ deg, uint64_t S, uint32_t H,
                                                      uint32_t* __restrict__ surv, uint64_t* __restrict__ desc,
-                                                     uint64_t* __restrict__ ctr) {
+                                                     uint64_t* __restrict__ ctr, uint64_t* __restrict__ stamp) {
+  static_assert(STEPS * 4 <= 32, "flag bits");
+  constexpr uint64_t TILE = (uint64_t)NT * 4 * STEPS;
   __shared__ uint64_t s_w[NWAVE];
   __shared__ uint64_t s_excl;
   const int lane = lane_id(), wv = wave_id();
   const uint32_t hm = H ? H : 0xffffffffu;
-  const uint64_t ntiles = (S + SV_TILE - 1) / SV_TILE;
+  const uint64_t ntiles = (S + TILE - 1) / TILE;
   const uint64_t lt = lane_mask_lt();
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t b0 = tile * SV_TILE + (uint64_t)wv * (64 * SV_STEPS) + lane;
-    uint32_t dv[SV_STEPS];
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
+    const uint64_t b0 = tile * TILE + (uint64_t)wv * (256 * STEPS) + 4 * (uint64_t)lane;
+    uint4 dv[STEPS];
 #pragma unroll
-    for (int i = 0; i < SV_STEPS; ++i) {
-      const uint64_t v = b0 + (uint64_t)i * 64;
-      dv[i] = v < S ? deg[v] : 0u;
+    for (int i = 0; i < STEPS; ++i) {
+      const uint64_t v = b0 + (uint64_t)i * 256;
+      if (v + 3 < S) {
+        dv[i] = *(const uint4*)(deg + v);
+      } else {
+        dv[i].x = v < S ? deg[v] : 0u;
+        dv[i].y = v + 1 < S ? deg[v + 1] : 0u;
+        dv[i].z = v + 2 < S ? deg[v + 2] : 0u;
+        dv[i].w = 0u;
+      }
     }
     uint32_t bits = 0;
 #pragma unroll
-    for (int i = 0; i < SV_STEPS; ++i) bits |= (uint32_t)(dv[i] - 1u < hm) << i;  // 1 <= d <= H
+    for (int i = 0; i < STEPS; ++i) {
+      bits |= (uint32_t)(dv[i].x - 1u < hm) << (4 * i);
+      bits |= (uint32_t)(dv[i].y - 1u < hm) << (4 * i + 1);
+      bits |= (uint32_t)(dv[i].z - 1u < hm) << (4 * i + 2);
+      bits |= (uint32_t)(dv[i].w - 1u < hm) << (4 * i + 3);
+    }
     uint64_t wt = (uint64_t)__popc(bits);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wt += __shfl_xor(wt, o, 64);
     if (lane == 0) s_w[wv] = wt;
     __syncthreads();
+    sp_stamp(stamp, first, 1);
     if (wv == 0) {
       uint64_t agg = 0;
 #pragma unroll
@@ -154,16 +179,28 @@ __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict_
       }
     }
     __syncthreads();
+    sp_stamp(stamp, first, 2);
     uint64_t run = s_excl;
     for (int w = 0; w < wv; ++w) run += s_w[w];
 #pragma unroll
-    for (int i = 0; i < SV_STEPS; ++i) {
-      const bool f = (bits >> i) & 1u;
-      const uint64_t m = __ballot(f);
-      if (f) surv[run + __popcll(m & lt)] = (uint32_t)(b0 + (uint64_t)i * 64);
-      run += __popcll(m);
+    for (int i = 0; i < STEPS; ++i) {
+      const uint32_t nib = (bits >> (4 * i)) & 0xfu;
+      uint64_t before = 0, stepn = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint64_t m = __ballot((nib >> e) & 1u);
+        before += __popcll(m & lt);
+        stepn += __popcll(m);
+      }
+      uint64_t o = run + before;
+      const uint64_t v = b0 + (uint64_t)i * 256;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((nib >> e) & 1u) surv[o++] = (uint32_t)(v + e);
+      run += stepn;
     }
     __syncthreads();
+    sp_stamp(stamp, first, 3);
   }
 }
 
@@ -171,15 +208,26 @@ __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict_
 // One thread per survivor v (ascending): for each in-edge u -> v with u in
 // [ua, ub), the wedges (u, v, w) with w in N(v), w > u.  Records beyond capW are
 // not written; the total still goes to ctr[C_W] (the host regrows and reruns).
+// HIST: also the histogram of record-key digit (key >> hshift) & 255 (the MSD
+// pass), accumulated per workgroup in LDS; the last tile stores the sortable
+// record count ctr[C_WSORT] (0 and F_OVERFLOW when the records exceed capW).
+template <bool HIST>
 __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                   const uint32_t* __restrict__ surv, uint64_t capW,
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
-                                                  uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr) {
+                                                  uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr,
+                                                  int hshift, uint32_t* __restrict__ ghist) {
   __shared__ uint64_t s_red[NWAVE + 1];
   __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_h[HIST ? RS_BINS : 1];
   const uint64_t n = ctr[C_NV];
   const uint64_t ntiles = (n + EX_TILE - 1) / EX_TILE;
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  if (blockIdx.x >= ntiles) return;
+  if (HIST) {
+    s_h[threadIdx.x] = 0;
+    __syncthreads();
+  }
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const uint64_t i = tile * EX_TILE + threadIdx.x;
     uint32_t v = 0, d = 0;
@@ -202,7 +250,14 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
       const uint64_t e = lb_lookback_r<4>(desc, tile, agg, err);
       if (lane_id() == 0) {
         s_excl = e;
-        if (tile == ntiles - 1) ctr[C_W] = e + agg;
+        if (tile == ntiles - 1) {
+          const uint64_t W = e + agg;
+          ctr[C_W] = W;
+          if (HIST) {
+            ctr[C_WSORT] = W <= capW ? W : 0;
+            if (W > capW) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_OVERFLOW);
+          }
+        }
       }
     }
     __syncthreads();
@@ -213,13 +268,19 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
         if (u < ua || u >= ub) continue;
         const uint64_t hi = (uint64_t)(u - ua) << wbits;
         for (uint32_t k = upper_bound_u32(nv, d, u); k < d; ++k) {
-          rkey[pos] = hi | nv[k];
+          const uint64_t key = hi | nv[k];
+          rkey[pos] = key;
           rval[pos] = v;
+          if (HIST) atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
           ++pos;
         }
       }
     }
     __syncthreads();
+  }
+  if (HIST) {
+    const uint32_t hc = s_h[threadIdx.x];
+    if (hc) atomicAdd(&ghist[threadIdx.x], hc);
   }
 }
 
@@ -228,7 +289,7 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
 // exceeds cap (then F_OVERFLOW is raised); block 0 stores the effective n.
 template <typename K>
 __global__ __launch_bounds__(NT) void k_sp_hist(const K* __restrict__ keys, const uint64_t* __restrict__ d_n,
-                                                uint64_t cap, int ndig, uint32_t* __restrict__ ghist,
+                                                uint64_t cap, int shift0, int ndig, uint32_t* __restrict__ ghist,
                                                 uint64_t* __restrict__ n_out, uint64_t* __restrict__ flags) {
   __shared__ uint32_t h[8][RS_BINS];
   for (int i = threadIdx.x; i < 8 * RS_BINS; i += NT) (&h[0][0])[i] = 0;
@@ -241,7 +302,7 @@ __global__ __launch_bounds__(NT) void k_sp_hist(const K* __restrict__ keys, cons
   if (n_out && blockIdx.x == 0 && threadIdx.x == 0) *n_out = n;
   for (uint64_t j = (uint64_t)blockIdx.x * NT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * NT) {
     const K k = keys[j];
-    for (int dd = 0; dd < ndig; ++dd) atomicAdd(&h[dd][(uint32_t)(k >> (8 * dd)) & 0xffu], 1u);
+    for (int dd = 0; dd < ndig; ++dd) atomicAdd(&h[dd][(uint32_t)(k >> (shift0 + 8 * dd)) & 0xffu], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ndig * RS_BINS; i += NT) {
@@ -307,37 +368,57 @@ __device__ __forceinline__ uint32_t os2_lookback(uint32_t* desc, uint64_t tile, 
 // One stable counting pass on digit (key >> shift) & 255.  Wave w of a tile owns
 // 64*OS2_IPT consecutive keys; ranks come from ballot multisplit plus a per-wave
 // running digit count in LDS, so the tile order is preserved exactly.
-template <typename K>
+// Candidate columns for the last ordering pass, which writes the caller's
+// edges directly (position < k) instead of the next key/value buffers.
+struct GatherOut {
+  const uint32_t* cu;
+  const uint32_t* cw;
+  const float* cs;
+  uint64_t k;
+  EdgeOut* out;
+};
+
+template <typename K, int IPT = OS2_IPT, bool GATHER = false>
 __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                 K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                 const uint64_t* __restrict__ d_n, int shift,
                                                 const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
-                                                uint32_t* __restrict__ err) {
-  constexpr int WT = 64 * OS2_IPT;
+                                                uint32_t* __restrict__ err, uint64_t* __restrict__ stamp,
+                                                GatherOut go) {
+  constexpr int WT = 64 * IPT;
   __shared__ uint32_t s_wcnt[NWAVE][RS_BINS];
   __shared__ uint32_t s_base[RS_BINS];
   __shared__ uint64_t s_red[NWAVE + 1];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t n = *d_n;
-  const uint64_t ntiles = (n + OS2_TILE - 1) / OS2_TILE;
+  const uint64_t ntiles = (n + (NT * IPT) - 1) / (NT * IPT);
   if (blockIdx.x >= ntiles) return;
   uint64_t tot;
   const uint32_t dbase = (uint32_t)block_excl_scan(ghist[t], s_red, &tot);
   const uint64_t lt = lane_mask_lt();
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
     for (int i = t; i < NWAVE * RS_BINS; i += NT) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t b0 = tile * OS2_TILE + (uint64_t)wv * WT + lane;
-    K k[OS2_IPT];
-    uint32_t v[OS2_IPT], dg[OS2_IPT], rk[OS2_IPT];
+    const uint64_t b0 = tile * (NT * IPT) + (uint64_t)wv * WT + lane;
+    K k[IPT];
+    uint32_t v[IPT], dg[IPT], rk[IPT];
 #pragma unroll
-    for (int i = 0; i < OS2_IPT; ++i) {
+    for (int i = 0; i < IPT; ++i) {
       const uint64_t j = b0 + (uint64_t)i * 64;
       k[i] = j < n ? kin[j] : (K)0;
       v[i] = j < n ? vin[j] : 0u;
     }
+    if (stamp) {  // phase 1 = keys landed
+      uint64_t z = 0;
 #pragma unroll
-    for (int i = 0; i < OS2_IPT; ++i) {
+      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
+      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
+      sp_stamp(stamp, first, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
       const bool ok = b0 + (uint64_t)i * 64 < n;
       const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
       dg[i] = d;
@@ -354,6 +435,7 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
       wave_lds_sync();
     }
     __syncthreads();
+    sp_stamp(stamp, first, 2);
     // thread t owns digit t: cross-wave exclusive prefix and the tile count
     uint32_t run = 0;
 #pragma unroll
@@ -364,16 +446,439 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
     }
     s_base[t] = dbase + os2_lookback(desc, tile, t, run, err);
     __syncthreads();
+    sp_stamp(stamp, first, 3);
 #pragma unroll
-    for (int i = 0; i < OS2_IPT; ++i) {
+    for (int i = 0; i < IPT; ++i) {
       if (b0 + (uint64_t)i * 64 < n) {
         const uint64_t pos = (uint64_t)s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
+        if (GATHER) {
+          if (pos < go.k) go.out[pos] = EdgeOut{go.cu[v[i]], go.cw[v[i]], go.cs[v[i]]};
+        } else {
+          kout[pos] = k[i];
+          vout[pos] = v[i];
+        }
+      }
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 4);
+  }
+}
+
+// ---------------------------------------------------------------- onesweep pass, 1024-thread tiles
+// Same contract as k_sp_pass.  A tile is 16 waves x IPT substeps x 64 keys, so a
+// tile needs few serial substeps per wave and a small grid covers the keys;
+// per-(substep, wave, digit) counts are u16 in LDS, written by the digit
+// group's leader lane without read-modify-write.  Four threads serve each
+// digit: they prefix-sum the counts and read 64 predecessors per look-back
+// round trip between them.
+constexpr int OSB_NT = 1024;
+constexpr int OSB_NW = OSB_NT / 64;
+
+__device__ __forceinline__ uint32_t osb_lookback(uint32_t* desc, uint64_t tile, int d, int q, uint32_t run,
+                                                 uint32_t* err) {
+  constexpr uint32_t AGG = 1u << 30, PFX = 2u << 30, VAL = AGG - 1;
+  constexpr int R = 16;
+  uint32_t* my = desc + tile * RS_BINS + d;
+  if (tile == 0) {
+    if (q == 0) st_u32(my, PFX | run);
+    return 0;
+  }
+  if (q == 0) st_u32(my, AGG | run);
+  const int gl = lane_id() & ~3;
+  uint32_t excl = 0, spins = 0;
+  int64_t j = (int64_t)tile - 1;
+  while (true) {
+    uint32_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t jj = j - (int64_t)(q * R + r);
+      x[r] = jj >= 0 ? ld_u32(desc + (uint64_t)jj * RS_BINS + d) : PFX;
+    }
+    uint32_t sum = 0;
+    int used = 0, state = 0;  // state: 0 open, 1 found a prefix, 2 blocked
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (state == 0) {
+        const uint32_t st = x[r] >> 30;
+        if (st == 0) {
+          state = 2;
+        } else {
+          sum += x[r] & VAL;
+          ++used;
+          if (st == 2) state = 1;
+        }
+      }
+    }
+    uint32_t tot = 0;
+    int adv = 0, fin = 0;
+    bool stop = false;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const uint32_t s_q = __shfl(sum, gl + qq, 64);
+      const int u_q = __shfl(used, gl + qq, 64);
+      const int st_q = __shfl(state, gl + qq, 64);
+      if (!stop) {
+        tot += s_q;
+        adv += u_q;
+        if (st_q != 0) {
+          stop = true;
+          fin = st_q == 1;
+        }
+      }
+    }
+    excl += tot;
+    if (fin) break;
+    j -= adv;
+    if (adv == 0) {
+      if (++spins > LB_SPIN_LIMIT) {
+        atomicOr(err, 4u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  if (q == 0) st_u32(my, PFX | (excl + run));
+  return excl;
+}
+
+template <typename K, int IPT>
+__global__ __launch_bounds__(OSB_NT) void k_sp_passb(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                     const uint64_t* __restrict__ d_n, int shift,
+                                                     const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
+                                                     uint32_t* __restrict__ err, uint64_t* __restrict__ stamp) {
+  constexpr int WT = 64 * IPT, TILE = OSB_NT * IPT;
+  __shared__ uint16_t s_cnt[IPT][OSB_NW][RS_BINS];
+  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_dbase[RS_BINS];
+  __shared__ uint32_t s_wsum[4];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t n = *d_n;
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
+  if (blockIdx.x >= ntiles) return;
+  // digit bases: exclusive scan of the global histogram (waves 0-3)
+  if (t < RS_BINS) {
+    const uint32_t h = ghist[t];
+    uint32_t inc = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    s_dbase[t] = inc - h;
+  }
+  __syncthreads();
+  if (t < RS_BINS)
+    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
+  const uint64_t lt = lane_mask_lt();
+  const int dg_d = t >> 2, dg_q = t & 3;  // digit group of this thread
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
+    {
+      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
+      for (int i = t; i < IPT * OSB_NW * RS_BINS / 2; i += OSB_NT) z[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
+    K k[IPT];
+    uint32_t v[IPT], dg[IPT], rk[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint64_t j = b0 + (uint64_t)i * 64;
+      k[i] = j < n ? kin[j] : (K)0;
+      v[i] = j < n ? vin[j] : 0u;
+    }
+    if (stamp) {
+      uint64_t z = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
+      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
+      sp_stamp(stamp, first, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const bool ok = b0 + (uint64_t)i * 64 < n;
+      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
+      dg[i] = d;
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      rk[i] = (uint32_t)__popcll(peers & lt);
+      if (ok && (peers & lt) == 0) s_cnt[i][wv][d] = (uint16_t)__popcll(peers);
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 2);
+    // digit group (d, q): waves 4q..4q+3 in tile order (wave-major, substep-minor)
+    uint32_t loc = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) loc += s_cnt[i][dg_q * 4 + w][dg_d];
+    const int gl = lane & ~3;
+    uint32_t before = 0, run = 0;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const uint32_t x = __shfl(loc, gl + qq, 64);
+      before += qq < dg_q ? x : 0u;
+      run += x;
+    }
+    uint32_t acc = before;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t c = s_cnt[i][dg_q * 4 + w][dg_d];
+        s_cnt[i][dg_q * 4 + w][dg_d] = (uint16_t)acc;
+        acc += c;
+      }
+    const uint32_t excl = osb_lookback(desc, tile, dg_d, dg_q, run, err);
+    if (dg_q == 0) s_base[dg_d] = s_dbase[dg_d] + excl;
+    __syncthreads();
+    sp_stamp(stamp, first, 3);
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (b0 + (uint64_t)i * 64 < n) {
+        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_cnt[i][wv][dg[i]] + rk[i];
         kout[pos] = k[i];
         vout[pos] = v[i];
       }
     }
     __syncthreads();
+    sp_stamp(stamp, first, 4);
   }
+}
+
+// ---------------------------------------------------------------- bucket kernel
+// After one stable MSD pass on the top 8 key bits the records form 256
+// buckets (ascending u), each in emission order (ascending v).  One 1024-thread
+// workgroup per bucket: bitonic sort of (key, position) in LDS -- position
+// breaks ties, so runs keep ascending v -- then one thread per position scores
+// the run starting there (first-order exclusion, metric, minScore filter) and
+// the bucket's candidates are compacted in (u, w) order behind the preceding
+// buckets (look-back over bucket ids).  A bucket above BK_CAP raises F_TOOBIG
+// (the host then takes the LSD path).
+constexpr int BK_NT = 1024;
+constexpr int BK_NW = BK_NT / 64;
+constexpr int BK_CAP = 4096;
+constexpr int BK_PER = BK_CAP / BK_NT;
+
+template <bool CUSTOM>
+__global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, float min_score, uint64_t ua,
+                                                     int wbits, const uint64_t* __restrict__ rkey,
+                                                     const uint32_t* __restrict__ rval,
+                                                     const uint32_t* __restrict__ bhist /*256*/,
+                                                     uint32_t* __restrict__ cu, uint32_t* __restrict__ cw,
+                                                     float* __restrict__ cs, uint32_t* __restrict__ okey,
+                                                     uint32_t* __restrict__ oval, uint64_t* __restrict__ desc,
+                                                     uint64_t* __restrict__ ctr, int lbits, uint64_t kmax,
+                                                     uint32_t* __restrict__ ohist /*4 x 256*/,
+                                                     uint64_t* __restrict__ stamp) {
+  __shared__ uint64_t s_k2[2][BK_CAP];
+  __shared__ uint32_t s_oh[4][RS_BINS];
+  __shared__ uint16_t s_p2[2][BK_CAP];
+  __shared__ uint16_t s_cnt[BK_PER][BK_NW][RS_BINS];
+  __shared__ uint32_t s_dig[RS_BINS];
+  __shared__ uint32_t s_wsum[BK_NW];
+  __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_start, s_bcnt;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint32_t b = blockIdx.x;
+  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  const uint64_t n = ctr[C_WSORT];
+  sp_stamp(stamp, true, 0);
+  // bucket bounds: exclusive prefix of the digit histogram (threads 0-255 hold the bins)
+  {
+    const uint32_t h = (n && t < RS_BINS) ? bhist[t] : 0u;
+    uint32_t inc = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = inc - h;
+    for (int w = 0; w < wv; ++w) pre += s_wsum[w];
+    if (t == (int)b) {
+      s_start = pre;
+      s_bcnt = h;
+    }
+    __syncthreads();
+  }
+  const uint32_t start = s_start, c = s_bcnt;
+  sp_stamp(stamp, true, 1);
+  s_oh[t >> 8][t & 255] = 0;
+  const bool toobig = c > (uint32_t)BK_CAP;
+  if (toobig && t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
+  const uint32_t m = toobig ? 0u : c;
+  for (uint32_t i = t; i < m; i += BK_NT) {
+    s_k2[0][i] = rkey[start + i];
+    s_p2[0][i] = (uint16_t)i;
+  }
+  __syncthreads();
+  sp_stamp(stamp, true, 2);
+  // stable LSD radix sort in LDS by the key bits below the bucket digit;
+  // items striped i = r * 1024 + t, ranked in (r, wave, lane) = index order
+  const uint64_t lt = lane_mask_lt();
+  const int rmax = (int)((m + BK_NT - 1) / BK_NT);
+  int cur = 0;
+  for (int sh = 0; sh < lbits; sh += 8) {
+    {
+      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
+      for (int i = t; i < BK_PER * BK_NW * RS_BINS / 2; i += BK_NT) z[i] = 0;
+    }
+    __syncthreads();
+    uint64_t kk[BK_PER];
+    uint16_t pp[BK_PER];
+    uint32_t dd[BK_PER], rk[BK_PER];
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      if (r < rmax) {
+        const uint32_t i = (uint32_t)r * BK_NT + t;
+        const bool ok = i < m;
+        kk[r] = ok ? s_k2[cur][i] : 0ull;
+        pp[r] = ok ? s_p2[cur][i] : (uint16_t)0;
+        const uint32_t d = (uint32_t)(kk[r] >> sh) & 0xffu;
+        dd[r] = d;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int bt = 0; bt < 8; ++bt) {
+          const uint64_t bb = __ballot((d >> bt) & 1u);
+          peers &= ((d >> bt) & 1u) ? bb : ~bb;
+        }
+        rk[r] = (uint32_t)__popcll(peers & lt);
+        if (ok && (peers & lt) == 0) s_cnt[r][wv][d] = (uint16_t)__popcll(peers);
+      }
+    }
+    __syncthreads();
+    // digit t: exclusive prefix over (r, wave); then the digit bases
+    uint32_t tot = 0;
+    if (t < RS_BINS) {
+      for (int r = 0; r < rmax; ++r)
+        for (int w = 0; w < BK_NW; ++w) {
+          const uint32_t c2 = s_cnt[r][w][t];
+          s_cnt[r][w][t] = (uint16_t)tot;
+          tot += c2;
+        }
+      uint32_t inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) s_wsum[wv] = inc;
+      s_dig[t] = inc - tot;
+    }
+    __syncthreads();
+    if (t < RS_BINS)
+      for (int w = 0; w < wv; ++w) s_dig[t] += s_wsum[w];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      if (r < rmax && (uint32_t)r * BK_NT + t < m) {
+        const uint32_t pos = s_dig[dd[r]] + s_cnt[r][wv][dd[r]] + rk[r];
+        s_k2[cur ^ 1][pos] = kk[r];
+        s_p2[cur ^ 1][pos] = pp[r];
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const uint64_t* s_key = s_k2[cur];
+  const uint16_t* s_pos = s_p2[cur];
+  float* s_sc = (float*)s_k2[cur ^ 1];                  // the free buffer holds scores ...
+  uint32_t* s_flag = (uint32_t*)s_k2[cur ^ 1] + BK_CAP;  // ... and flags
+  sp_stamp(stamp, true, 3);
+  // striped: one thread per position scores the run that starts there
+  const uint64_t wmask = (1ull << wbits) - 1;
+  for (uint32_t p = t; p < m; p += BK_NT) {
+    const uint64_t k = s_key[p];
+    uint32_t fl = 0;
+    if (p == 0 || s_key[p - 1] != k) {
+      uint32_t cnt = 0;
+      float acc = 0.0f;
+      for (uint32_t q = p; q < m && s_key[q] == k; ++q) {
+        ++cnt;
+        if (CUSTOM) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
+      }
+      const uint32_t u = (uint32_t)(ua + (k >> wbits)), w = (uint32_t)(k & wmask);
+      const bool excl = contains_u32(g.keys + g.off[u], g.deg[u], w);
+      float sc;
+      if (CUSTOM) sc = excl ? 0.0f : acc;
+      else sc = score_basic(metric, excl ? 0u : cnt, g.deg[u], g.deg[w]);
+      s_sc[p] = sc;
+      fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
+    }
+    s_flag[p] = fl;
+  }
+  __syncthreads();
+  sp_stamp(stamp, true, 4);
+  // blocked scan of the flags: thread t owns positions [4t, 4t+4)
+  uint32_t f[BK_PER], tsum = 0;
+#pragma unroll
+  for (int r = 0; r < BK_PER; ++r) {
+    const uint32_t p = (uint32_t)t * BK_PER + r;
+    f[r] = p < m ? s_flag[p] : 0u;
+    tsum += f[r];
+  }
+  uint32_t inc = tsum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_wsum[wv] = inc;
+  __syncthreads();
+  uint32_t pre = inc - tsum, agg = 0;
+  for (int w = 0; w < BK_NW; ++w) {
+    const uint32_t x = s_wsum[w];
+    pre += w < wv ? x : 0u;
+    agg += x;
+  }
+  if (wv == 0) {
+    const uint64_t e = lb_lookback_r<4>(desc, b, agg, err);
+    if (lane == 0) {
+      s_excl = e;
+      if (b == gridDim.x - 1) {
+        ctr[C_C] = e + agg;
+        ctr[C_OUT_N] = std::min<uint64_t>(e + agg, kmax);
+      }
+    }
+  }
+  __syncthreads();
+  sp_stamp(stamp, true, 5);
+  uint64_t o = s_excl + pre;
+  uint32_t nnan = 0;
+#pragma unroll
+  for (int r = 0; r < BK_PER; ++r) {
+    if (f[r]) {
+      const uint32_t p = (uint32_t)t * BK_PER + r;
+      const uint64_t k = s_key[p];
+      const float sc = s_sc[p];
+      cu[o] = (uint32_t)(ua + (k >> wbits));
+      cw[o] = (uint32_t)(k & wmask);
+      cs[o] = sc;
+      const uint32_t ok = ~score_key(sc);
+      okey[o] = ok;
+      oval[o] = (uint32_t)o;
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) atomicAdd(&s_oh[dd][(ok >> (8 * dd)) & 0xffu], 1u);
+      nnan += sc != sc;
+      ++o;
+    }
+  }
+  if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
+  __syncthreads();
+  {
+    const uint32_t hc = s_oh[t >> 8][t & 255];
+    if (hc) atomicAdd(&ohist[t], hc);
+  }
+  sp_stamp(stamp, true, 6);
 }
 
 // ---------------------------------------------------------------- generic single-pass scan

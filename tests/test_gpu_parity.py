@@ -229,7 +229,7 @@ def star_csr(leaves=12000):
     return np.array(off, np.uint64), np.array(keys, np.uint32)
 
 
-@pytest.mark.parametrize("grouping", ["sort", "bucket"])
+@pytest.mark.parametrize("grouping", ["sort", "lsd", "bucket"])
 def test_gpu_oversized_bucket_falls_back(gpu, oracle, grouping):
     """A source with a huge wedge bucket: the sort grouping has no size limit
     (path 1); the bucket grouping exceeds its LDS cap and falls back (path 3)."""
@@ -241,20 +241,22 @@ def test_gpu_oversized_bucket_falls_back(gpu, oracle, grouping):
                 u, w, s, t = G.predict(m, H, k)
                 eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
                 assert_canonical_equal(eu, ew, es, u, w, s)
-                assert t["path"] == (1 if grouping == "sort" else 3)
+                assert t["path"] == (3 if grouping == "bucket" else 1)
     finally:
         del os.environ["NLP_GROUPING"]
 
 
-def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle):
-    """The two sync-free groupings (wedge-record sort / per-source buckets)
-    give identical results and counters, IHub included (sort grouping only)."""
+@pytest.mark.parametrize("other", ["bucket", "lsd"])
+def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
+    """The sync-free groupings (wedge records: MSD buckets / full LSD sort;
+    per-source buckets) give identical results and counters, IHub included
+    (sort groupings only)."""
     off, keys = random_csr(8000, 14, 7)
     k = 3000
     with gpu.Graph(off, keys) as Gs:
         res = {(m, H): Gs.predict(m, H, k) for m in range(9) for H in (0, 1, 2, 4, 16)}
     try:
-        os.environ["NLP_GROUPING"] = "bucket"
+        os.environ["NLP_GROUPING"] = other
         with gpu.Graph(off, keys) as Gb:
             for (m, H), (u, w, s, t) in res.items():
                 assert t["path"] == 1
