@@ -65,6 +65,37 @@ __device__ __forceinline__ bool contains_u32(const uint32_t* __restrict__ a, uin
   return lo < n && a[lo] == x;
 }
 
+// Membership in a sorted array with 8-way splits: each round trip issues 7
+// independent pivot loads, so a lookup in a hub's adjacency costs about
+// log8(n) + 1 dependent loads instead of log2(n) (the loads, not the
+// compares, are what a latency-bound scoring thread waits on).
+__device__ __forceinline__ bool contains_u32_k8(const uint32_t* __restrict__ a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;  // the lower bound of x lies in [lo, hi]
+  while (hi - lo > 8) {
+    const uint32_t step = (hi - lo + 7) / 8;
+    uint32_t piv[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const uint32_t idx = lo + (uint32_t)(j + 1) * step;
+      piv[j] = idx < hi ? a[idx] : 0xffffffffu;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) c += (lo + (uint32_t)(j + 1) * step < hi && piv[j] < x) ? 1u : 0u;
+    const uint32_t nlo = c ? lo + c * step + 1 : lo;
+    const uint32_t p = lo + (c + 1) * step;
+    hi = (c < 7 && p < hi) ? p : hi;
+    lo = nlo;
+  }
+  bool f = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t idx = lo + (uint32_t)j;
+    f |= idx < hi && a[idx] == x;
+  }
+  return f || (hi < n && a[hi] == x);
+}
+
 // ---------------------------------------------------------------- graph build
 __global__ void k_degrees(const uint64_t* __restrict__ off, uint64_t span, uint32_t* __restrict__ deg,
                           uint32_t* __restrict__ maxdeg, uint32_t* __restrict__ bad) {

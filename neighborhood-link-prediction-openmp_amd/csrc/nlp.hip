@@ -130,6 +130,10 @@ struct nlp_graph {
   bool force_radix = false;                    // test hook: NLP_FORCE_RADIX=1
   bool sort_grouping = true;                   // NLP_GROUPING=bucket selects the per-source bucket grouping
   bool sort_lsd = false;                       // NLP_GROUPING=lsd: full LSD record sort (no MSD buckets)
+  // degree-class index (sortpath.hpp): vertices of degree 1..DCAP grouped by degree
+  uint32_t* vbydeg = nullptr;
+  std::vector<uint64_t> dstart;                // class d occupies [dstart[d], dstart[d + 1]) (class 1 at 0)
+  bool use_dindex = true;                      // NLP_NO_DINDEX=1: always scan deg[] for survivors
   // NLP_STAMP=<file>: per-workgroup phase stamps of the timed stage appended to <file> (diagnostics)
   uint64_t* d_stamp = nullptr;
   uint32_t stamp_blocks = 0;
@@ -222,6 +226,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->off) (void)hipFree(g->off);
   if (g->keys) (void)hipFree(g->keys);
   if (g->deg) (void)hipFree(g->deg);
+  if (g->vbydeg) (void)hipFree(g->vbydeg);
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   for (int i = 0; i < 8; ++i)
@@ -314,6 +319,28 @@ nlp_status finish_graph(nlp_graph* g) {
       TRY(hipFree(tkeys));
     }
   }
+  // Degree-class index: survivors of any H <= DCAP without a pass over deg[].
+  {
+    uint32_t* hist;
+    TRY(wsget(g->ws, B_C32, DCAP + 2, &hist));
+    TRY(hipMemsetAsync(hist, 0, (DCAP + 2) * 4, st));
+    hipLaunchKernelGGL(k_deg_class_hist, dim3(grid_for(S)), dim3(NT), 0, st, (const uint32_t*)g->deg, S, hist);
+    TRY(hipGetLastError());
+    std::vector<uint32_t> hh(DCAP + 2);
+    TRY(hipMemcpyAsync(hh.data(), hist, (DCAP + 2) * 4, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    g->dstart.assign(DCAP + 2, 0);
+    for (uint32_t d = 1; d <= DCAP; ++d) g->dstart[d + 1] = g->dstart[d] + hh[d];
+    const uint64_t nv = g->dstart[DCAP + 1];
+    TRY(hipMalloc(&g->vbydeg, std::max<uint64_t>(nv, 1) * 4));
+    unsigned long long* cur;
+    TRY(wsget(g->ws, B_SCAN, DCAP + 2, &cur));
+    TRY(hipMemcpyAsync(cur, g->dstart.data(), (DCAP + 2) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_deg_class_scatter, dim3(grid_for(S)), dim3(NT), 0, st, (const uint32_t*)g->deg, S, cur,
+                       g->vbydeg);
+    TRY(hipGetLastError());
+    TRY(hipStreamSynchronize(st));
+  }
   // AA / RA contribution tables, computed on the host with the same libm the
   // reference uses (glibc log), indexed by degree.
   std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
@@ -346,6 +373,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipMalloc(&g->d_stamp, 8 * 65536 * 8));
     TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
   }
+  if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
   if (const char* gr = getenv("NLP_GROUPING")) {
     g->sort_grouping = strcmp(gr, "bucket") != 0;
     g->sort_lsd = strcmp(gr, "lsd") == 0;
@@ -1123,6 +1151,9 @@ struct SpBufs {
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
   int msd_shift;  // shift of that digit
+  bool dindex;    // survivors = a prefix of the degree-class index (no k_sp_survivors)
+  uint64_t nv;    // survivors when dindex
+  const uint32_t* survivors;
 };
 
 inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 1)
@@ -1154,6 +1185,13 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd) {
   f.passes = (f.wbits + ubits + 7) / 8;
   f.msd = msd;
   f.msd_shift = std::max(0, f.wbits + ubits - 8);
+  // The count metrics do not depend on the order of a run's wedges, so their
+  // survivors can come from the degree-class index in any order; Adamic-Adar and
+  // Resource-Allocation sum in ascending v and keep the ordered survivor scan.
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  f.dindex = g->use_dindex && !custom && p.H >= 1 && p.H <= DCAP && g->vbydeg;
+  f.nv = f.dindex ? g->dstart[p.H + 1] : 0;
+  f.survivors = f.dindex ? g->vbydeg : f.surv;
   const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + EX_TILE - 1) / EX_TILE;
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, RS_BINS);
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
@@ -1209,19 +1247,20 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     if (s == 0) {
       CtrInit ci;
       for (int i = 0; i < NCTR; ++i) ci.v[i] = 0;
+      ci.v[C_NV] = f.nv;
       hipLaunchKernelGGL(k_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (f.arena_words + NT - 1) / NT)),
                          dim3(NT), 0, st, f.arena, f.arena_words, ci);
     } else if (s == 1) {
+      if (f.dindex) return NLP_OK;
       hipLaunchKernelGGL(k_sp_survivors<>, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
                          (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, ctr, hot == 1 ? g->d_stamp : nullptr);
     } else if (s == 2) {
       if (f.msd)  // the MSD digit histogram is fused into the expansion
         hipLaunchKernelGGL(k_sp_expand<true>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua,
-                           ub, f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr,
-                           f.msd_shift, hrec);
+                           ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, f.msd_shift, hrec);
       else
         hipLaunchKernelGGL(k_sp_expand<false>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv,
-                           ua, ub, f.wbits, (const uint32_t*)f.surv, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, 0,
+                           ua, ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, 0,
                            (uint32_t*)nullptr);
     } else if (s == 3) {
       if (f.msd) return NLP_OK;

@@ -204,6 +204,36 @@ __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- degree-class index
+// Built once per graph: the vertices of degree 1..DCAP grouped by degree, so
+// the survivors of any hub threshold H <= DCAP are one contiguous prefix and a
+// prediction needs no pass over deg[].  Order inside a class is arbitrary; it
+// is used only where the accumulation order of a run cannot matter (the count
+// metrics), the Adamic-Adar / Resource-Allocation sums keep k_sp_survivors.
+constexpr uint32_t DCAP = 1024;
+
+__global__ __launch_bounds__(NT) void k_deg_class_hist(const uint32_t* __restrict__ deg, uint64_t S,
+                                                       uint32_t* __restrict__ hist /*DCAP + 2*/) {
+  __shared__ uint32_t h[DCAP + 2];
+  for (uint32_t i = threadIdx.x; i < DCAP + 2; i += NT) h[i] = 0;
+  __syncthreads();
+  for (uint64_t v = (uint64_t)blockIdx.x * NT + threadIdx.x; v < S; v += (uint64_t)gridDim.x * NT)
+    atomicAdd(&h[std::min<uint32_t>(deg[v], DCAP + 1)], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < DCAP + 2; i += NT)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// cursor[d] starts at the first slot of class d (relative to class 1).
+__global__ __launch_bounds__(NT) void k_deg_class_scatter(const uint32_t* __restrict__ deg, uint64_t S,
+                                                          unsigned long long* __restrict__ cursor,
+                                                          uint32_t* __restrict__ vbydeg) {
+  for (uint64_t v = (uint64_t)blockIdx.x * NT + threadIdx.x; v < S; v += (uint64_t)gridDim.x * NT) {
+    const uint32_t d = deg[v];
+    if (d >= 1 && d <= DCAP) vbydeg[atomicAdd(&cursor[d], 1ull)] = (uint32_t)v;
+  }
+}
+
 // ---------------------------------------------------------------- wedge records
 // One thread per survivor v (ascending): for each in-edge u -> v with u in
 // [ua, ub), the wedges (u, v, w) with w in N(v), w > u.  Records beyond capW are
@@ -457,6 +487,200 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
           kout[pos] = k[i];
           vout[pos] = v[i];
         }
+      }
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 4);
+  }
+}
+
+// ---------------------------------------------------------------- onesweep pass, general tile shape
+// Same contract as k_sp_pass.  NTB threads (256 or 512) x IPT substeps per
+// tile.  Per-(substep, wave, digit) counts are written once by the digit
+// group's leader lane (no read-modify-write chain inside the ranking loop).
+// G = NTB / 256 threads serve each digit: they prefix-sum its counts and read
+// LBR predecessors each per look-back round trip (G * LBR per round trip).
+template <int G, int LBR>
+__device__ __forceinline__ uint32_t osg_lookback(uint32_t* desc, uint64_t tile, int d, int q, uint32_t run,
+                                                 uint32_t* err) {
+  constexpr uint32_t AGG = 1u << 30, PFX = 2u << 30, VAL = AGG - 1;
+  uint32_t* my = desc + tile * RS_BINS + d;
+  if (tile == 0) {
+    if (q == 0) st_u32(my, PFX | run);
+    return 0;
+  }
+  if (q == 0) st_u32(my, AGG | run);
+  const int gl = lane_id() & ~(G - 1);
+  uint32_t excl = 0, spins = 0;
+  int64_t j = (int64_t)tile - 1;
+  while (true) {
+    uint32_t x[LBR];
+#pragma unroll
+    for (int r = 0; r < LBR; ++r) {
+      const int64_t jj = j - (int64_t)(q * LBR + r);
+      x[r] = jj >= 0 ? ld_u32(desc + (uint64_t)jj * RS_BINS + d) : PFX;
+    }
+    uint32_t sum = 0;
+    int used = 0, state = 0;  // 0 open, 1 reached a prefix, 2 blocked on an unpublished tile
+#pragma unroll
+    for (int r = 0; r < LBR; ++r) {
+      if (state == 0) {
+        const uint32_t st = x[r] >> 30;
+        if (st == 0) {
+          state = 2;
+        } else {
+          sum += x[r] & VAL;
+          ++used;
+          if (st == 2) state = 1;
+        }
+      }
+    }
+    uint32_t tot = sum;
+    int adv = used, fin = state == 1;
+    if (G > 1) {
+      tot = 0;
+      adv = 0;
+      fin = 0;
+      bool stop = false;
+#pragma unroll
+      for (int qq = 0; qq < G; ++qq) {
+        const uint32_t s_q = __shfl(sum, gl + qq, 64);
+        const int u_q = __shfl(used, gl + qq, 64);
+        const int st_q = __shfl(state, gl + qq, 64);
+        if (!stop) {
+          tot += s_q;
+          adv += u_q;
+          if (st_q != 0) {
+            stop = true;
+            fin = st_q == 1;
+          }
+        }
+      }
+    }
+    excl += tot;
+    if (fin) break;
+    j -= adv;
+    if (adv == 0) {
+      if (++spins > LB_SPIN_LIMIT) {
+        atomicOr(err, 4u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  if (q == 0) st_u32(my, PFX | (excl + run));
+  return excl;
+}
+
+template <typename K, int NTB, int IPT, int LBR>
+__global__ __launch_bounds__(NTB) void k_sp_pass2(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                  const uint64_t* __restrict__ d_n, int shift,
+                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
+                                                  uint32_t* __restrict__ err, uint64_t* __restrict__ stamp) {
+  constexpr int NW = NTB / 64, G = NTB / RS_BINS, WT = 64 * IPT, TILE = NTB * IPT;
+  static_assert(G == 1 || G == 2 || G == 4, "threads per digit");
+  __shared__ uint16_t s_cnt[IPT][NW][RS_BINS];
+  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_dbase[RS_BINS];
+  __shared__ uint32_t s_wsum[4];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t n = *d_n;
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
+  if (blockIdx.x >= ntiles) return;
+  if (t < RS_BINS) {  // digit bases: exclusive scan of the global histogram
+    const uint32_t h = ghist[t];
+    uint32_t inc = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    s_dbase[t] = inc - h;
+  }
+  __syncthreads();
+  if (t < RS_BINS)
+    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
+  const uint64_t lt = lane_mask_lt();
+  const int dd_d = t / G, dd_q = t % G;  // digit group of this thread
+  constexpr int WPQ = NW / G;            // waves summed by each thread of a digit group
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
+    {
+      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
+      for (int i = t; i < IPT * NW * RS_BINS / 2; i += NTB) z[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
+    K k[IPT];
+    uint32_t v[IPT], dg[IPT], rk[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint64_t j = b0 + (uint64_t)i * 64;
+      k[i] = j < n ? kin[j] : (K)0;
+      v[i] = j < n ? vin[j] : 0u;
+    }
+    if (stamp) {
+      uint64_t z = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
+      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
+      sp_stamp(stamp, first, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const bool ok = b0 + (uint64_t)i * 64 < n;
+      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
+      dg[i] = d;
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      rk[i] = (uint32_t)__popcll(peers & lt);
+      if (ok && (peers & lt) == 0) s_cnt[i][wv][d] = (uint16_t)__popcll(peers);
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 2);
+    // digit group (d, q): waves [q WPQ, (q+1) WPQ) in tile order (wave-major, substep-minor)
+    uint32_t loc = 0;
+#pragma unroll
+    for (int w = 0; w < WPQ; ++w)
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) loc += s_cnt[i][dd_q * WPQ + w][dd_d];
+    uint32_t before = 0, run = loc;
+    if (G > 1) {
+      const int gl = lane & ~(G - 1);
+      run = 0;
+#pragma unroll
+      for (int qq = 0; qq < G; ++qq) {
+        const uint32_t x = __shfl(loc, gl + qq, 64);
+        before += qq < dd_q ? x : 0u;
+        run += x;
+      }
+    }
+    uint32_t acc = before;
+#pragma unroll
+    for (int w = 0; w < WPQ; ++w)
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) {
+        const uint32_t c = s_cnt[i][dd_q * WPQ + w][dd_d];
+        s_cnt[i][dd_q * WPQ + w][dd_d] = (uint16_t)acc;
+        acc += c;
+      }
+    const uint32_t excl = osg_lookback<G, LBR>(desc, tile, dd_d, dd_q, run, err);
+    if (dd_q == 0) s_base[dd_d] = s_dbase[dd_d] + excl;
+    __syncthreads();
+    sp_stamp(stamp, first, 3);
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (b0 + (uint64_t)i * 64 < n) {
+        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_cnt[i][wv][dg[i]] + rk[i];
+        kout[pos] = k[i];
+        vout[pos] = v[i];
       }
     }
     __syncthreads();
@@ -807,10 +1031,11 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
         if (CUSTOM) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
       }
       const uint32_t u = (uint32_t)(ua + (k >> wbits)), w = (uint32_t)(k & wmask);
-      const bool excl = contains_u32(g.keys + g.off[u], g.deg[u], w);
+      const uint32_t du = g.deg[u], dw = CUSTOM ? 0u : g.deg[w];
+      const bool excl = contains_u32(g.keys + g.off[u], du, w);
       float sc;
       if (CUSTOM) sc = excl ? 0.0f : acc;
-      else sc = score_basic(metric, excl ? 0u : cnt, g.deg[u], g.deg[w]);
+      else sc = score_basic(metric, excl ? 0u : cnt, du, dw);
       s_sc[p] = sc;
       fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
     }
@@ -866,10 +1091,26 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
       const uint32_t ok = ~score_key(sc);
       okey[o] = ok;
       oval[o] = (uint32_t)o;
-#pragma unroll
-      for (int dd = 0; dd < 4; ++dd) atomicAdd(&s_oh[dd][(ok >> (8 * dd)) & 0xffu], 1u);
+      atomicAdd(&s_oh[0][ok & 0xffu], 1u);
+      atomicAdd(&s_oh[1][(ok >> 8) & 0xffu], 1u);
       nnan += sc != sc;
       ++o;
+    }
+  }
+  // the two top digits of score keys are shared by many candidates (few
+  // exponents): peel one digit value per iteration and add its wave count once
+  for (int r = 0; r < BK_PER; ++r) {
+    const uint32_t ok = f[r] ? ~score_key(s_sc[(uint32_t)t * BK_PER + r]) : 0u;
+    for (int dd = 2; dd < 4; ++dd) {
+      const uint32_t d = (ok >> (8 * dd)) & 0xffu;
+      uint64_t todo = __ballot(f[r] != 0);
+      while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const uint32_t dl = __shfl(d, leader, 64);
+        const uint64_t same = todo & __ballot(d == dl);
+        if (lane == leader) atomicAdd(&s_oh[dd][dl], (uint32_t)__popcll(same));
+        todo &= ~same;
+      }
     }
   }
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);

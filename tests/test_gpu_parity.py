@@ -331,3 +331,25 @@ def test_gpu_graph_replay_equals_direct_launch(gpu, oracle):
                 assert_canonical_equal(eu, ew, es, u, w, s)
     finally:
         del os.environ["NLP_NO_GRAPH"]
+
+
+def test_gpu_degree_index_equals_survivor_scan(gpu, oracle):
+    """Count metrics take their survivors from the degree-class index (any
+    order within a degree); the result must equal the ordered survivor scan and
+    the oracle, including thresholds at and above the index cap."""
+    off, keys = random_csr(7000, 12, 11)
+    cases = [(m, H) for m in (0, 1, 2, 3, 4, 5, 6) for H in (1, 2, 4, 9, 1024, 2000)]
+    with gpu.Graph(off, keys) as G:
+        res = {c: G.predict(c[0], c[1], 2500) for c in cases}
+    try:
+        os.environ["NLP_NO_DINDEX"] = "1"
+        with gpu.Graph(off, keys) as G2:
+            for (m, H), (u, w, s, t) in res.items():
+                u2, w2, s2, t2 = G2.predict(m, H, 2500)
+                assert_canonical_equal(u2, w2, s2, u, w, s)
+                assert t["wedges"] == t2["wedges"] and t["candidates"] == t2["candidates"]
+    finally:
+        del os.environ["NLP_NO_DINDEX"]
+    for (m, H), (u, w, s, t) in list(res.items())[::5]:
+        eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=2500)
+        assert_canonical_equal(eu, ew, es, u, w, s)
