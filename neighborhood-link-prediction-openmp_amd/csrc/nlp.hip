@@ -1275,7 +1275,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                          odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT],
                          f.msd ? f.msd_shift : 8 * ps,
                          (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err,
-                         hot == s ? g->d_stamp : nullptr, GatherOut{});
+                         hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
     } else if (s == s_runs && f.msd) {
       if (custom)
         hipLaunchKernelGGL(k_sp_bucket<true>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
@@ -1307,11 +1307,16 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(NT), 0, st,
+      if (f.msd && ps == 0)  // k_sp_bucket counted digit 0; this pass counts digits 1-3
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true>), grid(tO, g->occ_p32), dim3(NT), 0, st,
+                           (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1, (const uint64_t*)&ctr[C_C],
+                           0, (const uint32_t*)hord, dord, err, (uint64_t*)nullptr, GatherOut{}, hord + RS_BINS);
+      else
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(NT), 0, st,
                            (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
                            odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
                            (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, err,
-                           (uint64_t*)nullptr, GatherOut{});
+                           (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr);
     } else {
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
@@ -1352,9 +1357,10 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
 static const int EV_SEG4[4] = {0, 3, 4, 1};  // bucket grouping: pre | hot | rest of scoring | selection
 static const int EV_SEG3[3] = {0, 3, 4};     // sort grouping: pre | hot (scoring) | selection
 
+// copy_src: the device counters the pipeline copies to host_small at its end.
 template <class L>
-nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, int mode, bool* replayed,
-                     L&& launch) {
+nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, int mode, const void* copy_src,
+                     bool* replayed, L&& launch) {
   *replayed = false;
   if (!g->use_graphs) return NLP_OK;
   const bool single = g->graph_single && mode != 0;  // the bucket grouping is captured in segments
@@ -1381,22 +1387,62 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
         fprintf(stderr, "nlp: graph capture failed (seg=%d launch=%d end=%s)\n", seg, (int)s, hipGetErrorString(e));
     }
     if (ok && single) {
-      // one graph: event-record nodes around the four segments as child graphs,
-      // so a call is a single launch and the events still time the hot kernel
+      // One flat graph: the segments' kernel nodes copied in order with
+      // event-record nodes between them, so a call is a single launch and the
+      // events still time the hot kernel.  (Child-graph nodes would work too but
+      // cost several microseconds per boundary.)  The segments are linear
+      // chains of kernel nodes plus the final counter copy, which is re-added.
       hipGraph_t top = nullptr;
       bool ok1 = hipGraphCreate(&top, 0) == hipSuccess;
       hipGraphNode_t prev = nullptr;
+      auto link = [&](hipGraphNode_t n) { prev = n; };
       auto chain_ev = [&](int e) {
         hipGraphNode_t n = nullptr;
         ok1 = ok1 && hipGraphAddEventRecordNode(&n, top, prev ? &prev : nullptr, prev ? 1 : 0, g->gev[e]) == hipSuccess;
-        prev = n;
+        link(n);
+      };
+      bool saw_copy = false;
+      auto append = [&](hipGraph_t sg) {
+        size_t nr = 0;
+        ok1 = ok1 && hipGraphGetRootNodes(sg, nullptr, &nr) == hipSuccess;
+        if (!ok1 || nr == 0) return;
+        if (nr != 1) { ok1 = false; return; }
+        hipGraphNode_t node = nullptr;
+        ok1 = hipGraphGetRootNodes(sg, &node, &nr) == hipSuccess;
+        while (ok1 && node) {
+          hipGraphNodeType ty;
+          ok1 = hipGraphNodeGetType(node, &ty) == hipSuccess;
+          if (!ok1) break;
+          if (ty == hipGraphNodeTypeKernel) {
+            hipKernelNodeParams kp;
+            hipGraphNode_t n = nullptr;
+            ok1 = hipGraphKernelNodeGetParams(node, &kp) == hipSuccess &&
+                  hipGraphAddKernelNode(&n, top, prev ? &prev : nullptr, prev ? 1 : 0, &kp) == hipSuccess;
+            link(n);
+          } else if (ty == hipGraphNodeTypeMemcpy) {
+            saw_copy = true;  // the counter copy, re-added at the end
+          } else {
+            ok1 = false;
+            break;
+          }
+          size_t nd = 0;
+          ok1 = ok1 && hipGraphNodeGetDependentNodes(node, nullptr, &nd) == hipSuccess;
+          if (!ok1 || nd == 0) break;
+          if (nd != 1) { ok1 = false; break; }
+          ok1 = hipGraphNodeGetDependentNodes(node, &node, &nd) == hipSuccess;
+        }
       };
       for (int seg = 0; seg < nseg && ok1; ++seg) {
         chain_ev(ev_before[seg]);
-        hipGraphNode_t n = nullptr;
-        ok1 = ok1 && hipGraphAddChildGraphNode(&n, top, &prev, 1, seg_graph[seg]) == hipSuccess;
-        prev = n;
+        append(seg_graph[seg]);
       }
+      if (ok1 && saw_copy) {
+        hipGraphNode_t n = nullptr;
+        ok1 = hipGraphAddMemcpyNode1D(&n, top, prev ? &prev : nullptr, prev ? 1 : 0, g->host_small, copy_src,
+                                      NCTR * 8, hipMemcpyDeviceToHost) == hipSuccess;
+        link(n);
+      }
+      ok1 = ok1 && saw_copy;
       if (ok1) chain_ev(2);
       if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
       if (top) (void)hipGraphDestroy(top);
@@ -1470,10 +1516,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     bool replayed = false;
     g->last_single = false;
     if (sorted)
-      s = run_graph(g, p, out, st, msd ? 2 : 1, &replayed,
+      s = run_graph(g, p, out, st, msd ? 2 : 1, sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
     else
-      s = run_graph(g, p, out, st, 0, &replayed,
+      s = run_graph(g, p, out, st, 0, f.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
     if (s != NLP_OK) return s;
     if (!replayed) {

@@ -40,10 +40,24 @@ namespace nlp {
 
 enum { C_WSORT = 11 };  // wedge records to sort (0 after a capacity overflow)
 
+// Digit histograms are kept in HCOPIES copies (workgroup b adds into copy
+// b % HCOPIES, readers sum the copies): thousands of workgroups adding into one
+// 4 KiB histogram serialise on a few cache lines.
+constexpr int HCOPIES = 16;
+constexpr uint32_t HSTRIDE = 8 * 256;  // u32 per copy: up to 8 digits of 256 bins
+
 // Arena (u64 words): counters [0, 16), digit histograms, look-back descriptors.
-constexpr uint64_t SP_HREC = 16;               // 8 x 256 u32: record-key digits
-constexpr uint64_t SP_HORD = SP_HREC + 1024;   // 4 x 256 u32: score-key digits
-constexpr uint64_t SP_DESC = SP_HORD + 512;    // descriptors follow
+constexpr uint64_t SP_HREC = 16;                                 // record-key digits
+constexpr uint64_t SP_HORD = SP_HREC + HCOPIES * HSTRIDE / 2;    // score-key digits
+constexpr uint64_t SP_DESC = SP_HORD + HCOPIES * HSTRIDE / 2;    // descriptors follow
+
+__device__ __forceinline__ uint32_t* hist_copy(uint32_t* h) { return h + (blockIdx.x % HCOPIES) * HSTRIDE; }
+__device__ __forceinline__ uint32_t hist_total(const uint32_t* h, uint32_t i) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < HCOPIES; ++c) s += h[c * HSTRIDE + i];
+  return s;
+}
 
 constexpr int SV_STEPS = 8;                    // survivor scan: 256-vertex steps per wave
 constexpr int SV_TILE = NT * 4 * SV_STEPS;     // 8192 vertices per tile
@@ -310,7 +324,7 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
   }
   if (HIST) {
     const uint32_t hc = s_h[threadIdx.x];
-    if (hc) atomicAdd(&ghist[threadIdx.x], hc);
+    if (hc) atomicAdd(&hist_copy(ghist)[threadIdx.x], hc);
   }
 }
 
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(NT) void k_sp_hist(const K* __restrict__ keys, cons
   __syncthreads();
   for (int i = threadIdx.x; i < ndig * RS_BINS; i += NT) {
     const uint32_t c = (&h[0][0])[i];
-    if (c) atomicAdd(&ghist[i], c);
+    if (c) atomicAdd(&hist_copy(ghist)[i], c);
   }
 }
 
@@ -408,15 +422,19 @@ struct GatherOut {
   EdgeOut* out;
 };
 
-template <typename K, int IPT = OS2_IPT, bool GATHER = false>
+// NEXT_HIST: also count digits 1..3 (shift 8, 16, 24) of the input keys into
+// the histogram copies at nhist (the first pass of a 32-bit sort whose later
+// histograms were not produced upstream).
+template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false>
 __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                 K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                 const uint64_t* __restrict__ d_n, int shift,
                                                 const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
                                                 uint32_t* __restrict__ err, uint64_t* __restrict__ stamp,
-                                                GatherOut go) {
+                                                GatherOut go, uint32_t* __restrict__ nhist = nullptr) {
   constexpr int WT = 64 * IPT;
   __shared__ uint32_t s_wcnt[NWAVE][RS_BINS];
+  __shared__ uint32_t s_nh[NEXT_HIST ? 3 : 1][NEXT_HIST ? RS_BINS : 1];
   __shared__ uint32_t s_base[RS_BINS];
   __shared__ uint64_t s_red[NWAVE + 1];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
@@ -424,8 +442,10 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
   const uint64_t ntiles = (n + (NT * IPT) - 1) / (NT * IPT);
   if (blockIdx.x >= ntiles) return;
   uint64_t tot;
-  const uint32_t dbase = (uint32_t)block_excl_scan(ghist[t], s_red, &tot);
+  const uint32_t dbase = (uint32_t)block_excl_scan(hist_total(ghist, t), s_red, &tot);
   const uint64_t lt = lane_mask_lt();
+  if (NEXT_HIST)
+    for (int i = t; i < 3 * RS_BINS; i += NT) (&s_nh[0][0])[i] = 0;
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const bool first = tile == blockIdx.x;
     sp_stamp(stamp, first, 0);
@@ -487,10 +507,21 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
           kout[pos] = k[i];
           vout[pos] = v[i];
         }
+        if (NEXT_HIST) {
+#pragma unroll
+          for (int dd = 0; dd < 3; ++dd) atomicAdd(&s_nh[dd][(uint32_t)(k[i] >> (8 * dd + 8)) & 0xffu], 1u);
+        }
       }
     }
     __syncthreads();
     sp_stamp(stamp, first, 4);
+  }
+  if (NEXT_HIST) {
+    uint32_t* hc = hist_copy(nhist);
+    for (int i = t; i < 3 * RS_BINS; i += NT) {
+      const uint32_t c = s_nh[i / RS_BINS][i % RS_BINS];
+      if (c) atomicAdd(&hc[i], c);
+    }
   }
 }
 
@@ -589,7 +620,7 @@ __global__ __launch_bounds__(NTB) void k_sp_pass2(const K* __restrict__ kin, con
   const uint64_t ntiles = (n + TILE - 1) / TILE;
   if (blockIdx.x >= ntiles) return;
   if (t < RS_BINS) {  // digit bases: exclusive scan of the global histogram
-    const uint32_t h = ghist[t];
+    const uint32_t h = hist_total(ghist, t);
     uint32_t inc = h;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -782,7 +813,7 @@ __global__ __launch_bounds__(OSB_NT) void k_sp_passb(const K* __restrict__ kin, 
   if (blockIdx.x >= ntiles) return;
   // digit bases: exclusive scan of the global histogram (waves 0-3)
   if (t < RS_BINS) {
-    const uint32_t h = ghist[t];
+    const uint32_t h = hist_total(ghist, t);
     uint32_t inc = h;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -903,7 +934,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
                                                      uint32_t* __restrict__ ohist /*4 x 256*/,
                                                      uint64_t* __restrict__ stamp) {
   __shared__ uint64_t s_k2[2][BK_CAP];
-  __shared__ uint32_t s_oh[4][RS_BINS];
+  __shared__ uint32_t s_oh[1][RS_BINS];
   __shared__ uint16_t s_p2[2][BK_CAP];
   __shared__ uint16_t s_cnt[BK_PER][BK_NW][RS_BINS];
   __shared__ uint32_t s_dig[RS_BINS];
@@ -917,7 +948,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   sp_stamp(stamp, true, 0);
   // bucket bounds: exclusive prefix of the digit histogram (threads 0-255 hold the bins)
   {
-    const uint32_t h = (n && t < RS_BINS) ? bhist[t] : 0u;
+    const uint32_t h = (n && t < RS_BINS) ? hist_total(bhist, t) : 0u;
     uint32_t inc = h;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -936,7 +967,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   }
   const uint32_t start = s_start, c = s_bcnt;
   sp_stamp(stamp, true, 1);
-  s_oh[t >> 8][t & 255] = 0;
+  if (t < RS_BINS) s_oh[0][t] = 0;
   const bool toobig = c > (uint32_t)BK_CAP;
   if (toobig && t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
   const uint32_t m = toobig ? 0u : c;
@@ -1018,28 +1049,82 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   float* s_sc = (float*)s_k2[cur ^ 1];                  // the free buffer holds scores ...
   uint32_t* s_flag = (uint32_t*)s_k2[cur ^ 1] + BK_CAP;  // ... and flags
   sp_stamp(stamp, true, 3);
-  // striped: one thread per position scores the run that starts there
+  // striped: thread t scores the runs starting at positions t + 1024 r.  A
+  // thread's (up to BK_PER) runs are scored together: their independent loads
+  // and the steps of their membership searches are issued side by side, so a
+  // thread waits for one search chain, not BK_PER of them in a row.
   const uint64_t wmask = (1ull << wbits) - 1;
-  for (uint32_t p = t; p < m; p += BK_NT) {
-    const uint64_t k = s_key[p];
-    uint32_t fl = 0;
-    if (p == 0 || s_key[p - 1] != k) {
-      uint32_t cnt = 0;
-      float acc = 0.0f;
-      for (uint32_t q = p; q < m && s_key[q] == k; ++q) {
-        ++cnt;
-        if (CUSTOM) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
+  uint32_t ru[BK_PER], rw[BK_PER], rc[BK_PER], lo[BK_PER], hi[BK_PER], du[BK_PER], dw[BK_PER];
+  uint64_t ro[BK_PER];
+  float racc[BK_PER];
+  bool start_r[BK_PER];
+#pragma unroll
+  for (int r = 0; r < BK_PER; ++r) {
+    const uint32_t p = (uint32_t)t + (uint32_t)r * BK_NT;
+    start_r[r] = false;
+    if (p < m) {
+      const uint64_t k = s_key[p];
+      if (p == 0 || s_key[p - 1] != k) {
+        uint32_t cnt = 0;
+        float acc = 0.0f;
+        for (uint32_t q = p; q < m && s_key[q] == k; ++q) {
+          ++cnt;
+          if (CUSTOM) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
+        }
+        start_r[r] = true;
+        ru[r] = (uint32_t)(ua + (k >> wbits));
+        rw[r] = (uint32_t)(k & wmask);
+        rc[r] = cnt;
+        racc[r] = acc;
       }
-      const uint32_t u = (uint32_t)(ua + (k >> wbits)), w = (uint32_t)(k & wmask);
-      const uint32_t du = g.deg[u], dw = CUSTOM ? 0u : g.deg[w];
-      const bool excl = contains_u32(g.keys + g.off[u], du, w);
-      float sc;
-      if (CUSTOM) sc = excl ? 0.0f : acc;
-      else sc = score_basic(metric, excl ? 0u : cnt, du, dw);
-      s_sc[p] = sc;
-      fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
     }
-    s_flag[p] = fl;
+  }
+#pragma unroll
+  for (int r = 0; r < BK_PER; ++r) {
+    if (start_r[r]) {
+      ro[r] = g.off[ru[r]];
+      du[r] = g.deg[ru[r]];
+      dw[r] = CUSTOM ? 0u : g.deg[rw[r]];
+      lo[r] = 0;
+      hi[r] = du[r];
+    } else {
+      lo[r] = hi[r] = 0;
+    }
+  }
+  // lower bound of w in N(u), the searches in lockstep
+  bool more = true;
+  while (more) {
+    more = false;
+    uint32_t mid[BK_PER], av[BK_PER];
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      mid[r] = (lo[r] + hi[r]) >> 1;
+      av[r] = lo[r] < hi[r] ? g.keys[ro[r] + mid[r]] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      if (lo[r] < hi[r]) {
+        if (av[r] < rw[r]) lo[r] = mid[r] + 1;
+        else hi[r] = mid[r];
+        more |= lo[r] < hi[r];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < BK_PER; ++r) {
+    const uint32_t p = (uint32_t)t + (uint32_t)r * BK_NT;
+    if (p < m) {
+      uint32_t fl = 0;
+      if (start_r[r]) {
+        const bool excl = lo[r] < du[r] && g.keys[ro[r] + lo[r]] == rw[r];
+        float sc;
+        if (CUSTOM) sc = excl ? 0.0f : racc[r];
+        else sc = score_basic(metric, excl ? 0u : rc[r], du[r], dw[r]);
+        s_sc[p] = sc;
+        fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
+      }
+      s_flag[p] = fl;
+    }
   }
   __syncthreads();
   sp_stamp(stamp, true, 4);
@@ -1091,33 +1176,16 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
       const uint32_t ok = ~score_key(sc);
       okey[o] = ok;
       oval[o] = (uint32_t)o;
-      atomicAdd(&s_oh[0][ok & 0xffu], 1u);
-      atomicAdd(&s_oh[1][(ok >> 8) & 0xffu], 1u);
+      atomicAdd(&s_oh[0][ok & 0xffu], 1u);  // digit 0 only: the first ordering pass counts the rest
       nnan += sc != sc;
       ++o;
     }
   }
-  // the two top digits of score keys are shared by many candidates (few
-  // exponents): peel one digit value per iteration and add its wave count once
-  for (int r = 0; r < BK_PER; ++r) {
-    const uint32_t ok = f[r] ? ~score_key(s_sc[(uint32_t)t * BK_PER + r]) : 0u;
-    for (int dd = 2; dd < 4; ++dd) {
-      const uint32_t d = (ok >> (8 * dd)) & 0xffu;
-      uint64_t todo = __ballot(f[r] != 0);
-      while (todo) {
-        const int leader = __ffsll((long long)todo) - 1;
-        const uint32_t dl = __shfl(d, leader, 64);
-        const uint64_t same = todo & __ballot(d == dl);
-        if (lane == leader) atomicAdd(&s_oh[dd][dl], (uint32_t)__popcll(same));
-        todo &= ~same;
-      }
-    }
-  }
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
   __syncthreads();
-  {
-    const uint32_t hc = s_oh[t >> 8][t & 255];
-    if (hc) atomicAdd(&ohist[t], hc);
+  if (t < RS_BINS) {
+    const uint32_t hc = s_oh[0][t];
+    if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
   }
   sp_stamp(stamp, true, 6);
 }

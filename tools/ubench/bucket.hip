@@ -49,9 +49,10 @@ int main(int argc, char** argv) {
   uint32_t *d_keys, *d_deg, *d_rv, *d_hist, *cu, *cw, *ok, *ov, *oh;
   float* cs;
   CK(hipMalloc(&d_off, (S + 1) * 8)); CK(hipMalloc(&d_keys, m * 4)); CK(hipMalloc(&d_deg, S * 4));
-  CK(hipMalloc(&d_rk, W * 8)); CK(hipMalloc(&d_rv, W * 4)); CK(hipMalloc(&d_hist, 256 * 4));
+  CK(hipMalloc(&d_rk, W * 8)); CK(hipMalloc(&d_rv, W * 4)); CK(hipMalloc(&d_hist, HCOPIES * HSTRIDE * 4));
+  CK(hipMemset(d_hist, 0, HCOPIES * HSTRIDE * 4));
   CK(hipMalloc(&cu, W * 4)); CK(hipMalloc(&cw, W * 4)); CK(hipMalloc(&cs, W * 4)); CK(hipMalloc(&ok, W * 4));
-  CK(hipMalloc(&ov, W * 4)); CK(hipMalloc(&oh, 1024 * 4)); CK(hipMalloc(&d_ctr, 16 * 8));
+  CK(hipMalloc(&ov, W * 4)); CK(hipMalloc(&oh, HCOPIES * HSTRIDE * 4)); CK(hipMalloc(&d_ctr, 16 * 8));
   CK(hipMalloc(&d_desc, 260 * 8)); CK(hipMalloc(&d_stamp, 256 * 8 * 8));
   CK(hipMemcpy(d_off, off.data(), (S + 1) * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_keys, keys.data(), m * 4, hipMemcpyHostToDevice));
@@ -68,7 +69,7 @@ int main(int argc, char** argv) {
     h[C_WSORT] = W;
     CK(hipMemcpy(d_ctr, h, 128, hipMemcpyHostToDevice));
     CK(hipMemset(d_desc, 0, 260 * 8));
-    CK(hipMemset(oh, 0, 4096));
+    CK(hipMemset(oh, 0, HCOPIES * HSTRIDE * 4));
     CK(hipMemset(d_stamp, 0, 256 * 64));
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(a, 0));

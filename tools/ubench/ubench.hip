@@ -139,7 +139,7 @@ void bench_pass(Timer& T, uint64_t n, int nbits, bool prefill) {
   CK(hipMalloc(&k1, n * 8));
   CK(hipMalloc(&v0, n * 4));
   CK(hipMalloc(&v1, n * 4));
-  CK(hipMalloc(&hist, 8 * 256 * 4));
+  CK(hipMalloc(&hist, HCOPIES * HSTRIDE * 4));
   CK(hipMalloc(&desc, tiles * 256 * 4));
   CK(hipMalloc(&err, 4));
   CK(hipMalloc(&dn, 8));
@@ -147,7 +147,7 @@ void bench_pass(Timer& T, uint64_t n, int nbits, bool prefill) {
   CK(hipMemcpy(k0, hk.data(), n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(v0, hv.data(), n * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dn, &n, 8, hipMemcpyHostToDevice));
-  CK(hipMemset(hist, 0, 8 * 256 * 4));
+  CK(hipMemset(hist, 0, HCOPIES * HSTRIDE * 4));
   CK(hipMemset(err, 0, 4));
   hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, 0, (const uint64_t*)k0, (const uint64_t*)dn,
                      n, 0, 1, hist, (uint64_t*)nullptr, (uint64_t*)nullptr);
