@@ -203,6 +203,15 @@ def main():
         hot_bytes //= args.steps
         achieved = hot_bytes / (hot_ms * 1e-3) / 1e9 if hot_ms > 0 else None
         traffic = pmc_traffic(args.config, world, metric, hub)
+        # Whole-call effective bandwidth against SURVEY.md §8(d)'s algorithmic
+        # bytes of the reference's wedge scan: B_alg(H) = 8(S+1) + 4M + 4M + 8 P_H
+        # + 4 W_H + 12 k_out, with P_H = sum deg v and W_H = sum deg(v)^2 over the
+        # surviving intermediates (H = 0: all).  Our kernels avoid most of these
+        # bytes, so this is an effective figure, reported beside the roofline.
+        degs = (off[1:] - off[:-1]).double()
+        surv = degs[(degs > 0) & ((degs <= hub) if hub > 0 else (degs > 0))]
+        b_call = 8 * (span + 1) + 8 * ginfo["nnz"] + 8 * float(surv.sum()) + 4 * float((surv * surv).sum()) + 12 * cnt
+        call_eff = b_call / (ms_per_step * 1e-3) / 1e9
         line = {
             "metric": "predicted edges/sec + F1, LHub Jaccard, 0.1|E| removed",
             "value": value,
@@ -232,6 +241,8 @@ def main():
                          "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
                          "traffic_source": traffic["source"] if traffic else None},
             "graph_replay": replays == args.steps,
+            "call_effective": {"algorithmic_bytes": b_call, "achieved": call_eff, "unit": "GB/s",
+                               "frac": call_eff / HBM_PEAK_GBS, "definition": "SURVEY.md 8(d) B_alg(H) per call"},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

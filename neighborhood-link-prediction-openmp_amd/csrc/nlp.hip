@@ -12,6 +12,7 @@
 #include <new>
 #include <vector>
 #include <string>
+#include <chrono>
 #include <algorithm>
 
 #include "../../include/nlp.h"
@@ -121,6 +122,8 @@ struct nlp_graph {
   double* ctab_aa = nullptr;  // 1.0 / log((double)d), d = 0..maxdeg  (predict.hxx:788)
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
   uint64_t* host_small = nullptr;  // pinned counters
+  uint64_t* host_ctr = nullptr;    // host-mapped counters written by the last kernel (sort path)
+  uint64_t* host_ctr_dev = nullptr;
   hipEvent_t ev[8] = {};
   hipEvent_t gev[5] = {};  // recorded only as event nodes of captured graphs
   bool last_single = false; // the last fast call replayed a single graph (timing in gev)
@@ -234,6 +237,7 @@ void destroy_graph(nlp_graph* g) {
   for (int i = 0; i < 5; ++i)
     if (g->gev[i]) (void)hipEventDestroy(g->gev[i]);
   if (g->host_small) (void)hipHostFree(g->host_small);
+  if (g->host_ctr) (void)hipHostFree(g->host_ctr);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
 }
@@ -408,7 +412,9 @@ nlp_status new_graph(int device, nlp_graph** out) {
   if (!g) return NLP_ERR_NOMEM;
   g->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc(&g->host_small, 64 * 8) != hipSuccess) {
+      hipHostMalloc(&g->host_small, 64 * 8) != hipSuccess ||
+      hipHostMalloc(&g->host_ctr, NCTR * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&g->host_ctr_dev, g->host_ctr, 0) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
@@ -1321,9 +1327,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
                          dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
-                         (const float*)f.cs, p.max_edges, out, ctr);
-      TRY(hipGetLastError());
-      TRY(hipMemcpyAsync(g->host_small, ctr, NCTR * 8, hipMemcpyDeviceToHost, st));
+                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev);
     }
     TRY(hipGetLastError());
     return NLP_OK;
@@ -1442,7 +1446,6 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
                                       NCTR * 8, hipMemcpyDeviceToHost) == hipSuccess;
         link(n);
       }
-      ok1 = ok1 && saw_copy;
       if (ok1) chain_ev(2);
       if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
       if (top) (void)hipGraphDestroy(top);
@@ -1500,8 +1503,21 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
 // Run the fast path; *handled = false when the caller must use the general
 // flow (wedges beyond the budget, or -- bucket grouping -- a bucket beyond the
 // LDS cap).
+// NLP_HOSTPROF=1: host-side phase times of the fast path, averaged and printed
+// every 100 calls (diagnostics of the per-call overhead outside the kernels).
+struct HostProf {
+  double prep = 0, launch = 0, wait = 0, post = 0;
+  int n = 0;
+};
+inline double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result, bool* handled) {
+  static const bool hprof = getenv("NLP_HOSTPROF") != nullptr;
+  static HostProf hp;
+  double t0 = hprof ? now_us() : 0, t1 = 0, t2 = 0, t3 = 0;
   *handled = false;
   const bool sorted = g->sort_grouping;
   bool msd = !g->sort_lsd;  // sort grouping: MSD bucket kernel first, full LSD sort when a bucket is too big
@@ -1515,6 +1531,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (s != NLP_OK) return s;
     bool replayed = false;
     g->last_single = false;
+    if (hprof) t1 = now_us();
     if (sorted)
       s = run_graph(g, p, out, st, msd ? 2 : 1, sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
@@ -1527,8 +1544,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       if (s != NLP_OK) return s;
     }
     hipEvent_t* E = (replayed && g->last_single) ? g->gev : g->ev;
+    if (hprof) t2 = now_us();
     TRY(wait_event(E[2]));
-    const uint64_t* h = g->host_small;
+    if (hprof) t3 = now_us();
+    const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;
     if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
     if (h[C_FLAGS] & F_OVERFLOW) {
       const uint64_t W = h[C_W];
@@ -1573,6 +1592,17 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
         // k_group_tiles: bucket counts, records, flags, runs
         t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
         t->hot_kernel = 3;
+      }
+    }
+    if (hprof) {
+      hp.prep += t1 - t0;
+      hp.launch += t2 - t1;
+      hp.wait += t3 - t2;
+      hp.post += now_us() - t3;
+      if (++hp.n == 100) {
+        fprintf(stderr, "nlp host us/call: prepare %.1f launch %.1f wait %.1f post %.1f\n", hp.prep / 100,
+                hp.launch / 100, hp.wait / 100, hp.post / 100);
+        hp = HostProf();
       }
     }
     if (g->d_stamp && !g->stamp_path.empty()) {  // diagnostics: append this call's stamps

@@ -938,6 +938,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   __shared__ uint16_t s_p2[2][BK_CAP];
   __shared__ uint16_t s_cnt[BK_PER][BK_NW][RS_BINS];
   __shared__ uint32_t s_dig[RS_BINS];
+  __shared__ uint16_t s_rs[BK_CAP + 1];  // start position of each (u, w) run
   __shared__ uint32_t s_wsum[BK_NW];
   __shared__ uint64_t s_excl;
   __shared__ uint32_t s_start, s_bcnt;
@@ -1049,91 +1050,125 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   float* s_sc = (float*)s_k2[cur ^ 1];                  // the free buffer holds scores ...
   uint32_t* s_flag = (uint32_t*)s_k2[cur ^ 1] + BK_CAP;  // ... and flags
   sp_stamp(stamp, true, 3);
-  // striped: thread t scores the runs starting at positions t + 1024 r.  A
-  // thread's (up to BK_PER) runs are scored together: their independent loads
-  // and the steps of their membership searches are issued side by side, so a
-  // thread waits for one search chain, not BK_PER of them in a row.
+  // (u, w) runs: block scan of the run starts (positions blocked 4 per thread)
+  // gives every run its start, so no thread walks a run position by position
+  // (two hubs can share long runs).
+  uint32_t R;
+  {
+    uint32_t sf[BK_PER], ns = 0;
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      const uint32_t p = (uint32_t)t * BK_PER + r;
+      sf[r] = (p < m && (p == 0 || s_key[p - 1] != s_key[p])) ? 1u : 0u;
+      ns += sf[r];
+    }
+    uint32_t inc = ns;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    __syncthreads();
+    uint32_t id = inc - ns;
+    R = 0;
+    for (int w = 0; w < BK_NW; ++w) {
+      const uint32_t x = s_wsum[w];
+      id += w < wv ? x : 0u;
+      R += x;
+    }
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r)
+      if (sf[r]) s_rs[id++] = (uint16_t)((uint32_t)t * BK_PER + r);
+    if (t == 0) s_rs[R] = (uint16_t)m;
+    __syncthreads();
+  }
+  // score the runs (striped r = t + 1024 j); a thread's runs issue their
+  // independent loads and the steps of their membership searches side by side
   const uint64_t wmask = (1ull << wbits) - 1;
-  uint32_t ru[BK_PER], rw[BK_PER], rc[BK_PER], lo[BK_PER], hi[BK_PER], du[BK_PER], dw[BK_PER];
-  uint64_t ro[BK_PER];
+  uint32_t ru[BK_PER], rw[BK_PER], rc[BK_PER], lo[BK_PER], hi[BK_PER], du[BK_PER], dw[BK_PER], tg[BK_PER];
+  uint32_t ln[BK_PER];
+  const uint32_t* rl[BK_PER];
   float racc[BK_PER];
-  bool start_r[BK_PER];
+  bool has[BK_PER];
 #pragma unroll
-  for (int r = 0; r < BK_PER; ++r) {
-    const uint32_t p = (uint32_t)t + (uint32_t)r * BK_NT;
-    start_r[r] = false;
-    if (p < m) {
+  for (int j = 0; j < BK_PER; ++j) {
+    const uint32_t r = (uint32_t)t + (uint32_t)j * BK_NT;
+    has[j] = r < R;
+    if (has[j]) {
+      const uint32_t p = s_rs[r], cnt = (uint32_t)s_rs[r + 1] - p;
       const uint64_t k = s_key[p];
-      if (p == 0 || s_key[p - 1] != k) {
-        uint32_t cnt = 0;
-        float acc = 0.0f;
-        for (uint32_t q = p; q < m && s_key[q] == k; ++q) {
-          ++cnt;
-          if (CUSTOM) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
-        }
-        start_r[r] = true;
-        ru[r] = (uint32_t)(ua + (k >> wbits));
-        rw[r] = (uint32_t)(k & wmask);
-        rc[r] = cnt;
-        racc[r] = acc;
-      }
+      float acc = 0.0f;
+      if (CUSTOM)  // the reference's order: ascending v (= ascending position)
+        for (uint32_t q = p; q < p + cnt; ++q) acc = (float)((double)acc + g.ctab[g.deg[rval[start + s_pos[q]]]]);
+      ru[j] = (uint32_t)(ua + (k >> wbits));
+      rw[j] = (uint32_t)(k & wmask);
+      rc[j] = cnt;
+      racc[j] = acc;
     }
   }
+  // First-order exclusion: w in N(u) <=> u in I(w) (the transposed lists, the
+  // same arrays when the graph is symmetric); search the shorter sorted list, so
+  // a hub u's candidates are checked against their small in-lists.
+  const bool sym = g.toff == g.off;
 #pragma unroll
-  for (int r = 0; r < BK_PER; ++r) {
-    if (start_r[r]) {
-      ro[r] = g.off[ru[r]];
-      du[r] = g.deg[ru[r]];
-      dw[r] = CUSTOM ? 0u : g.deg[rw[r]];
-      lo[r] = 0;
-      hi[r] = du[r];
+  for (int j = 0; j < BK_PER; ++j) {
+    if (has[j]) {
+      const uint64_t ou = g.off[ru[j]], ou1 = g.off[ru[j] + 1];
+      const uint64_t tw = g.toff[rw[j]], tw1 = g.toff[rw[j] + 1];
+      du[j] = (uint32_t)(ou1 - ou);
+      const uint32_t iw = (uint32_t)(tw1 - tw);
+      dw[j] = CUSTOM ? 0u : (sym ? iw : g.deg[rw[j]]);
+      const bool via_w = iw < du[j];
+      rl[j] = via_w ? g.tkeys + tw : g.keys + ou;
+      tg[j] = via_w ? ru[j] : rw[j];
+      ln[j] = via_w ? iw : du[j];
     } else {
-      lo[r] = hi[r] = 0;
+      rl[j] = g.keys;
+      tg[j] = 0;
+      ln[j] = 0;
     }
+    lo[j] = 0;
+    hi[j] = ln[j];
   }
-  // lower bound of w in N(u), the searches in lockstep
   bool more = true;
-  while (more) {
+  while (more) {  // lower bounds, in lockstep
     more = false;
     uint32_t mid[BK_PER], av[BK_PER];
 #pragma unroll
-    for (int r = 0; r < BK_PER; ++r) {
-      mid[r] = (lo[r] + hi[r]) >> 1;
-      av[r] = lo[r] < hi[r] ? g.keys[ro[r] + mid[r]] : 0u;
+    for (int j = 0; j < BK_PER; ++j) {
+      mid[j] = (lo[j] + hi[j]) >> 1;
+      av[j] = lo[j] < hi[j] ? rl[j][mid[j]] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < BK_PER; ++r) {
-      if (lo[r] < hi[r]) {
-        if (av[r] < rw[r]) lo[r] = mid[r] + 1;
-        else hi[r] = mid[r];
-        more |= lo[r] < hi[r];
+    for (int j = 0; j < BK_PER; ++j) {
+      if (lo[j] < hi[j]) {
+        if (av[j] < tg[j]) lo[j] = mid[j] + 1;
+        else hi[j] = mid[j];
+        more |= lo[j] < hi[j];
       }
     }
   }
 #pragma unroll
-  for (int r = 0; r < BK_PER; ++r) {
-    const uint32_t p = (uint32_t)t + (uint32_t)r * BK_NT;
-    if (p < m) {
-      uint32_t fl = 0;
-      if (start_r[r]) {
-        const bool excl = lo[r] < du[r] && g.keys[ro[r] + lo[r]] == rw[r];
-        float sc;
-        if (CUSTOM) sc = excl ? 0.0f : racc[r];
-        else sc = score_basic(metric, excl ? 0u : rc[r], du[r], dw[r]);
-        s_sc[p] = sc;
-        fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
-      }
-      s_flag[p] = fl;
+  for (int j = 0; j < BK_PER; ++j) {
+    if (has[j]) {
+      const uint32_t r = (uint32_t)t + (uint32_t)j * BK_NT;
+      const bool excl = lo[j] < ln[j] && rl[j][lo[j]] == tg[j];
+      float sc;
+      if (CUSTOM) sc = excl ? 0.0f : racc[j];
+      else sc = score_basic(metric, excl ? 0u : rc[j], du[j], dw[j]);
+      s_sc[r] = sc;
+      s_flag[r] = !(sc <= min_score) ? 1u : 0u;  // NaN passes
     }
   }
   __syncthreads();
   sp_stamp(stamp, true, 4);
-  // blocked scan of the flags: thread t owns positions [4t, 4t+4)
+  // blocked scan of the run flags: thread t owns runs [4t, 4t+4)
   uint32_t f[BK_PER], tsum = 0;
 #pragma unroll
   for (int r = 0; r < BK_PER; ++r) {
-    const uint32_t p = (uint32_t)t * BK_PER + r;
-    f[r] = p < m ? s_flag[p] : 0u;
+    const uint32_t q = (uint32_t)t * BK_PER + r;
+    f[r] = q < R ? s_flag[q] : 0u;
     tsum += f[r];
   }
   uint32_t inc = tsum;
@@ -1167,9 +1202,9 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
 #pragma unroll
   for (int r = 0; r < BK_PER; ++r) {
     if (f[r]) {
-      const uint32_t p = (uint32_t)t * BK_PER + r;
-      const uint64_t k = s_key[p];
-      const float sc = s_sc[p];
+      const uint32_t q = (uint32_t)t * BK_PER + r;
+      const uint64_t k = s_key[s_rs[q]];
+      const float sc = s_sc[q];
       cu[o] = (uint32_t)(ua + (k >> wbits));
       cw[o] = (uint32_t)(k & wmask);
       cs[o] = sc;
@@ -1296,13 +1331,19 @@ struct F_Runs {
   }
 };
 
-// The first min(k, C) candidates of the score order -> caller's edges.
+// The first min(k, C) candidates of the score order -> caller's edges.  Block 0
+// also publishes the call's counters into host-mapped memory (hctr): the host
+// reads them after the stream's final event, with no copy in between.
 __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ cu,
                                                   const uint32_t* __restrict__ cw, const float* __restrict__ cs,
                                                   uint64_t k, EdgeOut* __restrict__ out,
-                                                  uint64_t* __restrict__ ctr) {
+                                                  uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr) {
   const uint64_t m = std::min<uint64_t>(ctr[C_C], k);
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctr[C_OUT_N] = m;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) ctr[C_OUT_N] = m;
+    if (hctr && threadIdx.x < NCTR) hctr[threadIdx.x] = threadIdx.x == C_OUT_N ? m : ctr[threadIdx.x];
+    if (hctr) __threadfence_system();
+  }
   for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (uint64_t)gridDim.x * NT) {
     const uint32_t x = idx[i];
     out[i] = EdgeOut{cu[x], cw[x], cs[x]};
