@@ -59,7 +59,8 @@ def build(force=False, verbose=True):
     if not force and not needs_build():
         build_cpp_test(verbose)
         return LIB
-    cmd = [hipcc()] + HIPCC_FLAGS + SOURCES + ["-o", LIB + ".tmp"]
+    cmd = [hipcc()] + HIPCC_FLAGS + [f for f in os.environ.get("NLP_HIPCC_EXTRA", "").split() if f] + SOURCES + \
+        ["-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

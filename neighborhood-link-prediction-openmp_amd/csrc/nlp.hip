@@ -144,7 +144,8 @@ struct nlp_graph {
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
                                                // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
-  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256;
+  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256, occ_runs = 256;
+  bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
   bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
   bool graph_single = true;                    // NLP_GRAPH_SEGMENTS=1: four graph segments with host events
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
@@ -378,6 +379,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
   }
   if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
+  if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gr = getenv("NLP_GROUPING")) {
     g->sort_grouping = strcmp(gr, "bucket") != 0;
     g->sort_lsd = strcmp(gr, "lsd") == 0;
@@ -400,6 +402,9 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_scan<F_Runs<true>, RN_IPT>, &a));
     TRY(occ((const void*)k_sp_scan<F_Runs<false>, RN_IPT>, &b));
     g->occ_run = std::min(a, b);
+    TRY(occ((const void*)k_sp_runs<true>, &a));
+    TRY(occ((const void*)k_sp_runs<false>, &b));
+    g->occ_runs = std::min(a, b);
   }
   g->ws.release();  // drop build scratch; predict grows its own
   return NLP_OK;
@@ -1157,6 +1162,7 @@ struct SpBufs {
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
   int msd_shift;  // shift of that digit
+  bool split;     // msd: k_sp_bucket sorts only, k_sp_runs scores (else k_sp_bucket does both)
   bool dindex;    // survivors = a prefix of the degree-class index (no k_sp_survivors)
   uint64_t nv;    // survivors when dindex
   const uint32_t* survivors;
@@ -1190,6 +1196,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd) {
   const int ubits = key_bits(ub > ua ? ub - ua - 1 : 0);
   f.passes = (f.wbits + ubits + 7) / 8;
   f.msd = msd;
+  f.split = msd && g->split_bucket;
   f.msd_shift = std::max(0, f.wbits + ubits - 8);
   // The count metrics do not depend on the order of a run's wedges, so their
   // survivors can come from the degree-class index in any order; Adamic-Adar and
@@ -1220,6 +1227,8 @@ uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64
   if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
   const int P = f.msd ? 1 : f.passes;
   if (s >= 4 && s < 4 + P) return 24 * W;  // records in + out
+  if (f.split && s == 4 + P) return 8 * W + 8 * W + 4 * W;  // bucket sort: keys in, sorted keys + run lengths out
+  if (f.split && s == 5 + P) return 8 * W + 4 * W + 20 * C;  // runs: sorted keys, run lengths, candidates
   if (s == 4 + P) return f.msd ? 8 * W + 20 * C : 12 * W + 4 * W + 20 * C;  // records (+stash), candidates
   return 0;
 }
@@ -1240,7 +1249,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
   const int P = f.msd ? 1 : f.passes;
-  const int s_runs = 4 + P, n_st = s_runs + 7;
+  const int s_runs = 4 + P + (f.split ? 1 : 0), n_st = s_runs + 7;
   const int hot = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
   auto grid = [](uint64_t tiles, unsigned occ) {
     return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, occ)));
@@ -1273,7 +1282,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, st, (const uint64_t*)f.rk0,
                          (const uint64_t*)&ctr[C_W], capW, f.msd ? f.msd_shift : 0, P, hrec, &ctr[C_WSORT],
                          &ctr[C_FLAGS]);
-    } else if (s < s_runs) {
+    } else if (s < 4 + P) {
       const int ps = s - 4;
       const bool odd = ps & 1;
       hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(NT), 0, st,
@@ -1282,6 +1291,29 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                          f.msd ? f.msd_shift : 8 * ps,
                          (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err,
                          hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
+    } else if (f.split && s == s_runs - 1) {
+      if (custom)
+        hipLaunchKernelGGL((k_sp_bucket<true, true>), dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
+                           f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
+                           f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr, f.rk1, f.rv0, (uint32_t*)f.stash);
+      else
+        hipLaunchKernelGGL((k_sp_bucket<false, true>), dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score,
+                           ua, f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
+                           f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr, f.rk1, f.rv0, (uint32_t*)nullptr);
+    } else if (f.split && s == s_runs) {
+      const dim3 gr = grid((capW + RU_TILE - 1) / RU_TILE, g->occ_runs);
+      if (custom)
+        hipLaunchKernelGGL(k_sp_runs<true>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
+                           (const uint64_t*)f.rk1, (const uint32_t*)f.rv0, (const uint32_t*)f.stash, f.cu, f.cw,
+                           f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr);
+      else
+        hipLaunchKernelGGL(k_sp_runs<false>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
+                           (const uint64_t*)f.rk1, (const uint32_t*)f.rv0, (const uint32_t*)nullptr, f.cu, f.cw,
+                           f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr);
     } else if (s == s_runs && f.msd) {
       if (custom)
         hipLaunchKernelGGL(k_sp_bucket<true>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
@@ -1584,10 +1616,12 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->hot_ms = hot;
       t->graph_replay = replayed ? 1u : 0u;
       if (sorted) {
-        const int s_runs = 4 + (sp.msd ? 1 : sp.passes);
+        const int s_runs = 4 + (sp.msd ? 1 : sp.passes) + (sp.split ? 1 : 0);
         const int hs = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
         t->hot_bytes = sp_stage_bytes(g, sp, hs, h);
-        t->hot_kernel = hs == s_runs ? (sp.msd ? 1u : 2u) : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
+        t->hot_kernel = hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
+                        : (sp.split && hs == s_runs - 1) ? 1u
+                        : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
       } else {
         // k_group_tiles: bucket counts, records, flags, runs
         t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];

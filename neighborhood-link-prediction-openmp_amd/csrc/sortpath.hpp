@@ -922,7 +922,12 @@ constexpr int BK_NW = BK_NT / 64;
 constexpr int BK_CAP = 4096;
 constexpr int BK_PER = BK_CAP / BK_NT;
 
-template <bool CUSTOM>
+// SORT_ONLY: stop after the bucket sort and write it back in place -- sorted
+// keys to rkey, for every run start its length to rlen (0 elsewhere), and
+// (CUSTOM) the values in sorted order to vsorted -- for k_sp_runs, which scores
+// the runs with the whole chip instead of one workgroup per bucket (a hub's
+// bucket would otherwise keep one CU busy long after the others).
+template <bool CUSTOM, bool SORT_ONLY = false>
 __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, float min_score, uint64_t ua,
                                                      int wbits, const uint64_t* __restrict__ rkey,
                                                      const uint32_t* __restrict__ rval,
@@ -932,7 +937,9 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
                                                      uint32_t* __restrict__ oval, uint64_t* __restrict__ desc,
                                                      uint64_t* __restrict__ ctr, int lbits, uint64_t kmax,
                                                      uint32_t* __restrict__ ohist /*4 x 256*/,
-                                                     uint64_t* __restrict__ stamp) {
+                                                     uint64_t* __restrict__ stamp, uint64_t* __restrict__ skey = nullptr,
+                                                     uint32_t* __restrict__ rlen = nullptr,
+                                                     uint32_t* __restrict__ vsorted = nullptr) {
   __shared__ uint64_t s_k2[2][BK_CAP];
   __shared__ uint32_t s_oh[1][RS_BINS];
   __shared__ uint16_t s_p2[2][BK_CAP];
@@ -1083,6 +1090,19 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
     if (t == 0) s_rs[R] = (uint16_t)m;
     __syncthreads();
   }
+  if (SORT_ONLY) {
+    if (toobig)  // no runs from this bucket (the host reruns with the LSD sort)
+      for (uint32_t i = t; i < c; i += BK_NT) rlen[start + i] = 0u;
+    for (uint32_t i = t; i < m; i += BK_NT) {
+      skey[start + i] = s_key[i];
+      rlen[start + i] = 0u;
+      if (CUSTOM) vsorted[start + i] = rval[start + s_pos[i]];
+    }
+    __syncthreads();
+    for (uint32_t r = t; r < R; r += BK_NT) rlen[start + s_rs[r]] = (uint32_t)s_rs[r + 1] - s_rs[r];
+    sp_stamp(stamp, true, 4);
+    return;
+  }
   // score the runs (striped r = t + 1024 j); a thread's runs issue their
   // independent loads and the steps of their membership searches side by side
   const uint64_t wmask = (1ull << wbits) - 1;
@@ -1223,6 +1243,297 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
     if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
   }
   sp_stamp(stamp, true, 6);
+}
+
+// ---------------------------------------------------------------- onesweep pass, 512-thread tiles
+// Same contract as k_sp_pass (running per-wave digit counters), with 8 waves of
+// IPT keys each: a tile of 4096 keys takes half the serial ranking steps per
+// wave, and two threads per digit read 2 x LBR predecessors per look-back
+// round trip (one round trip for up to 64 tiles with LBR = 32).
+template <typename K, int IPT, int LBR>
+__global__ __launch_bounds__(512) void k_sp_pass3(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                  const uint64_t* __restrict__ d_n, int shift,
+                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
+                                                  uint32_t* __restrict__ err, uint64_t* __restrict__ stamp,
+                                                  uint32_t* __restrict__ nhist) {
+  constexpr int NTB = 512, NW = 8, WT = 64 * IPT, TILE = NTB * IPT;
+  __shared__ uint32_t s_wcnt[NW][RS_BINS];
+  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_dbase[RS_BINS];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_nh[3][RS_BINS];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t n = *d_n;
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
+  if (blockIdx.x >= ntiles) return;
+  if (t < RS_BINS) {
+    const uint32_t h = hist_total(ghist, t);
+    uint32_t inc = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    s_dbase[t] = inc - h;
+  }
+  if (nhist)
+    for (int i = t; i < 3 * RS_BINS; i += NTB) (&s_nh[0][0])[i] = 0;
+  __syncthreads();
+  if (t < RS_BINS)
+    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
+  const uint64_t lt = lane_mask_lt();
+  const int dd_d = t >> 1, dd_q = t & 1;  // two threads per digit
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
+    for (int i = t; i < NW * RS_BINS; i += NTB) (&s_wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
+    K k[IPT];
+    uint32_t v[IPT], dg[IPT], rk[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint64_t j = b0 + (uint64_t)i * 64;
+      k[i] = j < n ? kin[j] : (K)0;
+      v[i] = j < n ? vin[j] : 0u;
+    }
+    if (stamp) {
+      uint64_t z = 0;
+#pragma unroll
+      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
+      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
+      sp_stamp(stamp, first, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const bool ok = b0 + (uint64_t)i * 64 < n;
+      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
+      dg[i] = d;
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      const uint32_t before = ok ? s_wcnt[wv][d] : 0u;
+      rk[i] = before + (uint32_t)__popcll(peers & lt);
+      wave_lds_sync();
+      if (ok && (peers & lt) == 0) s_wcnt[wv][d] = before + (uint32_t)__popcll(peers);
+      wave_lds_sync();
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 2);
+    // digit pair (d, q): waves 4q..4q+3, combined by one shuffle
+    uint32_t loc = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) loc += s_wcnt[dd_q * 4 + w][dd_d];
+    const uint32_t other = __shfl_xor(loc, 1, 64);
+    const uint32_t run = loc + other;
+    uint32_t acc = dd_q ? other : 0u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t c = s_wcnt[dd_q * 4 + w][dd_d];
+      s_wcnt[dd_q * 4 + w][dd_d] = acc;
+      acc += c;
+    }
+    const uint32_t excl = osg_lookback<2, LBR>(desc, tile, dd_d, dd_q, run, err);
+    if (dd_q == 0) s_base[dd_d] = s_dbase[dd_d] + excl;
+    __syncthreads();
+    sp_stamp(stamp, first, 3);
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (b0 + (uint64_t)i * 64 < n) {
+        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
+        kout[pos] = k[i];
+        vout[pos] = v[i];
+        if (nhist) {
+#pragma unroll
+          for (int dd = 0; dd < 3; ++dd) atomicAdd(&s_nh[dd][(uint32_t)(k[i] >> (8 * dd + 8)) & 0xffu], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 4);
+  }
+  if (nhist) {
+    uint32_t* hc = hist_copy(nhist);
+    for (int i = t; i < 3 * RS_BINS; i += NTB) {
+      const uint32_t c = s_nh[i / RS_BINS][i % RS_BINS];
+      if (c) atomicAdd(&hc[i], c);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- balanced run scoring
+// Over the bucket-sorted records: thread j of a tile looks at records
+// base + r * NT + j; those that start a run (rlen > 0) are scored -- first-order
+// exclusion by searching the shorter of N(u) and I(w), the metric, the
+// minScore filter -- with the searches of a thread's runs in lockstep.  The
+// candidates are compacted in record order ((u, w) order) behind the preceding
+// tiles (look-back), and digit 0 of their order keys is counted.
+#ifndef NLP_RU_IPT
+#define NLP_RU_IPT 4
+#endif
+constexpr int RU_IPT = NLP_RU_IPT;
+constexpr int RU_TILE = NT * RU_IPT;
+
+template <bool CUSTOM>
+__global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float min_score, uint64_t ua, int wbits,
+                                                const uint64_t* __restrict__ skey, const uint32_t* __restrict__ rlen,
+                                                const uint32_t* __restrict__ vsorted, uint32_t* __restrict__ cu,
+                                                uint32_t* __restrict__ cw, float* __restrict__ cs,
+                                                uint32_t* __restrict__ okey, uint32_t* __restrict__ oval,
+                                                uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr, uint64_t kmax,
+                                                uint32_t* __restrict__ ohist, uint64_t* __restrict__ stamp) {
+  __shared__ uint32_t s_f[RU_TILE];
+  __shared__ float s_sc[RU_TILE];
+  __shared__ uint64_t s_red[NWAVE + 1];
+  __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_oh[RS_BINS];
+  const int t = threadIdx.x;
+  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  const uint64_t n = ctr[C_WSORT];
+  const uint64_t ntiles = (n + RU_TILE - 1) / RU_TILE;
+  if (blockIdx.x >= ntiles) return;
+  s_oh[t] = 0;
+  const uint64_t wmask = (1ull << wbits) - 1;
+  const bool sym = g.toff == g.off;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first = tile == blockIdx.x;
+    sp_stamp(stamp, first, 0);
+    const uint64_t base = tile * RU_TILE;
+    uint32_t ru[RU_IPT], rw[RU_IPT], rc[RU_IPT], lo[RU_IPT], hi[RU_IPT], du[RU_IPT], dw[RU_IPT], tg[RU_IPT],
+        ln[RU_IPT];
+    const uint32_t* rl[RU_IPT];
+    float racc[RU_IPT];
+    bool has[RU_IPT];
+#pragma unroll
+    for (int j = 0; j < RU_IPT; ++j) {
+      const uint64_t i = base + (uint64_t)j * NT + t;
+      rc[j] = i < n ? rlen[i] : 0u;
+      has[j] = rc[j] != 0;
+      const uint64_t k = has[j] ? skey[i] : 0ull;
+      ru[j] = (uint32_t)(ua + (k >> wbits));
+      rw[j] = (uint32_t)(k & wmask);
+      float acc = 0.0f;
+      if (CUSTOM && has[j])  // the reference's order: ascending v
+        for (uint32_t q = 0; q < rc[j]; ++q) acc = (float)((double)acc + g.ctab[g.deg[vsorted[i + q]]]);
+      racc[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < RU_IPT; ++j) {
+      if (has[j]) {
+        const uint64_t ou = g.off[ru[j]], ou1 = g.off[ru[j] + 1];
+        const uint64_t tw = g.toff[rw[j]], tw1 = g.toff[rw[j] + 1];
+        du[j] = (uint32_t)(ou1 - ou);
+        const uint32_t iw = (uint32_t)(tw1 - tw);
+        dw[j] = CUSTOM ? 0u : (sym ? iw : g.deg[rw[j]]);
+        const bool via_w = iw < du[j];
+        rl[j] = via_w ? g.tkeys + tw : g.keys + ou;
+        tg[j] = via_w ? ru[j] : rw[j];
+        ln[j] = via_w ? iw : du[j];
+      } else {
+        rl[j] = g.keys;
+        tg[j] = 0;
+        ln[j] = 0;
+        du[j] = dw[j] = 0;
+      }
+      lo[j] = 0;
+      hi[j] = ln[j];
+    }
+    // lower bounds, in lockstep, 4-way: the lower bound lies in [lo, hi]; each
+    // round trip loads the last element of the first three quarters, so a
+    // search takes log4 instead of log2 dependent loads
+    bool more = true;
+    while (more) {
+      more = false;
+      uint32_t st[RU_IPT], pv[RU_IPT][3];
+#pragma unroll
+      for (int j = 0; j < RU_IPT; ++j) {
+        st[j] = (hi[j] - lo[j] + 3) >> 2;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const uint32_t idx = lo[j] + (uint32_t)(q + 1) * st[j] - 1;
+          pv[j][q] = (lo[j] < hi[j] && idx < hi[j]) ? rl[j][idx] : 0xffffffffu;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RU_IPT; ++j) {
+        if (lo[j] < hi[j]) {
+          uint32_t c = 0;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) c += pv[j][q] < tg[j] ? 1u : 0u;  // ascending pivots: a prefix
+          const uint32_t p = lo[j] + (c + 1) * st[j] - 1;              // a[p] >= target when valid
+          hi[j] = (c < 3 && p < hi[j]) ? p : hi[j];
+          lo[j] = lo[j] + c * st[j];
+          more |= lo[j] < hi[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RU_IPT; ++j) {
+      uint32_t fl = 0;
+      float sc = 0.0f;
+      if (has[j]) {
+        const bool excl = lo[j] < ln[j] && rl[j][lo[j]] == tg[j];
+        if (CUSTOM) sc = excl ? 0.0f : racc[j];
+        else sc = score_basic(metric, excl ? 0u : rc[j], du[j], dw[j]);
+        fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
+      }
+      s_f[j * NT + t] = fl;
+      s_sc[j * NT + t] = sc;
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 1);
+    // blocked compaction: thread t owns tile items [4t, 4t+4)
+    uint32_t f[RU_IPT];
+    uint64_t tsum = 0;
+#pragma unroll
+    for (int r = 0; r < RU_IPT; ++r) {
+      f[r] = s_f[t * RU_IPT + r];
+      tsum += f[r];
+    }
+    uint64_t agg;
+    const uint64_t pre = block_excl_scan(tsum, s_red, &agg);
+    if (wave_id() == 0) {
+      const uint64_t e = lb_lookback_r<4>(desc, tile, agg, err);
+      if (lane_id() == 0) {
+        s_excl = e;
+        if (tile == ntiles - 1) {
+          ctr[C_C] = e + agg;
+          ctr[C_OUT_N] = std::min<uint64_t>(e + agg, kmax);
+        }
+      }
+    }
+    __syncthreads();
+    sp_stamp(stamp, first, 2);
+    uint64_t o = s_excl + pre;
+    uint32_t nnan = 0;
+#pragma unroll
+    for (int r = 0; r < RU_IPT; ++r) {
+      if (f[r]) {
+        const uint64_t i = base + (uint64_t)t * RU_IPT + r;
+        const uint64_t k = skey[i];
+        const float sc = s_sc[t * RU_IPT + r];
+        cu[o] = (uint32_t)(ua + (k >> wbits));
+        cw[o] = (uint32_t)(k & wmask);
+        cs[o] = sc;
+        const uint32_t ok = ~score_key(sc);
+        okey[o] = ok;
+        oval[o] = (uint32_t)o;
+        atomicAdd(&s_oh[ok & 0xffu], 1u);
+        nnan += sc != sc;
+        ++o;
+      }
+    }
+    if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
+    __syncthreads();
+    sp_stamp(stamp, first, 3);
+  }
+  const uint32_t hc = s_oh[t];
+  if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
 }
 
 // ---------------------------------------------------------------- generic single-pass scan

@@ -246,7 +246,7 @@ def test_gpu_oversized_bucket_falls_back(gpu, oracle, grouping):
         del os.environ["NLP_GROUPING"]
 
 
-@pytest.mark.parametrize("other", ["bucket", "lsd"])
+@pytest.mark.parametrize("other", ["bucket", "lsd", "fused"])
 def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
     """The sync-free groupings (wedge records: MSD buckets / full LSD sort;
     per-source buckets) give identical results and counters, IHub included
@@ -255,8 +255,9 @@ def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
     k = 3000
     with gpu.Graph(off, keys) as Gs:
         res = {(m, H): Gs.predict(m, H, k) for m in range(9) for H in (0, 1, 2, 4, 16)}
+    env = ("NLP_BUCKET_FUSED", "1") if other == "fused" else ("NLP_GROUPING", other)
     try:
-        os.environ["NLP_GROUPING"] = other
+        os.environ[env[0]] = env[1]
         with gpu.Graph(off, keys) as Gb:
             for (m, H), (u, w, s, t) in res.items():
                 assert t["path"] == 1
@@ -265,7 +266,7 @@ def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
                 assert t["wedges"] == tb["wedges"] and t["candidates"] == tb["candidates"]
                 assert t["nan_candidates"] == tb["nan_candidates"]
     finally:
-        del os.environ["NLP_GROUPING"]
+        del os.environ[env[0]]
 
 
 def test_gpu_radix_path_equals_bucket_path(gpu, oracle):

@@ -104,7 +104,11 @@ int occ_of(const void* k) {
 template <int IPT, int WIDE>
 void launch_pass(unsigned grid, uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t* dn, uint32_t* hist,
                  uint32_t* desc, uint32_t* err, uint64_t* stamp) {
-  if (WIDE == 2)
+  if (WIDE == 4)
+    hipLaunchKernelGGL((k_sp_pass3<uint64_t, IPT, 32>), dim3(grid), dim3(512), 0, 0, (const uint64_t*)k0,
+                       (const uint32_t*)v0, k1, v1, (const uint64_t*)dn, 0, (const uint32_t*)hist, desc, err, stamp,
+                       (uint32_t*)nullptr);
+  else if (WIDE == 2)
     hipLaunchKernelGGL((k_sp_pass2<uint64_t, 512, IPT, 32>), dim3(grid), dim3(512), 0, 0, (const uint64_t*)k0,
                        (const uint32_t*)v0, k1, v1, (const uint64_t*)dn, 0, (const uint32_t*)hist, desc, err, stamp);
   else if (WIDE == 3)
@@ -121,10 +125,11 @@ void launch_pass(unsigned grid, uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32
 
 template <int IPT, int WIDE>
 void bench_pass(Timer& T, uint64_t n, int nbits, bool prefill) {
-  constexpr int BT = WIDE == 1 ? OSB_NT : WIDE == 2 ? 512 : NT;
+  constexpr int BT = WIDE == 1 ? OSB_NT : (WIDE == 2 || WIDE == 4) ? 512 : NT;
   auto kern = WIDE == 1   ? (const void*)k_sp_passb<uint64_t, IPT>
               : WIDE == 2 ? (const void*)k_sp_pass2<uint64_t, 512, IPT, 32>
               : WIDE == 3 ? (const void*)k_sp_pass2<uint64_t, 256, IPT, 64>
+              : WIDE == 4 ? (const void*)k_sp_pass3<uint64_t, IPT, 32>
                           : (const void*)k_sp_pass<uint64_t, IPT>;
   std::vector<uint64_t> hk(n);
   std::vector<uint32_t> hv(n);
@@ -174,7 +179,7 @@ void bench_pass(Timer& T, uint64_t n, int nbits, bool prefill) {
     for (uint64_t i = 1; i < n; ++i)
       if ((out[i] & 255) < (out[i - 1] & 255)) { ok = false; break; }
   }
-  printf("pass%s<u64,IPT=%2d> n=%9llu tiles=%6llu grid=%5u %s: %8.2f us  %s\n", WIDE == 1 ? "B" : WIDE == 2 ? "2/512" : WIDE == 3 ? "2/256" : "", IPT,
+  printf("pass%s<u64,IPT=%2d> n=%9llu tiles=%6llu grid=%5u %s: %8.2f us  %s\n", WIDE == 1 ? "B" : WIDE == 2 ? "2/512" : WIDE == 3 ? "2/256" : WIDE == 4 ? "3/512" : "", IPT,
          (unsigned long long)n,
          (unsigned long long)tiles, grid, prefill ? "lookback-free" : "full         ", us, ok ? "" : "ORDER BAD");
   if (prefill) CK(hipMemcpy(desc, pre.data(), tiles * 256 * 4, hipMemcpyHostToDevice));
@@ -254,10 +259,8 @@ int main() {
   bench_surv<4>(T, 4847572, 0.02);
   for (uint64_t n : {245525ull, 1000000ull, 4000000ull}) {
     bench_pass<16, 0>(T, n, 46, false);
-    bench_pass<16, 3>(T, n, 46, false);
-    bench_pass<8, 3>(T, n, 46, false);
-    bench_pass<8, 2>(T, n, 46, false);
-    bench_pass<4, 2>(T, n, 46, false);
+    bench_pass<8, 4>(T, n, 46, false);
+    bench_pass<4, 4>(T, n, 46, false);
   }
   return 0;
 }
