@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
+KERNELS = ["k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
            "k_desc_keys_sel", "k_sel_hist"]
 
 
@@ -49,7 +49,7 @@ def main():
         config = sys.argv[sys.argv.index("--config") + 1]
     fetch = per_kernel(os.path.join(src, "p1"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "p2"), "WRITE_SIZE")
-    out = {"config": config, "n_gpus": 1, "metric": "JAC", "hub": 4, "hot_kernel": "k_sp_bucket",
+    out = {"config": config, "n_gpus": 1, "metric": "JAC", "hub": 4, "hot_kernel": "k_sp_runs",
            "source": "profiles/%s_pmc (rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE, "
                      "bench.py --steps 5 --warmup 2); traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024" % tag,
            "kernels": {}}
