@@ -1480,6 +1480,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
       }
       if (ok1) chain_ev(2);
       if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
+      if (ok1) (void)hipGraphUpload(c.exec[0], st);  // stage the executable graph on the device once
       if (top) (void)hipGraphDestroy(top);
       if (ok1) {
         c.single = true;
