@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libnlp.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("nlp.hip",)]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("prims.hpp", "kernels.hpp", "lookback.hpp", "group.hpp", "select.hpp")] + \
+DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("prims.hpp", "kernels.hpp", "lookback.hpp", "group.hpp", "select.hpp", "sortpath.hpp")] + \
     [os.path.join(ROOT, "include", "nlp.h")]
 
 HIPCC_FLAGS = [

@@ -146,6 +146,8 @@ struct nlp_graph {
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
   unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256, occ_runs = 256;
   bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
+  int group_sort = 2;                          // NLP_GROUP_SORT: 0 k_sp_bucket sort-only, 1 k_sp_group, 2 group only after 2 MSD passes
+  uint64_t last_wedges = 0;                    // wedges of the previous fast call (sizes the MSD passes)
   bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
   bool graph_single = true;                    // NLP_GRAPH_SEGMENTS=1: four graph segments with host events
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
@@ -380,6 +382,7 @@ nlp_status finish_graph(nlp_graph* g) {
   }
   if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
+  if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* gr = getenv("NLP_GROUPING")) {
     g->sort_grouping = strcmp(gr, "bucket") != 0;
     g->sort_lsd = strcmp(gr, "lsd") == 0;
@@ -1161,7 +1164,8 @@ struct SpBufs {
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
-  int msd_shift;  // shift of that digit
+  int msd_shift;  // shift of the lowest MSD digit (the fine-bucket boundary in split mode)
+  int msd_passes; // MSD passes before the group sort (split mode: 1 or 2; fused bucket kernel: 1)
   bool split;     // msd: k_sp_bucket sorts only, k_sp_runs scores (else k_sp_bucket does both)
   bool dindex;    // survivors = a prefix of the degree-class index (no k_sp_survivors)
   uint64_t nv;    // survivors when dindex
@@ -1174,7 +1178,7 @@ inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 
   return b;
 }
 
-nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd) {
+nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int msd_passes) {
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
   const uint64_t capW = g->capW;
@@ -1197,7 +1201,8 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd) {
   f.passes = (f.wbits + ubits + 7) / 8;
   f.msd = msd;
   f.split = msd && g->split_bucket;
-  f.msd_shift = std::max(0, f.wbits + ubits - 8);
+  f.msd_passes = f.split ? std::min(msd_passes, std::max(1, (f.wbits + ubits) / 8)) : 1;
+  f.msd_shift = std::max(0, f.wbits + ubits - 8 * f.msd_passes);
   // The count metrics do not depend on the order of a run's wedges, so their
   // survivors can come from the degree-class index in any order; Adamic-Adar and
   // Resource-Allocation sum in ascending v and keep the ordered survivor scan.
@@ -1225,7 +1230,7 @@ uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64
   const uint64_t S = g->span, V = h[C_NV], W = h[C_W], C = h[C_C];
   if (s == 1) return 4 * S + 4 * V;             // deg read, survivor ids written
   if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
-  const int P = f.msd ? 1 : f.passes;
+  const int P = f.msd ? f.msd_passes : f.passes;
   if (s >= 4 && s < 4 + P) return 24 * W;  // records in + out
   if (f.split && s == 4 + P) return 8 * W + 8 * W + 4 * W;  // bucket sort: keys in, sorted keys + run lengths out
   if (f.split && s == 5 + P) return 8 * W + 4 * W + 20 * C;  // runs: sorted keys, run lengths, candidates
@@ -1248,8 +1253,12 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint32_t* hord = (uint32_t*)(f.arena + SP_HORD);
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
-  const int P = f.msd ? 1 : f.passes;
+  const int P = f.msd ? f.msd_passes : f.passes;
   const int s_runs = 4 + P + (f.split ? 1 : 0), n_st = s_runs + 7;
+  // after the record passes the records sit in buffer 1 for an odd count, 0 for even
+  uint64_t* rk_m = (P & 1) ? f.rk1 : f.rk0;
+  uint32_t* rv_m = (P & 1) ? f.rv1 : f.rv0;
+  uint32_t* rv_free = (P & 1) ? f.rv0 : f.rv1;
   const int hot = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
   auto grid = [](uint64_t tiles, unsigned occ) {
     return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, occ)));
@@ -1272,7 +1281,8 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s == 2) {
       if (f.msd)  // the MSD digit histogram is fused into the expansion
         hipLaunchKernelGGL(k_sp_expand<true>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua,
-                           ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, f.msd_shift, hrec);
+                           ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, f.msd_shift, hrec,
+                           P);
       else
         hipLaunchKernelGGL(k_sp_expand<false>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv,
                            ua, ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, 0,
@@ -1288,30 +1298,39 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(NT), 0, st,
                          (const uint64_t*)(odd ? f.rk1 : f.rk0), (const uint32_t*)(odd ? f.rv1 : f.rv0),
                          odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT],
-                         f.msd ? f.msd_shift : 8 * ps,
+                         f.msd ? f.msd_shift + 8 * ps : 8 * ps,
                          (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err,
                          hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
-    } else if (f.split && s == s_runs - 1) {
+    } else if (f.split && s == s_runs - 1 && P == 1 && g->group_sort != 1) {
+      // one MSD pass: one workgroup per top-digit bucket, the bucket bounds from its histogram
       if (custom)
         hipLaunchKernelGGL((k_sp_bucket<true, true>), dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
-                           f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
-                           f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr, f.rk1, f.rv0, (uint32_t*)f.stash);
+                           f.wbits, (const uint64_t*)rk_m, (const uint32_t*)rv_m, (const uint32_t*)hrec, f.cu, f.cw,
+                           f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
+                           hot == s ? g->d_stamp : nullptr, rk_m, rv_free, (uint32_t*)f.stash);
       else
         hipLaunchKernelGGL((k_sp_bucket<false, true>), dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score,
-                           ua, f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
+                           ua, f.wbits, (const uint64_t*)rk_m, (const uint32_t*)rv_m, (const uint32_t*)hrec, f.cu,
                            f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr, f.rk1, f.rv0, (uint32_t*)nullptr);
+                           hot == s ? g->d_stamp : nullptr, rk_m, rv_free, (uint32_t*)nullptr);
+    } else if (f.split && s == s_runs - 1) {
+      const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + GR_T - 1) / GR_T));
+      if (custom)
+        hipLaunchKernelGGL(k_sp_group<true>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
+                           f.msd_shift, rk_m, rv_free, (uint32_t*)f.stash, ctr, hot == s ? g->d_stamp : nullptr);
+      else
+        hipLaunchKernelGGL(k_sp_group<false>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
+                           f.msd_shift, rk_m, rv_free, (uint32_t*)nullptr, ctr, hot == s ? g->d_stamp : nullptr);
     } else if (f.split && s == s_runs) {
       const dim3 gr = grid((capW + RU_TILE - 1) / RU_TILE, g->occ_runs);
       if (custom)
         hipLaunchKernelGGL(k_sp_runs<true>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
-                           (const uint64_t*)f.rk1, (const uint32_t*)f.rv0, (const uint32_t*)f.stash, f.cu, f.cw,
+                           (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)f.stash, f.cu, f.cw,
                            f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
                            hot == s ? g->d_stamp : nullptr);
       else
         hipLaunchKernelGGL(k_sp_runs<false>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
-                           (const uint64_t*)f.rk1, (const uint32_t*)f.rv0, (const uint32_t*)nullptr, f.cu, f.cw,
+                           (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)nullptr, f.cu, f.cw,
                            f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
                            hot == s ? g->d_stamp : nullptr);
     } else if (s == s_runs && f.msd) {
@@ -1554,19 +1573,23 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   *handled = false;
   const bool sorted = g->sort_grouping;
   bool msd = !g->sort_lsd;  // sort grouping: MSD bucket kernel first, full LSD sort when a bucket is too big
+  // MSD passes: fine buckets of about a thousand records on average, from the
+  // wedge count of the previous call (one more pass, then the full LSD sort,
+  // when a fine bucket is still above the LDS capacity)
+  int msd_passes = g->last_wedges > (256u << 10) ? 2 : 1;
   for (int attempt = 0; attempt < 4; ++attempt) {
     if (sorted && g->capW > SP_MAX_N) return NLP_OK;
     EdgeOut* out = d_out;
     if (!out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(std::min(p.max_edges, g->capW), 1), &out));
     FastBufs f;
     SpBufs sp;
-    nlp_status s = sorted ? prepare_sp(g, p, sp, msd) : prepare_fast(g, p, f, st);
+    nlp_status s = sorted ? prepare_sp(g, p, sp, msd, msd_passes) : prepare_fast(g, p, f, st);
     if (s != NLP_OK) return s;
     bool replayed = false;
     g->last_single = false;
     if (hprof) t1 = now_us();
     if (sorted)
-      s = run_graph(g, p, out, st, msd ? 2 : 1, sp.arena, &replayed,
+      s = run_graph(g, p, out, st, msd ? 1 + sp.msd_passes : 1, sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
     else
       s = run_graph(g, p, out, st, 0, f.arena, &replayed,
@@ -1593,9 +1616,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       continue;
     }
     if (sorted && msd && (h[C_FLAGS] & F_TOOBIG) && h[C_W] <= g->wedge_budget) {
-      msd = false;
+      if (sp.split && sp.msd_passes == 1) msd_passes = 2;
+      else msd = false;
       continue;
     }
+    g->last_wedges = h[C_W];
     if ((h[C_FLAGS] & F_TOOBIG) || h[C_W] > g->wedge_budget) return NLP_OK;
     *out_count = h[C_OUT_N];
     if (result) *result = out;
@@ -1617,11 +1642,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->hot_ms = hot;
       t->graph_replay = replayed ? 1u : 0u;
       if (sorted) {
-        const int s_runs = 4 + (sp.msd ? 1 : sp.passes) + (sp.split ? 1 : 0);
+        const int s_runs = 4 + (sp.msd ? sp.msd_passes : sp.passes) + (sp.split ? 1 : 0);
         const int hs = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
         t->hot_bytes = sp_stage_bytes(g, sp, hs, h);
         t->hot_kernel = hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
-                        : (sp.split && hs == s_runs - 1) ? 1u
+                        : (sp.split && hs == s_runs - 1) ? (sp.msd_passes == 1 && g->group_sort != 1 ? 1u : 8u)
                         : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
       } else {
         // k_group_tiles: bucket counts, records, flags, runs

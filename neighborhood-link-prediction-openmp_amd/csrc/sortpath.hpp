@@ -260,16 +260,17 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
                                                   const uint32_t* __restrict__ surv, uint64_t capW,
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
                                                   uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr,
-                                                  int hshift, uint32_t* __restrict__ ghist) {
+                                                  int hshift, uint32_t* __restrict__ ghist, int hdigits = 1) {
   __shared__ uint64_t s_red[NWAVE + 1];
   __shared__ uint64_t s_excl;
-  __shared__ uint32_t s_h[HIST ? RS_BINS : 1];
+  __shared__ uint32_t s_h[HIST ? 2 * RS_BINS : 1];
   const uint64_t n = ctr[C_NV];
   const uint64_t ntiles = (n + EX_TILE - 1) / EX_TILE;
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
   if (blockIdx.x >= ntiles) return;
   if (HIST) {
     s_h[threadIdx.x] = 0;
+    s_h[RS_BINS + threadIdx.x] = 0;
     __syncthreads();
   }
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -315,7 +316,10 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
           const uint64_t key = hi | nv[k];
           rkey[pos] = key;
           rval[pos] = v;
-          if (HIST) atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+          if (HIST) {
+            atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+            if (hdigits > 1) atomicAdd(&s_h[RS_BINS + ((uint32_t)(key >> (hshift + 8)) & 0xffu)], 1u);
+          }
           ++pos;
         }
       }
@@ -323,8 +327,11 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
     __syncthreads();
   }
   if (HIST) {
-    const uint32_t hc = s_h[threadIdx.x];
-    if (hc) atomicAdd(&hist_copy(ghist)[threadIdx.x], hc);
+    uint32_t* hc = hist_copy(ghist);
+    for (int dd = 0; dd < hdigits; ++dd) {
+      const uint32_t c = s_h[dd * RS_BINS + threadIdx.x];
+      if (c) atomicAdd(&hc[dd * RS_BINS + threadIdx.x], c);
+    }
   }
 }
 
@@ -1364,6 +1371,199 @@ __global__ __launch_bounds__(512) void k_sp_pass3(const K* __restrict__ kin, con
       if (c) atomicAdd(&hc[i], c);
     }
   }
+}
+
+// ---------------------------------------------------------------- group sort
+// After P stable MSD passes the records are grouped by their top 8P key bits
+// ("fine buckets", ascending).  Workgroup b takes the fine buckets that start
+// in records [b*GR_T, (b+1)*GR_T): its range is cut at fine-bucket boundaries
+// found by scanning the keys, so neighbouring workgroups agree and the ranges
+// partition the records.  It sorts the range in LDS by the key bits that vary
+// inside it (stable LSD, ballot multisplit), then writes back in place the
+// sorted keys, the run lengths at run starts (0 elsewhere) and, for the
+// Adamic-Adar / Resource-Allocation sums, the values in sorted order.  A range
+// above BK_CAP records raises F_TOOBIG (the host then reruns with more MSD
+// passes or the full LSD sort).
+constexpr uint32_t GR_T = 1024;
+
+template <bool CUSTOM>
+__global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__ rkey_in,
+                                                    const uint32_t* __restrict__ rval, int fshift,
+                                                    uint64_t* __restrict__ skey, uint32_t* __restrict__ rlen,
+                                                    uint32_t* __restrict__ vsorted, uint64_t* __restrict__ ctr,
+                                                    uint64_t* __restrict__ stamp) {
+  __shared__ uint64_t s_k2[2][BK_CAP];
+  __shared__ uint16_t s_p2[2][BK_CAP];
+  __shared__ uint16_t s_cnt[BK_PER][BK_NW][RS_BINS];
+  __shared__ uint32_t s_dig[RS_BINS];
+  __shared__ uint16_t s_rs[BK_CAP + 1];
+  __shared__ uint32_t s_wsum[BK_NW];
+  __shared__ uint64_t s_bnd[2];
+  __shared__ uint64_t s_or[BK_NW], s_and[BK_NW];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t n = ctr[C_WSORT];
+  const uint64_t x0 = (uint64_t)blockIdx.x * GR_T;
+  if (x0 >= n) return;
+  sp_stamp(stamp, true, 0);
+  // range bounds: the first fine-bucket boundary at or after x0 and x1
+  for (int e = 0; e < 2; ++e) {
+    const uint64_t x = std::min<uint64_t>(x0 + (uint64_t)e * GR_T, n);
+    if (t == 0) s_bnd[e] = ~0ull;
+    __syncthreads();
+    if (x == 0 || x == n) {
+      if (t == 0) s_bnd[e] = x;
+    } else {
+      for (uint64_t c0 = x; c0 < n && c0 < x + BK_CAP + 1; c0 += BK_NT) {
+        const uint64_t i = c0 + t;
+        const bool bd = i < n && (rkey_in[i] >> fshift) != (rkey_in[i - 1] >> fshift);
+        const bool end = i == n;
+        if (bd || end) atomicMin((unsigned long long*)&s_bnd[e], (unsigned long long)i);
+        __syncthreads();
+        if (s_bnd[e] != ~0ull) break;
+        __syncthreads();
+      }
+      if (t == 0 && s_bnd[e] == ~0ull) s_bnd[e] = std::min<uint64_t>(n, x + BK_CAP + 1);  // too long: flagged below
+    }
+    __syncthreads();
+  }
+  const uint64_t start = s_bnd[0], stop = s_bnd[1];
+  if (stop <= start) return;  // the range begins in a neighbour's fine bucket
+  const uint64_t c = stop - start;
+  if (c > BK_CAP) {
+    if (t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
+    for (uint64_t i = start + t; i < stop; i += BK_NT) rlen[i] = 0u;
+    return;
+  }
+  const uint32_t m = (uint32_t)c;
+  uint64_t ko = 0, ka = ~0ull;
+  for (uint32_t i = t; i < m; i += BK_NT) {
+    const uint64_t k = rkey_in[start + i];
+    s_k2[0][i] = k;
+    s_p2[0][i] = (uint16_t)i;
+    ko |= k;
+    ka &= k;
+  }
+  // the bits that vary inside the range decide the number of LDS passes
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ko |= __shfl_xor(ko, o, 64);
+    ka &= __shfl_xor(ka, o, 64);
+  }
+  if (lane == 0) {
+    s_or[wv] = ko;
+    s_and[wv] = ka;
+  }
+  __syncthreads();
+  uint64_t diff = 0;
+  for (int w = 0; w < BK_NW; ++w) diff |= s_or[w] ^ s_and[w];
+  const int lbits = diff ? 64 - __clzll((long long)diff) : 0;
+  sp_stamp(stamp, true, 1);
+  const uint64_t lt = lane_mask_lt();
+  const int rmax = (int)((m + BK_NT - 1) / BK_NT);
+  int cur = 0;
+  for (int sh = 0; sh < lbits; sh += 8) {
+    {
+      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
+      for (int i = t; i < BK_PER * BK_NW * RS_BINS / 2; i += BK_NT) z[i] = 0;
+    }
+    __syncthreads();
+    uint64_t kk[BK_PER];
+    uint16_t pp[BK_PER];
+    uint32_t dd[BK_PER], rk[BK_PER];
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      if (r < rmax) {
+        const uint32_t i = (uint32_t)r * BK_NT + t;
+        const bool ok = i < m;
+        kk[r] = ok ? s_k2[cur][i] : 0ull;
+        pp[r] = ok ? s_p2[cur][i] : (uint16_t)0;
+        const uint32_t d = (uint32_t)(kk[r] >> sh) & 0xffu;
+        dd[r] = d;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int bt = 0; bt < 8; ++bt) {
+          const uint64_t bb = __ballot((d >> bt) & 1u);
+          peers &= ((d >> bt) & 1u) ? bb : ~bb;
+        }
+        rk[r] = (uint32_t)__popcll(peers & lt);
+        if (ok && (peers & lt) == 0) s_cnt[r][wv][d] = (uint16_t)__popcll(peers);
+      }
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < RS_BINS) {
+      for (int r = 0; r < rmax; ++r)
+        for (int w = 0; w < BK_NW; ++w) {
+          const uint32_t c2 = s_cnt[r][w][t];
+          s_cnt[r][w][t] = (uint16_t)tot;
+          tot += c2;
+        }
+      uint32_t inc = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) s_wsum[wv] = inc;
+      s_dig[t] = inc - tot;
+    }
+    __syncthreads();
+    if (t < RS_BINS)
+      for (int w = 0; w < wv; ++w) s_dig[t] += s_wsum[w];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      if (r < rmax && (uint32_t)r * BK_NT + t < m) {
+        const uint32_t pos = s_dig[dd[r]] + s_cnt[r][wv][dd[r]] + rk[r];
+        s_k2[cur ^ 1][pos] = kk[r];
+        s_p2[cur ^ 1][pos] = pp[r];
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const uint64_t* s_key = s_k2[cur];
+  const uint16_t* s_pos = s_p2[cur];
+  sp_stamp(stamp, true, 2);
+  // run starts (blocked 4 per thread) -> run ids -> start positions
+  uint32_t R;
+  {
+    uint32_t sf[BK_PER], ns = 0;
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r) {
+      const uint32_t p = (uint32_t)t * BK_PER + r;
+      sf[r] = (p < m && (p == 0 || s_key[p - 1] != s_key[p])) ? 1u : 0u;
+      ns += sf[r];
+    }
+    uint32_t inc = ns;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    __syncthreads();
+    uint32_t id = inc - ns;
+    R = 0;
+    for (int w = 0; w < BK_NW; ++w) {
+      const uint32_t x = s_wsum[w];
+      id += w < wv ? x : 0u;
+      R += x;
+    }
+#pragma unroll
+    for (int r = 0; r < BK_PER; ++r)
+      if (sf[r]) s_rs[id++] = (uint16_t)((uint32_t)t * BK_PER + r);
+    if (t == 0) s_rs[R] = (uint16_t)m;
+    __syncthreads();
+  }
+  for (uint32_t i = t; i < m; i += BK_NT) {
+    skey[start + i] = s_key[i];
+    rlen[start + i] = 0u;
+    if (CUSTOM) vsorted[start + i] = rval[start + s_pos[i]];
+  }
+  __syncthreads();
+  for (uint32_t r = t; r < R; r += BK_NT) rlen[start + s_rs[r]] = (uint32_t)s_rs[r + 1] - s_rs[r];
+  sp_stamp(stamp, true, 3);
 }
 
 // ---------------------------------------------------------------- balanced run scoring
