@@ -86,8 +86,10 @@ typedef struct {
   uint64_t wedges;          /* (u, v, w) wedges scanned, w > u  (SURVEY §8(d) W_H) */
   uint64_t candidates;      /* candidates with score > min_score (NaN included) */
   uint64_t nan_candidates;  /* of which NaN */
-  uint32_t path;            /* 1 = intermediate-centric, 2 = source-centric */
-  uint32_t chunks;          /* source-range chunks used by path 2 */
+  uint32_t path;            /* 1 = intermediate-centric sort grouping, 2 = source-centric chunked sort,
+                               3 = intermediate-centric radix grouping, 4 = source-centric hash
+                               accumulation */
+  uint32_t chunks;          /* source-range chunks used by paths 2 and 4 */
   float hot_ms;             /* device time of the dominant kernel (HIP events around its launch) */
   uint32_t graph_replay;    /* 1 when the call replayed a captured hipGraph */
   uint64_t hot_bytes;       /* algorithmic bytes of that launch */

@@ -1,0 +1,669 @@
+// hashpath.hpp -- path 3: source-centric hash accumulation for large wedge counts.
+//
+// Reference: predictLinksWithIntersectionLoopOmpU (/root/reference/inc/predict.hxx:284-339).
+// Per source u the reference walks every first-hop v (hub filter deg v <= H,
+// predict.hxx:298-301), every second-hop w > u of N(v) (ft, 292-296), and
+// accumulates into a dense per-thread table V[S] (predictScanEdges[Basic]U,
+// 153-179); it then zeroes u and N(u) (306-307) and scores every touched w.
+//
+// Here one wave (small rows) or one 1024-thread workgroup (large rows) owns a
+// source row and accumulates the wedges of that row in an open-addressing hash
+// table: in LDS while the row's wedge count fits (W(u) <= 4096), in a
+// per-workgroup global slab beyond.  Nothing proportional to the wedge count is
+// ever materialised, so hub thresholds up to IHub (H = 0) run in bounded
+// memory; the wedge scan is flattened over the row's surviving intermediates
+// (a prefix of their degrees in LDS, a binary search per wedge) so that lanes
+// stay busy whatever the degree mix.
+//
+// Exactness.  Counts are order-free.  Adamic-Adar / Resource-Allocation add
+// (float)((double)acc + c_v) in the order of v in N(u) (predict.hxx:788, 828),
+// which an unordered hash cannot reproduce, so the table keeps the count and
+// the last inserting v: a count of 1 scores (float)(0.0 + c_v) directly, and a
+// count >= 2 re-walks the intersection N(u) x I(w) (I = transposed adjacency,
+// v in I(w) <=> w in N(v), with multiplicities) in ascending v -- the same
+// sequence of additions as the reference.
+//
+// Candidates are emitted unordered (wave-aggregated atomics) into a buffer
+// shared by the chunks of source rows; between chunks the host prunes the
+// buffer to the canonical top k (key desc, u asc, w asc) and raises the
+// emission threshold tau to the k-th key: later chunks hold larger u, so a
+// later candidate with key <= tau can never enter the top k.
+#pragma once
+#include "group.hpp"
+
+namespace nlp {
+
+constexpr uint32_t HP_EMPTY = 0xffffffffu;
+constexpr uint32_t HP_EXCL = 0x80000000u;   // count bit: w in N(u) (first-order exclusion)
+constexpr uint32_t HP_CMASK = 0x7fffffffu;
+constexpr int HP_WT = 1024;                 // wave table entries (bin 0)
+constexpr uint64_t HP_B0_MAX = HP_WT / 2;   // bin 0: W(u) <= 512
+constexpr int HP_BNT = 1024;                // workgroup size of the block bins
+constexpr int HP_BT = 8192;                 // LDS table entries (bin 1)
+constexpr uint64_t HP_B1_MAX = HP_BT / 2;   // bin 1: W(u) <= 4096
+constexpr int HP_T2_LOG = 20;               // bin 2 global table entries per workgroup (log2)
+constexpr uint64_t HP_B2_MAX = 1ull << (HP_T2_LOG - 1);
+constexpr int HP_NBINS = 4;                 // bin 3: the rest (T up to HP_T3_LOG, w-range passes beyond)
+constexpr int HP_T3_LOG_MAX = 24;
+
+// per-chunk counters (u64)
+enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_NCTR = 8 };
+
+struct HpArgs {
+  GraphView g;
+  uint64_t S;
+  uint32_t H;
+  int metric;
+  float min_score;
+  uint32_t* ckey;     // candidate columns (score key, u, w, score)
+  uint32_t* cu;
+  uint32_t* cw;
+  float* cs;
+  uint64_t base;      // first free slot
+  uint64_t cap;       // free slots from base on
+  const int64_t* tau; // emit only key > *tau
+  unsigned long long* ctr;
+};
+
+__device__ __forceinline__ bool hp_surv(uint32_t d, uint32_t H) { return d > 0 && (H == 0 || d <= H); }
+
+__device__ __forceinline__ uint32_t hp_hash(uint32_t w, int shift) { return (w * 0x9E3779B1u) >> shift; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+__device__ __forceinline__ int log2_ceil(uint64_t x) {
+  int b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------- table access
+// LDS tables use plain loads; global slabs go through agent-scope atomics so
+// that no stale L1 line of a previous row is ever read.
+template <bool GLOBAL>
+__device__ __forceinline__ uint32_t tload(const uint32_t* p) {
+  if (GLOBAL) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *(volatile const uint32_t*)p;
+}
+template <bool GLOBAL>
+__device__ __forceinline__ void tstore(uint32_t* p, uint32_t v) {
+  if (GLOBAL) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *(volatile uint32_t*)p = v;
+}
+
+// A table: keys (HP_EMPTY = free), counts (HP_EXCL bit = w in N(u)) and, for
+// AA / RA, the smallest and largest contributing v (empty: ~0 / 0).
+struct HpTable {
+  uint32_t* k;
+  uint32_t* c;
+  uint32_t* vmin;
+  uint32_t* vmax;
+};
+
+// Tables are sized for at most half load, so a probe sequence always ends; a
+// full table (a sizing bug) raises HPC_ERR instead of spinning.
+template <bool GLOBAL, bool CUSTOM>
+__device__ __forceinline__ void hp_insert(const HpTable& t, uint32_t mask, int shift, uint32_t w, uint32_t v,
+                                          unsigned long long* err) {
+  uint32_t h = hp_hash(w, shift);
+  for (uint32_t probe = 0;; ++probe) {
+    if (probe > mask) { atomicOr(err, 1ull); return; }
+    uint32_t cur = tload<GLOBAL>(&t.k[h]);
+    if (cur == HP_EMPTY) {
+      cur = atomicCAS(&t.k[h], HP_EMPTY, w);
+      if (cur == HP_EMPTY) cur = w;
+    }
+    if (cur == w) {
+      atomicAdd(&t.c[h], 1u);
+      if (CUSTOM) {
+        atomicMin(&t.vmin[h], v);
+        atomicMax(&t.vmax[h], v);
+      }
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+template <bool GLOBAL>
+__device__ __forceinline__ void hp_mark(const HpTable& t, uint32_t mask, int shift, uint32_t x) {
+  uint32_t h = hp_hash(x, shift);
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t cur = tload<GLOBAL>(&t.k[h]);
+    if (cur == x) { atomicOr(&t.c[h], HP_EXCL); return; }
+    if (cur == HP_EMPTY) return;
+    h = (h + 1) & mask;
+  }
+}
+
+// Read entry i and reset it to empty.
+template <bool GLOBAL, bool CUSTOM>
+__device__ __forceinline__ uint32_t hp_take(const HpTable& t, uint32_t i, uint32_t* c, uint32_t* v0, uint32_t* v1) {
+  const uint32_t w = tload<GLOBAL>(&t.k[i]);
+  if (w != HP_EMPTY) {
+    *c = tload<GLOBAL>(&t.c[i]);
+    tstore<GLOBAL>(&t.k[i], HP_EMPTY);
+    tstore<GLOBAL>(&t.c[i], 0u);
+    if (CUSTOM) {
+      *v0 = tload<GLOBAL>(&t.vmin[i]);
+      *v1 = tload<GLOBAL>(&t.vmax[i]);
+      tstore<GLOBAL>(&t.vmin[i], HP_EMPTY);
+      tstore<GLOBAL>(&t.vmax[i], 0u);
+    }
+  }
+  return w;
+}
+
+// Exact Adamic-Adar / Resource-Allocation value of (u, w) with n >= 3
+// contributions: the additions of predict.hxx:788/828 in ascending v over
+// N(u) x I(w) (multiplicities multiply), iterating the shorter list.
+__device__ float hp_ordered_sum(const HpArgs& a, uint32_t u, uint32_t w, uint32_t n) {
+  const uint64_t ou = a.g.off[u], tw = a.g.toff[w];
+  const uint32_t na = (uint32_t)(a.g.off[u + 1] - ou), nb = (uint32_t)(a.g.toff[w + 1] - tw);
+  const bool iter_a = na <= nb;
+  const uint32_t* X = iter_a ? a.g.keys + ou : a.g.tkeys + tw;
+  const uint32_t* Y = iter_a ? a.g.tkeys + tw : a.g.keys + ou;
+  const uint32_t nx = iter_a ? na : nb, ny = iter_a ? nb : na;
+  float acc = 0.0f;
+  uint32_t done = 0, lo = 0;
+  for (uint32_t i = 0; i < nx && done < n; ++i) {
+    const uint32_t v = X[i];
+    const uint32_t d = a.g.deg[v];
+    if (!hp_surv(d, a.H)) continue;
+    uint32_t l = lo, h = ny;
+    while (l < h) {
+      const uint32_t m = (l + h) >> 1;
+      if (Y[m] < v) l = m + 1; else h = m;
+    }
+    lo = l;
+    uint32_t m = 0;
+    while (l + m < ny && Y[l + m] == v) ++m;
+    const double c = a.g.ctab[d];
+    for (uint32_t q = 0; q < m; ++q) acc = (float)((double)acc + c);
+    done += m;
+  }
+  return acc;
+}
+
+// Score of a table entry.  AA / RA: one contribution is c(vmin); two are
+// c(vmin) then c(vmax) (ascending v, equal when one v contributes twice);
+// three or more re-walk the intersection.
+template <bool CUSTOM>
+__device__ __forceinline__ float hp_score(const HpArgs& a, uint32_t u, uint64_t du, uint32_t w, uint32_t c,
+                                          uint32_t v0, uint32_t v1) {
+  const bool ex = (c & HP_EXCL) != 0;
+  const uint32_t n = c & HP_CMASK;
+  if (!CUSTOM) return score_basic(a.metric, ex ? 0u : n, du, (uint64_t)a.g.deg[w]);
+  if (ex) return 0.0f;
+  if (n <= 2) {
+    float acc = (float)((double)0.0f + a.g.ctab[a.g.deg[v0]]);
+    if (n == 2) acc = (float)((double)acc + a.g.ctab[a.g.deg[v1]]);
+    return acc;
+  }
+  return hp_ordered_sum(a, u, w, n);
+}
+
+// ---------------------------------------------------------------- emission
+// Per-wave staging of emitted candidates in LDS: one global atomic per
+// HP_STG candidates instead of one per wave and iteration (a single counter
+// hammered by every wave of the chip serialises at one L2 channel).  The
+// candidate / NaN counts stay in registers until the kernel ends.
+constexpr int HP_STG = 128;
+
+struct HpStage {
+  uint32_t* key;  // HP_STG entries each
+  uint32_t* u;
+  uint32_t* w;
+  float* s;
+  uint32_t cap;   // entries per array
+  uint32_t n;     // wave-uniform fill
+  uint64_t cand, nan;
+};
+
+// Orders one wave's LDS accesses across lanes (staging, scan arrays, LDS
+// tables).  A wavefront-scope fence emits no instruction and the wave barrier
+// carries no memory semantics, so the machine scheduler may still move plain
+// DS reads and writes across them; a workgroup-scope fence is a real
+// s_waitcnt that nothing is scheduled across.
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+}
+
+__device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
+  if (st.n == 0) return;
+  wave_sync_lds();
+  const int lane = lane_id();
+  unsigned long long pos = 0;
+  if (lane == 0) pos = atomicAdd(&a.ctr[HPC_EMIT], (unsigned long long)st.n);
+  pos = __shfl(pos, 0, 64);
+  for (uint32_t i = lane; i < st.n; i += 64) {
+    const uint64_t p = pos + i;
+    if (p < a.cap) {
+      const uint64_t q = a.base + p;
+      a.ckey[q] = st.key[i];
+      a.cu[q] = st.u[i];
+      a.cw[q] = st.w[i];
+      a.cs[q] = st.s[i];
+    }
+  }
+  wave_sync_lds();
+  st.n = 0;
+}
+
+// Candidate filter (predict.hxx:309-311: score <= minScore skips, NaN passes)
+// and emission above tau; every active lane of the wave calls it.
+__device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid, float s, uint32_t u, uint32_t w,
+                                        int64_t tau) {
+  const bool cand = valid && !(s <= a.min_score);
+  st.cand += cand ? 1 : 0;
+  st.nan += (cand && s != s) ? 1 : 0;
+  const uint32_t key = cand ? score_key(s) : 0u;
+  const bool out = cand && (int64_t)key > tau;
+  const uint64_t mo = __ballot(out);
+  if (!mo) return;
+  const uint32_t n = (uint32_t)__popcll(mo);
+  if (st.n + n > st.cap) hp_flush(st, a);
+  if (out) {
+    const uint32_t i = st.n + (uint32_t)__popcll(mo & ((1ull << lane_id()) - 1));
+    st.key[i] = key;
+    st.u[i] = u;
+    st.w[i] = w;
+    st.s[i] = s;
+  }
+  st.n += n;
+}
+
+__device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t wedges) {
+  hp_flush(st, a);
+  const uint64_t c = wave_sum(st.cand), n = wave_sum(st.nan), wd = wave_sum(wedges);
+  if (lane_id() == 0) {
+    if (c) atomicAdd(&a.ctr[HPC_CAND], (unsigned long long)c);
+    if (n) atomicAdd(&a.ctr[HPC_NAN], (unsigned long long)n);
+    if (wd) atomicAdd(&a.ctr[HPC_WEDGE], (unsigned long long)wd);
+  }
+}
+
+__global__ void k_sum_deg2_above(const uint32_t* __restrict__ deg, uint64_t S, uint32_t above,
+                                 unsigned long long* __restrict__ out) {
+  unsigned long long s = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < S; v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t d = deg[v];
+    if (d > above) s += d * d;
+  }
+  s = wave_sum(s);
+  if (lane_id() == 0 && s) atomicAdd(out, s);
+}
+
+// ---------------------------------------------------------------- binning
+// Wave per source row: W(u) = sum of deg v over surviving v in N(u) (an upper
+// bound of the row's wedges; w > u is not applied), the row's bin, and one
+// flag byte per bin for the stable partition.  b1max: largest W of bin 1.
+__global__ __launch_bounds__(NT) void k_hp_work(GraphView g, uint32_t H, uint64_t ua, uint64_t nU,
+                                                uint64_t* __restrict__ wu, uint8_t* __restrict__ flags, int minbin,
+                                                uint64_t b1max) {
+  const uint64_t r = (uint64_t)blockIdx.x * NWAVE + wave_id();
+  if (r >= nU) return;
+  const int lane = lane_id();
+  const uint64_t u = ua + r;
+  const uint64_t o0 = g.off[u], o1 = g.off[u + 1];
+  uint64_t s = 0;
+  for (uint64_t i = o0 + lane; i < o1; i += 64) {
+    const uint32_t d = g.deg[g.keys[i]];
+    if (hp_surv(d, H)) s += d;
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    wu[r] = s;
+    int b = s == 0 ? -1 : s <= HP_B0_MAX ? 0 : s <= b1max ? 1 : s <= HP_B2_MAX ? 2 : 3;
+    if (b >= 0 && b < minbin) b = minbin;  // test hook: route rows to a larger bin
+#pragma unroll
+    for (int q = 0; q < HP_NBINS; ++q) flags[(uint64_t)q * nU + r] = b == q ? 1 : 0;
+  }
+}
+
+__global__ void k_hp_scatter(const uint8_t* __restrict__ flag, const uint64_t* __restrict__ pos, uint64_t nU,
+                             uint64_t ua, uint32_t* __restrict__ list) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nU; r += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[r]) list[pos[r]] = (uint32_t)(ua + r);
+}
+
+// Chunk end: the largest r1 in (r0, nU] with wpre[r1] - wpre[r0] <= target
+// (at least r0 + 1), and per bin the number of listed rows below ua + r1.
+__global__ void k_hp_bounds(const uint64_t* __restrict__ wpre, uint64_t nU, uint64_t r0, uint64_t target, uint64_t ua,
+                            const uint32_t* __restrict__ l0, const uint32_t* __restrict__ l1,
+                            const uint32_t* __restrict__ l2, const uint32_t* __restrict__ l3,
+                            const uint64_t* __restrict__ nl, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t base = wpre[r0];
+  uint64_t lo = r0 + 1, hi = nU;  // answer in [lo, hi]
+  while (lo < hi) {
+    const uint64_t m = (lo + hi + 1) >> 1;
+    if (wpre[m] - base <= target) lo = m; else hi = m - 1;
+  }
+  const uint64_t r1 = lo;
+  out[0] = r1;
+  const uint32_t* L[4] = {l0, l1, l2, l3};
+  const uint64_t x = ua + r1;
+  for (int b = 0; b < 4; ++b) {
+    uint64_t a = 0, c = nl[b];
+    while (a < c) {
+      const uint64_t m = (a + c) >> 1;
+      if ((uint64_t)L[b][m] < x) a = m + 1; else c = m;
+    }
+    out[1 + b] = a;
+  }
+}
+
+// ---------------------------------------------------------------- bin 0: wave per row, LDS table
+template <bool CUSTOM>
+__global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                const uint64_t* __restrict__ wu, uint64_t ua) {
+  constexpr int VT = CUSTOM ? HP_WT : 1;
+  __shared__ uint32_t s_k[NWAVE][HP_WT];
+  __shared__ uint32_t s_c[NWAVE][HP_WT];
+  __shared__ uint32_t s_v0[NWAVE][VT];
+  __shared__ uint32_t s_v1[NWAVE][VT];
+  __shared__ uint32_t s_incl[NWAVE][64];
+  __shared__ uint64_t s_start[NWAVE][64];
+  __shared__ uint32_t s_iv[NWAVE][64];
+  __shared__ uint32_t s_gk[NWAVE][HP_STG], s_gu[NWAVE][HP_STG], s_gw[NWAVE][HP_STG];
+  __shared__ float s_gs[NWAVE][HP_STG];
+  const int lane = lane_id(), wv = wave_id();
+  const HpTable tb{s_k[wv], s_c[wv], s_v0[wv], s_v1[wv]};
+  for (int i = lane; i < HP_WT; i += 64) {
+    s_k[wv][i] = HP_EMPTY;
+    s_c[wv][i] = 0;
+    if (CUSTOM) { s_v0[wv][i] = HP_EMPTY; s_v1[wv][i] = 0; }
+  }
+  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_STG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  wave_sync_lds();
+  for (uint64_t ri = (uint64_t)blockIdx.x * NWAVE + wv; ri < nrows; ri += (uint64_t)gridDim.x * NWAVE) {
+    const uint32_t u = rows[ri];
+    const uint64_t W = wu[u - ua];
+    const int lg = max(6, log2_ceil(2 * W));
+    const uint32_t T = 1u << lg, mask = T - 1;
+    const int shift = 32 - lg;
+    const uint64_t o0 = a.g.off[u], o1 = a.g.off[u + 1];
+    const uint64_t du = o1 - o0;
+    for (uint64_t base = 0; base < du; base += 64) {
+      const uint64_t i = base + lane;
+      uint32_t len = 0, v = 0;
+      uint64_t st = 0;
+      if (i < du) {
+        v = a.g.keys[o0 + i];
+        const uint32_t d = a.g.deg[v];
+        if (hp_surv(d, a.H)) {
+          len = d;
+          st = a.g.off[v];
+        }
+      }
+      const uint32_t incl = (uint32_t)wave_incl_scan(len);
+      s_incl[wv][lane] = incl;
+      s_start[wv][lane] = st;
+      s_iv[wv][lane] = v;
+      wave_sync_lds();
+      const uint32_t total = __shfl(incl, 63, 64);
+      for (uint32_t j = lane; j < total; j += 64) {
+        uint32_t lo = 0, hi = 63;  // first o with incl[o] > j
+        while (lo < hi) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (s_incl[wv][m] > j) hi = m; else lo = m + 1;
+        }
+        const uint32_t ex = lo ? s_incl[wv][lo - 1] : 0u;
+        const uint32_t w = a.g.keys[s_start[wv][lo] + (j - ex)];
+        if (w > u) {
+          ++wedges;
+          hp_insert<false, CUSTOM>(tb, mask, shift, w, s_iv[wv][lo], &a.ctr[HPC_ERR]);
+        }
+      }
+      wave_sync_lds();
+    }
+    for (uint64_t i = lane; i < du; i += 64) {  // first-order exclusion (predict.hxx:306-307)
+      const uint32_t x = a.g.keys[o0 + i];
+      if (x > u) hp_mark<false>(tb, mask, shift, x);
+    }
+    wave_sync_lds();
+    for (uint32_t i = lane; i < T; i += 64) {
+      uint32_t c = 0, v0 = 0, v1 = 0;
+      const uint32_t w = hp_take<false, CUSTOM>(tb, i, &c, &v0, &v1);
+      const bool valid = w != HP_EMPTY;
+      const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
+      hp_emit(sg, a, valid, s, u, w, tau);
+    }
+    wave_sync_lds();
+  }
+  hp_finish(sg, a, wedges);
+}
+
+// ---------------------------------------------------------------- bins 1-3: workgroup per row
+// GLOBAL = false: LDS table of up to HP_BT entries (HP_BT / 2 for AA / RA;
+// bin 1).  GLOBAL = true: per-workgroup slab of 2^tlog entries in global memory
+// (bins 2, 3); a row whose distinct-w bound exceeds the slab is split into
+// w-range passes.
+__device__ __forceinline__ uint64_t block_incl_scan_1024(uint64_t x, uint64_t* s_w /*16*/) {
+  const uint64_t inc = wave_incl_scan(x);
+  if (lane_id() == 63) s_w[wave_id()] = inc;
+  __syncthreads();
+  uint64_t pre = 0;
+  for (int q = 0; q < wave_id(); ++q) pre += s_w[q];
+  __syncthreads();
+  return pre + inc;
+}
+
+constexpr int HP_BSTG = 64;  // staging per wave in the block kernels
+
+// Workgroup barrier.  A global table is accessed with agent-scope atomics at
+// L2, so the barrier must also wait for this wave's outstanding global
+// operations (no-return atomics, the resets of the previous row): an
+// agent-scope release/acquire around the barrier.
+template <bool GLOBAL>
+__device__ __forceinline__ void hp_sync() {
+  if (GLOBAL) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (GLOBAL) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <bool CUSTOM, bool GLOBAL>
+__global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                     const uint64_t* __restrict__ wu, uint64_t ua,
+                                                     uint32_t* __restrict__ slab, int tlog) {
+  constexpr int LT = GLOBAL ? 1 : (CUSTOM ? HP_BT / 2 : HP_BT);
+  constexpr int VT = CUSTOM ? LT : 1;
+  constexpr int NW = HP_BNT / 64;
+  __shared__ uint32_t s_k[LT];
+  __shared__ uint32_t s_c[LT];
+  __shared__ uint32_t s_v0[VT];
+  __shared__ uint32_t s_v1[VT];
+  __shared__ uint64_t s_incl[HP_BNT];
+  __shared__ uint64_t s_start[HP_BNT];
+  __shared__ uint32_t s_iv[HP_BNT];
+  __shared__ uint64_t s_w[NW];
+  __shared__ uint64_t s_tot;
+  __shared__ uint32_t s_gk[NW][HP_BSTG], s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ float s_gs[NW][HP_BSTG];
+  const int t = threadIdx.x, wv = wave_id();
+  const uint64_t tmax = GLOBAL ? (1ull << tlog) : (uint64_t)LT;
+  HpTable tb;
+  if (GLOBAL) {
+    tb.k = slab + (uint64_t)blockIdx.x * tmax * 4;  // [keys | counts | vmin | vmax] per workgroup
+    tb.c = tb.k + tmax;
+    tb.vmin = tb.c + tmax;
+    tb.vmax = tb.vmin + tmax;
+  } else {
+    tb = HpTable{s_k, s_c, s_v0, s_v1};
+    for (int i = t; i < LT; i += HP_BNT) {
+      s_k[i] = HP_EMPTY;
+      s_c[i] = 0;
+      if (CUSTOM) { s_v0[i] = HP_EMPTY; s_v1[i] = 0; }
+    }
+  }
+  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  __syncthreads();
+  for (uint64_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+    const uint32_t u = rows[ri];
+    const uint64_t W = wu[u - ua];
+    const uint64_t o0 = a.g.off[u], o1 = a.g.off[u + 1];
+    const uint64_t du = o1 - o0;
+    const uint64_t span_w = a.S - 1 - u;              // candidate w in (u, S)
+    const uint64_t need = 2 * (W < span_w ? W : span_w);
+    const int tl = GLOBAL ? tlog : (CUSTOM ? 12 : 13);
+    int lg = max(6, log2_ceil(need));
+    uint64_t passes = 1;
+    if (lg > tl) {
+      // w-range passes no wider than half the table: at most tmax / 2 distinct w per pass
+      passes = (2 * span_w + tmax - 1) / tmax;
+      lg = tl;
+    }
+    const uint32_t T = 1u << lg, mask = T - 1;
+    const int shift = 32 - lg;
+    const uint64_t rw = (span_w + passes - 1) / passes;
+    for (uint64_t p = 0; p < passes; ++p) {
+      const uint64_t wlo = (uint64_t)u + 1 + p * rw;
+      const uint64_t whi = wlo + rw < a.S ? wlo + rw : a.S;
+      for (uint64_t base = 0; base < du; base += HP_BNT) {
+        const uint64_t i = base + t;
+        uint32_t v = 0;
+        uint64_t len = 0, st = 0;
+        if (i < du) {
+          v = a.g.keys[o0 + i];
+          const uint32_t d = a.g.deg[v];
+          if (hp_surv(d, a.H)) {
+            len = d;
+            st = a.g.off[v];
+          }
+        }
+        const uint64_t incl = block_incl_scan_1024(len, s_w);
+        s_incl[t] = incl;
+        s_start[t] = st;
+        s_iv[t] = v;
+        if (t == HP_BNT - 1) s_tot = incl;
+        hp_sync<GLOBAL>();
+        const uint64_t total = s_tot;
+        for (uint64_t j = t; j < total; j += HP_BNT) {
+          uint32_t lo = 0, hi = HP_BNT - 1;
+          while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s_incl[m] > j) hi = m; else lo = m + 1;
+          }
+          const uint64_t ex = lo ? s_incl[lo - 1] : 0ull;
+          const uint32_t w = a.g.keys[s_start[lo] + (j - ex)];
+          if (w > u) {
+            if (p == 0) ++wedges;
+            if ((uint64_t)w >= wlo && (uint64_t)w < whi)
+              hp_insert<GLOBAL, CUSTOM>(tb, mask, shift, w, s_iv[lo], &a.ctr[HPC_ERR]);
+          }
+        }
+        hp_sync<GLOBAL>();
+      }
+      for (uint64_t i = t; i < du; i += HP_BNT) {
+        const uint32_t x = a.g.keys[o0 + i];
+        if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
+      }
+      hp_sync<GLOBAL>();
+      for (uint32_t i = t; i < T; i += HP_BNT) {
+        uint32_t c = 0, v0 = 0, v1 = 0;
+        const uint32_t w = hp_take<GLOBAL, CUSTOM>(tb, i, &c, &v0, &v1);
+        const bool valid = w != HP_EMPTY;
+        const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
+        hp_emit(sg, a, valid, s, u, w, tau);
+      }
+      hp_sync<GLOBAL>();
+    }
+  }
+  hp_finish(sg, a, wedges);
+}
+
+// ---------------------------------------------------------------- pruning between chunks
+// Split the candidate buffer around the k-th key (sel[3] from the radix
+// select): keys above go to the target columns (unordered), ties to a list of
+// (u << 32 | w) records with their index, to be ordered canonically.
+__global__ __launch_bounds__(NT) void k_hp_split(const uint32_t* __restrict__ key, const uint32_t* __restrict__ u,
+                                                 const uint32_t* __restrict__ w, const float* __restrict__ s, uint64_t n,
+                                                 const uint64_t* __restrict__ sel, uint32_t* __restrict__ okey,
+                                                 uint32_t* __restrict__ ou, uint32_t* __restrict__ ow,
+                                                 float* __restrict__ os, uint64_t* __restrict__ tie_k,
+                                                 uint32_t* __restrict__ tie_i, unsigned long long* __restrict__ cnt) {
+  const uint32_t kth = (uint32_t)sel[3];
+  const int lane = lane_id();
+  for (uint64_t i0 = (uint64_t)blockIdx.x * NT; i0 < n; i0 += (uint64_t)gridDim.x * NT) {
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t k = i < n ? key[i] : 0u;
+    const bool above = i < n && k > kth, tie = i < n && k == kth;
+    const uint64_t ma = __ballot(above), mt = __ballot(tie);
+    const int leader = __ffsll((long long)(ma | mt | 1ull)) - 1;
+    unsigned long long pa = 0, pt = 0;
+    if (lane == leader) {
+      if (ma) pa = atomicAdd(&cnt[0], (unsigned long long)__popcll(ma));
+      if (mt) pt = atomicAdd(&cnt[1], (unsigned long long)__popcll(mt));
+    }
+    pa = __shfl(pa, leader, 64);
+    pt = __shfl(pt, leader, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    if (above) {
+      const uint64_t q = pa + __popcll(ma & below);
+      okey[q] = k;
+      ou[q] = u[i];
+      ow[q] = w[i];
+      os[q] = s[i];
+    } else if (tie) {
+      const uint64_t q = pt + __popcll(mt & below);
+      tie_k[q] = ((uint64_t)u[i] << 32) | w[i];
+      tie_i[q] = (uint32_t)i;
+    }
+  }
+}
+
+// the first `take` ties (canonical order) behind the `above` entries
+__global__ void k_hp_take(const uint32_t* __restrict__ idx, uint64_t take, uint64_t above,
+                          const uint32_t* __restrict__ key, const uint32_t* __restrict__ u,
+                          const uint32_t* __restrict__ w, const float* __restrict__ s, uint32_t* __restrict__ okey,
+                          uint32_t* __restrict__ ou, uint32_t* __restrict__ ow, float* __restrict__ os) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < take; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = idx[j];
+    okey[above + j] = key[i];
+    ou[above + j] = u[i];
+    ow[above + j] = w[i];
+    os[above + j] = s[i];
+  }
+}
+
+// (u << 32 | w) + identity index, for the canonical (u, w) order before the final sort
+__global__ void k_hp_uwkeys(const uint32_t* __restrict__ u, const uint32_t* __restrict__ w, uint64_t n,
+                            uint64_t* __restrict__ k, uint32_t* __restrict__ idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    k[i] = ((uint64_t)u[i] << 32) | w[i];
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ void k_hp_permute(const uint32_t* __restrict__ idx, uint64_t n, const uint32_t* __restrict__ key,
+                             const uint32_t* __restrict__ u, const uint32_t* __restrict__ w,
+                             const float* __restrict__ s, uint32_t* __restrict__ okey, uint32_t* __restrict__ ou,
+                             uint32_t* __restrict__ ow, float* __restrict__ os) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = idx[j];
+    okey[j] = key[i];
+    ou[j] = u[i];
+    ow[j] = w[i];
+    os[j] = s[i];
+  }
+}
+
+__global__ void k_hp_fill_slab(uint32_t* __restrict__ slab, uint64_t nblk, uint64_t tmax) {
+  const uint64_t n = nblk * tmax * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    slab[i] = ((i / tmax) % 2) == 0 ? HP_EMPTY : 0u;  // keys, vmin empty; counts, vmax 0
+}
+
+}  // namespace nlp

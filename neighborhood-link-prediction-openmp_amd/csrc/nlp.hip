@@ -22,6 +22,7 @@
 #include "group.hpp"
 #include "select.hpp"
 #include "sortpath.hpp"
+#include "hashpath.hpp"
 
 using namespace nlp;
 
@@ -65,6 +66,9 @@ enum Buf {
   // sort-grouped fast path (sortpath.hpp)
   B_SP_SURV, B_SP_RK0, B_SP_RK1, B_SP_RV0, B_SP_RV1, B_SP_STASH, B_SP_CU, B_SP_CW, B_SP_CS,
   B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
+  // hash path (hashpath.hpp)
+  B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
+  B_HP_TIEI0, B_HP_TIEI1,
   NBUF
 };
 
@@ -164,6 +168,18 @@ struct nlp_graph {
   };
   std::vector<Cached> graphs;
   uint64_t use_clock = 0;
+  // hash path: per-workgroup global tables of bins 2 and 3 (kept clean between calls)
+  uint32_t* hp_slab2 = nullptr;
+  uint32_t* hp_slab3 = nullptr;
+  unsigned hp_g2 = 0, hp_g3 = 0;
+  int hp_t3log = 0;
+  uint64_t hp_min_wedges = 1ull << 23;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 3 runs
+  int hash_mode = 0;                           // NLP_HASH: 0 auto, 1 always, -1 never
+  // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_T3LOG
+  uint64_t hp_emit = 0;
+  int hp_minbin = 0, hp_t3log_force = 0;
+  std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
+  uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
 };
 
 namespace {
@@ -224,6 +240,8 @@ void destroy_graph(nlp_graph* g) {
       if (x) (void)hipGraphExecDestroy(x);
   g->graphs.clear();
   if (g->d_stamp) (void)hipFree(g->d_stamp);
+  if (g->hp_slab2) (void)hipFree(g->hp_slab2);
+  if (g->hp_slab3) (void)hipFree(g->hp_slab3);
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -243,6 +261,12 @@ void destroy_graph(nlp_graph* g) {
   if (g->host_ctr) (void)hipHostFree(g->host_ctr);
   if (g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
+}
+
+int log2_host(uint64_t x) {  // ceil(log2(x)), x >= 1
+  int b = 0;
+  while (b < 63 && (1ull << b) < x) ++b;
+  return b;
 }
 
 int bits_for(uint64_t maxval) {  // bits needed to represent values <= maxval
@@ -336,6 +360,17 @@ nlp_status finish_graph(nlp_graph* g) {
     std::vector<uint32_t> hh(DCAP + 2);
     TRY(hipMemcpyAsync(hh.data(), hist, (DCAP + 2) * 4, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
+    g->deg_hist.assign(hh.begin(), hh.end());
+    g->deg_hist.resize(DCAP + 1);  // degrees 0..DCAP; above DCAP: big_deg2
+    {
+      unsigned long long* d2;
+      TRY(wsget(g->ws, B_HP_SMALL, 8, &d2));
+      TRY(hipMemsetAsync(d2, 0, 8, st));
+      hipLaunchKernelGGL(k_sum_deg2_above, dim3(grid_for(S)), dim3(NT), 0, st, (const uint32_t*)g->deg, S, DCAP, d2);
+      TRY(hipGetLastError());
+      TRY(hipMemcpyAsync(&g->big_deg2, d2, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+    }
     g->dstart.assign(DCAP + 2, 0);
     for (uint32_t d = 1; d <= DCAP; ++d) g->dstart[d + 1] = g->dstart[d] + hh[d];
     const uint64_t nv = g->dstart[DCAP + 1];
@@ -381,6 +416,11 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
   }
   if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
+  if (const char* hm = getenv("NLP_HASH")) g->hash_mode = hm[0] == '1' ? 1 : (hm[0] == '0' ? -1 : 0);
+  if (const char* hw = getenv("NLP_HASH_MIN_WEDGES")) g->hp_min_wedges = strtoull(hw, nullptr, 10);
+  if (const char* he = getenv("NLP_HASH_EMIT")) g->hp_emit = strtoull(he, nullptr, 10);
+  if (const char* hb = getenv("NLP_HASH_MINBIN")) g->hp_minbin = std::min(3, std::max(0, atoi(hb)));
+  if (const char* ht = getenv("NLP_HASH_T3LOG")) g->hp_t3log_force = std::min(HP_T3_LOG_MAX, std::max(6, atoi(ht)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* gr = getenv("NLP_GROUPING")) {
@@ -989,6 +1029,313 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a = bnd;
   }
   return NLP_OK;
+}
+
+// ================================================================ path 3 (hash accumulation)
+// hashpath.hpp: source rows binned by their wedge bound W(u), accumulated in
+// LDS / global hash tables, candidates emitted unordered above the running
+// threshold tau and pruned to the canonical top k between chunks of rows.
+
+// Global tables of bins 2 and 3, allocated once and kept clean (every row
+// resets the entries it used).
+nlp_status hp_slabs(nlp_graph* g, hipStream_t st) {
+  if (g->hp_slab2 && g->hp_slab3) return NLP_OK;
+  size_t fr = 0, tot = 0;
+  TRY(hipMemGetInfo(&fr, &tot));
+  const uint64_t budget = fr / 16;  // both slabs together
+  g->hp_t3log = g->hp_t3log_force ? g->hp_t3log_force
+                                  : std::min(HP_T3_LOG_MAX, std::max(HP_T2_LOG, log2_host(2 * g->span)));
+  const uint64_t per2 = (1ull << HP_T2_LOG) * 16, per3 = (1ull << g->hp_t3log) * 16;  // 4 u32 per entry
+  g->hp_g2 = (unsigned)std::max<uint64_t>(16, std::min<uint64_t>(256, budget / 2 / per2));
+  g->hp_g3 = (unsigned)std::max<uint64_t>(4, std::min<uint64_t>(64, budget / 2 / per3));
+  TRY(hipMalloc(&g->hp_slab2, g->hp_g2 * per2));
+  TRY(hipMalloc(&g->hp_slab3, g->hp_g3 * per3));
+  hipLaunchKernelGGL(k_hp_fill_slab, dim3(4096), dim3(NT), 0, st, g->hp_slab2, (uint64_t)g->hp_g2, 1ull << HP_T2_LOG);
+  hipLaunchKernelGGL(k_hp_fill_slab, dim3(4096), dim3(NT), 0, st, g->hp_slab3, (uint64_t)g->hp_g3,
+                     1ull << g->hp_t3log);
+  TRY(hipGetLastError());
+  return NLP_OK;
+}
+
+// Prune the (unordered) candidate buffer to the canonical top k:
+// radix-select the k-th key, keep every key above it and the first ties in
+// (u, w) order.  Returns the k-th key in *kth.
+nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* kth, hipStream_t st) {
+  Workspace& ws = g->ws;
+  const uint64_t n = C.n;
+  uint32_t *ckey = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
+  float* cs = (float*)ws.p[B_CS];
+  uint32_t* selhist;
+  uint64_t *sel, *small;
+  TRY(wsget(ws, B_SELHIST, SEL_BINS, &selhist));
+  TRY(wsget(ws, B_SEL, 8, &sel));
+  TRY(wsget(ws, B_HP_SMALL, 64, &small));
+  uint64_t* h = g->host_small;
+  h[8] = n;
+  h[9] = 0;  // sel: prefix, rank, above, key
+  h[10] = k;
+  h[11] = 0;
+  h[12] = 0;
+  TRY(hipMemcpyAsync(small + 32, &h[8], 8, hipMemcpyHostToDevice, st));
+  TRY(hipMemcpyAsync(sel, &h[9], 32, hipMemcpyHostToDevice, st));
+  TRY(hipMemsetAsync(selhist, 0, SEL_BINS * 4, st));
+  TRY(hipMemsetAsync(small + 40, 0, 16, st));
+  for (int pass = 0; pass < 3; ++pass) {
+    LAUNCH(k_sel_hist, n, st, ckey, small + 32, pass, sel, selhist);
+    hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(NT), 0, st, selhist, pass, sel);
+    TRY(hipGetLastError());
+  }
+  uint32_t *nk, *nu, *nw, *ti0, *ti1;
+  float* ns;
+  uint64_t *tk0, *tk1;
+  // the target becomes the candidate buffer: same capacity
+  TRY(wsget(ws, B_TKEY, std::max<uint64_t>(cap, 1), &nk));
+  TRY(wsget(ws, B_TU, std::max<uint64_t>(cap, 1), &nu));
+  TRY(wsget(ws, B_TW, std::max<uint64_t>(cap, 1), &nw));
+  TRY(wsget(ws, B_TS, std::max<uint64_t>(cap, 1), &ns));
+  TRY(wsget(ws, B_HP_TIEK0, n, &tk0));
+  TRY(wsget(ws, B_HP_TIEI0, n, &ti0));
+  LAUNCH(k_hp_split, n, st, ckey, cu, cw, cs, n, sel, nk, nu, nw, ns, tk0, ti0, (unsigned long long*)(small + 40));
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(&h[16], sel, 32, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(&h[20], small + 40, 16, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t quota = h[17], above = h[18], ties = h[21];
+  *kth = (uint32_t)h[19];
+  if (above != h[20] || quota > ties || above + quota != k) return NLP_ERR_DEVICE;
+  const uint32_t* take_idx = ti0;
+  if (ties > quota) {
+    // canonical tie order: (u asc, w asc)
+    TRY(wsget(ws, B_HP_TIEK1, ties, &tk1));
+    TRY(wsget(ws, B_HP_TIEI1, ties, &ti1));
+    uint64_t nb = rs_blocks(ties);
+    uint32_t* hist;
+    uint64_t *hoff, *scan;
+    TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+    TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+    TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(ties, RS_BINS * nb)) + 16, &scan));
+    const int vb = bits_for(g->span - 1);
+    int shifts[8], np = 0;
+    for (int b = 0; b < vb; b += 8) shifts[np++] = b;
+    for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
+    SortScratch sc{hist, hoff, scan, nb};
+    int which = 0;
+    TRY(sort_pairs_u64(tk0, ti0, tk1, ti1, ties, shifts, np, sc, &which, st));
+    take_idx = which ? ti1 : ti0;
+  }
+  if (quota)
+    LAUNCH(k_hp_take, quota, st, take_idx, quota, above, ckey, cu, cw, cs, nk, nu, nw, ns);
+  TRY(hipGetLastError());
+  std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
+  std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
+  std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
+  std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  C.n = k;
+  return NLP_OK;
+}
+
+// Put the held candidates in (u asc, w asc) order (the order order_v1 expects).
+nlp_status hp_uw_order(nlp_graph* g, Cands& C, hipStream_t st) {
+  if (C.n <= 1) return NLP_OK;
+  Workspace& ws = g->ws;
+  const uint64_t n = C.n;
+  uint64_t *k0, *k1, *hoff, *scan;
+  uint32_t *v0, *v1, *hist;
+  TRY(wsget(ws, B_SK0, n, &k0));
+  TRY(wsget(ws, B_SK1, n, &k1));
+  TRY(wsget(ws, B_SV0, n, &v0));
+  TRY(wsget(ws, B_SV1, n, &v1));
+  uint64_t nb = rs_blocks(n);
+  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(n, RS_BINS * nb)) + 16, &scan));
+  LAUNCH(k_hp_uwkeys, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], n, k0, v0);
+  TRY(hipGetLastError());
+  const int vb = bits_for(g->span - 1);
+  int shifts[8], np = 0;
+  for (int b = 0; b < vb; b += 8) shifts[np++] = b;
+  for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
+  SortScratch sc{hist, hoff, scan, nb};
+  int which = 0;
+  TRY(sort_pairs_u64(k0, v0, k1, v1, n, shifts, np, sc, &which, st));
+  uint32_t *nk, *nu, *nw;
+  float* ns;
+  TRY(wsget(ws, B_TKEY, n, &nk));
+  TRY(wsget(ws, B_TU, n, &nu));
+  TRY(wsget(ws, B_TW, n, &nw));
+  TRY(wsget(ws, B_TS, n, &ns));
+  LAUNCH(k_hp_permute, n, st, which ? v1 : v0, n, (const uint32_t*)ws.p[B_CKEY], (const uint32_t*)ws.p[B_CU],
+         (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], nk, nu, nw, ns);
+  TRY(hipGetLastError());
+  std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
+  std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
+  std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
+  std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  return NLP_OK;
+}
+
+// Estimated wedges (w > u) of a call: sum over surviving v of deg(v)^2 / 2,
+// scaled to the source range.
+double hp_estimate(const nlp_graph* g, const Params& p) {
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
+  double w = 0;
+  for (size_t d = 1; d < g->deg_hist.size(); ++d)
+    if (p.H == 0 || d <= p.H) w += (double)d * (double)d * (double)g->deg_hist[d];
+  if (p.H == 0 || p.H > DCAP) w += (double)g->big_deg2;  // upper bound for DCAP < H
+  return S ? 0.5 * w * (double)(ub - ua) / (double)S : 0.0;
+}
+
+nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks, hipStream_t st) {
+  Workspace& ws = g->ws;
+  const uint64_t S = g->span;
+  const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
+  uint64_t k = p.max_edges;
+  *nchunks = 0;
+  if (nU == 0 || g->nnz == 0) return NLP_OK;
+  { nlp_status s0 = hp_slabs(g, st); if (s0 != NLP_OK) return s0; }
+  uint64_t *wu, *pos, *small;
+  uint8_t* flags;
+  TRY(wsget(ws, B_HP_WU, nU + 1, &wu));
+  TRY(wsget(ws, B_HP_FLAGS, (uint64_t)HP_NBINS * nU, &flags));
+  TRY(wsget(ws, B_HP_POS, nU + 1, &pos));
+  TRY(wsget(ws, B_HP_SMALL, 64, &small));
+  uint64_t* scan;
+  TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
+  // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
+  const GraphView gv = view_of(g, p.metric);
+  hipLaunchKernelGGL(k_hp_work, dim3((unsigned)((nU + NWAVE - 1) / NWAVE)), dim3(NT), 0, st, gv, p.H, ua, nU, wu, flags,
+                     g->hp_minbin, (uint64_t)(custom ? HP_BT / 4 : HP_B1_MAX));
+  TRY(hipGetLastError());
+  uint32_t* lists[HP_NBINS];
+  const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
+  for (int b = 0; b < HP_NBINS; ++b) {
+    TRY(wsget(ws, lb[b], nU, &lists[b]));
+    TRY(scan_excl_u64<uint8_t>(flags + (uint64_t)b * nU, nU, pos, small + 24 + b, scan, st));
+    LAUNCH(k_hp_scatter, nU, st, flags + (uint64_t)b * nU, pos, nU, ua, lists[b]);
+    TRY(hipGetLastError());
+  }
+  // row prefix of W(u) (wu[nU] = total)
+  TRY(scan_excl_u64<uint64_t>(wu, nU, pos, small + 16, scan, st));
+  TRY(hipMemcpyAsync(pos + nU, small + 16, 8, hipMemcpyDeviceToDevice, st));
+  TRY(hipMemcpyAsync(&g->host_small[8], small + 16, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t wtot = g->host_small[8];  // >= the number of candidates
+  if (wtot == 0) return NLP_OK;
+  if (k > wtot) k = wtot;                   // maxEdges = all candidates
+  // candidate buffer: k held + E emitted per chunk
+  const uint64_t E = std::max<uint64_t>(g->hp_emit ? g->hp_emit : std::max<uint64_t>(1ull << 26, 4 * k), S);
+  const uint64_t capC = k + E;
+  { nlp_status s0 = cand_reserve(g, capC, 0, st); if (s0 != NLP_OK) return s0; }
+  int64_t tau = -1;
+  g->host_small[8] = (uint64_t)tau;
+  TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
+  uint64_t r0 = 0, q0[HP_NBINS] = {0, 0, 0, 0};
+  double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
+  bool full = false;  // k candidates held: tau is in force
+  uint64_t target = E;
+  while (r0 < nU) {
+    hipLaunchKernelGGL(k_hp_bounds, dim3(1), dim3(64), 0, st, (const uint64_t*)pos, nU, r0, target, ua,
+                       (const uint32_t*)lists[0], (const uint32_t*)lists[1], (const uint32_t*)lists[2],
+                       (const uint32_t*)lists[3], (const uint64_t*)(small + 24), small + 16);
+    TRY(hipGetLastError());
+    TRY(hipMemsetAsync(small, 0, 8 * HPC_NCTR, st));
+    // bounds are read back with the counters below; the kernels read them from the host copy
+    TRY(hipMemcpyAsync(&g->host_small[16], small + 16, 40, hipMemcpyDeviceToHost, st));
+    TRY(hipMemcpyAsync(&g->host_small[40], pos + r0, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t r1 = g->host_small[16];
+    uint64_t q1[HP_NBINS];
+    for (int b = 0; b < HP_NBINS; ++b) q1[b] = g->host_small[17 + b];
+    TRY(hipMemcpyAsync(&g->host_small[41], pos + r1, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t wchunk = g->host_small[41] - g->host_small[40];
+    HpArgs a;
+    a.g = gv;
+    a.S = S;
+    a.H = p.H;
+    a.metric = p.metric;
+    a.min_score = p.min_score;
+    a.ckey = (uint32_t*)ws.p[B_CKEY];
+    a.cu = (uint32_t*)ws.p[B_CU];
+    a.cw = (uint32_t*)ws.p[B_CW];
+    a.cs = (float*)ws.p[B_CS];
+    a.base = C.n;
+    a.cap = capC - C.n;
+    a.tau = (const int64_t*)(small + 8);
+    a.ctr = (unsigned long long*)small;
+    const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1], n2 = q1[2] - q0[2], n3 = q1[3] - q0[3];
+    if (n0) {
+      const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
+      if (custom) hipLaunchKernelGGL(k_hp_wave<true>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
+      else hipLaunchKernelGGL(k_hp_wave<false>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
+      TRY(hipGetLastError());
+    }
+    if (n1) {
+      const unsigned gr = (unsigned)std::min<uint64_t>(n1, 2048);
+      if (custom) hipLaunchKernelGGL((k_hp_block<true, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13);
+      else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13);
+      TRY(hipGetLastError());
+    }
+    if (n2) {
+      const unsigned gr = (unsigned)std::min<uint64_t>(n2, g->hp_g2);
+      if (custom) hipLaunchKernelGGL((k_hp_block<true, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[2] + q0[2], n2, wu, ua, g->hp_slab2, HP_T2_LOG);
+      else hipLaunchKernelGGL((k_hp_block<false, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[2] + q0[2], n2, wu, ua, g->hp_slab2, HP_T2_LOG);
+      TRY(hipGetLastError());
+    }
+    if (n3) {
+      const unsigned gr = (unsigned)std::min<uint64_t>(n3, g->hp_g3);
+      if (custom) hipLaunchKernelGGL((k_hp_block<true, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[3] + q0[3], n3, wu, ua, g->hp_slab3, g->hp_t3log);
+      else hipLaunchKernelGGL((k_hp_block<false, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[3] + q0[3], n3, wu, ua, g->hp_slab3, g->hp_t3log);
+      TRY(hipGetLastError());
+    }
+    TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t emitted = g->host_small[HPC_EMIT];
+    if (g->host_small[HPC_ERR]) return NLP_ERR_DEVICE;
+    if (emitted > a.cap) {
+      // overflow: nothing of this chunk is kept; prune what is held and retry a smaller chunk
+      rate = std::max(rate, (double)emitted / (double)std::max<uint64_t>(wchunk, 1));
+      target = std::max<uint64_t>(1, wchunk / 4);
+      if (C.n > k) {
+        uint32_t kth = 0;
+        nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+        if (s != NLP_OK) return s;
+        tau = (int64_t)kth;
+        full = true;
+        g->host_small[8] = (uint64_t)tau;
+        TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
+      } else if (r1 == r0 + 1) {
+        return NLP_ERR_DEVICE;  // one row cannot exceed E >= S free slots
+      }
+      continue;
+    }
+    ++*nchunks;
+    C.n += emitted;
+    C.total += g->host_small[HPC_CAND];
+    C.nan += g->host_small[HPC_NAN];
+    C.wedges += g->host_small[HPC_WEDGE];
+    rate = (double)emitted / (double)std::max<uint64_t>(wchunk, 1);
+    r0 = r1;
+    for (int b = 0; b < HP_NBINS; ++b) q0[b] = q1[b];
+    if (C.n > k && (C.n > k + E / 2 || r0 >= nU)) {
+      uint32_t kth = 0;
+      nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+      if (s != NLP_OK) return s;
+      tau = (int64_t)kth;
+      full = true;
+      g->host_small[8] = (uint64_t)tau;
+      TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
+    }
+    // next chunk: aim at half of the free buffer at the last emission rate
+    const uint64_t free_slots = capC - C.n;
+    const double want = 0.5 * (double)free_slots / std::max(rate, 1e-9);
+    target = (uint64_t)std::min(want, 1e18);
+    if (!full && target > free_slots) target = free_slots;  // no threshold yet: emissions <= W(u)
+    if (target == 0) target = 1;
+  }
+  return hp_uw_order(g, C, st);
 }
 
 // ================================================================ fast path
@@ -1681,7 +2028,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
 
 nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result) {
-  if ((p.H > 0 || g->sort_grouping) && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
+  // path 3 (hash accumulation) once the wedge count is large: bounded memory,
+  // no wedge materialisation (NLP_HASH=1 forces it, NLP_HASH=0 disables it)
+  const bool use_hash = !g->force_radix && p.max_edges > 0 &&
+                        (g->hash_mode > 0 || (g->hash_mode == 0 && hp_estimate(g, p) > (double)g->hp_min_wedges));
+  if (!use_hash && (p.H > 0 || g->sort_grouping) && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
     bool handled = false;
     nlp_status s = predict_fast(g, p, d_out, out_count, t, st, result, &handled);
     if (s != NLP_OK || handled) return s;
@@ -1692,7 +2043,14 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   TRY(hipEventRecord(g->ev[0], st));
   if (p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
     bool done = false;
-    if (p.H > 0 && !g->force_radix) {
+    if (use_hash) {
+      nlp_status s = run_path3(g, p, C, &chunks, st);
+      if (s != NLP_OK) return s;
+      done = true;
+      path = 4;
+      have_nan = true;
+    }
+    if (!done && p.H > 0 && !g->force_radix) {
       uint64_t fl = 0;
       bool over = false;
       nlp_status s = run_path1_v1(g, p, C, &fl, &over, st);

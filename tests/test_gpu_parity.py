@@ -354,3 +354,131 @@ def test_gpu_degree_index_equals_survivor_scan(gpu, oracle):
     for (m, H), (u, w, s, t) in list(res.items())[::5]:
         eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=2500)
         assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+class _env:
+    """Set environment variables for the graphs created inside the block (the
+    library reads its switches at graph creation)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+# path 4 (hash accumulation) with every bin forced: 0 wave/LDS, 1 workgroup/LDS,
+# 2 workgroup/global slab, 3 workgroup/global slab with w-range passes (tiny slab)
+HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_T3LOG="6")]
+
+
+@pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
+def test_gpu_hash_path_vs_oracle(gpu, oracle, golden, variant):
+    """Path 4 against the oracle: every metric, IHub and LHub, top-k smaller and
+    larger than the candidate count, tiny emission buffers (many chunks, pruning
+    and the running threshold), multigraphs with duplicates and asymmetry."""
+    graphs = [(golden["g3k"]["offsets"], golden["g3k"]["keys"]), (golden["edge"]["offsets"], golden["edge"]["keys"]),
+              random_csr(3000, 12, 11)]
+    with _env(NLP_HASH="1", NLP_HASH_EMIT="1", **HASH_VARIANTS[variant]):
+        for off, keys in graphs:
+            with gpu.Graph(off, keys) as G:
+                for m in range(9):
+                    for H in (0, 2, 4, 16):
+                        for k in (40, 4000):
+                            u, w, s, t = G.predict(m, H, k)
+                            eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k)
+                            assert t["path"] == 4
+                            assert_canonical_equal(eu, ew, es, u, w, s)
+                            assert t["wedges"] == info["wedges_gt"]
+                            assert t["candidates"] == info["candidates"] and t["nan_candidates"] == info["nan"]
+
+
+def test_gpu_hash_path_all_candidates_and_min_score(gpu, golden, oracle):
+    """maxEdges = all (no pruning) and minScore < 0 (excluded first-order pairs
+    with score 0 become candidates, predict.hxx:306-311)."""
+    with _env(NLP_HASH="1"):
+        for name in ("g300", "edge"):  # every reference candidate list of these fixtures
+            g = golden[name]
+            with gpu.Graph(g["offsets"], g["keys"]) as G:
+                for key in g:
+                    if key.startswith("cand_") and key.endswith("_u"):
+                        _, m, H, _ = key.split("_")
+                        u, w, s, t = G.predict(int(m), int(H), None)
+                        assert t["path"] == 4 or len(u) == 0  # no candidates: the fetch call has maxEdges 0
+                        assert_same_candidates(g[key], g["cand_%s_%s_w" % (m, H)], g["cand_%s_%s_s" % (m, H)], u, w, s)
+        g = golden["g3k"]
+        with gpu.Graph(g["offsets"], g["keys"]) as G:
+            for m in (0, 1, 7, 8):
+                for H in (0, 4):
+                    u, w, s, t = G.predict(m, H, 5000, min_score=-1.0)
+                    eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], m, H, max_edges=5000, min_score=-1.0)
+                    assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_hash_path_star_hub(gpu, oracle):
+    """A hub source whose row holds > 10^4 distinct second hops (bins 2 and 3)."""
+    off, keys = star_csr(20000)
+    for v in (dict(), dict(NLP_HASH_T3LOG="8")):
+        with _env(NLP_HASH="1", **v):
+            with gpu.Graph(off, keys) as G:
+                for m, H, k in ((0, 0, 500), (7, 0, 30000), (1, 2, 10 ** 6), (8, 4, 100)):
+                    u, w, s, t = G.predict(m, H, k)
+                    eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                    assert t["path"] == 4
+                    assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_hash_routing_and_shards(gpu, oracle):
+    """Automatic routing by the wedge estimate, and per-shard path-4 results
+    merged on the device equal the single-range result."""
+    import torch
+    off, keys = random_csr(8000, 16, 12)
+    span = len(off) - 1
+    k = 3000
+    with _env(NLP_HASH_MIN_WEDGES="1000"):
+        with gpu.Graph(off, keys) as G:
+            for m, H in ((1, 16), (7, 0), (0, 32)):
+                u, w, s, t = G.predict(m, H, k)
+                assert t["path"] == 4
+                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                assert_canonical_equal(eu, ew, es, u, w, s)
+                parts = []
+                for r in range(3):
+                    out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+                    n, _ = G.predict_device(m, H, k, out, span * r // 3, span * (r + 1) // 3)
+                    parts.append(out[:n])
+                allv = torch.cat(parts)
+                res = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+                kk = G.select_edges_device(allv, allv.shape[0], k, res)
+                u2, w2, s2 = gpu.edges_from_tensor(res, kk)
+                assert_canonical_equal(eu, ew, es, u2, w2, s2)
+
+
+def test_gpu_full_size_c2_large_hub_threshold(gpu, oracle, nlp):
+    """C2 stand-in at H = 16 (1.8e8 wedges, automatic routing to path 4) against
+    the oracle, for Jaccard and Adamic-Adar."""
+    import torch
+    import nlp_loader
+    gg = nlp_loader.load_sub("graphgen")
+    off_t, keys_t, du, dw, info = gg.make_workload("C2-soc-LiveJournal1", "cuda")
+    with gpu.Graph.from_device(off_t, keys_t) as G:
+        off = off_t.cpu().numpy().astype(np.uint64)
+        keys = keys_t.cpu().numpy().view(np.uint32)
+        k = info["k"]
+        out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+        for m in (1, 7):
+            n, t = G.predict_device(m, 16, k, out)
+            assert t["path"] == 4
+            u, w, s = gpu.edges_from_tensor(out, n)
+            eu, ew, es, oi = oracle.predict(off, keys, m, 16, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+            assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
