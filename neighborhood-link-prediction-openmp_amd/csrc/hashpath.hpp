@@ -41,10 +41,8 @@ constexpr uint64_t HP_B0_MAX = HP_WT / 2;   // bin 0: W(u) <= 512
 constexpr int HP_BNT = 1024;                // workgroup size of the block bins
 constexpr int HP_BT = 8192;                 // LDS table entries (bin 1)
 constexpr uint64_t HP_B1_MAX = HP_BT / 2;   // bin 1: W(u) <= 4096
-constexpr int HP_T2_LOG = 20;               // bin 2 global table entries per workgroup (log2)
-constexpr uint64_t HP_B2_MAX = 1ull << (HP_T2_LOG - 1);
-constexpr int HP_NBINS = 4;                 // bin 3: the rest (T up to HP_T3_LOG, w-range passes beyond)
-constexpr int HP_T3_LOG_MAX = 24;
+constexpr uint64_t HP_B2_MAX = 1ull << 19;  // bin 2: W(u) <= 2^19, bin 3: the rest (both k_hp_part)
+constexpr int HP_NBINS = 4;
 
 // per-chunk counters (u64)
 enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_NCTR = 8 };
@@ -63,6 +61,7 @@ struct HpArgs {
   uint64_t cap;       // free slots from base on
   const int64_t* tau; // emit only key > *tau
   unsigned long long* ctr;
+  int one_bucket;     // test hook (k_hp_part): one w-bucket per row
 };
 
 __device__ __forceinline__ bool hp_surv(uint32_t d, uint32_t H) { return d > 0 && (H == 0 || d <= H); }
@@ -584,6 +583,244 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   hp_finish(sg, a, wedges);
 }
 
+// ---------------------------------------------------------------- bins 2-3: partitioned rows
+// A row whose wedges overflow an LDS table is cut into P w-buckets of width
+// 2^shift (P <= HP_PMAX).  Pass A counts the row's wedges per bucket (LDS
+// histogram), pass B scatters them bucket by bucket into the workgroup's
+// scratch (w, and v for AA / RA), and every bucket is then accumulated in the
+// LDS table from its contiguous scratch range -- one streaming write and read
+// of the wedges instead of two global atomics each.  Buckets are processed in
+// ascending w, so the first-order exclusion walks N(u) with a single cursor.
+// Groups of buckets are formed so that a group's wedges fit the scratch; a
+// single bucket beyond the scratch is accumulated directly from the row
+// enumeration (rare: hub-hub concentrations).
+constexpr int HP_PMAX = 4096;
+
+// Row expansion shared by the passes: calls f(w, v) for every wedge (u, v, w)
+// with w > u, v surviving; every thread of the workgroup must call it.
+template <class F>
+__device__ __forceinline__ void hp_enum_row(const HpArgs& a, uint32_t u, uint64_t o0, uint64_t du, uint64_t* s_incl,
+                                            uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f) {
+  const int t = threadIdx.x;
+  for (uint64_t base = 0; base < du; base += HP_BNT) {
+    const uint64_t i = base + t;
+    uint32_t v = 0;
+    uint64_t len = 0, st = 0;
+    if (i < du) {
+      v = a.g.keys[o0 + i];
+      const uint32_t d = a.g.deg[v];
+      if (hp_surv(d, a.H)) {
+        len = d;
+        st = a.g.off[v];
+      }
+    }
+    const uint64_t incl = block_incl_scan_1024(len, s_w);
+    s_incl[t] = incl;
+    s_start[t] = st;
+    s_iv[t] = v;
+    if (t == HP_BNT - 1) *s_tot = incl;
+    __syncthreads();
+    const uint64_t total = *s_tot;
+    for (uint64_t j = t; j < total; j += HP_BNT) {
+      uint32_t lo = 0, hi = HP_BNT - 1;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (s_incl[m] > j) hi = m; else lo = m + 1;
+      }
+      const uint64_t ex = lo ? s_incl[lo - 1] : 0ull;
+      const uint32_t w = a.g.keys[s_start[lo] + (j - ex)];
+      if (w > u) f(w, s_iv[lo]);
+    }
+    __syncthreads();
+  }
+}
+
+// exclusive scan of s[0..n) in place (n <= HP_PMAX)
+__device__ __forceinline__ void hp_scan_buckets(uint32_t* s, uint32_t n, uint64_t* s_w) {
+  constexpr int PER = HP_PMAX / HP_BNT;
+  const int t = threadIdx.x;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t i = (uint32_t)t * PER + q;
+    v[q] = i < n ? s[i] : 0u;
+    sum += v[q];
+  }
+  const uint64_t incl = block_incl_scan_1024(sum, s_w);
+  uint32_t run = (uint32_t)(incl - sum);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t i = (uint32_t)t * PER + q;
+    if (i < n) s[i] = run;
+    run += v[q];
+  }
+  __syncthreads();
+}
+
+template <bool CUSTOM>
+__global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                    const uint64_t* __restrict__ wu, uint64_t ua,
+                                                    uint32_t* __restrict__ scratch, uint64_t scap) {
+  constexpr int LT = CUSTOM ? HP_BT / 2 : HP_BT;
+  constexpr int VT = CUSTOM ? LT : 1;
+  constexpr int NW = HP_BNT / 64;
+  constexpr int TL = CUSTOM ? 12 : 13;
+  __shared__ uint32_t s_k[LT];
+  __shared__ uint32_t s_c[LT];
+  __shared__ uint32_t s_v0[VT];
+  __shared__ uint32_t s_v1[VT];
+  __shared__ uint64_t s_incl[HP_BNT];
+  __shared__ uint64_t s_start[HP_BNT];
+  __shared__ uint32_t s_iv[HP_BNT];
+  __shared__ uint64_t s_w[NW];
+  __shared__ uint64_t s_tot;
+  __shared__ uint32_t s_bc[HP_PMAX];   // wedges per bucket
+  __shared__ uint32_t s_bo[HP_PMAX];   // scratch offset per bucket (group-relative), then scatter cursor
+  __shared__ uint32_t s_g1, s_gdirect, s_xcur;
+  __shared__ uint32_t s_gk[NW][HP_BSTG], s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ float s_gs[NW][HP_BSTG];
+  const int t = threadIdx.x, wv = wave_id();
+  const HpTable tb{s_k, s_c, s_v0, s_v1};
+  for (int i = t; i < LT; i += HP_BNT) {
+    s_k[i] = HP_EMPTY;
+    s_c[i] = 0;
+    if (CUSTOM) { s_v0[i] = HP_EMPTY; s_v1[i] = 0; }
+  }
+  uint32_t* sw = scratch + (uint64_t)blockIdx.x * scap * (CUSTOM ? 2 : 1);
+  uint32_t* sv = sw + scap;
+  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  __syncthreads();
+  for (uint64_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+    const uint32_t u = rows[ri];
+    const uint64_t W = wu[u - ua];
+    const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
+    const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
+    if (span_w == 0) continue;
+    // buckets: about 1024 wedges each, never narrower than needed
+    uint64_t pd = (W + 1023) / 1024;
+    const uint64_t pspan = (span_w + (LT / 2) - 1) / (LT / 2);
+    if (pd > pspan) pd = pspan;
+    if (a.one_bucket) pd = 1;  // test hook: one bucket per row (sub-range passes)
+    if (pd < 1) pd = 1;
+    if (pd > HP_PMAX) pd = HP_PMAX;
+    const int shift = log2_ceil((span_w + pd - 1) / pd);
+    const uint32_t P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
+    for (uint32_t b = t; b < P; b += HP_BNT) s_bc[b] = 0;
+    if (t == 0) {  // exclusion cursor: first entry of N(u) above u
+      uint64_t lo = 0, hi = du;
+      while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        if (a.g.keys[o0 + m] <= u) lo = m + 1; else hi = m;
+      }
+      s_xcur = (uint32_t)lo;
+    }
+    __syncthreads();
+    // pass A: wedges per bucket
+    hp_enum_row(a, u, o0, du, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t) {
+      ++wedges;
+      atomicAdd(&s_bc[(w - u - 1) >> shift], 1u);
+    });
+    for (uint32_t b0 = 0; b0 < P;) {
+      if (t == 0) {
+        uint64_t sum = 0;
+        uint32_t b = b0;
+        while (b < P && sum + s_bc[b] <= scap) sum += s_bc[b++];
+        s_gdirect = b == b0 ? 1u : 0u;
+        s_g1 = b == b0 ? b0 + 1 : b;
+      }
+      __syncthreads();
+      const uint32_t b1 = s_g1;
+      const bool direct = s_gdirect != 0;
+      if (!direct) {
+        // group offsets and pass B: scatter the group's wedges bucket by bucket
+        for (uint32_t b = t; b < b1 - b0; b += HP_BNT) s_bo[b] = s_bc[b0 + b];
+        __syncthreads();
+        hp_scan_buckets(s_bo, b1 - b0, s_w);
+        hp_enum_row(a, u, o0, du, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t v) {
+          const uint32_t b = (w - u - 1) >> shift;
+          if (b >= b0 && b < b1) {
+            const uint32_t p = atomicAdd(&s_bo[b - b0], 1u);
+            sw[p] = w;
+            if (CUSTOM) sv[p] = v;
+          }
+        });
+        hp_sync<true>();
+      }
+      // buckets of the group, ascending w
+      uint32_t boff = 0;
+      for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t nb = s_bc[b];
+        const uint32_t off = boff;
+        boff += nb;
+        if (nb == 0) continue;
+        const uint64_t lo = (uint64_t)u + 1 + ((uint64_t)b << shift);
+        const uint64_t hi = lo + (1ull << shift) < a.S ? lo + (1ull << shift) : a.S;
+        const uint64_t width = hi - lo;
+        const uint64_t need = 2 * ((uint64_t)nb < width ? (uint64_t)nb : width);
+        int lg = max(6, log2_ceil(need));
+        uint64_t sub = 1;
+        if (lg > TL) {
+          sub = (2 * width + (1ull << TL) - 1) >> TL;
+          lg = TL;
+        }
+        const uint32_t T = 1u << lg, mask = T - 1;
+        const int hs = 32 - lg;
+        const uint64_t sw_w = (width + sub - 1) / sub;
+        for (uint64_t q = 0; q < sub; ++q) {
+          const uint64_t slo = lo + q * sw_w;
+          const uint64_t shi = slo + sw_w < hi ? slo + sw_w : hi;
+          if (!direct) {
+            for (uint32_t i = t; i < nb; i += HP_BNT) {
+              const uint32_t w = sw[off + i];
+              if (sub == 1 || ((uint64_t)w >= slo && (uint64_t)w < shi))
+                hp_insert<false, CUSTOM>(tb, mask, hs, w, CUSTOM ? sv[off + i] : 0u, &a.ctr[HPC_ERR]);
+            }
+            __syncthreads();
+          } else {
+            hp_enum_row(a, u, o0, du, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t v) {
+              if ((uint64_t)w >= slo && (uint64_t)w < shi) hp_insert<false, CUSTOM>(tb, mask, hs, w, v, &a.ctr[HPC_ERR]);
+            });
+          }
+          // first-order exclusion: the entries of N(u) in [slo, shi) (cursor walk)
+          for (;;) {
+            const uint32_t xc = s_xcur;
+            const uint64_t i = (uint64_t)xc + t;
+            bool in = false;
+            if (i < du) {
+              const uint32_t x = a.g.keys[o0 + i];
+              in = (uint64_t)x < shi;
+              if (in) hp_mark<false>(tb, mask, hs, x);
+            }
+            const uint64_t m = __ballot(in);
+            if (lane_id() == 0) s_w[wv] = (uint64_t)__popcll(m);
+            __syncthreads();
+            uint32_t adv = 0;
+            for (int q2 = 0; q2 < NW; ++q2) adv += (uint32_t)s_w[q2];
+            __syncthreads();
+            if (t == 0) s_xcur = xc + adv;
+            __syncthreads();
+            if (adv < HP_BNT) break;
+          }
+          __syncthreads();
+          for (uint32_t i = t; i < T; i += HP_BNT) {
+            uint32_t c = 0, v0 = 0, v1 = 0;
+            const uint32_t w = hp_take<false, CUSTOM>(tb, i, &c, &v0, &v1);
+            const bool valid = w != HP_EMPTY;
+            const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
+            hp_emit(sg, a, valid, s, u, w, tau);
+          }
+          __syncthreads();
+        }
+      }
+      b0 = b1;
+    }
+    __syncthreads();  // the next row rewrites s_bc / s_xcur
+  }
+  hp_finish(sg, a, wedges);
+}
+
 // ---------------------------------------------------------------- pruning between chunks
 // Split the candidate buffer around the k-th key (sel[3] from the radix
 // select): keys above go to the target columns (unordered), ties to a list of
@@ -660,10 +897,5 @@ __global__ void k_hp_permute(const uint32_t* __restrict__ idx, uint64_t n, const
   }
 }
 
-__global__ void k_hp_fill_slab(uint32_t* __restrict__ slab, uint64_t nblk, uint64_t tmax) {
-  const uint64_t n = nblk * tmax * 4;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    slab[i] = ((i / tmax) % 2) == 0 ? HP_EMPTY : 0u;  // keys, vmin empty; counts, vmax 0
-}
 
 }  // namespace nlp

@@ -169,15 +169,16 @@ struct nlp_graph {
   std::vector<Cached> graphs;
   uint64_t use_clock = 0;
   // hash path: per-workgroup global tables of bins 2 and 3 (kept clean between calls)
-  uint32_t* hp_slab2 = nullptr;
-  uint32_t* hp_slab3 = nullptr;
-  unsigned hp_g2 = 0, hp_g3 = 0;
-  int hp_t3log = 0;
+  uint32_t* hp_scratch = nullptr;              // k_hp_part: per-workgroup wedge scratch (w and v)
+  unsigned hp_gp = 0;                          // workgroups of k_hp_part
+  uint64_t hp_scap = 0;                        // scratch words per workgroup and array
   uint64_t hp_min_wedges = 1ull << 23;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 3 runs
   int hash_mode = 0;                           // NLP_HASH: 0 auto, 1 always, -1 never
-  // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_T3LOG
+  // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_SCAP
+  // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
   uint64_t hp_emit = 0;
-  int hp_minbin = 0, hp_t3log_force = 0;
+  int hp_minbin = 0, hp_one_bucket = 0;
+  uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
   uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
 };
@@ -240,8 +241,7 @@ void destroy_graph(nlp_graph* g) {
       if (x) (void)hipGraphExecDestroy(x);
   g->graphs.clear();
   if (g->d_stamp) (void)hipFree(g->d_stamp);
-  if (g->hp_slab2) (void)hipFree(g->hp_slab2);
-  if (g->hp_slab3) (void)hipFree(g->hp_slab3);
+  if (g->hp_scratch) (void)hipFree(g->hp_scratch);
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -420,7 +420,8 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hw = getenv("NLP_HASH_MIN_WEDGES")) g->hp_min_wedges = strtoull(hw, nullptr, 10);
   if (const char* he = getenv("NLP_HASH_EMIT")) g->hp_emit = strtoull(he, nullptr, 10);
   if (const char* hb = getenv("NLP_HASH_MINBIN")) g->hp_minbin = std::min(3, std::max(0, atoi(hb)));
-  if (const char* ht = getenv("NLP_HASH_T3LOG")) g->hp_t3log_force = std::min(HP_T3_LOG_MAX, std::max(6, atoi(ht)));
+  if (const char* hc = getenv("NLP_HASH_SCAP")) g->hp_scap_force = std::max<uint64_t>(64, strtoull(hc, nullptr, 10));
+  if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* gr = getenv("NLP_GROUPING")) {
@@ -1036,24 +1037,17 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
 // LDS / global hash tables, candidates emitted unordered above the running
 // threshold tau and pruned to the canonical top k between chunks of rows.
 
-// Global tables of bins 2 and 3, allocated once and kept clean (every row
-// resets the entries it used).
-nlp_status hp_slabs(nlp_graph* g, hipStream_t st) {
-  if (g->hp_slab2 && g->hp_slab3) return NLP_OK;
+// Wedge scratch of k_hp_part (bins 2 and 3), allocated once per graph: 2 x
+// hp_scap words per workgroup (w and, for AA / RA, v).
+nlp_status hp_alloc_scratch(nlp_graph* g) {
+  if (g->hp_scratch) return NLP_OK;
   size_t fr = 0, tot = 0;
   TRY(hipMemGetInfo(&fr, &tot));
-  const uint64_t budget = fr / 16;  // both slabs together
-  g->hp_t3log = g->hp_t3log_force ? g->hp_t3log_force
-                                  : std::min(HP_T3_LOG_MAX, std::max(HP_T2_LOG, log2_host(2 * g->span)));
-  const uint64_t per2 = (1ull << HP_T2_LOG) * 16, per3 = (1ull << g->hp_t3log) * 16;  // 4 u32 per entry
-  g->hp_g2 = (unsigned)std::max<uint64_t>(16, std::min<uint64_t>(256, budget / 2 / per2));
-  g->hp_g3 = (unsigned)std::max<uint64_t>(4, std::min<uint64_t>(64, budget / 2 / per3));
-  TRY(hipMalloc(&g->hp_slab2, g->hp_g2 * per2));
-  TRY(hipMalloc(&g->hp_slab3, g->hp_g3 * per3));
-  hipLaunchKernelGGL(k_hp_fill_slab, dim3(4096), dim3(NT), 0, st, g->hp_slab2, (uint64_t)g->hp_g2, 1ull << HP_T2_LOG);
-  hipLaunchKernelGGL(k_hp_fill_slab, dim3(4096), dim3(NT), 0, st, g->hp_slab3, (uint64_t)g->hp_g3,
-                     1ull << g->hp_t3log);
-  TRY(hipGetLastError());
+  g->hp_gp = 256;
+  uint64_t scap = g->hp_scap_force ? g->hp_scap_force : (1ull << 21);
+  while (scap > 4096 && (uint64_t)g->hp_gp * scap * 8 > fr / 16) scap >>= 1;
+  g->hp_scap = scap;
+  TRY(hipMalloc(&g->hp_scratch, (uint64_t)g->hp_gp * scap * 8));
   return NLP_OK;
 }
 
@@ -1194,7 +1188,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t k = p.max_edges;
   *nchunks = 0;
   if (nU == 0 || g->nnz == 0) return NLP_OK;
-  { nlp_status s0 = hp_slabs(g, st); if (s0 != NLP_OK) return s0; }
+  { nlp_status s0 = hp_alloc_scratch(g); if (s0 != NLP_OK) return s0; }
   uint64_t *wu, *pos, *small;
   uint8_t* flags;
   TRY(wsget(ws, B_HP_WU, nU + 1, &wu));
@@ -1265,7 +1259,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.cap = capC - C.n;
     a.tau = (const int64_t*)(small + 8);
     a.ctr = (unsigned long long*)small;
-    const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1], n2 = q1[2] - q0[2], n3 = q1[3] - q0[3];
+    a.one_bucket = g->hp_one_bucket;
+    const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     if (n0) {
       const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
       if (custom) hipLaunchKernelGGL(k_hp_wave<true>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
@@ -1278,16 +1273,12 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13);
       TRY(hipGetLastError());
     }
-    if (n2) {
-      const unsigned gr = (unsigned)std::min<uint64_t>(n2, g->hp_g2);
-      if (custom) hipLaunchKernelGGL((k_hp_block<true, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[2] + q0[2], n2, wu, ua, g->hp_slab2, HP_T2_LOG);
-      else hipLaunchKernelGGL((k_hp_block<false, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[2] + q0[2], n2, wu, ua, g->hp_slab2, HP_T2_LOG);
-      TRY(hipGetLastError());
-    }
-    if (n3) {
-      const unsigned gr = (unsigned)std::min<uint64_t>(n3, g->hp_g3);
-      if (custom) hipLaunchKernelGGL((k_hp_block<true, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[3] + q0[3], n3, wu, ua, g->hp_slab3, g->hp_t3log);
-      else hipLaunchKernelGGL((k_hp_block<false, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[3] + q0[3], n3, wu, ua, g->hp_slab3, g->hp_t3log);
+    for (int b = 2; b < HP_NBINS; ++b) {  // rows beyond an LDS table: w-bucket partitioning
+      const uint64_t nb = q1[b] - q0[b];
+      if (!nb) continue;
+      const unsigned gr = (unsigned)std::min<uint64_t>(nb, g->hp_gp);
+      if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap);
+      else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap);
       TRY(hipGetLastError());
     }
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));

@@ -375,10 +375,12 @@ class _env:
                 os.environ[k] = v
 
 
-# path 4 (hash accumulation) with every bin forced: 0 wave/LDS, 1 workgroup/LDS,
-# 2 workgroup/global slab, 3 workgroup/global slab with w-range passes (tiny slab)
+# path 4 (hash accumulation) with every kernel forced: 0 wave/LDS, 1 workgroup/LDS,
+# 2 w-bucket partitioning, 3 partitioning with a tiny scratch (bucket groups and
+# direct accumulation), 4 one bucket per row (sub-range passes)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
-                 dict(NLP_HASH_MINBIN="3", NLP_HASH_T3LOG="6")]
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
@@ -427,7 +429,7 @@ def test_gpu_hash_path_all_candidates_and_min_score(gpu, golden, oracle):
 def test_gpu_hash_path_star_hub(gpu, oracle):
     """A hub source whose row holds > 10^4 distinct second hops (bins 2 and 3)."""
     off, keys = star_csr(20000)
-    for v in (dict(), dict(NLP_HASH_T3LOG="8")):
+    for v in (dict(), dict(NLP_HASH_SCAP="5000"), dict(NLP_HASH_ONE_BUCKET="1")):
         with _env(NLP_HASH="1", **v):
             with gpu.Graph(off, keys) as G:
                 for m, H, k in ((0, 0, 500), (7, 0, 30000), (1, 2, 10 ** 6), (8, 4, 100)):
