@@ -38,6 +38,7 @@ constexpr uint32_t HP_EXCL = 0x80000000u;   // count bit: w in N(u) (first-order
 constexpr uint32_t HP_CMASK = 0x7fffffffu;
 constexpr int HP_WT = 1024;                 // wave table entries (bin 0)
 constexpr uint64_t HP_B0_MAX = HP_WT / 2;   // bin 0: W(u) <= 512
+constexpr uint64_t HP_B0_DEG = 1024;        //        and deg(u) <= 1024
 constexpr int HP_BNT = 1024;                // workgroup size of the block bins
 constexpr int HP_BT = 8192;                 // LDS table entries (bin 1)
 constexpr uint64_t HP_B1_MAX = HP_BT / 2;   // bin 1: W(u) <= 4096
@@ -301,26 +302,94 @@ __global__ void k_sum_deg2_above(const uint32_t* __restrict__ deg, uint64_t S, u
 }
 
 // ---------------------------------------------------------------- binning
-// Wave per source row: W(u) = sum of deg v over surviving v in N(u) (an upper
-// bound of the row's wedges; w > u is not applied), the row's bin, and one
-// flag byte per bin for the stable partition.  b1max: largest W of bin 1.
-__global__ __launch_bounds__(NT) void k_hp_work(GraphView g, uint32_t H, uint64_t ua, uint64_t nU,
-                                                uint64_t* __restrict__ wu, uint8_t* __restrict__ flags, int minbin,
-                                                uint64_t b1max) {
-  const uint64_t r = (uint64_t)blockIdx.x * NWAVE + wave_id();
-  if (r >= nU) return;
-  const int lane = lane_id();
-  const uint64_t u = ua + r;
-  const uint64_t o0 = g.off[u], o1 = g.off[u + 1];
-  uint64_t s = 0;
-  for (uint64_t i = o0 + lane; i < o1; i += 64) {
-    const uint32_t d = g.deg[g.keys[i]];
-    if (hp_surv(d, H)) s += d;
+// W(u) = sum of deg v over surviving v in N(u): an upper bound of the row's
+// wedges (w > u is not applied).  Edge-parallel, so hub rows cost no more than
+// their entries: a wave takes HP_WR x 64 consecutive adjacency entries
+// (coalesced keys, HP_WR independent degree gathers per lane in flight),
+// locates each entry's row among the next 64 row ends (held one per lane,
+// searched with lane permutes), sums per row in LDS and adds each row's
+// partial sum with one global atomic.  wu must be zeroed first.
+constexpr int HP_WR = 8;
+constexpr uint64_t HP_WTILE = 64 * HP_WR;  // adjacency entries per wave tile
+
+// Per graph: the row of the first entry of every wave tile (tile_row[t] = the
+// row u with off[u] <= t * HP_WTILE < off[u + 1]), so that a tile finds its
+// rows without a search.
+__global__ void k_hp_tile_rows(const uint64_t* __restrict__ off, uint64_t S, uint32_t* __restrict__ tile_row) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < S; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = off[u], b = off[u + 1];
+    for (uint64_t t = (a + HP_WTILE - 1) / HP_WTILE; t * HP_WTILE < b; ++t) tile_row[t] = (uint32_t)u;
   }
-  s = wave_sum(s);
-  if (lane == 0) {
-    wu[r] = s;
-    int b = s == 0 ? -1 : s <= HP_B0_MAX ? 0 : s <= b1max ? 1 : s <= HP_B2_MAX ? 2 : 3;
+}
+
+__global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, uint64_t ua, uint64_t nU, uint64_t e0,
+                                                      uint64_t e1, const uint32_t* __restrict__ tile_row,
+                                                      unsigned long long* __restrict__ wu) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  s_acc[wv][lane] = 0;
+  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t tr = tile_row[tile];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;  // first row of the tile inside the range
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < nU ? g.off[ua + rl + 1] : ~0ull;  // end of row r0 + lane
+    const uint64_t last_end = __shfl(rend, 63, 64);
+    uint32_t c[HP_WR];
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      c[i] = 0;
+      if (e >= e0 && e < e1) {
+        const uint32_t d = g.deg[g.keys[e]];
+        c[i] = hp_surv(d, H) ? d : 0u;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      // local row: the number of the 64 row ends <= e (every lane searches: lane permutes)
+      int lo = 0, hi = 64;
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        const uint64_t v = __shfl(rend, m, 64);
+        if (v <= e) lo = m + 1; else hi = m;
+      }
+      if (c[i] == 0) continue;
+      if (e < last_end) {
+        atomicAdd(&s_acc[wv][lo], (unsigned long long)c[i]);
+      } else {  // more than 64 rows in this tile: search the offsets
+        uint64_t a = r0, b = nU;
+        while (b - a > 1) {
+          const uint64_t m = (a + b) >> 1;
+          if (g.off[ua + m] <= e) a = m; else b = m;
+        }
+        atomicAdd(&wu[a], (unsigned long long)c[i]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const unsigned long long v = s_acc[wv][lane];
+    if (v) {
+      atomicAdd(&wu[rl], v);
+      s_acc[wv][lane] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
+}
+
+// The row's bin from W(u) and its degree (a wave walks N(u) in bin 0, so bin 0
+// also bounds the degree), and one flag byte per bin for the stable partition.
+__global__ __launch_bounds__(NT) void k_hp_bin(const uint64_t* __restrict__ off, uint64_t ua, uint64_t nU,
+                                               const uint64_t* __restrict__ wu, uint8_t* __restrict__ flags, int minbin,
+                                               uint64_t b1max) {
+  for (uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x; r < nU; r += (uint64_t)gridDim.x * NT) {
+    const uint64_t s = wu[r], du = off[ua + r + 1] - off[ua + r];
+    int b = s == 0 ? -1 : (s <= HP_B0_MAX && du <= HP_B0_DEG) ? 0 : s <= b1max ? 1 : s <= HP_B2_MAX ? 2 : 3;
     if (b >= 0 && b < minbin) b = minbin;  // test hook: route rows to a larger bin
 #pragma unroll
     for (int q = 0; q < HP_NBINS; ++q) flags[(uint64_t)q * nU + r] = b == q ? 1 : 0;
@@ -825,38 +894,55 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
 // Split the candidate buffer around the k-th key (sel[3] from the radix
 // select): keys above go to the target columns (unordered), ties to a list of
 // (u << 32 | w) records with their index, to be ordered canonically.
+constexpr int HP_SPLIT_IPL = 16;  // elements per lane: one wave-tile = 1024 candidates, two atomics
+
 __global__ __launch_bounds__(NT) void k_hp_split(const uint32_t* __restrict__ key, const uint32_t* __restrict__ u,
                                                  const uint32_t* __restrict__ w, const float* __restrict__ s, uint64_t n,
                                                  const uint64_t* __restrict__ sel, uint32_t* __restrict__ okey,
                                                  uint32_t* __restrict__ ou, uint32_t* __restrict__ ow,
                                                  float* __restrict__ os, uint64_t* __restrict__ tie_k,
                                                  uint32_t* __restrict__ tie_i, unsigned long long* __restrict__ cnt) {
+  constexpr uint64_t WT = 64 * HP_SPLIT_IPL;
   const uint32_t kth = (uint32_t)sel[3];
   const int lane = lane_id();
-  for (uint64_t i0 = (uint64_t)blockIdx.x * NT; i0 < n; i0 += (uint64_t)gridDim.x * NT) {
-    const uint64_t i = i0 + threadIdx.x;
-    const uint32_t k = i < n ? key[i] : 0u;
-    const bool above = i < n && k > kth, tie = i < n && k == kth;
-    const uint64_t ma = __ballot(above), mt = __ballot(tie);
-    const int leader = __ffsll((long long)(ma | mt | 1ull)) - 1;
-    unsigned long long pa = 0, pt = 0;
-    if (lane == leader) {
-      if (ma) pa = atomicAdd(&cnt[0], (unsigned long long)__popcll(ma));
-      if (mt) pt = atomicAdd(&cnt[1], (unsigned long long)__popcll(mt));
+  const uint64_t below = (1ull << lane) - 1;
+  const uint64_t nwt = (n + WT - 1) / WT;
+  for (uint64_t wt = (uint64_t)blockIdx.x * NWAVE + wave_id(); wt < nwt; wt += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = wt * WT;
+    uint32_t k[HP_SPLIT_IPL];
+    uint32_t na = 0, nt = 0;
+#pragma unroll
+    for (int r = 0; r < HP_SPLIT_IPL; ++r) {
+      const uint64_t i = base + (uint64_t)r * 64 + lane;
+      k[r] = i < n ? key[i] : 0u;
+      na += (uint32_t)__popcll(__ballot(i < n && k[r] > kth));
+      nt += (uint32_t)__popcll(__ballot(i < n && k[r] == kth));
     }
-    pa = __shfl(pa, leader, 64);
-    pt = __shfl(pt, leader, 64);
-    const uint64_t below = (1ull << lane) - 1;
-    if (above) {
-      const uint64_t q = pa + __popcll(ma & below);
-      okey[q] = k;
-      ou[q] = u[i];
-      ow[q] = w[i];
-      os[q] = s[i];
-    } else if (tie) {
-      const uint64_t q = pt + __popcll(mt & below);
-      tie_k[q] = ((uint64_t)u[i] << 32) | w[i];
-      tie_i[q] = (uint32_t)i;
+    unsigned long long pa = 0, pt = 0;
+    if (lane == 0) {
+      if (na) pa = atomicAdd(&cnt[0], (unsigned long long)na);
+      if (nt) pt = atomicAdd(&cnt[1], (unsigned long long)nt);
+    }
+    pa = __shfl(pa, 0, 64);
+    pt = __shfl(pt, 0, 64);
+#pragma unroll
+    for (int r = 0; r < HP_SPLIT_IPL; ++r) {
+      const uint64_t i = base + (uint64_t)r * 64 + lane;
+      const bool above = i < n && k[r] > kth, tie = i < n && k[r] == kth;
+      const uint64_t ma = __ballot(above), mt = __ballot(tie);
+      if (above) {
+        const uint64_t q = pa + __popcll(ma & below);
+        okey[q] = k[r];
+        ou[q] = u[i];
+        ow[q] = w[i];
+        os[q] = s[i];
+      } else if (tie) {
+        const uint64_t q = pt + __popcll(mt & below);
+        tie_k[q] = ((uint64_t)u[i] << 32) | w[i];
+        tie_i[q] = (uint32_t)i;
+      }
+      pa += __popcll(ma);
+      pt += __popcll(mt);
     }
   }
 }

@@ -170,9 +170,10 @@ struct nlp_graph {
   uint64_t use_clock = 0;
   // hash path: per-workgroup global tables of bins 2 and 3 (kept clean between calls)
   uint32_t* hp_scratch = nullptr;              // k_hp_part: per-workgroup wedge scratch (w and v)
+  uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
   unsigned hp_gp = 0;                          // workgroups of k_hp_part
   uint64_t hp_scap = 0;                        // scratch words per workgroup and array
-  uint64_t hp_min_wedges = 1ull << 23;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 3 runs
+  uint64_t hp_min_wedges = 1ull << 24;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 4 runs
   int hash_mode = 0;                           // NLP_HASH: 0 auto, 1 always, -1 never
   // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_SCAP
   // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
@@ -242,6 +243,7 @@ void destroy_graph(nlp_graph* g) {
   g->graphs.clear();
   if (g->d_stamp) (void)hipFree(g->d_stamp);
   if (g->hp_scratch) (void)hipFree(g->hp_scratch);
+  if (g->tile_row) (void)hipFree(g->tile_row);
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -383,6 +385,11 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipGetLastError());
     TRY(hipStreamSynchronize(st));
   }
+  // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
+  TRY(hipMalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
+  TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
+  LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
+  TRY(hipGetLastError());
   // AA / RA contribution tables, computed on the host with the same libm the
   // reference uses (glibc log), indexed by degree.
   std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
@@ -435,7 +442,9 @@ nlp_status finish_graph(nlp_graph* g) {
     auto occ = [&](const void* k, unsigned* out) -> hipError_t {
       int nb = 0;
       hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, NT, 0);
-      if (e == hipSuccess) *out = cus * (unsigned)std::max(nb, 1);
+      // half of the reported residency: the blockIdx-ordered persistent scans
+      // deadlock (look-back timeout) if any of their workgroups is not resident
+      if (e == hipSuccess) *out = cus * (unsigned)std::max(nb / 2, 1);
       return e;
     };
     TRY(occ((const void*)k_sp_survivors<>, &g->occ_surv));
@@ -1089,7 +1098,9 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   TRY(wsget(ws, B_TS, std::max<uint64_t>(cap, 1), &ns));
   TRY(wsget(ws, B_HP_TIEK0, n, &tk0));
   TRY(wsget(ws, B_HP_TIEI0, n, &ti0));
-  LAUNCH(k_hp_split, n, st, ckey, cu, cw, cs, n, sel, nk, nu, nw, ns, tk0, ti0, (unsigned long long*)(small + 40));
+  hipLaunchKernelGGL(k_hp_split, dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>(n / (NT * HP_SPLIT_IPL), 1), 4096)),
+                     dim3(NT), 0, st, ckey, cu, cw, cs, n, sel, nk, nu, nw, ns, tk0, ti0,
+                     (unsigned long long*)(small + 40));
   TRY(hipGetLastError());
   TRY(hipMemcpyAsync(&h[16], sel, 32, hipMemcpyDeviceToHost, st));
   TRY(hipMemcpyAsync(&h[20], small + 40, 16, hipMemcpyDeviceToHost, st));
@@ -1199,9 +1210,22 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
   // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
   const GraphView gv = view_of(g, p.metric);
-  hipLaunchKernelGGL(k_hp_work, dim3((unsigned)((nU + NWAVE - 1) / NWAVE)), dim3(NT), 0, st, gv, p.H, ua, nU, wu, flags,
-                     g->hp_minbin, (uint64_t)(custom ? HP_BT / 4 : HP_B1_MAX));
-  TRY(hipGetLastError());
+  {
+    TRY(hipMemsetAsync(wu, 0, nU * 8, st));
+    TRY(hipMemcpyAsync(&g->host_small[8], g->off + ua, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipMemcpyAsync(&g->host_small[9], g->off + ub, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t e0 = g->host_small[8], e1 = g->host_small[9];
+    const uint64_t b1max = custom ? HP_BT / 4 : HP_B1_MAX;
+    if (e1 > e0)
+      hipLaunchKernelGGL(k_hp_work_edges,
+                         dim3((unsigned)std::min<uint64_t>((e1 - e0 + NT * HP_WR - 1) / (NT * HP_WR) + 1, 8192)),
+                         dim3(NT), 0, st, gv, p.H, ua, nU, e0, e1, (const uint32_t*)g->tile_row,
+                         (unsigned long long*)wu);
+    hipLaunchKernelGGL(k_hp_bin, dim3(grid_for(nU)), dim3(NT), 0, st, (const uint64_t*)g->off, ua, nU,
+                       (const uint64_t*)wu, flags, g->hp_minbin, b1max);
+    TRY(hipGetLastError());
+  }
   uint32_t* lists[HP_NBINS];
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
   for (int b = 0; b < HP_NBINS; ++b) {
@@ -1915,6 +1939,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   // wedge count of the previous call (one more pass, then the full LSD sort,
   // when a fine bucket is still above the LDS capacity)
   int msd_passes = g->last_wedges > (256u << 10) ? 2 : 1;
+  // size the record buffers from the wedge estimate up front (an overflow costs a rerun)
+  if (sorted) {
+    const double est = hp_estimate(g, p);
+    if (est * 1.1 > (double)g->capW && est * 1.1 < (double)SP_MAX_N) g->capW = (uint64_t)(est * 1.1) + 1024;
+  }
   for (int attempt = 0; attempt < 4; ++attempt) {
     if (sorted && g->capW > SP_MAX_N) return NLP_OK;
     EdgeOut* out = d_out;
@@ -1942,7 +1971,13 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     TRY(wait_event(E[2]));
     if (hprof) t3 = now_us();
     const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;
-    if (h[C_FLAGS] >> 32) return NLP_ERR_DEVICE;  // look-back timeout
+    if (h[C_FLAGS] >> 32) {  // look-back timeout
+      if (debug_on())
+        fprintf(stderr, "nlp: look-back timeout, flags %llx W %llu C %llu msd %d passes %d\n",
+                (unsigned long long)h[C_FLAGS], (unsigned long long)h[C_W], (unsigned long long)h[C_C], (int)msd,
+                msd_passes);
+      return NLP_ERR_DEVICE;
+    }
     if (h[C_FLAGS] & F_OVERFLOW) {
       const uint64_t W = h[C_W];
       if (!sorted) {  // the grouping did not run: its counters are dirty
@@ -2021,8 +2056,12 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
                         hipStream_t st, EdgeOut** result) {
   // path 3 (hash accumulation) once the wedge count is large: bounded memory,
   // no wedge materialisation (NLP_HASH=1 forces it, NLP_HASH=0 disables it)
+  // Adamic-Adar / Resource-Allocation stay on the sort paths unless forced: their
+  // ordered sums of three or more contributions re-walk intersections in path 4
+  const bool custom = p.metric == M_AA || p.metric == M_RA;
   const bool use_hash = !g->force_radix && p.max_edges > 0 &&
-                        (g->hash_mode > 0 || (g->hash_mode == 0 && hp_estimate(g, p) > (double)g->hp_min_wedges));
+                        (g->hash_mode > 0 ||
+                         (g->hash_mode == 0 && !custom && hp_estimate(g, p) > (double)g->hp_min_wedges));
   if (!use_hash && (p.H > 0 || g->sort_grouping) && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
     bool handled = false;
     nlp_status s = predict_fast(g, p, d_out, out_count, t, st, result, &handled);
