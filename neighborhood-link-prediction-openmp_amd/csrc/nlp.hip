@@ -152,6 +152,9 @@ struct nlp_graph {
   bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
   int group_sort = 2;                          // NLP_GROUP_SORT: 0 k_sp_bucket sort-only, 1 k_sp_group, 2 group only after 2 MSD passes
   uint64_t last_wedges = 0;                    // wedges of the previous fast call (sizes the MSD passes)
+  double last_ok_w = 0;                        // wedge estimate of the last successful sort-path call
+  bool last_ok_msd = true;                     //   and its grouping (MSD bucket passes or full LSD sort)
+  int last_ok_passes = 1;
   bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
   bool graph_single = true;                    // NLP_GRAPH_SEGMENTS=1: four graph segments with host events
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
@@ -173,7 +176,7 @@ struct nlp_graph {
   uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
   unsigned hp_gp = 0;                          // workgroups of k_hp_part
   uint64_t hp_scap = 0;                        // scratch words per workgroup and array
-  uint64_t hp_min_wedges = 1ull << 24;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 4 runs
+  uint64_t hp_min_wedges = 1ull << 26;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 4 runs
   int hash_mode = 0;                           // NLP_HASH: 0 auto, 1 always, -1 never
   // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_SCAP
   // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
@@ -1939,9 +1942,16 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   // wedge count of the previous call (one more pass, then the full LSD sort,
   // when a fine bucket is still above the LDS capacity)
   int msd_passes = g->last_wedges > (256u << 10) ? 2 : 1;
+  // start from the grouping that succeeded last time for a similar wedge count
+  // (each failed attempt costs a full pipeline run)
+  const double est_w = hp_estimate(g, p);
+  if (msd && g->last_ok_w > 0 && est_w < 2.0 * (double)g->last_ok_w && est_w > 0.5 * (double)g->last_ok_w) {
+    msd = g->last_ok_msd;
+    msd_passes = g->last_ok_passes;
+  }
   // size the record buffers from the wedge estimate up front (an overflow costs a rerun)
   if (sorted) {
-    const double est = hp_estimate(g, p);
+    const double est = est_w;
     if (est * 1.1 > (double)g->capW && est * 1.1 < (double)SP_MAX_N) g->capW = (uint64_t)(est * 1.1) + 1024;
   }
   for (int attempt = 0; attempt < 4; ++attempt) {
@@ -1994,6 +2004,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       continue;
     }
     g->last_wedges = h[C_W];
+    if (sorted && !(h[C_FLAGS] & F_TOOBIG)) {
+      g->last_ok_w = est_w;
+      g->last_ok_msd = msd;
+      g->last_ok_passes = msd_passes;
+    }
     if ((h[C_FLAGS] & F_TOOBIG) || h[C_W] > g->wedge_budget) return NLP_OK;
     *out_count = h[C_OUT_N];
     if (result) *result = out;
@@ -2032,9 +2047,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       hp.launch += t2 - t1;
       hp.wait += t3 - t2;
       hp.post += now_us() - t3;
-      if (++hp.n == 100) {
-        fprintf(stderr, "nlp host us/call: prepare %.1f launch %.1f wait %.1f post %.1f\n", hp.prep / 100,
-                hp.launch / 100, hp.wait / 100, hp.post / 100);
+      static const int every = std::max(1, atoi(getenv("NLP_HOSTPROF")));
+      if (++hp.n == every) {
+        fprintf(stderr, "nlp host us/call: prepare %.1f launch %.1f wait %.1f post %.1f (replayed %d)\n",
+                hp.prep / every, hp.launch / every, hp.wait / every, hp.post / every, (int)replayed);
         hp = HostProf();
       }
     }
