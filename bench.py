@@ -37,15 +37,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def f1_on_device(out, n, du, dw, span):
-    """main.cxx:48-57,199-206: P = |ins1 ∩ del0| / |ins1|, R = ... / |del0|."""
-    e = out[:n].long()
-    u, v = e[:, 0] & 0xffffffff, e[:, 1] & 0xffffffff
-    ins = torch.unique(torch.cat([u * span + v, v * span + u]))
-    dels = torch.unique(du.long() * span + dw.long())
-    common = int(torch.isin(ins, dels).sum())
-    p = common / max(ins.numel(), 1)
-    r = common / max(dels.numel(), 1)
+def f1_on_device(G, out, n, du, dw):
+    """main.cxx:48-57,199-206: P = |ins1 ∩ del0| / |ins1|, R = ... / |del0|, with
+    |ins1 ∩ del0| counted by the library's evaluation kernel (nlp_set_truth,
+    nlp_count_common_device); |ins1| = 2n (both directions of n distinct links)."""
+    G.set_truth(du.cpu().numpy().astype(np.uint32), dw.cpu().numpy().astype(np.uint32))
+    common = G.count_common_device(out, n)
+    p = common / max(2 * n, 1)
+    r = common / max(int(du.numel()), 1)
     return p, r, (0.0 if p + r == 0 else 2 * p * r / (p + r))
 
 
@@ -189,7 +188,7 @@ def main():
     value = cnt / (elapsed / args.steps)
 
     if rank == 0:
-        p, r, f1 = f1_on_device(out, cnt, du, dw, span)
+        p, r, f1 = f1_on_device(G, out, cnt, du, dw)
         score_ms /= args.steps
         select_ms /= args.steps
         # Roofline of the dominant kernel, k_group_tiles: its

@@ -146,6 +146,19 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
 nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,
                                    nlp_edge* d_out, uint64_t* out_count, void* stream);
 
+/* Evaluation of main.cxx:48-57 on the device.  nlp_set_truth
+ * keeps the directed deletions (main.cxx `deletions0`, both directions, host
+ * arrays; sorted and deduplicated here) on the handle's device.
+ * nlp_count_common_device counts |insertions1 ∩ deletions0| for `n` device
+ * edges: both directions of every predicted link (directedInsertions,
+ * main.cxx:111-119) looked up in the truth set; then precision =
+ * common / (2 n) and recall = common / |deletions0| (main.cxx:199-201).
+ * nlp_last_common does the same for the last prediction made on the handle. */
+nlp_status nlp_set_truth(nlp_graph* g, const uint32_t* u, const uint32_t* v, uint64_t n);
+nlp_status nlp_count_common_device(nlp_graph* g, const nlp_edge* d_edges, uint64_t n, uint64_t* common,
+                                   void* stream);
+nlp_status nlp_last_common(nlp_graph* g, uint64_t* common);
+
 const char* nlp_status_string(nlp_status s);
 const char* nlp_metric_name(nlp_metric m);
 

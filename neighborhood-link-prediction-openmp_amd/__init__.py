@@ -57,7 +57,8 @@ class Timing(ctypes.Structure):
 
 EXPORTS = [
     "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
-    "nlp_predict_device", "nlp_select_edges_device", "nlp_status_string", "nlp_metric_name", "nlp_version",
+    "nlp_predict_device", "nlp_select_edges_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common",
+    "nlp_status_string", "nlp_metric_name", "nlp_version",
 ]
 
 _lib = None
@@ -83,13 +84,17 @@ def lib(build_if_missing=True):
     L.nlp_predict.argtypes = [vp, i32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
     L.nlp_predict_device.argtypes = [vp, i32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
     L.nlp_select_edges_device.argtypes = [vp, vp, u64, u64, vp, P(u64), vp]
+    L.nlp_set_truth.argtypes = [vp, vp, vp, u64]
+    L.nlp_count_common_device.argtypes = [vp, vp, u64, P(u64), vp]
+    L.nlp_last_common.argtypes = [vp, P(u64)]
     L.nlp_status_string.argtypes = [i32]
     L.nlp_status_string.restype = ctypes.c_char_p
     L.nlp_metric_name.argtypes = [i32]
     L.nlp_metric_name.restype = ctypes.c_char_p
     L.nlp_version.restype = i32
     for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict",
-              "nlp_predict_device", "nlp_select_edges_device"):
+              "nlp_predict_device", "nlp_select_edges_device", "nlp_set_truth", "nlp_count_common_device",
+              "nlp_last_common"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -213,6 +218,24 @@ class Graph:
         _check(lib().nlp_select_edges_device(self._h, edges_in.data_ptr(), int(n), int(max_edges), out.data_ptr(),
                                              ctypes.byref(cnt), _stream_ptr(stream, out)), "nlp_select_edges_device")
         return cnt.value
+
+    def set_truth(self, del_u, del_w):
+        """Directed deletions (main.cxx deletions0) for the device evaluation."""
+        u = np.ascontiguousarray(np.asarray(del_u, dtype=np.uint32))
+        w = np.ascontiguousarray(np.asarray(del_w, dtype=np.uint32))
+        _check(lib().nlp_set_truth(self._h, u.ctypes.data, w.ctypes.data, len(u)), "nlp_set_truth")
+
+    def count_common_device(self, edges, n, stream=None):
+        """|insertions1 ∩ deletions0| for the first n device edges (torch int32 [>= n, 3])."""
+        c = ctypes.c_uint64()
+        _check(lib().nlp_count_common_device(self._h, edges.data_ptr(), int(n), ctypes.byref(c),
+                                             _stream_ptr(stream, edges)), "nlp_count_common_device")
+        return c.value
+
+    def last_common(self):
+        c = ctypes.c_uint64()
+        _check(lib().nlp_last_common(self._h, ctypes.byref(c)), "nlp_last_common")
+        return c.value
 
     def close(self):
         if getattr(self, "_h", None):

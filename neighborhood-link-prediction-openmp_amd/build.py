@@ -55,9 +55,28 @@ def build_cpp_test(verbose=True):
     return CPP_TEST_BIN
 
 
+MAIN_SRC = os.path.join(HERE, "nlp_main.cxx")
+MAIN_BIN = os.path.join(HERE, "nlp_main")
+
+
+def build_main(verbose=True):
+    """nlp_main: the main.cxx-style experiment driver (host ingest + sweep) over libnlp.so."""
+    deps = [MAIN_SRC, LIB] + [os.path.join(ROOT, "include", "nlp", f) for f in ("predict.hxx", "ingest.hxx")]
+    if os.path.exists(MAIN_BIN) and all(os.path.getmtime(d) <= os.path.getmtime(MAIN_BIN) for d in deps):
+        return MAIN_BIN
+    cmd = ["g++", "-std=c++17", "-O3", "-fopenmp", "-Wall", "-Wno-unknown-pragmas", "-I", os.path.join(ROOT, "include"),
+           MAIN_SRC, "-L", HERE,
+           "-lnlp", "-Wl,-rpath," + HERE, "-o", MAIN_BIN]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return MAIN_BIN
+
+
 def build(force=False, verbose=True):
     if not force and not needs_build():
         build_cpp_test(verbose)
+        build_main(verbose)
         return LIB
     cmd = [hipcc()] + HIPCC_FLAGS + [f for f in os.environ.get("NLP_HIPCC_EXTRA", "").split() if f] + SOURCES + \
         ["-o", LIB + ".tmp"]
@@ -66,6 +85,7 @@ def build(force=False, verbose=True):
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
     build_cpp_test(verbose)
+    build_main(verbose)
     return LIB
 
 

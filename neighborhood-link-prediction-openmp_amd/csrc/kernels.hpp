@@ -343,6 +343,31 @@ struct EdgeOut {
   float score;
 };
 
+// ---------------------------------------------------------------- evaluation (main.cxx:48-57)
+// |insertions1 ∩ deletions0|: both directions of every predicted link looked
+// up in the sorted directed deletion keys (u << 32 | v).
+__global__ void k_count_common(const EdgeOut* __restrict__ e, uint64_t n, const uint64_t* __restrict__ keys,
+                               uint64_t nk, unsigned long long* __restrict__ common) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const EdgeOut x = e[i];
+    const uint64_t a = ((uint64_t)x.u << 32) | x.v, b = ((uint64_t)x.v << 32) | x.u;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint64_t k = q ? b : a;
+      uint64_t lo = 0, hi = nk;
+      while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        if (keys[m] < k) lo = m + 1; else hi = m;
+      }
+      c += (lo < nk && keys[lo] == k) ? 1 : 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(common, c);
+}
+
+
 __global__ void k_gather_edges(const uint32_t* __restrict__ idx, uint64_t n, const uint32_t* __restrict__ cu,
                                const uint32_t* __restrict__ cw, const float* __restrict__ cs,
                                EdgeOut* __restrict__ out) {

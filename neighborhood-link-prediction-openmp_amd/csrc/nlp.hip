@@ -68,7 +68,7 @@ enum Buf {
   B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
-  B_HP_TIEI0, B_HP_TIEI1,
+  B_HP_TIEI0, B_HP_TIEI1, B_EVAL,
   NBUF
 };
 
@@ -174,6 +174,12 @@ struct nlp_graph {
   // hash path: per-workgroup global tables of bins 2 and 3 (kept clean between calls)
   uint32_t* hp_scratch = nullptr;              // k_hp_part: per-workgroup wedge scratch (w and v)
   uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
+  // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
+  uint64_t* truth = nullptr;
+  uint64_t ntruth = 0;
+  const EdgeOut* last_out = nullptr;
+  uint64_t last_n = 0;
+  hipStream_t last_stream = nullptr;
   unsigned hp_gp = 0;                          // workgroups of k_hp_part
   uint64_t hp_scap = 0;                        // scratch words per workgroup and array
   uint64_t hp_min_wedges = 1ull << 26;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 4 runs
@@ -247,6 +253,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->d_stamp) (void)hipFree(g->d_stamp);
   if (g->hp_scratch) (void)hipFree(g->hp_scratch);
   if (g->tile_row) (void)hipFree(g->tile_row);
+  if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
     if (g->toff) (void)hipFree(g->toff);
@@ -2239,6 +2246,11 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
   memset(&tt, 0, sizeof(tt));
   nlp_status s = predict_impl(g, p, (EdgeOut*)d_out, out_count, &tt, st, nullptr);
   if (t) *t = tt;
+  if (s == NLP_OK) {
+    g->last_out = (const EdgeOut*)d_out;
+    g->last_n = *out_count;
+    g->last_stream = st;
+  }
   return s;
 }
 
@@ -2274,7 +2286,50 @@ nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree,
   }
   *out_count = n;
   if (t) *t = last;
+  g->last_out = d_res;
+  g->last_n = n;
+  g->last_stream = st;
   return NLP_OK;
+}
+
+nlp_status nlp_set_truth(nlp_graph* g, const uint32_t* u, const uint32_t* v, uint64_t n) {
+  if (!g || (n && (!u || !v))) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  std::vector<uint64_t> k(n);
+  for (uint64_t i = 0; i < n; ++i) k[i] = ((uint64_t)u[i] << 32) | v[i];
+  std::sort(k.begin(), k.end());
+  k.erase(std::unique(k.begin(), k.end()), k.end());
+  if (g->truth) TRY(hipFree(g->truth));
+  g->truth = nullptr;
+  g->ntruth = k.size();
+  TRY(hipMalloc(&g->truth, std::max<uint64_t>(k.size(), 1) * 8));
+  if (!k.empty()) TRY(hipMemcpy(g->truth, k.data(), k.size() * 8, hipMemcpyHostToDevice));
+  return NLP_OK;
+}
+
+nlp_status nlp_count_common_device(nlp_graph* g, const nlp_edge* d_edges, uint64_t n, uint64_t* common,
+                                   void* stream) {
+  if (!g || !common || (n && !d_edges)) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  *common = 0;
+  if (!n || !g->ntruth) return NLP_OK;
+  if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
+  unsigned long long* c;
+  TRY(wsget(g->ws, B_EVAL, 1, &c));
+  TRY(hipMemsetAsync(c, 0, 8, st));
+  LAUNCH(k_count_common, n, st, (const EdgeOut*)d_edges, n, (const uint64_t*)g->truth, g->ntruth, c);
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(&g->host_small[0], c, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  *common = g->host_small[0];
+  return NLP_OK;
+}
+
+nlp_status nlp_last_common(nlp_graph* g, uint64_t* common) {
+  if (!g || !common) return NLP_ERR_INVALID;
+  if (!g->last_out && g->last_n) return NLP_ERR_INVALID;
+  return nlp_count_common_device(g, (const nlp_edge*)g->last_out, g->last_n, common, g->last_stream);
 }
 
 nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,

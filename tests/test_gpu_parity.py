@@ -485,3 +485,59 @@ def test_gpu_full_size_c2_large_hub_threshold(gpu, oracle, nlp):
             eu, ew, es, oi = oracle.predict(off, keys, m, 16, max_edges=k)
             assert_canonical_equal(eu, ew, es, u, w, s)
             assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
+
+
+def test_gpu_device_evaluation_matches_host(gpu, golden):
+    """N3: |insertions1 ∩ deletions0| on the device (nlp_last_common,
+    nlp_count_common_device) equals main.cxx's host evaluation."""
+    import torch
+    g = golden["g3k"]
+    k = int(g["k"][0])
+    with gpu.Graph(g["offsets"], g["keys"]) as G:
+        G.set_truth(g["del_u"], g["del_w"])
+        for m, H in ((1, 4), (0, 0), (7, 8)):
+            u, w, s, t = G.predict(m, H, k)
+            ins = set(zip(u.tolist(), w.tolist())) | set(zip(w.tolist(), u.tolist()))
+            dels = set(zip(g["del_u"].tolist(), g["del_w"].tolist()))
+            assert G.last_common() == len(ins & dels)
+            out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+            n, _ = G.predict_device(m, H, k, out)
+            assert G.count_common_device(out, n) == len(ins & dels)
+            assert G.last_common() == len(ins & dels)
+
+
+def test_gpu_experiment_driver(gpu, golden, oracle, tmp_path):
+    """N4: nlp_main (main.cxx flow: ingest, deletion batch, PREDICT_LINKS sweep,
+    process.js log lines) on g300's MatrixMarket input with seed 42, d = 0.1 --
+    the same graph and deletions as the fixture, so precision / recall must equal
+    the oracle's top-k evaluated as main.cxx does."""
+    import re
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import chung_lu_mtx
+    from parity import f1_score
+    from nlp_amd import build as B
+    binary = B.build_main(verbose=False)
+    mtx = str(tmp_path / "g300.mtx")
+    chung_lu_mtx(mtx, 300, 1200, 0.6, 1)
+    env = dict(os.environ, NLP_SEED="42", BATCH_DELETIONS_BEGIN="0.1", BATCH_DELETIONS_END="0.1",
+               NLP_METRICS="CN,JAC,AA,RA", NLP_HUBS="0,4,64")
+    r = subprocess.run([binary, mtx, "0", "0"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    g = golden["g300"]
+    k = int(g["k"][0])
+    rx = re.compile(r"^\{\-(.+?)\/\+(.+?) batchf, (.+?) threads\} -> \{(.+?)ms, (.+?) scoring, (.+?) precision, "
+                    r"(.+?) recall\} predictLinks(\w+)Hip(\d+)$")
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{-")]
+    assert len(lines) == 4 * 3
+    assert re.search(r"^order: \d+ size: \d+ \[directed\] \{\} \(removeSelfLoops\)$", r.stdout, re.M)
+    names = {"CommonNeighbors": 0, "JaccardCoefficient": 1, "AdamicAdarCoefficient": 7, "ResourceAllocationScore": 8}
+    for ln in lines:
+        m = rx.match(ln)
+        assert m, ln
+        metric, H = names[m.group(8)], int(m.group(9))
+        u, w, s, _ = oracle.predict(g["offsets"], g["keys"], metric, H, max_edges=k)
+        p, rc, _ = f1_score(u, w, g["del_u"], g["del_w"])
+        assert float(m.group(6)) == pytest.approx(p, rel=1e-3, abs=1e-12)
+        assert float(m.group(7)) == pytest.approx(rc, rel=1e-3, abs=1e-12)
