@@ -146,10 +146,11 @@ def main():
     span = ginfo["span"]
     k = info["k"]
     stream = torch.cuda.current_stream()
-    out_local = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+    out_local = torch.empty((k + 1, 3), dtype=torch.int32, device="cuda")  # block: header + local top-k
     out = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
     mid = nlp.METRICS.index(metric)
     last = {}
+    xstate = dmod.Exchange()  # all_gather stride, learnt by the first (warmup) step
 
     def step():
         if world == 1:
@@ -157,7 +158,7 @@ def main():
             last.update(t)
             return cnt
         res, cnt, inf = dmod.predict_sharded(dmod.hip_local_predict(G, mid, hub, k, out_local, stream),
-                                             dmod.hip_merge(G, out, stream), span, k)
+                                             dmod.hip_merge(G, out, stream), span, k, state=xstate)
         last.update(inf)
         return cnt
 

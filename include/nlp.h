@@ -146,6 +146,22 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
 nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,
                                    nlp_edge* d_out, uint64_t* out_count, void* stream);
 
+/* The same merge over the layout one all_gather produces (the multi-GPU
+ * exchange; replaces the serial k-way heap merge of
+ * predict.hxx:431-460): `nblocks` blocks of `stride` entries, block r at
+ * d_blocks + r * stride holding shard r's canonical result (shards in ascending
+ * source-range order).  Entry 0 of a block is its header
+ * {u = count & 0xffffffff, v = count >> 32, score = bits NLP_BLOCK_MAGIC},
+ * entries 1..count the result.  One pass: every entry's output position is its
+ * index plus, for every other block, the number of that block's entries ranked
+ * before it (binary search; ties rank lower blocks first).  Writes the
+ * canonical global top max_edges into d_out.  NLP_ERR_CAPACITY when a count
+ * exceeds stride - 1 or a header is malformed; *out_count then holds the
+ * largest count (the caller regathers with a larger stride). */
+#define NLP_BLOCK_MAGIC 0x4E4C5042u
+nlp_status nlp_merge_blocks_device(nlp_graph* g, const nlp_edge* d_blocks, uint64_t stride, uint32_t nblocks,
+                                   uint64_t max_edges, nlp_edge* d_out, uint64_t* out_count, void* stream);
+
 /* Evaluation of main.cxx:48-57 on the device.  nlp_set_truth
  * keeps the directed deletions (main.cxx `deletions0`, both directions, host
  * arrays; sorted and deduplicated here) on the handle's device.

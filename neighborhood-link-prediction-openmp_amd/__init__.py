@@ -57,8 +57,8 @@ class Timing(ctypes.Structure):
 
 EXPORTS = [
     "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
-    "nlp_predict_device", "nlp_select_edges_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common",
-    "nlp_status_string", "nlp_metric_name", "nlp_version",
+    "nlp_predict_device", "nlp_select_edges_device", "nlp_merge_blocks_device", "nlp_set_truth",
+    "nlp_count_common_device", "nlp_last_common", "nlp_status_string", "nlp_metric_name", "nlp_version",
 ]
 
 _lib = None
@@ -84,6 +84,7 @@ def lib(build_if_missing=True):
     L.nlp_predict.argtypes = [vp, i32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
     L.nlp_predict_device.argtypes = [vp, i32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
     L.nlp_select_edges_device.argtypes = [vp, vp, u64, u64, vp, P(u64), vp]
+    L.nlp_merge_blocks_device.argtypes = [vp, vp, u64, u32, u64, vp, P(u64), vp]
     L.nlp_set_truth.argtypes = [vp, vp, vp, u64]
     L.nlp_count_common_device.argtypes = [vp, vp, u64, P(u64), vp]
     L.nlp_last_common.argtypes = [vp, P(u64)]
@@ -93,7 +94,7 @@ def lib(build_if_missing=True):
     L.nlp_metric_name.restype = ctypes.c_char_p
     L.nlp_version.restype = i32
     for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict",
-              "nlp_predict_device", "nlp_select_edges_device", "nlp_set_truth", "nlp_count_common_device",
+              "nlp_predict_device", "nlp_select_edges_device", "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device",
               "nlp_last_common"):
         getattr(L, f).restype = i32
     _lib = L
@@ -217,6 +218,21 @@ class Graph:
         cnt = ctypes.c_uint64()
         _check(lib().nlp_select_edges_device(self._h, edges_in.data_ptr(), int(n), int(max_edges), out.data_ptr(),
                                              ctypes.byref(cnt), _stream_ptr(stream, out)), "nlp_select_edges_device")
+        return cnt.value
+
+    def merge_blocks_device(self, blocks, max_edges, out, stream=None):
+        """Merge the gathered shard blocks (torch int32 [nblocks, stride, 3], entry 0
+        of each block a header, nlp.h nlp_merge_blocks_device) into `out`.  Returns
+        the merged count, or raises NlpError(NLP_ERR_CAPACITY) with .count = the
+        largest block count when a block overflowed its stride."""
+        cnt = ctypes.c_uint64()
+        st = lib().nlp_merge_blocks_device(self._h, blocks.data_ptr(), int(blocks.shape[1]), int(blocks.shape[0]),
+                                           int(max_edges), out.data_ptr(), ctypes.byref(cnt), _stream_ptr(stream, out))
+        if st == 5:
+            e = NlpError(st, "nlp_merge_blocks_device")
+            e.count = cnt.value
+            raise e
+        _check(st, "nlp_merge_blocks_device")
         return cnt.value
 
     def set_truth(self, del_u, del_w):

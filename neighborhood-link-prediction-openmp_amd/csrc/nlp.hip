@@ -150,6 +150,7 @@ struct nlp_graph {
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
   unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256, occ_runs = 256;
   bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
+  int msd_force = 0;                           // NLP_MSD_PASSES: force 1 or 2 MSD passes (tests)
   int group_sort = 2;                          // NLP_GROUP_SORT: 0 k_sp_bucket sort-only, 1 k_sp_group, 2 group only after 2 MSD passes
   uint64_t last_wedges = 0;                    // wedges of the previous fast call (sizes the MSD passes)
   double last_ok_w = 0;                        // wedge estimate of the last successful sort-path call
@@ -441,6 +442,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
+  if (const char* mp = getenv("NLP_MSD_PASSES")) g->msd_force = std::min(2, std::max(0, atoi(mp)));
   if (const char* gr = getenv("NLP_GROUPING")) {
     g->sort_grouping = strcmp(gr, "bucket") != 0;
     g->sort_lsd = strcmp(gr, "lsd") == 0;
@@ -1956,6 +1958,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     msd = g->last_ok_msd;
     msd_passes = g->last_ok_passes;
   }
+  if (g->msd_force) {
+    msd = true;
+    msd_passes = g->msd_force;
+  }
   // size the record buffers from the wedge estimate up front (an overflow costs a rerun)
   if (sorted) {
     const double est = est_w;
@@ -1988,6 +1994,75 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     TRY(wait_event(E[2]));
     if (hprof) t3 = now_us();
     const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;
+    if (debug_on())
+      fprintf(stderr, "nlp: fast attempt %d range [%llu,%llu) msd %d passes %d split %d capW %llu W %llu C %llu "
+              "flags %llx replayed %d\n", attempt, (unsigned long long)p.ua, (unsigned long long)p.ub, (int)msd,
+              sorted ? sp.msd_passes : 0, sorted ? (int)sp.split : 0, (unsigned long long)g->capW,
+              (unsigned long long)h[C_W], (unsigned long long)h[C_C], (unsigned long long)h[C_FLAGS], (int)replayed);
+    if (sorted && sp.msd && getenv("NLP_CHECK_SORT")) {  // diagnostics: records sorted after grouping?
+      const uint64_t n = h[C_WSORT];
+      const int P = sp.msd_passes;
+      std::vector<uint64_t> rk(n);
+      TRY(hipMemcpy(rk.data(), (P & 1) ? sp.rk1 : sp.rk0, n * 8, hipMemcpyDeviceToHost));
+      uint64_t bad = 0, first = ~0ull;
+      for (uint64_t i = 1; i < n; ++i)
+        if (rk[i] < rk[i - 1]) {
+          if (!bad) first = i;
+          ++bad;
+        }
+      fprintf(stderr, "nlp: sort check n %llu shift %d wbits %d: %llu inversions", (unsigned long long)n,
+              sp.msd_shift, sp.wbits, (unsigned long long)bad);
+      if (bad) {
+        fprintf(stderr, " first at %llu: %llx > %llx (fine %llx %llx)\n  around:", (unsigned long long)first,
+                (unsigned long long)rk[first - 1], (unsigned long long)rk[first],
+                (unsigned long long)(rk[first - 1] >> sp.msd_shift), (unsigned long long)(rk[first] >> sp.msd_shift));
+        for (uint64_t i = first > 6 ? first - 6 : 0; i < std::min(n, first + 6); ++i)
+          fprintf(stderr, " %llx", (unsigned long long)(rk[i] >> sp.msd_shift));
+        // device digit histograms (sum of the copies) vs the records' own
+        std::vector<uint32_t> hd(HCOPIES * HSTRIDE);
+        TRY(hipMemcpy(hd.data(), sp.arena + SP_HREC, hd.size() * 4, hipMemcpyDeviceToHost));
+        for (int dg = 0; dg < P; ++dg) {
+          std::vector<uint64_t> hh(256, 0);
+          for (uint64_t i = 0; i < n; ++i) ++hh[(rk[i] >> (sp.msd_shift + 8 * dg)) & 255];
+          int mism = 0;
+          for (int b = 0; b < 256; ++b) {
+            uint64_t s = 0;
+            for (int c = 0; c < HCOPIES; ++c) s += hd[c * HSTRIDE + dg * 256 + b];
+            if (s != hh[b]) {
+              if (mism < 4) fprintf(stderr, "\n  digit %d bin %d: device %llu records %llu", dg, b,
+                                    (unsigned long long)s, (unsigned long long)hh[b]);
+              ++mism;
+            }
+          }
+          fprintf(stderr, "\n  digit %d: %d bins differ", dg, mism);
+        }
+        // run-length encoding of the top digit in the final records
+        fprintf(stderr, "\n  top-digit runs:");
+        {
+          const int tsh = sp.msd_shift + 8 * (P - 1);
+          uint64_t i = 0;
+          while (i < n) {
+            uint64_t j = i;
+            while (j < n && ((rk[j] >> tsh) & 255) == ((rk[i] >> tsh) & 255)) ++j;
+            if (j - i < 4 || ((rk[i] >> tsh) & 255) >= 0x30) fprintf(stderr, " %llx@%llu+%llu", (unsigned long long)((rk[i] >> tsh) & 255),
+                                      (unsigned long long)i, (unsigned long long)(j - i));
+            i = j;
+          }
+        }
+        if (P == 2) {  // pass-0 output (rk1) must be sorted by digit 0
+          std::vector<uint64_t> r1(n);
+          TRY(hipMemcpy(r1.data(), sp.rk1, n * 8, hipMemcpyDeviceToHost));
+          uint64_t b0 = 0;
+          for (uint64_t i = 1; i < n; ++i)
+            if (((r1[i] >> sp.msd_shift) & 255) < ((r1[i - 1] >> sp.msd_shift) & 255)) ++b0;
+          fprintf(stderr, "\n  pass-0 output digit-0 inversions: %llu", (unsigned long long)b0);
+        }
+        // the k_sp_group ranges containing the inversion
+        fprintf(stderr, "\n  GR_T tile of the inversion: %llu (offset %llu)", (unsigned long long)(first / GR_T),
+                (unsigned long long)(first % GR_T));
+      }
+      fprintf(stderr, "\n");
+    }
     if (h[C_FLAGS] >> 32) {  // look-back timeout
       if (debug_on())
         fprintf(stderr, "nlp: look-back timeout, flags %llx W %llu C %llu msd %d passes %d\n",
@@ -2356,6 +2431,35 @@ nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t 
   if (s != NLP_OK) return s;
   TRY(hipStreamSynchronize(st));
   *out_count = C.n;
+  return NLP_OK;
+}
+
+nlp_status nlp_merge_blocks_device(nlp_graph* g, const nlp_edge* d_blocks, uint64_t stride, uint32_t nblocks,
+                                   uint64_t max_edges, nlp_edge* d_out, uint64_t* out_count, void* stream) {
+  if (!g || !out_count || !d_blocks || stride < 1 || nblocks < 1 || nblocks > 65535 || (max_edges && !d_out))
+    return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
+  unsigned long long* c;
+  TRY(wsget(g->ws, B_EVAL, 4, &c));
+  hipLaunchKernelGGL(k_merge_blocks_check, dim3(1), dim3(64), 0, st, (const EdgeOut*)d_blocks, stride, nblocks, c);
+  TRY(hipGetLastError());
+  if (max_edges && stride > 1) {
+    const uint64_t gx = (stride - 1 + NT - 1) / NT;
+    if (gx > 0x7fffffffull) return NLP_ERR_INVALID;
+    hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)gx, nblocks), dim3(NT), 0, st, (const EdgeOut*)d_blocks,
+                       stride, nblocks, max_edges, (const unsigned long long*)c, (EdgeOut*)d_out);
+    TRY(hipGetLastError());
+  }
+  TRY(hipMemcpyAsync(g->host_small, c, 24, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t tot = g->host_small[0], mx = g->host_small[1], bad = g->host_small[2];
+  if (bad) {
+    *out_count = mx;
+    return NLP_ERR_CAPACITY;
+  }
+  *out_count = std::min(tot, max_edges);
   return NLP_OK;
 }
 

@@ -163,3 +163,80 @@ __global__ void k_gather_sel(const uint32_t* __restrict__ idx, CandBufs a, CandB
 }
 
 }  // namespace nlp
+
+namespace nlp {
+
+// ---------------------------------------------------------------- block merge (multi-GPU exchange)
+// The reference merges its per-thread heaps with a serial k-way heap merge
+// (predict.hxx:431-460).  Here the shards' canonical lists arrive as the fixed-
+// stride blocks of one all_gather (nlp.h nlp_merge_blocks_device): entry 0 of a
+// block is {count lo, count hi, magic}, entries 1..count are sorted by score key
+// descending.  Entry i of block r goes to
+//   i + sum_{r' < r} #{j in r' : key_j >= key} + sum_{r' > r} #{j in r' : key_j > key},
+// which is the canonical order (score desc, then block order = u asc, then the
+// block's own (u, w) order).  Consecutive entries of a wave have nearby keys, so
+// the lanes' binary searches in another block walk the same cache lines.
+constexpr uint32_t BLOCK_MAGIC = 0x4E4C5042u;
+
+__device__ __forceinline__ bool block_count(const EdgeOut* __restrict__ b, uint64_t stride, uint64_t* cnt) {
+  const EdgeOut h = b[0];
+  const uint64_t c = (uint64_t)h.u | ((uint64_t)h.v << 32);
+  *cnt = c;
+  return __float_as_uint(h.score) == BLOCK_MAGIC && c < stride;
+}
+
+// first j in [0, n) with key(list[j]) < key (STRICT = false) or <= key (STRICT = true)
+template <bool STRICT>
+__device__ __forceinline__ uint64_t block_rank(const EdgeOut* __restrict__ list, uint64_t n, uint32_t key) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint32_t km = score_key(list[mid].score);
+    if (STRICT ? km > key : km >= key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ctr[0] = sum of counts, ctr[1] = largest count, ctr[2] = 1 when a header is bad
+__global__ void k_merge_blocks_check(const EdgeOut* __restrict__ blocks, uint64_t stride, uint32_t nb,
+                                     unsigned long long* __restrict__ ctr) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t tot = 0, mx = 0;
+    bool bad = false;
+    for (uint32_t r = 0; r < nb; ++r) {
+      uint64_t c;
+      if (!block_count(blocks + (uint64_t)r * stride, stride, &c)) bad = true;
+      tot += c;
+      mx = c > mx ? c : mx;
+    }
+    ctr[0] = tot;
+    ctr[1] = mx;
+    ctr[2] = bad ? 1 : 0;
+  }
+}
+
+// grid (ceil((stride - 1) / NT), nb); reads nothing when a header is bad
+__global__ __launch_bounds__(NT) void k_merge_blocks(const EdgeOut* __restrict__ blocks, uint64_t stride, uint32_t nb,
+                                                     uint64_t k, const unsigned long long* __restrict__ ctr,
+                                                     EdgeOut* __restrict__ out) {
+  if (ctr[2]) return;
+  const uint32_t r = blockIdx.y;
+  const EdgeOut* b = blocks + (uint64_t)r * stride;
+  const uint64_t n = (uint64_t)b[0].u | ((uint64_t)b[0].v << 32);
+  const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const EdgeOut e = b[1 + i];
+  const uint32_t key = score_key(e.score);
+  uint64_t pos = i;
+  if (pos >= k) return;  // its own block already ranks k entries before it
+  for (uint32_t q = 0; q < nb && pos < k; ++q) {
+    if (q == r) continue;
+    const EdgeOut* o = blocks + (uint64_t)q * stride;
+    const uint64_t m = (uint64_t)o[0].u | ((uint64_t)o[0].v << 32);
+    pos += q < r ? block_rank<false>(o + 1, m, key) : block_rank<true>(o + 1, m, key);
+  }
+  if (pos < k) out[pos] = e;
+}
+
+}  // namespace nlp

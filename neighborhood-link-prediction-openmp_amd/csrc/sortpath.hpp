@@ -1454,8 +1454,15 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
     s_and[wv] = ka;
   }
   __syncthreads();
-  uint64_t diff = 0;
-  for (int w = 0; w < BK_NW; ++w) diff |= s_or[w] ^ s_and[w];
+  // bits that differ anywhere in the range: (OR of all keys) ^ (AND of all keys)
+  // -- per-wave OR ^ AND would miss bits constant inside each wave but different
+  // between waves (consecutive fine buckets split across waves)
+  uint64_t all_or = 0, all_and = ~0ull;
+  for (int w = 0; w < BK_NW; ++w) {
+    all_or |= s_or[w];
+    all_and &= s_and[w];
+  }
+  const uint64_t diff = m ? all_or ^ all_and : 0;
   const int lbits = diff ? 64 - __clzll((long long)diff) : 0;
   sp_stamp(stamp, true, 1);
   const uint64_t lt = lane_mask_lt();

@@ -8,11 +8,14 @@ SURVEY.md §8(e).  The reference has a single OpenMP team over source vertices
   1. every rank holds a full CSR replica (second-hop lists are arbitrary, so
      the adjacency cannot be partitioned) and predicts the canonical top-k of
      its own contiguous source range [u_begin, u_end)  -> nlp_predict_device;
-  2. one all_gather of the per-rank counts and one all_gather of the (padded)
-     per-rank top-k lists over xGMI;
-  3. every rank merges: the concatenation in rank order is in (u asc) order
-     for equal scores, so a stable select by score gives exactly the
-     single-GPU canonical result                   -> nlp_select_edges_device.
+  2. ONE all_gather over xGMI of fixed-stride blocks: entry 0 of a rank's
+     block is a header with its count, entries 1..n its top-k list.  The
+     stride is learnt once per job (one extra all_gather of the counts on the
+     first call) and kept; a block that outgrows it is seen by every rank in
+     the gathered headers, and all ranks regather with a larger stride;
+  3. every rank merges in one kernel: block order is u order, so ranking each
+     entry against the other blocks by score (ties: lower block first) gives
+     exactly the single-GPU canonical result        -> nlp_merge_blocks_device.
 
 Every rank ends with the identical global result (so rank 0 can report it
 and any rank can evaluate F1).  The local predictor and the merge are
@@ -42,50 +45,104 @@ def shard_ranges(span, world, weights=None):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
-def gather_edges(local, n_local, group=None):
-    """all_gather a [n_local, 3] int32 edge block from every rank (padded to the
-    largest count).  Returns (concatenated [sum n, 3] tensor in rank order, counts)."""
+BLOCK_MAGIC = 0x4E4C5042  # nlp.h NLP_BLOCK_MAGIC
+
+
+class BlockOverflow(RuntimeError):
+    """A gathered block held more entries than the exchange stride (count = the
+    largest block count); the exchange regathers with a larger stride."""
+
+    def __init__(self, count):
+        super().__init__("block count %d exceeds the exchange stride" % count)
+        self.count = count
+
+
+class Exchange:
+    """Exchange state of one sharded job.  `cap` (entries per gathered block,
+    header excluded) is identical on every rank: it is set from gathered data
+    only, so every rank takes the same branch."""
+
+    def __init__(self):
+        self.cap = None
+
+
+def _grow(mx, max_edges):
+    return int(min(max_edges, max(1024, mx + mx // 4)))
+
+
+def write_header(block, n):
+    """Entry 0 of a block: {count lo, count hi, NLP_BLOCK_MAGIC} (nlp.h)."""
+    import numpy as np
+    h = np.array([n & 0xFFFFFFFF, n >> 32, BLOCK_MAGIC], np.uint32).view(np.int32)
+    block[0].copy_(torch.from_numpy(h))
+
+
+def block_counts(blocks):
+    """Per-block counts from the headers of gathered blocks [world, stride, 3]."""
+    h = blocks[:, 0, :2].to(torch.int64).cpu() & 0xFFFFFFFF
+    return [int(lo) | (int(hi) << 32) for lo, hi in h.tolist()]
+
+
+def gather_blocks(block, cap, group=None):
+    """One all_gather of every rank's first cap + 1 entries (header + result)
+    into [world, cap + 1, 3]."""
     world = dist.get_world_size(group)
-    dev = local.device
-    cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
-    mx = max(counts) if counts else 0
-    if mx == 0:
-        return local[:0], counts
-    pad = torch.zeros((mx, 3), dtype=local.dtype, device=dev)
-    pad[:n_local] = local[:n_local]
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)]), counts
+    stride = cap + 1
+    recv = torch.empty((world * stride, 3), dtype=block.dtype, device=block.device)
+    dist.all_gather_into_tensor(recv, block[:stride].contiguous(), group=group)
+    return recv.view(world, stride, 3)
 
 
-def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=None):
+def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=None, state=None):
     """Run the sharded pipeline on this rank.
 
-    local_predict(u_begin, u_end) -> (edges [n, 3] int32 tensor, n, info)
-    merge(edges [N, 3], N, max_edges) -> (edges [k, 3], k)
+    local_predict(u_begin, u_end) -> (block [>= max_edges + 1, 3] int32 tensor
+        whose entries 1..n hold the shard's canonical result, n, info)
+    merge(blocks [world, stride, 3], max_edges) -> (edges [>= k, 3], k); raises
+        BlockOverflow when a header count exceeds stride - 1
+    state: an Exchange kept across calls (the stride learnt by the first call);
+        a fresh one costs one extra all_gather of the counts.
     Returns (edges, k, info) -- identical on every rank."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     ub, ue = shard_ranges(span, world, weights)[rank]
-    local, n, info = local_predict(ub, ue)
-    allv, counts = gather_edges(local, n, group)
-    out, k = merge(allv, int(sum(counts)), max_edges)
-    info = dict(info or {}, shard=(ub, ue), counts=counts)
+    block, n, info = local_predict(ub, ue)
+    if block.shape[0] < max_edges + 1:
+        raise ValueError("local block must hold max_edges + 1 entries")
+    write_header(block, n)
+    state = state if state is not None else Exchange()
+    if state.cap is None:
+        cnt = torch.tensor([n], dtype=torch.int64, device=block.device)
+        counts = torch.empty(world, dtype=torch.int64, device=block.device)
+        dist.all_gather_into_tensor(counts, cnt, group=group)
+        state.cap = _grow(int(counts.max()), max_edges)
+    while True:
+        blocks = gather_blocks(block, state.cap, group)
+        try:
+            out, k = merge(blocks, max_edges)
+            break
+        except BlockOverflow as e:  # every rank sees the same headers, so all regather
+            state.cap = _grow(e.count, max_edges)
+    info = dict(info or {}, shard=(ub, ue), blocks=blocks, stride=state.cap + 1)
     return out, k, info
 
 
-def hip_local_predict(graph, metric, hub, max_edges, out, stream=None, min_score=0.0):
-    """Local predictor bound to libnlp (device output buffer `out` >= max_edges rows)."""
+def hip_local_predict(graph, metric, hub, max_edges, block, stream=None, min_score=0.0):
+    """Local predictor bound to libnlp: the shard's result goes to entries
+    1..n of the device block buffer (>= max_edges + 1 rows)."""
     def fn(ub, ue):
-        n, t = graph.predict_device(metric, hub, max_edges, out, ub, ue, min_score=min_score, stream=stream)
-        return out, n, t
+        n, t = graph.predict_device(metric, hub, max_edges, block[1:], ub, ue, min_score=min_score, stream=stream)
+        return block, n, t
     return fn
 
 
 def hip_merge(graph, out, stream=None):
-    def fn(allv, n, max_edges):
-        k = graph.select_edges_device(allv, n, max_edges, out, stream=stream)
+    """Merge bound to libnlp (nlp_merge_blocks_device, one kernel over the gathered blocks)."""
+    def fn(blocks, max_edges):
+        try:
+            k = graph.merge_blocks_device(blocks, max_edges, out, stream=stream)
+        except Exception as e:  # NLP_ERR_CAPACITY carries the largest count
+            if getattr(e, "status", None) == 5 and hasattr(e, "count"):
+                raise BlockOverflow(e.count) from None
+            raise
         return out, k
     return fn

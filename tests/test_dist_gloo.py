@@ -32,19 +32,29 @@ def _edges_tensor(u, w, s):
     return torch.from_numpy(a)
 
 
-def _canonical_merge(allv, n, k):
-    """Reference merge rule: stable sort of the rank-ordered concatenation by
-    score key descending, first k (what nlp_select_edges_device computes)."""
+def _canonical_merge(blocks, k):
+    """Reference merge rule over the gathered blocks: headers checked like
+    nlp_merge_blocks_device (overflow -> BlockOverflow), then a stable sort of
+    the rank-ordered concatenation by score key descending, first k."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import nlp_loader
     from parity import keys_of
-    a = allv[:n].numpy()
+    dmod = nlp_loader.load_sub("dist")
+    b = blocks.numpy()
+    stride = b.shape[1]
+    hdr = b[:, 0, :].view(np.uint32)
+    counts = [int(h[0]) | (int(h[1]) << 32) for h in hdr]
+    assert all(int(h[2]) == dmod.BLOCK_MAGIC for h in hdr)
+    if max(counts) > stride - 1:
+        raise dmod.BlockOverflow(max(counts))
+    a = np.concatenate([b[r, 1:1 + c] for r, c in enumerate(counts)])
     s = a[:, 2].view(np.float32)
     kk = keys_of(s).astype(np.int64)
     order = np.lexsort((np.arange(len(kk)), -kk))[:k]
     return torch.from_numpy(a[order].copy()), len(order)
 
 
-def _worker(rank, world, port, name, metric, hub, q):
+def _worker(rank, world, port, name, metric, hub, q, cap0=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -58,21 +68,30 @@ def _worker(rank, world, port, name, metric, hub, q):
 
         def local(ub, ue):
             u, w, s, info = pyoracle.predict(off, keys, metric, hub, max_edges=k, u_begin=ub, u_end=ue)
-            return _edges_tensor(u, w, s), len(u), info
+            block = torch.zeros((k + 1, 3), dtype=torch.int32)
+            block[1:1 + len(u)] = _edges_tensor(u, w, s)
+            return block, len(u), info
 
-        out, n, info = dmod.predict_sharded(local, _canonical_merge, len(off) - 1, k)
-        q.put((rank, out[:n].numpy().copy(), info["shard"], info["counts"]))
+        state = dmod.Exchange()
+        state.cap = cap0  # None: learnt from a counts all_gather; small: forces the regather path
+        outs = []
+        for _ in range(2):  # the second call reuses the learnt stride
+            out, n, info = dmod.predict_sharded(local, _canonical_merge, len(off) - 1, k, state=state)
+            outs.append(out[:n].numpy().copy())
+        assert np.array_equal(outs[0], outs[1])
+        q.put((rank, outs[1], info["shard"], dmod.block_counts(info["blocks"])))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,metric,hub", [("g3k", 1, 4), ("g3k", 7, 8), ("g300", 0, 0)])
-def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub):
+@pytest.mark.parametrize("name,metric,hub,cap0", [("g3k", 1, 4, None), ("g3k", 7, 8, None), ("g300", 0, 0, None),
+                                                  ("g3k", 1, 4, 1)])
+def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub, cap0):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, metric, hub, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, metric, hub, q, cap0)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

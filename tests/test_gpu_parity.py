@@ -144,6 +144,32 @@ def test_gpu_shard_ranges_and_merge(gpu, oracle):
             u, w, s = gpu.edges_from_tensor(res, kk)
             eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
             assert_canonical_equal(eu, ew, es, u, w, s)
+            # the all_gather layout: fixed-stride blocks with count headers (nlp_merge_blocks_device),
+            # at k and at smaller k (truncation inside the tie runs)
+            stride = max(p.shape[0] for p in parts) + 7
+            blocks = _blocks(parts, stride)
+            for kk_ in (k, 777, 1):
+                res = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+                kk = G.merge_blocks_device(blocks, kk_, res)
+                u, w, s = gpu.edges_from_tensor(res, kk)
+                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=kk_)
+                assert_canonical_equal(eu, ew, es, u, w, s)
+            # a block beyond its stride: NLP_ERR_CAPACITY with the largest count
+            small = _blocks(parts, stride)[:, : stride // 2].contiguous()
+            with pytest.raises(gpu.NlpError) as ei:
+                G.merge_blocks_device(small, k, res)
+            assert ei.value.status == 5 and ei.value.count == max(p.shape[0] for p in parts)
+
+
+def _blocks(parts, stride):
+    """[len(parts), stride, 3] int32 device blocks, entry 0 = {count lo, count hi, NLP_BLOCK_MAGIC}."""
+    import torch
+    b = torch.zeros((len(parts), stride, 3), dtype=torch.int32, device="cuda")
+    for r, p in enumerate(parts):
+        n = p.shape[0]
+        b[r, 0] = torch.from_numpy(np.array([n & 0xFFFFFFFF, n >> 32, 0x4E4C5042], np.uint32).view(np.int32))
+        b[r, 1:1 + n] = p
+    return b
 
 
 def test_gpu_edge_cases(gpu, oracle):
@@ -463,6 +489,9 @@ def test_gpu_hash_routing_and_shards(gpu, oracle):
                 kk = G.select_edges_device(allv, allv.shape[0], k, res)
                 u2, w2, s2 = gpu.edges_from_tensor(res, kk)
                 assert_canonical_equal(eu, ew, es, u2, w2, s2)
+                kk = G.merge_blocks_device(_blocks(parts, k + 1), k, res)
+                u2, w2, s2 = gpu.edges_from_tensor(res, kk)
+                assert_canonical_equal(eu, ew, es, u2, w2, s2)
 
 
 def test_gpu_full_size_c2_large_hub_threshold(gpu, oracle, nlp):
@@ -541,3 +570,29 @@ def test_gpu_experiment_driver(gpu, golden, oracle, tmp_path):
         p, rc, _ = f1_score(u, w, g["del_u"], g["del_w"])
         assert float(m.group(6)) == pytest.approx(p, rel=1e-3, abs=1e-12)
         assert float(m.group(7)) == pytest.approx(rc, rel=1e-3, abs=1e-12)
+
+
+@pytest.mark.parametrize("passes", [1, 2])
+def test_gpu_msd_passes_on_source_ranges(gpu, oracle, passes):
+    """Sort path with 1 and 2 MSD passes forced, on sub-ranges whose record key
+    is narrower than the full-range key (odd and even MSD shifts), vs the oracle."""
+    import torch
+    off, keys = random_csr(20000, 12, 21)
+    span = len(off) - 1
+    k = 50000
+    with _env(NLP_MSD_PASSES=str(passes)):
+        with gpu.Graph(off, keys) as G:
+            bad = []
+            for m, H in ((1, 4), (7, 4), (0, 8)):
+                for ub, ue in ((0, span), (0, span // 2), (span // 3, span), (5, span // 2 + 7)):
+                    out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+                    n, t = G.predict_device(m, H, k, out, ub, ue)
+                    u, w, s = gpu.edges_from_tensor(out, n)
+                    eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k, u_begin=ub, u_end=ue)
+                    assert t["path"] == 1
+                    try:
+                        assert_canonical_equal(eu, ew, es, u, w, s)
+                    except AssertionError as e:
+                        bad.append((m, H, ub, ue, len(eu), int((eu != u).sum()) if len(eu) == len(u) else -1,
+                                    str(e)[:40]))
+            assert not bad, bad
