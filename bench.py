@@ -151,6 +151,8 @@ def main():
     mid = nlp.METRICS.index(metric)
     last = {}
     xstate = dmod.Exchange()  # all_gather stride, learnt by the first (warmup) step
+    # shard bounds balanced by the per-source wedge estimate, once per graph
+    weights = dmod.source_weights(off, keys, hub) if world > 1 else None
 
     def step():
         if world == 1:
@@ -158,7 +160,8 @@ def main():
             last.update(t)
             return cnt
         res, cnt, inf = dmod.predict_sharded(dmod.hip_local_predict(G, mid, hub, k, out_local, stream),
-                                             dmod.hip_merge(G, out, stream), span, k, state=xstate)
+                                             dmod.hip_merge(G, out, stream), span, k, state=xstate,
+                                             weights=weights)
         last.update(inf)
         return cnt
 

@@ -68,7 +68,7 @@ enum Buf {
   B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
-  B_HP_TIEI0, B_HP_TIEI1, B_EVAL,
+  B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND,
   NBUF
 };
 
@@ -2442,18 +2442,37 @@ nlp_status nlp_merge_blocks_device(nlp_graph* g, const nlp_edge* d_blocks, uint6
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
   if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
   unsigned long long* c;
-  TRY(wsget(g->ws, B_EVAL, 4, &c));
+  TRY(wsget(g->ws, B_EVAL, 8, &c));
+  TRY(hipMemsetAsync(c + 4, 0, 32, st));
   hipLaunchKernelGGL(k_merge_blocks_check, dim3(1), dim3(64), 0, st, (const EdgeOut*)d_blocks, stride, nblocks, c);
   TRY(hipGetLastError());
   if (max_edges && stride > 1) {
     const uint64_t gx = (stride - 1 + NT - 1) / NT;
     if (gx > 0x7fffffffull) return NLP_ERR_INVALID;
-    hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)gx, nblocks), dim3(NT), 0, st, (const EdgeOut*)d_blocks,
-                       stride, nblocks, max_edges, (const unsigned long long*)c, (EdgeOut*)d_out);
+    uint32_t* keys;
+    TRY(wsget(g->ws, B_MKEY, stride * nblocks, &keys));
+    hipLaunchKernelGGL(k_merge_keys, dim3((unsigned)gx, nblocks), dim3(NT), 0, st, (const EdgeOut*)d_blocks, stride,
+                       (const unsigned long long*)c, keys);
+    TRY(hipGetLastError());
+    const uint64_t tiles = (stride - 1 + MT_T - 1) / MT_T;
+    uint64_t* bnd;
+    TRY(wsget(g->ws, B_MBND, 4 * (uint64_t)nblocks * nblocks * tiles, &bnd));
+    hipLaunchKernelGGL(k_merge_bounds, dim3(grid_full(4 * (uint64_t)nblocks * nblocks * tiles)), dim3(NT), 0, st,
+                       (const EdgeOut*)d_blocks, stride, nblocks, tiles, (const unsigned long long*)c,
+                       (const uint32_t*)keys, bnd);
+    TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)tiles, nblocks), dim3(MT_NT), 0, st, (const EdgeOut*)d_blocks,
+                       stride, nblocks, max_edges, (const unsigned long long*)c, (const uint32_t*)keys,
+                       (const uint64_t*)bnd, (EdgeOut*)d_out, debug_on() ? c + 4 : nullptr);
     TRY(hipGetLastError());
   }
-  TRY(hipMemcpyAsync(g->host_small, c, 24, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(g->host_small, c, 64, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
+  if (debug_on())
+    fprintf(stderr, "nlp: merge windows %llu mean len %.1f beyond LDS %llu distinct keys/tile %.1f\n",
+            (unsigned long long)g->host_small[4], g->host_small[4] ? (double)g->host_small[5] / g->host_small[4] : 0.0,
+            (unsigned long long)g->host_small[6],
+            g->host_small[4] ? (double)g->host_small[7] * (nblocks - 1) / g->host_small[4] : 0.0);
   const uint64_t tot = g->host_small[0], mx = g->host_small[1], bad = g->host_small[2];
   if (bad) {
     *out_count = mx;

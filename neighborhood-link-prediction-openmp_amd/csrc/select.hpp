@@ -216,27 +216,204 @@ __global__ void k_merge_blocks_check(const EdgeOut* __restrict__ blocks, uint64_
   }
 }
 
-// grid (ceil((stride - 1) / NT), nb); reads nothing when a header is bad
-__global__ __launch_bounds__(NT) void k_merge_blocks(const EdgeOut* __restrict__ blocks, uint64_t stride, uint32_t nb,
-                                                     uint64_t k, const unsigned long long* __restrict__ ctr,
-                                                     EdgeOut* __restrict__ out) {
+// Dense score keys of the blocks: keys[r * stride + i] = score_key(entry 1 + i of
+// block r), so the searches below touch 4-byte keys instead of 12-byte entries.
+__global__ __launch_bounds__(NT) void k_merge_keys(const EdgeOut* __restrict__ blocks, uint64_t stride,
+                                                   const unsigned long long* __restrict__ ctr,
+                                                   uint32_t* __restrict__ keys) {
+  if (ctr[2]) return;
+  const EdgeOut* b = blocks + (uint64_t)blockIdx.y * stride;
+  const uint64_t n = (uint64_t)b[0].u | ((uint64_t)b[0].v << 32);
+  const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) keys[(uint64_t)blockIdx.y * stride + i] = score_key(b[1 + i].score);
+}
+
+// rank of `key` in list[lo, hi): the first j with list[j] < key (lower block,
+// LOWER = true: its ties come first) or list[j] <= key (higher block)
+template <bool LOWER, typename P>
+__device__ __forceinline__ uint64_t merge_rank(P list, uint64_t lo, uint64_t hi, uint32_t key) {
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint32_t km = list[mid];
+    if (LOWER ? km >= key : km > key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// MT_W: windows average ~MT_T / 2 keys on balanced shards (C2 x8: 404, none
+// beyond 2048; at 512 a third of them fall back to global searches).
+constexpr int MT_NT = NT, MT_PER = 4, MT_T = MT_NT * MT_PER, MT_G = 8, MT_W = 2048;
+
+// Bounds of every (block r, tile x, block q), 4 words at bnd[4 * ((r * tiles + x) * nb + q)]:
+// {rank of the tile's first (largest) key, rank of its last (smallest) key,
+//  window [lo, hi) holding the ranks of the keys strictly between them}.
+// The window leaves out the tie runs of the two end keys in q (a count metric
+// has long runs of equal scores): for a lower block q those ties rank before
+// the first key and after every inner key, for a higher block the other way.
+// One thread per search: every dependent chain runs concurrently.
+__global__ __launch_bounds__(NT) void k_merge_bounds(const EdgeOut* __restrict__ blocks, uint64_t stride, uint32_t nb,
+                                                     uint64_t tiles, const unsigned long long* __restrict__ ctr,
+                                                     const uint32_t* __restrict__ keys, uint64_t* __restrict__ bnd) {
+  if (ctr[2]) return;
+  const uint64_t total = 4 * (uint64_t)nb * tiles * nb;
+  for (uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x; g < total; g += (uint64_t)gridDim.x * NT) {
+    const uint32_t w = (uint32_t)(g & 3);
+    const uint64_t rest = g >> 2;
+    const uint32_t q = (uint32_t)(rest % nb);
+    const uint64_t rx = rest / nb;
+    const uint64_t x = rx % tiles;
+    const uint32_t r = (uint32_t)(rx / tiles);
+    const EdgeOut hr = blocks[(uint64_t)r * stride];
+    const uint64_t n = (uint64_t)hr.u | ((uint64_t)hr.v << 32);
+    const uint64_t i0 = x * MT_T;
+    uint64_t v = 0;
+    if (q != r && i0 < n) {
+      const uint64_t i1 = n < i0 + MT_T ? n : i0 + MT_T;
+      const uint32_t kf = keys[(uint64_t)r * stride + i0], kl = keys[(uint64_t)r * stride + i1 - 1];
+      const EdgeOut h = blocks[(uint64_t)q * stride];
+      const uint64_t m = (uint64_t)h.u | ((uint64_t)h.v << 32);
+      const uint32_t* kq = keys + (uint64_t)q * stride;
+      const bool lower = q < r;
+      // w: 0 rank(first), 1 rank(last), 2 window lo, 3 window hi
+      if (w == 0) v = lower ? merge_rank<true>(kq, 0, m, kf) : merge_rank<false>(kq, 0, m, kf);
+      else if (w == 1) v = lower ? merge_rank<true>(kq, 0, m, kl) : merge_rank<false>(kq, 0, m, kl);
+      else if (w == 2) v = merge_rank<true>(kq, 0, m, kf);   // past the ties of the first key
+      else v = merge_rank<false>(kq, 0, m, kl);              // before the ties of the last key
+      if (w == 3 && kf == kl) v = merge_rank<true>(kq, 0, m, kf);  // one key: empty window
+    }
+    bnd[g] = v;
+  }
+}
+
+// grid (ceil((stride - 1) / MT_T), nb), MT_NT threads; reads nothing when a
+// header is bad.  A workgroup takes MT_T consecutive entries of block r.  Equal
+// keys share their rank in every other block, so ranks are searched once per
+// distinct key of the tile (score ties are common: a count metric has few
+// distinct scores).  The ranks in block q lie between those of the tile's first
+// (largest) and last (smallest) keys: two global searches bound a window of q's
+// keys, staged in LDS when it fits MT_W keys, else searched in place.  Blocks
+// are taken MT_G at a time.
+__global__ __launch_bounds__(MT_NT) void k_merge_blocks(const EdgeOut* __restrict__ blocks, uint64_t stride,
+                                                        uint32_t nb, uint64_t k,
+                                                        const unsigned long long* __restrict__ ctr,
+                                                        const uint32_t* __restrict__ keys,
+                                                        const uint64_t* __restrict__ bnd, EdgeOut* __restrict__ out,
+                                                        unsigned long long* __restrict__ dbg) {
+  __shared__ uint32_t s_win[MT_G][MT_W];
+  __shared__ uint32_t s_dkey[MT_T];
+  __shared__ uint64_t s_drank[MT_T];
+  __shared__ uint64_t s_b[MT_G][4];
+  __shared__ uint64_t s_red[NWAVE + 1];
   if (ctr[2]) return;
   const uint32_t r = blockIdx.y;
   const EdgeOut* b = blocks + (uint64_t)r * stride;
   const uint64_t n = (uint64_t)b[0].u | ((uint64_t)b[0].v << 32);
-  const uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= n) return;
-  const EdgeOut e = b[1 + i];
-  const uint32_t key = score_key(e.score);
-  uint64_t pos = i;
-  if (pos >= k) return;  // its own block already ranks k entries before it
-  for (uint32_t q = 0; q < nb && pos < k; ++q) {
-    if (q == r) continue;
-    const EdgeOut* o = blocks + (uint64_t)q * stride;
-    const uint64_t m = (uint64_t)o[0].u | ((uint64_t)o[0].v << 32);
-    pos += q < r ? block_rank<false>(o + 1, m, key) : block_rank<true>(o + 1, m, key);
+  const uint64_t i0 = (uint64_t)blockIdx.x * MT_T;
+  if (i0 >= n || i0 >= k) return;  // entry i has at least i entries before it
+  const uint64_t i1 = n < i0 + MT_T ? n : i0 + MT_T;
+  const uint32_t* kr = keys + (uint64_t)r * stride;
+  const int t = threadIdx.x;
+  // blocked: thread t owns entries i0 + 4t .. +3; distinct keys numbered in order
+  uint32_t key[MT_PER];
+  EdgeOut ent[MT_PER];
+  uint32_t heads = 0;
+#pragma unroll
+  for (int e = 0; e < MT_PER; ++e) {
+    const uint64_t i = i0 + (uint64_t)t * MT_PER + e;
+    key[e] = i < i1 ? kr[i] : 0u;
+    ent[e] = i < i1 ? b[1 + i] : EdgeOut{0u, 0u, 0.0f};  // issued early: lands while the ranks are searched
+    if (i < i1 && (i == i0 || kr[i - 1] != key[e])) ++heads;
   }
-  if (pos < k) out[pos] = e;
+  uint64_t nd;
+  uint32_t slot = (uint32_t)block_excl_scan(heads, s_red, &nd);
+  uint32_t dslot[MT_PER];
+#pragma unroll
+  for (int e = 0; e < MT_PER; ++e) {
+    const uint64_t i = i0 + (uint64_t)t * MT_PER + e;
+    if (i < i1 && (i == i0 || kr[i - 1] != key[e])) {
+      s_dkey[slot] = key[e];
+      s_drank[slot] = 0;
+      ++slot;
+    }
+    dslot[e] = slot - 1;  // the slot of this entry's key
+  }
+  const uint32_t D = (uint32_t)nd;
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < nb; q0 += MT_G) {
+    if (t < 4 * MT_G) {  // bounds from k_merge_bounds
+      const uint32_t j = t >> 2, q = q0 + j;
+      s_b[j][t & 3] = q < nb ? bnd[4 * (((uint64_t)r * gridDim.x + blockIdx.x) * nb + q) + (t & 3)] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MT_G; ++j) {
+      const uint64_t lo = s_b[j][2], len = s_b[j][3] > lo ? s_b[j][3] - lo : 0;
+      if (len <= MT_W) {
+        const uint32_t* kq = keys + (uint64_t)(q0 + j) * stride + lo;
+        for (uint32_t x = t; x < len; x += MT_NT) s_win[j][x] = kq[x];
+      }
+    }
+    __syncthreads();
+    // per block: window length, LDS staged or not
+    uint32_t wl[MT_G];
+    bool inl[MT_G];
+#pragma unroll
+    for (int j = 0; j < MT_G; ++j) {
+      const uint64_t lo = s_b[j][2], len = s_b[j][3] > lo ? s_b[j][3] - lo : 0;
+      inl[j] = q0 + j < nb && q0 + j != r && len <= MT_W;
+      wl[j] = inl[j] ? (uint32_t)len : 0u;
+      if (dbg && t == 0 && q0 + j < nb && q0 + j != r) {  // diagnostics (NLP_DEBUG): windows, fallbacks, distinct keys
+        atomicAdd(&dbg[0], 1ull);
+        atomicAdd(&dbg[1], (unsigned long long)len);
+        if (!inl[j]) atomicAdd(&dbg[2], 1ull);
+        if (j == 0) atomicAdd(&dbg[3], (unsigned long long)D);
+      }
+    }
+    for (uint32_t d = t; d < D; d += MT_NT) {
+      const uint32_t kd = s_dkey[d];
+      const bool inner = d != 0 && d != D - 1;
+      // branchless searches of the staged windows, all blocks in lockstep (independent LDS reads per step)
+      uint32_t pos[MT_G];
+#pragma unroll
+      for (int j = 0; j < MT_G; ++j) pos[j] = 0;
+#pragma unroll
+      for (uint32_t step = MT_W; step >= 1; step >>= 1) {
+#pragma unroll
+        for (int j = 0; j < MT_G; ++j) {
+          if (inner && pos[j] + step <= wl[j]) {
+            const uint32_t v = s_win[j][pos[j] + step - 1];
+            if (q0 + j < r ? v >= kd : v > kd) pos[j] += step;
+          }
+        }
+      }
+      uint64_t add = 0;
+#pragma unroll
+      for (int j = 0; j < MT_G; ++j) {
+        const uint32_t q = q0 + j;
+        if (q >= nb || q == r) continue;
+        if (d == 0) {
+          add += s_b[j][0];
+        } else if (d == D - 1) {
+          add += s_b[j][1];
+        } else if (inl[j]) {
+          add += s_b[j][2] + pos[j];
+        } else {
+          const uint64_t lo = s_b[j][2], hi = s_b[j][3];
+          const uint32_t* kq = keys + (uint64_t)q * stride;
+          add += q < r ? merge_rank<true>(kq, lo, hi, kd) : merge_rank<false>(kq, lo, hi, kd);
+        }
+      }
+      s_drank[d] += add;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int e = 0; e < MT_PER; ++e) {
+    const uint64_t i = i0 + (uint64_t)t * MT_PER + e;
+    const uint64_t pos = i + (i < i1 ? s_drank[dslot[e]] : 0);
+    if (i < i1 && pos < k) out[pos] = ent[e];
+  }
 }
 
 }  // namespace nlp

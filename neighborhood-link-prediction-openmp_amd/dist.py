@@ -45,6 +45,32 @@ def shard_ranges(span, world, weights=None):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+def source_weights(off, keys, hub, chunk=1 << 27):
+    """Per-source work estimate for balancing the shards (SURVEY.md §8(e):
+    balance by the wedge prefix, not by vertex count): W(u) = sum of deg v over
+    the surviving intermediates v in N(u) (deg v <= hub; hub = 0: all), times
+    (span - u) / span, the share of second-hop vertices w > u when ids carry no
+    order (predict.hxx:221 keeps only w > u, so low ids own more candidates).
+    Computed on the CSR's device in chunks; identical on every rank (integer
+    sums, then float64 elementwise).  Returns a float64 CPU tensor [span]."""
+    off = off.to(torch.int64)
+    span = off.numel() - 1
+    deg = (off[1:] - off[:-1]).to(torch.int32)
+    surv = deg >= 1 if hub <= 0 else (deg >= 1) & (deg <= hub)
+    cdeg = torch.where(surv, deg, torch.zeros_like(deg))
+    m = keys.numel()
+    pref = torch.zeros(m + 1, dtype=torch.int64, device=keys.device)
+    carry = torch.zeros((), dtype=torch.int64, device=keys.device)
+    for b in range(0, m, chunk):
+        e = min(m, b + chunk)
+        c = cdeg[keys[b:e].to(torch.int64)].to(torch.int64)
+        pref[b + 1:e + 1] = torch.cumsum(c, 0) + carry
+        carry = pref[e]
+    w = (pref[off[1:]] - pref[off[:-1]]).to(torch.float64)
+    w *= (span - torch.arange(span, device=w.device, dtype=torch.float64)) / max(span, 1)
+    return w.cpu()
+
+
 BLOCK_MAGIC = 0x4E4C5042  # nlp.h NLP_BLOCK_MAGIC
 
 
@@ -64,10 +90,11 @@ class Exchange:
 
     def __init__(self):
         self.cap = None
+        self.ranges = None  # shard bounds, computed once (the weights' prefix sum is O(span))
 
 
 def _grow(mx, max_edges):
-    return int(min(max_edges, max(1024, mx + mx // 4)))
+    return int(min(max_edges, max(1024, mx + mx // 16)))
 
 
 def write_header(block, n):
@@ -104,12 +131,14 @@ def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=N
         a fresh one costs one extra all_gather of the counts.
     Returns (edges, k, info) -- identical on every rank."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    ub, ue = shard_ranges(span, world, weights)[rank]
+    state = state if state is not None else Exchange()
+    if state.ranges is None:
+        state.ranges = shard_ranges(span, world, weights)
+    ub, ue = state.ranges[rank]
     block, n, info = local_predict(ub, ue)
     if block.shape[0] < max_edges + 1:
         raise ValueError("local block must hold max_edges + 1 entries")
     write_header(block, n)
-    state = state if state is not None else Exchange()
     if state.cap is None:
         cnt = torch.tensor([n], dtype=torch.int64, device=block.device)
         counts = torch.empty(world, dtype=torch.int64, device=block.device)

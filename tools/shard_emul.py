@@ -37,7 +37,8 @@ def main():
     res = {"ranks": N, "k": k}
     with nlp.Graph.from_device(off, keys) as G:
         span = G.info()["span"]
-        ranges = dmod.shard_ranges(span, N)
+        ranges = dmod.shard_ranges(span, N, dmod.source_weights(off, keys, hub) if os.environ.get("BALANCE", "1") == "1"
+                                   else None)
         local = [torch.empty((k + 1, 3), dtype=torch.int32, device="cuda") for _ in range(N)]
         out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
         full = torch.empty((k, 3), dtype=torch.int32, device="cuda")
