@@ -48,7 +48,32 @@ struct GraphView {
   const uint64_t* toff;
   const uint32_t* tkeys;
   const double* ctab;
+  const uint32_t* efilt;  // edge filter: bit edge_slot(u, w) set for every adjacency entry w in N(u)
+  uint32_t efbits;        // log2 of its bit count (0: no filter)
 };
+
+// Slot of (u, w) in the edge filter: a 64-bit mix (murmur3 finaliser), top bits.
+__device__ __forceinline__ uint64_t edge_slot(uint32_t u, uint32_t w, uint32_t bits) {
+  uint64_t x = ((uint64_t)u << 32) | w;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x >> (64 - bits);
+}
+
+// One wave per row u: set the filter bit of every (u, w), w in N(u).
+__global__ __launch_bounds__(256) void k_edge_filter(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                                                     uint64_t S, uint32_t* __restrict__ filt, uint32_t bits) {
+  const uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= S) return;
+  const uint64_t a = off[u], b = off[u + 1];
+  for (uint64_t j = a + (threadIdx.x & 63); j < b; j += 64) {
+    const uint64_t h = edge_slot((uint32_t)u, keys[j], bits);
+    atomicOr(&filt[h >> 5], 1u << (h & 31));
+  }
+}
 
 // ---------------------------------------------------------------- path 1 scans
 // Compaction of surviving intermediates v (0 < deg v <= H, |I(v)| > 0); also

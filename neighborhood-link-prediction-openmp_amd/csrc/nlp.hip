@@ -125,6 +125,8 @@ struct nlp_graph {
   uint32_t maxdeg = 0;
   double* ctab_aa = nullptr;  // 1.0 / log((double)d), d = 0..maxdeg  (predict.hxx:788)
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
+  uint32_t* efilt = nullptr;  // edge filter of the first-order exclusion (k_sp_runs)
+  uint32_t efbits = 0;
   uint64_t* host_small = nullptr;  // pinned counters
   uint64_t* host_ctr = nullptr;    // host-mapped counters written by the last kernel (sort path)
   uint64_t* host_ctr_dev = nullptr;
@@ -141,6 +143,13 @@ struct nlp_graph {
   uint32_t* vbydeg = nullptr;
   std::vector<uint64_t> dstart;                // class d occupies [dstart[d], dstart[d + 1]) (class 1 at 0)
   bool use_dindex = true;                      // NLP_NO_DINDEX=1: always scan deg[] for survivors
+  // the same index restricted to a source range (k_range_index; multi-GPU shards)
+  uint32_t* rx_vbydeg = nullptr;               // capacity dstart[DCAP + 1], allocated once
+  unsigned long long* rx_cnt = nullptr;        // DCAP + 1 class counters / cursors
+  std::vector<uint64_t> rx_dstart;             // class starts of the range index
+  uint64_t rx_ua = 0, rx_ub = 0;
+  uint32_t rx_H = 0;                           // classes 1..rx_H built (0: none)
+  bool use_rindex = true;                      // NLP_NO_RINDEX=1: ranged calls scan the full index
   // NLP_STAMP=<file>: per-workgroup phase stamps of the timed stage appended to <file> (diagnostics)
   uint64_t* d_stamp = nullptr;
   uint32_t stamp_blocks = 0;
@@ -266,6 +275,9 @@ void destroy_graph(nlp_graph* g) {
   if (g->vbydeg) (void)hipFree(g->vbydeg);
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
+  if (g->efilt) (void)hipFree(g->efilt);
+  if (g->rx_vbydeg) (void)hipFree(g->rx_vbydeg);
+  if (g->rx_cnt) (void)hipFree(g->rx_cnt);
   for (int i = 0; i < 8; ++i)
     if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
   for (int i = 0; i < 5; ++i)
@@ -401,6 +413,26 @@ nlp_status finish_graph(nlp_graph* g) {
   TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
   LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
   TRY(hipGetLastError());
+  // Edge filter for the first-order exclusion of the scoring kernel: one bit per
+  // (u, w) hash slot, 16 slots per adjacency entry (~6 % of non-edges hit a set
+  // bit and are searched; every edge is).  NLP_EDGE_FILTER=0 disables it.
+  {
+    const char* ef = getenv("NLP_EDGE_FILTER");
+    if (M > 0 && !(ef && ef[0] == '0')) {
+      uint32_t bits = 20;
+      while (bits < 33 && (1ull << bits) < 16 * M) ++bits;
+      size_t fr = 0, tot = 0;
+      TRY(hipMemGetInfo(&fr, &tot));
+      if ((1ull << bits) / 8 < fr / 16) {
+        TRY(hipMalloc(&g->efilt, (1ull << bits) / 8));
+        TRY(hipMemsetAsync(g->efilt, 0, (1ull << bits) / 8, st));
+        hipLaunchKernelGGL(k_edge_filter, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, (const uint64_t*)g->off,
+                           (const uint32_t*)g->keys, S, g->efilt, bits);
+        TRY(hipGetLastError());
+        g->efbits = bits;
+      }
+    }
+  }
   // AA / RA contribution tables, computed on the host with the same libm the
   // reference uses (glibc log), indexed by degree.
   std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
@@ -434,6 +466,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
   }
   if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
+  if (const char* nr = getenv("NLP_NO_RINDEX")) g->use_rindex = nr[0] != '1';
   if (const char* hm = getenv("NLP_HASH")) g->hash_mode = hm[0] == '1' ? 1 : (hm[0] == '0' ? -1 : 0);
   if (const char* hw = getenv("NLP_HASH_MIN_WEDGES")) g->hp_min_wedges = strtoull(hw, nullptr, 10);
   if (const char* he = getenv("NLP_HASH_EMIT")) g->hp_emit = strtoull(he, nullptr, 10);
@@ -729,7 +762,8 @@ nlp_status arena_init(nlp_graph* g, int id, uint64_t desc_words, Arena& A, const
 }
 
 GraphView view_of(nlp_graph* g, int metric) {
-  return GraphView{g->off, g->keys, g->deg, g->toff, g->tkeys, metric == M_AA ? g->ctab_aa : g->ctab_ra};
+  return GraphView{g->off,  g->keys, g->deg, g->toff, g->tkeys, metric == M_AA ? g->ctab_aa : g->ctab_ra,
+                   g->efilt, g->efbits};
 }
 
 template <class F>
@@ -1552,6 +1586,40 @@ inline int key_bits(uint64_t x) {  // bits needed for the values 0..x (at least 
   return b;
 }
 
+// Degree-class index of classes 1..H restricted to the intermediates with an
+// in-neighbour in [ua, ub) (k_range_index), built on the graph's stream once per
+// (range, H) and kept; every ranged call checks it before its kernels run, so a
+// replayed graph of another range never sees a stale index.
+nlp_status ensure_range_index(nlp_graph* g, uint64_t ua, uint64_t ub, uint32_t H) {
+  if (g->rx_H >= H && g->rx_ua == ua && g->rx_ub == ub) return NLP_OK;
+  hipStream_t st = g->stream;
+  if (!g->rx_vbydeg) {
+    TRY(hipMalloc(&g->rx_vbydeg, std::max<uint64_t>(g->dstart[DCAP + 1], 1) * 4));
+    TRY(hipMalloc(&g->rx_cnt, (DCAP + 1) * 8));
+  }
+  const uint64_t n = g->dstart[H + 1];
+  const GraphView gv = view_of(g, M_CN);
+  TRY(hipMemsetAsync(g->rx_cnt, 0, (DCAP + 1) * 8, st));
+  hipLaunchKernelGGL(k_range_index<false>, dim3(grid_for(n)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg, n, H,
+                     ua, ub, g->rx_cnt, (uint32_t*)nullptr);
+  TRY(hipGetLastError());
+  std::vector<unsigned long long> c(H + 1);
+  TRY(hipMemcpyAsync(c.data(), g->rx_cnt, (H + 1) * 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  g->rx_dstart.assign(H + 2, 0);
+  for (uint32_t d = 1; d <= H; ++d) g->rx_dstart[d + 1] = g->rx_dstart[d] + c[d];
+  std::vector<unsigned long long> cur(g->rx_dstart.begin(), g->rx_dstart.begin() + H + 1);
+  TRY(hipMemcpyAsync(g->rx_cnt, cur.data(), (H + 1) * 8, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_range_index<true>, dim3(grid_for(n)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg, n, H, ua,
+                     ub, g->rx_cnt, g->rx_vbydeg);
+  TRY(hipGetLastError());
+  TRY(hipStreamSynchronize(st));
+  g->rx_ua = ua;
+  g->rx_ub = ub;
+  g->rx_H = H;
+  return NLP_OK;
+}
+
 nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int msd_passes) {
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
@@ -1584,6 +1652,12 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.dindex = g->use_dindex && !custom && p.H >= 1 && p.H <= DCAP && g->vbydeg;
   f.nv = f.dindex ? g->dstart[p.H + 1] : 0;
   f.survivors = f.dindex ? g->vbydeg : f.surv;
+  if (f.dindex && g->use_rindex && (ua > 0 || ub < S)) {  // a shard: its own, smaller index
+    nlp_status s = ensure_range_index(g, ua, ub, p.H);
+    if (s != NLP_OK) return s;
+    f.nv = g->rx_dstart[p.H + 1];
+    f.survivors = g->rx_vbydeg;
+  }
   const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + EX_TILE - 1) / EX_TILE;
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, RS_BINS);
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;

@@ -248,6 +248,52 @@ __global__ __launch_bounds__(NT) void k_deg_class_scatter(const uint32_t* __rest
   }
 }
 
+// ---------------------------------------------------------------- per-range degree-class index
+// A multi-GPU rank predicts one source range [ua, ub) of its graph replica; only
+// the intermediates with an in-neighbour u in the range emit wedges.  The
+// index of classes 1..H restricted to them is built once per (range, H): pass 1
+// counts them per class, the host turns the counts into class starts, pass 2
+// scatters them (order inside a class arbitrary, like the full index).
+__device__ __forceinline__ bool in_neighbour_in_range(const GraphView& g, uint32_t v, uint64_t ua, uint64_t ub) {
+  uint64_t lo = g.toff[v], hi = g.toff[v + 1];
+  const uint64_t end = hi;
+  while (lo < hi) {  // first u >= ua in the ascending list I(v)
+    const uint64_t mid = (lo + hi) >> 1;
+    if (g.tkeys[mid] < ua) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < end && g.tkeys[lo] < ub;
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(NT) void k_range_index(GraphView g, const uint32_t* __restrict__ vbydeg, uint64_t n,
+                                                    uint32_t H, uint64_t ua, uint64_t ub,
+                                                    unsigned long long* __restrict__ cnt, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_c[DCAP + 1];
+  __shared__ unsigned long long s_base[DCAP + 1];
+  for (uint64_t base = (uint64_t)blockIdx.x * NT; base < n; base += (uint64_t)gridDim.x * NT) {
+    for (uint32_t d = threadIdx.x; d <= H; d += NT) s_c[d] = 0;
+    __syncthreads();
+    const uint64_t i = base + threadIdx.x;
+    uint32_t v = 0, d = 0, slot = 0;
+    bool keep = false;
+    if (i < n) {
+      v = vbydeg[i];
+      keep = in_neighbour_in_range(g, v, ua, ub);
+      if (keep) {
+        d = g.deg[v];
+        slot = atomicAdd(&s_c[d], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c <= H; c += NT)
+      if (s_c[c]) s_base[c] = atomicAdd(&cnt[c], (unsigned long long)s_c[c]);
+    __syncthreads();
+    if (SCATTER && keep) out[s_base[d] + slot] = v;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- wedge records
 // One thread per survivor v (ascending): for each in-edge u -> v with u in
 // [ua, ub), the wedges (u, v, w) with w in N(v), w > u.  Records beyond capW are
@@ -1641,6 +1687,10 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
         rl[j] = via_w ? g.tkeys + tw : g.keys + ou;
         tg[j] = via_w ? ru[j] : rw[j];
         ln[j] = via_w ? iw : du[j];
+        if (g.efbits) {  // not in the edge filter: w is not in N(u), no search
+          const uint64_t h = edge_slot(ru[j], rw[j], g.efbits);
+          if (!((g.efilt[h >> 5] >> (h & 31)) & 1u)) ln[j] = 0;
+        }
       } else {
         rl[j] = g.keys;
         tg[j] = 0;

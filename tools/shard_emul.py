@@ -43,28 +43,35 @@ def main():
         out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
         full = torch.empty((k, 3), dtype=torch.int32, device="cuda")
         nf, _ = G.predict_device(mid, hub, k, full)  # warm + the single-range answer
-        pred_ms, merge_ms, copy_ms = [], [], []
-        counts = None
-        for step in range(args.steps + 1):
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(N + 3)]
-            counts = []
-            ev[0].record(st)
-            for r, (ub, ue) in enumerate(ranges):
+        # each rank's steps back to back on its own range (a rank keeps one range,
+        # so its per-range state -- the range index, captured graphs -- stays warm)
+        pred_ms, counts = [], []
+        for r, (ub, ue) in enumerate(ranges):
+            ts = []
+            for step in range(args.steps + 1):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
                 c, _ = G.predict_device(mid, hub, k, local[r][1:], ub, ue, stream=st)
                 dmod.write_header(local[r], c)
-                counts.append(c)
-                ev[r + 1].record(st)
-            stride = dmod._grow(max(counts), k) + 1
+                e1.record(st)
+                torch.cuda.synchronize()
+                if step:
+                    ts.append(e0.elapsed_time(e1))
+            pred_ms.append(float(np.mean(ts)))
+            counts.append(c)
+        stride = dmod._grow(max(counts), k) + 1
+        merge_ms, copy_ms = [], []
+        for step in range(args.steps + 1):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record(st)
             blocks = torch.stack([b[:stride] for b in local])  # stands in for the all_gather
-            ev[N + 1].record(st)
+            ev[1].record(st)
             kk = G.merge_blocks_device(blocks, k, out, stream=st)
-            ev[N + 2].record(st)
+            ev[2].record(st)
             torch.cuda.synchronize()
-            if step == 0:
-                continue  # warmup
-            pred_ms.append([ev[r].elapsed_time(ev[r + 1]) for r in range(N)])
-            copy_ms.append(ev[N].elapsed_time(ev[N + 1]))
-            merge_ms.append(ev[N + 1].elapsed_time(ev[N + 2]))
+            if step:
+                copy_ms.append(ev[0].elapsed_time(ev[1]))
+                merge_ms.append(ev[1].elapsed_time(ev[2]))
         ok = kk == nf and torch.equal(out[:kk], full[:nf])
         if not ok:  # diagnose: each rank's block against the single-range result restricted to its range
             fa = full[:nf].cpu().numpy()
@@ -84,7 +91,7 @@ def main():
                 diag["merge_first_diff"] = [i, fa[i].view(np.uint32).tolist(), mo[i].view(np.uint32).tolist()]
             res["diag"] = diag
         res.update(counts=counts, stride=stride, merged=kk, equal_single_range=bool(ok),
-                   predict_ms_per_rank=[float(np.mean([p[r] for p in pred_ms])) for r in range(N)],
+                   predict_ms_per_rank=pred_ms,
                    block_copy_ms=float(np.mean(copy_ms)), merge_ms=float(np.mean(merge_ms)))
     print(json.dumps(res), flush=True)
     if not res["equal_single_range"]:
