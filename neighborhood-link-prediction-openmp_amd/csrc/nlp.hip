@@ -2510,7 +2510,8 @@ nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t 
 
 nlp_status nlp_merge_blocks_device(nlp_graph* g, const nlp_edge* d_blocks, uint64_t stride, uint32_t nblocks,
                                    uint64_t max_edges, nlp_edge* d_out, uint64_t* out_count, void* stream) {
-  if (!g || !out_count || !d_blocks || stride < 1 || nblocks < 1 || nblocks > 65535 || (max_edges && !d_out))
+  if (!g || !out_count || !d_blocks || stride < 1 || nblocks < 1 || nblocks > 65535 || (max_edges && !d_out) ||
+      (uint64_t)nblocks * stride >= (1ull << 32))  // merge ranks are 32-bit
     return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;

@@ -241,9 +241,11 @@ __device__ __forceinline__ uint64_t merge_rank(P list, uint64_t lo, uint64_t hi,
   return lo;
 }
 
-// MT_W: windows average ~MT_T / 2 keys on balanced shards (C2 x8: 404, none
-// beyond 2048; at 512 a third of them fall back to global searches).
+// MT_W: windows average ~0.4 MT_T keys on balanced shards (C2 x8: 404, none
+// beyond 2048; at 512 a third fall back to global searches, with 2048-entry
+// tiles a fifth).
 constexpr int MT_NT = NT, MT_PER = 4, MT_T = MT_NT * MT_PER, MT_G = 8, MT_W = 2048;
+static_assert((MT_W & (MT_W - 1)) == 0, "the branchless window search steps by powers of two");
 
 // Bounds of every (block r, tile x, block q), 4 words at bnd[4 * ((r * tiles + x) * nb + q)]:
 // {rank of the tile's first (largest) key, rank of its last (smallest) key,
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(MT_NT) void k_merge_blocks(const EdgeOut* __restric
                                                         unsigned long long* __restrict__ dbg) {
   __shared__ uint32_t s_win[MT_G][MT_W];
   __shared__ uint32_t s_dkey[MT_T];
-  __shared__ uint64_t s_drank[MT_T];
+  __shared__ uint32_t s_drank[MT_T];  // < 2^32: the host caps the total entries
   __shared__ uint64_t s_b[MT_G][4];
   __shared__ uint64_t s_red[NWAVE + 1];
   if (ctr[2]) return;
@@ -346,12 +348,30 @@ __global__ __launch_bounds__(MT_NT) void k_merge_blocks(const EdgeOut* __restric
       s_b[j][t & 3] = q < nb ? bnd[4 * (((uint64_t)r * gridDim.x + blockIdx.x) * nb + q) + (t & 3)] : 0;
     }
     __syncthreads();
+    {
+      // stage the windows: the first 2 * MT_NT keys of every window with all loads
+      // in flight at once (one round trip), the rare longer tails after
+      constexpr int C0 = 2;
+      uint32_t wv[MT_G][C0];
 #pragma unroll
-    for (int j = 0; j < MT_G; ++j) {
-      const uint64_t lo = s_b[j][2], len = s_b[j][3] > lo ? s_b[j][3] - lo : 0;
-      if (len <= MT_W) {
+      for (int j = 0; j < MT_G; ++j) {
+        const uint64_t lo = s_b[j][2], len = s_b[j][3] > lo ? s_b[j][3] - lo : 0;
         const uint32_t* kq = keys + (uint64_t)(q0 + j) * stride + lo;
-        for (uint32_t x = t; x < len; x += MT_NT) s_win[j][x] = kq[x];
+#pragma unroll
+        for (int c = 0; c < C0; ++c) {
+          const uint32_t x = t + c * MT_NT;
+          wv[j][c] = (len <= MT_W && x < len) ? kq[x] : 0u;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MT_G; ++j) {
+        const uint64_t lo = s_b[j][2], len = s_b[j][3] > lo ? s_b[j][3] - lo : 0;
+        if (len > MT_W) continue;
+#pragma unroll
+        for (int c = 0; c < C0; ++c)
+          if (t + c * MT_NT < len) s_win[j][t + c * MT_NT] = wv[j][c];
+        const uint32_t* kq = keys + (uint64_t)(q0 + j) * stride + lo;
+        for (uint32_t x = t + C0 * MT_NT; x < len; x += MT_NT) s_win[j][x] = kq[x];
       }
     }
     __syncthreads();
@@ -404,7 +424,7 @@ __global__ __launch_bounds__(MT_NT) void k_merge_blocks(const EdgeOut* __restric
           add += q < r ? merge_rank<true>(kq, lo, hi, kd) : merge_rank<false>(kq, lo, hi, kd);
         }
       }
-      s_drank[d] += add;
+      s_drank[d] += (uint32_t)add;
     }
     __syncthreads();
   }
