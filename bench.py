@@ -136,6 +136,7 @@ def main():
     spec = (n * world, m * world, alpha, seed, d, metric, hub)
     t0 = time.time()
     off, keys, du, dw, info = gg.make_workload(spec, "cuda")
+    torch.cuda.empty_cache()  # hand the generator's cached blocks back: libnlp allocates with hipMalloc
     torch.cuda.synchronize()
     gen_s = time.time() - t0
     t0 = time.time()

@@ -77,6 +77,47 @@ def permutation(n, seed, stream, device):
     return torch.sort(k, stable=True).indices
 
 
+# Device sorts, boolean indexing and nonzero break beyond 2^31 items on this
+# torch build: larger tensors go through the chunked helpers below.
+BIG = 1 << 30
+
+
+def masked(x, m, limit=None):
+    """x[m] in chunks (boolean indexing breaks beyond 2^31 items)."""
+    limit = limit or BIG
+    if x.numel() <= limit:
+        return x[m]
+    return torch.cat([a[b] for a, b in zip(torch.split(x, limit), torch.split(m, limit))])
+
+
+def nonzero1(m, limit=None):
+    """torch.nonzero(m)[:, 0] of a 1-d mask, in chunks."""
+    limit = limit or BIG
+    if m.numel() <= limit:
+        return torch.nonzero(m).squeeze(1)
+    return torch.cat([torch.nonzero(c).squeeze(1) + i * limit for i, c in enumerate(torch.split(m, limit))])
+
+
+def big_unique(x, limit=None):
+    """torch.unique (sorted) for tensors beyond the device sort's 2^31-item
+    limit: the value range is cut into buckets of at most ~limit items each."""
+    limit = limit or BIG
+    if x.numel() <= limit:
+        return torch.unique(x)
+    lo, hi = int(x.min()), int(x.max()) + 1
+    nb = 2 * ((x.numel() + limit - 1) // limit)
+    if hi - lo < 2 * nb:  # few distinct values: nothing to split on
+        return torch.unique(x)
+    edges = [lo + (hi - lo) * i // nb for i in range(nb + 1)]
+    parts = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        # boolean indexing breaks beyond 2^31 items: mask chunk by chunk
+        sub = torch.cat([c[(c >= a) & (c < b)] for c in torch.split(x, limit)])
+        parts.append(big_unique(sub, limit) if sub.numel() > limit else torch.unique(sub))
+        del sub
+    return torch.cat(parts)
+
+
 def chung_lu_edges(n, m, alpha, seed, device="cpu"):
     """Return (src, dst) int64 tensors of m distinct directed edges, ids in 1..n.
 
@@ -105,17 +146,37 @@ def chung_lu_edges(n, m, alpha, seed, device="cpu"):
         del u, v, ok
         have += todo
         if have >= draws:
-            allk = torch.unique(torch.cat(keys))
+            allk = big_unique(torch.cat(keys))
             keys = [allk]
             if allk.numel() >= m:
                 break
             draws = int((m - allk.numel()) * 1.3) + 1024
             have = 0
     allk = keys[0]
-    if allk.numel() > m:
+    if allk.numel() > m and allk.numel() > BIG:
+        allk = _select_m(allk, m, seed, device)
+    elif allk.numel() > m:
         sel = permutation(allk.numel(), seed, 4, device)[:m]
         allk = torch.sort(allk[sel]).values
     return allk // (n + 1), allk % (n + 1)
+
+
+def _select_m(allk, m, seed, device):
+    """m of the sorted keys allk, chosen by the smallest random 64-bit tags
+    (splitmix64 of the position), without sorting all of them (the device sort
+    stops at 2^31 items): a histogram of the tags' top 16 bits fixes the cut,
+    only the boundary bin is sorted.  Returns the chosen keys in sorted order."""
+    base = _s64(((seed * 0x100000001B3) ^ (4 * 0xC2B2AE3D27D4EB4F)) & _M64)
+    tag = splitmix64(torch.arange(allk.numel(), dtype=torch.int64, device=device) + base)
+    top = _srl(tag, 48)
+    cnt = torch.cumsum(torch.bincount(top, minlength=1 << 16), 0)
+    b = int(torch.searchsorted(cnt, torch.tensor(m, device=device, dtype=cnt.dtype)))
+    below = int(cnt[b - 1]) if b > 0 else 0
+    keep = top < b
+    inb = nonzero1(top == b)
+    order = torch.sort(tag[inb]).indices[: m - below]
+    keep[inb[order]] = True
+    return masked(allk, keep)  # allk is sorted, so is the selection
 
 
 def symmetric_csr(n, src, dst):
@@ -123,7 +184,7 @@ def symmetric_csr(n, src, dst):
     deduplicated graph, span = n+1 (row 0 empty)."""
     span = n + 1
     a = torch.cat([src * span + dst, dst * span + src])
-    a = torch.unique(a)  # sorted
+    a = big_unique(a)  # sorted
     rows = a // span
     keys = (a % span).to(torch.int32)
     del a
@@ -162,14 +223,13 @@ def delete_edges(offsets, keys, frac, seed, n=None):
     r = uniform(seed, 6, 0, u.numel(), dev)
     vi = torch.floor(r * deg[u].double()).long()
     v = keys[offsets[u] + vi].long()
-    pairs = torch.unique(torch.cat([u * span + v, v * span + u]))
+    pairs = big_unique(torch.cat([u * span + v, v * span + u]))
     rows = csr_rows(offsets, M)
     ek = rows * span + keys.long()
-    pos = torch.searchsorted(pairs, ek).clamp_(max=pairs.numel() - 1)
-    drop = pairs[pos] == ek
-    keep = ~drop
-    keys2 = keys[keep]
-    counts = torch.bincount(rows[keep], minlength=span)
+    keep = torch.cat([pairs[torch.searchsorted(pairs, c).clamp_(max=pairs.numel() - 1)] != c
+                      for c in torch.split(ek, BIG)])  # chunked: searchsorted stops at 2^31 items
+    keys2 = masked(keys, keep)
+    counts = torch.bincount(masked(rows, keep), minlength=span)
     off2 = torch.zeros(span + 1, dtype=torch.int64, device=dev)
     off2[1:] = torch.cumsum(counts, 0)
     return off2, keys2, (pairs // span).to(torch.int32), (pairs % span).to(torch.int32)

@@ -37,6 +37,8 @@ def main():
     gg = nlp_loader.load_sub("graphgen")
     off, keys, du, dw, info = gg.make_workload(gg.CONFIGS[args.config], "cuda")
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # hand the generator's cached blocks back: libnlp allocates with hipMalloc
+    torch.cuda.synchronize()
     k = info["k"]
     G = nlp.Graph.from_device(off, keys)
     out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
@@ -45,14 +47,24 @@ def main():
         cores = min(16, len(os.sched_getaffinity(0)))
     except AttributeError:
         cores = min(16, os.cpu_count() or 1)
-    tmp = tempfile.mkdtemp()
-    csr = os.path.join(tmp, "g.csr")
-    with open(csr, "wb") as f:
-        o = off.cpu().numpy().astype(np.uint64)
-        np.array([len(o) - 1, keys.numel()], np.uint64).tofile(f)
-        o.tofile(f)
-        keys.cpu().numpy().view(np.uint32).tofile(f)
     cpu_hubs = {int(h) for h in args.cpu_hubs.split(",") if h}
+    csr = None
+    if cpu_hubs:  # the reference driver reads the CSR from a file
+        tmp = tempfile.mkdtemp()
+        csr = os.path.join(tmp, "g.csr")
+        with open(csr, "wb") as f:
+            o = off.cpu().numpy().astype(np.uint64)
+            np.array([len(o) - 1, keys.numel()], np.uint64).tofile(f)
+            o.tofile(f)
+            keys.cpu().numpy().view(np.uint32).tofile(f)
+    # algorithmic bytes of the reference's wedge scan per call,
+    # B_alg(H) = 8(S+1) + 4M + 4M + 8 P_H + 4 W_H + 12 k_out
+    degs = (off[1:] - off[:-1]).double()
+    span, nnz = off.numel() - 1, keys.numel()
+
+    def b_alg(H, kout):
+        sv = degs[(degs > 0) & ((degs <= H) if H > 0 else (degs > 0))]
+        return 8 * (span + 1) + 8 * nnz + 8 * float(sv.sum()) + 4 * float((sv * sv).sum()) + 12 * kout
     cpu_metrics = set(args.cpu_metrics.split(","))
     for metric in args.metrics.split(","):
         mid = nlp.METRICS.index(metric)
@@ -65,8 +77,11 @@ def main():
             line = {"config": args.config, "metric": metric, "H": H, "k": k, "predicted": cnt,
                     "gpu_ms": wall, "score_ms": t["score_ms"], "select_ms": t["select_ms"], "path": t["path"],
                     "chunks": t["chunks"], "wedges": t["wedges"], "candidates": t["candidates"],
-                    "gpu_predicted_per_s": cnt / (wall / 1e3), "gpu_wedges_per_s": t["wedges"] / (wall / 1e3)}
-            if H in cpu_hubs and metric in cpu_metrics and os.path.exists(drv):
+                    "gpu_predicted_per_s": cnt / (wall / 1e3), "gpu_wedges_per_s": t["wedges"] / (wall / 1e3),
+                    "n": span - 1, "M": nnz}
+            ba = b_alg(H, cnt)
+            line.update(call_alg_bytes=ba, call_effective_gbs=ba / (wall / 1e3) / 1e9)
+            if csr and H in cpu_hubs and metric in cpu_metrics and os.path.exists(drv):
                 me = min(k, t["candidates"])
                 env = dict(os.environ, OMP_NUM_THREADS=str(cores))
                 r = subprocess.run([drv, "time", csr, str(mid), str(H), str(me), str(cores), "1"], capture_output=True,
