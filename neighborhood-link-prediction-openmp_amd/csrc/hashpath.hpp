@@ -216,7 +216,6 @@ __device__ __forceinline__ float hp_score(const HpArgs& a, uint32_t u, uint64_t 
 constexpr int HP_STG = 128;
 
 struct HpStage {
-  uint32_t* key;  // HP_STG entries each
   uint32_t* u;
   uint32_t* w;
   float* s;
@@ -247,7 +246,7 @@ __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
     const uint64_t p = pos + i;
     if (p < a.cap) {
       const uint64_t q = a.base + p;
-      a.ckey[q] = st.key[i];
+      a.ckey[q] = score_key(st.s[i]);  // recomputed: 12 B per staged entry
       a.cu[q] = st.u[i];
       a.cw[q] = st.w[i];
       a.cs[q] = st.s[i];
@@ -272,7 +271,6 @@ __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid
   if (st.n + n > st.cap) hp_flush(st, a);
   if (out) {
     const uint32_t i = st.n + (uint32_t)__popcll(mo & ((1ull << lane_id()) - 1));
-    st.key[i] = key;
     st.u[i] = u;
     st.w[i] = w;
     st.s[i] = s;
@@ -430,27 +428,103 @@ __global__ void k_hp_bounds(const uint64_t* __restrict__ wpre, uint64_t nU, uint
 }
 
 // ---------------------------------------------------------------- bin 0: wave per row, LDS table
-template <bool CUSTOM>
+// Bin 0 is split into table-size tiers (HP_TIER_W): a row of W(u) <= 128 needs
+// at most a 256-entry table, and the LDS of a 1024-entry table per wave
+// (45 KB per workgroup) holds the kernel to 3 waves per SIMD -- too few to
+// hide the random graph reads of a small row.  k_hp_tier partitions the
+// chunk's bin-0 rows by tier (order within a tier is free: candidates are
+// emitted unordered), and one k_hp_wave<TW> launch per tier reads its slice
+// and row count from the device.
+constexpr int HP_NTIER = 3;
+__host__ __device__ constexpr uint64_t hp_tier_w(int t) { return t == 0 ? 128 : t == 1 ? 256 : HP_B0_MAX; }
+
+// tcnt: [0, 3) rows per tier (counted by the first pass), [3, 6) cursors.
+// Counts and cursor reservations are aggregated per workgroup in LDS (one
+// global atomic per workgroup and tier: a chip-wide stream of atomics on
+// three words serialises at their L2 channel).
+template <bool SCATTER>
+__global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ rows, uint64_t nrows,
+                                                const uint64_t* __restrict__ wu, uint64_t ua,
+                                                uint32_t* __restrict__ tcnt, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_n[NWAVE][HP_NTIER];
+  __shared__ uint32_t s_base[HP_NTIER];
+  const int lane = lane_id(), wv = wave_id();
+  uint32_t tb[HP_NTIER] = {0, 0, 0};
+  if (SCATTER)
+    for (int q = 1; q < HP_NTIER; ++q) tb[q] = tb[q - 1] + tcnt[q - 1];
+  uint32_t cnt[HP_NTIER] = {0, 0, 0};  // COUNT pass: this thread's rows per tier (lane 0 holds the wave's)
+  for (uint64_t b0 = (uint64_t)blockIdx.x * NT; b0 < nrows; b0 += (uint64_t)gridDim.x * NT) {
+    const uint64_t i = b0 + threadIdx.x;
+    uint32_t u = 0;
+    int t = -1;
+    if (i < nrows) {
+      u = rows[i];
+      const uint64_t W = wu[u - ua];
+      t = W <= hp_tier_w(0) ? 0 : W <= hp_tier_w(1) ? 1 : 2;
+    }
+    uint64_t m[HP_NTIER];
+#pragma unroll
+    for (int q = 0; q < HP_NTIER; ++q) {
+      m[q] = __ballot(t == q);
+      if (!SCATTER) cnt[q] += lane == 0 ? (uint32_t)__popcll(m[q]) : 0u;
+    }
+    if (!SCATTER) continue;
+    if (lane == 0)
+      for (int q = 0; q < HP_NTIER; ++q) s_n[wv][q] = (uint32_t)__popcll(m[q]);
+    __syncthreads();
+    if (threadIdx.x < HP_NTIER) {
+      uint32_t tot = 0;
+      for (int w = 0; w < NWAVE; ++w) tot += s_n[w][threadIdx.x];
+      s_base[threadIdx.x] = tot ? atomicAdd(&tcnt[HP_NTIER + threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    if (t >= 0) {
+      uint32_t pre = 0;
+      for (int w = 0; w < wv; ++w) pre += s_n[w][t];
+      out[tb[t] + s_base[t] + pre + (uint32_t)__popcll(m[t] & ((1ull << lane) - 1))] = u;
+    }
+    __syncthreads();
+  }
+  if (!SCATTER) {
+    if (lane == 0)
+      for (int q = 0; q < HP_NTIER; ++q) s_n[wv][q] = cnt[q];
+    __syncthreads();
+    if (threadIdx.x < HP_NTIER) {
+      uint32_t tot = 0;
+      for (int w = 0; w < NWAVE; ++w) tot += s_n[w][threadIdx.x];
+      if (tot) atomicAdd(&tcnt[threadIdx.x], tot);
+    }
+  }
+}
+
+template <bool CUSTOM, int TW = HP_WT, int STG = HP_STG>
 __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
-                                                const uint64_t* __restrict__ wu, uint64_t ua) {
-  constexpr int VT = CUSTOM ? HP_WT : 1;
-  __shared__ uint32_t s_k[NWAVE][HP_WT];
-  __shared__ uint32_t s_c[NWAVE][HP_WT];
+                                                const uint64_t* __restrict__ wu, uint64_t ua,
+                                                const uint32_t* __restrict__ tcnt = nullptr, int tier = 0) {
+  constexpr int VT = CUSTOM ? TW : 1;
+  __shared__ uint32_t s_k[NWAVE][TW];
+  __shared__ uint32_t s_c[NWAVE][TW];
   __shared__ uint32_t s_v0[NWAVE][VT];
   __shared__ uint32_t s_v1[NWAVE][VT];
   __shared__ uint32_t s_incl[NWAVE][64];
   __shared__ uint64_t s_start[NWAVE][64];
   __shared__ uint32_t s_iv[NWAVE][64];
-  __shared__ uint32_t s_gk[NWAVE][HP_STG], s_gu[NWAVE][HP_STG], s_gw[NWAVE][HP_STG];
-  __shared__ float s_gs[NWAVE][HP_STG];
+  __shared__ uint32_t s_gu[NWAVE][STG], s_gw[NWAVE][STG];
+  __shared__ float s_gs[NWAVE][STG];
   const int lane = lane_id(), wv = wave_id();
+  if (tcnt) {  // tier slice of the partitioned list
+    uint32_t base = 0;
+    for (int r = 0; r < tier; ++r) base += tcnt[r];
+    rows += base;
+    nrows = tcnt[tier];
+  }
   const HpTable tb{s_k[wv], s_c[wv], s_v0[wv], s_v1[wv]};
-  for (int i = lane; i < HP_WT; i += 64) {
+  for (int i = lane; i < TW; i += 64) {
     s_k[wv][i] = HP_EMPTY;
     s_c[wv][i] = 0;
     if (CUSTOM) { s_v0[wv][i] = HP_EMPTY; s_v1[wv][i] = 0; }
   }
-  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_STG, 0, 0, 0};
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   wave_sync_lds();
@@ -459,6 +533,10 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
     const uint64_t W = wu[u - ua];
     const int lg = max(6, log2_ceil(2 * W));
     const uint32_t T = 1u << lg, mask = T - 1;
+    if (T > (uint32_t)TW) {  // a row outside this tier (a partition bug): fail the call, never overrun LDS
+      if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+      continue;
+    }
     const int shift = 32 - lg;
     const uint64_t o0 = a.g.off[u], o1 = a.g.off[u + 1];
     const uint64_t du = o1 - o0;
@@ -527,7 +605,7 @@ __device__ __forceinline__ uint64_t block_incl_scan_1024(uint64_t x, uint64_t* s
   return pre + inc;
 }
 
-constexpr int HP_BSTG = 64;  // staging per wave in the block kernels
+constexpr int HP_BSTG = 128;  // staging per wave in the block kernels
 
 // Workgroup barrier.  A global table is accessed with agent-scope atomics at
 // L2, so the barrier must also wait for this wave's outstanding global
@@ -556,7 +634,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   __shared__ uint32_t s_iv[HP_BNT];
   __shared__ uint64_t s_w[NW];
   __shared__ uint64_t s_tot;
-  __shared__ uint32_t s_gk[NW][HP_BSTG], s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
   const int t = threadIdx.x, wv = wave_id();
   const uint64_t tmax = GLOBAL ? (1ull << tlog) : (uint64_t)LT;
@@ -574,7 +652,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
       if (CUSTOM) { s_v0[i] = HP_EMPTY; s_v1[i] = 0; }
     }
   }
-  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   __syncthreads();
@@ -746,7 +824,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
   __shared__ uint32_t s_bc[HP_PMAX];   // wedges per bucket
   __shared__ uint32_t s_bo[HP_PMAX];   // scratch offset per bucket (group-relative), then scatter cursor
   __shared__ uint32_t s_g1, s_gdirect, s_xcur;
-  __shared__ uint32_t s_gk[NW][HP_BSTG], s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
   const int t = threadIdx.x, wv = wave_id();
   const HpTable tb{s_k, s_c, s_v0, s_v1};
@@ -757,7 +835,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
   }
   uint32_t* sw = scratch + (uint64_t)blockIdx.x * scap * (CUSTOM ? 2 : 1);
   uint32_t* sv = sw + scap;
-  HpStage sg{s_gk[wv], s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   __syncthreads();

@@ -68,7 +68,7 @@ enum Buf {
   B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
-  B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND,
+  B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER,
   NBUF
 };
 
@@ -198,6 +198,7 @@ struct nlp_graph {
   // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
   uint64_t hp_emit = 0;
   int hp_minbin = 0, hp_one_bucket = 0;
+  int hp_tiers = 1;  // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
   uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
@@ -473,6 +474,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hb = getenv("NLP_HASH_MINBIN")) g->hp_minbin = std::min(3, std::max(0, atoi(hb)));
   if (const char* hc = getenv("NLP_HASH_SCAP")) g->hp_scap_force = std::max<uint64_t>(64, strtoull(hc, nullptr, 10));
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
+  if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* mp = getenv("NLP_MSD_PASSES")) g->msd_force = std::min(2, std::max(0, atoi(mp)));
@@ -1273,6 +1275,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipGetLastError());
   }
   uint32_t* lists[HP_NBINS];
+  uint32_t* tlist;  // bin-0 rows of a chunk by tier, then 8 tier counters
+  TRY(wsget(ws, B_HP_TIER, nU + 8, &tlist));
+  uint32_t* tcnt = tlist + nU;
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
   for (int b = 0; b < HP_NBINS; ++b) {
     TRY(wsget(ws, lb[b], nU, &lists[b]));
@@ -1331,7 +1336,29 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.ctr = (unsigned long long*)small;
     a.one_bucket = g->hp_one_bucket;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
-    if (n0) {
+    if (n0 && g->hp_tiers) {
+      // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
+      TRY(hipMemsetAsync(tcnt, 0, 8 * sizeof(uint32_t), st));
+      const unsigned gt = (unsigned)std::min<uint64_t>((n0 + NT - 1) / NT, 512);
+      hipLaunchKernelGGL(k_hp_tier<false>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[0] + q0[0]), n0,
+                         (const uint64_t*)wu, ua, tcnt, tlist);
+      hipLaunchKernelGGL(k_hp_tier<true>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[0] + q0[0]), n0,
+                         (const uint64_t*)wu, ua, tcnt, tlist);
+      TRY(hipGetLastError());
+      const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
+      const uint32_t* tl = tlist;
+      const uint32_t* tc = tcnt;
+      if (custom) {
+        hipLaunchKernelGGL((k_hp_wave<true, 256, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 0);
+        hipLaunchKernelGGL((k_hp_wave<true, 512, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 1);
+        hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
+      } else {
+        hipLaunchKernelGGL((k_hp_wave<false, 256, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 0);
+        hipLaunchKernelGGL((k_hp_wave<false, 512, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 1);
+        hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
+      }
+      TRY(hipGetLastError());
+    } else if (n0) {
       const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
       if (custom) hipLaunchKernelGGL(k_hp_wave<true>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
       else hipLaunchKernelGGL(k_hp_wave<false>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);

@@ -403,10 +403,11 @@ class _env:
 
 # path 4 (hash accumulation) with every kernel forced: 0 wave/LDS, 1 workgroup/LDS,
 # 2 w-bucket partitioning, 3 partitioning with a tiny scratch (bucket groups and
-# direct accumulation), 4 one bucket per row (sub-range passes)
+# direct accumulation), 4 one bucket per row (sub-range passes), 5 bin 0 as one
+# 1024-entry launch (no table-size tiers)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1")]
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_TIERS="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
