@@ -807,7 +807,7 @@ __device__ __forceinline__ void hp_scan_buckets(uint32_t* s, uint32_t n, uint64_
 template <bool CUSTOM>
 __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
                                                     const uint64_t* __restrict__ wu, uint64_t ua,
-                                                    uint32_t* __restrict__ scratch, uint64_t scap) {
+                                                    uint32_t* __restrict__ scratch, uint64_t scap, uint32_t nsl) {
   constexpr int LT = CUSTOM ? HP_BT / 2 : HP_BT;
   constexpr int VT = CUSTOM ? LT : 1;
   constexpr int NW = HP_BNT / 64;
@@ -839,7 +839,14 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   __syncthreads();
-  for (uint64_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+  // Work items are (row, slice): slice sl of a row owns buckets
+  // [P sl / nsl, P (sl + 1) / nsl), so that a few huge rows (bin 3) spread
+  // over many workgroups instead of holding one CU each while the chip idles.
+  // Every slice enumerates the whole row (the lists are hot in L2) and keeps
+  // only its buckets' wedges.
+  for (uint64_t it = blockIdx.x; it < nrows * nsl; it += gridDim.x) {
+    const uint64_t ri = it / nsl;
+    const uint32_t sl = (uint32_t)(it - ri * nsl);
     const uint32_t u = rows[ri];
     const uint64_t W = wu[u - ua];
     const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
@@ -854,26 +861,32 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
     if (pd > HP_PMAX) pd = HP_PMAX;
     const int shift = log2_ceil((span_w + pd - 1) / pd);
     const uint32_t P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
+    const uint32_t bs0 = (uint32_t)((uint64_t)P * sl / nsl), bs1 = (uint32_t)((uint64_t)P * (sl + 1) / nsl);
+    if (bs0 == bs1) continue;  // an empty slice (uniform across the workgroup)
     for (uint32_t b = t; b < P; b += HP_BNT) s_bc[b] = 0;
-    if (t == 0) {  // exclusion cursor: first entry of N(u) above u
+    if (t == 0) {  // exclusion cursor: first entry of N(u) in the slice, i.e. >= u + 1 + (bs0 << shift)
+      const uint64_t x0 = (uint64_t)u + 1 + ((uint64_t)bs0 << shift);
       uint64_t lo = 0, hi = du;
       while (lo < hi) {
         const uint64_t m = (lo + hi) >> 1;
-        if (a.g.keys[o0 + m] <= u) lo = m + 1; else hi = m;
+        if ((uint64_t)a.g.keys[o0 + m] < x0) lo = m + 1; else hi = m;
       }
       s_xcur = (uint32_t)lo;
     }
     __syncthreads();
-    // pass A: wedges per bucket
+    // pass A: wedges per bucket of the slice
     hp_enum_row(a, u, o0, du, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t) {
-      ++wedges;
-      atomicAdd(&s_bc[(w - u - 1) >> shift], 1u);
+      const uint32_t b = (w - u - 1) >> shift;
+      if (b >= bs0 && b < bs1) {
+        ++wedges;
+        atomicAdd(&s_bc[b], 1u);
+      }
     });
-    for (uint32_t b0 = 0; b0 < P;) {
+    for (uint32_t b0 = bs0; b0 < bs1;) {
       if (t == 0) {
         uint64_t sum = 0;
         uint32_t b = b0;
-        while (b < P && sum + s_bc[b] <= scap) sum += s_bc[b++];
+        while (b < bs1 && sum + s_bc[b] <= scap) sum += s_bc[b++];
         s_gdirect = b == b0 ? 1u : 0u;
         s_g1 = b == b0 ? b0 + 1 : b;
       }

@@ -198,7 +198,8 @@ struct nlp_graph {
   // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
   uint64_t hp_emit = 0;
   int hp_minbin = 0, hp_one_bucket = 0;
-  int hp_tiers = 1;  // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
+  int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
+  uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
   uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
@@ -475,6 +476,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hc = getenv("NLP_HASH_SCAP")) g->hp_scap_force = std::max<uint64_t>(64, strtoull(hc, nullptr, 10));
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
+  if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* mp = getenv("NLP_MSD_PASSES")) g->msd_force = std::min(2, std::max(0, atoi(mp)));
@@ -1373,9 +1375,12 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     for (int b = 2; b < HP_NBINS; ++b) {  // rows beyond an LDS table: w-bucket partitioning
       const uint64_t nb = q1[b] - q0[b];
       if (!nb) continue;
-      const unsigned gr = (unsigned)std::min<uint64_t>(nb, g->hp_gp);
-      if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap);
-      else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap);
+      // fewer rows than workgroups: slice each row's w-buckets over several workgroups
+      const uint32_t nsl = g->hp_slices ? g->hp_slices
+                                        : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g->hp_gp / nb, 256));
+      const unsigned gr = (unsigned)std::min<uint64_t>(nb * nsl, g->hp_gp);
+      if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl);
+      else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl);
       TRY(hipGetLastError());
     }
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));

@@ -404,10 +404,13 @@ class _env:
 # path 4 (hash accumulation) with every kernel forced: 0 wave/LDS, 1 workgroup/LDS,
 # 2 w-bucket partitioning, 3 partitioning with a tiny scratch (bucket groups and
 # direct accumulation), 4 one bucket per row (sub-range passes), 5 bin 0 as one
-# 1024-entry launch (no table-size tiers)
+# 1024-entry launch (no table-size tiers), 6/7 partitioned rows sliced over
+# several workgroups (bucket slices, exclusion cursor per slice)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_TIERS="0")]
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_TIERS="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_SLICES="7"),
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
@@ -456,7 +459,8 @@ def test_gpu_hash_path_all_candidates_and_min_score(gpu, golden, oracle):
 def test_gpu_hash_path_star_hub(gpu, oracle):
     """A hub source whose row holds > 10^4 distinct second hops (bins 2 and 3)."""
     off, keys = star_csr(20000)
-    for v in (dict(), dict(NLP_HASH_SCAP="5000"), dict(NLP_HASH_ONE_BUCKET="1")):
+    for v in (dict(), dict(NLP_HASH_SCAP="5000"), dict(NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_SLICES="1"),
+              dict(NLP_HASH_SLICES="13", NLP_HASH_SCAP="5000")):
         with _env(NLP_HASH="1", **v):
             with gpu.Graph(off, keys) as G:
                 for m, H, k in ((0, 0, 500), (7, 0, 30000), (1, 2, 10 ** 6), (8, 4, 100)):
