@@ -745,9 +745,13 @@ constexpr int HP_PMAX = 4096;
 
 // Row expansion shared by the passes: calls f(w, v) for every wedge (u, v, w)
 // with w > u, v surviving; every thread of the workgroup must call it.
-template <class F>
+// With a w-range [wlo, whi) (a row slice of k_hp_part) each list N(v) is cut to
+// that range by two binary searches (lists are sorted), so a slice enumerates
+// only its own wedges; wlo = 0 enumerates whole lists.
+template <typename F>
 __device__ __forceinline__ void hp_enum_row(const HpArgs& a, uint32_t u, uint64_t o0, uint64_t du, uint64_t* s_incl,
-                                            uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f) {
+                                            uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f,
+                                            uint64_t wlo = 0, uint64_t whi = 0) {
   const int t = threadIdx.x;
   for (uint64_t base = 0; base < du; base += HP_BNT) {
     const uint64_t i = base + t;
@@ -759,6 +763,21 @@ __device__ __forceinline__ void hp_enum_row(const HpArgs& a, uint32_t u, uint64_
       if (hp_surv(d, a.H)) {
         len = d;
         st = a.g.off[v];
+        if (wlo) {
+          const uint32_t* L = a.g.keys + st;
+          uint32_t l = 0, h = d;
+          while (l < h) {
+            const uint32_t m = (l + h) >> 1;
+            if ((uint64_t)L[m] < wlo) l = m + 1; else h = m;
+          }
+          uint32_t e = l, h2 = d;
+          while (e < h2) {
+            const uint32_t m = (e + h2) >> 1;
+            if ((uint64_t)L[m] < whi) e = m + 1; else h2 = m;
+          }
+          st += l;
+          len = e - l;
+        }
       }
     }
     const uint64_t incl = block_incl_scan_1024(len, s_w);
@@ -863,6 +882,9 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
     const uint32_t P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
     const uint32_t bs0 = (uint32_t)((uint64_t)P * sl / nsl), bs1 = (uint32_t)((uint64_t)P * (sl + 1) / nsl);
     if (bs0 == bs1) continue;  // an empty slice (uniform across the workgroup)
+    // w-range of the slice for the enumeration (0: whole lists when the row is not sliced)
+    const uint64_t slo0 = nsl > 1 ? (uint64_t)u + 1 + ((uint64_t)bs0 << shift) : 0;
+    const uint64_t shi0 = nsl > 1 ? std::min<uint64_t>(a.S, (uint64_t)u + 1 + ((uint64_t)bs1 << shift)) : 0;
     for (uint32_t b = t; b < P; b += HP_BNT) s_bc[b] = 0;
     if (t == 0) {  // exclusion cursor: first entry of N(u) in the slice, i.e. >= u + 1 + (bs0 << shift)
       const uint64_t x0 = (uint64_t)u + 1 + ((uint64_t)bs0 << shift);
@@ -881,7 +903,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
         ++wedges;
         atomicAdd(&s_bc[b], 1u);
       }
-    });
+    }, slo0, shi0);
     for (uint32_t b0 = bs0; b0 < bs1;) {
       if (t == 0) {
         uint64_t sum = 0;
@@ -905,7 +927,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
             sw[p] = w;
             if (CUSTOM) sv[p] = v;
           }
-        });
+        }, slo0, shi0);
         hp_sync<true>();
       }
       // buckets of the group, ascending w
@@ -941,7 +963,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
           } else {
             hp_enum_row(a, u, o0, du, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t v) {
               if ((uint64_t)w >= slo && (uint64_t)w < shi) hp_insert<false, CUSTOM>(tb, mask, hs, w, v, &a.ctr[HPC_ERR]);
-            });
+            }, slo, shi);
           }
           // first-order exclusion: the entries of N(u) in [slo, shi) (cursor walk)
           for (;;) {
