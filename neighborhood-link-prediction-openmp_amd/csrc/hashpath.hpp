@@ -621,7 +621,8 @@ __device__ __forceinline__ void hp_sync() {
 template <bool CUSTOM, bool GLOBAL>
 __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
                                                      const uint64_t* __restrict__ wu, uint64_t ua,
-                                                     uint32_t* __restrict__ slab, int tlog) {
+                                                     uint32_t* __restrict__ slab, int tlog,
+                                                     uint32_t* __restrict__ queue = nullptr) {
   constexpr int LT = GLOBAL ? 1 : (CUSTOM ? HP_BT / 2 : HP_BT);
   constexpr int VT = CUSTOM ? LT : 1;
   constexpr int NW = HP_BNT / 64;
@@ -636,6 +637,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   __shared__ uint64_t s_tot;
   __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
+  __shared__ uint64_t s_it;
   const int t = threadIdx.x, wv = wave_id();
   const uint64_t tmax = GLOBAL ? (1ull << tlog) : (uint64_t)LT;
   HpTable tb;
@@ -656,7 +658,16 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   __syncthreads();
-  for (uint64_t ri = blockIdx.x; ri < nrows; ri += gridDim.x) {
+  // rows from a work queue when one is given (row costs vary), else a static stride
+  for (uint64_t r0 = blockIdx.x;; r0 += gridDim.x) {
+    uint64_t ri = r0;
+    if (queue) {
+      if (t == 0) s_it = atomicAdd(queue, 1u);
+      __syncthreads();
+      ri = s_it;
+      __syncthreads();
+    }
+    if (ri >= nrows) break;
     const uint32_t u = rows[ri];
     const uint64_t W = wu[u - ua];
     const uint64_t o0 = a.g.off[u], o1 = a.g.off[u + 1];
@@ -826,7 +837,8 @@ __device__ __forceinline__ void hp_scan_buckets(uint32_t* s, uint32_t n, uint64_
 template <bool CUSTOM>
 __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
                                                     const uint64_t* __restrict__ wu, uint64_t ua,
-                                                    uint32_t* __restrict__ scratch, uint64_t scap, uint32_t nsl) {
+                                                    uint32_t* __restrict__ scratch, uint64_t scap, uint32_t nsl,
+                                                    uint32_t* __restrict__ queue) {
   constexpr int LT = CUSTOM ? HP_BT / 2 : HP_BT;
   constexpr int VT = CUSTOM ? LT : 1;
   constexpr int NW = HP_BNT / 64;
@@ -843,6 +855,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
   __shared__ uint32_t s_bc[HP_PMAX];   // wedges per bucket
   __shared__ uint32_t s_bo[HP_PMAX];   // scratch offset per bucket (group-relative), then scatter cursor
   __shared__ uint32_t s_g1, s_gdirect, s_xcur;
+  __shared__ uint64_t s_it;
   __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
   const int t = threadIdx.x, wv = wave_id();
@@ -862,8 +875,16 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
   // [P sl / nsl, P (sl + 1) / nsl), so that a few huge rows (bin 3) spread
   // over many workgroups instead of holding one CU each while the chip idles.
   // Every slice enumerates the whole row (the lists are hot in L2) and keeps
-  // only its buckets' wedges.
-  for (uint64_t it = blockIdx.x; it < nrows * nsl; it += gridDim.x) {
+  // only its buckets' wedges.  Items are taken from a work queue (one atomic
+  // per item): row costs vary by orders of magnitude, and a static stride left
+  // a few workgroups with the heavy rows.
+  const uint64_t nit = nrows * nsl;
+  for (;;) {
+    if (t == 0) s_it = atomicAdd(queue, 1u);
+    __syncthreads();
+    const uint64_t it = s_it;
+    __syncthreads();
+    if (it >= nit) break;
     const uint64_t ri = it / nsl;
     const uint32_t sl = (uint32_t)(it - ri * nsl);
     const uint32_t u = rows[ri];

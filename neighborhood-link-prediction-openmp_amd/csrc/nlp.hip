@@ -1277,8 +1277,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipGetLastError());
   }
   uint32_t* lists[HP_NBINS];
-  uint32_t* tlist;  // bin-0 rows of a chunk by tier, then 8 tier counters
-  TRY(wsget(ws, B_HP_TIER, nU + 8, &tlist));
+  uint32_t* tlist;  // bin-0 rows of a chunk by tier, then counters: [0, 6) tiers, [6, 9) work queues of bins 2, 3, 1
+  TRY(wsget(ws, B_HP_TIER, nU + 16, &tlist));
   uint32_t* tcnt = tlist + nU;
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
   for (int b = 0; b < HP_NBINS; ++b) {
@@ -1366,10 +1366,11 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       else hipLaunchKernelGGL(k_hp_wave<false>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
       TRY(hipGetLastError());
     }
+    TRY(hipMemsetAsync(tcnt + 6, 0, 3 * sizeof(uint32_t), st));  // work queues of bins 2, 3 and 1
     if (n1) {
       const unsigned gr = (unsigned)std::min<uint64_t>(n1, 2048);
-      if (custom) hipLaunchKernelGGL((k_hp_block<true, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13);
-      else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13);
+      if (custom) hipLaunchKernelGGL((k_hp_block<true, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
+      else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
       TRY(hipGetLastError());
     }
     for (int b = 2; b < HP_NBINS; ++b) {  // rows beyond an LDS table: w-bucket partitioning
@@ -1379,8 +1380,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       const uint32_t nsl = g->hp_slices ? g->hp_slices
                                         : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g->hp_gp / nb, 256));
       const unsigned gr = (unsigned)std::min<uint64_t>(nb * nsl, g->hp_gp);
-      if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl);
-      else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl);
+      if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl, tcnt + 4 + b);
+      else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl, tcnt + 4 + b);
       TRY(hipGetLastError());
     }
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
