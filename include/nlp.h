@@ -120,15 +120,34 @@ nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uin
                           int* symmetric);
 
 /* predictLinks<Metric>Omp<hub_max_degree>(G, {repeat, max_edges, min_score}).
- * `out` is a caller-owned HOST array of at least max_edges entries (it may be
- * NULL when max_edges == 0).  *out_count receives the number of predicted
+ * `out` is a caller-owned HOST array of at least min(max_edges, number of
+ * candidates) entries, or NULL.  *out_count receives the number of predicted
  * links (< max_edges when there are fewer candidates; the reference's
  * OpenMP merge reads out of bounds in that case).
- * max_edges = UINT64_MAX means "all candidates" (then `out` must hold them:
- * query the count first with max_edges = 0 -> t->candidates). */
+ * max_edges = UINT64_MAX means "all candidates".  Count query: pass
+ * out = NULL (any max_edges, typically UINT64_MAX); the links are computed and
+ * kept on the device, *out_count holds their number, and nlp_copy_last
+ * fetches them without predicting again.  max_edges = 0 predicts nothing
+ * (*out_count = 0, t->candidates = 0), like the reference's `o.maxEdges > 0`
+ * guard (predict.hxx:367,429). */
 nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
                        uint64_t max_edges, int repeat, nlp_edge* out, uint64_t* out_count,
                        nlp_timing* t);
+
+/* Same with the reference's MAXFACTOR2 template parameter (predict.hxx:221,295):
+ * max_factor2 > 0 keeps a second-hop candidate w of source u only when
+ * deg(w) <= max_factor2 * deg(u) (the clause deg(u) <= MAXFACTOR2 * deg(u) of
+ * that filter always holds for MAXFACTOR2 >= 1).  max_factor2 = 0 is
+ * nlp_predict. */
+nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
+                          float min_score, uint64_t max_edges, int repeat, nlp_edge* out, uint64_t* out_count,
+                          nlp_timing* t);
+
+/* Copy the first min(n, *count of the last prediction*) links of the last
+ * nlp_predict / nlp_predict_ex / nlp_predict_device result of this handle to the
+ * HOST array `out` (*copied = how many).  Valid until the next prediction on
+ * the handle.  This is the second half of the count query above. */
+nlp_status nlp_copy_last(nlp_graph* g, nlp_edge* out, uint64_t n, uint64_t* copied);
 
 /* Device-resident variant for a source-vertex range [u_begin, u_end) (the
  * multi-GPU shard; pass 0, UINT64_MAX for all).  `d_out` is a DEVICE array of
@@ -138,6 +157,11 @@ nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree,
 nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
                               uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
                               uint64_t* out_count, nlp_timing* t, void* stream);
+
+/* nlp_predict_device with MAXFACTOR2 (see nlp_predict_ex). */
+nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
+                                 float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end,
+                                 nlp_edge* d_out, uint64_t* out_count, nlp_timing* t, void* stream);
 
 /* Merge step of the multi-GPU path: given `n` device-resident edges that are the
  * concatenation, in ascending source-range order, of per-shard canonical

@@ -20,9 +20,10 @@
 //     schedule;
 //   * with fewer candidates than maxEdges all candidates are returned (the
 //     reference's OpenMP merge reads out of bounds, A.2);
-//   * MAXFACTOR2 != 0 and FORCEHEAP are accepted and ignored (MAXFACTOR2 is
-//     always 0 in the reference and its branch is a no-op bug, predict.hxx:295;
-//     FORCEHEAP only changes the reference's heap bookkeeping);
+//   * MAXFACTOR2 > 0 keeps a candidate w of u only when deg(w) <= MAXFACTOR2 *
+//     deg(u), the reference's second-hop filter (predict.hxx:221,295; its other
+//     clause, deg(u) <= MAXFACTOR2 * deg(u), always holds); FORCEHEAP only
+//     changes the reference's heap bookkeeping and is accepted and ignored;
 //   * the generic predictLinksWithIntersection[Omp](x, o, VT, fs, fu) takes
 //     arbitrary lambdas, which cannot cross the C ABI: not provided;
 //   * errors throw std::runtime_error (the reference has no error reporting).
@@ -136,21 +137,23 @@ class HipGraph {
 /** predictLinks<Metric>Omp on a resident graph. */
 template <class K = uint32_t, class W = float>
 inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric metric, uint32_t mindegree1,
-                                               const PredictLinkOptions<W>& o) {
+                                               const PredictLinkOptions<W>& o, uint32_t maxfactor2 = 0) {
   nlp_timing t{};
   uint64_t n = 0;
   const uint64_t me = o.maxEdges == size_t(-1) ? UINT64_MAX : uint64_t(o.maxEdges);
   std::vector<nlp_edge> buf;
-  if (me == UINT64_MAX) {  // all candidates: count, then fetch
-    check(nlp_predict(g.get(), metric, mindegree1, float(o.minScore), me, o.repeat, nullptr, &n, &t), "nlp_predict");
+  if (me == UINT64_MAX) {  // all candidates: predict once (count query), then fetch the kept result
+    check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat, nullptr, &n, &t),
+          "nlp_predict_ex");
     buf.resize(n);
-    check(nlp_predict(g.get(), metric, mindegree1, float(o.minScore), n, o.repeat, buf.data(), &n, &t),
-          "nlp_predict");
+    uint64_t got = 0;
+    check(nlp_copy_last(g.get(), buf.data(), n, &got), "nlp_copy_last");
+    n = got;
   } else {
     buf.resize(me);
-    check(nlp_predict(g.get(), metric, mindegree1, float(o.minScore), me, o.repeat, me ? buf.data() : nullptr, &n,
-                      &t),
-          "nlp_predict");
+    check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat,
+                         me ? buf.data() : nullptr, &n, &t),
+          "nlp_predict_ex");
   }
   std::vector<std::tuple<K, K, W>> a;
   a.reserve(n);
@@ -161,15 +164,16 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
 template <class G, class W>
 inline PredictLinkResult<typename G::key_type, W> predictLinksHipAny(const G& x, nlp_metric metric,
                                                                      uint32_t mindegree1,
-                                                                     const PredictLinkOptions<W>& o) {
+                                                                     const PredictLinkOptions<W>& o,
+                                                                     uint32_t maxfactor2 = 0) {
   HipGraph g(x);
-  return predictLinksHip<typename G::key_type, W>(g, metric, mindegree1, o);
+  return predictLinksHip<typename G::key_type, W>(g, metric, mindegree1, o, maxfactor2);
 }
 
 template <class W>
 inline PredictLinkResult<uint32_t, W> predictLinksHipAny(const HipGraph& g, nlp_metric metric, uint32_t mindegree1,
-                                                         const PredictLinkOptions<W>& o) {
-  return predictLinksHip<uint32_t, W>(g, metric, mindegree1, o);
+                                                         const PredictLinkOptions<W>& o, uint32_t maxfactor2 = 0) {
+  return predictLinksHip<uint32_t, W>(g, metric, mindegree1, o, maxfactor2);
 }
 
 }  // namespace nlp
@@ -178,15 +182,18 @@ inline PredictLinkResult<uint32_t, W> predictLinksHipAny(const HipGraph& g, nlp_
 #define NLP_DEFINE_PREDICTOR(NAME, METRIC)                                                                 \
   template <int MINDEGREE1 = 4, int MAXFACTOR2 = 0, bool FORCEHEAP = false, class G, class W = float>    \
   inline auto predictLinks##NAME(const G& x, const PredictLinkOptions<W>& o = {}) {                      \
-    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o);                                  \
+    static_assert(MINDEGREE1 >= 0 && MAXFACTOR2 >= 0, "negative MINDEGREE1 / MAXFACTOR2");              \
+    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o, uint32_t(MAXFACTOR2));           \
   }                                                                                                       \
   template <int MINDEGREE1 = 4, int MAXFACTOR2 = 0, bool FORCEHEAP = false, class G, class W = float>    \
   inline auto predictLinks##NAME##Omp(const G& x, const PredictLinkOptions<W>& o = {}) {                 \
-    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o);                                  \
+    static_assert(MINDEGREE1 >= 0 && MAXFACTOR2 >= 0, "negative MINDEGREE1 / MAXFACTOR2");              \
+    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o, uint32_t(MAXFACTOR2));           \
   }                                                                                                       \
   template <int MINDEGREE1 = 4, int MAXFACTOR2 = 0, bool FORCEHEAP = false, class G, class W = float>    \
   inline auto predictLinks##NAME##Hip(const G& x, const PredictLinkOptions<W>& o = {}) {                 \
-    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o);                                  \
+    static_assert(MINDEGREE1 >= 0 && MAXFACTOR2 >= 0, "negative MINDEGREE1 / MAXFACTOR2");              \
+    return nlp::predictLinksHipAny(x, METRIC, uint32_t(MINDEGREE1), o, uint32_t(MAXFACTOR2));           \
   }
 
 NLP_DEFINE_PREDICTOR(CommonNeighbors, NLP_CN)

@@ -57,8 +57,9 @@ class Timing(ctypes.Structure):
 
 EXPORTS = [
     "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
-    "nlp_predict_device", "nlp_select_edges_device", "nlp_merge_blocks_device", "nlp_set_truth",
-    "nlp_count_common_device", "nlp_last_common", "nlp_status_string", "nlp_metric_name", "nlp_version",
+    "nlp_predict_ex", "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_select_edges_device",
+    "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
+    "nlp_metric_name", "nlp_version",
 ]
 
 _lib = None
@@ -82,7 +83,10 @@ def lib(build_if_missing=True):
     L.nlp_graph_destroy.restype = None
     L.nlp_graph_info.argtypes = [vp, P(u64), P(u64), P(u32), P(i32)]
     L.nlp_predict.argtypes = [vp, i32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
+    L.nlp_predict_ex.argtypes = [vp, i32, u32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
+    L.nlp_copy_last.argtypes = [vp, vp, u64, P(u64)]
     L.nlp_predict_device.argtypes = [vp, i32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
+    L.nlp_predict_device_ex.argtypes = [vp, i32, u32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
     L.nlp_select_edges_device.argtypes = [vp, vp, u64, u64, vp, P(u64), vp]
     L.nlp_merge_blocks_device.argtypes = [vp, vp, u64, u32, u64, vp, P(u64), vp]
     L.nlp_set_truth.argtypes = [vp, vp, vp, u64]
@@ -93,9 +97,9 @@ def lib(build_if_missing=True):
     L.nlp_metric_name.argtypes = [i32]
     L.nlp_metric_name.restype = ctypes.c_char_p
     L.nlp_version.restype = i32
-    for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict",
-              "nlp_predict_device", "nlp_select_edges_device", "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device",
-              "nlp_last_common"):
+    for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict", "nlp_predict_ex",
+              "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_select_edges_device",
+              "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -112,6 +116,28 @@ def _metric(m):
     if not 0 <= int(m) <= 8:
         raise ValueError("metric out of range")
     return int(m)
+
+
+def _check_tensor(t, name, dtypes, device=None, min_numel=0):
+    """Raise ValueError unless `t` is a contiguous torch tensor of one of
+    `dtypes` on the GPU (`device`: the graph's ordinal) with >= min_numel
+    elements: the library gets t.data_ptr() and trusts its layout."""
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise ValueError("%s must be a torch tensor" % name)
+    if t.dtype not in dtypes:
+        raise ValueError("%s must have dtype %s, got %s" % (name, "/".join(str(d) for d in dtypes), t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    if not t.is_cuda or (device is not None and t.device.index != device):
+        raise ValueError("%s must live on cuda:%s, got %s" % (name, device, t.device))
+    if t.numel() < min_numel:
+        raise ValueError("%s too small: %d elements, need %d" % (name, t.numel(), min_numel))
+
+
+def _edge_dtypes():
+    import torch
+    return (torch.int32, torch.uint32) if hasattr(torch, "uint32") else (torch.int32,)
 
 
 def _stream_ptr(stream, tensor=None):
@@ -166,9 +192,13 @@ class Graph:
     @classmethod
     def from_device(cls, offsets, keys, device=None, stream=None):
         """From torch tensors already on the GPU (int64 offsets, int32 keys)."""
+        import torch
         L = lib()
         g = cls.__new__(cls)
         dev = offsets.device.index if device is None else device
+        _check_tensor(offsets, "offsets", (torch.int64,) + ((torch.uint64,) if hasattr(torch, "uint64") else ()),
+                      dev, 1)
+        _check_tensor(keys, "keys", (torch.int32,) + ((torch.uint32,) if hasattr(torch, "uint32") else ()), dev)
         span = offsets.numel() - 1
         h = ctypes.c_void_p()
         _check(L.nlp_graph_create_device(offsets.data_ptr(), keys.data_ptr() if keys.numel() else None, span,
@@ -184,37 +214,46 @@ class Graph:
                "nlp_graph_info")
         return dict(span=s.value, nnz=m.value, max_degree=d.value, symmetric=bool(y.value))
 
-    def predict(self, metric, hub, max_edges=None, min_score=0.0, repeat=1):
-        """Host-output predict: returns (u, v, score) numpy arrays and the timing dict."""
+    def predict(self, metric, hub, max_edges=None, min_score=0.0, repeat=1, maxfactor2=0):
+        """Host-output predict: returns (u, v, score) numpy arrays and the timing dict.
+        maxfactor2: the reference's MAXFACTOR2 template parameter (0 = off)."""
         L = lib()
         m = _metric(metric)
         me = UINT64_MAX if max_edges is None or max_edges < 0 else int(max_edges)
         t = Timing()
         cnt = ctypes.c_uint64()
         if me == UINT64_MAX:
-            # count first (out = NULL), then fetch
-            _check(L.nlp_predict(self._h, m, int(hub), float(min_score), me, int(repeat), None,
-                                 ctypes.byref(cnt), ctypes.byref(t)), "nlp_predict")
-            me = cnt.value
-        out = np.zeros(max(me, 1), dtype=EDGE_DTYPE)
-        _check(L.nlp_predict(self._h, m, int(hub), float(min_score), me, int(repeat), out.ctypes.data if me else None,
-                             ctypes.byref(cnt), ctypes.byref(t)), "nlp_predict")
-        n = cnt.value
+            # all candidates: one prediction kept on the device (out = NULL), then fetched
+            _check(L.nlp_predict_ex(self._h, m, int(hub), int(maxfactor2), float(min_score), me, int(repeat), None,
+                                    ctypes.byref(cnt), ctypes.byref(t)), "nlp_predict_ex")
+            out = np.zeros(max(cnt.value, 1), dtype=EDGE_DTYPE)
+            got = ctypes.c_uint64()
+            _check(L.nlp_copy_last(self._h, out.ctypes.data, cnt.value, ctypes.byref(got)), "nlp_copy_last")
+            n = got.value
+        else:
+            out = np.zeros(max(me, 1), dtype=EDGE_DTYPE)
+            _check(L.nlp_predict_ex(self._h, m, int(hub), int(maxfactor2), float(min_score), me, int(repeat),
+                                    out.ctypes.data if me else None, ctypes.byref(cnt), ctypes.byref(t)),
+                   "nlp_predict_ex")
+            n = cnt.value
         out = out[:n]
         return out["u"].copy(), out["v"].copy(), out["score"].copy(), t.as_dict()
 
-    def predict_device(self, metric, hub, max_edges, out, u_begin=0, u_end=UINT64_MAX, min_score=0.0, stream=None):
+    def predict_device(self, metric, hub, max_edges, out, u_begin=0, u_end=UINT64_MAX, min_score=0.0, stream=None,
+                       maxfactor2=0):
         """Device-output predict into `out` (torch int32 [>= max_edges, 3]).  Returns (count, timing)."""
-        if out.numel() < 3 * max_edges or out.element_size() * out.numel() < 12 * max_edges:
-            raise ValueError("output tensor too small")
+        _check_tensor(out, "out", _edge_dtypes(), self.device, 3 * int(max_edges))
         t = Timing()
         cnt = ctypes.c_uint64()
-        _check(lib().nlp_predict_device(self._h, _metric(metric), int(hub), float(min_score), int(max_edges),
-                                        int(u_begin), int(u_end), out.data_ptr(), ctypes.byref(cnt),
-                                        ctypes.byref(t), _stream_ptr(stream, out)), "nlp_predict_device")
+        _check(lib().nlp_predict_device_ex(self._h, _metric(metric), int(hub), int(maxfactor2), float(min_score),
+                                           int(max_edges), int(u_begin), int(u_end), out.data_ptr(),
+                                           ctypes.byref(cnt), ctypes.byref(t), _stream_ptr(stream, out)),
+               "nlp_predict_device_ex")
         return cnt.value, t.as_dict()
 
     def select_edges_device(self, edges_in, n, max_edges, out, stream=None):
+        _check_tensor(edges_in, "edges_in", _edge_dtypes(), self.device, 3 * int(n))
+        _check_tensor(out, "out", _edge_dtypes(), self.device, 3 * min(int(n), int(max_edges)))
         cnt = ctypes.c_uint64()
         _check(lib().nlp_select_edges_device(self._h, edges_in.data_ptr(), int(n), int(max_edges), out.data_ptr(),
                                              ctypes.byref(cnt), _stream_ptr(stream, out)), "nlp_select_edges_device")
@@ -225,6 +264,11 @@ class Graph:
         of each block a header, nlp.h nlp_merge_blocks_device) into `out`.  Returns
         the merged count, or raises NlpError(NLP_ERR_CAPACITY) with .count = the
         largest block count when a block overflowed its stride."""
+        _check_tensor(blocks, "blocks", _edge_dtypes(), self.device)
+        if blocks.dim() != 3 or blocks.shape[2] != 3:
+            raise ValueError("blocks must be [nblocks, stride, 3]")
+        _check_tensor(out, "out", _edge_dtypes(), self.device,
+                      3 * min(int(max_edges), int(blocks.shape[0]) * int(blocks.shape[1])))
         cnt = ctypes.c_uint64()
         st = lib().nlp_merge_blocks_device(self._h, blocks.data_ptr(), int(blocks.shape[1]), int(blocks.shape[0]),
                                            int(max_edges), out.data_ptr(), ctypes.byref(cnt), _stream_ptr(stream, out))
@@ -243,6 +287,7 @@ class Graph:
 
     def count_common_device(self, edges, n, stream=None):
         """|insertions1 ∩ deletions0| for the first n device edges (torch int32 [>= n, 3])."""
+        _check_tensor(edges, "edges", _edge_dtypes(), self.device, 3 * int(n))
         c = ctypes.c_uint64()
         _check(lib().nlp_count_common_device(self._h, edges.data_ptr(), int(n), ctypes.byref(c),
                                              _stream_ptr(stream, edges)), "nlp_count_common_device")
@@ -272,14 +317,15 @@ class Graph:
 
 
 def _make_predictor(metric):
-    def fn(x, o=None, mindegree1=4):
+    def fn(x, o=None, mindegree1=4, maxfactor2=0):
         o = o or PredictLinkOptions()
-        u, v, s, t = x.predict(metric, mindegree1, None if o.maxEdges < 0 else o.maxEdges, o.minScore, o.repeat)
+        u, v, s, t = x.predict(metric, mindegree1, None if o.maxEdges < 0 else o.maxEdges, o.minScore, o.repeat,
+                               maxfactor2)
         edges = list(zip(u.tolist(), v.tolist(), s.tolist()))
         return PredictLinkResult(edges, t["total_ms"], t["score_ms"], t)
     fn.__name__ = "predictLinks%sHip" % METRIC_FUNCS[metric]
-    fn.__doc__ = ("predictLinks%sOmp<MINDEGREE1>(x, o) of predict.hxx on the GPU (mindegree1=0 -> IHub)."
-                  % METRIC_FUNCS[metric])
+    fn.__doc__ = ("predictLinks%sOmp<MINDEGREE1, MAXFACTOR2>(x, o) of predict.hxx on the GPU "
+                  "(mindegree1=0 -> IHub, maxfactor2=0 -> off)." % METRIC_FUNCS[metric])
     return fn
 
 

@@ -50,7 +50,62 @@ struct GraphView {
   const double* ctab;
   const uint32_t* efilt;  // edge filter: bit edge_slot(u, w) set for every adjacency entry w in N(u)
   uint32_t efbits;        // log2 of its bit count (0: no filter)
+  uint32_t maxf2;         // MAXFACTOR2 (0: off)
+  const uint64_t* etab;   // exact membership table of the entries (u, w), w > u (null: none)
+  uint32_t etbits;        // log2 of its bucket count
 };
+
+// One wave per row u: count (pass 0) or insert (pass 1) the entries w > u.
+template <bool INSERT>
+__global__ __launch_bounds__(256) void k_etab_build(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                                                    uint64_t S, uint64_t* __restrict__ tab, uint32_t bits,
+                                                    unsigned long long* __restrict__ count) {
+  const uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  uint64_t c = 0;
+  if (u < S) {
+    const uint64_t a = off[u], e = off[u + 1];
+    const uint64_t mask = (1ull << bits) - 1;
+    for (uint64_t i = a + lane; i < e; i += 64) {
+      const uint32_t w = keys[i];
+      if (w <= u) continue;
+      ++c;
+      if (!INSERT) continue;
+      const uint64_t key = (u << 32) | w;
+      uint64_t b = et_mix(key) >> (64 - bits);
+      bool done = false;
+      for (uint64_t probe = 0; probe <= mask && !done; ++probe) {
+        for (int s = 0; s < ET_SLOTS && !done; ++s) {
+          unsigned long long* q = (unsigned long long*)&tab[b * ET_SLOTS + s];
+          unsigned long long cur = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cur == ET_EMPTY) cur = atomicCAS(q, ET_EMPTY, key);
+          done = cur == ET_EMPTY || cur == key;
+        }
+        b = (b + 1) & mask;
+      }
+    }
+  }
+  if (!INSERT) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0 && c) atomicAdd(count, (unsigned long long)c);
+  }
+}
+
+// w in N(u)?  (u < w; the table when there is one, else a search of N(u))
+__device__ __forceinline__ bool first_order(const GraphView& g, uint32_t u, uint32_t w) {
+  if (g.etab) return et_has(g.etab, g.etbits, u, w);
+  return contains_u32(g.keys + g.off[u], g.deg[u], w);
+}
+
+// The reference's MAXFACTOR2 filter on second-hop keys (predict.hxx:221,295):
+// ft(w) = w > u && deg(u) <= F deg(u) && deg(w) <= F deg(u), size_t products.
+// Its first clause holds for F >= 1; the second is a per-(u, w) predicate, so a
+// w it rejects is never counted, never touched and never a candidate -- the
+// same as dropping the pair where it is scored.
+__device__ __forceinline__ bool f2_drop(const GraphView& g, uint32_t u, uint32_t w) {
+  return g.maxf2 != 0 && (uint64_t)g.deg[w] > (uint64_t)g.maxf2 * (uint64_t)g.deg[u];
+}
 
 // Slot of (u, w) in the edge filter: a 64-bit mix (murmur3 finaliser), top bits.
 __device__ __forceinline__ uint64_t edge_slot(uint32_t u, uint32_t w, uint32_t bits) {
@@ -353,13 +408,13 @@ __global__ __launch_bounds__(NT) void k_score_runs(GraphView g, int metric, floa
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < W; i += (uint64_t)gridDim.x * blockDim.x) {
     if (!st.flag[i]) continue;
     const uint32_t u = st.u[i], w = st.w[i];
-    const bool excl = contains_u32(g.keys + g.off[u], g.deg[u], w);
+    const bool excl = first_order(g, u, w);
     float sc;
     if (CUSTOM) sc = excl ? 0.0f : st.s[i];
     else sc = score_basic(metric, excl ? 0u : st.key[i], g.deg[u], g.deg[w]);
     st.key[i] = score_key(sc);
     st.s[i] = sc;
-    st.flag[i] = !(sc <= min_score) ? 1u : 0u;  // NaN passes
+    st.flag[i] = (!(sc <= min_score) && !f2_drop(g, u, w)) ? 1u : 0u;  // NaN passes
   }
 }
 
@@ -414,10 +469,12 @@ __device__ __forceinline__ void group_small(const GraphView& g, int metric, floa
 }
 
 // LDS ordering point for one wave: every lane's LDS writes before, reads after.
+// Workgroup-scope fences: a wavefront-scope fence emits no instruction and the
+// scheduler may move DS accesses across it (path 4).
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // Sort r[0..c) (padded to a power of two >= 64) in LDS by one wave, then walk

@@ -260,7 +260,7 @@ __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
 // and emission above tau; every active lane of the wave calls it.
 __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid, float s, uint32_t u, uint32_t w,
                                         int64_t tau) {
-  const bool cand = valid && !(s <= a.min_score);
+  const bool cand = valid && !(s <= a.min_score) && !f2_drop(a.g, u, w);
   st.cand += cand ? 1 : 0;
   st.nan += (cand && s != s) ? 1 : 0;
   const uint32_t key = cand ? score_key(s) : 0u;

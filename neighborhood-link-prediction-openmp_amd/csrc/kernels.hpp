@@ -46,6 +46,47 @@ __device__ __forceinline__ float score_basic(int m, uint32_t c, uint64_t du, uin
   return 0.0f;
 }
 
+// ---------------------------------------------------------------- edge membership table
+// The first-order exclusion (predict.hxx:306-307) asks, for a candidate (u, w)
+// with w > u, whether w is in N(u).  A search of the sorted list costs
+// log(deg) dependent loads; this table answers with one 64-byte line.  Built
+// once per graph (k_etab_build): open addressing over buckets of 8 u64 keys
+// (u << 32 | w), one bucket = one cache line, linear probing by bucket, at most
+// half full.  Only entries with w > u are stored (a candidate always has
+// w > u); duplicate entries (the reference's multiset rows) are stored once.
+constexpr uint64_t ET_EMPTY = ~0ull;  // u = 0xffffffff never occurs (span <= 2^32 - 1)
+constexpr int ET_SLOTS = 8;
+
+__device__ __forceinline__ uint64_t et_mix(uint64_t x) {  // murmur3 finaliser
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ bool et_has(const uint64_t* __restrict__ tab, uint32_t bits, uint32_t u, uint32_t w) {
+  const uint64_t key = ((uint64_t)u << 32) | w;
+  const uint64_t mask = (1ull << bits) - 1;
+  uint64_t b = et_mix(key) >> (64 - bits);
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const ulonglong2* p = (const ulonglong2*)(tab + b * ET_SLOTS);
+    const ulonglong2 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const uint64_t s[ET_SLOTS] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+    bool hit = false, open = false;
+#pragma unroll
+    for (int i = 0; i < ET_SLOTS; ++i) {
+      hit |= s[i] == key;
+      open |= s[i] == ET_EMPTY;
+    }
+    if (hit) return true;
+    if (open) return false;
+    b = (b + 1) & mask;
+  }
+  return false;
+}
+
 // number of entries <= x in the sorted list a[0..n)
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
@@ -258,13 +299,14 @@ __global__ void k_score(const uint64_t* __restrict__ rstart, const uint64_t* __r
                         const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
                         const uint32_t* __restrict__ deg, const double* __restrict__ ctab, int metric,
                         float min_score, uint32_t* __restrict__ ckey, uint32_t* __restrict__ cu,
-                        uint32_t* __restrict__ cw, float* __restrict__ cs, uint32_t* __restrict__ cflag) {
+                        uint32_t* __restrict__ cw, float* __restrict__ cs, uint32_t* __restrict__ cflag,
+                        uint32_t maxf2, const uint64_t* __restrict__ etab, uint32_t etbits) {
   const uint64_t R = *d_R;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t s = rstart[r], e = rstart[r + 1];
     uint64_t k = wkey[s];
     uint32_t u = (uint32_t)(k >> 32), w = (uint32_t)k;
-    bool excl = contains_u32(keys + off[u], deg[u], w);
+    bool excl = etab ? et_has(etab, etbits, u, w) : contains_u32(keys + off[u], deg[u], w);
     float sc;
     if (CUSTOM) {
       float acc = 0.0f;  // entry += 1.0/log(deg v) | 1.0/deg v, in v order
@@ -275,7 +317,8 @@ __global__ void k_score(const uint64_t* __restrict__ rstart, const uint64_t* __r
       uint32_t c = excl ? 0u : (uint32_t)(e - s);
       sc = score_basic(metric, c, deg[u], deg[w]);
     }
-    bool keep = !(sc <= min_score);
+    // MAXFACTOR2 (predict.hxx:221,295), see f2_drop
+    bool keep = !(sc <= min_score) && !(maxf2 && (uint64_t)deg[w] > (uint64_t)maxf2 * (uint64_t)deg[u]);
     ckey[r] = score_key(sc);
     cu[r] = u;
     cw[r] = w;

@@ -65,7 +65,7 @@ enum Buf {
   B_FARENA, B_FAGG,
   // sort-grouped fast path (sortpath.hpp)
   B_SP_SURV, B_SP_RK0, B_SP_RK1, B_SP_RV0, B_SP_RV1, B_SP_STASH, B_SP_CU, B_SP_CW, B_SP_CS,
-  B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA,
+  B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA, B_SP_SEGCNT,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER,
@@ -125,8 +125,10 @@ struct nlp_graph {
   uint32_t maxdeg = 0;
   double* ctab_aa = nullptr;  // 1.0 / log((double)d), d = 0..maxdeg  (predict.hxx:788)
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
-  uint32_t* efilt = nullptr;  // edge filter of the first-order exclusion (k_sp_runs)
+  uint32_t* efilt = nullptr;  // edge filter of the first-order exclusion (k_sp_runs; only without etab)
   uint32_t efbits = 0;
+  uint64_t* etab = nullptr;   // exact membership table of the entries w > u (group.hpp k_etab_build)
+  uint32_t etbits = 0;
   uint64_t* host_small = nullptr;  // pinned counters
   uint64_t* host_ctr = nullptr;    // host-mapped counters written by the last kernel (sort path)
   uint64_t* host_ctr_dev = nullptr;
@@ -154,10 +156,12 @@ struct nlp_graph {
   uint64_t* d_stamp = nullptr;
   uint32_t stamp_blocks = 0;
   std::string stamp_path;
+  int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
+  bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
                                                // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
-  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256, occ_runs = 256;
+  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256;
   bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
   int msd_force = 0;                           // NLP_MSD_PASSES: force 1 or 2 MSD passes (tests)
   int group_sort = 2;                          // NLP_GROUP_SORT: 0 k_sp_bucket sort-only, 1 k_sp_group, 2 group only after 2 MSD passes
@@ -173,6 +177,7 @@ struct nlp_graph {
     uint32_t H;
     float min_score;
     uint64_t max_edges, ua, ub, capW, gen;
+    uint32_t maxf2;
     int mode;  // fast-path variant (graph shapes differ)
     void* out;
     hipGraphExec_t exec[4];
@@ -278,6 +283,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   if (g->efilt) (void)hipFree(g->efilt);
+  if (g->etab) (void)hipFree(g->etab);
   if (g->rx_vbydeg) (void)hipFree(g->rx_vbydeg);
   if (g->rx_cnt) (void)hipFree(g->rx_cnt);
   for (int i = 0; i < 8; ++i)
@@ -415,12 +421,45 @@ nlp_status finish_graph(nlp_graph* g) {
   TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
   LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
   TRY(hipGetLastError());
-  // Edge filter for the first-order exclusion of the scoring kernel: one bit per
-  // (u, w) hash slot, 16 slots per adjacency entry (~6 % of non-edges hit a set
-  // bit and are searched; every edge is).  NLP_EDGE_FILTER=0 disables it.
+  // Exact membership table of the entries w > u for the first-order exclusion
+  // (kernels.hpp et_has): one 64-byte bucket read per candidate instead of a
+  // search of N(u).  At most half full; skipped (NLP_ETAB=0, or when it would
+  // take more than a quarter of the free HBM) in favour of the edge filter.
+  {
+    const char* et = getenv("NLP_ETAB");
+    if (M > 0 && !(et && et[0] == '0')) {
+      unsigned long long* cnt;
+      TRY(wsget(g->ws, B_HP_SMALL, 8, &cnt));
+      TRY(hipMemsetAsync(cnt, 0, 8, st));
+      hipLaunchKernelGGL(k_etab_build<false>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, (const uint64_t*)g->off,
+                         (const uint32_t*)g->keys, S, (uint64_t*)nullptr, 1u, cnt);
+      TRY(hipGetLastError());
+      uint64_t upper = 0;
+      TRY(hipMemcpyAsync(&upper, cnt, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      uint32_t bits = 4;
+      while (bits < 40 && (1ull << bits) * ET_SLOTS < 2 * upper) ++bits;  // load <= 1/2
+      const uint64_t bytes = (1ull << bits) * ET_SLOTS * 8;
+      size_t fr = 0, tot = 0;
+      TRY(hipMemGetInfo(&fr, &tot));
+      if (upper > 0 && bytes < fr / 4) {
+        TRY(hipMalloc(&g->etab, bytes));
+        TRY(hipMemsetAsync(g->etab, 0xff, bytes, st));
+        hipLaunchKernelGGL(k_etab_build<true>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st,
+                           (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->etab, bits,
+                           (unsigned long long*)nullptr);
+        TRY(hipGetLastError());
+        g->etbits = bits;
+      }
+    }
+  }
+  // Edge filter for the first-order exclusion of the scoring kernel when there
+  // is no table: one bit per (u, w) hash slot, 16 slots per adjacency entry
+  // (~6 % of non-edges hit a set bit and are searched; every edge is).
+  // NLP_EDGE_FILTER=0 disables it.
   {
     const char* ef = getenv("NLP_EDGE_FILTER");
-    if (M > 0 && !(ef && ef[0] == '0')) {
+    if (M > 0 && !g->etab && !(ef && ef[0] == '0')) {
       uint32_t bits = 20;
       while (bits < 33 && (1ull << bits) < 16 * M) ++bits;
       size_t fr = 0, tot = 0;
@@ -461,6 +500,8 @@ nlp_status finish_graph(nlp_graph* g) {
     if (v > 0) g->wedge_budget = v;
   }
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
+  if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
+  if (const char* xi = getenv("NLP_EX_IPT")) g->ex_ipt = atoi(xi) >= 4 ? 4 : (atoi(xi) >= 2 ? 2 : 1);
   if (const char* gs = getenv("NLP_GRAPH_SEGMENTS")) g->graph_single = gs[0] != '1';
   if (const char* sp = getenv("NLP_STAMP")) {
     g->stamp_path = sp;
@@ -488,25 +529,23 @@ nlp_status finish_graph(nlp_graph* g) {
     hipDeviceProp_t prop;
     TRY(hipGetDeviceProperties(&prop, g->device));
     const unsigned cus = (unsigned)std::max(prop.multiProcessorCount, 1);
-    auto occ = [&](const void* k, unsigned* out) -> hipError_t {
+    // grid caps of the ticketed single-pass kernels: at most one resident
+    // round of workgroups (the tiles are claimed in order, so correctness does
+    // not depend on residency; surplus workgroups would only draw tickets)
+    auto occ = [&](const void* k, unsigned* out, int block = NT) -> hipError_t {
       int nb = 0;
-      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, NT, 0);
-      // half of the reported residency: the blockIdx-ordered persistent scans
-      // deadlock (look-back timeout) if any of their workgroups is not resident
-      if (e == hipSuccess) *out = cus * (unsigned)std::max(nb / 2, 1);
+      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, block, 0);
+      if (e == hipSuccess) *out = cus * (unsigned)std::max(nb, 1);
       return e;
     };
-    TRY(occ((const void*)k_sp_survivors<>, &g->occ_surv));
+    TRY(occ((const void*)k_sp_survivors, &g->occ_surv));
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
-    TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64));
-    TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32));
+    TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
+    TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     unsigned a = 0, b = 0;
     TRY(occ((const void*)k_sp_scan<F_Runs<true>, RN_IPT>, &a));
     TRY(occ((const void*)k_sp_scan<F_Runs<false>, RN_IPT>, &b));
     g->occ_run = std::min(a, b);
-    TRY(occ((const void*)k_sp_runs<true>, &a));
-    TRY(occ((const void*)k_sp_runs<false>, &b));
-    g->occ_runs = std::min(a, b);
   }
   g->ws.release();  // drop build scratch; predict grows its own
   return NLP_OK;
@@ -547,6 +586,7 @@ struct Params {
   float min_score;
   uint64_t max_edges;
   uint64_t ua, ub;
+  uint32_t maxf2 = 0;  // MAXFACTOR2 (predict.hxx:221,295), 0 = off
 };
 
 struct Cands {
@@ -604,10 +644,10 @@ nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* 
   const double* ctab = p.metric == M_AA ? g->ctab_aa : g->ctab_ra;
   if (custom)
     LAUNCH(k_score<true>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru, rw,
-           rs, rfl);
+           rs, rfl, p.maxf2, g->etab, g->etbits);
   else
     LAUNCH(k_score<false>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru,
-           rw, rs, rfl);
+           rw, rs, rfl, p.maxf2, g->etab, g->etbits);
   TRY(hipGetLastError());
   // 4. append flagged candidates
   TRY(scan_excl_u64<uint32_t>(rfl, R, rpos, cnt + 1, scan, st));
@@ -765,9 +805,9 @@ nlp_status arena_init(nlp_graph* g, int id, uint64_t desc_words, Arena& A, const
   return NLP_OK;
 }
 
-GraphView view_of(nlp_graph* g, int metric) {
+GraphView view_of(nlp_graph* g, int metric, uint32_t maxf2 = 0) {
   return GraphView{g->off,  g->keys, g->deg, g->toff, g->tkeys, metric == M_AA ? g->ctab_aa : g->ctab_ra,
-                   g->efilt, g->efbits};
+                   g->efilt, g->efbits, maxf2, g->etab, g->etbits};
 }
 
 template <class F>
@@ -830,7 +870,7 @@ nlp_status run_path1_v1(nlp_graph* g, const Params& p, Cands& C, uint64_t* flags
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
   const bool custom = p.metric == M_AA || p.metric == M_RA;
-  const GraphView gv = view_of(g, p.metric);
+  const GraphView gv = view_of(g, p.metric, p.maxf2);
   Workspace& ws = g->ws;
   *over_budget = false;
   // zero-invariant counters: allocate (and zero) once
@@ -1259,7 +1299,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t* scan;
   TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
   // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
-  const GraphView gv = view_of(g, p.metric);
+  const GraphView gv = view_of(g, p.metric, p.maxf2);
   {
     TRY(hipMemsetAsync(wu, 0, nU * 8, st));
     TRY(hipMemcpyAsync(&g->host_small[8], g->off + ua, 8, hipMemcpyDeviceToHost, st));
@@ -1502,7 +1542,7 @@ nlp_status launch_fast(nlp_graph* g, const Params& p, const FastBufs& f, EdgeOut
   const uint64_t S = g->span;
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S), nU = ub - ua;
   const bool custom = p.metric == M_AA || p.metric == M_RA;
-  const GraphView gv = view_of(g, p.metric);
+  const GraphView gv = view_of(g, p.metric, p.maxf2);
   const uint64_t capW = g->capW;
   constexpr int IPT_S = 16, IPT_W = 4;
   uint64_t *gU = f.aggs, *gW = f.aggs + f.aU, *gT = gW + f.aW;
@@ -1599,9 +1639,11 @@ struct SpBufs {
   uint64_t *rk0, *rk1;
   uint32_t *rv0, *rv1, *cu, *cw, *ok0, *ok1, *ov0, *ov1;
   float *stash, *cs;
+  uint32_t* segcnt;  // k_sp_runs: candidates per RU_SEG-record segment (gapped layout)
   uint64_t* arena;
   uint64_t arena_words;
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
+  uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
@@ -1671,6 +1713,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   TRY(wsget(ws, B_SP_OK1, capW, &f.ok1));
   TRY(wsget(ws, B_SP_OV0, capW, &f.ov0));
   TRY(wsget(ws, B_SP_OV1, capW, &f.ov1));
+  TRY(wsget(ws, B_SP_SEGCNT, (capW + RU_SEG - 1) / RU_SEG + 1, &f.segcnt));
   f.wbits = key_bits(S ? S - 1 : 0);
   const int ubits = key_bits(ub > ua ? ub - ua - 1 : 0);
   f.passes = (f.wbits + ubits + 7) / 8;
@@ -1691,11 +1734,12 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
     f.nv = g->rx_dstart[p.H + 1];
     f.survivors = g->rx_vbydeg;
   }
-  const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + EX_TILE - 1) / EX_TILE;
+  const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + NT - 1) / NT;
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, RS_BINS);
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
-  f.d_surv = SP_DESC;
+  f.d_tick = SP_DESC;
+  f.d_surv = f.d_tick + SP_NTICK / 2;
   f.d_exp = f.d_surv + tS + 1;
   f.d_run = f.d_exp + tE + 1;
   f.d_rec = f.d_run + tR + 1;
@@ -1727,13 +1771,14 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   const uint64_t ua = std::min(p.ua, S), ub = std::min(p.ub, S);
   const uint64_t capW = g->capW;
   const bool custom = p.metric == M_AA || p.metric == M_RA;
-  const GraphView gv = view_of(g, p.metric);
+  const GraphView gv = view_of(g, p.metric, p.maxf2);
   uint64_t* ctr = f.arena;
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
   uint32_t* hrec = (uint32_t*)(f.arena + SP_HREC);
   uint32_t* hord = (uint32_t*)(f.arena + SP_HORD);
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
+  uint32_t* tick = (uint32_t*)(f.arena + f.d_tick);
   const int P = f.msd ? f.msd_passes : f.passes;
   const int s_runs = 4 + P + (f.split ? 1 : 0), n_st = s_runs + 7;
   // after the record passes the records sit in buffer 1 for an odd count, 0 for even
@@ -1757,17 +1802,27 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                          dim3(NT), 0, st, f.arena, f.arena_words, ci);
     } else if (s == 1) {
       if (f.dindex) return NLP_OK;
-      hipLaunchKernelGGL(k_sp_survivors<>, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
-                         (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, ctr, hot == 1 ? g->d_stamp : nullptr);
+      hipLaunchKernelGGL(k_sp_survivors, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
+                         (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, tick + TK_SURV, ctr,
+                         hot == 1 ? g->d_stamp : nullptr);
     } else if (s == 2) {
-      if (f.msd)  // the MSD digit histogram is fused into the expansion
-        hipLaunchKernelGGL(k_sp_expand<true>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv, ua,
-                           ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, f.msd_shift, hrec,
-                           P);
-      else
-        hipLaunchKernelGGL(k_sp_expand<false>, grid((S + EX_TILE - 1) / EX_TILE, g->occ_exp), dim3(NT), 0, st, gv,
-                           ua, ub, f.wbits, f.survivors, capW, f.rk0, f.rv0, f.arena + f.d_exp, ctr, 0,
-                           (uint32_t*)nullptr);
+      // survivors: known exactly with the degree-class index, else at most S
+      const uint64_t nsv = f.dindex ? f.nv : S;
+      const int xi = g->ex_ipt;
+      const dim3 gx = grid((nsv + (uint64_t)NT * xi - 1) / ((uint64_t)NT * xi), g->occ_exp);
+#define NLP_EXPAND(IPT)                                                                                          \
+  do {                                                                                                           \
+    if (f.msd) /* the MSD digit histogram is fused into the expansion */                                         \
+      hipLaunchKernelGGL((k_sp_expand<true, IPT>), gx, dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, capW,  \
+                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, f.msd_shift, hrec, P);             \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_sp_expand<false, IPT>), gx, dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, capW, \
+                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, 0, (uint32_t*)nullptr, 1);         \
+  } while (0)
+      if (xi == 4) NLP_EXPAND(4);
+      else if (xi == 2) NLP_EXPAND(2);
+      else NLP_EXPAND(1);
+#undef NLP_EXPAND
     } else if (s == 3) {
       if (f.msd) return NLP_OK;
       hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, st, (const uint64_t*)f.rk0,
@@ -1776,12 +1831,12 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < 4 + P) {
       const int ps = s - 4;
       const bool odd = ps & 1;
-      hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(NT), 0, st,
+      hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(OS_NT), 0, st,
                          (const uint64_t*)(odd ? f.rk1 : f.rk0), (const uint32_t*)(odd ? f.rv1 : f.rv0),
                          odd ? f.rk0 : f.rk1, odd ? f.rv0 : f.rv1, (const uint64_t*)&ctr[C_WSORT],
                          f.msd ? f.msd_shift + 8 * ps : 8 * ps,
-                         (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, err,
-                         hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
+                         (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, tick + TK_REC + ps,
+                         err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
     } else if (f.split && s == s_runs - 1 && P == 1 && g->group_sort != 1) {
       // one MSD pass: one workgroup per top-digit bucket, the bucket bounds from its histogram
       if (custom)
@@ -1803,40 +1858,41 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
         hipLaunchKernelGGL(k_sp_group<false>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
                            f.msd_shift, rk_m, rv_free, (uint32_t*)nullptr, ctr, hot == s ? g->d_stamp : nullptr);
     } else if (f.split && s == s_runs) {
-      const dim3 gr = grid((capW + RU_TILE - 1) / RU_TILE, g->occ_runs);
+      // one workgroup per RU_TILE records, no hand-off (gapped output)
+      const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + RU_TILE - 1) / RU_TILE));
       if (custom)
         hipLaunchKernelGGL(k_sp_runs<true>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
                            (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)f.stash, f.cu, f.cw,
-                           f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr);
+                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr);
       else
         hipLaunchKernelGGL(k_sp_runs<false>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
                            (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)nullptr, f.cu, f.cw,
-                           f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr);
+                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr);
     } else if (s == s_runs && f.msd) {
       if (custom)
         hipLaunchKernelGGL(k_sp_bucket<true>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
                            f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
                            f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr);
+                           hot == s ? g->d_stamp : nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                           (uint32_t*)nullptr, tick + TK_BUCKET);
       else
         hipLaunchKernelGGL(k_sp_bucket<false>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
                            f.wbits, (const uint64_t*)f.rk1, (const uint32_t*)f.rv1, (const uint32_t*)hrec, f.cu,
                            f.cw, f.cs, f.ok0, f.ov0, f.arena + f.d_run, ctr, f.msd_shift, p.max_edges, hord,
-                           hot == s ? g->d_stamp : nullptr);
+                           hot == s ? g->d_stamp : nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                           (uint32_t*)nullptr, tick + TK_BUCKET);
     } else if (s == s_runs) {
       const dim3 gr = grid((capW + RN_TILE - 1) / RN_TILE, g->occ_run);
       if (custom) {
         F_Runs<true> fr{gv, p.metric, p.min_score, ua, f.wbits, rks, rvs, f.stash, f.cu, f.cw, f.cs, f.ok0, f.ov0,
                         &ctr[C_NAN]};
         hipLaunchKernelGGL((k_sp_scan<F_Runs<true>, RN_IPT>), gr, dim3(NT), 0, st, fr, (const uint64_t*)&ctr[C_WSORT],
-                           f.arena + f.d_run, err, &ctr[C_C]);
+                           f.arena + f.d_run, tick + TK_RUNS, err, &ctr[C_C]);
       } else {
         F_Runs<false> fr{gv, p.metric, p.min_score, ua, f.wbits, rks, rvs, f.stash, f.cu, f.cw, f.cs, f.ok0, f.ov0,
                          &ctr[C_NAN]};
         hipLaunchKernelGGL((k_sp_scan<F_Runs<false>, RN_IPT>), gr, dim3(NT), 0, st, fr,
-                           (const uint64_t*)&ctr[C_WSORT], f.arena + f.d_run, err, &ctr[C_C]);
+                           (const uint64_t*)&ctr[C_WSORT], f.arena + f.d_run, tick + TK_RUNS, err, &ctr[C_C]);
       }
     } else if (s == s_runs + 1) {
       if (f.msd) return NLP_OK;  // fused into k_sp_bucket
@@ -1845,17 +1901,30 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.msd && ps == 0)  // k_sp_bucket counted digit 0; this pass counts digits 1-3
-        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true>), grid(tO, g->occ_p32), dim3(NT), 0, st,
+      if (f.split && ps == 0)  // k_sp_runs' gapped candidates (and digit 0); this pass counts digits 1-3
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
+                           (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
+                           (const uint64_t*)&ctr[C_WSORT], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
+                           (uint64_t*)nullptr, GatherOut{}, hord + RS_BINS, (const uint32_t*)f.segcnt, &ctr[C_C]);
+      else if (f.msd && ps == 0)  // k_sp_bucket counted digit 0; this pass counts digits 1-3
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1, (const uint64_t*)&ctr[C_C],
-                           0, (const uint32_t*)hord, dord, err, (uint64_t*)nullptr, GatherOut{}, hord + RS_BINS);
+                           0, (const uint32_t*)hord, dord, tick + TK_ORD, err, (uint64_t*)nullptr, GatherOut{},
+                           hord + RS_BINS);
+      else if (ps == 3 && g->fuse_gather)  // the last pass writes the caller's edges
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
+                           (const uint32_t*)f.ok1, (const uint32_t*)f.ov1, f.ok0, f.ov0, (const uint64_t*)&ctr[C_C], 24,
+                           (const uint32_t*)(hord + 3 * RS_BINS), dord + 3 * f.ostride, tick + TK_ORD + 3, err,
+                           (uint64_t*)nullptr,
+                           GatherOut{f.cu, f.cw, f.cs, p.max_edges, out, ctr, g->host_ctr_dev}, (uint32_t*)nullptr);
       else
-        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(NT), 0, st,
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
                            odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
-                           (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, err,
-                           (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr);
+                           (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, tick + TK_ORD + ps,
+                           err, (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr);
     } else {
+      if (g->fuse_gather) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
                          dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
@@ -1904,10 +1973,12 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
   nlp_graph::Cached* hit = nullptr;
   for (auto& c : g->graphs)
     if (c.metric == p.metric && c.H == p.H && c.min_score == p.min_score && c.max_edges == p.max_edges &&
-        c.ua == p.ua && c.ub == p.ub && c.capW == g->capW && c.gen == gen && c.mode == mode && c.out == (void*)out)
+        c.ua == p.ua && c.ub == p.ub && c.capW == g->capW && c.gen == gen && c.maxf2 == p.maxf2 && c.mode == mode &&
+        c.out == (void*)out)
       hit = &c;
   if (!hit) {
-    nlp_graph::Cached c{p.metric, p.H, p.min_score, p.max_edges, p.ua, p.ub, g->capW, gen, mode, (void*)out, {}, false, 0};
+    nlp_graph::Cached c{p.metric, p.H,  p.min_score, p.max_edges, p.ua,  p.ub, g->capW,
+                        gen,      p.maxf2, mode,   (void*)out,  {},    false, 0};
     hipStream_t gs = g->stream;
     bool ok = true;
     c.single = false;
@@ -2414,18 +2485,20 @@ nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uin
   return NLP_OK;
 }
 
-nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
-                              uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
-                              uint64_t* out_count, nlp_timing* t, void* stream) {
+nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
+                                 float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
+                                 uint64_t* out_count, nlp_timing* t, void* stream) {
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
   // the graph's own stream does not order after other streams: with no caller
   // stream, wait for all prior device work (inputs/outputs may come from it)
   if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
-  Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span)};
+  Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span), max_factor2};
   nlp_timing tt;
   memset(&tt, 0, sizeof(tt));
+  g->last_out = nullptr;
+  g->last_n = 0;
   nlp_status s = predict_impl(g, p, (EdgeOut*)d_out, out_count, &tt, st, nullptr);
   if (t) *t = tt;
   if (s == NLP_OK) {
@@ -2436,13 +2509,21 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
   return s;
 }
 
-nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score, uint64_t max_edges,
-                       int repeat, nlp_edge* out, uint64_t* out_count, nlp_timing* t) {
+nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score,
+                              uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
+                              uint64_t* out_count, nlp_timing* t, void* stream) {
+  return nlp_predict_device_ex(g, metric, hub_max_degree, 0, min_score, max_edges, u_begin, u_end, d_out, out_count,
+                               t, stream);
+}
+
+nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
+                          float min_score, uint64_t max_edges, int repeat, nlp_edge* out, uint64_t* out_count,
+                          nlp_timing* t) {
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8) return NLP_ERR_INVALID;
   if (repeat < 1) repeat = 1;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = g->stream;
-  Params p{(int)metric, hub_max_degree, min_score, max_edges, 0, g->span};
+  Params p{(int)metric, hub_max_degree, min_score, max_edges, 0, g->span, max_factor2};
   // measureDuration(fn, repeat) semantics (_utility.hxx:345-352): the timed
   // work runs `repeat` times and the reported times are averages.
   float score_sum = 0, select_sum = 0;
@@ -2450,6 +2531,8 @@ nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree,
   memset(&last, 0, sizeof(last));
   EdgeOut* d_res = nullptr;
   uint64_t n = 0;
+  g->last_out = nullptr;
+  g->last_n = 0;
   for (int r = 0; r < repeat; ++r) {
     nlp_status s = predict_impl(g, p, nullptr, &n, &last, st, &d_res);
     if (s != NLP_OK) return s;
@@ -2471,6 +2554,24 @@ nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree,
   g->last_out = d_res;
   g->last_n = n;
   g->last_stream = st;
+  return NLP_OK;
+}
+
+nlp_status nlp_predict(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, float min_score, uint64_t max_edges,
+                       int repeat, nlp_edge* out, uint64_t* out_count, nlp_timing* t) {
+  return nlp_predict_ex(g, metric, hub_max_degree, 0, min_score, max_edges, repeat, out, out_count, t);
+}
+
+nlp_status nlp_copy_last(nlp_graph* g, nlp_edge* out, uint64_t n, uint64_t* copied) {
+  if (!g || !copied || (n && !out)) return NLP_ERR_INVALID;
+  *copied = 0;
+  const uint64_t m = std::min(n, g->last_n);
+  if (!m) return NLP_OK;
+  if (!g->last_out) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  TRY(hipMemcpyAsync(out, g->last_out, m * sizeof(EdgeOut), hipMemcpyDeviceToHost, g->last_stream));
+  TRY(hipStreamSynchronize(g->last_stream));
+  *copied = m;
   return NLP_OK;
 }
 

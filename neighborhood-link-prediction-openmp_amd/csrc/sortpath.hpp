@@ -28,11 +28,12 @@
 // O(W) afterwards -- no per-source arrays, so a small wedge count stays cheap
 // on a large graph.
 //
-// Inter-workgroup hand-offs: the single-pass scans use blockIdx-ordered tiles
-// in a persistent loop whose grid never exceeds the number of co-resident
-// workgroups (the host sizes it from the occupancy query), so every tile a
-// look-back waits on is running or done.  Spins are bounded and report
-// through the error word like lookback.hpp.
+// Inter-workgroup hand-offs: the single-pass scans claim their tiles with an
+// ordered ticket (one atomic per tile on a per-launch counter in the arena),
+// so every tile a look-back waits on is held by a running workgroup or done,
+// whatever the grid size, dispatch order or other work on the device.  Spins
+// are bounded and report through the error word like lookback.hpp.  k_sp_runs
+// needs no hand-off at all (gapped output, see there).
 #pragma once
 #include "select.hpp"
 
@@ -49,7 +50,9 @@ constexpr uint32_t HSTRIDE = 8 * 256;  // u32 per copy: up to 8 digits of 256 bi
 // Arena (u64 words): counters [0, 16), digit histograms, look-back descriptors.
 constexpr uint64_t SP_HREC = 16;                                 // record-key digits
 constexpr uint64_t SP_HORD = SP_HREC + HCOPIES * HSTRIDE / 2;    // score-key digits
-constexpr uint64_t SP_DESC = SP_HORD + HCOPIES * HSTRIDE / 2;    // descriptors follow
+constexpr uint64_t SP_DESC = SP_HORD + HCOPIES * HSTRIDE / 2;    // ticket counters and descriptors follow
+// u32 ticket counters of the ticketed launches of one call (zeroed with the arena)
+enum { TK_SURV = 0, TK_EXP = 1, TK_RUNS = 2, TK_BUCKET = 3, TK_REC = 8, TK_ORD = 16, SP_NTICK = 24 };
 
 __device__ __forceinline__ uint32_t* hist_copy(uint32_t* h) { return h + (blockIdx.x % HCOPIES) * HSTRIDE; }
 __device__ __forceinline__ uint32_t hist_total(const uint32_t* h, uint32_t i) {
@@ -59,15 +62,13 @@ __device__ __forceinline__ uint32_t hist_total(const uint32_t* h, uint32_t i) {
   return s;
 }
 
-constexpr int SV_STEPS = 8;                    // survivor scan: 256-vertex steps per wave
-constexpr int SV_TILE = NT * 4 * SV_STEPS;     // 8192 vertices per tile
-constexpr int EX_TILE = NT;                    // expansion: one survivor per thread
+constexpr int EX_IPT = 4;                      // expansion: survivors per thread (blocked)
+constexpr int EX_TILE = NT * EX_IPT;           //            survivors per tile
 constexpr int RN_IPT = 4;
-constexpr int RN_TILE = NT * RN_IPT;           // run scoring: 1024 records per tile
-constexpr int OS2_IPT = 16;
-constexpr int OS2_TILE = NT * OS2_IPT;         // onesweep: 4096 keys per tile
-constexpr int OS2_LBR = 16;                    // predecessors read per look-back round trip
-constexpr uint64_t SP_MAX_N = (1ull << 30) - 1;  // u32 onesweep descriptors: 30-bit values
+constexpr int RN_TILE = NT * RN_IPT;           // run scoring (k_sp_scan<F_Runs>): 1024 records per tile
+constexpr int RU_IPT = 4;
+constexpr int RU_SEG = 64 * RU_IPT;            // k_sp_runs: records per wave = one segment of the gapped layout
+constexpr int RU_TILE = NT * RU_IPT;           //            records per workgroup
 
 // Look-back of one wave over 64*R predecessors per round trip (lane l reads
 // tiles base-lR .. base-lR-R+1).  Returns the exclusive prefix (wave 0 of the
@@ -135,52 +136,75 @@ __device__ __forceinline__ uint64_t lane_mask_lt() {
 }
 
 // ---------------------------------------------------------------- survivors
-// Tile = 4 waves x STEPS steps x 256 consecutive vertices (16-byte loads, lane l
-// of step i holds vertices base + 256 i + 4 l .. +3); a vertex survives when
-// 1 <= deg v <= H (H = 0: IHub, every vertex with edges).  Output ascending v.
-template <int STEPS = SV_STEPS>
+// Tile = 4 waves x SV_STEPS steps x 256 consecutive vertices (16-byte loads,
+// lane l of step i holds vertices base + 256 i + 4 l .. +3); a vertex survives
+// when 1 <= deg v <= H (H = 0: IHub, every vertex with edges).  Output
+// ascending v.  Tiles come from an ordered ticket (see k_sp_pass).
+constexpr int SV_STEPS = 32;
+constexpr uint64_t SV_TILE = (uint64_t)NT * 4 * SV_STEPS;  // 32768 vertices per tile
+
+// Ordered tile claim for the persistent scans: thread 0 draws, LDS broadcast.
+// s_tk[par] holds the current tile, s_tk[par ^ 1] the prefetched next one
+// (draw it after the iteration's first barrier; read after its last).
+__device__ __forceinline__ void tk_draw(uint32_t* tick, uint32_t* slot) {
+  if (threadIdx.x == 0) *slot = atomicAdd(tick, 1u);
+}
+
 __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict__ deg, uint64_t S, uint32_t H,
                                                      uint32_t* __restrict__ surv, uint64_t* __restrict__ desc,
-                                                     uint64_t* __restrict__ ctr, uint64_t* __restrict__ stamp) {
-  static_assert(STEPS * 4 <= 32, "flag bits");
-  constexpr uint64_t TILE = (uint64_t)NT * 4 * STEPS;
+                                                     uint32_t* __restrict__ tick, uint64_t* __restrict__ ctr,
+                                                     uint64_t* __restrict__ stamp) {
+  constexpr int NB = SV_STEPS / 8;  // u32 flag words per lane (8 steps x 4 vertices each)
   __shared__ uint64_t s_w[NWAVE];
   __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_tk[2];
   const int lane = lane_id(), wv = wave_id();
   const uint32_t hm = H ? H : 0xffffffffu;
-  const uint64_t ntiles = (S + TILE - 1) / TILE;
+  const uint64_t ntiles = (S + SV_TILE - 1) / SV_TILE;
   const uint64_t lt = lane_mask_lt();
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
+  if (blockIdx.x >= ntiles) return;  // only as many claimants as tiles
+  tk_draw(tick, &s_tk[0]);
+  __syncthreads();
+  bool first = true;
+  for (int par = 0;; par ^= 1) {
+    const uint64_t tile = s_tk[par];
+    if (tile >= ntiles) break;
     sp_stamp(stamp, first, 0);
-    const uint64_t b0 = tile * TILE + (uint64_t)wv * (256 * STEPS) + 4 * (uint64_t)lane;
-    uint4 dv[STEPS];
+    const uint64_t b0 = tile * SV_TILE + (uint64_t)wv * (256 * SV_STEPS) + 4 * (uint64_t)lane;
+    uint32_t bits[NB];
+    uint64_t wt = 0;
 #pragma unroll
-    for (int i = 0; i < STEPS; ++i) {
-      const uint64_t v = b0 + (uint64_t)i * 256;
-      if (v + 3 < S) {
-        dv[i] = *(const uint4*)(deg + v);
-      } else {
-        dv[i].x = v < S ? deg[v] : 0u;
-        dv[i].y = v + 1 < S ? deg[v + 1] : 0u;
-        dv[i].z = v + 2 < S ? deg[v + 2] : 0u;
-        dv[i].w = 0u;
+    for (int q = 0; q < NB; ++q) {
+      uint4 dv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint64_t v = b0 + (uint64_t)(8 * q + i) * 256;
+        if (v + 3 < S) {
+          dv[i] = *(const uint4*)(deg + v);
+        } else {
+          dv[i].x = v < S ? deg[v] : 0u;
+          dv[i].y = v + 1 < S ? deg[v + 1] : 0u;
+          dv[i].z = v + 2 < S ? deg[v + 2] : 0u;
+          dv[i].w = 0u;
+        }
       }
-    }
-    uint32_t bits = 0;
+      uint32_t m = 0;
 #pragma unroll
-    for (int i = 0; i < STEPS; ++i) {
-      bits |= (uint32_t)(dv[i].x - 1u < hm) << (4 * i);
-      bits |= (uint32_t)(dv[i].y - 1u < hm) << (4 * i + 1);
-      bits |= (uint32_t)(dv[i].z - 1u < hm) << (4 * i + 2);
-      bits |= (uint32_t)(dv[i].w - 1u < hm) << (4 * i + 3);
+      for (int i = 0; i < 8; ++i) {
+        m |= (uint32_t)(dv[i].x - 1u < hm) << (4 * i);
+        m |= (uint32_t)(dv[i].y - 1u < hm) << (4 * i + 1);
+        m |= (uint32_t)(dv[i].z - 1u < hm) << (4 * i + 2);
+        m |= (uint32_t)(dv[i].w - 1u < hm) << (4 * i + 3);
+      }
+      bits[q] = m;
+      wt += (uint64_t)__popc(m);
     }
-    uint64_t wt = (uint64_t)__popc(bits);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wt += __shfl_xor(wt, o, 64);
     if (lane == 0) s_w[wv] = wt;
     __syncthreads();
+    tk_draw(tick, &s_tk[par ^ 1]);
     sp_stamp(stamp, first, 1);
     if (wv == 0) {
       uint64_t agg = 0;
@@ -197,8 +221,8 @@ __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict_
     uint64_t run = s_excl;
     for (int w = 0; w < wv; ++w) run += s_w[w];
 #pragma unroll
-    for (int i = 0; i < STEPS; ++i) {
-      const uint32_t nib = (bits >> (4 * i)) & 0xfu;
+    for (int i = 0; i < SV_STEPS; ++i) {
+      const uint32_t nib = (bits[i / 8] >> (4 * (i % 8))) & 0xfu;
       uint64_t before = 0, stepn = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -215,6 +239,7 @@ __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict_
     }
     __syncthreads();
     sp_stamp(stamp, first, 3);
+    first = false;
   }
 }
 
@@ -295,48 +320,140 @@ __global__ __launch_bounds__(NT) void k_range_index(GraphView g, const uint32_t*
 }
 
 // ---------------------------------------------------------------- wedge records
-// One thread per survivor v (ascending): for each in-edge u -> v with u in
-// [ua, ub), the wedges (u, v, w) with w in N(v), w > u.  Records beyond capW are
-// not written; the total still goes to ctr[C_W] (the host regrows and reruns).
-// HIST: also the histogram of record-key digit (key >> hshift) & 255 (the MSD
-// pass), accumulated per workgroup in LDS; the last tile stores the sortable
-// record count ctr[C_WSORT] (0 and F_OVERFLOW when the records exceed capW).
-template <bool HIST>
+// Thread t of a tile owns EX_IPT consecutive survivors v (ascending index):
+// for each in-edge u -> v with u in [ua, ub), the wedges (u, v, w) with w in
+// N(v), w > u.  Records land in survivor order (single-pass scan over
+// ticketed tiles).  A survivor whose N(v) and I(v) both fit EX_REG entries is
+// enumerated from registers (no search: one round of independent loads);
+// larger ones walk I(v) with an upper_bound into N(v).  Records beyond capW
+// are not written; the total still goes to ctr[C_W] (the host regrows and
+// reruns).  HIST: also the histogram of record-key digit (key >> hshift) & 255
+// (the MSD pass), accumulated per workgroup in LDS; the last tile stores the
+// sortable record count ctr[C_WSORT] (0 and F_OVERFLOW when the records exceed
+// capW).
+constexpr int EX_REG = 8;
+
+struct ExSurv {
+  uint32_t v, d, nin;
+  uint64_t a;             // toff[v]
+  const uint32_t* nv;     // N(v)
+  bool reg;
+  uint32_t N[EX_REG], I[EX_REG];
+};
+
+__device__ __forceinline__ void ex_load(const GraphView& g, uint32_t v, ExSurv& x) {
+  x.v = v;
+  x.d = g.deg[v];
+  x.a = g.toff[v];
+  x.nin = (uint32_t)(g.toff[v + 1] - x.a);
+  x.nv = g.keys + g.off[v];
+  x.reg = x.d <= EX_REG && x.nin <= EX_REG;
+  if (x.reg) {
+#pragma unroll
+    for (int q = 0; q < EX_REG; ++q) {
+      x.N[q] = q < (int)x.d ? x.nv[q] : 0u;
+      x.I[q] = q < (int)x.nin ? g.tkeys[x.a + q] : 0u;
+    }
+  }
+}
+
+// wedges of survivor x (w > u, u in [ua, ub)); EMIT: write them from `pos`
+template <bool EMIT, bool HIST>
+__device__ __forceinline__ uint64_t ex_walk(const GraphView& g, const ExSurv& x, uint64_t ua, uint64_t ub, int wbits,
+                                            uint64_t pos, uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
+                                            uint32_t* s_h, int hshift, int hdigits) {
+  uint64_t c = 0;
+  auto put = [&](uint32_t u, uint32_t w) {
+    if (EMIT) {
+      const uint64_t key = ((uint64_t)(u - ua) << wbits) | w;
+      rkey[pos + c] = key;
+      rval[pos + c] = x.v;
+      if (HIST) {
+        atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+        if (hdigits > 1) atomicAdd(&s_h[RS_BINS + ((uint32_t)(key >> (hshift + 8)) & 0xffu)], 1u);
+      }
+    }
+    ++c;
+  };
+  if (x.reg) {
+#pragma unroll
+    for (int p = 0; p < EX_REG; ++p) {
+      const uint32_t u = x.I[p];
+      if (p < (int)x.nin && u >= ua && u < ub) {
+        if (EMIT) {
+#pragma unroll
+          for (int q = 0; q < EX_REG; ++q)
+            if (q < (int)x.d && x.N[q] > u) put(u, x.N[q]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < EX_REG; ++q) c += (q < (int)x.d && x.N[q] > u) ? 1u : 0u;
+        }
+      }
+    }
+  } else {
+    for (uint32_t p = 0; p < x.nin; ++p) {
+      const uint32_t u = g.tkeys[x.a + p];
+      if (u < ua || u >= ub) continue;
+      const uint32_t k0 = upper_bound_u32(x.nv, x.d, u);
+      if (EMIT) {
+        for (uint32_t k = k0; k < x.d; ++k) put(u, x.nv[k]);
+      } else {
+        c += x.d - k0;
+      }
+    }
+  }
+  return c;
+}
+
+template <bool HIST, int IPT = EX_IPT>
 __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                   const uint32_t* __restrict__ surv, uint64_t capW,
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
-                                                  uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr,
-                                                  int hshift, uint32_t* __restrict__ ghist, int hdigits = 1) {
+                                                  uint64_t* __restrict__ desc, uint32_t* __restrict__ tick,
+                                                  uint64_t* __restrict__ ctr, int hshift, uint32_t* __restrict__ ghist,
+                                                  int hdigits = 1) {
   __shared__ uint64_t s_red[NWAVE + 1];
   __shared__ uint64_t s_excl;
   __shared__ uint32_t s_h[HIST ? 2 * RS_BINS : 1];
+  __shared__ uint32_t s_tk[2];
+  constexpr uint64_t TILE = (uint64_t)NT * IPT;
   const uint64_t n = ctr[C_NV];
-  const uint64_t ntiles = (n + EX_TILE - 1) / EX_TILE;
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
-  if (blockIdx.x >= ntiles) return;
+  if (blockIdx.x >= ntiles) return;  // only as many claimants as tiles
   if (HIST) {
     s_h[threadIdx.x] = 0;
     s_h[RS_BINS + threadIdx.x] = 0;
-    __syncthreads();
   }
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t i = tile * EX_TILE + threadIdx.x;
-    uint32_t v = 0, d = 0;
-    uint64_t a = 0, b = 0, c = 0;
-    const uint32_t* nv = g.keys;
-    if (i < n) {
-      v = surv[i];
-      d = g.deg[v];
-      a = g.toff[v];
-      b = g.toff[v + 1];
-      nv = g.keys + g.off[v];
-      for (uint64_t j = a; j < b; ++j) {
-        const uint32_t u = g.tkeys[j];
-        if (u >= ua && u < ub) c += d - upper_bound_u32(nv, d, u);
+  tk_draw(tick, &s_tk[0]);
+  __syncthreads();
+  for (int par = 0;; par ^= 1) {
+    const uint64_t tile = s_tk[par];
+    if (tile >= ntiles) break;
+    const uint64_t i0 = tile * TILE + (uint64_t)threadIdx.x * IPT;
+    ExSurv x[IPT];
+    uint64_t c[IPT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      if (i0 + j < n) {
+        ex_load(g, surv[i0 + j], x[j]);
+      } else {
+        x[j].nin = 0;
+        x[j].d = 0;
+        x[j].reg = true;
+        x[j].v = 0;
+        x[j].a = 0;
+        x[j].nv = g.keys;
       }
     }
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      c[j] = ex_walk<false, false>(g, x[j], ua, ub, wbits, 0, rkey, rval, s_h, hshift, hdigits);
+      sum += c[j];
+    }
     uint64_t agg;
-    const uint64_t x = block_excl_scan(c, s_red, &agg);
+    uint64_t pos = block_excl_scan(sum, s_red, &agg);  // syncs
+    tk_draw(tick, &s_tk[par ^ 1]);
     if (wave_id() == 0) {
       const uint64_t e = lb_lookback_r<4>(desc, tile, agg, err);
       if (lane_id() == 0) {
@@ -352,22 +469,12 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
       }
     }
     __syncthreads();
-    uint64_t pos = s_excl + x;
-    if (c && pos + c <= capW) {
-      for (uint64_t j = a; j < b; ++j) {
-        const uint32_t u = g.tkeys[j];
-        if (u < ua || u >= ub) continue;
-        const uint64_t hi = (uint64_t)(u - ua) << wbits;
-        for (uint32_t k = upper_bound_u32(nv, d, u); k < d; ++k) {
-          const uint64_t key = hi | nv[k];
-          rkey[pos] = key;
-          rval[pos] = v;
-          if (HIST) {
-            atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
-            if (hdigits > 1) atomicAdd(&s_h[RS_BINS + ((uint32_t)(key >> (hshift + 8)) & 0xffu)], 1u);
-          }
-          ++pos;
-        }
+    pos += s_excl;
+    if (sum && pos + sum <= capW) {
+#pragma unroll
+      for (int j = 0; j < IPT; ++j) {
+        if (c[j]) ex_walk<true, HIST>(g, x[j], ua, ub, wbits, pos, rkey, rval, s_h, hshift, hdigits);
+        pos += c[j];
       }
     }
     __syncthreads();
@@ -408,6 +515,15 @@ __global__ __launch_bounds__(NT) void k_sp_hist(const K* __restrict__ keys, cons
   }
 }
 
+// ---------------------------------------------------------------- onesweep pass
+constexpr int OS_NT = 1024;                      // threads per tile: 16 waves
+constexpr int OS_NW = OS_NT / 64;
+constexpr int OS2_IPT = 4;                       // keys per thread
+constexpr int OS2_TILE = OS_NT * OS2_IPT;        // 4096 keys per tile
+constexpr int OS_LBW = 64;                       // predecessors read per look-back round trip
+constexpr uint32_t OS_AGG = 1u << 30, OS_PFX = 2u << 30, OS_VAL = OS_AGG - 1;
+constexpr uint64_t SP_MAX_N = (1ull << 30) - 1;  // u32 descriptors: 30-bit counts
+
 __device__ __forceinline__ void st_u32(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -415,36 +531,32 @@ __device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Per-digit look-back of digit t: descriptors are u32 {status:2, count:30};
-// each round trip reads OS2_LBR predecessors and resumes exactly where a
-// not-yet-published one stopped it.
-__device__ __forceinline__ uint32_t os2_lookback(uint32_t* desc, uint64_t tile, int t, uint32_t run,
-                                                 uint32_t* err) {
-  constexpr uint32_t AGG = 1u << 30, PFX = 2u << 30, VAL = AGG - 1;
-  uint32_t* my = desc + tile * RS_BINS + t;
-  if (tile == 0) {
-    st_u32(my, PFX | run);
-    return 0;
-  }
-  st_u32(my, AGG | run);
+// Exclusive prefix of digit d over tiles [0, tile): sum of the nearest
+// predecessors' values back to (and including) the first inclusive prefix.
+// The window loads are unconditional (clamped to tile 0, whose descriptor is
+// always a prefix) so they issue back to back without branches.
+__device__ __forceinline__ uint32_t os_lookback(const uint32_t* desc, uint64_t tile, int d, uint32_t* err) {
   uint32_t excl = 0, spins = 0;
   int64_t j = (int64_t)tile - 1;
-  while (true) {
-    uint32_t x[OS2_LBR];
+  while (j >= 0) {
+    uint32_t x[OS_LBW];
 #pragma unroll
-    for (int r = 0; r < OS2_LBR; ++r) x[r] = j - r >= 0 ? ld_u32(desc + (uint64_t)(j - r) * RS_BINS + t) : PFX;
+    for (int r = 0; r < OS_LBW; ++r) {
+      const int64_t q = j - r;
+      x[r] = ld_u32(desc + (uint64_t)(q >= 0 ? q : 0) * RS_BINS + d);
+    }
     int used = 0;
     bool done = false, blocked = false;
 #pragma unroll
-    for (int r = 0; r < OS2_LBR; ++r) {
+    for (int r = 0; r < OS_LBW; ++r) {
       if (!done && !blocked) {
-        const uint32_t s = x[r] >> 30;
-        if (s == 0) {
+        const uint32_t st = x[r] >> 30;
+        if (st == 0) {
           blocked = true;
         } else {
-          excl += x[r] & VAL;
+          excl += x[r] & OS_VAL;
           ++used;
-          done = s == 2;
+          done = st == 2;
         }
       }
     }
@@ -458,104 +570,177 @@ __device__ __forceinline__ uint32_t os2_lookback(uint32_t* desc, uint64_t tile, 
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  st_u32(my, PFX | (excl + run));
   return excl;
 }
 
-// One stable counting pass on digit (key >> shift) & 255.  Wave w of a tile owns
-// 64*OS2_IPT consecutive keys; ranks come from ballot multisplit plus a per-wave
-// running digit count in LDS, so the tile order is preserved exactly.
-// Candidate columns for the last ordering pass, which writes the caller's
-// edges directly (position < k) instead of the next key/value buffers.
+// One stable counting pass on digit (key >> shift) & 255 (onesweep, after
+// Adinets & Merrill, restated for gfx950): 1024-thread tiles, wave w owning
+// 64 * IPT consecutive keys, so a wave ranks its keys in IPT ballot-multisplit
+// substeps (short dependent chain); threads 0-255 then own one digit each for
+// the wave prefix, the look-back and the inclusive prefix.  Tiles are claimed
+// with an ordered ticket (one atomic per tile on a per-launch counter): a tile
+// only waits on tiles held by running workgroups -- no co-residency
+// assumption, any grid size.  Descriptors are u32 {status:2, count:30} at
+// desc[tile * 256 + digit], each written by one agent-scope atomic store and
+// read by agent-scope atomic loads (the data is the flag: no fences).
+//
+// GAPPED: the input is k_sp_runs' layout -- slot j is valid when j < n and
+// j % RU_SEG < seg_cnt[j / RU_SEG] -- and the pass writes the number of valid
+// keys (the candidate count) to *tot_out.
+// NEXT_HIST: also count digits 1..3 (shift 8, 16, 24) of the input keys into
+// the histogram copies at nhist (the first pass of a 32-bit sort whose later
+// histograms were not produced upstream).
+// GATHER: the last ordering pass writes the caller's edges (position < k)
+// instead of the next key/value buffers.
 struct GatherOut {
   const uint32_t* cu;
   const uint32_t* cw;
   const float* cs;
   uint64_t k;
   EdgeOut* out;
+  uint64_t* ctr;   // the call's counters: C_OUT_N is set, all are published to hctr
+  uint64_t* hctr;  // host-mapped copy of the counters (read after the call's final event)
 };
 
-// NEXT_HIST: also count digits 1..3 (shift 8, 16, 24) of the input keys into
-// the histogram copies at nhist (the first pass of a 32-bit sort whose later
-// histograms were not produced upstream).
-template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false>
-__global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                const uint64_t* __restrict__ d_n, int shift,
-                                                const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
-                                                uint32_t* __restrict__ err, uint64_t* __restrict__ stamp,
-                                                GatherOut go, uint32_t* __restrict__ nhist = nullptr) {
+// Exclusive scan of one value per digit (threads 0-255, 0 elsewhere) over the
+// 256 digits, by all threads of an OS_NT workgroup; also returns the total.
+__device__ __forceinline__ uint32_t os_digit_scan(uint32_t x, uint32_t* s_w, uint64_t* total) {
+  const int lane = lane_id(), wv = wave_id();
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63 && wv < 4) s_w[wv] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    pre += w < wv ? s_w[w] : 0u;
+    tot += s_w[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + inc - x;
+}
+
+template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false, bool GAPPED = false>
+__global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                   K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                   const uint64_t* __restrict__ d_n, int shift,
+                                                   const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
+                                                   uint32_t* __restrict__ tick, uint32_t* __restrict__ err,
+                                                   uint64_t* __restrict__ stamp, GatherOut go,
+                                                   uint32_t* __restrict__ nhist = nullptr,
+                                                   const uint32_t* __restrict__ seg_cnt = nullptr,
+                                                   uint64_t* __restrict__ tot_out = nullptr) {
   constexpr int WT = 64 * IPT;
-  __shared__ uint32_t s_wcnt[NWAVE][RS_BINS];
-  __shared__ uint32_t s_nh[NEXT_HIST ? 3 : 1][NEXT_HIST ? RS_BINS : 1];
+  constexpr int TILE = OS_NT * IPT;
+  static_assert(!GAPPED || (RU_SEG % 64 == 0), "a wave substep must lie in one segment");
+  __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
   __shared__ uint32_t s_base[RS_BINS];
-  __shared__ uint64_t s_red[NWAVE + 1];
+  __shared__ uint32_t s_nh[NEXT_HIST ? 3 : 1][NEXT_HIST ? RS_BINS : 1];
+  __shared__ uint32_t s_w[4];
+  __shared__ uint32_t s_tile[2];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t n = *d_n;
-  const uint64_t ntiles = (n + (NT * IPT) - 1) / (NT * IPT);
-  if (blockIdx.x >= ntiles) return;
-  uint64_t tot;
-  const uint32_t dbase = (uint32_t)block_excl_scan(hist_total(ghist, t), s_red, &tot);
-  const uint64_t lt = lane_mask_lt();
+  const uint64_t ntiles = (n + TILE - 1) / TILE;
+  // GATHER: every counter is final by now; they are published by the workgroup
+  // of the last tile after its scatter (or by workgroup 0 when there is no tile)
+  auto publish = [&]() {
+    if (GATHER && t < NCTR) {
+      const uint64_t m = n < go.k ? n : go.k;
+      if (t == C_OUT_N) go.ctr[C_OUT_N] = m;
+      // host-coherent memory; the call's final event (a system-scope release)
+      // orders these stores before the host reads them
+      if (go.hctr) go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
+    }
+  };
+  if (GATHER && ntiles == 0 && blockIdx.x == 0) publish();
+  if (blockIdx.x >= ntiles) return;  // only as many claimants as tiles
+  sp_stamp(stamp, true, 7);           // entry (diagnostics: ticket + digit bases until phase 0)
+  if (t == 0) s_tile[0] = atomicAdd(tick, 1u);
   if (NEXT_HIST)
-    for (int i = t; i < 3 * RS_BINS; i += NT) (&s_nh[0][0])[i] = 0;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
+    for (int i = t; i < 3 * RS_BINS; i += OS_NT) (&s_nh[0][0])[i] = 0;
+  uint64_t tot;
+  const uint32_t dbase = os_digit_scan(t < RS_BINS ? hist_total(ghist, t) : 0u, s_w, &tot);  // syncs
+  const uint64_t lt = lane_mask_lt();
+  bool first = true;
+  for (int par = 0;; par ^= 1) {
+    const uint64_t tile = s_tile[par];
+    if (tile >= ntiles) break;
+    if (GAPPED && tile == 0 && t == 0 && tot_out) *tot_out = tot;
     sp_stamp(stamp, first, 0);
-    for (int i = t; i < NWAVE * RS_BINS; i += NT) (&s_wcnt[0][0])[i] = 0;
+    for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t b0 = tile * (NT * IPT) + (uint64_t)wv * WT + lane;
+    if (t == 0) s_tile[par ^ 1] = atomicAdd(tick, 1u);  // claim the next tile meanwhile
+    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
     K k[IPT];
     uint32_t v[IPT], dg[IPT], rk[IPT];
+    bool ok[IPT];
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint64_t j = b0 + (uint64_t)i * 64;
-      k[i] = j < n ? kin[j] : (K)0;
-      v[i] = j < n ? vin[j] : 0u;
+      ok[i] = j < n;
+      if (GAPPED && ok[i]) ok[i] = (uint32_t)(j % RU_SEG) < seg_cnt[j / RU_SEG];
+      k[i] = ok[i] ? kin[j] : (K)0;
+      v[i] = ok[i] ? vin[j] : 0u;
     }
-    if (stamp) {  // phase 1 = keys landed
-      uint64_t z = 0;
+    EdgeOut eo[GATHER ? IPT : 1];
+    if (GATHER) {  // the output columns are fetched now, in flight during ranking and look-back
 #pragma unroll
-      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
-      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
-      sp_stamp(stamp, first, 1);
+      for (int i = 0; i < IPT; ++i)
+        if (ok[i]) eo[i] = EdgeOut{go.cu[v[i]], go.cw[v[i]], go.cs[v[i]]};
     }
+    sp_stamp(stamp, first, 1);
+    // wave ranks: ballot multisplit + the wave's running digit counts
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const bool ok = b0 + (uint64_t)i * 64 < n;
       const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
       dg[i] = d;
-      uint64_t peers = __ballot(ok);
+      uint64_t peers = __ballot(ok[i]);
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const uint64_t bb = __ballot((d >> b) & 1u);
         peers &= ((d >> b) & 1u) ? bb : ~bb;
       }
-      const uint32_t before = ok ? s_wcnt[wv][d] : 0u;
+      const uint32_t before = ok[i] ? s_wcnt[wv][d] : 0u;
       rk[i] = before + (uint32_t)__popcll(peers & lt);
       wave_lds_sync();
-      if (ok && (peers & lt) == 0) s_wcnt[wv][d] = before + (uint32_t)__popcll(peers);
+      if (ok[i] && (peers & lt) == 0) s_wcnt[wv][d] = before + (uint32_t)__popcll(peers);
       wave_lds_sync();
     }
     __syncthreads();
     sp_stamp(stamp, first, 2);
-    // thread t owns digit t: cross-wave exclusive prefix and the tile count
-    uint32_t run = 0;
+    // thread t < 256 owns digit t: wave prefix, aggregate, look-back, inclusive prefix
+    if (t < RS_BINS) {
+      uint32_t run = 0;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) {
-      const uint32_t c = s_wcnt[w][t];
-      s_wcnt[w][t] = run;
-      run += c;
+      for (int w = 0; w < OS_NW; ++w) {
+        const uint32_t c = s_wcnt[w][t];
+        s_wcnt[w][t] = run;
+        run += c;
+      }
+      uint32_t* my = desc + tile * RS_BINS + t;
+      uint32_t excl = 0;
+      if (tile == 0) {
+        st_u32(my, OS_PFX | run);
+      } else {
+        st_u32(my, OS_AGG | run);
+        excl = os_lookback(desc, tile, t, err);
+        st_u32(my, OS_PFX | (excl + run));
+      }
+      s_base[t] = dbase + excl;
     }
-    s_base[t] = dbase + os2_lookback(desc, tile, t, run, err);
     __syncthreads();
     sp_stamp(stamp, first, 3);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      if (b0 + (uint64_t)i * 64 < n) {
+      if (ok[i]) {
         const uint64_t pos = (uint64_t)s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
         if (GATHER) {
-          if (pos < go.k) go.out[pos] = EdgeOut{go.cu[v[i]], go.cw[v[i]], go.cs[v[i]]};
+          if (pos < go.k) go.out[pos] = eo[i];
         } else {
           kout[pos] = k[i];
           vout[pos] = v[i];
@@ -568,396 +753,15 @@ __global__ __launch_bounds__(NT) void k_sp_pass(const K* __restrict__ kin, const
     }
     __syncthreads();
     sp_stamp(stamp, first, 4);
+    if (GATHER && tile == ntiles - 1) publish();
+    first = false;
   }
   if (NEXT_HIST) {
     uint32_t* hc = hist_copy(nhist);
-    for (int i = t; i < 3 * RS_BINS; i += NT) {
+    for (int i = t; i < 3 * RS_BINS; i += OS_NT) {
       const uint32_t c = s_nh[i / RS_BINS][i % RS_BINS];
       if (c) atomicAdd(&hc[i], c);
     }
-  }
-}
-
-// ---------------------------------------------------------------- onesweep pass, general tile shape
-// Same contract as k_sp_pass.  NTB threads (256 or 512) x IPT substeps per
-// tile.  Per-(substep, wave, digit) counts are written once by the digit
-// group's leader lane (no read-modify-write chain inside the ranking loop).
-// G = NTB / 256 threads serve each digit: they prefix-sum its counts and read
-// LBR predecessors each per look-back round trip (G * LBR per round trip).
-template <int G, int LBR>
-__device__ __forceinline__ uint32_t osg_lookback(uint32_t* desc, uint64_t tile, int d, int q, uint32_t run,
-                                                 uint32_t* err) {
-  constexpr uint32_t AGG = 1u << 30, PFX = 2u << 30, VAL = AGG - 1;
-  uint32_t* my = desc + tile * RS_BINS + d;
-  if (tile == 0) {
-    if (q == 0) st_u32(my, PFX | run);
-    return 0;
-  }
-  if (q == 0) st_u32(my, AGG | run);
-  const int gl = lane_id() & ~(G - 1);
-  uint32_t excl = 0, spins = 0;
-  int64_t j = (int64_t)tile - 1;
-  while (true) {
-    uint32_t x[LBR];
-#pragma unroll
-    for (int r = 0; r < LBR; ++r) {
-      const int64_t jj = j - (int64_t)(q * LBR + r);
-      x[r] = jj >= 0 ? ld_u32(desc + (uint64_t)jj * RS_BINS + d) : PFX;
-    }
-    uint32_t sum = 0;
-    int used = 0, state = 0;  // 0 open, 1 reached a prefix, 2 blocked on an unpublished tile
-#pragma unroll
-    for (int r = 0; r < LBR; ++r) {
-      if (state == 0) {
-        const uint32_t st = x[r] >> 30;
-        if (st == 0) {
-          state = 2;
-        } else {
-          sum += x[r] & VAL;
-          ++used;
-          if (st == 2) state = 1;
-        }
-      }
-    }
-    uint32_t tot = sum;
-    int adv = used, fin = state == 1;
-    if (G > 1) {
-      tot = 0;
-      adv = 0;
-      fin = 0;
-      bool stop = false;
-#pragma unroll
-      for (int qq = 0; qq < G; ++qq) {
-        const uint32_t s_q = __shfl(sum, gl + qq, 64);
-        const int u_q = __shfl(used, gl + qq, 64);
-        const int st_q = __shfl(state, gl + qq, 64);
-        if (!stop) {
-          tot += s_q;
-          adv += u_q;
-          if (st_q != 0) {
-            stop = true;
-            fin = st_q == 1;
-          }
-        }
-      }
-    }
-    excl += tot;
-    if (fin) break;
-    j -= adv;
-    if (adv == 0) {
-      if (++spins > LB_SPIN_LIMIT) {
-        atomicOr(err, 4u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  if (q == 0) st_u32(my, PFX | (excl + run));
-  return excl;
-}
-
-template <typename K, int NTB, int IPT, int LBR>
-__global__ __launch_bounds__(NTB) void k_sp_pass2(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                  const uint64_t* __restrict__ d_n, int shift,
-                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
-                                                  uint32_t* __restrict__ err, uint64_t* __restrict__ stamp) {
-  constexpr int NW = NTB / 64, G = NTB / RS_BINS, WT = 64 * IPT, TILE = NTB * IPT;
-  static_assert(G == 1 || G == 2 || G == 4, "threads per digit");
-  __shared__ uint16_t s_cnt[IPT][NW][RS_BINS];
-  __shared__ uint32_t s_base[RS_BINS];
-  __shared__ uint32_t s_dbase[RS_BINS];
-  __shared__ uint32_t s_wsum[4];
-  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint64_t n = *d_n;
-  const uint64_t ntiles = (n + TILE - 1) / TILE;
-  if (blockIdx.x >= ntiles) return;
-  if (t < RS_BINS) {  // digit bases: exclusive scan of the global histogram
-    const uint32_t h = hist_total(ghist, t);
-    uint32_t inc = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    if (lane == 63) s_wsum[wv] = inc;
-    s_dbase[t] = inc - h;
-  }
-  __syncthreads();
-  if (t < RS_BINS)
-    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
-  const uint64_t lt = lane_mask_lt();
-  const int dd_d = t / G, dd_q = t % G;  // digit group of this thread
-  constexpr int WPQ = NW / G;            // waves summed by each thread of a digit group
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
-    sp_stamp(stamp, first, 0);
-    {
-      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
-      for (int i = t; i < IPT * NW * RS_BINS / 2; i += NTB) z[i] = 0;
-    }
-    __syncthreads();
-    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
-    K k[IPT];
-    uint32_t v[IPT], dg[IPT], rk[IPT];
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const uint64_t j = b0 + (uint64_t)i * 64;
-      k[i] = j < n ? kin[j] : (K)0;
-      v[i] = j < n ? vin[j] : 0u;
-    }
-    if (stamp) {
-      uint64_t z = 0;
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
-      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
-      sp_stamp(stamp, first, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const bool ok = b0 + (uint64_t)i * 64 < n;
-      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
-      dg[i] = d;
-      uint64_t peers = __ballot(ok);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint64_t bb = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bb : ~bb;
-      }
-      rk[i] = (uint32_t)__popcll(peers & lt);
-      if (ok && (peers & lt) == 0) s_cnt[i][wv][d] = (uint16_t)__popcll(peers);
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 2);
-    // digit group (d, q): waves [q WPQ, (q+1) WPQ) in tile order (wave-major, substep-minor)
-    uint32_t loc = 0;
-#pragma unroll
-    for (int w = 0; w < WPQ; ++w)
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) loc += s_cnt[i][dd_q * WPQ + w][dd_d];
-    uint32_t before = 0, run = loc;
-    if (G > 1) {
-      const int gl = lane & ~(G - 1);
-      run = 0;
-#pragma unroll
-      for (int qq = 0; qq < G; ++qq) {
-        const uint32_t x = __shfl(loc, gl + qq, 64);
-        before += qq < dd_q ? x : 0u;
-        run += x;
-      }
-    }
-    uint32_t acc = before;
-#pragma unroll
-    for (int w = 0; w < WPQ; ++w)
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) {
-        const uint32_t c = s_cnt[i][dd_q * WPQ + w][dd_d];
-        s_cnt[i][dd_q * WPQ + w][dd_d] = (uint16_t)acc;
-        acc += c;
-      }
-    const uint32_t excl = osg_lookback<G, LBR>(desc, tile, dd_d, dd_q, run, err);
-    if (dd_q == 0) s_base[dd_d] = s_dbase[dd_d] + excl;
-    __syncthreads();
-    sp_stamp(stamp, first, 3);
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (b0 + (uint64_t)i * 64 < n) {
-        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_cnt[i][wv][dg[i]] + rk[i];
-        kout[pos] = k[i];
-        vout[pos] = v[i];
-      }
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 4);
-  }
-}
-
-// ---------------------------------------------------------------- onesweep pass, 1024-thread tiles
-// Same contract as k_sp_pass.  A tile is 16 waves x IPT substeps x 64 keys, so a
-// tile needs few serial substeps per wave and a small grid covers the keys;
-// per-(substep, wave, digit) counts are u16 in LDS, written by the digit
-// group's leader lane without read-modify-write.  Four threads serve each
-// digit: they prefix-sum the counts and read 64 predecessors per look-back
-// round trip between them.
-constexpr int OSB_NT = 1024;
-constexpr int OSB_NW = OSB_NT / 64;
-
-__device__ __forceinline__ uint32_t osb_lookback(uint32_t* desc, uint64_t tile, int d, int q, uint32_t run,
-                                                 uint32_t* err) {
-  constexpr uint32_t AGG = 1u << 30, PFX = 2u << 30, VAL = AGG - 1;
-  constexpr int R = 16;
-  uint32_t* my = desc + tile * RS_BINS + d;
-  if (tile == 0) {
-    if (q == 0) st_u32(my, PFX | run);
-    return 0;
-  }
-  if (q == 0) st_u32(my, AGG | run);
-  const int gl = lane_id() & ~3;
-  uint32_t excl = 0, spins = 0;
-  int64_t j = (int64_t)tile - 1;
-  while (true) {
-    uint32_t x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t jj = j - (int64_t)(q * R + r);
-      x[r] = jj >= 0 ? ld_u32(desc + (uint64_t)jj * RS_BINS + d) : PFX;
-    }
-    uint32_t sum = 0;
-    int used = 0, state = 0;  // state: 0 open, 1 found a prefix, 2 blocked
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (state == 0) {
-        const uint32_t st = x[r] >> 30;
-        if (st == 0) {
-          state = 2;
-        } else {
-          sum += x[r] & VAL;
-          ++used;
-          if (st == 2) state = 1;
-        }
-      }
-    }
-    uint32_t tot = 0;
-    int adv = 0, fin = 0;
-    bool stop = false;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const uint32_t s_q = __shfl(sum, gl + qq, 64);
-      const int u_q = __shfl(used, gl + qq, 64);
-      const int st_q = __shfl(state, gl + qq, 64);
-      if (!stop) {
-        tot += s_q;
-        adv += u_q;
-        if (st_q != 0) {
-          stop = true;
-          fin = st_q == 1;
-        }
-      }
-    }
-    excl += tot;
-    if (fin) break;
-    j -= adv;
-    if (adv == 0) {
-      if (++spins > LB_SPIN_LIMIT) {
-        atomicOr(err, 4u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  if (q == 0) st_u32(my, PFX | (excl + run));
-  return excl;
-}
-
-template <typename K, int IPT>
-__global__ __launch_bounds__(OSB_NT) void k_sp_passb(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                     K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                     const uint64_t* __restrict__ d_n, int shift,
-                                                     const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
-                                                     uint32_t* __restrict__ err, uint64_t* __restrict__ stamp) {
-  constexpr int WT = 64 * IPT, TILE = OSB_NT * IPT;
-  __shared__ uint16_t s_cnt[IPT][OSB_NW][RS_BINS];
-  __shared__ uint32_t s_base[RS_BINS];
-  __shared__ uint32_t s_dbase[RS_BINS];
-  __shared__ uint32_t s_wsum[4];
-  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint64_t n = *d_n;
-  const uint64_t ntiles = (n + TILE - 1) / TILE;
-  if (blockIdx.x >= ntiles) return;
-  // digit bases: exclusive scan of the global histogram (waves 0-3)
-  if (t < RS_BINS) {
-    const uint32_t h = hist_total(ghist, t);
-    uint32_t inc = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    if (lane == 63) s_wsum[wv] = inc;
-    s_dbase[t] = inc - h;
-  }
-  __syncthreads();
-  if (t < RS_BINS)
-    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
-  const uint64_t lt = lane_mask_lt();
-  const int dg_d = t >> 2, dg_q = t & 3;  // digit group of this thread
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
-    sp_stamp(stamp, first, 0);
-    {
-      uint32_t* z = (uint32_t*)&s_cnt[0][0][0];
-      for (int i = t; i < IPT * OSB_NW * RS_BINS / 2; i += OSB_NT) z[i] = 0;
-    }
-    __syncthreads();
-    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
-    K k[IPT];
-    uint32_t v[IPT], dg[IPT], rk[IPT];
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const uint64_t j = b0 + (uint64_t)i * 64;
-      k[i] = j < n ? kin[j] : (K)0;
-      v[i] = j < n ? vin[j] : 0u;
-    }
-    if (stamp) {
-      uint64_t z = 0;
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
-      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
-      sp_stamp(stamp, first, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const bool ok = b0 + (uint64_t)i * 64 < n;
-      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
-      dg[i] = d;
-      uint64_t peers = __ballot(ok);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint64_t bb = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bb : ~bb;
-      }
-      rk[i] = (uint32_t)__popcll(peers & lt);
-      if (ok && (peers & lt) == 0) s_cnt[i][wv][d] = (uint16_t)__popcll(peers);
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 2);
-    // digit group (d, q): waves 4q..4q+3 in tile order (wave-major, substep-minor)
-    uint32_t loc = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) loc += s_cnt[i][dg_q * 4 + w][dg_d];
-    const int gl = lane & ~3;
-    uint32_t before = 0, run = 0;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const uint32_t x = __shfl(loc, gl + qq, 64);
-      before += qq < dg_q ? x : 0u;
-      run += x;
-    }
-    uint32_t acc = before;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) {
-        const uint32_t c = s_cnt[i][dg_q * 4 + w][dg_d];
-        s_cnt[i][dg_q * 4 + w][dg_d] = (uint16_t)acc;
-        acc += c;
-      }
-    const uint32_t excl = osb_lookback(desc, tile, dg_d, dg_q, run, err);
-    if (dg_q == 0) s_base[dg_d] = s_dbase[dg_d] + excl;
-    __syncthreads();
-    sp_stamp(stamp, first, 3);
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (b0 + (uint64_t)i * 64 < n) {
-        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_cnt[i][wv][dg[i]] + rk[i];
-        kout[pos] = k[i];
-        vout[pos] = v[i];
-      }
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 4);
   }
 }
 
@@ -992,7 +796,8 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
                                                      uint32_t* __restrict__ ohist /*4 x 256*/,
                                                      uint64_t* __restrict__ stamp, uint64_t* __restrict__ skey = nullptr,
                                                      uint32_t* __restrict__ rlen = nullptr,
-                                                     uint32_t* __restrict__ vsorted = nullptr) {
+                                                     uint32_t* __restrict__ vsorted = nullptr,
+                                                     uint32_t* __restrict__ tick = nullptr) {
   __shared__ uint64_t s_k2[2][BK_CAP];
   __shared__ uint32_t s_oh[1][RS_BINS];
   __shared__ uint16_t s_p2[2][BK_CAP];
@@ -1001,9 +806,12 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
   __shared__ uint16_t s_rs[BK_CAP + 1];  // start position of each (u, w) run
   __shared__ uint32_t s_wsum[BK_NW];
   __shared__ uint64_t s_excl;
-  __shared__ uint32_t s_start, s_bcnt;
+  __shared__ uint32_t s_start, s_bcnt, s_b;
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint32_t b = blockIdx.x;
+  // the fused variant compacts behind the preceding buckets (look-back): its
+  // bucket ids come from an ordered ticket, so a bucket only waits on buckets
+  // whose workgroups are running
+  if (t == 0) s_b = tick ? atomicAdd(tick, 1u) : blockIdx.x;
   uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
   const uint64_t n = ctr[C_WSORT];
   sp_stamp(stamp, true, 0);
@@ -1020,13 +828,13 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
     __syncthreads();
     uint32_t pre = inc - h;
     for (int w = 0; w < wv; ++w) pre += s_wsum[w];
-    if (t == (int)b) {
+    if (t == (int)s_b) {
       s_start = pre;
       s_bcnt = h;
     }
     __syncthreads();
   }
-  const uint32_t start = s_start, c = s_bcnt;
+  const uint32_t start = s_start, c = s_bcnt, b = s_b;
   sp_stamp(stamp, true, 1);
   if (t < RS_BINS) s_oh[0][t] = 0;
   const bool toobig = c > (uint32_t)BK_CAP;
@@ -1231,7 +1039,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
       if (CUSTOM) sc = excl ? 0.0f : racc[j];
       else sc = score_basic(metric, excl ? 0u : rc[j], du[j], dw[j]);
       s_sc[r] = sc;
-      s_flag[r] = !(sc <= min_score) ? 1u : 0u;  // NaN passes
+      s_flag[r] = (!(sc <= min_score) && !f2_drop(g, ru[j], rw[j])) ? 1u : 0u;  // NaN passes
     }
   }
   __syncthreads();
@@ -1296,127 +1104,6 @@ __global__ __launch_bounds__(BK_NT) void k_sp_bucket(GraphView g, int metric, fl
     if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
   }
   sp_stamp(stamp, true, 6);
-}
-
-// ---------------------------------------------------------------- onesweep pass, 512-thread tiles
-// Same contract as k_sp_pass (running per-wave digit counters), with 8 waves of
-// IPT keys each: a tile of 4096 keys takes half the serial ranking steps per
-// wave, and two threads per digit read 2 x LBR predecessors per look-back
-// round trip (one round trip for up to 64 tiles with LBR = 32).
-template <typename K, int IPT, int LBR>
-__global__ __launch_bounds__(512) void k_sp_pass3(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                  const uint64_t* __restrict__ d_n, int shift,
-                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ desc,
-                                                  uint32_t* __restrict__ err, uint64_t* __restrict__ stamp,
-                                                  uint32_t* __restrict__ nhist) {
-  constexpr int NTB = 512, NW = 8, WT = 64 * IPT, TILE = NTB * IPT;
-  __shared__ uint32_t s_wcnt[NW][RS_BINS];
-  __shared__ uint32_t s_base[RS_BINS];
-  __shared__ uint32_t s_dbase[RS_BINS];
-  __shared__ uint32_t s_wsum[4];
-  __shared__ uint32_t s_nh[3][RS_BINS];
-  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint64_t n = *d_n;
-  const uint64_t ntiles = (n + TILE - 1) / TILE;
-  if (blockIdx.x >= ntiles) return;
-  if (t < RS_BINS) {
-    const uint32_t h = hist_total(ghist, t);
-    uint32_t inc = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    if (lane == 63) s_wsum[wv] = inc;
-    s_dbase[t] = inc - h;
-  }
-  if (nhist)
-    for (int i = t; i < 3 * RS_BINS; i += NTB) (&s_nh[0][0])[i] = 0;
-  __syncthreads();
-  if (t < RS_BINS)
-    for (int w = 0; w < wv; ++w) s_dbase[t] += s_wsum[w];
-  const uint64_t lt = lane_mask_lt();
-  const int dd_d = t >> 1, dd_q = t & 1;  // two threads per digit
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
-    sp_stamp(stamp, first, 0);
-    for (int i = t; i < NW * RS_BINS; i += NTB) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
-    K k[IPT];
-    uint32_t v[IPT], dg[IPT], rk[IPT];
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const uint64_t j = b0 + (uint64_t)i * 64;
-      k[i] = j < n ? kin[j] : (K)0;
-      v[i] = j < n ? vin[j] : 0u;
-    }
-    if (stamp) {
-      uint64_t z = 0;
-#pragma unroll
-      for (int i = 0; i < IPT; ++i) z |= (uint64_t)k[i] ^ v[i];
-      if (z == 0x5a5a5a5a5a5aull) stamp[0] = z;
-      sp_stamp(stamp, first, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const bool ok = b0 + (uint64_t)i * 64 < n;
-      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
-      dg[i] = d;
-      uint64_t peers = __ballot(ok);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint64_t bb = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? bb : ~bb;
-      }
-      const uint32_t before = ok ? s_wcnt[wv][d] : 0u;
-      rk[i] = before + (uint32_t)__popcll(peers & lt);
-      wave_lds_sync();
-      if (ok && (peers & lt) == 0) s_wcnt[wv][d] = before + (uint32_t)__popcll(peers);
-      wave_lds_sync();
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 2);
-    // digit pair (d, q): waves 4q..4q+3, combined by one shuffle
-    uint32_t loc = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) loc += s_wcnt[dd_q * 4 + w][dd_d];
-    const uint32_t other = __shfl_xor(loc, 1, 64);
-    const uint32_t run = loc + other;
-    uint32_t acc = dd_q ? other : 0u;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t c = s_wcnt[dd_q * 4 + w][dd_d];
-      s_wcnt[dd_q * 4 + w][dd_d] = acc;
-      acc += c;
-    }
-    const uint32_t excl = osg_lookback<2, LBR>(desc, tile, dd_d, dd_q, run, err);
-    if (dd_q == 0) s_base[dd_d] = s_dbase[dd_d] + excl;
-    __syncthreads();
-    sp_stamp(stamp, first, 3);
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (b0 + (uint64_t)i * 64 < n) {
-        const uint64_t pos = (uint64_t)s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
-        kout[pos] = k[i];
-        vout[pos] = v[i];
-        if (nhist) {
-#pragma unroll
-          for (int dd = 0; dd < 3; ++dd) atomicAdd(&s_nh[dd][(uint32_t)(k[i] >> (8 * dd + 8)) & 0xffu], 1u);
-        }
-      }
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 4);
-  }
-  if (nhist) {
-    uint32_t* hc = hist_copy(nhist);
-    for (int i = t; i < 3 * RS_BINS; i += NTB) {
-      const uint32_t c = s_nh[i / RS_BINS][i % RS_BINS];
-      if (c) atomicAdd(&hc[i], c);
-    }
-  }
 }
 
 // ---------------------------------------------------------------- group sort
@@ -1620,69 +1307,77 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
 }
 
 // ---------------------------------------------------------------- balanced run scoring
-// Over the bucket-sorted records: thread j of a tile looks at records
-// base + r * NT + j; those that start a run (rlen > 0) are scored -- first-order
-// exclusion by searching the shorter of N(u) and I(w), the metric, the
-// minScore filter -- with the searches of a thread's runs in lockstep.  The
-// candidates are compacted in record order ((u, w) order) behind the preceding
-// tiles (look-back), and digit 0 of their order keys is counted.
-#ifndef NLP_RU_IPT
-#define NLP_RU_IPT 4
-#endif
-constexpr int RU_IPT = NLP_RU_IPT;
-constexpr int RU_TILE = NT * RU_IPT;
-
+// Over the bucket-sorted records, one workgroup per tile of RU_TILE records,
+// wave w on records [base + 64 RU_IPT w, +64 RU_IPT): those that start a run
+// (rlen > 0) are scored -- first-order exclusion (predict.hxx:306-307), the
+// metric, the minScore filter (predict.hxx:311).  No hand-off between
+// workgroups: tile t writes its candidates, in record ((u, w)) order, to the
+// slots [t RU_TILE, t RU_TILE + seg_cnt[t]) of the candidate columns (a
+// "gapped" layout), and the first ordering pass (k_sp_pass<.., GAPPED>) reads
+// each tile as one wave segment.  Digit 0 of the order keys is counted.
+//
+// Exclusion: with the membership table (kernels.hpp et_has) every run costs
+// the same two dependent round trips (its key, then table line and degrees);
+// without it, the edge filter and a lockstep 4-way search of the shorter of
+// N(u) and I(w).
 template <bool CUSTOM>
 __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float min_score, uint64_t ua, int wbits,
                                                 const uint64_t* __restrict__ skey, const uint32_t* __restrict__ rlen,
                                                 const uint32_t* __restrict__ vsorted, uint32_t* __restrict__ cu,
                                                 uint32_t* __restrict__ cw, float* __restrict__ cs,
                                                 uint32_t* __restrict__ okey, uint32_t* __restrict__ oval,
-                                                uint64_t* __restrict__ desc, uint64_t* __restrict__ ctr, uint64_t kmax,
+                                                uint32_t* __restrict__ seg_cnt, uint64_t* __restrict__ ctr,
                                                 uint32_t* __restrict__ ohist, uint64_t* __restrict__ stamp) {
-  __shared__ uint32_t s_f[RU_TILE];
-  __shared__ float s_sc[RU_TILE];
-  __shared__ uint64_t s_red[NWAVE + 1];
-  __shared__ uint64_t s_excl;
   __shared__ uint32_t s_oh[RS_BINS];
-  const int t = threadIdx.x;
-  uint32_t* err = (uint32_t*)&ctr[C_FLAGS] + 1;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t n = ctr[C_WSORT];
-  const uint64_t ntiles = (n + RU_TILE - 1) / RU_TILE;
-  if (blockIdx.x >= ntiles) return;
+  const uint64_t tile = blockIdx.x;
+  if (tile * RU_TILE >= n) return;
   s_oh[t] = 0;
+  __syncthreads();
+  sp_stamp(stamp, true, 0);
   const uint64_t wmask = (1ull << wbits) - 1;
-  const bool sym = g.toff == g.off;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const bool first = tile == blockIdx.x;
-    sp_stamp(stamp, first, 0);
-    const uint64_t base = tile * RU_TILE;
-    uint32_t ru[RU_IPT], rw[RU_IPT], rc[RU_IPT], lo[RU_IPT], hi[RU_IPT], du[RU_IPT], dw[RU_IPT], tg[RU_IPT],
-        ln[RU_IPT];
+  const uint64_t b0 = tile * RU_TILE + (uint64_t)wv * RU_SEG + lane;
+  uint32_t ru[RU_IPT], rw[RU_IPT], rc[RU_IPT], du[RU_IPT], dw[RU_IPT];
+  bool has[RU_IPT], ex[RU_IPT];
+  float racc[RU_IPT];
+#pragma unroll
+  for (int j = 0; j < RU_IPT; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * 64;
+    const bool in = i < n;
+    rc[j] = in ? rlen[i] : 0u;
+    const uint64_t k = in ? skey[i] : 0ull;
+    has[j] = rc[j] != 0;
+    ru[j] = (uint32_t)(ua + (k >> wbits));
+    rw[j] = (uint32_t)(k & wmask);
+  }
+#pragma unroll
+  for (int j = 0; j < RU_IPT; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * 64;
+    float acc = 0.0f;
+    if (CUSTOM && has[j])  // the reference's order: ascending v
+      for (uint32_t q = 0; q < rc[j]; ++q) acc = (float)((double)acc + g.ctab[g.deg[vsorted[i + q]]]);
+    racc[j] = acc;
+    du[j] = has[j] ? g.deg[ru[j]] : 0u;
+    dw[j] = (has[j] && !CUSTOM) ? g.deg[rw[j]] : 0u;
+  }
+  if (g.etab) {
+#pragma unroll
+    for (int j = 0; j < RU_IPT; ++j) ex[j] = has[j] && et_has(g.etab, g.etbits, ru[j], rw[j]);
+  } else {
+    // w in N(u) <=> u in I(w): search the shorter list, lockstep, 4-way
+    const bool sym = g.toff == g.off;
+    uint32_t lo[RU_IPT], hi[RU_IPT], tg[RU_IPT], ln[RU_IPT];
     const uint32_t* rl[RU_IPT];
-    float racc[RU_IPT];
-    bool has[RU_IPT];
 #pragma unroll
     for (int j = 0; j < RU_IPT; ++j) {
-      const uint64_t i = base + (uint64_t)j * NT + t;
-      rc[j] = i < n ? rlen[i] : 0u;
-      has[j] = rc[j] != 0;
-      const uint64_t k = has[j] ? skey[i] : 0ull;
-      ru[j] = (uint32_t)(ua + (k >> wbits));
-      rw[j] = (uint32_t)(k & wmask);
-      float acc = 0.0f;
-      if (CUSTOM && has[j])  // the reference's order: ascending v
-        for (uint32_t q = 0; q < rc[j]; ++q) acc = (float)((double)acc + g.ctab[g.deg[vsorted[i + q]]]);
-      racc[j] = acc;
-    }
-#pragma unroll
-    for (int j = 0; j < RU_IPT; ++j) {
+      rl[j] = g.keys;
+      tg[j] = 0;
+      ln[j] = 0;
       if (has[j]) {
-        const uint64_t ou = g.off[ru[j]], ou1 = g.off[ru[j] + 1];
+        const uint64_t ou = g.off[ru[j]];
         const uint64_t tw = g.toff[rw[j]], tw1 = g.toff[rw[j] + 1];
-        du[j] = (uint32_t)(ou1 - ou);
-        const uint32_t iw = (uint32_t)(tw1 - tw);
-        dw[j] = CUSTOM ? 0u : (sym ? iw : g.deg[rw[j]]);
+        const uint32_t iw = sym ? dw[j] : (uint32_t)(tw1 - tw);
         const bool via_w = iw < du[j];
         rl[j] = via_w ? g.tkeys + tw : g.keys + ou;
         tg[j] = via_w ? ru[j] : rw[j];
@@ -1691,20 +1386,12 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
           const uint64_t h = edge_slot(ru[j], rw[j], g.efbits);
           if (!((g.efilt[h >> 5] >> (h & 31)) & 1u)) ln[j] = 0;
         }
-      } else {
-        rl[j] = g.keys;
-        tg[j] = 0;
-        ln[j] = 0;
-        du[j] = dw[j] = 0;
       }
       lo[j] = 0;
       hi[j] = ln[j];
     }
-    // lower bounds, in lockstep, 4-way: the lower bound lies in [lo, hi]; each
-    // round trip loads the last element of the first three quarters, so a
-    // search takes log4 instead of log2 dependent loads
     bool more = true;
-    while (more) {
+    while (more) {  // the lower bound lies in [lo, hi]; 3 pivots per round trip
       more = false;
       uint32_t st[RU_IPT], pv[RU_IPT][3];
 #pragma unroll
@@ -1730,82 +1417,72 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
       }
     }
 #pragma unroll
-    for (int j = 0; j < RU_IPT; ++j) {
-      uint32_t fl = 0;
-      float sc = 0.0f;
-      if (has[j]) {
-        const bool excl = lo[j] < ln[j] && rl[j][lo[j]] == tg[j];
-        if (CUSTOM) sc = excl ? 0.0f : racc[j];
-        else sc = score_basic(metric, excl ? 0u : rc[j], du[j], dw[j]);
-        fl = !(sc <= min_score) ? 1u : 0u;  // NaN passes
-      }
-      s_f[j * NT + t] = fl;
-      s_sc[j * NT + t] = sc;
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 1);
-    // blocked compaction: thread t owns tile items [4t, 4t+4)
-    uint32_t f[RU_IPT];
-    uint64_t tsum = 0;
-#pragma unroll
-    for (int r = 0; r < RU_IPT; ++r) {
-      f[r] = s_f[t * RU_IPT + r];
-      tsum += f[r];
-    }
-    uint64_t agg;
-    const uint64_t pre = block_excl_scan(tsum, s_red, &agg);
-    if (wave_id() == 0) {
-      const uint64_t e = lb_lookback_r<4>(desc, tile, agg, err);
-      if (lane_id() == 0) {
-        s_excl = e;
-        if (tile == ntiles - 1) {
-          ctr[C_C] = e + agg;
-          ctr[C_OUT_N] = std::min<uint64_t>(e + agg, kmax);
-        }
-      }
-    }
-    __syncthreads();
-    sp_stamp(stamp, first, 2);
-    uint64_t o = s_excl + pre;
-    uint32_t nnan = 0;
-#pragma unroll
-    for (int r = 0; r < RU_IPT; ++r) {
-      if (f[r]) {
-        const uint64_t i = base + (uint64_t)t * RU_IPT + r;
-        const uint64_t k = skey[i];
-        const float sc = s_sc[t * RU_IPT + r];
-        cu[o] = (uint32_t)(ua + (k >> wbits));
-        cw[o] = (uint32_t)(k & wmask);
-        cs[o] = sc;
-        const uint32_t ok = ~score_key(sc);
-        okey[o] = ok;
-        oval[o] = (uint32_t)o;
-        atomicAdd(&s_oh[ok & 0xffu], 1u);
-        nnan += sc != sc;
-        ++o;
-      }
-    }
-    if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
-    __syncthreads();
-    sp_stamp(stamp, first, 3);
+    for (int j = 0; j < RU_IPT; ++j) ex[j] = lo[j] < ln[j] && rl[j][lo[j]] == tg[j];
   }
+  sp_stamp(stamp, true, 1);
+  // wave-local compaction in record order
+  uint32_t pos = 0, nnan = 0;
+  const uint64_t lt = lane_mask_lt();
+  uint32_t sbase = (uint32_t)(tile * RU_TILE + (uint64_t)wv * RU_SEG);
+  float sc[RU_IPT];
+  bool keep[RU_IPT];
+  uint32_t rank[RU_IPT];
+#pragma unroll
+  for (int j = 0; j < RU_IPT; ++j) {
+    sc[j] = 0.0f;
+    keep[j] = false;
+    if (has[j]) {
+      if (CUSTOM) sc[j] = ex[j] ? 0.0f : racc[j];
+      else sc[j] = score_basic(metric, ex[j] ? 0u : rc[j], du[j], dw[j]);
+      keep[j] = !(sc[j] <= min_score) && !f2_drop(g, ru[j], rw[j]);  // NaN passes
+    }
+    const uint64_t m = __ballot(keep[j]);
+    rank[j] = pos + (uint32_t)__popcll(m & lt);
+    pos += (uint32_t)__popcll(m);
+  }
+  // candidates of wave wv go to its own segment: slots [sbase, sbase + pos)
+#pragma unroll
+  for (int j = 0; j < RU_IPT; ++j) {
+    if (keep[j]) {
+      const uint32_t o = sbase + rank[j];
+      cu[o] = ru[j];
+      cw[o] = rw[j];
+      cs[o] = sc[j];
+      const uint32_t k = ~score_key(sc[j]);
+      okey[o] = k;
+      oval[o] = o;
+      atomicAdd(&s_oh[k & 0xffu], 1u);
+      nnan += sc[j] != sc[j];
+    }
+  }
+  if (lane == 0) seg_cnt[tile * NWAVE + wv] = pos;
+  if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
+  __syncthreads();
+  sp_stamp(stamp, true, 2);
   const uint32_t hc = s_oh[t];
   if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
 }
 
 // ---------------------------------------------------------------- generic single-pass scan
-// F: count(i) -> u32 (evaluated once, striped), emit(i, off, c).  Persistent
-// blockIdx-ordered tiles; the grand total goes to *total.
+// F: count(i) -> u32 (evaluated once, striped), emit(i, off, c).  Ticketed
+// tiles (see k_sp_pass); the grand total goes to *total.
 template <class F, int IPT>
 __global__ __launch_bounds__(NT) void k_sp_scan(F f, const uint64_t* __restrict__ d_n, uint64_t* __restrict__ desc,
-                                                uint32_t* __restrict__ err, uint64_t* __restrict__ total) {
+                                                uint32_t* __restrict__ tick, uint32_t* __restrict__ err,
+                                                uint64_t* __restrict__ total) {
   constexpr int TILE = NT * IPT;
   __shared__ uint32_t s_cnt[TILE];
   __shared__ uint64_t s_red[NWAVE + 1];
   __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_tk[2];
   const uint64_t n = *d_n;
   const uint64_t ntiles = (n + TILE - 1) / TILE;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  if (blockIdx.x >= ntiles) return;  // only as many claimants as tiles
+  tk_draw(tick, &s_tk[0]);
+  __syncthreads();
+  for (int par = 0;; par ^= 1) {
+    const uint64_t tile = s_tk[par];
+    if (tile >= ntiles) break;
     const uint64_t base = tile * TILE;
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
@@ -1813,6 +1490,7 @@ __global__ __launch_bounds__(NT) void k_sp_scan(F f, const uint64_t* __restrict_
       s_cnt[i * NT + threadIdx.x] = j < n ? f.count(j, n) : 0u;
     }
     __syncthreads();
+    tk_draw(tick, &s_tk[par ^ 1]);
     uint32_t cs[IPT];
     uint64_t s = 0;
 #pragma unroll
@@ -1879,12 +1557,12 @@ struct F_Runs {
     }
     const uint32_t u = (uint32_t)(ua + (k >> wbits));
     const uint32_t w = (uint32_t)(k & ((1ull << wbits) - 1));
-    const bool excl = contains_u32(g.keys + g.off[u], g.deg[u], w);
+    const bool excl = first_order(g, u, w);
     float sc;
     if (CUSTOM) sc = excl ? 0.0f : acc;
     else sc = score_basic(metric, excl ? 0u : c, g.deg[u], g.deg[w]);
     stash[i] = sc;
-    return !(sc <= min_score) ? 1u : 0u;  // NaN passes
+    return (!(sc <= min_score) && !f2_drop(g, u, w)) ? 1u : 0u;  // NaN passes
   }
   __device__ void emit(uint64_t i, uint64_t off, uint32_t c) const {
     if (!c) return;

@@ -20,6 +20,9 @@
  *   - predictScanEdgesBasicU / predictScanEdgesU inc/predict.hxx:153-179
  *   - predictClearScanW                         inc/predict.hxx:187-192
  *   - the nine metric score/update lambdas      inc/predict.hxx:502-831
+ *   - the MAXFACTOR2 clause of ft (predict.hxx:221,295): with F > 0 a
+ *     second-hop w is counted only when deg(w) <= F * deg(u) (its
+ *     deg(u) <= F * deg(u) clause always holds for F >= 1)
  *   - degree() counts duplicate adjacency entries (Graph.hxx:167-169,
  *     _bitset.hxx:53), so every list is treated as a sorted multiset.
  *
@@ -125,7 +128,7 @@ static int cmp_cand(const void *x, const void *y) {
  * the number of those with w > u (the wedges that reach the counter table).
  */
 static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
-                     int metric, uint32_t hub, float min_score,
+                     int metric, uint32_t hub, uint32_t maxf2, float min_score,
                      uint64_t u_begin, uint64_t u_end, cvec_t *out,
                      uint64_t *wedges_out, uint64_t *wedges_gt_out) {
   int custom = (metric == NLPO_AA || metric == NLPO_RA);
@@ -148,6 +151,8 @@ static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
         ++wedges;
         if (!(w > u)) continue;                      /* ft: predict.hxx:221 */
         ++wedges_gt;
+        if (maxf2 && (w < span ? off[w + 1] - off[w] : 0) > (uint64_t)maxf2 * du)
+          continue;                                  /* ft, MAXFACTOR2 clause */
         if (custom) {
           if (!acc[w]) touched[nt++] = w;            /* predict.hxx:176 */
           acc[w] = (float)((double)acc[w] + c);      /* fu: entry += 1.0/..  */
@@ -192,14 +197,14 @@ static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
  * candidates that passed the score filter, *n_nan those with NaN score,
  * *n_wedges the wedges scanned.  Returns 0 on success, -1 on allocation failure.
  */
-int nlpo_predict_range(const uint64_t *off, const uint32_t *keys, uint64_t span,
-                       int metric, uint32_t hub, float min_score, uint64_t max_edges,
-                       uint64_t u_begin, uint64_t u_end,
-                       uint32_t *out_u, uint32_t *out_w, float *out_score,
-                       uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
-                       uint64_t *n_wedges, uint64_t *n_wedges_gt) {
+int nlpo_predict_range2(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                        int metric, uint32_t hub, uint32_t maxf2, float min_score, uint64_t max_edges,
+                        uint64_t u_begin, uint64_t u_end,
+                        uint32_t *out_u, uint32_t *out_w, float *out_score,
+                        uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
+                        uint64_t *n_wedges, uint64_t *n_wedges_gt) {
   cvec_t c = {0, 0, 0};
-  if (enumerate(off, keys, span, metric, hub, min_score, u_begin, u_end, &c, n_wedges, n_wedges_gt)) {
+  if (enumerate(off, keys, span, metric, hub, maxf2, min_score, u_begin, u_end, &c, n_wedges, n_wedges_gt)) {
     free(c.a); return -1;
   }
   uint64_t nn = 0;
@@ -240,6 +245,16 @@ int nlpo_predict_range(const uint64_t *off, const uint32_t *keys, uint64_t span,
   if (out_count) *out_count = c.n;
   free(c.a);
   return 0;
+}
+
+int nlpo_predict_range(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                       int metric, uint32_t hub, float min_score, uint64_t max_edges,
+                       uint64_t u_begin, uint64_t u_end,
+                       uint32_t *out_u, uint32_t *out_w, float *out_score,
+                       uint64_t *out_count, uint64_t *n_candidates, uint64_t *n_nan,
+                       uint64_t *n_wedges, uint64_t *n_wedges_gt) {
+  return nlpo_predict_range2(off, keys, span, metric, hub, 0, min_score, max_edges, u_begin, u_end,
+                             out_u, out_w, out_score, out_count, n_candidates, n_nan, n_wedges, n_wedges_gt);
 }
 
 int nlpo_predict(const uint64_t *off, const uint32_t *keys, uint64_t span,

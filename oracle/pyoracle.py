@@ -36,14 +36,20 @@ def lib():
             ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p, u64p, u64p, u64p, u64p]
         L.nlpo_predict_range.restype = ctypes.c_int
+        L.nlpo_predict_range2.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p, u64p, u64p, u64p, u64p]
+        L.nlpo_predict_range2.restype = ctypes.c_int
         L.nlpo_score_key.argtypes = [ctypes.c_float]
         L.nlpo_score_key.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
 
-def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0, u_end=None):
-    """Canonical top-k from the C restatement.
+def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0, u_end=None, maxfactor2=0):
+    """Canonical top-k from the C restatement (maxfactor2: the reference's
+    MAXFACTOR2 template parameter, predict.hxx:221,295).
 
     Returns (u, w, score, info) with info = dict(candidates, nan, wedges, wedges_gt):
     wedges = all (u, v, w) the reference scans, wedges_gt = those with w > u."""
@@ -58,8 +64,8 @@ def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0
     ncand, nnan, nw, nwg, cnt = (ctypes.c_uint64() for _ in range(5))
     if max_edges is None:
         # first pass: count, so the output buffer can be sized exactly
-        rc = L.nlpo_predict_range(offsets.ctypes.data, keys.ctypes.data, span, metric, hub,
-                                  min_score, 0, u_begin, u_end, None, None, None,
+        rc = L.nlpo_predict_range2(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, maxfactor2,
+                                   min_score, 0, u_begin, u_end, None, None, None,
                                   ctypes.byref(cnt), ctypes.byref(ncand), ctypes.byref(nnan),
                                   ctypes.byref(nw), ctypes.byref(nwg))
         if rc:
@@ -69,8 +75,8 @@ def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0
     ou = np.empty(cap, np.uint32)
     ow = np.empty(cap, np.uint32)
     os_ = np.empty(cap, np.float32)
-    rc = L.nlpo_predict_range(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, min_score,
-                              int(max_edges), u_begin, u_end, ou.ctypes.data, ow.ctypes.data,
+    rc = L.nlpo_predict_range2(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, maxfactor2, min_score,
+                               int(max_edges), u_begin, u_end, ou.ctypes.data, ow.ctypes.data,
                               os_.ctypes.data, ctypes.byref(cnt), ctypes.byref(ncand),
                               ctypes.byref(nnan), ctypes.byref(nw), ctypes.byref(nwg))
     if rc:
@@ -120,13 +126,13 @@ def read_deletions(path):
     return p[:, 0].copy(), p[:, 1].copy()
 
 
-def ref_predict(csr_path, metric, hub, max_edges=-1, mode="seq", threads=1, repeat=1, out=None):
+def ref_predict(csr_path, metric, hub, max_edges=-1, mode="seq", threads=1, repeat=1, out=None, maxfactor2=0):
     """Run the compiled reference (oracle/_ref/ref_driver) -- only where it exists."""
     if isinstance(metric, str):
         metric = METRICS.index(metric)
     out = out or csr_path + ".pred.%d.%d.%s" % (metric, hub, mode)
     r = subprocess.run([REF_DRIVER, "predict", csr_path, str(metric), str(hub), str(max_edges), mode,
-                        str(threads), str(repeat), out], check=True, capture_output=True, text=True)
+                        str(threads), str(repeat), out, str(maxfactor2)], check=True, capture_output=True, text=True)
     t, ts, n = r.stdout.split()
     u, w, s = read_edges(out)
     return u, w, s, dict(time_ms=float(t), scoring_ms=float(ts))

@@ -15,10 +15,11 @@
 //       tidyBatchUpdateU; applyBatchUpdateOmpU                  (main.cxx:164-169)
 //       writes <out_prefix>.csr  (u64 span, u64 M, u64 off[span+1], u32 keys[M])
 //              <out_prefix>.del  (u64 n, u32 pairs[2n])  directed, sorted, unique
-//   predict <csr> <metric 0..8> <H> <maxEdges|-1> <seq|omp> <threads> <repeat> <out>
-//       runs predictLinks<Metric>[Omp]<H>(G, {repeat, maxEdges}) on a DiGraphCsr
-//       built from <csr>; writes u64 n, then n x {u32 u, u32 w, f32 score};
-//       prints "time_ms scoring_ms n" on stdout.
+//   predict <csr> <metric 0..8> <H> <maxEdges|-1> <seq|omp> <threads> <repeat> <out> [maxfactor2]
+//       runs predictLinks<Metric>[Omp]<H, MAXFACTOR2>(G, {repeat, maxEdges}) on a
+//       DiGraphCsr built from <csr>; writes u64 n, then n x {u32 u, u32 w, f32 score};
+//       prints "time_ms scoring_ms n" on stdout.  MAXFACTOR2 in {0, 1, 2, 4}
+//       (non-zero only with H in {0, 4}).
 //   time    <csr> <metric> <H> <maxEdges> <threads> <repeat>
 //       same as predict/omp without writing the edges (CPU baseline).
 #include <cstdio>
@@ -96,25 +97,43 @@ static int doIngest(int argc, char** argv) {
   return 0;
 }
 
-template <int H, bool OMP>
+template <int H, bool OMP, int F = 0>
 static PredictLinkResult<K, float> runMetric(const Csr& g, int metric, const PredictLinkOptions<float>& o) {
   switch (metric) {
-    case 0: return OMP ? predictLinksCommonNeighborsOmp<H>(g, o)         : predictLinksCommonNeighbors<H>(g, o);
-    case 1: return OMP ? predictLinksJaccardCoefficientOmp<H>(g, o)      : predictLinksJaccardCoefficient<H>(g, o);
-    case 2: return OMP ? predictLinksSorensenIndexOmp<H>(g, o)           : predictLinksSorensenIndex<H>(g, o);
-    case 3: return OMP ? predictLinksSaltonCosineSimilarityOmp<H>(g, o)  : predictLinksSaltonCosineSimilarity<H>(g, o);
-    case 4: return OMP ? predictLinksHubPromotedOmp<H>(g, o)             : predictLinksHubPromoted<H>(g, o);
-    case 5: return OMP ? predictLinksHubDepressedOmp<H>(g, o)            : predictLinksHubDepressed<H>(g, o);
-    case 6: return OMP ? predictLinksLeichtHolmeNermanScoreOmp<H>(g, o)  : predictLinksLeichtHolmeNermanScore<H>(g, o);
-    case 7: return OMP ? predictLinksAdamicAdarCoefficientOmp<H>(g, o)   : predictLinksAdamicAdarCoefficient<H>(g, o);
-    case 8: return OMP ? predictLinksResourceAllocationScoreOmp<H>(g, o) : predictLinksResourceAllocationScore<H>(g, o);
+    case 0: return OMP ? predictLinksCommonNeighborsOmp<H, F>(g, o)         : predictLinksCommonNeighbors<H, F>(g, o);
+    case 1: return OMP ? predictLinksJaccardCoefficientOmp<H, F>(g, o)      : predictLinksJaccardCoefficient<H, F>(g, o);
+    case 2: return OMP ? predictLinksSorensenIndexOmp<H, F>(g, o)           : predictLinksSorensenIndex<H, F>(g, o);
+    case 3: return OMP ? predictLinksSaltonCosineSimilarityOmp<H, F>(g, o)  : predictLinksSaltonCosineSimilarity<H, F>(g, o);
+    case 4: return OMP ? predictLinksHubPromotedOmp<H, F>(g, o)             : predictLinksHubPromoted<H, F>(g, o);
+    case 5: return OMP ? predictLinksHubDepressedOmp<H, F>(g, o)            : predictLinksHubDepressed<H, F>(g, o);
+    case 6: return OMP ? predictLinksLeichtHolmeNermanScoreOmp<H, F>(g, o)  : predictLinksLeichtHolmeNermanScore<H, F>(g, o);
+    case 7: return OMP ? predictLinksAdamicAdarCoefficientOmp<H, F>(g, o)   : predictLinksAdamicAdarCoefficient<H, F>(g, o);
+    case 8: return OMP ? predictLinksResourceAllocationScoreOmp<H, F>(g, o) : predictLinksResourceAllocationScore<H, F>(g, o);
   }
   die("bad metric");
   return {};
 }
 
+template <bool OMP, int F>
+static PredictLinkResult<K, float> dispatchF(const Csr& g, int metric, int H, const PredictLinkOptions<float>& o) {
+  switch (H) {
+    case 0: return runMetric<0, OMP, F>(g, metric, o);
+    case 4: return runMetric<4, OMP, F>(g, metric, o);
+  }
+  die("MAXFACTOR2 needs H in {0, 4}");
+  return {};
+}
+
 template <bool OMP>
-static PredictLinkResult<K, float> dispatch(const Csr& g, int metric, int H, const PredictLinkOptions<float>& o) {
+static PredictLinkResult<K, float> dispatch(const Csr& g, int metric, int H, const PredictLinkOptions<float>& o,
+                                            int F) {
+  switch (F) {
+    case 0: break;
+    case 1: return dispatchF<OMP, 1>(g, metric, H, o);
+    case 2: return dispatchF<OMP, 2>(g, metric, H, o);
+    case 4: return dispatchF<OMP, 4>(g, metric, H, o);
+    default: die("unsupported MAXFACTOR2");
+  }
   switch (H) {  // the MINDEGREE1 sweep of main.cxx:67-80, plus 1 and 3 for edge cases
     case 0:    return runMetric<0, OMP>(g, metric, o);
     case 1:    return runMetric<1, OMP>(g, metric, o);
@@ -147,9 +166,10 @@ static int doPredict(int argc, char** argv, bool write) {
   bool omp = write ? string(argv[6]) == "omp" : true;
   int threads = atoi(argv[write ? 7 : 6]);
   int repeat = atoi(argv[write ? 8 : 7]);
+  const int F = write && argc > 10 ? atoi(argv[10]) : 0;
   omp_set_num_threads(threads);
   PredictLinkOptions<float> o(repeat, maxEdges);
-  auto r = omp ? dispatch<true>(g, metric, H, o) : dispatch<false>(g, metric, H, o);
+  auto r = omp ? dispatch<true>(g, metric, H, o, F) : dispatch<false>(g, metric, H, o, F);
   printf("%.3f %.3f %zu\n", r.time, r.scoringTime, r.edges.size());
   if (write) {
     FILE* f = fopen(argv[9], "wb"); if (!f) die("cannot write out");

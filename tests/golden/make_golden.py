@@ -19,6 +19,12 @@ Per graph file <name>.npz:
                             (the OpenMP merge is UB there)
     topk_<m>_<H>_omp        1 if topk came from the OpenMP path (0 also when the OpenMP
                             run crashed on NaN scores, A.2/A.4)
+
+maxf2.npz (python tests/golden/make_golden.py maxf2): the MAXFACTOR2 template
+parameter (predict.hxx:221,295) on the g300 and edge graphs of the files above:
+    <graph>_cand_<F>_<m>_<H>_{u,w,s}   predictLinks<M><H, F>(y, {1, SIZE_MAX})
+    <graph>_topk_<F>_<m>_<H>_{u,w,s}   predictLinks<M>Omp<H, F>(y, {1, k}) (sequential
+                                       when the candidates < k, as above)
 """
 import os
 import subprocess
@@ -126,9 +132,41 @@ def run_graph(name, csr_path, off, keys, dels, tmp):
     print(name, "span", len(off) - 1, "nnz", len(keys), "k", k, flush=True)
 
 
+MAXF2_CASES = {"g300": ([1, 2, 4], [0, 4]), "edge": ([1, 2], [0, 4])}
+
+
+def make_maxf2():
+    """MAXFACTOR2 fixtures on the committed g300 / edge graphs (their CSR and k)."""
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, (fs, hs) in MAXF2_CASES.items():
+            g = dict(np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False))
+            csr = os.path.join(tmp, name + ".csr")
+            O.write_csr(csr, g["offsets"], g["keys"])
+            k = int(g["k"][0])
+            for F in fs:
+                for m in range(9):
+                    for H in hs:
+                        tag = "%s_%%s_%d_%d_%d" % (name, F, m, H)
+                        u, w, s_, _ = O.ref_predict(csr, m, H, -1, "seq", 1, 1, os.path.join(tmp, "p.bin"), F)
+                        out[tag % "cand" + "_u"], out[tag % "cand" + "_w"], out[tag % "cand" + "_s"] = u, w, s_
+                        omp = len(u) >= k and k > 0
+                        try:
+                            u, w, s_, _ = O.ref_predict(csr, m, H, k, "omp" if omp else "seq", 4, 1,
+                                                        os.path.join(tmp, "t.bin"), F)
+                        except subprocess.CalledProcessError:
+                            u, w, s_, _ = O.ref_predict(csr, m, H, k, "seq", 1, 1, os.path.join(tmp, "t.bin"), F)
+                        out[tag % "topk" + "_u"], out[tag % "topk" + "_w"], out[tag % "topk" + "_s"] = u, w, s_
+    np.savez_compressed(os.path.join(HERE, "maxf2.npz"), **out)
+    print("maxf2", len(out) // 6, "cases", flush=True)
+
+
 def main():
     if not os.path.exists(O.REF_DRIVER):
         sys.exit("build the reference driver first: make -C oracle")
+    if len(sys.argv) > 1 and sys.argv[1] == "maxf2":
+        make_maxf2()
+        return
     with tempfile.TemporaryDirectory() as tmp:
         for name, (n, m, alpha, seed, d, dseed) in {"g300": (300, 1200, 0.6, 1, 0.1, 42),
                                                    "g3k": (3000, 20000, 0.6, 7, 0.1, 42)}.items():

@@ -601,3 +601,119 @@ def test_gpu_msd_passes_on_source_ranges(gpu, oracle, passes):
                         bad.append((m, H, ub, ue, len(eu), int((eu != u).sum()) if len(eu) == len(u) else -1,
                                     str(e)[:40]))
             assert not bad, bad
+
+
+def _maxf2_cases(f):
+    out = []
+    for key in f:
+        if "_topk_" in key and key.endswith("_u"):
+            name, _, F, m, H, _ = key.split("_")
+            out.append((name, int(F), int(m), int(H)))
+    return sorted(out)
+
+
+def test_gpu_maxfactor2_matches_reference(gpu, golden, oracle):
+    """MAXFACTOR2 (predict.hxx:221,295) through nlp_predict_ex: all candidates
+    against the compiled reference (tests/golden/maxf2.npz), top-k against the
+    reference (contract) and the oracle (exact)."""
+    from conftest import load_golden
+    f = load_golden("maxf2")
+    graphs = {}
+    try:
+        for name, F, m, H in _maxf2_cases(f):
+            g = golden[name]
+            if name not in graphs:
+                graphs[name] = gpu.Graph(g["offsets"], g["keys"])
+            G = graphs[name]
+            k = int(g["k"][0])
+            tag = "%s_%%s_%d_%d_%d" % (name, F, m, H)
+            cu, cw, cs = f[tag % "cand" + "_u"], f[tag % "cand" + "_w"], f[tag % "cand" + "_s"]
+            u, w, s, t = G.predict(m, H, None, maxfactor2=F)
+            assert_same_candidates(cu, cw, cs, u, w, s)
+            u, w, s, t = G.predict(m, H, k, maxfactor2=F)
+            eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], m, H, max_edges=k, maxfactor2=F)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+            if not np.isnan(cs).any():
+                assert_topk_matches_reference(f[tag % "topk" + "_u"], f[tag % "topk" + "_w"],
+                                              f[tag % "topk" + "_s"], u, w, s, (cu, cw, cs))
+    finally:
+        for G in graphs.values():
+            G.close()
+
+
+@pytest.mark.parametrize("env", [dict(), dict(NLP_HASH="1"), dict(NLP_WEDGE_BUDGET="3000"),
+                                 dict(NLP_BUCKET_FUSED="1"), dict(NLP_GROUPING="lsd")])
+def test_gpu_maxfactor2_every_path_vs_oracle(gpu, oracle, env):
+    """The MAXFACTOR2 filter on every path (sort path, hash path, chunked
+    path 2, fused bucket, LSD grouping) against the oracle on a multigraph."""
+    off, keys = random_csr(6000, 12, 11)
+    with _env(**env):
+        with gpu.Graph(off, keys) as G:
+            for m in (0, 1, 3, 7):
+                for H in (0, 4, 16):
+                    for F in (1, 3):
+                        u, w, s, t = G.predict(m, H, 2000, maxfactor2=F)
+                        eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=2000, maxfactor2=F)
+                        assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_count_query_and_copy_last(gpu, golden, oracle):
+    """nlp.h count query: out = NULL predicts and keeps the result on the
+    device (*out_count = its size), nlp_copy_last fetches it; max_edges = 0
+    predicts nothing (the reference's o.maxEdges > 0 guard)."""
+    import ctypes
+    g = golden["g3k"]
+    L = gpu.lib()
+    with gpu.Graph(g["offsets"], g["keys"]) as G:
+        for m, H in ((1, 4), (7, 8), (0, 0)):
+            eu, ew, es, info = oracle.predict(g["offsets"], g["keys"], m, H)
+            cnt, t = ctypes.c_uint64(), gpu.Timing()
+            assert L.nlp_predict(G._h, m, H, 0.0, gpu.UINT64_MAX, 1, None, ctypes.byref(cnt), ctypes.byref(t)) == 0
+            assert cnt.value == len(eu) == t.candidates
+            out = np.zeros(cnt.value + 5, dtype=gpu.EDGE_DTYPE)
+            got = ctypes.c_uint64()
+            assert L.nlp_copy_last(G._h, out.ctypes.data, cnt.value + 5, ctypes.byref(got)) == 0
+            assert got.value == cnt.value
+            assert_canonical_equal(eu, ew, es, out["u"][:got.value], out["v"][:got.value], out["score"][:got.value])
+            # a shorter copy takes the first n links
+            assert L.nlp_copy_last(G._h, out.ctypes.data, 7, ctypes.byref(got)) == 0 and got.value == min(7, len(eu))
+            t0 = gpu.Timing()
+            assert L.nlp_predict(G._h, m, H, 0.0, 0, 1, None, ctypes.byref(cnt), ctypes.byref(t0)) == 0
+            assert cnt.value == 0 and t0.candidates == 0
+            assert L.nlp_copy_last(G._h, out.ctypes.data, 10, ctypes.byref(got)) == 0 and got.value == 0
+
+
+def test_gpu_exclusion_without_edge_table(gpu, oracle):
+    """First-order exclusion by the edge filter + list search (NLP_ETAB=0, the
+    path taken when the membership table does not fit) equals the table path
+    and the oracle."""
+    off, keys = random_csr(8000, 14, 5)
+    k = 3000
+    with gpu.Graph(off, keys) as Gt:
+        res = {(m, H): Gt.predict(m, H, k) for m in (0, 1, 3, 7, 8) for H in (0, 2, 4, 16)}
+    with _env(NLP_ETAB="0"):
+        with gpu.Graph(off, keys) as G:
+            for (m, H), (u, w, s, t) in res.items():
+                u2, w2, s2, t2 = G.predict(m, H, k)
+                assert_canonical_equal(u, w, s, u2, w2, s2)
+                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                assert_canonical_equal(eu, ew, es, u2, w2, s2)
+
+
+@pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"),
+                                 dict(NLP_MSD_PASSES="2")])
+def test_gpu_sort_path_variants_equal(gpu, oracle, env):
+    """Sort-path build variants (separate output gather, several survivors per
+    expansion thread, two MSD passes + group sort) give the default's results."""
+    off, keys = random_csr(9000, 14, 21)
+    k = 2500
+    with gpu.Graph(off, keys) as G:
+        res = {(m, H): G.predict(m, H, k) for m in (0, 1, 7) for H in (1, 2, 4, 8)}
+    with _env(**env):
+        with gpu.Graph(off, keys) as G:
+            for (m, H), (u, w, s, t) in res.items():
+                u2, w2, s2, t2 = G.predict(m, H, k)
+                assert_canonical_equal(u, w, s, u2, w2, s2)
+                assert t["candidates"] == t2["candidates"]
+    eu, ew, es, _ = oracle.predict(off, keys, 1, 4, max_edges=k)
+    assert_canonical_equal(eu, ew, es, *res[(1, 4)][:3])

@@ -21,3 +21,8 @@ for i, j in zip(ok, ok[1:]):
     d = (blocks[:, j] - blocks[:, i]) / 100.0
     print("phase %d->%d: mean %.2f us  p50 %.2f  max %.2f" % (i, j, d.mean(), np.median(d), d.max()))
 print("span %.2f us" % ((blocks[:, ok[-1]].max() - t0) / 100))
+if nph > 7 and 7 in ok and 0 in ok:
+    d = (blocks[:, 0] - blocks[:, 7]) / 100.0
+    e0 = blocks[:, 7].min()
+    print("entry (phase 7) -> phase 0: mean %.2f us max %.2f; entry spread %.2f us; entry -> last end %.2f us"
+          % (d.mean(), d.max(), (blocks[:, 7].max() - e0) / 100, (blocks[:, ok[-2] if ok[-1] == 7 else ok[-1]].max() - e0) / 100))
