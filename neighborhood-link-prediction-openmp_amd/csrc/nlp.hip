@@ -158,6 +158,7 @@ struct nlp_graph {
   std::string stamp_path;
   int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
+  bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
                                                // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
@@ -500,6 +501,7 @@ nlp_status finish_graph(nlp_graph* g) {
     if (v > 0) g->wedge_budget = v;
   }
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
+  if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
   if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
   if (const char* xi = getenv("NLP_EX_IPT")) g->ex_ipt = atoi(xi) >= 4 ? 4 : (atoi(xi) >= 2 ? 2 : 1);
   if (const char* gs = getenv("NLP_GRAPH_SEGMENTS")) g->graph_single = gs[0] != '1';
@@ -559,7 +561,7 @@ nlp_status new_graph(int device, nlp_graph** out) {
   g->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(&g->host_small, 64 * 8) != hipSuccess ||
-      hipHostMalloc(&g->host_ctr, NCTR * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc(&g->host_ctr, (NCTR + TS_WORDS) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&g->host_ctr_dev, g->host_ctr, 0) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_DEVICE;
@@ -1644,6 +1646,9 @@ struct SpBufs {
   uint64_t arena_words;
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
   uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
+  uint64_t d_bcur;                              // 256 u32 bucket cursors (direct emission)
+  uint64_t d_ts;                                // TS_WORDS u64 call-timing stamps (sortpath.hpp ts_enter)
+  bool direct;    // count metrics, one MSD pass: k_sp_excount + k_sp_exemit instead of k_sp_expand + MSD pass
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
@@ -1721,6 +1726,8 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.split = msd && g->split_bucket;
   f.msd_passes = f.split ? std::min(msd_passes, std::max(1, (f.wbits + ubits) / 8)) : 1;
   f.msd_shift = std::max(0, f.wbits + ubits - 8 * f.msd_passes);
+  f.direct = g->direct_emit && f.split && f.msd_passes == 1 && g->group_sort != 1 && p.metric != M_AA &&
+             p.metric != M_RA;
   // The count metrics do not depend on the order of a run's wedges, so their
   // survivors can come from the degree-class index in any order; Adamic-Adar and
   // Resource-Allocation sum in ascending v and keep the ordered survivor scan.
@@ -1739,7 +1746,9 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
   f.d_tick = SP_DESC;
-  f.d_surv = f.d_tick + SP_NTICK / 2;
+  f.d_bcur = f.d_tick + SP_NTICK / 2;
+  f.d_ts = f.d_bcur + RS_BINS / 2;
+  f.d_surv = f.d_ts + TS_WORDS;
   f.d_exp = f.d_surv + tS + 1;
   f.d_run = f.d_exp + tE + 1;
   f.d_rec = f.d_run + tR + 1;
@@ -1779,6 +1788,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
   uint32_t* tick = (uint32_t*)(f.arena + f.d_tick);
+  uint64_t* ts = f.arena + f.d_ts;
   const int P = f.msd ? f.msd_passes : f.passes;
   const int s_runs = 4 + P + (f.split ? 1 : 0), n_st = s_runs + 7;
   // after the record passes the records sit in buffer 1 for an odd count, 0 for even
@@ -1804,31 +1814,46 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       if (f.dindex) return NLP_OK;
       hipLaunchKernelGGL(k_sp_survivors, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
                          (const uint32_t*)g->deg, S, p.H, f.surv, f.arena + f.d_surv, tick + TK_SURV, ctr,
-                         hot == 1 ? g->d_stamp : nullptr);
+                         hot == 1 ? g->d_stamp : nullptr, ts);
     } else if (s == 2) {
       // survivors: known exactly with the degree-class index, else at most S
       const uint64_t nsv = f.dindex ? f.nv : S;
+      if (f.direct) {
+        hipLaunchKernelGGL(k_sp_excount, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
+                           gv, ua, ub, f.wbits, f.survivors, ctr, f.msd_shift, hrec, ts);
+        TRY(hipGetLastError());
+        return NLP_OK;
+      }
       const int xi = g->ex_ipt;
       const dim3 gx = grid((nsv + (uint64_t)NT * xi - 1) / ((uint64_t)NT * xi), g->occ_exp);
 #define NLP_EXPAND(IPT)                                                                                          \
   do {                                                                                                           \
     if (f.msd) /* the MSD digit histogram is fused into the expansion */                                         \
       hipLaunchKernelGGL((k_sp_expand<true, IPT>), gx, dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, capW,  \
-                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, f.msd_shift, hrec, P);             \
+                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, f.msd_shift, hrec, P, ts);         \
     else                                                                                                         \
       hipLaunchKernelGGL((k_sp_expand<false, IPT>), gx, dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, capW, \
-                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, 0, (uint32_t*)nullptr, 1);         \
+                         f.rk0, f.rv0, f.arena + f.d_exp, tick + TK_EXP, ctr, 0, (uint32_t*)nullptr, 1, ts);     \
   } while (0)
       if (xi == 4) NLP_EXPAND(4);
       else if (xi == 2) NLP_EXPAND(2);
       else NLP_EXPAND(1);
 #undef NLP_EXPAND
     } else if (s == 3) {
+      if (f.direct) {  // records straight into their MSD buckets (the buffers the bucket sort reads)
+        const uint64_t nsv = f.dindex ? f.nv : S;
+        hipLaunchKernelGGL(k_sp_exemit, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
+                           gv, ua, ub, f.wbits, f.survivors, capW, rk_m, rv_m, ctr, f.msd_shift,
+                           (const uint32_t*)hrec, (uint32_t*)(f.arena + f.d_bcur));
+        TRY(hipGetLastError());
+        return NLP_OK;
+      }
       if (f.msd) return NLP_OK;
       hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(128), dim3(NT), 0, st, (const uint64_t*)f.rk0,
                          (const uint64_t*)&ctr[C_W], capW, f.msd ? f.msd_shift : 0, P, hrec, &ctr[C_WSORT],
                          &ctr[C_FLAGS]);
     } else if (s < 4 + P) {
+      if (f.direct) return NLP_OK;  // the records are already in their buckets
       const int ps = s - 4;
       const bool odd = ps & 1;
       hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), grid(tO, g->occ_p64), dim3(OS_NT), 0, st,
@@ -1863,11 +1888,11 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       if (custom)
         hipLaunchKernelGGL(k_sp_runs<true>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
                            (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)f.stash, f.cu, f.cw,
-                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr);
+                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr, ts);
       else
         hipLaunchKernelGGL(k_sp_runs<false>, gr, dim3(NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,
                            (const uint64_t*)rk_m, (const uint32_t*)rv_free, (const uint32_t*)nullptr, f.cu, f.cw,
-                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr);
+                           f.cs, f.ok0, f.ov0, f.segcnt, ctr, hord, hot == s ? g->d_stamp : nullptr, ts);
     } else if (s == s_runs && f.msd) {
       if (custom)
         hipLaunchKernelGGL(k_sp_bucket<true>, dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
@@ -1916,7 +1941,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)f.ok1, (const uint32_t*)f.ov1, f.ok0, f.ov0, (const uint64_t*)&ctr[C_C], 24,
                            (const uint32_t*)(hord + 3 * RS_BINS), dord + 3 * f.ostride, tick + TK_ORD + 3, err,
                            (uint64_t*)nullptr,
-                           GatherOut{f.cu, f.cw, f.cs, p.max_edges, out, ctr, g->host_ctr_dev}, (uint32_t*)nullptr);
+                           GatherOut{f.cu, f.cw, f.cs, p.max_edges, out, ctr, g->host_ctr_dev, ts}, (uint32_t*)nullptr);
       else
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
@@ -1928,7 +1953,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
                          dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
-                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev);
+                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev, (const uint64_t*)ts);
     }
     TRY(hipGetLastError());
     return NLP_OK;
@@ -1963,9 +1988,11 @@ static const int EV_SEG4[4] = {0, 3, 4, 1};  // bucket grouping: pre | hot | res
 static const int EV_SEG3[3] = {0, 3, 4};     // sort grouping: pre | hot (scoring) | selection
 
 // copy_src: the device counters the pipeline copies to host_small at its end.
+// stamps: the hot kernel times itself (sortpath.hpp ts_enter): no event-record
+// nodes between the segments of the single graph, only at its start and end.
 template <class L>
 nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, int mode, const void* copy_src,
-                     bool* replayed, L&& launch) {
+                     bool* replayed, L&& launch, bool stamps = false) {
   *replayed = false;
   if (!g->use_graphs) return NLP_OK;
   const bool single = g->graph_single && mode != 0;  // the bucket grouping is captured in segments
@@ -2040,7 +2067,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
         }
       };
       for (int seg = 0; seg < nseg && ok1; ++seg) {
-        chain_ev(ev_before[seg]);
+        if (!stamps || seg == 0) chain_ev(ev_before[seg]);
         append(seg_graph[seg]);
       }
       if (ok1 && saw_copy) {
@@ -2156,9 +2183,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     bool replayed = false;
     g->last_single = false;
     if (hprof) t1 = now_us();
+    const bool stamps = sorted && sp.split && g->hot_stage < 0;
     if (sorted)
       s = run_graph(g, p, out, st, msd ? 1 + sp.msd_passes : 1, sp.arena, &replayed,
-                    [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); });
+                    [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps);
     else
       s = run_graph(g, p, out, st, 0, f.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
@@ -2274,10 +2302,21 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (result) *result = out;
     if (t) {
       float a = 0, b = 0, hot = 0;
-      const hipEvent_t split = sorted ? E[4] : E[1];  // sort grouping: event 4 ends the scoring kernel
-      TRY(hipEventElapsedTime(&a, E[0], split));
-      TRY(hipEventElapsedTime(&b, split, E[2]));
-      TRY(hipEventElapsedTime(&hot, E[3], E[4]));
+      if (stamps && replayed && g->last_single) {
+        // events at the call's ends; the hot kernel's own stamps (10 ns ticks)
+        float tot = 0;
+        TRY(hipEventElapsedTime(&tot, E[0], E[2]));
+        const uint64_t* ts = h + NCTR;
+        hot = ts[TS_HOT_OUT] > ~ts[TS_HOT_IN] ? (float)((ts[TS_HOT_OUT] - ~ts[TS_HOT_IN]) * 1e-5) : 0.0f;
+        a = ts[TS_HOT_OUT] > ~ts[TS_FIRST] ? (float)((ts[TS_HOT_OUT] - ~ts[TS_FIRST]) * 1e-5) : 0.0f;
+        a = std::min(a, tot);
+        b = tot - a;
+      } else {
+        const hipEvent_t split = sorted ? E[4] : E[1];  // sort grouping: event 4 ends the scoring kernel
+        TRY(hipEventElapsedTime(&a, E[0], split));
+        TRY(hipEventElapsedTime(&b, split, E[2]));
+        TRY(hipEventElapsedTime(&hot, E[3], E[4]));
+      }
       const uint64_t nU = std::min(p.ub, g->span) - std::min(p.ua, g->span);
       t->score_ms = a;
       t->select_ms = b;

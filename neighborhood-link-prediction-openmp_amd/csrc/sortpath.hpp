@@ -124,6 +124,21 @@ __device__ __forceinline__ uint64_t lb_lookback_r(uint64_t* desc, uint64_t tile,
   return excl;
 }
 
+// Call timing without event nodes (an event-record node costs ~4.6 us of GPU
+// time inside a replayed graph): ts[0] = ~(earliest workgroup entry of the
+// call's first kernel), ts[1] = ~(earliest entry of the hot kernel), ts[2] =
+// latest exit of the hot kernel; s_memrealtime ticks (100 MHz).  Minima are
+// kept as maxima of the complement so that a zeroed arena is the identity.
+enum { TS_FIRST = 0, TS_HOT_IN = 1, TS_HOT_OUT = 2, TS_WORDS = 4 };
+__device__ __forceinline__ void ts_enter(uint64_t* ts, int slot) {
+  if (ts && threadIdx.x == 0)
+    atomicMax((unsigned long long*)&ts[slot], (unsigned long long)~__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void ts_exit(uint64_t* ts, int slot) {
+  if (ts && threadIdx.x == 0)
+    atomicMax((unsigned long long*)&ts[slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 // Optional phase stamps for tools/ubench (nullptr in the product): workgroup b
 // writes s_memrealtime (100 MHz) of phase i of its first tile to stamp[8 b + i].
 __device__ __forceinline__ void sp_stamp(uint64_t* stamp, bool first, int i) {
@@ -153,7 +168,8 @@ __device__ __forceinline__ void tk_draw(uint32_t* tick, uint32_t* slot) {
 __global__ __launch_bounds__(NT) void k_sp_survivors(const uint32_t* __restrict__ deg, uint64_t S, uint32_t H,
                                                      uint32_t* __restrict__ surv, uint64_t* __restrict__ desc,
                                                      uint32_t* __restrict__ tick, uint64_t* __restrict__ ctr,
-                                                     uint64_t* __restrict__ stamp) {
+                                                     uint64_t* __restrict__ stamp, uint64_t* __restrict__ ts) {
+  ts_enter(ts, TS_FIRST);
   constexpr int NB = SV_STEPS / 8;  // u32 flag words per lane (8 steps x 4 vertices each)
   __shared__ uint64_t s_w[NWAVE];
   __shared__ uint64_t s_excl;
@@ -357,52 +373,78 @@ __device__ __forceinline__ void ex_load(const GraphView& g, uint32_t v, ExSurv& 
   }
 }
 
-// wedges of survivor x (w > u, u in [ua, ub)); EMIT: write them from `pos`
-template <bool EMIT, bool HIST>
-__device__ __forceinline__ uint64_t ex_walk(const GraphView& g, const ExSurv& x, uint64_t ua, uint64_t ub, int wbits,
-                                            uint64_t pos, uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
-                                            uint32_t* s_h, int hshift, int hdigits) {
-  uint64_t c = 0;
-  auto put = [&](uint32_t u, uint32_t w) {
-    if (EMIT) {
-      const uint64_t key = ((uint64_t)(u - ua) << wbits) | w;
-      rkey[pos + c] = key;
-      rval[pos + c] = x.v;
-      if (HIST) {
-        atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
-        if (hdigits > 1) atomicAdd(&s_h[RS_BINS + ((uint32_t)(key >> (hshift + 8)) & 0xffu)], 1u);
-      }
-    }
-    ++c;
-  };
+// Every wedge (u, v = x.v, w) of survivor x with u in [ua, ub) and w > u, in
+// the order (u ascending over I(v), w ascending over N(v)): put(u, w).
+template <class Put>
+__device__ __forceinline__ void ex_enum(const GraphView& g, const ExSurv& x, uint64_t ua, uint64_t ub, Put&& put) {
   if (x.reg) {
 #pragma unroll
     for (int p = 0; p < EX_REG; ++p) {
       const uint32_t u = x.I[p];
       if (p < (int)x.nin && u >= ua && u < ub) {
-        if (EMIT) {
 #pragma unroll
-          for (int q = 0; q < EX_REG; ++q)
-            if (q < (int)x.d && x.N[q] > u) put(u, x.N[q]);
-        } else {
-#pragma unroll
-          for (int q = 0; q < EX_REG; ++q) c += (q < (int)x.d && x.N[q] > u) ? 1u : 0u;
-        }
+        for (int q = 0; q < EX_REG; ++q)
+          if (q < (int)x.d && x.N[q] > u) put(u, x.N[q]);
       }
     }
   } else {
     for (uint32_t p = 0; p < x.nin; ++p) {
       const uint32_t u = g.tkeys[x.a + p];
       if (u < ua || u >= ub) continue;
-      const uint32_t k0 = upper_bound_u32(x.nv, x.d, u);
-      if (EMIT) {
-        for (uint32_t k = k0; k < x.d; ++k) put(u, x.nv[k]);
-      } else {
-        c += x.d - k0;
+      for (uint32_t k = upper_bound_u32(x.nv, x.d, u); k < x.d; ++k) put(u, x.nv[k]);
+    }
+  }
+}
+
+// Number of wedges of survivor x (same set as ex_enum).
+__device__ __forceinline__ uint64_t ex_count(const GraphView& g, const ExSurv& x, uint64_t ua, uint64_t ub) {
+  uint64_t c = 0;
+  if (x.reg) {
+#pragma unroll
+    for (int p = 0; p < EX_REG; ++p) {
+      const uint32_t u = x.I[p];
+      if (p < (int)x.nin && u >= ua && u < ub) {
+#pragma unroll
+        for (int q = 0; q < EX_REG; ++q) c += (q < (int)x.d && x.N[q] > u) ? 1u : 0u;
       }
+    }
+  } else {
+    for (uint32_t p = 0; p < x.nin; ++p) {
+      const uint32_t u = g.tkeys[x.a + p];
+      if (u >= ua && u < ub) c += x.d - upper_bound_u32(x.nv, x.d, u);
     }
   }
   return c;
+}
+
+__device__ __forceinline__ uint64_t ex_key(uint32_t u, uint32_t w, uint64_t ua, int wbits) {
+  return ((uint64_t)(u - ua) << wbits) | w;
+}
+
+__device__ __forceinline__ void ex_empty(const GraphView& g, ExSurv& x) {
+  x.nin = 0;
+  x.d = 0;
+  x.reg = true;
+  x.v = 0;
+  x.a = 0;
+  x.nv = g.keys;
+}
+
+// wedges of survivor x written from `pos` (HIST: MSD digit histogram in LDS)
+template <bool HIST>
+__device__ __forceinline__ void ex_write(const GraphView& g, const ExSurv& x, uint64_t ua, uint64_t ub, int wbits,
+                                         uint64_t pos, uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
+                                         uint32_t* s_h, int hshift, int hdigits) {
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    const uint64_t key = ex_key(u, w, ua, wbits);
+    rkey[pos] = key;
+    rval[pos] = x.v;
+    if (HIST) {
+      atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+      if (hdigits > 1) atomicAdd(&s_h[RS_BINS + ((uint32_t)(key >> (hshift + 8)) & 0xffu)], 1u);
+    }
+    ++pos;
+  });
 }
 
 template <bool HIST, int IPT = EX_IPT>
@@ -411,7 +453,8 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
                                                   uint64_t* __restrict__ desc, uint32_t* __restrict__ tick,
                                                   uint64_t* __restrict__ ctr, int hshift, uint32_t* __restrict__ ghist,
-                                                  int hdigits = 1) {
+                                                  int hdigits, uint64_t* __restrict__ ts) {
+  ts_enter(ts, TS_FIRST);
   __shared__ uint64_t s_red[NWAVE + 1];
   __shared__ uint64_t s_excl;
   __shared__ uint32_t s_h[HIST ? 2 * RS_BINS : 1];
@@ -435,20 +478,12 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
     uint64_t c[IPT], sum = 0;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-      if (i0 + j < n) {
-        ex_load(g, surv[i0 + j], x[j]);
-      } else {
-        x[j].nin = 0;
-        x[j].d = 0;
-        x[j].reg = true;
-        x[j].v = 0;
-        x[j].a = 0;
-        x[j].nv = g.keys;
-      }
+      if (i0 + j < n) ex_load(g, surv[i0 + j], x[j]);
+      else ex_empty(g, x[j]);
     }
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-      c[j] = ex_walk<false, false>(g, x[j], ua, ub, wbits, 0, rkey, rval, s_h, hshift, hdigits);
+      c[j] = ex_count(g, x[j], ua, ub);
       sum += c[j];
     }
     uint64_t agg;
@@ -473,7 +508,7 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
     if (sum && pos + sum <= capW) {
 #pragma unroll
       for (int j = 0; j < IPT; ++j) {
-        if (c[j]) ex_walk<true, HIST>(g, x[j], ua, ub, wbits, pos, rkey, rval, s_h, hshift, hdigits);
+        if (c[j]) ex_write<HIST>(g, x[j], ua, ub, wbits, pos, rkey, rval, s_h, hshift, hdigits);
         pos += c[j];
       }
     }
@@ -486,6 +521,91 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
       if (c) atomicAdd(&hc[dd * RS_BINS + threadIdx.x], c);
     }
   }
+}
+
+// ---------------------------------------------------------------- direct bucket emission
+// The count metrics do not depend on the order of the wedges inside a (u, w)
+// run, so their records can go straight to their MSD bucket (key digit at
+// hshift) in any order: k_sp_excount counts the records per bucket (histogram
+// copies) and in total (ctr[C_W]); k_sp_exemit reserves one slot range per
+// (workgroup, bucket) with a global cursor and writes the records there.  No
+// look-back and no MSD pass; k_sp_bucket then sorts every bucket by key.  One
+// survivor per thread, no hand-off between workgroups.
+__global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uint64_t ub, int wbits,
+                                                   const uint32_t* __restrict__ surv, uint64_t* __restrict__ ctr,
+                                                   int hshift, uint32_t* __restrict__ ghist, uint64_t* __restrict__ ts) {
+  ts_enter(ts, TS_FIRST);
+  __shared__ uint32_t s_h[RS_BINS];
+  __shared__ uint64_t s_wt[NWAVE];
+  const int t = threadIdx.x;
+  const uint64_t n = ctr[C_NV];
+  if ((uint64_t)blockIdx.x * NT >= n) return;
+  s_h[t] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * NT + t;
+  ExSurv x;
+  if (i < n) ex_load(g, surv[i], x);
+  else ex_empty(g, x);
+  uint64_t c = 0;
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & 0xffu], 1u);
+    ++c;
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane_id() == 0) s_wt[wave_id()] = c;
+  __syncthreads();
+  const uint32_t h = s_h[t];
+  if (h) atomicAdd(&hist_copy(ghist)[t], h);
+  if (t == 0) {
+    uint64_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) tot += s_wt[w];
+    if (tot) atomicAdd((unsigned long long*)&ctr[C_W], (unsigned long long)tot);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_sp_exemit(GraphView g, uint64_t ua, uint64_t ub, int wbits,
+                                                  const uint32_t* __restrict__ surv, uint64_t capW,
+                                                  uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
+                                                  uint64_t* __restrict__ ctr, int hshift,
+                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bcur) {
+  __shared__ uint32_t s_h[RS_BINS];  // records per bucket, then the next free slot per bucket
+  __shared__ uint32_t s_start[RS_BINS];
+  __shared__ uint64_t s_red[NWAVE + 1];
+  const int t = threadIdx.x;
+  const uint64_t n = ctr[C_NV];
+  if ((uint64_t)blockIdx.x * NT >= n) return;
+  const uint64_t W = ctr[C_W];
+  const bool fits = W <= capW;
+  if (blockIdx.x == 0 && t == 0) {
+    ctr[C_WSORT] = fits ? W : 0;
+    if (!fits) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_OVERFLOW);
+  }
+  if (!fits) return;
+  uint64_t tot;
+  s_start[t] = (uint32_t)block_excl_scan(hist_total(ghist, t), s_red, &tot);  // bucket starts (syncs)
+  s_h[t] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * NT + t;
+  ExSurv x;
+  if (i < n) ex_load(g, surv[i], x);
+  else ex_empty(g, x);
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & 0xffu], 1u);
+  });
+  __syncthreads();
+  const uint32_t c = s_h[t];
+  const uint32_t base = c ? atomicAdd(&bcur[t], c) : 0u;
+  __syncthreads();
+  s_h[t] = s_start[t] + base;
+  __syncthreads();
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    const uint64_t key = ex_key(u, w, ua, wbits);
+    const uint32_t pos = atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+    rkey[pos] = key;
+    rval[pos] = x.v;
+  });
 }
 
 // ---------------------------------------------------------------- onesweep radix sort
@@ -600,6 +720,7 @@ struct GatherOut {
   EdgeOut* out;
   uint64_t* ctr;   // the call's counters: C_OUT_N is set, all are published to hctr
   uint64_t* hctr;  // host-mapped copy of the counters (read after the call's final event)
+  const uint64_t* ts;  // the call's timing stamps, published to hctr[NCTR ..]
 };
 
 // Exclusive scan of one value per digit (threads 0-255, 0 elsewhere) over the
@@ -655,6 +776,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       // host-coherent memory; the call's final event (a system-scope release)
       // orders these stores before the host reads them
       if (go.hctr) go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
+      if (go.hctr && go.ts && t < TS_WORDS) go.hctr[NCTR + t] = go.ts[t];
     }
   };
   if (GATHER && ntiles == 0 && blockIdx.x == 0) publish();
@@ -1327,12 +1449,14 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
                                                 uint32_t* __restrict__ cw, float* __restrict__ cs,
                                                 uint32_t* __restrict__ okey, uint32_t* __restrict__ oval,
                                                 uint32_t* __restrict__ seg_cnt, uint64_t* __restrict__ ctr,
-                                                uint32_t* __restrict__ ohist, uint64_t* __restrict__ stamp) {
+                                                uint32_t* __restrict__ ohist, uint64_t* __restrict__ stamp,
+                                                uint64_t* __restrict__ ts) {
   __shared__ uint32_t s_oh[RS_BINS];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t n = ctr[C_WSORT];
   const uint64_t tile = blockIdx.x;
   if (tile * RU_TILE >= n) return;
+  ts_enter(ts, TS_HOT_IN);
   s_oh[t] = 0;
   __syncthreads();
   sp_stamp(stamp, true, 0);
@@ -1461,6 +1585,7 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
   sp_stamp(stamp, true, 2);
   const uint32_t hc = s_oh[t];
   if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
+  ts_exit(ts, TS_HOT_OUT);
 }
 
 // ---------------------------------------------------------------- generic single-pass scan
@@ -1583,11 +1708,13 @@ struct F_Runs {
 __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ cu,
                                                   const uint32_t* __restrict__ cw, const float* __restrict__ cs,
                                                   uint64_t k, EdgeOut* __restrict__ out,
-                                                  uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr) {
+                                                  uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr,
+                                                  const uint64_t* __restrict__ ts) {
   const uint64_t m = std::min<uint64_t>(ctr[C_C], k);
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) ctr[C_OUT_N] = m;
     if (hctr && threadIdx.x < NCTR) hctr[threadIdx.x] = threadIdx.x == C_OUT_N ? m : ctr[threadIdx.x];
+    if (hctr && ts && threadIdx.x >= NCTR && threadIdx.x < NCTR + TS_WORDS) hctr[threadIdx.x] = ts[threadIdx.x - NCTR];
     if (hctr) __threadfence_system();
   }
   for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (uint64_t)gridDim.x * NT) {

@@ -700,7 +700,7 @@ def test_gpu_exclusion_without_edge_table(gpu, oracle):
                 assert_canonical_equal(eu, ew, es, u2, w2, s2)
 
 
-@pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"),
+@pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"), dict(NLP_DIRECT="0"),
                                  dict(NLP_MSD_PASSES="2")])
 def test_gpu_sort_path_variants_equal(gpu, oracle, env):
     """Sort-path build variants (separate output gather, several survivors per
