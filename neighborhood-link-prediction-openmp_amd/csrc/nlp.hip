@@ -159,6 +159,8 @@ struct nlp_graph {
   int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
+  double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
+  int dx_bits = 0;                             // direct buckets: forced width (NLP_DX_BITS, 0 = from dx_target)
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
                                                // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
@@ -502,6 +504,8 @@ nlp_status finish_graph(nlp_graph* g) {
   }
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
+  if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
+  if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
   if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
   if (const char* xi = getenv("NLP_EX_IPT")) g->ex_ipt = atoi(xi) >= 4 ? 4 : (atoi(xi) >= 2 ? 2 : 1);
   if (const char* gs = getenv("NLP_GRAPH_SEGMENTS")) g->graph_single = gs[0] != '1';
@@ -1646,9 +1650,11 @@ struct SpBufs {
   uint64_t arena_words;
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
   uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
-  uint64_t d_bcur;                              // 256 u32 bucket cursors (direct emission)
+  uint64_t d_bcur;                              // DX_MAXB u32 bucket cursors (direct emission)
   uint64_t d_ts;                                // TS_WORDS u64 call-timing stamps (sortpath.hpp ts_enter)
-  bool direct;    // count metrics, one MSD pass: k_sp_excount + k_sp_exemit instead of k_sp_expand + MSD pass
+  bool direct;    // count metrics, one MSD pass: k_sp_excount + k_sp_exemit + k_sp_group instead of
+                  // k_sp_expand + MSD pass + k_sp_bucket
+  int dbits, dshift;  // direct buckets: the key's top dbits bits (key >> dshift)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
@@ -1728,6 +1734,14 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.msd_shift = std::max(0, f.wbits + ubits - 8 * f.msd_passes);
   f.direct = g->direct_emit && f.split && f.msd_passes == 1 && g->group_sort != 1 && p.metric != M_AA &&
              p.metric != M_RA;
+  {  // direct buckets of ~256 records on average (8 to 12 bits)
+    const double est = std::max(1.0, hp_estimate(g, p));
+    int db = 8;
+    while (db < DX_MAXBITS && est / (double)(1u << db) > g->dx_target) ++db;
+    if (g->dx_bits) db = std::min(g->dx_bits, DX_MAXBITS);
+    f.dbits = std::min(db, std::max(1, f.wbits + ubits));
+    f.dshift = std::max(0, f.wbits + ubits - f.dbits);
+  }
   // The count metrics do not depend on the order of a run's wedges, so their
   // survivors can come from the degree-class index in any order; Adamic-Adar and
   // Resource-Allocation sum in ascending v and keep the ordered survivor scan.
@@ -1747,7 +1761,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.ostride = tO * RS_BINS;
   f.d_tick = SP_DESC;
   f.d_bcur = f.d_tick + SP_NTICK / 2;
-  f.d_ts = f.d_bcur + RS_BINS / 2;
+  f.d_ts = f.d_bcur + DX_MAXB / 2;
   f.d_surv = f.d_ts + TS_WORDS;
   f.d_exp = f.d_surv + tS + 1;
   f.d_run = f.d_exp + tE + 1;
@@ -1820,7 +1834,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       const uint64_t nsv = f.dindex ? f.nv : S;
       if (f.direct) {
         hipLaunchKernelGGL(k_sp_excount, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
-                           gv, ua, ub, f.wbits, f.survivors, ctr, f.msd_shift, hrec, ts);
+                           gv, ua, ub, f.wbits, f.survivors, ctr, f.dshift, f.dbits, hrec, ts);
         TRY(hipGetLastError());
         return NLP_OK;
       }
@@ -1843,7 +1857,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       if (f.direct) {  // records straight into their MSD buckets (the buffers the bucket sort reads)
         const uint64_t nsv = f.dindex ? f.nv : S;
         hipLaunchKernelGGL(k_sp_exemit, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
-                           gv, ua, ub, f.wbits, f.survivors, capW, rk_m, rv_m, ctr, f.msd_shift,
+                           gv, ua, ub, f.wbits, f.survivors, capW, rk_m, rv_m, ctr, f.dshift, f.dbits,
                            (const uint32_t*)hrec, (uint32_t*)(f.arena + f.d_bcur));
         TRY(hipGetLastError());
         return NLP_OK;
@@ -1862,7 +1876,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                          f.msd ? f.msd_shift + 8 * ps : 8 * ps,
                          (const uint32_t*)(hrec + ps * RS_BINS), drec + (uint64_t)ps * f.ostride, tick + TK_REC + ps,
                          err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
-    } else if (f.split && s == s_runs - 1 && P == 1 && g->group_sort != 1) {
+    } else if (f.split && s == s_runs - 1 && P == 1 && g->group_sort != 1 && !f.direct) {
       // one MSD pass: one workgroup per top-digit bucket, the bucket bounds from its histogram
       if (custom)
         hipLaunchKernelGGL((k_sp_bucket<true, true>), dim3(RS_BINS), dim3(BK_NT), 0, st, gv, p.metric, p.min_score, ua,
@@ -1879,9 +1893,10 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       if (custom)
         hipLaunchKernelGGL(k_sp_group<true>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
                            f.msd_shift, rk_m, rv_free, (uint32_t*)f.stash, ctr, hot == s ? g->d_stamp : nullptr);
-      else
+      else  // after direct emission the fine buckets are the dbits-bit buckets
         hipLaunchKernelGGL(k_sp_group<false>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
-                           f.msd_shift, rk_m, rv_free, (uint32_t*)nullptr, ctr, hot == s ? g->d_stamp : nullptr);
+                           f.direct ? f.dshift : f.msd_shift, rk_m, rv_free, (uint32_t*)nullptr, ctr,
+                           hot == s ? g->d_stamp : nullptr);
     } else if (f.split && s == s_runs) {
       // one workgroup per RU_TILE records, no hand-off (gapped output)
       const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + RU_TILE - 1) / RU_TILE));

@@ -525,22 +525,29 @@ __global__ __launch_bounds__(NT) void k_sp_expand(GraphView g, uint64_t ua, uint
 
 // ---------------------------------------------------------------- direct bucket emission
 // The count metrics do not depend on the order of the wedges inside a (u, w)
-// run, so their records can go straight to their MSD bucket (key digit at
-// hshift) in any order: k_sp_excount counts the records per bucket (histogram
-// copies) and in total (ctr[C_W]); k_sp_exemit reserves one slot range per
-// (workgroup, bucket) with a global cursor and writes the records there.  No
-// look-back and no MSD pass; k_sp_bucket then sorts every bucket by key.  One
+// run, so their records can go straight to their bucket (the key's top
+// `dbits` bits, key >> hshift) in any order: k_sp_excount counts the records
+// per bucket (DX_COPIES histogram copies) and in total (ctr[C_W]);
+// k_sp_exemit reserves one slot range per (workgroup, bucket) with a global
+// cursor and writes the records there.  No look-back and no MSD pass;
+// k_sp_group then sorts balanced ranges of whole buckets by key.  One
 // survivor per thread, no hand-off between workgroups.
+constexpr int DX_MAXBITS = 12;
+constexpr uint32_t DX_MAXB = 1u << DX_MAXBITS;  // buckets at most
+constexpr int DX_COPIES = 4;                     // histogram copies (contention of the adds)
+
 __global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                    const uint32_t* __restrict__ surv, uint64_t* __restrict__ ctr,
-                                                   int hshift, uint32_t* __restrict__ ghist, uint64_t* __restrict__ ts) {
+                                                   int hshift, int dbits, uint32_t* __restrict__ ghist,
+                                                   uint64_t* __restrict__ ts) {
   ts_enter(ts, TS_FIRST);
-  __shared__ uint32_t s_h[RS_BINS];
-  __shared__ uint64_t s_wt[NWAVE];
+  __shared__ uint32_t s_h[DX_MAXB];
+  __shared__ uint64_t s_red[NWAVE];
   const int t = threadIdx.x;
+  const uint32_t nb = 1u << dbits, bm = nb - 1;
   const uint64_t n = ctr[C_NV];
   if ((uint64_t)blockIdx.x * NT >= n) return;
-  s_h[t] = 0;
+  for (uint32_t i = t; i < nb; i += NT) s_h[i] = 0;
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * NT + t;
   ExSurv x;
@@ -548,19 +555,22 @@ __global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uin
   else ex_empty(g, x);
   uint64_t c = 0;
   ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
-    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & 0xffu], 1u);
+    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & bm], 1u);
     ++c;
   });
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if (lane_id() == 0) s_wt[wave_id()] = c;
+  if (lane_id() == 0) s_red[wave_id()] = c;
   __syncthreads();
-  const uint32_t h = s_h[t];
-  if (h) atomicAdd(&hist_copy(ghist)[t], h);
+  uint32_t* hc = ghist + (blockIdx.x % DX_COPIES) * DX_MAXB;
+  for (uint32_t b = t; b < nb; b += NT) {
+    const uint32_t h = s_h[b];
+    if (h) atomicAdd(&hc[b], h);
+  }
   if (t == 0) {
     uint64_t tot = 0;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) tot += s_wt[w];
+    for (int w = 0; w < NWAVE; ++w) tot += s_red[w];
     if (tot) atomicAdd((unsigned long long*)&ctr[C_W], (unsigned long long)tot);
   }
 }
@@ -568,12 +578,14 @@ __global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uin
 __global__ __launch_bounds__(NT) void k_sp_exemit(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                   const uint32_t* __restrict__ surv, uint64_t capW,
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
-                                                  uint64_t* __restrict__ ctr, int hshift,
+                                                  uint64_t* __restrict__ ctr, int hshift, int dbits,
                                                   const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bcur) {
-  __shared__ uint32_t s_h[RS_BINS];  // records per bucket, then the next free slot per bucket
-  __shared__ uint32_t s_start[RS_BINS];
+  constexpr uint32_t PER = DX_MAXB / NT;  // buckets per thread in the start scan
+  __shared__ uint32_t s_h[DX_MAXB];       // records per bucket, then the next free slot per bucket
+  __shared__ uint32_t s_start[DX_MAXB];
   __shared__ uint64_t s_red[NWAVE + 1];
   const int t = threadIdx.x;
+  const uint32_t nb = 1u << dbits, bm = nb - 1;
   const uint64_t n = ctr[C_NV];
   if ((uint64_t)blockIdx.x * NT >= n) return;
   const uint64_t W = ctr[C_W];
@@ -583,26 +595,50 @@ __global__ __launch_bounds__(NT) void k_sp_exemit(GraphView g, uint64_t ua, uint
     if (!fits) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_OVERFLOW);
   }
   if (!fits) return;
-  uint64_t tot;
-  s_start[t] = (uint32_t)block_excl_scan(hist_total(ghist, t), s_red, &tot);  // bucket starts (syncs)
-  s_h[t] = 0;
+  // bucket starts: exclusive scan of the summed histogram copies (thread t: PER consecutive buckets)
+  {
+    const uint32_t per = (nb + NT - 1) / NT;
+    uint32_t hv[PER], sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t b = t * per + q;
+      uint32_t h = 0;
+      if (q < per && b < nb) {
+#pragma unroll
+        for (int cpy = 0; cpy < DX_COPIES; ++cpy) h += ghist[cpy * DX_MAXB + b];
+      }
+      hv[q] = h;
+      sum += h;
+    }
+    uint64_t tot;
+    uint32_t run = (uint32_t)block_excl_scan(sum, s_red, &tot);  // syncs
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t b = t * per + q;
+      if (q < per && b < nb) {
+        s_start[b] = run;
+        s_h[b] = 0;
+      }
+      run += hv[q];
+    }
+  }
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * NT + t;
   ExSurv x;
   if (i < n) ex_load(g, surv[i], x);
   else ex_empty(g, x);
   ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
-    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & 0xffu], 1u);
+    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & bm], 1u);
   });
   __syncthreads();
-  const uint32_t c = s_h[t];
-  const uint32_t base = c ? atomicAdd(&bcur[t], c) : 0u;
-  __syncthreads();
-  s_h[t] = s_start[t] + base;
+  for (uint32_t b = t; b < nb; b += NT) {
+    const uint32_t c = s_h[b];
+    s_h[b] = s_start[b] + (c ? atomicAdd(&bcur[b], c) : 0u);
+  }
   __syncthreads();
   ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
     const uint64_t key = ex_key(u, w, ua, wbits);
-    const uint32_t pos = atomicAdd(&s_h[(uint32_t)(key >> hshift) & 0xffu], 1u);
+    const uint32_t pos = atomicAdd(&s_h[(uint32_t)(key >> hshift) & bm], 1u);
     rkey[pos] = key;
     rval[pos] = x.v;
   });

@@ -14,6 +14,7 @@ last = a[-rec:].reshape(65536, 8)[:, :nph].astype(np.int64)
 blocks = last[last[:, 0] != 0]
 # phases that were stamped by every block
 ok = [i for i in range(nph) if (blocks[:, i] != 0).all()]
+ok.sort(key=lambda i: blocks[:, i].mean())  # phases in time order
 t0 = blocks[:, 0].min()
 print("blocks %d, phases stamped %s" % (len(blocks), ok))
 print("start offset: mean %.2f us max %.2f us" % ((blocks[:, 0] - t0).mean() / 100, (blocks[:, 0] - t0).max() / 100))
