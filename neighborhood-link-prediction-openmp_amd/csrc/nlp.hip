@@ -65,7 +65,7 @@ enum Buf {
   B_FARENA, B_FAGG,
   // sort-grouped fast path (sortpath.hpp)
   B_SP_SURV, B_SP_RK0, B_SP_RK1, B_SP_RV0, B_SP_RV1, B_SP_STASH, B_SP_CU, B_SP_CW, B_SP_CS,
-  B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA, B_SP_SEGCNT,
+  B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA, B_SP_SEGCNT, B_SP_BKT,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER,
@@ -159,6 +159,7 @@ struct nlp_graph {
   int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
+  bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
   int dx_bits = 0;                             // direct buckets: forced width (NLP_DX_BITS, 0 = from dx_target)
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
@@ -504,6 +505,7 @@ nlp_status finish_graph(nlp_graph* g) {
   }
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
+  if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
   if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
@@ -1650,11 +1652,16 @@ struct SpBufs {
   uint64_t arena_words;
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
   uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
+  uint64_t d_wsum;                              // WSUM_COPIES wedge-count copies (direct emission)
   uint64_t d_bcur;                              // DX_MAXB u32 bucket cursors (direct emission)
   uint64_t d_ts;                                // TS_WORDS u64 call-timing stamps (sortpath.hpp ts_enter)
   bool direct;    // count metrics, one MSD pass: k_sp_excount + k_sp_exemit + k_sp_group instead of
                   // k_sp_expand + MSD pass + k_sp_bucket
   int dbits, dshift;  // direct buckets: the key's top dbits bits (key >> dshift)
+  bool fused;         // direct, small W: fixed-capacity buckets (k_sp_exbucket) sorted and scored by
+                      // k_sp_grouprun, one workgroup per bucket
+  int caplog;         // fused: log2 of the slots per bucket
+  uint64_t* bkt;      // fused: the buckets' record slots (2^(dbits + caplog) keys)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
@@ -1742,6 +1749,34 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
     f.dbits = std::min(db, std::max(1, f.wbits + ubits));
     f.dshift = std::max(0, f.wbits + ubits - f.dbits);
   }
+  // fixed-capacity buckets: ~CAP/4 records per bucket on average (skew headroom),
+  // CAP = 1024 or 2048, at most DX_MAXB buckets
+  f.fused = false;
+  f.caplog = 10;
+  if (f.direct && g->fuse_runs) {
+    const double est = std::max(1.0, hp_estimate(g, p));
+    for (int cl = 10; cl <= 11 && !f.fused; ++cl) {
+      int db = 8;
+      while (db < DX_MAXBITS && est / (double)(1u << db) > (double)(1u << cl) / 4) ++db;
+      if (g->dx_bits) db = std::min(g->dx_bits, DX_MAXBITS);
+      db = std::min(db, std::max(1, f.wbits + ubits));
+      if (g->dx_bits || est / (double)(1u << db) <= (double)(1u << cl) / 4) {
+        const uint64_t slots = (uint64_t)1 << (db + cl);
+        TRY(wsget(ws, B_SP_BKT, slots, &f.bkt));
+        // the candidate columns are indexed by bucket slot
+        TRY(wsget(ws, B_SP_CU, std::max(capW, slots), &f.cu));
+        TRY(wsget(ws, B_SP_CW, std::max(capW, slots), &f.cw));
+        TRY(wsget(ws, B_SP_CS, std::max(capW, slots), &f.cs));
+        TRY(wsget(ws, B_SP_OK0, std::max(capW, slots), &f.ok0));
+        TRY(wsget(ws, B_SP_OV0, std::max(capW, slots), &f.ov0));
+        TRY(wsget(ws, B_SP_SEGCNT, std::max<uint64_t>((capW + RU_SEG - 1) / RU_SEG + 1, DX_MAXB), &f.segcnt));
+        f.fused = true;
+        f.caplog = cl;
+        f.dbits = db;
+        f.dshift = std::max(0, f.wbits + ubits - db);
+      }
+    }
+  }
   // The count metrics do not depend on the order of a run's wedges, so their
   // survivors can come from the degree-class index in any order; Adamic-Adar and
   // Resource-Allocation sum in ascending v and keep the ordered survivor scan.
@@ -1756,13 +1791,14 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
     f.survivors = g->rx_vbydeg;
   }
   const uint64_t tS = (S + SV_TILE - 1) / SV_TILE, tE = (S + NT - 1) / NT;
-  const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, RS_BINS);
+  const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, DX_MAXB);  // also k_sp_grouprun's buckets
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
   f.d_tick = SP_DESC;
   f.d_bcur = f.d_tick + SP_NTICK / 2;
   f.d_ts = f.d_bcur + DX_MAXB / 2;
-  f.d_surv = f.d_ts + TS_WORDS;
+  f.d_wsum = f.d_ts + TS_WORDS;
+  f.d_surv = f.d_wsum + WSUM_COPIES;
   f.d_exp = f.d_surv + tS + 1;
   f.d_run = f.d_exp + tE + 1;
   f.d_rec = f.d_run + tR + 1;
@@ -1770,6 +1806,12 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.arena_words = f.d_ord + (4 * f.ostride + 1) / 2;
   TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
   return NLP_OK;
+}
+
+// The stage timed as the dominant kernel by default: the scoring kernel.
+int sp_hot_default(const SpBufs& f) {
+  const int s_runs = 4 + (f.msd ? f.msd_passes : f.passes) + (f.split ? 1 : 0);
+  return f.fused ? s_runs - 1 : s_runs;
 }
 
 // Algorithmic bytes of one launch of sort-path stage `s`,
@@ -1780,6 +1822,8 @@ uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64
   if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
   const int P = f.msd ? f.msd_passes : f.passes;
   if (s >= 4 && s < 4 + P) return 24 * W;  // records in + out
+  if (f.fused && s == 4 + P) return 8 * W + 4 * ((uint64_t)1 << f.dbits) + 20 * C;  // grouprun: counts + keys in,
+                                                                                    // candidates out (u, w, score, key, slot)
   if (f.split && s == 4 + P) return 8 * W + 8 * W + 4 * W;  // bucket sort: keys in, sorted keys + run lengths out
   if (f.split && s == 5 + P) return 8 * W + 4 * W + 20 * C;  // runs: sorted keys, run lengths, candidates
   if (s == 4 + P) return f.msd ? 8 * W + 20 * C : 12 * W + 4 * W + 20 * C;  // records (+stash), candidates
@@ -1809,7 +1853,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint64_t* rk_m = (P & 1) ? f.rk1 : f.rk0;
   uint32_t* rv_m = (P & 1) ? f.rv1 : f.rv0;
   uint32_t* rv_free = (P & 1) ? f.rv0 : f.rv1;
-  const int hot = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
+  const int hot = g->hot_stage < 0 ? sp_hot_default(f) : std::min(std::max(g->hot_stage, 1), n_st - 1);
   auto grid = [](uint64_t tiles, unsigned occ) {
     return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, occ)));
   };
@@ -1832,9 +1876,16 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s == 2) {
       // survivors: known exactly with the degree-class index, else at most S
       const uint64_t nsv = f.dindex ? f.nv : S;
+      if (f.fused) {
+        hipLaunchKernelGGL(k_sp_exbucket, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
+                           gv, ua, ub, f.wbits, f.survivors, f.dshift, f.dbits, f.caplog, f.bkt,
+                           (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts);
+        TRY(hipGetLastError());
+        return NLP_OK;
+      }
       if (f.direct) {
         hipLaunchKernelGGL(k_sp_excount, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
-                           gv, ua, ub, f.wbits, f.survivors, ctr, f.dshift, f.dbits, hrec, ts);
+                           gv, ua, ub, f.wbits, f.survivors, ctr, f.dshift, f.dbits, hrec, f.arena + f.d_wsum, ts);
         TRY(hipGetLastError());
         return NLP_OK;
       }
@@ -1854,11 +1905,13 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       else NLP_EXPAND(1);
 #undef NLP_EXPAND
     } else if (s == 3) {
+      if (f.fused) return NLP_OK;  // k_sp_exbucket placed the records
       if (f.direct) {  // records straight into their MSD buckets (the buffers the bucket sort reads)
         const uint64_t nsv = f.dindex ? f.nv : S;
         hipLaunchKernelGGL(k_sp_exemit, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
                            gv, ua, ub, f.wbits, f.survivors, capW, rk_m, rv_m, ctr, f.dshift, f.dbits,
-                           (const uint32_t*)hrec, (uint32_t*)(f.arena + f.d_bcur));
+                           (const uint32_t*)hrec, (uint32_t*)(f.arena + f.d_bcur),
+                           (const uint64_t*)(f.arena + f.d_wsum));
         TRY(hipGetLastError());
         return NLP_OK;
       }
@@ -1890,7 +1943,18 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            hot == s ? g->d_stamp : nullptr, rk_m, rv_free, (uint32_t*)nullptr);
     } else if (f.split && s == s_runs - 1) {
       const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + GR_T - 1) / GR_T));
-      if (custom)
+      if (f.fused) {
+        const uint32_t nb = 1u << f.dbits;
+#define NLP_GROUPRUN(CL)                                                                                         \
+  hipLaunchKernelGGL(k_sp_grouprun<CL>, dim3(nb), dim3(GR_NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,  \
+                     (const uint64_t*)f.bkt, (const uint32_t*)(f.arena + f.d_bcur), f.cu, f.cw, f.cs, f.ok0,    \
+                     f.ov0, f.segcnt, ctr, hord, (const uint64_t*)(f.arena + f.d_wsum),                        \
+                     hot == s ? g->d_stamp : nullptr, ts)
+        if (f.caplog == 11) NLP_GROUPRUN(11);
+        else NLP_GROUPRUN(10);
+#undef NLP_GROUPRUN
+      }
+      else if (custom)
         hipLaunchKernelGGL(k_sp_group<true>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,
                            f.msd_shift, rk_m, rv_free, (uint32_t*)f.stash, ctr, hot == s ? g->d_stamp : nullptr);
       else  // after direct emission the fine buckets are the dbits-bit buckets
@@ -1898,6 +1962,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            f.direct ? f.dshift : f.msd_shift, rk_m, rv_free, (uint32_t*)nullptr, ctr,
                            hot == s ? g->d_stamp : nullptr);
     } else if (f.split && s == s_runs) {
+      if (f.fused) return NLP_OK;  // scored by k_sp_grouprun
       // one workgroup per RU_TILE records, no hand-off (gapped output)
       const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + RU_TILE - 1) / RU_TILE));
       if (custom)
@@ -1941,11 +2006,18 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.split && ps == 0)  // k_sp_runs' gapped candidates (and digit 0); this pass counts digits 1-3
-        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
+      if (f.fused && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts digits 1-3
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_BUCKETS>), grid(tO, g->occ_p32),
+                           dim3(OS_NT), 0, st, (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
+                           (const uint64_t*)&ctr[C_C], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
+                           hot == s ? g->d_stamp : nullptr, GatherOut{}, hord + RS_BINS, (const uint32_t*)f.segcnt,
+                           &ctr[C_C], (const uint64_t*)nullptr, 1u << f.dbits, f.caplog, ts + TS_HOT_OUT);
+      else if (f.split && ps == 0)  // k_sp_runs' gapped candidates (and digit 0); this pass counts digits 1-3
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_SEGMENTS>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
                            (const uint64_t*)&ctr[C_WSORT], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
-                           (uint64_t*)nullptr, GatherOut{}, hord + RS_BINS, (const uint32_t*)f.segcnt, &ctr[C_C]);
+                           hot == s ? g->d_stamp : nullptr, GatherOut{}, hord + RS_BINS, (const uint32_t*)f.segcnt,
+                           &ctr[C_C], (const uint64_t*)&ctr[C_FLAGS], 0u, 0, ts + TS_HOT_OUT);
       else if (f.msd && ps == 0)  // k_sp_bucket counted digit 0; this pass counts digits 1-3
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1, (const uint64_t*)&ctr[C_C],
@@ -1962,7 +2034,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
                            odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
                            (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, tick + TK_ORD + ps,
-                           err, (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr);
+                           err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
     } else {
       if (g->fuse_gather) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
@@ -2345,10 +2417,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       t->graph_replay = replayed ? 1u : 0u;
       if (sorted) {
         const int s_runs = 4 + (sp.msd ? sp.msd_passes : sp.passes) + (sp.split ? 1 : 0);
-        const int hs = g->hot_stage < 0 ? s_runs : std::min(std::max(g->hot_stage, 1), s_runs);
+        const int hs = g->hot_stage < 0 ? sp_hot_default(sp) : std::min(std::max(g->hot_stage, 1), s_runs);
         t->hot_bytes = sp_stage_bytes(g, sp, hs, h);
-        t->hot_kernel = hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
-                        : (sp.split && hs == s_runs - 1) ? (sp.msd_passes == 1 && g->group_sort != 1 ? 1u : 8u)
+        t->hot_kernel = (sp.fused && hs == s_runs - 1) ? 9u
+                        : hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
+                        : (sp.split && hs == s_runs - 1) ? (sp.msd_passes == 1 && g->group_sort != 1 && !sp.direct ? 1u : 8u)
                         : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
       } else {
         // k_group_tiles: bucket counts, records, flags, runs

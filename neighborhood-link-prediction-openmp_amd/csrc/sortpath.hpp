@@ -130,19 +130,34 @@ __device__ __forceinline__ uint64_t lb_lookback_r(uint64_t* desc, uint64_t tile,
 // latest exit of the hot kernel; s_memrealtime ticks (100 MHz).  Minima are
 // kept as maxima of the complement so that a zeroed arena is the identity.
 enum { TS_FIRST = 0, TS_HOT_IN = 1, TS_HOT_OUT = 2, TS_WORDS = 4 };
+// Workgroup 0 only (dispatched first): thousands of same-address atomics
+// serialise for microseconds, and a workgroup's later loads wait behind its own.
 __device__ __forceinline__ void ts_enter(uint64_t* ts, int slot) {
-  if (ts && threadIdx.x == 0)
+  if (ts && blockIdx.x == 0 && threadIdx.x == 0)
     atomicMax((unsigned long long*)&ts[slot], (unsigned long long)~__builtin_amdgcn_s_memrealtime());
 }
-__device__ __forceinline__ void ts_exit(uint64_t* ts, int slot) {
-  if (ts && threadIdx.x == 0)
-    atomicMax((unsigned long long*)&ts[slot], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+// The end of a kernel = the entry of workgroup 0 of the kernel after it.
+__device__ __forceinline__ void ts_mark_end(uint64_t* slot) {
+  if (slot && blockIdx.x == 0 && threadIdx.x == 0)
+    atomicMax((unsigned long long*)slot, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+// Wedge totals in WSUM_COPIES counters (workgroup b adds into b % WSUM_COPIES)
+constexpr int WSUM_COPIES = 16;
+__device__ __forceinline__ uint64_t wsum_total(const uint64_t* w) {
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < WSUM_COPIES; ++i) s += w[i];
+  return s;
 }
 
 // Optional phase stamps for tools/ubench (nullptr in the product): workgroup b
 // writes s_memrealtime (100 MHz) of phase i of its first tile to stamp[8 b + i].
 __device__ __forceinline__ void sp_stamp(uint64_t* stamp, bool first, int i) {
   if (stamp && first && threadIdx.x == 0) stamp[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+// shader-clock counter beside a stamp (the clock rate = its rate / the 100 MHz stamps')
+__device__ __forceinline__ void sp_clock(uint64_t* stamp, int i) {
+  if (stamp && threadIdx.x == 0) stamp[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memtime();
 }
 
 __device__ __forceinline__ uint64_t lane_mask_lt() {
@@ -539,7 +554,7 @@ constexpr int DX_COPIES = 4;                     // histogram copies (contention
 __global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                    const uint32_t* __restrict__ surv, uint64_t* __restrict__ ctr,
                                                    int hshift, int dbits, uint32_t* __restrict__ ghist,
-                                                   uint64_t* __restrict__ ts) {
+                                                   uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts) {
   ts_enter(ts, TS_FIRST);
   __shared__ uint32_t s_h[DX_MAXB];
   __shared__ uint64_t s_red[NWAVE];
@@ -571,7 +586,7 @@ __global__ __launch_bounds__(NT) void k_sp_excount(GraphView g, uint64_t ua, uin
     uint64_t tot = 0;
 #pragma unroll
     for (int w = 0; w < NWAVE; ++w) tot += s_red[w];
-    if (tot) atomicAdd((unsigned long long*)&ctr[C_W], (unsigned long long)tot);
+    if (tot) atomicAdd((unsigned long long*)&wsum[blockIdx.x % WSUM_COPIES], (unsigned long long)tot);
   }
 }
 
@@ -579,7 +594,8 @@ __global__ __launch_bounds__(NT) void k_sp_exemit(GraphView g, uint64_t ua, uint
                                                   const uint32_t* __restrict__ surv, uint64_t capW,
                                                   uint64_t* __restrict__ rkey, uint32_t* __restrict__ rval,
                                                   uint64_t* __restrict__ ctr, int hshift, int dbits,
-                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bcur) {
+                                                  const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bcur,
+                                                  const uint64_t* __restrict__ wsum) {
   constexpr uint32_t PER = DX_MAXB / NT;  // buckets per thread in the start scan
   __shared__ uint32_t s_h[DX_MAXB];       // records per bucket, then the next free slot per bucket
   __shared__ uint32_t s_start[DX_MAXB];
@@ -588,9 +604,10 @@ __global__ __launch_bounds__(NT) void k_sp_exemit(GraphView g, uint64_t ua, uint
   const uint32_t nb = 1u << dbits, bm = nb - 1;
   const uint64_t n = ctr[C_NV];
   if ((uint64_t)blockIdx.x * NT >= n) return;
-  const uint64_t W = ctr[C_W];
+  const uint64_t W = wsum_total(wsum);
   const bool fits = W <= capW;
   if (blockIdx.x == 0 && t == 0) {
+    ctr[C_W] = W;
     ctr[C_WSORT] = fits ? W : 0;
     if (!fits) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_OVERFLOW);
   }
@@ -740,9 +757,9 @@ __device__ __forceinline__ uint32_t os_lookback(const uint32_t* desc, uint64_t t
 // desc[tile * 256 + digit], each written by one agent-scope atomic store and
 // read by agent-scope atomic loads (the data is the flag: no fences).
 //
-// GAPPED: the input is k_sp_runs' layout -- slot j is valid when j < n and
-// j % RU_SEG < seg_cnt[j / RU_SEG] -- and the pass writes the number of valid
-// keys (the candidate count) to *tot_out.
+// GAPPED (GAP_SEGMENTS): the input is k_sp_runs' layout -- slot j is valid
+// when j < n and j % RU_SEG < seg_cnt[j / RU_SEG] -- and the pass writes the
+// number of valid keys (the candidate count) to *tot_out.
 // NEXT_HIST: also count digits 1..3 (shift 8, 16, 24) of the input keys into
 // the histogram copies at nhist (the first pass of a 32-bit sort whose later
 // histograms were not produced upstream).
@@ -782,7 +799,31 @@ __device__ __forceinline__ uint32_t os_digit_scan(uint32_t x, uint32_t* s_w, uin
   return pre + inc - x;
 }
 
-template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false, bool GAPPED = false>
+enum { GAP_NONE = 0, GAP_SEGMENTS = 1, GAP_BUCKETS = 2 };
+// Exclusive scan of one value per thread over an OS_NT workgroup (s_w: OS_NW
+// words); also returns the total.
+__device__ __forceinline__ uint32_t os_block_scan(uint32_t x, uint32_t* s_w, uint64_t* total) {
+  const int lane = lane_id(), wv = wave_id();
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < OS_NW; ++w) {
+    pre += w < wv ? s_w[w] : 0u;
+    tot += s_w[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return pre + inc - x;
+}
+
+template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false, int GAPPED = GAP_NONE>
 __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    const uint64_t* __restrict__ d_n, int shift,
@@ -791,7 +832,10 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
                                                    uint64_t* __restrict__ stamp, GatherOut go,
                                                    uint32_t* __restrict__ nhist = nullptr,
                                                    const uint32_t* __restrict__ seg_cnt = nullptr,
-                                                   uint64_t* __restrict__ tot_out = nullptr) {
+                                                   uint64_t* __restrict__ tot_out = nullptr,
+                                                   const uint64_t* __restrict__ abort_flags = nullptr,
+                                                   uint32_t nseg = 0, int seglog = 0,
+                                                   uint64_t* __restrict__ end_mark = nullptr) {
   constexpr int WT = 64 * IPT;
   constexpr int TILE = OS_NT * IPT;
   static_assert(!GAPPED || (RU_SEG % 64 == 0), "a wave substep must lie in one segment");
@@ -800,9 +844,39 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
   __shared__ uint32_t s_nh[NEXT_HIST ? 3 : 1][NEXT_HIST ? RS_BINS : 1];
   __shared__ uint32_t s_w[4];
   __shared__ uint32_t s_tile[2];
+  __shared__ uint32_t s_pre[GAPPED == GAP_BUCKETS ? DX_MAXB + 1 : 1];
+  __shared__ uint32_t s_w16[GAPPED == GAP_BUCKETS ? OS_NW : 1];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint64_t n = *d_n;
+  ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel's, for the first ordering pass)
+  // abort_flags: a range of the grouping raised F_TOOBIG, so the input holds
+  // stale slots and the call is redone -- order nothing (and count 0 candidates)
+  const bool abort = abort_flags && (*abort_flags & F_TOOBIG);
+  uint64_t n = abort ? 0 : *d_n;
+  if (GAPPED == GAP_BUCKETS) {
+    // GAP_BUCKETS: segment b holds seg_cnt[b] keys at slots [b 2^seglog, ...);
+    // dense index j lies in the segment with s_pre[b] <= j < s_pre[b + 1]
+    constexpr uint32_t PER = (DX_MAXB + OS_NT - 1) / OS_NT;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t b = (uint32_t)t * PER + q;
+      c[q] = b < nseg ? seg_cnt[b] : 0u;
+      sum += c[q];
+    }
+    uint64_t tot;
+    uint32_t run = os_block_scan(sum, s_w16, &tot);
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      const uint32_t b = (uint32_t)t * PER + q;
+      if (b < nseg) s_pre[b] = run;
+      run += c[q];
+    }
+    if (t == 0) s_pre[nseg] = (uint32_t)tot;
+    __syncthreads();
+    n = tot;
+  }
   const uint64_t ntiles = (n + TILE - 1) / TILE;
+  if (GAPPED && abort && tot_out && blockIdx.x == 0 && t == 0) *tot_out = 0;
   // GATHER: every counter is final by now; they are published by the workgroup
   // of the last tile after its scatter (or by workgroup 0 when there is no tile)
   auto publish = [&]() {
@@ -841,9 +915,19 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
     for (int i = 0; i < IPT; ++i) {
       const uint64_t j = b0 + (uint64_t)i * 64;
       ok[i] = j < n;
-      if (GAPPED && ok[i]) ok[i] = (uint32_t)(j % RU_SEG) < seg_cnt[j / RU_SEG];
-      k[i] = ok[i] ? kin[j] : (K)0;
-      v[i] = ok[i] ? vin[j] : 0u;
+      if (GAPPED == GAP_SEGMENTS && ok[i]) ok[i] = (uint32_t)(j % RU_SEG) < seg_cnt[j / RU_SEG];
+      uint64_t sj = j;
+      if (GAPPED == GAP_BUCKETS && ok[i]) {  // the segment holding dense index j: last b with s_pre[b] <= j
+        uint32_t lo = 0, hi = nseg;  // s_pre[lo] <= j < s_pre[hi]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_pre[mid] <= (uint32_t)j) lo = mid;
+          else hi = mid;
+        }
+        sj = ((uint64_t)lo << seglog) + ((uint32_t)j - s_pre[lo]);
+      }
+      k[i] = ok[i] ? kin[sj] : (K)0;
+      v[i] = ok[i] ? vin[sj] : 0u;
     }
     EdgeOut eo[GATHER ? IPT : 1];
     if (GATHER) {  // the output columns are fetched now, in flight during ranking and look-back
@@ -1464,6 +1548,273 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
   sp_stamp(stamp, true, 3);
 }
 
+// ---------------------------------------------------------------- fixed-capacity buckets
+// Count metrics at small wedge counts: the records go straight into 2^dbits
+// buckets (the key's top dbits bits, key >> hshift) of CAP slots each -- no
+// counting pass, no scan: k_sp_exbucket counts a workgroup's records per
+// bucket in LDS, reserves its slots with one atomic per used bucket and
+// writes them (any order: the count metrics ignore the wedge order).  A bucket
+// beyond CAP raises F_TOOBIG (the host then takes the grouped path).  Then
+// k_sp_grouprun, one workgroup per bucket: sort the bucket's
+// keys in registers (bitonic network, E keys per thread: shuffles for partner
+// distances below 64, LDS beyond), find the runs, score each (first-order
+// exclusion, metric, minScore, MAXFACTOR2 -- as k_sp_runs), and write the
+// candidates in (u, w) order into the bucket's own slots, counting digit 0 of
+// their order keys.
+constexpr int GR_NT = 256;
+constexpr int GR_NW = GR_NT / 64;
+
+__global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, uint64_t ub, int wbits,
+                                                    const uint32_t* __restrict__ surv, int hshift, int dbits,
+                                                    int caplog, uint64_t* __restrict__ rkey,
+                                                    uint32_t* __restrict__ bcnt, uint64_t* __restrict__ ctr,
+                                                    uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts) {
+  ts_enter(ts, TS_FIRST);
+  __shared__ uint32_t s_h[DX_MAXB];
+  __shared__ uint64_t s_red[NWAVE];
+  const int t = threadIdx.x;
+  const uint32_t nb = 1u << dbits, bm = nb - 1, cap = 1u << caplog;
+  const uint64_t n = ctr[C_NV];
+  if ((uint64_t)blockIdx.x * NT >= n) return;
+  for (uint32_t i = t; i < nb; i += NT) s_h[i] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * NT + t;
+  ExSurv x;
+  if (i < n) ex_load(g, surv[i], x);
+  else ex_empty(g, x);
+  uint64_t c = 0;
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & bm], 1u);
+    ++c;
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane_id() == 0) s_red[wave_id()] = c;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) tot += s_red[w];
+    if (tot) atomicAdd((unsigned long long*)&wsum[blockIdx.x % WSUM_COPIES], (unsigned long long)tot);
+  }
+  for (uint32_t b = t; b < nb; b += NT) {  // reserve: s_h[b] = this workgroup's first slot in bucket b
+    const uint32_t h = s_h[b];
+    s_h[b] = h ? atomicAdd(&bcnt[b], h) : 0u;
+  }
+  __syncthreads();
+  bool over = false;
+  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
+    const uint64_t key = ex_key(u, w, ua, wbits);
+    const uint32_t b = (uint32_t)(key >> hshift) & bm;
+    const uint32_t pos = atomicAdd(&s_h[b], 1u);
+    if (pos < cap) rkey[((uint64_t)b << caplog) + pos] = key;
+    else over = true;
+  });
+  if (__ballot(over) && lane_id() == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
+}
+
+// Ascending bitonic network over E * GR_NT keys, element i = t + r GR_NT in
+// k[r].  Partners at distance j < 64 are fetched with ds_bpermute, 64 <= j <
+// GR_NT through LDS, j >= GR_NT are in the same thread.  One compare-exchange
+// is a 64-bit compare and two selects: keep the partner's key when it is on
+// the wanted side.
+template <int E>
+__device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int t) {
+  constexpr uint32_t N = (uint32_t)GR_NT * E;
+  const int lane = t & 63;
+#pragma unroll 1
+  for (uint32_t size = 2; size <= N; size <<= 1) {
+#pragma unroll 1
+    for (uint32_t j = size >> 1; j > 0; j >>= 1) {
+      if (j >= (uint32_t)GR_NT) {  // partner in the same thread: element r ^ (j / GR_NT)
+        const uint32_t jr = j / GR_NT;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          if (((uint32_t)r & jr) == 0) {
+            const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+            const bool asc = (i & size) == 0;
+            const uint64_t x = k[r], y = k[r | jr];
+            const bool sw = (x > y) == asc;
+            k[r] = sw ? y : x;
+            k[r | jr] = sw ? x : y;
+          }
+        }
+        continue;
+      }
+      uint64_t o[E];
+      if (j >= 64) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) s[t + r * GR_NT] = k[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) o[r] = s[(t ^ (int)j) + r * GR_NT];
+      } else {
+        const int idx = (lane ^ (int)j) << 2;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)(uint32_t)k[r]);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)(uint32_t)(k[r] >> 32));
+          o[r] = ((uint64_t)hi << 32) | lo;
+        }
+      }
+      const bool upper = ((uint32_t)t & j) != 0;
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+        // keep the minimum when (ascending block) == (lower element)
+        const bool keep_min = ((i & size) != 0) == upper;
+        k[r] = ((k[r] > o[r]) == keep_min) ? o[r] : k[r];
+      }
+    }
+  }
+}
+
+// the range's m <= E GR_NT keys, sorted, to s_key[0, m)
+template <int E>
+__device__ __forceinline__ void gr_sort(const uint64_t* __restrict__ rkey, uint64_t start, uint32_t m,
+                                        uint64_t* s_key, int t, uint64_t* stamp = nullptr) {
+  uint64_t k[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+    k[r] = i < m ? rkey[start + i] : ~0ull;
+  }
+  if (stamp) {  // diagnostics: the keys have arrived
+    uint64_t x = 0;
+#pragma unroll
+    for (int r = 0; r < E; ++r) x ^= k[r];
+    if (x == 0x5a5a5a5a5a5a5a5aull) s_key[0] = x;
+    sp_stamp(stamp, true, 5);
+  }
+  bitonic_sort<E>(k, s_key, t);
+  sp_stamp(stamp, true, 6);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < E; ++r) s_key[t + r * GR_NT] = k[r];
+  __syncthreads();
+}
+
+// exclusive scan over a GR_NT workgroup (s_w: GR_NW words); *total = the sum
+__device__ __forceinline__ uint32_t gr_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();  // s_w reuse
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < GR_NW; ++w) {
+    pre += w < wv ? s_w[w] : 0u;
+    tot += s_w[w];
+  }
+  *total = tot;
+  return pre + inc - x;
+}
+
+// one workgroup per bucket (CAP = 2^CAPLOG slots, grid = nb).  Candidates go
+// to the bucket's own slots [b CAP, b CAP + kcnt[b]) of the candidate columns,
+// in (u, w) order; the first ordering pass (k_sp_pass<.., GAP_BUCKETS>) reads
+// them densely through the prefix of kcnt.
+template <int CAPLOG>
+__global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, float min_score, uint64_t ua,
+                                                       int wbits, const uint64_t* __restrict__ rkey,
+                                                       const uint32_t* __restrict__ bcnt,
+                                                       uint32_t* __restrict__ cu, uint32_t* __restrict__ cw,
+                                                       float* __restrict__ cs, uint32_t* __restrict__ okey,
+                                                       uint32_t* __restrict__ oval, uint32_t* __restrict__ kcnt,
+                                                       uint64_t* __restrict__ ctr, uint32_t* __restrict__ ohist,
+                                                       const uint64_t* __restrict__ wsum,
+                                                       uint64_t* __restrict__ stamp, uint64_t* __restrict__ ts) {
+  constexpr uint32_t CAP = 1u << CAPLOG;
+  static_assert(GR_NT == RS_BINS, "one digit-0 bin per thread");
+  __shared__ uint64_t s_key[CAP];
+  __shared__ uint16_t s_rs[CAP + 1];
+  __shared__ uint32_t s_oh[RS_BINS];
+  __shared__ uint32_t s_w[GR_NW];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  ts_enter(ts, TS_HOT_IN);
+  sp_stamp(stamp, true, 0);
+  if (b == 0 && t == 0) ctr[C_W] = ctr[C_WSORT] = wsum_total(wsum);  // k_sp_exbucket's wedge count
+  // after an over-full bucket the call is redone: every bucket reports empty
+  const bool abort = (ctr[C_FLAGS] & F_TOOBIG) != 0;
+  const uint32_t m = abort ? 0u : bcnt[b];
+  if (m == 0) {
+    if (t == 0) kcnt[b] = 0;
+    return;
+  }
+  const uint64_t start = (uint64_t)b << CAPLOG;
+  s_oh[t] = 0;
+  sp_stamp(stamp, true, 4);
+  if (m <= GR_NT) gr_sort<1>(rkey, start, m, s_key, t, stamp);
+  else if (m <= 2 * GR_NT) gr_sort<2>(rkey, start, m, s_key, t, stamp);
+  else if (CAP >= 4 * GR_NT && m <= 4 * GR_NT) gr_sort<(CAP >= 4 * GR_NT ? 4 : 1)>(rkey, start, m, s_key, t, stamp);
+  else if (CAP >= 8 * GR_NT) gr_sort<(CAP >= 8 * GR_NT ? 8 : 1)>(rkey, start, m, s_key, t, stamp);
+  sp_stamp(stamp, true, 1);
+  // run starts (blocked: thread t owns keys [t P, t P + P)) -> run ids -> start positions
+  const uint32_t P = (m + GR_NT - 1) / GR_NT;
+  uint32_t R;
+  {
+    uint32_t ns = 0;
+    for (uint32_t r = 0; r < P; ++r) {
+      const uint32_t q = (uint32_t)t * P + r;
+      ns += (q < m && (q == 0 || s_key[q - 1] != s_key[q])) ? 1u : 0u;
+    }
+    uint32_t id = gr_scan(ns, s_w, &R);
+    for (uint32_t r = 0; r < P; ++r) {
+      const uint32_t q = (uint32_t)t * P + r;
+      if (q < m && (q == 0 || s_key[q - 1] != s_key[q])) s_rs[id++] = (uint16_t)q;
+    }
+    if (t == 0) s_rs[R] = (uint16_t)m;
+    __syncthreads();
+  }
+  sp_stamp(stamp, true, 2);
+  // score the runs, GR_NT per round, compacting in run order
+  const uint64_t wmask = (1ull << wbits) - 1;
+  uint32_t K = 0, nnan = 0;
+  for (uint32_t q0 = 0; q0 < R; q0 += GR_NT) {
+    const uint32_t q = q0 + t;
+    bool keep = false;
+    uint32_t ru = 0, rw = 0;
+    float sc = 0.0f;
+    if (q < R) {
+      const uint32_t p0 = s_rs[q], c = (uint32_t)s_rs[q + 1] - p0;
+      const uint64_t key = s_key[p0];
+      ru = (uint32_t)(ua + (key >> wbits));
+      rw = (uint32_t)(key & wmask);
+      const bool ex = first_order(g, ru, rw);
+      sc = score_basic(metric, ex ? 0u : c, g.deg[ru], g.deg[rw]);
+      keep = !(sc <= min_score) && !f2_drop(g, ru, rw);  // NaN passes
+    }
+    uint32_t kept;
+    const uint32_t pos = K + gr_scan(keep ? 1u : 0u, s_w, &kept);
+    if (keep) {
+      const uint32_t o = (uint32_t)start + pos;
+      cu[o] = ru;
+      cw[o] = rw;
+      cs[o] = sc;
+      const uint32_t k = ~score_key(sc);
+      okey[o] = k;
+      oval[o] = o;
+      atomicAdd(&s_oh[k & 0xffu], 1u);
+      nnan += sc != sc;
+    }
+    K += kept;
+  }
+  if (t == 0) kcnt[b] = K;
+  if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
+  __syncthreads();
+  const uint32_t hc = s_oh[t];
+  if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
+  sp_stamp(stamp, true, 3);
+}
+
 // ---------------------------------------------------------------- balanced run scoring
 // Over the bucket-sorted records, one workgroup per tile of RU_TILE records,
 // wave w on records [base + 64 RU_IPT w, +64 RU_IPT): those that start a run
@@ -1492,6 +1843,7 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
   const uint64_t n = ctr[C_WSORT];
   const uint64_t tile = blockIdx.x;
   if (tile * RU_TILE >= n) return;
+  if (ctr[C_FLAGS] & F_TOOBIG) return;  // stale run lengths: the call is redone (the next pass orders nothing)
   ts_enter(ts, TS_HOT_IN);
   s_oh[t] = 0;
   __syncthreads();
@@ -1621,7 +1973,6 @@ __global__ __launch_bounds__(NT) void k_sp_runs(GraphView g, int metric, float m
   sp_stamp(stamp, true, 2);
   const uint32_t hc = s_oh[t];
   if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
-  ts_exit(ts, TS_HOT_OUT);
 }
 
 // ---------------------------------------------------------------- generic single-pass scan
