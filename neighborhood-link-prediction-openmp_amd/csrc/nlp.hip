@@ -159,6 +159,7 @@ struct nlp_graph {
   int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
+  uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
   int dx_bits = 0;                             // direct buckets: forced width (NLP_DX_BITS, 0 = from dx_target)
@@ -1662,6 +1663,8 @@ struct SpBufs {
                       // k_sp_grouprun, one workgroup per bucket
   int caplog;         // fused: log2 of the slots per bucket
   uint64_t* bkt;      // fused: the buckets' record slots (2^(dbits + caplog) keys)
+  ArenaZero zero;     // arena words reset per call (fused: counters, score-digit histograms, descriptors up to the
+                      // survivor tiles; its ordering descriptors clean themselves)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
@@ -1805,6 +1808,8 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.d_ord = f.d_rec + ((uint64_t)f.passes * f.ostride + 1) / 2;
   f.arena_words = f.d_ord + (4 * f.ostride + 1) / 2;
   TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
+  f.zero = ArenaZero{{0, 0, 0}, {f.arena_words, 0, 0}};
+  if (f.fused) f.zero = ArenaZero{{0, SP_HORD, 0}, {SP_HREC, f.d_surv, 0}};
   return NLP_OK;
 }
 
@@ -1866,8 +1871,9 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       CtrInit ci;
       for (int i = 0; i < NCTR; ++i) ci.v[i] = 0;
       ci.v[C_NV] = f.nv;
-      hipLaunchKernelGGL(k_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (f.arena_words + NT - 1) / NT)),
-                         dim3(NT), 0, st, f.arena, f.arena_words, ci);
+      const uint64_t zw = (f.zero.hi[0] - f.zero.lo[0]) + (f.zero.hi[1] - f.zero.lo[1]);
+      hipLaunchKernelGGL(k_sp_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (zw + NT - 1) / NT)), dim3(NT), 0, st,
+                         f.arena, f.zero, ci);
     } else if (s == 1) {
       if (f.dindex) return NLP_OK;
       hipLaunchKernelGGL(k_sp_survivors, grid((S + SV_TILE - 1) / SV_TILE, g->occ_surv), dim3(NT), 0, st,
@@ -2023,7 +2029,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1, (const uint64_t*)&ctr[C_C],
                            0, (const uint32_t*)hord, dord, tick + TK_ORD, err, (uint64_t*)nullptr, GatherOut{},
                            hord + RS_BINS);
-      else if (ps == 3 && g->fuse_gather)  // the last pass writes the caller's edges
+      else if (ps == 3 && g->fuse_gather && !f.fused)  // the last pass writes the caller's edges
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, true>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)f.ok1, (const uint32_t*)f.ov1, f.ok0, f.ov0, (const uint64_t*)&ctr[C_C], 24,
                            (const uint32_t*)(hord + 3 * RS_BINS), dord + 3 * f.ostride, tick + TK_ORD + 3, err,
@@ -2034,13 +2040,16 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)(odd ? f.ok1 : f.ok0), (const uint32_t*)(odd ? f.ov1 : f.ov0),
                            odd ? f.ok0 : f.ok1, odd ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 8 * ps,
                            (const uint32_t*)(hord + ps * RS_BINS), dord + (uint64_t)ps * f.ostride, tick + TK_ORD + ps,
-                           err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr);
+                           err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (uint64_t*)nullptr, (const uint64_t*)nullptr, 0u, 0,
+                           (uint64_t*)nullptr, f.fused ? dord + (uint64_t)(ps - 1) * f.ostride : (uint32_t*)nullptr);
     } else {
-      if (g->fuse_gather) return NLP_OK;  // done by the last ordering pass
+      if (g->fuse_gather && !f.fused) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
                          dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
-                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev, (const uint64_t*)ts);
+                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev, (const uint64_t*)ts,
+                         f.fused ? dord + 3 * f.ostride : (uint32_t*)nullptr);
     }
     TRY(hipGetLastError());
     return NLP_OK;
@@ -2154,7 +2163,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
         }
       };
       for (int seg = 0; seg < nseg && ok1; ++seg) {
-        if (!stamps || seg == 0) chain_ev(ev_before[seg]);
+        if (!stamps) chain_ev(ev_before[seg]);  // stamps: the kernels time the call themselves
         append(seg_graph[seg]);
       }
       if (ok1 && saw_copy) {
@@ -2267,6 +2276,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     SpBufs sp;
     nlp_status s = sorted ? prepare_sp(g, p, sp, msd, msd_passes) : prepare_fast(g, p, f, st);
     if (s != NLP_OK) return s;
+    // the fused path leaves its ordering descriptors zero; after any other call
+    // (or a new arena) they are zeroed here, outside the captured pipeline
+    if (sorted && sp.fused && g->ord_clean != sp.arena)
+      TRY(hipMemsetAsync(sp.arena + sp.d_ord, 0, 4 * sp.ostride * sizeof(uint32_t), st));
+    g->ord_clean = nullptr;
     bool replayed = false;
     g->last_single = false;
     if (hprof) t1 = now_us();
@@ -2378,6 +2392,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       else msd = false;
       continue;
     }
+    if (sorted && sp.fused && !(h[C_FLAGS] >> 32)) g->ord_clean = sp.arena;  // self-cleaned (or never written)
     g->last_wedges = h[C_W];
     if (sorted && !(h[C_FLAGS] & F_TOOBIG)) {
       g->last_ok_w = est_w;
@@ -2390,10 +2405,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (t) {
       float a = 0, b = 0, hot = 0;
       if (stamps && replayed && g->last_single) {
-        // events at the call's ends; the hot kernel's own stamps (10 ns ticks)
-        float tot = 0;
-        TRY(hipEventElapsedTime(&tot, E[0], E[2]));
+        // the kernels' own stamps (10 ns ticks): first kernel entry, hot kernel
+        // entry and end, the gather's exit -- no event nodes in the graph
         const uint64_t* ts = h + NCTR;
+        const float tot = ts[TS_END] > ~ts[TS_FIRST] ? (float)((ts[TS_END] - ~ts[TS_FIRST]) * 1e-5) : 0.0f;
         hot = ts[TS_HOT_OUT] > ~ts[TS_HOT_IN] ? (float)((ts[TS_HOT_OUT] - ~ts[TS_HOT_IN]) * 1e-5) : 0.0f;
         a = ts[TS_HOT_OUT] > ~ts[TS_FIRST] ? (float)((ts[TS_HOT_OUT] - ~ts[TS_FIRST]) * 1e-5) : 0.0f;
         a = std::min(a, tot);

@@ -129,7 +129,7 @@ __device__ __forceinline__ uint64_t lb_lookback_r(uint64_t* desc, uint64_t tile,
 // call's first kernel), ts[1] = ~(earliest entry of the hot kernel), ts[2] =
 // latest exit of the hot kernel; s_memrealtime ticks (100 MHz).  Minima are
 // kept as maxima of the complement so that a zeroed arena is the identity.
-enum { TS_FIRST = 0, TS_HOT_IN = 1, TS_HOT_OUT = 2, TS_WORDS = 4 };
+enum { TS_FIRST = 0, TS_HOT_IN = 1, TS_HOT_OUT = 2, TS_END = 3, TS_WORDS = 4 };
 // Workgroup 0 only (dispatched first): thousands of same-address atomics
 // serialise for microseconds, and a workgroup's later loads wait behind its own.
 __device__ __forceinline__ void ts_enter(uint64_t* ts, int slot) {
@@ -163,6 +163,18 @@ __device__ __forceinline__ void sp_clock(uint64_t* stamp, int i) {
 __device__ __forceinline__ uint64_t lane_mask_lt() {
   const int lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// Arena reset of one sort-path call: counters from init, up to three word ranges zeroed.
+struct ArenaZero {
+  uint64_t lo[3], hi[3];
+};
+__global__ void k_sp_arena_init(uint64_t* __restrict__ base, ArenaZero z, CtrInit init) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    for (uint64_t i = z.lo[r] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < z.hi[r]; i += stride)
+      base[i] = i < NCTR ? init.v[i] : 0ull;
 }
 
 // ---------------------------------------------------------------- survivors
@@ -710,14 +722,14 @@ __device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
 // always a prefix) so they issue back to back without branches.
 __device__ __forceinline__ uint32_t os_lookback(const uint32_t* desc, uint64_t tile, int d, uint32_t* err) {
   uint32_t excl = 0, spins = 0;
-  int64_t j = (int64_t)tile - 1;
+  int32_t j = (int32_t)tile - 1;  // tiles < 2^22: SP_MAX_N / OS2_TILE
   while (j >= 0) {
+    // predecessors j, j-1, ..: only those that exist are read (32-bit offsets
+    // from the descriptor base); the window beyond tile 0 reads as a zero prefix
     uint32_t x[OS_LBW];
 #pragma unroll
-    for (int r = 0; r < OS_LBW; ++r) {
-      const int64_t q = j - r;
-      x[r] = ld_u32(desc + (uint64_t)(q >= 0 ? q : 0) * RS_BINS + d);
-    }
+    for (int r = 0; r < OS_LBW; ++r)
+      x[r] = r <= j ? ld_u32(&desc[(uint32_t)(j - r) * (uint32_t)RS_BINS + (uint32_t)d]) : OS_PFX;
     int used = 0;
     bool done = false, blocked = false;
 #pragma unroll
@@ -835,7 +847,8 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
                                                    uint64_t* __restrict__ tot_out = nullptr,
                                                    const uint64_t* __restrict__ abort_flags = nullptr,
                                                    uint32_t nseg = 0, int seglog = 0,
-                                                   uint64_t* __restrict__ end_mark = nullptr) {
+                                                   uint64_t* __restrict__ end_mark = nullptr,
+                                                   uint32_t* __restrict__ clean_desc = nullptr) {
   constexpr int WT = 64 * IPT;
   constexpr int TILE = OS_NT * IPT;
   static_assert(!GAPPED || (RU_SEG % 64 == 0), "a wave substep must lie in one segment");
@@ -886,7 +899,8 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       // host-coherent memory; the call's final event (a system-scope release)
       // orders these stores before the host reads them
       if (go.hctr) go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
-      if (go.hctr && go.ts && t < TS_WORDS) go.hctr[NCTR + t] = go.ts[t];
+      if (go.hctr && go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
+      if (go.hctr && t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();  // the last tile: ~the end
     }
   };
   if (GATHER && ntiles == 0 && blockIdx.x == 0) publish();
@@ -993,6 +1007,9 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
         }
       }
     }
+    // clean_desc: the previous pass's descriptors (same tile count), finished
+    // with -- row `tile` back to zero for the next call (no zeroing pass)
+    if (clean_desc && t < RS_BINS) st_u32(&clean_desc[tile * RS_BINS + t], 0u);
     __syncthreads();
     sp_stamp(stamp, first, 4);
     if (GATHER && tile == ntiles - 1) publish();
@@ -2096,18 +2113,28 @@ __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ i
                                                   const uint32_t* __restrict__ cw, const float* __restrict__ cs,
                                                   uint64_t k, EdgeOut* __restrict__ out,
                                                   uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr,
-                                                  const uint64_t* __restrict__ ts) {
+                                                  const uint64_t* __restrict__ ts,
+                                                  uint32_t* __restrict__ clean_desc = nullptr) {
   const uint64_t m = std::min<uint64_t>(ctr[C_C], k);
+  if (clean_desc) {  // the last ordering pass's descriptor rows back to zero (see k_sp_pass)
+    const uint64_t words = (ctr[C_C] + OS2_TILE - 1) / OS2_TILE * RS_BINS;
+    for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < words; i += (uint64_t)gridDim.x * NT)
+      clean_desc[i] = 0u;
+  }
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) ctr[C_OUT_N] = m;
     if (hctr && threadIdx.x < NCTR) hctr[threadIdx.x] = threadIdx.x == C_OUT_N ? m : ctr[threadIdx.x];
-    if (hctr && ts && threadIdx.x >= NCTR && threadIdx.x < NCTR + TS_WORDS) hctr[threadIdx.x] = ts[threadIdx.x - NCTR];
+    if (hctr && ts && threadIdx.x >= NCTR && threadIdx.x < NCTR + TS_END) hctr[threadIdx.x] = ts[threadIdx.x - NCTR];
     if (hctr) __threadfence_system();
   }
   for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (uint64_t)gridDim.x * NT) {
     const uint32_t x = idx[i];
     out[i] = EdgeOut{cu[x], cw[x], cs[x]};
   }
+  // the call's end (the last-dispatched workgroup's exit, approximately the
+  // last one), straight into the host copy: the call's final event orders it
+  if (hctr && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace nlp
