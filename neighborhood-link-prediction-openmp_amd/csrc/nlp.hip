@@ -159,6 +159,7 @@ struct nlp_graph {
   int ex_ipt = 1;                              // k_sp_expand survivors per thread (NLP_EX_IPT: 1, 2 or 4)
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
+  bool ord11 = false;                          // fused path: three 11-bit ordering passes (NLP_ORD11=1) instead of four 8-bit
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
@@ -166,7 +167,7 @@ struct nlp_graph {
   int hot_stage = -1;                          // sort path: stage timed as the dominant kernel (-1: the scoring
                                                // kernel k_sp_bucket / k_sp_scan<F_Runs>; NLP_HOT_STAGE)
   // co-resident workgroups of the persistent single-pass kernels (occupancy x CUs)
-  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_run = 256;
+  unsigned occ_surv = 256, occ_exp = 256, occ_p64 = 256, occ_p32 = 256, occ_p11 = 256, occ_run = 256;
   bool split_bucket = true;                    // NLP_BUCKET_FUSED=1: score inside k_sp_bucket (one block per bucket)
   int msd_force = 0;                           // NLP_MSD_PASSES: force 1 or 2 MSD passes (tests)
   int group_sort = 2;                          // NLP_GROUP_SORT: 0 k_sp_bucket sort-only, 1 k_sp_group, 2 group only after 2 MSD passes
@@ -507,6 +508,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
   if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
+  if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
   if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
@@ -551,6 +553,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
+    TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
     unsigned a = 0, b = 0;
     TRY(occ((const void*)k_sp_scan<F_Runs<true>, RN_IPT>, &a));
     TRY(occ((const void*)k_sp_scan<F_Runs<false>, RN_IPT>, &b));
@@ -1666,6 +1669,8 @@ struct SpBufs {
   ArenaZero zero;     // arena words reset per call (fused: counters, score-digit histograms, descriptors up to the
                       // survivor tiles; its ordering descriptors clean themselves)
   uint64_t ostride;                             // u32 onesweep descriptors per pass
+  uint64_t ostride11;                           // the same for 11-bit digits (the fused path's three passes)
+  bool ord11;                                   // fused path: three 11-bit passes
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
   int msd_shift;  // shift of the lowest MSD digit (the fine-bucket boundary in split mode)
@@ -1755,6 +1760,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   // fixed-capacity buckets: ~CAP/4 records per bucket on average (skew headroom),
   // CAP = 1024 or 2048, at most DX_MAXB buckets
   f.fused = false;
+  f.ord11 = false;
   f.caplog = 10;
   if (f.direct && g->fuse_runs) {
     const double est = std::max(1.0, hp_estimate(g, p));
@@ -1774,6 +1780,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
         TRY(wsget(ws, B_SP_OV0, std::max(capW, slots), &f.ov0));
         TRY(wsget(ws, B_SP_SEGCNT, std::max<uint64_t>((capW + RU_SEG - 1) / RU_SEG + 1, DX_MAXB), &f.segcnt));
         f.fused = true;
+        f.ord11 = g->ord11;
         f.caplog = cl;
         f.dbits = db;
         f.dshift = std::max(0, f.wbits + ubits - db);
@@ -1797,6 +1804,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, DX_MAXB);  // also k_sp_grouprun's buckets
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
+  f.ostride11 = tO * 2048;
   f.d_tick = SP_DESC;
   f.d_bcur = f.d_tick + SP_NTICK / 2;
   f.d_ts = f.d_bcur + DX_MAXB / 2;
@@ -1806,7 +1814,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.d_run = f.d_exp + tE + 1;
   f.d_rec = f.d_run + tR + 1;
   f.d_ord = f.d_rec + ((uint64_t)f.passes * f.ostride + 1) / 2;
-  f.arena_words = f.d_ord + (4 * f.ostride + 1) / 2;
+  f.arena_words = f.d_ord + (std::max(4 * f.ostride, 3 * f.ostride11) + 1) / 2;
   TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
   f.zero = ArenaZero{{0, 0, 0}, {f.arena_words, 0, 0}};
   if (f.fused) f.zero = ArenaZero{{0, SP_HORD, 0}, {SP_HREC, f.d_surv, 0}};
@@ -1951,13 +1959,15 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + GR_T - 1) / GR_T));
       if (f.fused) {
         const uint32_t nb = 1u << f.dbits;
-#define NLP_GROUPRUN(CL)                                                                                         \
-  hipLaunchKernelGGL(k_sp_grouprun<CL>, dim3(nb), dim3(GR_NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,  \
+#define NLP_GROUPRUN(CL, DB)                                                                                     \
+  hipLaunchKernelGGL((k_sp_grouprun<CL, DB>), dim3(nb), dim3(GR_NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,  \
                      (const uint64_t*)f.bkt, (const uint32_t*)(f.arena + f.d_bcur), f.cu, f.cw, f.cs, f.ok0,    \
                      f.ov0, f.segcnt, ctr, hord, (const uint64_t*)(f.arena + f.d_wsum),                        \
                      hot == s ? g->d_stamp : nullptr, ts)
-        if (f.caplog == 11) NLP_GROUPRUN(11);
-        else NLP_GROUPRUN(10);
+        if (f.caplog == 11 && f.ord11) NLP_GROUPRUN(11, 11);
+        else if (f.caplog == 11) NLP_GROUPRUN(11, 8);
+        else if (f.ord11) NLP_GROUPRUN(10, 11);
+        else NLP_GROUPRUN(10, 8);
 #undef NLP_GROUPRUN
       }
       else if (custom)
@@ -2012,12 +2022,29 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.fused && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts digits 1-3
+      if (f.fused && !f.ord11 && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts 1-3
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_BUCKETS>), grid(tO, g->occ_p32),
                            dim3(OS_NT), 0, st, (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
                            (const uint64_t*)&ctr[C_C], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
                            hot == s ? g->d_stamp : nullptr, GatherOut{}, hord + RS_BINS, (const uint32_t*)f.segcnt,
                            &ctr[C_C], (const uint64_t*)nullptr, 1u << f.dbits, f.caplog, ts + TS_HOT_OUT);
+      else if (f.fused && ps == 0)  // the same with 11-bit digits; this pass counts digits 1-2
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_BUCKETS, 11>), grid(tO, g->occ_p11),
+                           dim3(OS_NT), 0, st, (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
+                           (const uint64_t*)&ctr[C_C], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
+                           hot == s ? g->d_stamp : nullptr, GatherOut{}, hord + 2048, (const uint32_t*)f.segcnt,
+                           &ctr[C_C], (const uint64_t*)nullptr, 1u << f.dbits, f.caplog, ts + TS_HOT_OUT);
+      else if (f.fused && f.ord11 && ps < 3)  // 11-bit digits 1 and 2 (bits 11-21, 22-31)
+        hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>), grid(tO, g->occ_p11),
+                           dim3(OS_NT), 0, st, (const uint32_t*)(ps == 1 ? f.ok1 : f.ok0),
+                           (const uint32_t*)(ps == 1 ? f.ov1 : f.ov0), ps == 1 ? f.ok0 : f.ok1,
+                           ps == 1 ? f.ov0 : f.ov1, (const uint64_t*)&ctr[C_C], 11 * ps,
+                           (const uint32_t*)(hord + 2048 * ps), dord + (uint64_t)ps * f.ostride11, tick + TK_ORD + ps,
+                           err, hot == s ? g->d_stamp : nullptr, GatherOut{}, (uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (uint64_t*)nullptr, (const uint64_t*)nullptr, 0u, 0,
+                           (uint64_t*)nullptr, dord + (uint64_t)(ps - 1) * f.ostride11);
+      else if (f.fused && f.ord11)
+        return NLP_OK;  // three 11-bit passes
       else if (f.split && ps == 0)  // k_sp_runs' gapped candidates (and digit 0); this pass counts digits 1-3
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_SEGMENTS>), grid(tO, g->occ_p32), dim3(OS_NT), 0, st,
                            (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
@@ -2047,9 +2074,11 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       if (g->fuse_gather && !f.fused) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
-                         dim3(NT), 0, st, (const uint32_t*)f.ov0, (const uint32_t*)f.cu, (const uint32_t*)f.cw,
-                         (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev, (const uint64_t*)ts,
-                         f.fused ? dord + 3 * f.ostride : (uint32_t*)nullptr);
+                         dim3(NT), 0, st, (const uint32_t*)(f.ord11 ? f.ov1 : f.ov0), (const uint32_t*)f.cu,
+                         (const uint32_t*)f.cw, (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev,
+                         (const uint64_t*)ts,
+                         f.fused ? (f.ord11 ? dord + 2 * f.ostride11 : dord + 3 * f.ostride) : (uint32_t*)nullptr,
+                         f.ord11 ? 2048u : (uint32_t)RS_BINS);
     }
     TRY(hipGetLastError());
     return NLP_OK;
@@ -2279,7 +2308,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     // the fused path leaves its ordering descriptors zero; after any other call
     // (or a new arena) they are zeroed here, outside the captured pipeline
     if (sorted && sp.fused && g->ord_clean != sp.arena)
-      TRY(hipMemsetAsync(sp.arena + sp.d_ord, 0, 4 * sp.ostride * sizeof(uint32_t), st));
+      TRY(hipMemsetAsync(sp.arena + sp.d_ord, 0, std::max(4 * sp.ostride, 3 * sp.ostride11) * sizeof(uint32_t), st));
     g->ord_clean = nullptr;
     bool replayed = false;
     g->last_single = false;

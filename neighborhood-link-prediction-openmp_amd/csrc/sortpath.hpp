@@ -702,6 +702,7 @@ __global__ __launch_bounds__(NT) void k_sp_hist(const K* __restrict__ keys, cons
 
 // ---------------------------------------------------------------- onesweep pass
 constexpr int OS_NT = 1024;                      // threads per tile: 16 waves
+constexpr int OS_NT_C = OS_NT;
 constexpr int OS_NW = OS_NT / 64;
 constexpr int OS2_IPT = 4;                       // keys per thread
 constexpr int OS2_TILE = OS_NT * OS2_IPT;        // 4096 keys per tile
@@ -716,38 +717,59 @@ __device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive prefix of digit d over tiles [0, tile): sum of the nearest
-// predecessors' values back to (and including) the first inclusive prefix.
-// The window loads are unconditional (clamped to tile 0, whose descriptor is
-// always a prefix) so they issue back to back without branches.
-__device__ __forceinline__ uint32_t os_lookback(const uint32_t* desc, uint64_t tile, int d, uint32_t* err) {
-  uint32_t excl = 0, spins = 0;
-  int32_t j = (int32_t)tile - 1;  // tiles < 2^22: SP_MAX_N / OS2_TILE
-  while (j >= 0) {
-    // predecessors j, j-1, ..: only those that exist are read (32-bit offsets
-    // from the descriptor base); the window beyond tile 0 reads as a zero prefix
-    uint32_t x[OS_LBW];
+// Exclusive prefixes of ND digits d[k] over tiles [0, tile): per digit, the
+// sum of the nearest predecessors' values back to (and including) the first
+// inclusive prefix.  W predecessors per digit per round trip, all loads of a
+// round issued before any is inspected; only existing predecessors are read
+// (32-bit offsets from the descriptor base, nb descriptors per tile), the
+// window beyond tile 0 reads as a zero prefix.
+template <int ND, int W>
+__device__ __forceinline__ void os_lookback(const uint32_t* desc, uint32_t nb, uint64_t tile, const uint32_t (&d)[ND],
+                                            uint32_t (&excl)[ND], uint32_t* err) {
+  int32_t j[ND];  // tiles < 2^22: SP_MAX_N / OS2_TILE
+  bool done[ND];
 #pragma unroll
-    for (int r = 0; r < OS_LBW; ++r)
-      x[r] = r <= j ? ld_u32(&desc[(uint32_t)(j - r) * (uint32_t)RS_BINS + (uint32_t)d]) : OS_PFX;
-    int used = 0;
-    bool done = false, blocked = false;
+  for (int q = 0; q < ND; ++q) {
+    excl[q] = 0;
+    j[q] = (int32_t)tile - 1;
+    done[q] = j[q] < 0;
+  }
+  uint32_t spins = 0;
+  while (true) {
+    bool all = true;
 #pragma unroll
-    for (int r = 0; r < OS_LBW; ++r) {
-      if (!done && !blocked) {
-        const uint32_t st = x[r] >> 30;
-        if (st == 0) {
-          blocked = true;
-        } else {
-          excl += x[r] & OS_VAL;
-          ++used;
-          done = st == 2;
+    for (int q = 0; q < ND; ++q) all &= done[q];
+    if (all) break;
+    uint32_t x[ND][W];
+#pragma unroll
+    for (int q = 0; q < ND; ++q)
+#pragma unroll
+      for (int r = 0; r < W; ++r)
+        x[q][r] = (!done[q] && r <= j[q]) ? ld_u32(&desc[(uint32_t)(j[q] - r) * nb + d[q]]) : OS_PFX;
+    bool moved = false;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      if (done[q]) continue;
+      int used = 0;
+      bool fin = false, blocked = false;
+#pragma unroll
+      for (int r = 0; r < W; ++r) {
+        if (!fin && !blocked) {
+          const uint32_t st = x[q][r] >> 30;
+          if (st == 0) {
+            blocked = true;
+          } else {
+            excl[q] += x[q][r] & OS_VAL;
+            ++used;
+            fin = st == 2;
+          }
         }
       }
+      done[q] = fin;
+      j[q] -= used;
+      moved |= used > 0;
     }
-    if (done) break;
-    j -= used;
-    if (used == 0) {
+    if (!moved) {
       if (++spins > LB_SPIN_LIMIT) {
         atomicOr(err, 4u);
         break;
@@ -755,7 +777,31 @@ __device__ __forceinline__ uint32_t os_lookback(const uint32_t* desc, uint64_t t
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  return excl;
+}
+
+// Digit geometry of a counting pass with DB-bit digits: NB bins; the digit
+// histograms of the later passes in HC copies of HS words (digit p of a copy
+// at p NB); per-wave counts fit u16 at 11 bits (<= 64 IPT per wave).
+template <int DB>
+struct PassDigits {
+  static constexpr int NB = 1 << DB;
+  static constexpr int HC = DB == 8 ? HCOPIES : 4;
+  static constexpr uint32_t HS = DB == 8 ? HSTRIDE : 3u * (1u << DB);
+  static constexpr int ND = NB > OS_NT_C ? NB / OS_NT_C : 1;  // digits per owner thread
+  static constexpr int LBW = ND == 1 ? 64 : 32;                // look-back window per digit
+  static constexpr int NHD = (32 - DB + DB - 1) / DB;          // later digits of a 32-bit key
+  using CT = typename std::conditional<(DB > 8), uint16_t, uint32_t>::type;
+};
+template <int DB>
+__device__ __forceinline__ uint32_t* hist_copy_db(uint32_t* h) {
+  return h + (blockIdx.x % PassDigits<DB>::HC) * PassDigits<DB>::HS;
+}
+template <int DB>
+__device__ __forceinline__ uint32_t hist_total_db(const uint32_t* h, uint32_t i) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int c = 0; c < PassDigits<DB>::HC; ++c) s += h[c * PassDigits<DB>::HS + i];
+  return s;
 }
 
 // One stable counting pass on digit (key >> shift) & 255 (onesweep, after
@@ -835,7 +881,7 @@ __device__ __forceinline__ uint32_t os_block_scan(uint32_t x, uint32_t* s_w, uin
   return pre + inc - x;
 }
 
-template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false, int GAPPED = GAP_NONE>
+template <typename K, int IPT = OS2_IPT, bool GATHER = false, bool NEXT_HIST = false, int GAPPED = GAP_NONE, int DB = 8>
 __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    const uint64_t* __restrict__ d_n, int shift,
@@ -851,11 +897,17 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
                                                    uint32_t* __restrict__ clean_desc = nullptr) {
   constexpr int WT = 64 * IPT;
   constexpr int TILE = OS_NT * IPT;
+  using PD = PassDigits<DB>;
+  constexpr int NB = PD::NB, ND = PD::ND, NHD = PD::NHD;
+  constexpr uint32_t DMASK = NB - 1;
+  using CT = typename PD::CT;
   static_assert(!GAPPED || (RU_SEG % 64 == 0), "a wave substep must lie in one segment");
-  __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
-  __shared__ uint32_t s_base[RS_BINS];
-  __shared__ uint32_t s_nh[NEXT_HIST ? 3 : 1][NEXT_HIST ? RS_BINS : 1];
-  __shared__ uint32_t s_w[4];
+  static_assert(DB == 8 || sizeof(K) == 4, "11-bit digits: 32-bit keys");
+  __shared__ CT s_wcnt[OS_NW][NB];
+  __shared__ uint32_t s_base[NB];
+  __shared__ uint32_t s_dbase[DB == 8 ? 1 : NB];
+  __shared__ uint32_t s_nh[NEXT_HIST ? NHD : 1][NEXT_HIST ? NB : 1];
+  __shared__ uint32_t s_w[OS_NW];
   __shared__ uint32_t s_tile[2];
   __shared__ uint32_t s_pre[GAPPED == GAP_BUCKETS ? DX_MAXB + 1 : 1];
   __shared__ uint32_t s_w16[GAPPED == GAP_BUCKETS ? OS_NW : 1];
@@ -877,7 +929,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       sum += c[q];
     }
     uint64_t tot;
-    uint32_t run = os_block_scan(sum, s_w16, &tot);
+    uint32_t run = os_block_scan(sum, s_w16, &tot);  // (GAP_BUCKETS prologue)
 #pragma unroll
     for (uint32_t q = 0; q < PER; ++q) {
       const uint32_t b = (uint32_t)t * PER + q;
@@ -908,9 +960,25 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
   sp_stamp(stamp, true, 7);           // entry (diagnostics: ticket + digit bases until phase 0)
   if (t == 0) s_tile[0] = atomicAdd(tick, 1u);
   if (NEXT_HIST)
-    for (int i = t; i < 3 * RS_BINS; i += OS_NT) (&s_nh[0][0])[i] = 0;
+    for (int i = t; i < NHD * NB; i += OS_NT) (&s_nh[0][0])[i] = 0;
   uint64_t tot;
-  const uint32_t dbase = os_digit_scan(t < RS_BINS ? hist_total(ghist, t) : 0u, s_w, &tot);  // syncs
+  uint32_t dbase = 0;  // DB == 8: digit t's base (t < 256); else s_dbase
+  if (DB == 8) {
+    dbase = os_digit_scan(t < RS_BINS ? hist_total(ghist, t) : 0u, s_w, &tot);  // syncs
+  } else {  // thread t: digits [ND t, ND t + ND)
+    uint32_t c[ND], sum = 0;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      c[q] = hist_total_db<DB>(ghist, (uint32_t)t * ND + q);
+      sum += c[q];
+    }
+    uint32_t run = os_block_scan(sum, s_w, &tot);  // syncs
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      s_dbase[t * ND + q] = run;
+      run += c[q];
+    }
+  }
   const uint64_t lt = lane_mask_lt();
   bool first = true;
   for (int par = 0;; par ^= 1) {
@@ -918,7 +986,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
     if (tile >= ntiles) break;
     if (GAPPED && tile == 0 && t == 0 && tot_out) *tot_out = tot;
     sp_stamp(stamp, first, 0);
-    for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
+    for (int i = t; i < OS_NW * NB * (int)sizeof(CT) / 4; i += OS_NT) ((uint32_t*)&s_wcnt[0][0])[i] = 0;
     __syncthreads();
     if (t == 0) s_tile[par ^ 1] = atomicAdd(tick, 1u);  // claim the next tile meanwhile
     const uint64_t b0 = tile * TILE + (uint64_t)wv * WT + lane;
@@ -953,41 +1021,43 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
     // wave ranks: ballot multisplit + the wave's running digit counts
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const uint32_t d = (uint32_t)(k[i] >> shift) & 0xffu;
+      const uint32_t d = (uint32_t)(k[i] >> shift) & DMASK;
       dg[i] = d;
       uint64_t peers = __ballot(ok[i]);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
+      for (int b = 0; b < DB; ++b) {
         const uint64_t bb = __ballot((d >> b) & 1u);
         peers &= ((d >> b) & 1u) ? bb : ~bb;
       }
       const uint32_t before = ok[i] ? s_wcnt[wv][d] : 0u;
       rk[i] = before + (uint32_t)__popcll(peers & lt);
       wave_lds_sync();
-      if (ok[i] && (peers & lt) == 0) s_wcnt[wv][d] = before + (uint32_t)__popcll(peers);
+      if (ok[i] && (peers & lt) == 0) s_wcnt[wv][d] = (CT)(before + (uint32_t)__popcll(peers));
       wave_lds_sync();
     }
     __syncthreads();
     sp_stamp(stamp, first, 2);
-    // thread t < 256 owns digit t: wave prefix, aggregate, look-back, inclusive prefix
-    if (t < RS_BINS) {
-      uint32_t run = 0;
+    // thread t owns digits t, t + OS_NT, ..: wave prefix, aggregate, look-back, inclusive prefix
+    if (t < NB) {
+      uint32_t dd[ND], run[ND], excl[ND];
 #pragma unroll
-      for (int w = 0; w < OS_NW; ++w) {
-        const uint32_t c = s_wcnt[w][t];
-        s_wcnt[w][t] = run;
-        run += c;
+      for (int q = 0; q < ND; ++q) {
+        dd[q] = (uint32_t)t + (uint32_t)q * OS_NT;
+        run[q] = 0;
+#pragma unroll
+        for (int w = 0; w < OS_NW; ++w) {
+          const uint32_t c = s_wcnt[w][dd[q]];
+          s_wcnt[w][dd[q]] = (CT)run[q];
+          run[q] += c;
+        }
+        st_u32(desc + tile * NB + dd[q], (tile == 0 ? OS_PFX : OS_AGG) | run[q]);
       }
-      uint32_t* my = desc + tile * RS_BINS + t;
-      uint32_t excl = 0;
-      if (tile == 0) {
-        st_u32(my, OS_PFX | run);
-      } else {
-        st_u32(my, OS_AGG | run);
-        excl = os_lookback(desc, tile, t, err);
-        st_u32(my, OS_PFX | (excl + run));
+      os_lookback<ND, PD::LBW>(desc, (uint32_t)NB, tile, dd, excl, err);
+#pragma unroll
+      for (int q = 0; q < ND; ++q) {
+        if (tile != 0) st_u32(desc + tile * NB + dd[q], OS_PFX | (excl[q] + run[q]));
+        s_base[dd[q]] = (DB == 8 ? dbase : s_dbase[dd[q]]) + excl[q];
       }
-      s_base[t] = dbase + excl;
     }
     __syncthreads();
     sp_stamp(stamp, first, 3);
@@ -1003,22 +1073,22 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
         }
         if (NEXT_HIST) {
 #pragma unroll
-          for (int dd = 0; dd < 3; ++dd) atomicAdd(&s_nh[dd][(uint32_t)(k[i] >> (8 * dd + 8)) & 0xffu], 1u);
+          for (int dd = 0; dd < NHD; ++dd) atomicAdd(&s_nh[dd][(uint32_t)(k[i] >> (DB * dd + DB)) & DMASK], 1u);
         }
       }
     }
     // clean_desc: the previous pass's descriptors (same tile count), finished
     // with -- row `tile` back to zero for the next call (no zeroing pass)
-    if (clean_desc && t < RS_BINS) st_u32(&clean_desc[tile * RS_BINS + t], 0u);
+    for (int i = t; clean_desc && i < NB; i += OS_NT) st_u32(&clean_desc[tile * NB + i], 0u);
     __syncthreads();
     sp_stamp(stamp, first, 4);
     if (GATHER && tile == ntiles - 1) publish();
     first = false;
   }
   if (NEXT_HIST) {
-    uint32_t* hc = hist_copy(nhist);
-    for (int i = t; i < 3 * RS_BINS; i += OS_NT) {
-      const uint32_t c = s_nh[i / RS_BINS][i % RS_BINS];
+    uint32_t* hc = hist_copy_db<DB>(nhist);
+    for (int i = t; i < NHD * NB; i += OS_NT) {
+      const uint32_t c = s_nh[i / NB][i % NB];
       if (c) atomicAdd(&hc[i], c);
     }
   }
@@ -1738,7 +1808,7 @@ __device__ __forceinline__ uint32_t gr_scan(uint32_t x, uint32_t* s_w, uint32_t*
 // to the bucket's own slots [b CAP, b CAP + kcnt[b]) of the candidate columns,
 // in (u, w) order; the first ordering pass (k_sp_pass<.., GAP_BUCKETS>) reads
 // them densely through the prefix of kcnt.
-template <int CAPLOG>
+template <int CAPLOG, int DB>
 __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, float min_score, uint64_t ua,
                                                        int wbits, const uint64_t* __restrict__ rkey,
                                                        const uint32_t* __restrict__ bcnt,
@@ -1749,10 +1819,10 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
                                                        const uint64_t* __restrict__ wsum,
                                                        uint64_t* __restrict__ stamp, uint64_t* __restrict__ ts) {
   constexpr uint32_t CAP = 1u << CAPLOG;
-  static_assert(GR_NT == RS_BINS, "one digit-0 bin per thread");
+  constexpr uint32_t NB = 1u << DB;  // digit 0 of the order keys (the first ordering pass's digits)
   __shared__ uint64_t s_key[CAP];
   __shared__ uint16_t s_rs[CAP + 1];
-  __shared__ uint32_t s_oh[RS_BINS];
+  __shared__ uint32_t s_oh[NB];
   __shared__ uint32_t s_w[GR_NW];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
@@ -1767,7 +1837,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
     return;
   }
   const uint64_t start = (uint64_t)b << CAPLOG;
-  s_oh[t] = 0;
+  for (uint32_t i = t; i < NB; i += GR_NT) s_oh[i] = 0;
   sp_stamp(stamp, true, 4);
   if (m <= GR_NT) gr_sort<1>(rkey, start, m, s_key, t, stamp);
   else if (m <= 2 * GR_NT) gr_sort<2>(rkey, start, m, s_key, t, stamp);
@@ -1819,7 +1889,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
       const uint32_t k = ~score_key(sc);
       okey[o] = k;
       oval[o] = o;
-      atomicAdd(&s_oh[k & 0xffu], 1u);
+      atomicAdd(&s_oh[k & (NB - 1)], 1u);
       nnan += sc != sc;
     }
     K += kept;
@@ -1827,8 +1897,11 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
   if (t == 0) kcnt[b] = K;
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
   __syncthreads();
-  const uint32_t hc = s_oh[t];
-  if (hc) atomicAdd(&hist_copy(ohist)[t], hc);
+  uint32_t* hcp = hist_copy_db<DB>(ohist);
+  for (uint32_t i = t; i < NB; i += GR_NT) {
+    const uint32_t hc = s_oh[i];
+    if (hc) atomicAdd(&hcp[i], hc);
+  }
   sp_stamp(stamp, true, 3);
 }
 
@@ -2114,10 +2187,10 @@ __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ i
                                                   uint64_t k, EdgeOut* __restrict__ out,
                                                   uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr,
                                                   const uint64_t* __restrict__ ts,
-                                                  uint32_t* __restrict__ clean_desc = nullptr) {
+                                                  uint32_t* __restrict__ clean_desc = nullptr, uint32_t clean_nb = 0) {
   const uint64_t m = std::min<uint64_t>(ctr[C_C], k);
-  if (clean_desc) {  // the last ordering pass's descriptor rows back to zero (see k_sp_pass)
-    const uint64_t words = (ctr[C_C] + OS2_TILE - 1) / OS2_TILE * RS_BINS;
+  if (clean_desc) {  // the last ordering pass's descriptor rows (clean_nb words each) back to zero (see k_sp_pass)
+    const uint64_t words = (ctr[C_C] + OS2_TILE - 1) / OS2_TILE * clean_nb;
     for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < words; i += (uint64_t)gridDim.x * NT)
       clean_desc[i] = 0u;
   }
