@@ -241,6 +241,14 @@ inline bool debug_on() {
 
 // Wait for an event by polling: a blocking wait can add tens of microseconds
 // of wake-up latency to every call, which is a large share of a fast prediction.
+// The same for everything queued on a stream (a graph without an end event).
+hipError_t wait_stream(hipStream_t st) {
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q != hipErrorNotReady) return q;
+  }
+}
+
 hipError_t wait_event(hipEvent_t e) {
   for (;;) {
     const hipError_t q = hipEventQuery(e);
@@ -571,7 +579,7 @@ nlp_status new_graph(int device, nlp_graph** out) {
   g->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(&g->host_small, 64 * 8) != hipSuccess ||
-      hipHostMalloc(&g->host_ctr, (NCTR + TS_WORDS) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostMalloc(&g->host_ctr, HC_WORDS * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&g->host_ctr_dev, g->host_ctr, 0) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_DEVICE;
@@ -2073,7 +2081,8 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else {
       if (g->fuse_gather && !f.fused) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
-      hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (m + NT - 1) / NT))),
+      // one workgroup per CU at most: the last one to finish is found with one atomic each
+      hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(256, std::max<uint64_t>(1, (m + NT - 1) / NT))),
                          dim3(NT), 0, st, (const uint32_t*)(f.ord11 ? f.ov1 : f.ov0), (const uint32_t*)f.cu,
                          (const uint32_t*)f.cw, (const float*)f.cs, p.max_edges, out, ctr, g->host_ctr_dev,
                          (const uint64_t*)ts,
@@ -2117,7 +2126,7 @@ static const int EV_SEG3[3] = {0, 3, 4};     // sort grouping: pre | hot (scorin
 // nodes between the segments of the single graph, only at its start and end.
 template <class L>
 nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st, int mode, const void* copy_src,
-                     bool* replayed, L&& launch, bool stamps = false) {
+                     bool* replayed, L&& launch, bool stamps = false, bool seq_end = false) {
   *replayed = false;
   if (!g->use_graphs) return NLP_OK;
   const bool single = g->graph_single && mode != 0;  // the bucket grouping is captured in segments
@@ -2201,7 +2210,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
                                       NCTR * 8, hipMemcpyDeviceToHost) == hipSuccess;
         link(n);
       }
-      if (ok1) chain_ev(2);
+      if (ok1 && !seq_end) chain_ev(2);  // seq_end: the host polls the stream instead
       if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
       if (ok1) (void)hipGraphUpload(c.exec[0], st);  // stage the executable graph on the device once
       if (top) (void)hipGraphDestroy(top);
@@ -2314,9 +2323,15 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     g->last_single = false;
     if (hprof) t1 = now_us();
     const bool stamps = sorted && sp.split && g->hot_stage < 0;
+    // NLP_STREAM_WAIT=1: no end event node in the stamp-timed graph, the host
+    // polls the stream instead (measured equal on C2: the event node costs
+    // graph-launch time, stream polling costs completion latency)
+    static const bool stream_wait = getenv("NLP_STREAM_WAIT") && getenv("NLP_STREAM_WAIT")[0] == '1';
+    const bool gseq = stream_wait && sorted;
     if (sorted)
       s = run_graph(g, p, out, st, msd ? 1 + sp.msd_passes : 1, sp.arena, &replayed,
-                    [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps);
+                    [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps,
+                    stamps && gseq);
     else
       s = run_graph(g, p, out, st, 0, f.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
@@ -2327,7 +2342,8 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     }
     hipEvent_t* E = (replayed && g->last_single) ? g->gev : g->ev;
     if (hprof) t2 = now_us();
-    TRY(wait_event(E[2]));
+    if (gseq && stamps && replayed && g->last_single) TRY(wait_stream(st));
+    else TRY(wait_event(E[2]));
     if (hprof) t3 = now_us();
     const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;
     if (debug_on())

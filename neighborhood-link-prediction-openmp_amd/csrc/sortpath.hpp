@@ -130,6 +130,8 @@ __device__ __forceinline__ uint64_t lb_lookback_r(uint64_t* desc, uint64_t tile,
 // latest exit of the hot kernel; s_memrealtime ticks (100 MHz).  Minima are
 // kept as maxima of the complement so that a zeroed arena is the identity.
 enum { TS_FIRST = 0, TS_HOT_IN = 1, TS_HOT_OUT = 2, TS_END = 3, TS_WORDS = 4 };
+// host_ctr layout: [0, NCTR) counters, [NCTR, NCTR + TS_WORDS) stamps
+constexpr int HC_WORDS = NCTR + TS_WORDS;
 // Workgroup 0 only (dispatched first): thousands of same-address atomics
 // serialise for microseconds, and a workgroup's later loads wait behind its own.
 __device__ __forceinline__ void ts_enter(uint64_t* ts, int slot) {
@@ -2205,7 +2207,8 @@ __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ i
     out[i] = EdgeOut{cu[x], cw[x], cs[x]};
   }
   // the call's end (the last-dispatched workgroup's exit, approximately the
-  // last one), straight into the host copy: the call's final event orders it
+  // last one; finding the last one would take one same-address atomic per
+  // workgroup, ~0.1 us each, serialised), straight into the host copy
   if (hctr && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
     hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
 }
