@@ -15,6 +15,7 @@ There is no CPU fallback: without libnlp.so or a gfx950 device every call
 raises NlpError (the oracle under oracle/ is test infrastructure only).
 """
 import ctypes
+import operator
 import os
 
 import numpy as np
@@ -52,8 +53,11 @@ class Timing(ctypes.Structure):
                 ("hot_kernel", ctypes.c_uint32)]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        return dict(zip(_TIMING_FIELDS, _timing_get(self)))
 
+
+_TIMING_FIELDS = tuple(f for f, _ in Timing._fields_)
+_timing_get = operator.attrgetter(*_TIMING_FIELDS)
 
 EXPORTS = [
     "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
@@ -135,9 +139,15 @@ def _check_tensor(t, name, dtypes, device=None, min_numel=0):
         raise ValueError("%s too small: %d elements, need %d" % (name, t.numel(), min_numel))
 
 
+_EDGE_DTYPES = None
+
+
 def _edge_dtypes():
-    import torch
-    return (torch.int32, torch.uint32) if hasattr(torch, "uint32") else (torch.int32,)
+    global _EDGE_DTYPES
+    if _EDGE_DTYPES is None:
+        import torch
+        _EDGE_DTYPES = (torch.int32, torch.uint32) if hasattr(torch, "uint32") else (torch.int32,)
+    return _EDGE_DTYPES
 
 
 def _stream_ptr(stream, tensor=None):

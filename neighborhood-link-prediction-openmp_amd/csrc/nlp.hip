@@ -161,6 +161,7 @@ struct nlp_graph {
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
   bool ord11 = false;                          // fused path: three 11-bit ordering passes (NLP_ORD11=1) instead of four 8-bit
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
+  int exb_spt = 2;                             // k_sp_exbucket: survivors per thread (NLP_EXB_SPT 1, 2, 4)
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
   int dx_bits = 0;                             // direct buckets: forced width (NLP_DX_BITS, 0 = from dx_target)
@@ -516,6 +517,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
   if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
+  if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
   if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
@@ -1899,9 +1901,15 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       // survivors: known exactly with the degree-class index, else at most S
       const uint64_t nsv = f.dindex ? f.nv : S;
       if (f.fused) {
-        hipLaunchKernelGGL(k_sp_exbucket, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT - 1) / NT)), dim3(NT), 0, st,
-                           gv, ua, ub, f.wbits, f.survivors, f.dshift, f.dbits, f.caplog, f.bkt,
-                           (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts);
+        const int spt = g->exb_spt;
+#define NLP_EXBUCKET(SPT)                                                                                        \
+  hipLaunchKernelGGL(k_sp_exbucket<SPT>, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT * SPT - 1) / (NT * SPT))),  \
+                     dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, f.dshift, f.dbits, f.caplog, f.bkt,     \
+                     (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts, hot == s ? g->d_stamp : nullptr)
+        if (spt >= 4) NLP_EXBUCKET(4);
+        else if (spt == 2) NLP_EXBUCKET(2);
+        else NLP_EXBUCKET(1);
+#undef NLP_EXBUCKET
         TRY(hipGetLastError());
         return NLP_OK;
       }

@@ -1001,14 +1001,21 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       ok[i] = j < n;
       if (GAPPED == GAP_SEGMENTS && ok[i]) ok[i] = (uint32_t)(j % RU_SEG) < seg_cnt[j / RU_SEG];
       uint64_t sj = j;
-      if (GAPPED == GAP_BUCKETS && ok[i]) {  // the segment holding dense index j: last b with s_pre[b] <= j
-        uint32_t lo = 0, hi = nseg;  // s_pre[lo] <= j < s_pre[hi]
+      if (GAPPED == GAP_BUCKETS) {
+        // the segment holding dense index j (last b with s_pre[b] <= j): one
+        // search for the wave's first index (uniform), then a short walk per
+        // lane -- a wave's 64 consecutive indices cross few segment boundaries
+        const uint32_t j0 = (uint32_t)(b0 - lane + (uint64_t)i * 64);
+        uint32_t lo = 0, hi = nseg;  // s_pre[lo] <= j0 < s_pre[hi]
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= (uint32_t)j) lo = mid;
+          if (s_pre[mid] <= j0) lo = mid;
           else hi = mid;
         }
-        sj = ((uint64_t)lo << seglog) + ((uint32_t)j - s_pre[lo]);
+        if (ok[i]) {
+          while (s_pre[lo + 1] <= (uint32_t)j) ++lo;
+          sj = ((uint64_t)lo << seglog) + ((uint32_t)j - s_pre[lo]);
+        }
       }
       k[i] = ok[i] ? kin[sj] : (K)0;
       v[i] = ok[i] ? vin[sj] : 0u;
@@ -1653,29 +1660,37 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
 constexpr int GR_NT = 256;
 constexpr int GR_NW = GR_NT / 64;
 
+template <int SPT>  // survivors per thread: fewer workgroups contending for each bucket's cursor
 __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, uint64_t ub, int wbits,
                                                     const uint32_t* __restrict__ surv, int hshift, int dbits,
                                                     int caplog, uint64_t* __restrict__ rkey,
                                                     uint32_t* __restrict__ bcnt, uint64_t* __restrict__ ctr,
-                                                    uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts) {
+                                                    uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts,
+                                                    uint64_t* __restrict__ stamp = nullptr) {
   ts_enter(ts, TS_FIRST);
+  sp_stamp(stamp, true, 0);
   __shared__ uint32_t s_h[DX_MAXB];
   __shared__ uint64_t s_red[NWAVE];
   const int t = threadIdx.x;
   const uint32_t nb = 1u << dbits, bm = nb - 1, cap = 1u << caplog;
   const uint64_t n = ctr[C_NV];
-  if ((uint64_t)blockIdx.x * NT >= n) return;
+  if ((uint64_t)blockIdx.x * NT * SPT >= n) return;
   for (uint32_t i = t; i < nb; i += NT) s_h[i] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * NT + t;
-  ExSurv x;
-  if (i < n) ex_load(g, surv[i], x);
-  else ex_empty(g, x);
+  ExSurv x[SPT];
+#pragma unroll
+  for (int p = 0; p < SPT; ++p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * SPT + p) * NT + t;
+    if (i < n) ex_load(g, surv[i], x[p]);
+    else ex_empty(g, x[p]);
+  }
   uint64_t c = 0;
-  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
-    atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & bm], 1u);
-    ++c;
-  });
+#pragma unroll
+  for (int p = 0; p < SPT; ++p)
+    ex_enum(g, x[p], ua, ub, [&](uint32_t u, uint32_t w) {
+      atomicAdd(&s_h[(uint32_t)(ex_key(u, w, ua, wbits) >> hshift) & bm], 1u);
+      ++c;
+    });
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if (lane_id() == 0) s_red[wave_id()] = c;
@@ -1686,20 +1701,25 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
     for (int w = 0; w < NWAVE; ++w) tot += s_red[w];
     if (tot) atomicAdd((unsigned long long*)&wsum[blockIdx.x % WSUM_COPIES], (unsigned long long)tot);
   }
+  sp_stamp(stamp, true, 1);
   for (uint32_t b = t; b < nb; b += NT) {  // reserve: s_h[b] = this workgroup's first slot in bucket b
     const uint32_t h = s_h[b];
     s_h[b] = h ? atomicAdd(&bcnt[b], h) : 0u;
   }
   __syncthreads();
+  sp_stamp(stamp, true, 2);
   bool over = false;
-  ex_enum(g, x, ua, ub, [&](uint32_t u, uint32_t w) {
-    const uint64_t key = ex_key(u, w, ua, wbits);
-    const uint32_t b = (uint32_t)(key >> hshift) & bm;
-    const uint32_t pos = atomicAdd(&s_h[b], 1u);
-    if (pos < cap) rkey[((uint64_t)b << caplog) + pos] = key;
-    else over = true;
-  });
+#pragma unroll
+  for (int p = 0; p < SPT; ++p)
+    ex_enum(g, x[p], ua, ub, [&](uint32_t u, uint32_t w) {
+      const uint64_t key = ex_key(u, w, ua, wbits);
+      const uint32_t b = (uint32_t)(key >> hshift) & bm;
+      const uint32_t pos = atomicAdd(&s_h[b], 1u);
+      if (pos < cap) rkey[((uint64_t)b << caplog) + pos] = key;
+      else over = true;
+    });
   if (__ballot(over) && lane_id() == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
+  sp_stamp(stamp, true, 3);
 }
 
 // Ascending bitonic network over E * GR_NT keys, element i = t + r GR_NT in
@@ -1769,15 +1789,7 @@ __device__ __forceinline__ void gr_sort(const uint64_t* __restrict__ rkey, uint6
     const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
     k[r] = i < m ? rkey[start + i] : ~0ull;
   }
-  if (stamp) {  // diagnostics: the keys have arrived
-    uint64_t x = 0;
-#pragma unroll
-    for (int r = 0; r < E; ++r) x ^= k[r];
-    if (x == 0x5a5a5a5a5a5a5a5aull) s_key[0] = x;
-    sp_stamp(stamp, true, 5);
-  }
   bitonic_sort<E>(k, s_key, t);
-  sp_stamp(stamp, true, 6);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < E; ++r) s_key[t + r * GR_NT] = k[r];
@@ -1841,10 +1853,10 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
   const uint64_t start = (uint64_t)b << CAPLOG;
   for (uint32_t i = t; i < NB; i += GR_NT) s_oh[i] = 0;
   sp_stamp(stamp, true, 4);
-  if (m <= GR_NT) gr_sort<1>(rkey, start, m, s_key, t, stamp);
-  else if (m <= 2 * GR_NT) gr_sort<2>(rkey, start, m, s_key, t, stamp);
-  else if (CAP >= 4 * GR_NT && m <= 4 * GR_NT) gr_sort<(CAP >= 4 * GR_NT ? 4 : 1)>(rkey, start, m, s_key, t, stamp);
-  else if (CAP >= 8 * GR_NT) gr_sort<(CAP >= 8 * GR_NT ? 8 : 1)>(rkey, start, m, s_key, t, stamp);
+  if (m <= GR_NT) gr_sort<1>(rkey, start, m, s_key, t);
+  else if (m <= 2 * GR_NT) gr_sort<2>(rkey, start, m, s_key, t);
+  else if (CAP >= 4 * GR_NT && m <= 4 * GR_NT) gr_sort<(CAP >= 4 * GR_NT ? 4 : 1)>(rkey, start, m, s_key, t);
+  else if (CAP >= 8 * GR_NT) gr_sort<(CAP >= 8 * GR_NT ? 8 : 1)>(rkey, start, m, s_key, t);
   sp_stamp(stamp, true, 1);
   // run starts (blocked: thread t owns keys [t P, t P + P)) -> run ids -> start positions
   const uint32_t P = (m + GR_NT - 1) / GR_NT;
@@ -1881,8 +1893,13 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
       sc = score_basic(metric, ex ? 0u : c, g.deg[ru], g.deg[rw]);
       keep = !(sc <= min_score) && !f2_drop(g, ru, rw);  // NaN passes
     }
+    if (q0 == 0 && stamp) {  // diagnostics: the scoring loads have arrived
+      if (keep && sc == -12345.0f) s_w[0] = 1u;
+      sp_stamp(stamp, true, 5);
+    }
     uint32_t kept;
     const uint32_t pos = K + gr_scan(keep ? 1u : 0u, s_w, &kept);
+    if (q0 == 0) sp_stamp(stamp, true, 6);
     if (keep) {
       const uint32_t o = (uint32_t)start + pos;
       cu[o] = ru;
@@ -1896,6 +1913,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
     }
     K += kept;
   }
+  sp_stamp(stamp, true, 7);
   if (t == 0) kcnt[b] = K;
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
   __syncthreads();
