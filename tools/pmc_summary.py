@@ -1,6 +1,6 @@
 """Summarise tools/gpu_pmc.sh's counter passes into profiles/pmc_traffic.json.
 
-    python tools/pmc_summary.py gpurun_out/pmc <round-tag> [--config C2-soc-LiveJournal1]
+    python tools/pmc_summary.py gpurun_out/pmc <round-tag> [--config C2-soc-LiveJournal1] [--hot k_sp_grouprun]
 
 HBM bytes per launch, following MI355X_MICROARCH.md ("HBM [CDNA4]"):
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes (they do not fit one
@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
+KERNELS = ["k_sp_grouprun", "k_sp_exbucket", "k_sp_gather", "k_sp_arena_init", "k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
            "k_desc_keys_sel", "k_sel_hist"]
 
 
@@ -49,7 +49,10 @@ def main():
         config = sys.argv[sys.argv.index("--config") + 1]
     fetch = per_kernel(os.path.join(src, "p1"), "FETCH_SIZE")
     write = per_kernel(os.path.join(src, "p2"), "WRITE_SIZE")
-    out = {"config": config, "n_gpus": 1, "metric": "JAC", "hub": 4, "hot_kernel": "k_sp_runs",
+    hot = "k_sp_grouprun"
+    if "--hot" in sys.argv:
+        hot = sys.argv[sys.argv.index("--hot") + 1]
+    out = {"config": config, "n_gpus": 1, "metric": "JAC", "hub": 4, "hot_kernel": hot,
            "source": "profiles/%s_pmc (rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE, "
                      "bench.py --steps 5 --warmup 2); traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024" % tag,
            "kernels": {}}
