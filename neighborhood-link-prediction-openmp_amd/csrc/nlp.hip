@@ -161,6 +161,7 @@ struct nlp_graph {
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
   bool ord11 = false;                          // fused path: three 11-bit ordering passes (NLP_ORD11=1) instead of four 8-bit
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
+  bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
   int exb_spt = 2;                             // k_sp_exbucket: survivors per thread (NLP_EXB_SPT 1, 2, 4)
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
@@ -517,6 +518,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
   if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
+  if (const char* dl = getenv("NLP_DIRECT_LAUNCH")) {
+    g->direct_launch = dl[0] == '1';
+    if (g->direct_launch) g->use_graphs = false;
+  }
   if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
   if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
@@ -2105,8 +2110,10 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   // also splits scoring from selection
   const int lo[3] = {0, hot, hot + 1}, hi[3] = {hot, hot + 1, n_st};
   static const int ev_at[3] = {0, 3, 4};
-  // seg -1: direct launch with event records (captured segments carry none)
+  // seg -1: direct launch with event records (captured segments carry none);
+  // seg -2: direct launch without events (stamp-timed, the host polls the stream)
   auto mark = [&](int e) -> hipError_t { return seg == -1 ? hipEventRecord(g->ev[e], st) : hipSuccess; };
+  if (seg == -2) seg = -3;  // every segment, no marks
   for (int sg = 0; sg < 3; ++sg) {
     if (seg >= 0 && seg != sg) continue;
     TRY(mark(ev_at[sg]));
@@ -2344,13 +2351,17 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       s = run_graph(g, p, out, st, 0, f.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_fast(g, p, f, out, gs, seg); });
     if (s != NLP_OK) return s;
+    // NLP_DIRECT_LAUNCH=1 (stamp-timed sort path): kernels launched one by one,
+    // no graph and no events -- the GPU starts after the first launch and the
+    // later launches overlap the running kernels
+    const bool direct_nomark = stamps && g->direct_launch;
     if (!replayed) {
-      s = sorted ? launch_sp(g, p, sp, out, st, -1) : launch_fast(g, p, f, out, st, -1);
+      s = sorted ? launch_sp(g, p, sp, out, st, direct_nomark ? -2 : -1) : launch_fast(g, p, f, out, st, -1);
       if (s != NLP_OK) return s;
     }
     hipEvent_t* E = (replayed && g->last_single) ? g->gev : g->ev;
     if (hprof) t2 = now_us();
-    if (gseq && stamps && replayed && g->last_single) TRY(wait_stream(st));
+    if ((gseq && stamps && replayed && g->last_single) || direct_nomark) TRY(wait_stream(st));
     else TRY(wait_event(E[2]));
     if (hprof) t3 = now_us();
     const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;
@@ -2457,7 +2468,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (result) *result = out;
     if (t) {
       float a = 0, b = 0, hot = 0;
-      if (stamps && replayed && g->last_single) {
+      if (stamps && ((replayed && g->last_single) || direct_nomark)) {
         // the kernels' own stamps (10 ns ticks): first kernel entry, hot kernel
         // entry and end, the gather's exit -- no event nodes in the graph
         const uint64_t* ts = h + NCTR;
