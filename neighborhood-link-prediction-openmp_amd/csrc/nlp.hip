@@ -161,6 +161,7 @@ struct nlp_graph {
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
   bool ord11 = false;                          // fused path: three 11-bit ordering passes (NLP_ORD11=1) instead of four 8-bit
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
+  int gr_nt = GR_NT;                           // k_sp_grouprun threads per bucket (NLP_GR_NT=512)
   bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
   int exb_spt = 2;                             // k_sp_exbucket: survivors per thread (NLP_EXB_SPT 1, 2, 4)
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
@@ -522,6 +523,7 @@ nlp_status finish_graph(nlp_graph* g) {
     g->direct_launch = dl[0] == '1';
     if (g->direct_launch) g->use_graphs = false;
   }
+  if (const char* gt = getenv("NLP_GR_NT")) g->gr_nt = atoi(gt) == 512 ? 512 : GR_NT;
   if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
   if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
@@ -1980,16 +1982,25 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       const dim3 gr((unsigned)std::max<uint64_t>(1, (capW + GR_T - 1) / GR_T));
       if (f.fused) {
         const uint32_t nb = 1u << f.dbits;
-#define NLP_GROUPRUN(CL, DB)                                                                                     \
-  hipLaunchKernelGGL((k_sp_grouprun<CL, DB>), dim3(nb), dim3(GR_NT), 0, st, gv, p.metric, p.min_score, ua, f.wbits,  \
+#define NLP_GROUPRUN3(CL, DB, NTH)                                                                               \
+  hipLaunchKernelGGL((k_sp_grouprun<CL, DB, NTH>), dim3(nb), dim3(NTH), 0, st, gv, p.metric, p.min_score, ua,      \
+                     f.wbits,                                                                                    \
                      (const uint64_t*)f.bkt, (const uint32_t*)(f.arena + f.d_bcur), f.cu, f.cw, f.cs, f.ok0,    \
                      f.ov0, f.segcnt, ctr, hord, (const uint64_t*)(f.arena + f.d_wsum),                        \
                      hot == s ? g->d_stamp : nullptr, ts)
+#define NLP_GROUPRUN(CL, DB)                \
+  do {                                      \
+    if (g->gr_nt == 512)                    \
+      NLP_GROUPRUN3(CL, DB, 512);           \
+    else                                    \
+      NLP_GROUPRUN3(CL, DB, GR_NT);         \
+  } while (0)
         if (f.caplog == 11 && f.ord11) NLP_GROUPRUN(11, 11);
         else if (f.caplog == 11) NLP_GROUPRUN(11, 8);
         else if (f.ord11) NLP_GROUPRUN(10, 11);
         else NLP_GROUPRUN(10, 8);
 #undef NLP_GROUPRUN
+#undef NLP_GROUPRUN3
       }
       else if (custom)
         hipLaunchKernelGGL(k_sp_group<true>, gr, dim3(BK_NT), 0, st, (const uint64_t*)rk_m, (const uint32_t*)rv_m,

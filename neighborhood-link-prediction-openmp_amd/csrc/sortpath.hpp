@@ -1657,8 +1657,7 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
 // exclusion, metric, minScore, MAXFACTOR2 -- as k_sp_runs), and write the
 // candidates in (u, w) order into the bucket's own slots, counting digit 0 of
 // their order keys.
-constexpr int GR_NT = 256;
-constexpr int GR_NW = GR_NT / 64;
+constexpr int GR_NT = 256;  // k_sp_grouprun threads per bucket workgroup (default; 512 with NLP_GR_NT=512)
 
 template <int SPT>  // survivors per thread: fewer workgroups contending for each bucket's cursor
 __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, uint64_t ub, int wbits,
@@ -1727,20 +1726,20 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
 // GR_NT through LDS, j >= GR_NT are in the same thread.  One compare-exchange
 // is a 64-bit compare and two selects: keep the partner's key when it is on
 // the wanted side.
-template <int E>
+template <int E, int NTH>
 __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int t) {
-  constexpr uint32_t N = (uint32_t)GR_NT * E;
+  constexpr uint32_t N = (uint32_t)NTH * E;
   const int lane = t & 63;
 #pragma unroll 1
   for (uint32_t size = 2; size <= N; size <<= 1) {
 #pragma unroll 1
     for (uint32_t j = size >> 1; j > 0; j >>= 1) {
-      if (j >= (uint32_t)GR_NT) {  // partner in the same thread: element r ^ (j / GR_NT)
-        const uint32_t jr = j / GR_NT;
+      if (j >= (uint32_t)NTH) {  // partner in the same thread: element r ^ (j / NTH)
+        const uint32_t jr = j / NTH;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
           if (((uint32_t)r & jr) == 0) {
-            const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+            const uint32_t i = (uint32_t)t + (uint32_t)r * NTH;
             const bool asc = (i & size) == 0;
             const uint64_t x = k[r], y = k[r | jr];
             const bool sw = (x > y) == asc;
@@ -1754,10 +1753,10 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int 
       if (j >= 64) {
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < E; ++r) s[t + r * GR_NT] = k[r];
+        for (int r = 0; r < E; ++r) s[t + r * NTH] = k[r];
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < E; ++r) o[r] = s[(t ^ (int)j) + r * GR_NT];
+        for (int r = 0; r < E; ++r) o[r] = s[(t ^ (int)j) + r * NTH];
       } else {
         const int idx = (lane ^ (int)j) << 2;
 #pragma unroll
@@ -1770,7 +1769,7 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int 
       const bool upper = ((uint32_t)t & j) != 0;
 #pragma unroll
       for (int r = 0; r < E; ++r) {
-        const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+        const uint32_t i = (uint32_t)t + (uint32_t)r * NTH;
         // keep the minimum when (ascending block) == (lower element)
         const bool keep_min = ((i & size) != 0) == upper;
         k[r] = ((k[r] > o[r]) == keep_min) ? o[r] : k[r];
@@ -1779,24 +1778,25 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int 
   }
 }
 
-// the range's m <= E GR_NT keys, sorted, to s_key[0, m)
-template <int E>
+// the range's m <= E NTH keys, sorted, to s_key[0, m)
+template <int E, int NTH>
 __device__ __forceinline__ void gr_sort(const uint64_t* __restrict__ rkey, uint64_t start, uint32_t m,
                                         uint64_t* s_key, int t, uint64_t* stamp = nullptr) {
   uint64_t k[E];
 #pragma unroll
   for (int r = 0; r < E; ++r) {
-    const uint32_t i = (uint32_t)t + (uint32_t)r * GR_NT;
+    const uint32_t i = (uint32_t)t + (uint32_t)r * NTH;
     k[r] = i < m ? rkey[start + i] : ~0ull;
   }
-  bitonic_sort<E>(k, s_key, t);
+  bitonic_sort<E, NTH>(k, s_key, t);
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < E; ++r) s_key[t + r * GR_NT] = k[r];
+  for (int r = 0; r < E; ++r) s_key[t + r * NTH] = k[r];
   __syncthreads();
 }
 
-// exclusive scan over a GR_NT workgroup (s_w: GR_NW words); *total = the sum
+// exclusive scan over a NTH workgroup (s_w: (NTH / 64) words); *total = the sum
+template <int NTH>
 __device__ __forceinline__ uint32_t gr_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
   const int lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t inc = x;
@@ -1810,7 +1810,7 @@ __device__ __forceinline__ uint32_t gr_scan(uint32_t x, uint32_t* s_w, uint32_t*
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < GR_NW; ++w) {
+  for (int w = 0; w < (NTH / 64); ++w) {
     pre += w < wv ? s_w[w] : 0u;
     tot += s_w[w];
   }
@@ -1822,8 +1822,8 @@ __device__ __forceinline__ uint32_t gr_scan(uint32_t x, uint32_t* s_w, uint32_t*
 // to the bucket's own slots [b CAP, b CAP + kcnt[b]) of the candidate columns,
 // in (u, w) order; the first ordering pass (k_sp_pass<.., GAP_BUCKETS>) reads
 // them densely through the prefix of kcnt.
-template <int CAPLOG, int DB>
-__global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, float min_score, uint64_t ua,
+template <int CAPLOG, int DB, int NTH>
+__global__ __launch_bounds__(NTH) void k_sp_grouprun(GraphView g, int metric, float min_score, uint64_t ua,
                                                        int wbits, const uint64_t* __restrict__ rkey,
                                                        const uint32_t* __restrict__ bcnt,
                                                        uint32_t* __restrict__ cu, uint32_t* __restrict__ cw,
@@ -1837,7 +1837,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
   __shared__ uint64_t s_key[CAP];
   __shared__ uint16_t s_rs[CAP + 1];
   __shared__ uint32_t s_oh[NB];
-  __shared__ uint32_t s_w[GR_NW];
+  __shared__ uint32_t s_w[(NTH / 64)];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   ts_enter(ts, TS_HOT_IN);
@@ -1851,15 +1851,15 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
     return;
   }
   const uint64_t start = (uint64_t)b << CAPLOG;
-  for (uint32_t i = t; i < NB; i += GR_NT) s_oh[i] = 0;
+  for (uint32_t i = t; i < NB; i += NTH) s_oh[i] = 0;
   sp_stamp(stamp, true, 4);
-  if (m <= GR_NT) gr_sort<1>(rkey, start, m, s_key, t);
-  else if (m <= 2 * GR_NT) gr_sort<2>(rkey, start, m, s_key, t);
-  else if (CAP >= 4 * GR_NT && m <= 4 * GR_NT) gr_sort<(CAP >= 4 * GR_NT ? 4 : 1)>(rkey, start, m, s_key, t);
-  else if (CAP >= 8 * GR_NT) gr_sort<(CAP >= 8 * GR_NT ? 8 : 1)>(rkey, start, m, s_key, t);
+  if (m <= NTH) gr_sort<1, NTH>(rkey, start, m, s_key, t);
+  else if (m <= 2 * NTH) gr_sort<2, NTH>(rkey, start, m, s_key, t);
+  else if (CAP >= 4 * NTH && m <= 4 * NTH) gr_sort<(CAP >= 4 * NTH ? 4 : 1), NTH>(rkey, start, m, s_key, t);
+  else if (CAP >= 8 * NTH) gr_sort<(CAP >= 8 * NTH ? 8 : 1), NTH>(rkey, start, m, s_key, t);
   sp_stamp(stamp, true, 1);
   // run starts (blocked: thread t owns keys [t P, t P + P)) -> run ids -> start positions
-  const uint32_t P = (m + GR_NT - 1) / GR_NT;
+  const uint32_t P = (m + NTH - 1) / NTH;
   uint32_t R;
   {
     uint32_t ns = 0;
@@ -1867,7 +1867,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
       const uint32_t q = (uint32_t)t * P + r;
       ns += (q < m && (q == 0 || s_key[q - 1] != s_key[q])) ? 1u : 0u;
     }
-    uint32_t id = gr_scan(ns, s_w, &R);
+    uint32_t id = gr_scan<NTH>(ns, s_w, &R);
     for (uint32_t r = 0; r < P; ++r) {
       const uint32_t q = (uint32_t)t * P + r;
       if (q < m && (q == 0 || s_key[q - 1] != s_key[q])) s_rs[id++] = (uint16_t)q;
@@ -1876,10 +1876,10 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
     __syncthreads();
   }
   sp_stamp(stamp, true, 2);
-  // score the runs, GR_NT per round, compacting in run order
+  // score the runs, NTH per round, compacting in run order
   const uint64_t wmask = (1ull << wbits) - 1;
   uint32_t K = 0, nnan = 0;
-  for (uint32_t q0 = 0; q0 < R; q0 += GR_NT) {
+  for (uint32_t q0 = 0; q0 < R; q0 += NTH) {
     const uint32_t q = q0 + t;
     bool keep = false;
     uint32_t ru = 0, rw = 0;
@@ -1898,7 +1898,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
       sp_stamp(stamp, true, 5);
     }
     uint32_t kept;
-    const uint32_t pos = K + gr_scan(keep ? 1u : 0u, s_w, &kept);
+    const uint32_t pos = K + gr_scan<NTH>(keep ? 1u : 0u, s_w, &kept);
     if (q0 == 0) sp_stamp(stamp, true, 6);
     if (keep) {
       const uint32_t o = (uint32_t)start + pos;
@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(GR_NT) void k_sp_grouprun(GraphView g, int metric, 
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
   __syncthreads();
   uint32_t* hcp = hist_copy_db<DB>(ohist);
-  for (uint32_t i = t; i < NB; i += GR_NT) {
+  for (uint32_t i = t; i < NB; i += NTH) {
     const uint32_t hc = s_oh[i];
     if (hc) atomicAdd(&hcp[i], hc);
   }
