@@ -252,13 +252,20 @@ class Graph:
     def predict_device(self, metric, hub, max_edges, out, u_begin=0, u_end=UINT64_MAX, min_score=0.0, stream=None,
                        maxfactor2=0):
         """Device-output predict into `out` (torch int32 [>= max_edges, 3]).  Returns (count, timing)."""
-        _check_tensor(out, "out", _edge_dtypes(), self.device, 3 * int(max_edges))
-        t = Timing()
-        cnt = ctypes.c_uint64()
-        _check(lib().nlp_predict_device_ex(self._h, _metric(metric), int(hub), int(maxfactor2), float(min_score),
-                                           int(max_edges), int(u_begin), int(u_end), out.data_ptr(),
-                                           ctypes.byref(cnt), ctypes.byref(t), _stream_ptr(stream, out)),
-               "nlp_predict_device_ex")
+        # the per-call Python is part of every step: the output tensor's checks
+        # are remembered for the same tensor and size, the result structs reused
+        need = 3 * int(max_edges)
+        memo = (id(out), out.data_ptr(), need)
+        if getattr(self, "_out_ok", None) != memo:
+            _check_tensor(out, "out", _edge_dtypes(), self.device, need)
+            self._out_ok = memo
+        io = getattr(self, "_io", None)
+        if io is None:
+            t, cnt = Timing(), ctypes.c_uint64()
+            io = self._io = (t, cnt, ctypes.byref(cnt), ctypes.byref(t), lib().nlp_predict_device_ex)
+        t, cnt, rcnt, rt, fn = io
+        _check(fn(self._h, _metric(metric), int(hub), int(maxfactor2), float(min_score), int(max_edges), int(u_begin),
+                  int(u_end), out.data_ptr(), rcnt, rt, _stream_ptr(stream, out)), "nlp_predict_device_ex")
         return cnt.value, t.as_dict()
 
     def select_edges_device(self, edges_in, n, max_edges, out, stream=None):

@@ -134,6 +134,9 @@ struct nlp_graph {
   uint64_t* host_ctr_dev = nullptr;
   hipEvent_t ev[8] = {};
   hipEvent_t gev[5] = {};  // recorded only as event nodes of captured graphs
+  hipEvent_t gev_end = nullptr;  // end of a stamp-timed graph: no timestamp (NLP_END_MODE)
+  int end_mode = 1;              // stamp-timed graphs end with: 0 a timing event node, 1 a no-timing event node,
+                                 // 2 a no-timing event recorded on the stream after the launch
   bool last_single = false; // the last fast call replayed a single graph (timing in gev)
   Workspace ws;
   uint64_t wedge_budget = 0;
@@ -307,6 +310,7 @@ void destroy_graph(nlp_graph* g) {
     if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
   for (int i = 0; i < 5; ++i)
     if (g->gev[i]) (void)hipEventDestroy(g->gev[i]);
+  if (g->gev_end) (void)hipEventDestroy(g->gev_end);
   if (g->host_small) (void)hipHostFree(g->host_small);
   if (g->host_ctr) (void)hipHostFree(g->host_ctr);
   if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -603,6 +607,11 @@ nlp_status new_graph(int device, nlp_graph** out) {
       destroy_graph(g);
       return NLP_ERR_DEVICE;
     }
+  if (hipEventCreateWithFlags(&g->gev_end, hipEventDisableTiming) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  if (const char* em = getenv("NLP_END_MODE")) g->end_mode = std::min(2, std::max(0, atoi(em)));
   *out = g;
   return NLP_OK;
 }
@@ -2236,7 +2245,15 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
                                       NCTR * 8, hipMemcpyDeviceToHost) == hipSuccess;
         link(n);
       }
-      if (ok1 && !seq_end) chain_ev(2);  // seq_end: the host polls the stream instead
+      if (ok1 && !seq_end) {  // seq_end: the host polls the stream instead
+        if (stamps && g->end_mode == 1) {
+          hipGraphNode_t n = nullptr;
+          ok1 = hipGraphAddEventRecordNode(&n, top, prev ? &prev : nullptr, prev ? 1 : 0, g->gev_end) == hipSuccess;
+          link(n);
+        } else if (!(stamps && g->end_mode == 2)) {
+          chain_ev(2);
+        }
+      }
       if (ok1) ok1 = hipGraphInstantiate(&c.exec[0], top, nullptr, nullptr, 0) == hipSuccess;
       if (ok1) (void)hipGraphUpload(c.exec[0], st);  // stage the executable graph on the device once
       if (top) (void)hipGraphDestroy(top);
@@ -2278,6 +2295,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
   g->last_single = hit->single;
   if (hit->single) {
     TRY(hipGraphLaunch(hit->exec[0], st));
+    if (stamps && !seq_end && g->end_mode == 2) TRY(hipEventRecord(g->gev_end, st));
   } else {
     const int nseg = mode == 0 ? 4 : 3;
     const int* ev_before = mode == 0 ? EV_SEG4 : EV_SEG3;
@@ -2373,6 +2391,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     hipEvent_t* E = (replayed && g->last_single) ? g->gev : g->ev;
     if (hprof) t2 = now_us();
     if ((gseq && stamps && replayed && g->last_single) || direct_nomark) TRY(wait_stream(st));
+    else if (stamps && replayed && g->last_single && g->end_mode != 0) TRY(wait_event(g->gev_end));
     else TRY(wait_event(E[2]));
     if (hprof) t3 = now_us();
     const uint64_t* h = sorted ? (const uint64_t*)g->host_ctr : g->host_small;

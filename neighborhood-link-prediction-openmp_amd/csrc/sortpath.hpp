@@ -995,6 +995,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
     K k[IPT];
     uint32_t v[IPT], dg[IPT], rk[IPT];
     bool ok[IPT];
+    uint32_t seg_lo = 0;  // GAP_BUCKETS: the segment of the wave's first index
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
       const uint64_t j = b0 + (uint64_t)i * 64;
@@ -1003,16 +1004,20 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       uint64_t sj = j;
       if (GAPPED == GAP_BUCKETS) {
         // the segment holding dense index j (last b with s_pre[b] <= j): one
-        // search for the wave's first index (uniform), then a short walk per
-        // lane -- a wave's 64 consecutive indices cross few segment boundaries
-        const uint32_t j0 = (uint32_t)(b0 - lane + (uint64_t)i * 64);
-        uint32_t lo = 0, hi = nseg;  // s_pre[lo] <= j0 < s_pre[hi]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= j0) lo = mid;
-          else hi = mid;
+        // search for the wave's first index of the first substep (uniform),
+        // then short walks -- consecutive indices cross few segment boundaries
+        if (i == 0) {
+          const uint32_t j0 = (uint32_t)(b0 - lane);
+          uint32_t hi = nseg;  // s_pre[seg_lo] <= j0 < s_pre[hi]
+          seg_lo = 0;
+          while (hi - seg_lo > 1) {
+            const uint32_t mid = (seg_lo + hi) >> 1;
+            if (s_pre[mid] <= j0) seg_lo = mid;
+            else hi = mid;
+          }
         }
         if (ok[i]) {
+          uint32_t lo = seg_lo;
           while (s_pre[lo + 1] <= (uint32_t)j) ++lo;
           sj = ((uint64_t)lo << seglog) + ((uint32_t)j - s_pre[lo]);
         }
