@@ -146,6 +146,7 @@ struct nlp_graph {
   bool sort_lsd = false;                       // NLP_GROUPING=lsd: full LSD record sort (no MSD buckets)
   // degree-class index (sortpath.hpp): vertices of degree 1..DCAP grouped by degree
   uint32_t* vbydeg = nullptr;
+  uint64_t* sv_pack = nullptr;  // symmetric graphs: (deg v << 48 | off v) per vbydeg entry (k_sv_pack)
   std::vector<uint64_t> dstart;                // class d occupies [dstart[d], dstart[d + 1]) (class 1 at 0)
   bool use_dindex = true;                      // NLP_NO_DINDEX=1: always scan deg[] for survivors
   // the same index restricted to a source range (k_range_index; multi-GPU shards)
@@ -300,6 +301,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->keys) (void)hipFree(g->keys);
   if (g->deg) (void)hipFree(g->deg);
   if (g->vbydeg) (void)hipFree(g->vbydeg);
+  if (g->sv_pack) (void)hipFree(g->sv_pack);
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   if (g->efilt) (void)hipFree(g->efilt);
@@ -435,6 +437,12 @@ nlp_status finish_graph(nlp_graph* g) {
     hipLaunchKernelGGL(k_deg_class_scatter, dim3(grid_for(S)), dim3(NT), 0, st, (const uint32_t*)g->deg, S, cur,
                        g->vbydeg);
     TRY(hipGetLastError());
+    if (g->symmetric && nv > 0 && g->nnz < (1ull << SV_PACK_SHIFT)) {
+      TRY(hipMalloc(&g->sv_pack, nv * 8));
+      hipLaunchKernelGGL(k_sv_pack, dim3(grid_for(nv)), dim3(NT), 0, st, (const uint32_t*)g->vbydeg, nv,
+                         (const uint64_t*)g->off, (const uint32_t*)g->deg, g->sv_pack);
+      TRY(hipGetLastError());
+    }
     TRY(hipStreamSynchronize(st));
   }
   // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
@@ -1683,7 +1691,7 @@ struct SpBufs {
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
   uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
   uint64_t d_wsum;                              // WSUM_COPIES wedge-count copies (direct emission)
-  uint64_t d_bcur;                              // DX_MAXB u32 bucket cursors (direct emission)
+  uint64_t d_bcur;                              // DX_MAXB x EXB_SUB u32 bucket cursors (direct emission)
   uint64_t d_ts;                                // TS_WORDS u64 call-timing stamps (sortpath.hpp ts_enter)
   bool direct;    // count metrics, one MSD pass: k_sp_excount + k_sp_exemit + k_sp_group instead of
                   // k_sp_expand + MSD pass + k_sp_bucket
@@ -1796,8 +1804,8 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
       if (g->dx_bits) db = std::min(g->dx_bits, DX_MAXBITS);
       db = std::min(db, std::max(1, f.wbits + ubits));
       if (g->dx_bits || est / (double)(1u << db) <= (double)(1u << cl) / 4) {
-        const uint64_t slots = (uint64_t)1 << (db + cl);
-        TRY(wsget(ws, B_SP_BKT, slots, &f.bkt));
+        const uint64_t slots = (uint64_t)1 << (db + cl);  // candidate slots: one CAP range per bucket
+        TRY(wsget(ws, B_SP_BKT, slots * EXB_SUB, &f.bkt));   // record slots: EXB_SUB sub-buckets per bucket
         // the candidate columns are indexed by bucket slot
         TRY(wsget(ws, B_SP_CU, std::max(capW, slots), &f.cu));
         TRY(wsget(ws, B_SP_CW, std::max(capW, slots), &f.cw));
@@ -1833,7 +1841,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.ostride11 = tO * 2048;
   f.d_tick = SP_DESC;
   f.d_bcur = f.d_tick + SP_NTICK / 2;
-  f.d_ts = f.d_bcur + DX_MAXB / 2;
+  f.d_ts = f.d_bcur + DX_MAXB * EXB_SUB / 2;
   f.d_wsum = f.d_ts + TS_WORDS;
   f.d_surv = f.d_wsum + WSUM_COPIES;
   f.d_exp = f.d_surv + tS + 1;
@@ -1921,7 +1929,9 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
 #define NLP_EXBUCKET(SPT)                                                                                        \
   hipLaunchKernelGGL(k_sp_exbucket<SPT>, dim3((unsigned)std::max<uint64_t>(1, (nsv + NT * SPT - 1) / (NT * SPT))),  \
                      dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, f.dshift, f.dbits, f.caplog, f.bkt,     \
-                     (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts, hot == s ? g->d_stamp : nullptr)
+                     (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts,                             \
+                     (const uint64_t*)(f.survivors == g->vbydeg ? g->sv_pack : nullptr),                         \
+                     hot == s ? g->d_stamp : nullptr)
         if (spt >= 4) NLP_EXBUCKET(4);
         else if (spt == 2) NLP_EXBUCKET(2);
         else NLP_EXBUCKET(1);

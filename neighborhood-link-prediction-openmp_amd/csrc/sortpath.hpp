@@ -446,6 +446,34 @@ __device__ __forceinline__ uint64_t ex_count(const GraphView& g, const ExSurv& x
   return c;
 }
 
+// Symmetric graphs: the degree-class index's (deg v << 48 | off v) words
+// (k_sv_pack, built once per graph) give a survivor's row in the same round
+// trip as its id, and I(v) = N(v).
+constexpr int SV_PACK_SHIFT = 48;
+__global__ void k_sv_pack(const uint32_t* __restrict__ vbydeg, uint64_t n, const uint64_t* __restrict__ off,
+                          const uint32_t* __restrict__ deg, uint64_t* __restrict__ pack) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = vbydeg[i];
+    pack[i] = ((uint64_t)deg[v] << SV_PACK_SHIFT) | off[v];
+  }
+}
+
+__device__ __forceinline__ void ex_load_packed(const GraphView& g, uint32_t v, uint64_t pk, ExSurv& x) {
+  x.v = v;
+  x.d = (uint32_t)(pk >> SV_PACK_SHIFT);
+  x.a = pk & ((1ull << SV_PACK_SHIFT) - 1);
+  x.nin = x.d;
+  x.nv = g.keys + x.a;
+  x.reg = x.d <= EX_REG;
+  if (x.reg) {
+#pragma unroll
+    for (int q = 0; q < EX_REG; ++q) {
+      x.N[q] = q < (int)x.d ? x.nv[q] : 0u;
+      x.I[q] = x.N[q];
+    }
+  }
+}
+
 __device__ __forceinline__ uint64_t ex_key(uint32_t u, uint32_t w, uint64_t ua, int wbits) {
   return ((uint64_t)(u - ua) << wbits) | w;
 }
@@ -1663,6 +1691,10 @@ __global__ __launch_bounds__(BK_NT) void k_sp_group(const uint64_t* __restrict__
 // candidates in (u, w) order into the bucket's own slots, counting digit 0 of
 // their order keys.
 constexpr int GR_NT = 256;  // k_sp_grouprun threads per bucket workgroup (default; 512 with NLP_GR_NT=512)
+// Each bucket is split into EXB_SUB sub-buckets of CAP slots, workgroup w of
+// k_sp_exbucket reserving in sub-bucket w % EXB_SUB: a sub-bucket's cursor sees
+// 1/EXB_SUB of the workgroups (same-address atomics serialise).
+constexpr uint32_t EXB_SUB = 8;
 
 template <int SPT>  // survivors per thread: fewer workgroups contending for each bucket's cursor
 __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, uint64_t ub, int wbits,
@@ -1670,6 +1702,7 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
                                                     int caplog, uint64_t* __restrict__ rkey,
                                                     uint32_t* __restrict__ bcnt, uint64_t* __restrict__ ctr,
                                                     uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts,
+                                                    const uint64_t* __restrict__ pack,
                                                     uint64_t* __restrict__ stamp = nullptr) {
   ts_enter(ts, TS_FIRST);
   sp_stamp(stamp, true, 0);
@@ -1685,8 +1718,9 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
 #pragma unroll
   for (int p = 0; p < SPT; ++p) {
     const uint64_t i = ((uint64_t)blockIdx.x * SPT + p) * NT + t;
-    if (i < n) ex_load(g, surv[i], x[p]);
-    else ex_empty(g, x[p]);
+    if (i >= n) ex_empty(g, x[p]);
+    else if (pack) ex_load_packed(g, surv[i], pack[i], x[p]);
+    else ex_load(g, surv[i], x[p]);
   }
   uint64_t c = 0;
 #pragma unroll
@@ -1706,9 +1740,10 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
     if (tot) atomicAdd((unsigned long long*)&wsum[blockIdx.x % WSUM_COPIES], (unsigned long long)tot);
   }
   sp_stamp(stamp, true, 1);
-  for (uint32_t b = t; b < nb; b += NT) {  // reserve: s_h[b] = this workgroup's first slot in bucket b
+  const uint32_t sub = blockIdx.x % EXB_SUB;
+  for (uint32_t b = t; b < nb; b += NT) {  // reserve: s_h[b] = this workgroup's first slot in its sub-bucket of b
     const uint32_t h = s_h[b];
-    s_h[b] = h ? atomicAdd(&bcnt[b], h) : 0u;
+    s_h[b] = h ? atomicAdd(&bcnt[b * EXB_SUB + sub], h) : 0u;
   }
   __syncthreads();
   sp_stamp(stamp, true, 2);
@@ -1719,7 +1754,7 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
       const uint64_t key = ex_key(u, w, ua, wbits);
       const uint32_t b = (uint32_t)(key >> hshift) & bm;
       const uint32_t pos = atomicAdd(&s_h[b], 1u);
-      if (pos < cap) rkey[((uint64_t)b << caplog) + pos] = key;
+      if (pos < cap) rkey[((uint64_t)(b * EXB_SUB + sub) << caplog) + pos] = key;
       else over = true;
     });
   if (__ballot(over) && lane_id() == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
@@ -1786,12 +1821,20 @@ __device__ __forceinline__ void bitonic_sort(uint64_t (&k)[E], uint64_t* s, int 
 // the range's m <= E NTH keys, sorted, to s_key[0, m)
 template <int E, int NTH>
 __device__ __forceinline__ void gr_sort(const uint64_t* __restrict__ rkey, uint64_t start, uint32_t m,
-                                        uint64_t* s_key, int t, uint64_t* stamp = nullptr) {
+                                        uint64_t* s_key, int t, const uint32_t* sub_pre = nullptr,
+                                        int caplog = 0) {
   uint64_t k[E];
 #pragma unroll
   for (int r = 0; r < E; ++r) {
     const uint32_t i = (uint32_t)t + (uint32_t)r * NTH;
-    k[r] = i < m ? rkey[start + i] : ~0ull;
+    uint64_t slot = start + i;
+    if (sub_pre && i < m) {  // key i of the bucket: in sub-bucket q with sub_pre[q] <= i < sub_pre[q + 1]
+      uint32_t q = 0;
+#pragma unroll
+      for (uint32_t x = 1; x < EXB_SUB; ++x) q += sub_pre[x] <= i ? 1u : 0u;
+      slot = start + ((uint64_t)q << caplog) + (i - sub_pre[q]);
+    }
+    k[r] = i < m ? rkey[slot] : ~0ull;
   }
   bitonic_sort<E, NTH>(k, s_key, t);
   __syncthreads();
@@ -1848,20 +1891,28 @@ __global__ __launch_bounds__(NTH) void k_sp_grouprun(GraphView g, int metric, fl
   ts_enter(ts, TS_HOT_IN);
   sp_stamp(stamp, true, 0);
   if (b == 0 && t == 0) ctr[C_W] = ctr[C_WSORT] = wsum_total(wsum);  // k_sp_exbucket's wedge count
-  // after an over-full bucket the call is redone: every bucket reports empty
+  // after an over-full sub-bucket the call is redone: every bucket reports empty
   const bool abort = (ctr[C_FLAGS] & F_TOOBIG) != 0;
-  const uint32_t m = abort ? 0u : bcnt[b];
-  if (m == 0) {
-    if (t == 0) kcnt[b] = 0;
+  uint32_t pre[EXB_SUB + 1];  // the bucket's sub-bucket counts, prefix-summed (uniform loads)
+  pre[0] = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < EXB_SUB; ++q) pre[q + 1] = pre[q] + (abort ? 0u : bcnt[b * EXB_SUB + q]);
+  const uint32_t m = pre[EXB_SUB];
+  if (m == 0 || m > CAP) {  // a bucket beyond the workgroup's sort capacity: the call is redone
+    if (t == 0) {
+      kcnt[b] = 0;
+      if (m > CAP) atomicOr((unsigned long long*)&ctr[C_FLAGS], F_TOOBIG);
+    }
     return;
   }
-  const uint64_t start = (uint64_t)b << CAPLOG;
+  const uint64_t start = (uint64_t)b * EXB_SUB << CAPLOG;
   for (uint32_t i = t; i < NB; i += NTH) s_oh[i] = 0;
   sp_stamp(stamp, true, 4);
-  if (m <= NTH) gr_sort<1, NTH>(rkey, start, m, s_key, t);
-  else if (m <= 2 * NTH) gr_sort<2, NTH>(rkey, start, m, s_key, t);
-  else if (CAP >= 4 * NTH && m <= 4 * NTH) gr_sort<(CAP >= 4 * NTH ? 4 : 1), NTH>(rkey, start, m, s_key, t);
-  else if (CAP >= 8 * NTH) gr_sort<(CAP >= 8 * NTH ? 8 : 1), NTH>(rkey, start, m, s_key, t);
+  if (m <= NTH) gr_sort<1, NTH>(rkey, start, m, s_key, t, pre, CAPLOG);
+  else if (m <= 2 * NTH) gr_sort<2, NTH>(rkey, start, m, s_key, t, pre, CAPLOG);
+  else if (CAP >= 4 * NTH && m <= 4 * NTH)
+    gr_sort<(CAP >= 4 * NTH ? 4 : 1), NTH>(rkey, start, m, s_key, t, pre, CAPLOG);
+  else if (CAP >= 8 * NTH) gr_sort<(CAP >= 8 * NTH ? 8 : 1), NTH>(rkey, start, m, s_key, t, pre, CAPLOG);
   sp_stamp(stamp, true, 1);
   // run starts (blocked: thread t owns keys [t P, t P + P)) -> run ids -> start positions
   const uint32_t P = (m + NTH - 1) / NTH;
@@ -1906,7 +1957,7 @@ __global__ __launch_bounds__(NTH) void k_sp_grouprun(GraphView g, int metric, fl
     const uint32_t pos = K + gr_scan<NTH>(keep ? 1u : 0u, s_w, &kept);
     if (q0 == 0) sp_stamp(stamp, true, 6);
     if (keep) {
-      const uint32_t o = (uint32_t)start + pos;
+      const uint32_t o = (b << CAPLOG) + pos;  // the bucket's candidate slots
       cu[o] = ru;
       cw[o] = rw;
       cs[o] = sc;
