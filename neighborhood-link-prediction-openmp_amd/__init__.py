@@ -23,7 +23,7 @@ import numpy as np
 from . import build as _build
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnlp.so")
+LIB_PATH = os.environ.get("NLP_LIB_PATH") or os.path.join(HERE, "libnlp.so")  # NLP_LIB_PATH: a variant build (experiments)
 
 CN, JAC, SOR, SAL, HPI, HDI, LHN, AA, RA = range(9)
 METRICS = ["CN", "JAC", "SOR", "SAL", "HPI", "HDI", "LHN", "AA", "RA"]

@@ -244,7 +244,10 @@ __device__ __forceinline__ uint64_t merge_rank(P list, uint64_t lo, uint64_t hi,
 // MT_W: windows average ~0.4 MT_T keys on balanced shards (C2 x8: 404, none
 // beyond 2048; at 512 a third fall back to global searches, with 2048-entry
 // tiles a fifth).
-constexpr int MT_NT = NT, MT_PER = 4, MT_T = MT_NT * MT_PER, MT_G = 8, MT_W = 2048;
+#ifndef MERGE_MT_W
+#define MERGE_MT_W 2048
+#endif
+constexpr int MT_NT = NT, MT_PER = 4, MT_T = MT_NT * MT_PER, MT_G = 8, MT_W = MERGE_MT_W;
 static_assert((MT_W & (MT_W - 1)) == 0, "the branchless window search steps by powers of two");
 
 // Bounds of every (block r, tile x, block q), 4 words at bnd[4 * ((r * tiles + x) * nb + q)]:
