@@ -40,6 +40,8 @@ enum {
   NCTR = 16
 };
 constexpr uint64_t F_OVERFLOW = 1, F_TOOBIG = 2;
+// the counted ordering passes (k_sp_cpass) got more than CP_MAXT tiles: the call is redone with look-back passes
+constexpr uint64_t F_CPASS = 4;
 
 struct GraphView {
   const uint64_t* off;

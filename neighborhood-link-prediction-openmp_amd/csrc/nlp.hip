@@ -164,6 +164,10 @@ struct nlp_graph {
   bool fuse_gather = false;                    // the last ordering pass writes the edges (NLP_FUSE_GATHER=1; measured slower)
   bool direct_emit = true;                     // count metrics: records straight into MSD buckets (NLP_DIRECT=0: off)
   bool ord11 = false;                          // fused path: three 11-bit ordering passes (NLP_ORD11=1) instead of four 8-bit
+  double cp_off_w = 0;                         // wedge estimate of the last call whose counted passes overflowed
+  bool counted_force = false;
+  bool counted = true;                         // fused path: ordering passes 2-4 from per-tile digit counts (k_sp_cpass,
+                                               // no look-back) when the candidates fit CP_MAXT tiles (NLP_COUNTED=0: off)
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   int gr_nt = GR_NT;                           // k_sp_grouprun threads per bucket (NLP_GR_NT=512)
   bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
@@ -538,6 +542,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* gt = getenv("NLP_GR_NT")) g->gr_nt = atoi(gt) == 512 ? 512 : GR_NT;
   if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
   if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
+  if (const char* cp = getenv("NLP_COUNTED")) {  // 0: off, 2: whatever the estimate (tests the F_CPASS redo)
+    g->counted = cp[0] != '0';
+    g->counted_force = cp[0] == '2';
+  }
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
   if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
@@ -1689,6 +1697,7 @@ struct SpBufs {
   uint64_t* arena;
   uint64_t arena_words;
   uint64_t d_surv, d_exp, d_run, d_rec, d_ord;  // descriptor offsets in the arena (u64 words)
+  uint64_t d_cm;                                // counted passes: 4 count matrices of CP_MAXT x 256 u32 (after d_ord)
   uint64_t d_tick;                              // SP_NTICK u32 ticket counters (one per ticketed launch)
   uint64_t d_wsum;                              // WSUM_COPIES wedge-count copies (direct emission)
   uint64_t d_bcur;                              // DX_MAXB x EXB_SUB u32 bucket cursors (direct emission)
@@ -1705,6 +1714,8 @@ struct SpBufs {
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   uint64_t ostride11;                           // the same for 11-bit digits (the fused path's three passes)
   bool ord11;                                   // fused path: three 11-bit passes
+  bool counted;                                 // fused path: passes 2-4 are k_sp_cpass (tile digit counts from the
+                                                // pass before, count matrix p at d_cm; the last pass gathers)
   int wbits, passes;
   bool msd;       // one MSD pass on the top 8 key bits + k_sp_bucket (else: full LSD sort + k_sp_scan<F_Runs>)
   int msd_shift;  // shift of the lowest MSD digit (the fine-bucket boundary in split mode)
@@ -1838,6 +1849,11 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, DX_MAXB);  // also k_sp_grouprun's buckets
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
+  {  // counted passes when the candidates (<= wedges) should fit CP_MAXT tiles, unless a similar call overflowed
+    const double est = hp_estimate(g, p), cap = (double)CP_MAXT * OS2_TILE;  // est >= candidates, mostly
+    f.counted = f.fused && !f.ord11 && g->counted && (g->counted_force || est < cap) &&
+                !(g->cp_off_w > 0 && est > 0.5 * g->cp_off_w);
+  }
   f.ostride11 = tO * 2048;
   f.d_tick = SP_DESC;
   f.d_bcur = f.d_tick + SP_NTICK / 2;
@@ -1848,10 +1864,13 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.d_run = f.d_exp + tE + 1;
   f.d_rec = f.d_run + tR + 1;
   f.d_ord = f.d_rec + ((uint64_t)f.passes * f.ostride + 1) / 2;
-  f.arena_words = f.d_ord + (std::max(4 * f.ostride, 3 * f.ostride11) + 1) / 2;
+  f.d_cm = f.d_ord + (std::max(4 * f.ostride, 3 * f.ostride11) + 1) / 2;
+  f.arena_words = f.d_cm + 4 * (uint64_t)CP_MAXT * RS_BINS / 2;
   TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
   f.zero = ArenaZero{{0, 0, 0}, {f.arena_words, 0, 0}};
   if (f.fused) f.zero = ArenaZero{{0, SP_HORD, 0}, {SP_HREC, f.d_surv, 0}};
+  // counted passes: no score-digit histogram copies to reset (the tickets: the survivor scan's)
+  if (f.counted) f.zero = ArenaZero{{0, SP_DESC, 0}, {SP_HREC, f.d_surv, 0}};
   return NLP_OK;
 }
 
@@ -1892,6 +1911,14 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   uint32_t* hord = (uint32_t*)(f.arena + SP_HORD);
   uint32_t* drec = (uint32_t*)(f.arena + f.d_rec);
   uint32_t* dord = (uint32_t*)(f.arena + f.d_ord);
+  uint32_t* cmat = (uint32_t*)(f.arena + f.d_cm);  // counted passes: matrix j at cmat + j CP_M
+  constexpr uint64_t CP_M = (uint64_t)CP_MAXT * RS_BINS;
+  // bucket groups of the counted pass 0 over the buckets that can hold keys
+  // (the top bucket bits cover 2^ubits sources, the range only ub - ua of them)
+  const uint64_t nb_used = std::min<uint64_t>(
+      (uint64_t)1 << f.dbits, (((ub - ua - 1) << f.wbits | ((1ull << f.wbits) - 1)) >> f.dshift) + 1);
+  const uint32_t cp_g = (uint32_t)((nb_used + CP_MAXT - 1) / CP_MAXT);        // buckets per group (<= CP_MAXG)
+  const uint32_t cp_groups = (uint32_t)((nb_used + cp_g - 1) / cp_g);
   uint32_t* tick = (uint32_t*)(f.arena + f.d_tick);
   uint64_t* ts = f.arena + f.d_ts;
   const int P = f.msd ? f.msd_passes : f.passes;
@@ -1913,7 +1940,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
       CtrInit ci;
       for (int i = 0; i < NCTR; ++i) ci.v[i] = 0;
       ci.v[C_NV] = f.nv;
-      const uint64_t zw = (f.zero.hi[0] - f.zero.lo[0]) + (f.zero.hi[1] - f.zero.lo[1]);
+      const uint64_t zw = (f.zero.hi[0] - f.zero.lo[0]) + (f.zero.hi[1] - f.zero.lo[1]) + (f.zero.hi[2] - f.zero.lo[2]);
       hipLaunchKernelGGL(k_sp_arena_init, dim3((unsigned)std::min<uint64_t>(1024, (zw + NT - 1) / NT)), dim3(NT), 0, st,
                          f.arena, f.zero, ci);
     } else if (s == 1) {
@@ -2005,8 +2032,8 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
   hipLaunchKernelGGL((k_sp_grouprun<CL, DB, NTH>), dim3(nb), dim3(NTH), 0, st, gv, p.metric, p.min_score, ua,      \
                      f.wbits,                                                                                    \
                      (const uint64_t*)f.bkt, (const uint32_t*)(f.arena + f.d_bcur), f.cu, f.cw, f.cs, f.ok0,    \
-                     f.ov0, f.segcnt, ctr, hord, (const uint64_t*)(f.arena + f.d_wsum),                        \
-                     hot == s ? g->d_stamp : nullptr, ts)
+                     f.ov0, f.segcnt, ctr, f.counted ? cmat : hord, (const uint64_t*)(f.arena + f.d_wsum),    \
+                     hot == s ? g->d_stamp : nullptr, ts, f.counted ? cp_g : 0u)
 #define NLP_GROUPRUN(CL, DB)                \
   do {                                      \
     if (g->gr_nt == 512)                    \
@@ -2073,7 +2100,34 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.fused && !f.ord11 && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts 1-3
+      if (f.counted && ps == 0) {  // bucket groups of k_sp_grouprun's candidates (it counted digit 0 per group)
+        hipLaunchKernelGGL(k_sp_cpass0, dim3(cp_groups), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
+                           (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
+                           cp_g, f.caplog, (const uint32_t*)cmat, cmat + CP_M, f.ok1, (uint64_t*)f.rk0, f.ov1, ctr,
+                           ts + TS_HOT_OUT, hot == s ? g->d_stamp : nullptr);
+      } else if (f.counted) {  // pass ps from matrix ps; cleans matrix ps - 1
+        const uint32_t* m_in = cmat + (uint64_t)ps * CP_M;
+        uint32_t* const m_old = cmat + (uint64_t)(ps - 1) * CP_M;
+        const uint32_t rows_old = ps == 1 ? cp_groups : 0u;  // matrix 0 has a row per bucket group
+        // matrix 3 (read by every tile of the last pass, so not cleaned there) is zeroed by pass 1
+        uint32_t* const m_last = ps == 1 ? cmat + 3 * CP_M : nullptr;
+        // payload ping-pong: A = (ok1, rk0, ov1) after passes 0 and 2, B = (ok0, rk1, ov0) after pass 1
+        const uint32_t* kA = f.ok1; const uint64_t* uwA = (const uint64_t*)f.rk0; const uint32_t* sA = f.ov1;
+        if (ps == 1)
+          hipLaunchKernelGGL(k_sp_cpass<true>, dim3(CP_MAXT), dim3(OS_NT), 0, st, kA, uwA, sA, f.ok0,
+                             (uint64_t*)f.rk1, f.ov0, (const uint64_t*)&ctr[C_C], 8, m_in, cmat + 2 * CP_M, m_old,
+                             rows_old, hot == s ? g->d_stamp : nullptr, GatherOut{}, m_last);
+        else if (ps == 2)
+          hipLaunchKernelGGL(k_sp_cpass<true>, dim3(CP_MAXT), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
+                             (const uint64_t*)f.rk1, (const uint32_t*)f.ov0, f.ok1, (uint64_t*)f.rk0, f.ov1,
+                             (const uint64_t*)&ctr[C_C], 16, m_in, cmat + 3 * CP_M, m_old, rows_old,
+                             hot == s ? g->d_stamp : nullptr, GatherOut{});
+        else  // the last pass writes the caller's edges and publishes the counters
+          hipLaunchKernelGGL((k_sp_cpass<false, true>), dim3(CP_MAXT), dim3(OS_NT), 0, st, kA, uwA, sA,
+                             (uint32_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr, (const uint64_t*)&ctr[C_C], 24,
+                             m_in, (uint32_t*)nullptr, m_old, rows_old, hot == s ? g->d_stamp : nullptr,
+                             GatherOut{nullptr, nullptr, nullptr, p.max_edges, out, ctr, g->host_ctr_dev, ts});
+      } else if (f.fused && !f.ord11 && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts 1-3
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_BUCKETS>), grid(tO, g->occ_p32),
                            dim3(OS_NT), 0, st, (const uint32_t*)f.ok0, (const uint32_t*)f.ov0, f.ok1, f.ov1,
                            (const uint64_t*)&ctr[C_C], 0, (const uint32_t*)hord, dord, tick + TK_ORD, err,
@@ -2122,7 +2176,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)nullptr, (uint64_t*)nullptr, (const uint64_t*)nullptr, 0u, 0,
                            (uint64_t*)nullptr, f.fused ? dord + (uint64_t)(ps - 1) * f.ostride : (uint32_t*)nullptr);
     } else {
-      if (g->fuse_gather && !f.fused) return NLP_OK;  // done by the last ordering pass
+      if ((g->fuse_gather && !f.fused) || f.counted) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       // one workgroup per CU at most: the last one to finish is found with one atomic each
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(256, std::max<uint64_t>(1, (m + NT - 1) / NT))),
@@ -2371,7 +2425,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     // the fused path leaves its ordering descriptors zero; after any other call
     // (or a new arena) they are zeroed here, outside the captured pipeline
     if (sorted && sp.fused && g->ord_clean != sp.arena)
-      TRY(hipMemsetAsync(sp.arena + sp.d_ord, 0, std::max(4 * sp.ostride, 3 * sp.ostride11) * sizeof(uint32_t), st));
+      TRY(hipMemsetAsync(sp.arena + sp.d_ord, 0, (sp.arena_words - sp.d_ord) * sizeof(uint64_t), st));
     g->ord_clean = nullptr;
     bool replayed = false;
     g->last_single = false;
@@ -2383,7 +2437,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     static const bool stream_wait = getenv("NLP_STREAM_WAIT") && getenv("NLP_STREAM_WAIT")[0] == '1';
     const bool gseq = stream_wait && sorted;
     if (sorted)
-      s = run_graph(g, p, out, st, msd ? 1 + sp.msd_passes : 1, sp.arena, &replayed,
+      s = run_graph(g, p, out, st, (msd ? 1 + sp.msd_passes : 1) + (sp.counted ? 16 : 0), sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps,
                     stamps && gseq);
     else
@@ -2494,6 +2548,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (sorted && msd && (h[C_FLAGS] & F_TOOBIG) && h[C_W] <= g->wedge_budget) {
       if (sp.split && sp.msd_passes == 1) msd_passes = 2;
       else msd = false;
+      continue;
+    }
+    if (sorted && sp.counted && (h[C_FLAGS] & F_CPASS)) {  // more than CP_MAXT candidate tiles: look-back passes
+      g->cp_off_w = est_w;
       continue;
     }
     if (sorted && sp.fused && !(h[C_FLAGS] >> 32)) g->ord_clean = sp.arena;  // self-cleaned (or never written)

@@ -888,6 +888,10 @@ __device__ __forceinline__ uint32_t os_digit_scan(uint32_t x, uint32_t* s_w, uin
 }
 
 enum { GAP_NONE = 0, GAP_SEGMENTS = 1, GAP_BUCKETS = 2 };
+// Counted passes (k_sp_cpass): at most CP_MAXT tiles of OS2_TILE keys, so the
+// per-tile digit counts of a pass fit one LDS matrix of u16 pairs.
+constexpr int CP_MAXT = 128;
+constexpr int CP_THW = CP_MAXT * 256 / 2;
 // Exclusive scan of one value per thread over an OS_NT workgroup (s_w: OS_NW
 // words); also returns the total.
 __device__ __forceinline__ uint32_t os_block_scan(uint32_t x, uint32_t* s_w, uint64_t* total) {
@@ -1134,6 +1138,304 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       if (c) atomicAdd(&hc[i], c);
     }
   }
+}
+
+// ---------------------------------------------------------------- counted passes
+// The fused path's four ordering passes without look-back (round 2).  Each
+// pass reads, instead of a look-back, a count matrix that the kernel before it
+// produced: m[tile][digit] = the keys of input tile `tile` with digit `digit`.
+// A tile's base for digit d is (sum over d' < d of the digit totals) + (digit
+// d's counts in the tiles before it): tiles share no descriptor, no ticket and
+// wait on nothing, so any grid size and dispatch order works.
+//
+//   k_sp_grouprun   counts digit 0 per bucket group into m0
+//   k_sp_cpass0     tile = a group of G consecutive buckets (their slots, in bucket
+//                   order = (u, w) order); counts digit 1 per output tile (m1)
+//   k_sp_cpass x3   tile = OS2_TILE consecutive keys; passes 1 and 2 count the
+//                   next digit per output tile (m2, m3); pass 3 writes the
+//                   caller's edges (GATHER) and publishes the counters
+//
+// The keys travel with their payload (u << 32 | w, score bits), so the last
+// pass writes the edges without a random gather of candidate columns.  The
+// per-output-tile counts are kept in LDS as u16 pairs (a bin holds at most
+// OS2_TILE keys) and flushed with one atomic per non-zero bin, which bounds the
+// output to CP_MAXT tiles: beyond it k_sp_cpass0 raises F_CPASS, every later
+// pass returns at once, and the host redoes the call with look-back passes.
+// Cleaning: pass 1 zeroes m0, pass 2 m1, pass 3 m2 (row = its workgroup,
+// before any early exit); m3 -- read by every tile of the last pass -- is
+// zeroed by pass 1 of the next call (all CP_MAXT rows), before pass 2 counts
+// into it.
+constexpr int CP_MAXG = 32;  // buckets per group (DX_MAXB / CP_MAXT)
+
+// Digit bases of tile `tile` of `ntiles` from the count matrix m: s_base[d] =
+// (totals of the digits below d) + (digit d in tiles < tile); returns the key
+// total n.  All threads of an OS_NT workgroup; ends with a barrier.
+__device__ __forceinline__ uint64_t cp_bases(const uint32_t* __restrict__ m, uint32_t ntiles, uint32_t tile,
+                                             uint32_t (&s_part)[2][OS_NT / RS_BINS][RS_BINS], uint32_t* s_base,
+                                             uint32_t* s_w) {
+  constexpr uint32_t Q = OS_NT / RS_BINS;
+  const int t = threadIdx.x;
+  {  // thread t: digit t % 256 over the tiles r = t / 256 (mod Q), all loads in one round trip
+    constexpr int R = CP_MAXT / Q;
+    const uint32_t d = (uint32_t)t % RS_BINS, q = (uint32_t)t / RS_BINS;
+    uint32_t c[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t r = q + (uint32_t)i * Q;
+      c[i] = m[(r < ntiles ? r : 0u) * RS_BINS + d];  // ntiles >= 1
+    }
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t r = q + (uint32_t)i * Q;
+      total += r < ntiles ? c[i] : 0u;
+      before += r < tile ? c[i] : 0u;
+    }
+    s_part[0][q][d] = before;
+    s_part[1][q][d] = total;
+  }
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  if (t < RS_BINS) {
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+      before += s_part[0][q][t];
+      total += s_part[1][q][t];
+    }
+  }
+  uint64_t n;
+  const uint32_t dbase = os_digit_scan(total, s_w, &n);  // syncs
+  if (t < RS_BINS) s_base[t] = dbase + before;
+  __syncthreads();
+  return n;
+}
+
+// Ballot-multisplit ranks of IPT keys per lane (wave wv owns 64 IPT
+// consecutive keys): rk = rank among the wave's earlier keys of the same digit;
+// s_wcnt[wv][d] = the wave's count of digit d (zeroed by the caller).
+template <int IPT>
+__device__ __forceinline__ void cp_rank(const uint32_t (&k)[IPT], const bool (&ok)[IPT], int shift,
+                                        uint32_t (&dg)[IPT], uint32_t (&rk)[IPT], uint32_t (*s_wcnt)[RS_BINS]) {
+  const int wv = wave_id();
+  const uint64_t lt = lane_mask_lt();
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t d = (k[i] >> shift) & 255u;
+    dg[i] = d;
+    uint64_t peers = __ballot(ok[i]);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bb = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    const uint32_t pre = ok[i] ? s_wcnt[wv][d] : 0u;
+    rk[i] = pre + (uint32_t)__popcll(peers & lt);
+    wave_lds_sync();
+    if (ok[i] && (peers & lt) == 0) s_wcnt[wv][d] = pre + (uint32_t)__popcll(peers);
+    wave_lds_sync();
+  }
+}
+
+// Wave prefixes of digit t (t < 256): s_wcnt[w][t] <- keys of digit t in
+// waves < w; returns the tile's count of digit t.
+__device__ __forceinline__ uint32_t cp_wave_prefix(uint32_t (*s_wcnt)[RS_BINS], int t) {
+  uint32_t run = 0;
+#pragma unroll
+  for (int w = 0; w < OS_NW; ++w) {
+    const uint32_t c = s_wcnt[w][t];
+    s_wcnt[w][t] = run;
+    run += c;
+  }
+  return run;
+}
+
+// Count of (output tile, next digit) of one placed key, into the LDS u16 pairs.
+__device__ __forceinline__ void cp_count_next(uint32_t* s_th, uint32_t pos, uint32_t key, int nshift) {
+  const uint32_t bin = (pos / OS2_TILE) * RS_BINS + ((key >> nshift) & 255u);
+  atomicAdd(&s_th[bin >> 1], 1u << ((bin & 1u) * 16));  // a bin holds <= OS2_TILE keys: no carry
+}
+__device__ __forceinline__ void cp_flush_next(const uint32_t* s_th, uint32_t ntiles, uint32_t* __restrict__ hout) {
+  for (uint32_t i = threadIdx.x; i < ntiles * (RS_BINS / 2); i += OS_NT) {
+    const uint32_t c = s_th[i];
+    if (c & 0xffffu) atomicAdd(&hout[2 * i], c & 0xffffu);
+    if (c >> 16) atomicAdd(&hout[2 * i + 1], c >> 16);
+  }
+}
+
+// Pass 0: tile = bucket group `blockIdx` (buckets [G blockIdx, G blockIdx +
+// G), gridDim = groups <= CP_MAXT, G <= CP_MAXG; the host spreads the groups
+// over the buckets that can hold keys); its keys in chunks of OS2_TILE, each
+// chunk ranked and placed behind the previous one (stable).  The candidate
+// count (the matrix total) goes to ctr[C_C].
+__global__ __launch_bounds__(OS_NT) void k_sp_cpass0(const uint32_t* __restrict__ okey, const uint32_t* __restrict__ cu,
+                                                     const uint32_t* __restrict__ cw, const float* __restrict__ cs,
+                                                     const uint32_t* __restrict__ kcnt, uint32_t G, int caplog,
+                                                     const uint32_t* __restrict__ m0, uint32_t* __restrict__ m1,
+                                                     uint32_t* __restrict__ kout, uint64_t* __restrict__ uwout,
+                                                     uint32_t* __restrict__ sout, uint64_t* __restrict__ ctr,
+                                                     uint64_t* __restrict__ end_mark, uint64_t* __restrict__ stamp) {
+  constexpr int IPT = OS2_IPT, WT = 64 * IPT, TILE = OS2_TILE;
+  __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
+  __shared__ uint32_t s_part[2][OS_NT / RS_BINS][RS_BINS];
+  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_w[OS_NW];
+  __shared__ uint32_t s_gp[CP_MAXG + 1];
+  __shared__ uint32_t s_th[CP_THW];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint32_t group = blockIdx.x;
+  ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel)
+  sp_stamp(stamp, true, 7);
+  if (wv == 0) {  // the group's bucket counts, prefix-summed (G <= 64)
+    const uint32_t c = (uint32_t)lane < G ? kcnt[group * G + lane] : 0u;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if ((uint32_t)lane <= G && lane <= CP_MAXG) s_gp[lane] = inc - c;
+  }
+  const uint64_t n = cp_bases(m0, gridDim.x, group, s_part, s_base, s_w);  // syncs (s_gp too)
+  sp_stamp(stamp, true, 0);
+  if (group == 0 && t == 0) ctr[C_C] = n;
+  const uint32_t nout = (uint32_t)((n + TILE - 1) / TILE);
+  if (nout > (uint32_t)CP_MAXT) {  // beyond the counted passes: redone with look-back passes
+    if (group == 0 && t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], (unsigned long long)F_CPASS);
+    return;
+  }
+  for (uint32_t i = t; i < nout * (RS_BINS / 2); i += OS_NT) s_th[i] = 0;
+  const uint32_t ng = s_gp[G];
+  for (uint32_t c0 = 0; c0 < ng; c0 += TILE) {
+    for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t k[IPT], uu[IPT], ww[IPT], ss[IPT], dg[IPT], rk[IPT];
+    bool ok[IPT];
+    uint32_t bi = 0;  // bucket of the wave's current key (keys ascend: a short walk)
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      const uint32_t j = c0 + (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
+      ok[i] = j < ng;
+      if (ok[i]) {
+        while (bi + 1 < G && s_gp[bi + 1] <= j) ++bi;
+        const uint64_t slot = ((uint64_t)(group * G + bi) << caplog) + (j - s_gp[bi]);
+        k[i] = okey[slot];
+        uu[i] = cu[slot];
+        ww[i] = cw[slot];
+        ss[i] = __float_as_uint(cs[slot]);
+      } else {
+        k[i] = uu[i] = ww[i] = ss[i] = 0u;
+      }
+    }
+    cp_rank<IPT>(k, ok, 0, dg, rk, s_wcnt);
+    __syncthreads();
+    sp_stamp(stamp, c0 == 0, 2);
+    uint32_t cnt = 0;
+    if (t < RS_BINS) cnt = cp_wave_prefix(s_wcnt, t);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+      if (ok[i]) {
+        const uint32_t pos = s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
+        kout[pos] = k[i];
+        uwout[pos] = ((uint64_t)uu[i] << 32) | ww[i];
+        sout[pos] = ss[i];
+        cp_count_next(s_th, pos, k[i], 8);
+      }
+    }
+    __syncthreads();
+    if (t < RS_BINS) s_base[t] += cnt;  // the next chunk lands behind this one
+  }
+  __syncthreads();
+  cp_flush_next(s_th, nout, m1);
+  sp_stamp(stamp, true, 4);
+}
+
+// Passes 1-3: tile = blockIdx (OS2_TILE consecutive keys).  NEXT: count the
+// next digit per output tile into hout.  clean: row blockIdx (< clean_rows,
+// 0 = this pass's tile count) of a finished pass's matrix back to zero.
+// GATHER (the last pass): the caller's edges at positions below go.k;
+// workgroup 0 publishes the counters and stamps (the call's counters are final),
+// the last tile the end stamp.
+template <bool NEXT, bool GATHER = false>
+__global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__ kin, const uint64_t* __restrict__ uwin,
+                                                    const uint32_t* __restrict__ sin, uint32_t* __restrict__ kout,
+                                                    uint64_t* __restrict__ uwout, uint32_t* __restrict__ sout,
+                                                    const uint64_t* __restrict__ d_n, int shift,
+                                                    const uint32_t* __restrict__ hin, uint32_t* __restrict__ hout,
+                                                    uint32_t* __restrict__ clean, uint32_t clean_rows,
+                                                    uint64_t* __restrict__ stamp, GatherOut go,
+                                                    uint32_t* __restrict__ clean_all = nullptr) {
+  constexpr int IPT = OS2_IPT, WT = 64 * IPT, TILE = OS2_TILE;
+  __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
+  __shared__ uint32_t s_part[2][OS_NT / RS_BINS][RS_BINS];
+  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_w[OS_NW];
+  __shared__ uint32_t s_th[NEXT ? CP_THW : 1];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t n = *d_n;
+  const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
+  const uint32_t tile = blockIdx.x;
+  if (clean && tile < (clean_rows ? clean_rows : ntiles))
+    for (int i = t; i < RS_BINS; i += OS_NT) clean[(uint64_t)tile * RS_BINS + i] = 0u;
+  if (clean_all)  // every row (gridDim = CP_MAXT): a matrix of the previous call, whatever its tile count
+    for (int i = t; i < RS_BINS; i += OS_NT) clean_all[(uint64_t)tile * RS_BINS + i] = 0u;
+  if (GATHER && tile == 0 && t < NCTR) {  // every counter is final: published now (also with no tile)
+    const uint64_t m = n < go.k ? n : go.k;
+    if (t == C_OUT_N) go.ctr[C_OUT_N] = m;
+    if (go.hctr) {
+      go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
+      if (go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
+      if (t == 0 && (ntiles == 0 || ntiles > (uint32_t)CP_MAXT))
+        go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
+      __threadfence_system();
+    }
+  }
+  if (tile >= ntiles || ntiles > (uint32_t)CP_MAXT) return;  // beyond CP_MAXT: F_CPASS is raised, the call redone
+  sp_stamp(stamp, true, 7);
+  const uint64_t b0 = (uint64_t)tile * TILE + (uint64_t)wv * WT + lane;
+  uint32_t k[IPT], ss[IPT], dg[IPT], rk[IPT];
+  uint64_t uw[IPT];
+  bool ok[IPT];
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {  // the tile's keys, in flight during the matrix reads
+    const uint64_t j = b0 + (uint64_t)i * 64;
+    ok[i] = j < n;
+    k[i] = ok[i] ? kin[j] : 0u;
+    uw[i] = ok[i] ? uwin[j] : 0ull;
+    ss[i] = ok[i] ? sin[j] : 0u;
+  }
+  for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
+  if (NEXT)
+    for (uint32_t i = t; i < ntiles * (RS_BINS / 2); i += OS_NT) s_th[i] = 0;
+  cp_bases(hin, ntiles, tile, s_part, s_base, s_w);  // syncs
+  sp_stamp(stamp, true, 0);
+  cp_rank<IPT>(k, ok, shift, dg, rk, s_wcnt);
+  __syncthreads();
+  sp_stamp(stamp, true, 2);
+  if (t < RS_BINS) cp_wave_prefix(s_wcnt, t);
+  __syncthreads();
+  sp_stamp(stamp, true, 3);
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    if (ok[i]) {
+      const uint32_t pos = s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
+      if (GATHER) {
+        if (pos < go.k) go.out[pos] = EdgeOut{(uint32_t)(uw[i] >> 32), (uint32_t)uw[i], __uint_as_float(ss[i])};
+      } else {
+        kout[pos] = k[i];
+        uwout[pos] = uw[i];
+        sout[pos] = ss[i];
+      }
+      if (NEXT) cp_count_next(s_th, pos, k[i], shift + 8);
+    }
+  }
+  if (NEXT) {
+    __syncthreads();
+    cp_flush_next(s_th, ntiles, hout);
+  }
+  sp_stamp(stamp, true, 4);
+  // the call's end: the last tile's exit (approximately the last workgroup's)
+  if (GATHER && go.hctr && tile == ntiles - 1 && t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------- bucket kernel
@@ -1879,7 +2181,8 @@ __global__ __launch_bounds__(NTH) void k_sp_grouprun(GraphView g, int metric, fl
                                                        uint32_t* __restrict__ oval, uint32_t* __restrict__ kcnt,
                                                        uint64_t* __restrict__ ctr, uint32_t* __restrict__ ohist,
                                                        const uint64_t* __restrict__ wsum,
-                                                       uint64_t* __restrict__ stamp, uint64_t* __restrict__ ts) {
+                                                       uint64_t* __restrict__ stamp, uint64_t* __restrict__ ts,
+                                                       uint32_t m0_group = 0) {
   constexpr uint32_t CAP = 1u << CAPLOG;
   constexpr uint32_t NB = 1u << DB;  // digit 0 of the order keys (the first ordering pass's digits)
   __shared__ uint64_t s_key[CAP];
@@ -1973,7 +2276,9 @@ __global__ __launch_bounds__(NTH) void k_sp_grouprun(GraphView g, int metric, fl
   if (t == 0) kcnt[b] = K;
   if (nnan) atomicAdd((unsigned long long*)&ctr[C_NAN], (unsigned long long)nnan);
   __syncthreads();
-  uint32_t* hcp = hist_copy_db<DB>(ohist);
+  // digit 0 into the histogram copies, or (m0_group > 0: counted passes) into
+  // row b / m0_group (the bucket's group) of the count matrix m0
+  uint32_t* hcp = m0_group ? ohist + (b / m0_group) * NB : hist_copy_db<DB>(ohist);
   for (uint32_t i = t; i < NB; i += NTH) {
     const uint32_t hc = s_oh[i];
     if (hc) atomicAdd(&hcp[i], hc);

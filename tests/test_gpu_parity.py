@@ -703,13 +703,14 @@ def test_gpu_exclusion_without_edge_table(gpu, oracle):
 @pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"), dict(NLP_DIRECT="0"),
                                  dict(NLP_MSD_PASSES="2"), dict(NLP_FUSE_RUNS="0"), dict(NLP_DX_BITS="1"),
                                  dict(NLP_DX_BITS="2"), dict(NLP_DX_BITS="3"), dict(NLP_DX_BITS="12"),
-                                 dict(NLP_ORD11="1"), dict(NLP_GR_NT="512")])
+                                 dict(NLP_ORD11="1"), dict(NLP_GR_NT="512"), dict(NLP_COUNTED="0")])
 def test_gpu_sort_path_variants_equal(gpu, oracle, env):
     """Sort-path build variants (fused output gather, several survivors per
     expansion thread, two MSD passes + group sort, separate grouping and
     scoring, direct buckets so wide that k_sp_grouprun sorts 2 or 4 keys per
-    thread or falls back on too-big ranges, three 11-bit ordering passes) give
-    the default's results."""
+    thread or falls back on too-big ranges, three 11-bit ordering passes,
+    look-back ordering passes instead of the counted k_sp_cpass) give the
+    default's results."""
     off, keys = random_csr(9000, 14, 21)
     k = 2500
     with gpu.Graph(off, keys) as G:
@@ -722,3 +723,24 @@ def test_gpu_sort_path_variants_equal(gpu, oracle, env):
                 assert t["candidates"] == t2["candidates"]
     eu, ew, es, _ = oracle.predict(off, keys, 1, 4, max_edges=k)
     assert_canonical_equal(eu, ew, es, *res[(1, 4)][:3])
+
+
+@pytest.mark.parametrize("n,avg,H,env", [(100000, 8, 6, {}), (150000, 6, 6, dict(NLP_COUNTED="2"))])
+def test_gpu_counted_passes_tiles_and_redo(gpu, oracle, n, avg, H, env):
+    """Counted ordering passes (k_sp_cpass: per-tile digit counts from the pass
+    before instead of a look-back) over ~97 candidate tiles, and -- forced
+    beyond CP_MAXT = 128 tiles (~148) by NLP_COUNTED=2 -- the F_CPASS redo
+    with look-back passes; both equal the oracle and the look-back build."""
+    off, keys = random_csr(n, avg, 5, alpha=0.5)
+    eu, ew, es, _ = oracle.predict(off, keys, 1, H, max_edges=10**9)
+    k = len(eu)
+    with _env(**env):
+        with gpu.Graph(off, keys) as G:
+            for _ in range(2):  # capture, then replay
+                u, w, s, t = G.predict(1, H, k)
+                assert_canonical_equal(eu, ew, es, u, w, s)
+                assert t["candidates"] == k
+    with _env(NLP_COUNTED="0"):
+        with gpu.Graph(off, keys) as G:
+            u, w, s, _ = G.predict(1, H, k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
