@@ -1849,9 +1849,13 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   const uint64_t tR = std::max<uint64_t>((capW + RN_TILE - 1) / RN_TILE, DX_MAXB);  // also k_sp_grouprun's buckets
   const uint64_t tO = (capW + OS2_TILE - 1) / OS2_TILE;
   f.ostride = tO * RS_BINS;
-  {  // counted passes when the candidates (<= wedges) should fit CP_MAXT tiles, unless a similar call overflowed
-    const double est = hp_estimate(g, p), cap = (double)CP_MAXT * OS2_TILE;  // est >= candidates, mostly
-    f.counted = f.fused && !f.ord11 && g->counted && (g->counted_force || est < cap) &&
+  {  // counted passes when the candidates may fit CP_MAXT tiles, unless a similar call overflowed.  The
+     // estimate is 0.5 sum deg^2 over the survivors scaled by the range's share of the sources: it
+     // overstates the candidates (w > u, exclusion, duplicates) and, for the wedge-balanced ranges of
+     // a sharded job, can be off by the range's weight -- so try up to 4x the capacity; an overflow
+     // (F_CPASS) costs one redo and is remembered
+    const double est = hp_estimate(g, p), cap = (double)CP_MAXT * OS2_TILE;
+    f.counted = f.fused && !f.ord11 && g->counted && (g->counted_force || est < 4.0 * cap) &&
                 !(g->cp_off_w > 0 && est > 0.5 * g->cp_off_w);
   }
   f.ostride11 = tO * 2048;
