@@ -10,7 +10,13 @@ with the graph resident in HBM; for N > 1 it also includes the RCCL exchange
 and merge.  Scaling is weak: at N GPUs the graph is N x configs[1] (n and m
 scaled) and each rank owns 1/N of the source vertices.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+At N = 1 the K timed calls are enqueued back to back (nlp_predict_device_async,
+one nlp_sync at the end: every call recomputes the whole prediction, only the
+host wait between calls is gone -- a serving loop); the synchronous per-call
+latency of the drop-in API is reported beside it (sync_call_ms), and --sync
+times the synchronous calls instead.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sync]
 """
 import argparse
 import json
@@ -118,6 +124,7 @@ def main():
     ap.add_argument("--metric", default=None)
     ap.add_argument("--hub", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync", action="store_true", help="N = 1: time synchronous calls (no pipelining)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,14 +182,33 @@ def main():
     # per-phase device time of the library's own events, averaged over the timed steps
     score_ms = select_ms = hot_ms = 0.0
     hot_bytes = replays = 0
+    pipelined = world == 1 and not args.sync
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cnt = step()
-        score_ms += last.get("score_ms", 0.0)
-        select_ms += last.get("select_ms", 0.0)
-        hot_ms += last.get("hot_ms", 0.0)
-        hot_bytes += int(last.get("hot_bytes", 0))
-        replays += int(last.get("graph_replay", 0))
+    if pipelined:
+        for _ in range(args.steps):
+            G.predict_device_async(mid, hub, k, out, stream=stream)
+        try:
+            cnt, t = G.sync()
+        except nlp.NlpError as e:  # a call of the batch needs a synchronous redo: time synchronous calls
+            if e.status != 6:
+                raise
+            log("bench: asynchronous batch needs a redo (%s); timing synchronous calls" % e)
+            pipelined = False
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        else:
+            last.update(t)
+            score_ms, select_ms, hot_ms = (args.steps * last.get(x, 0.0) for x in ("score_ms", "select_ms", "hot_ms"))
+            hot_bytes = args.steps * int(last.get("hot_bytes", 0))
+            replays = args.steps * int(last.get("graph_replay", 0))
+    if not pipelined:
+        for _ in range(args.steps):
+            cnt = step()
+            score_ms += last.get("score_ms", 0.0)
+            select_ms += last.get("select_ms", 0.0)
+            hot_ms += last.get("hot_ms", 0.0)
+            hot_bytes += int(last.get("hot_bytes", 0))
+            replays += int(last.get("graph_replay", 0))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -193,6 +219,12 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = cnt / (elapsed / args.steps)
 
+    sync_call_ms = None
+    if world == 1:  # the drop-in API's synchronous call latency (outside the timed region)
+        t1 = time.perf_counter()
+        for _ in range(max(5, min(args.steps, 50))):
+            step()
+        sync_call_ms = (time.perf_counter() - t1) / max(5, min(args.steps, 50)) * 1e3
     if rank == 0:
         p, r, f1 = f1_on_device(G, out, cnt, du, dw)
         score_ms /= args.steps
@@ -246,6 +278,7 @@ def main():
                          "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
                          "traffic_source": traffic["source"] if traffic else None},
             "graph_replay": replays == args.steps,
+            "pipelined": pipelined, "sync_call_ms": sync_call_ms,
             "call_effective": {"algorithmic_bytes": b_call, "achieved": call_eff, "unit": "GB/s",
                                "frac": call_eff / HBM_PEAK_GBS, "definition": "SURVEY.md 8(d) B_alg(H) per call"},
             "cpu_baseline": None,

@@ -48,7 +48,8 @@ typedef enum {
   NLP_ERR_DEVICE = 2,     /* HIP runtime / kernel failure */
   NLP_ERR_NOMEM = 3,      /* device or host allocation failed */
   NLP_ERR_NODEVICE = 4,   /* no usable gfx950 device */
-  NLP_ERR_CAPACITY = 5    /* caller buffer too small (see out_count) */
+  NLP_ERR_CAPACITY = 5,   /* caller buffer too small (see out_count) */
+  NLP_ERR_RETRY = 6       /* nlp_sync: a call of the asynchronous batch needs a synchronous redo */
 } nlp_status;
 
 /* The nine similarity metrics of predict.hxx (enum order = main.cxx:212-220). */
@@ -162,6 +163,26 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
 nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
                                  float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end,
                                  nlp_edge* d_out, uint64_t* out_count, nlp_timing* t, void* stream);
+
+/* Asynchronous device prediction (serving: back-to-back calls without a host
+ * wait, no counterpart in the reference).  Enqueues the same computation as
+ * nlp_predict_device_ex on `stream` and returns at once when this handle's
+ * last synchronous call had the same arguments and output array and ran as
+ * one replayed graph; otherwise the call runs synchronously.  All calls of a
+ * batch use one stream.  Results (d_out of each call, the last call's count
+ * and timing) are valid after nlp_sync.  Not thread-safe with other calls on
+ * the handle. */
+nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
+                                    float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end,
+                                    nlp_edge* d_out, void* stream);
+
+/* Wait for the batch of nlp_predict_device_async calls: *out_count and t of
+ * the last one.  NLP_ERR_RETRY when any call of the batch hit a condition the
+ * synchronous path handles by redoing the call (a bucket or buffer overflow,
+ * more candidate tiles than the counted passes hold): its output is not
+ * valid, the caller redoes it with nlp_predict_device_ex.  NLP_ERR_INVALID
+ * when nothing is pending. */
+nlp_status nlp_sync(nlp_graph* g, uint64_t* out_count, nlp_timing* t);
 
 /* Merge step of the multi-GPU path: given `n` device-resident edges that are the
  * concatenation, in ascending source-range order, of per-shard canonical

@@ -61,7 +61,8 @@ _timing_get = operator.attrgetter(*_TIMING_FIELDS)
 
 EXPORTS = [
     "nlp_graph_create", "nlp_graph_create_device", "nlp_graph_destroy", "nlp_graph_info", "nlp_predict",
-    "nlp_predict_ex", "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_select_edges_device",
+    "nlp_predict_ex", "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_predict_device_async",
+    "nlp_sync", "nlp_select_edges_device",
     "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
     "nlp_metric_name", "nlp_version",
 ]
@@ -91,6 +92,8 @@ def lib(build_if_missing=True):
     L.nlp_copy_last.argtypes = [vp, vp, u64, P(u64)]
     L.nlp_predict_device.argtypes = [vp, i32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
     L.nlp_predict_device_ex.argtypes = [vp, i32, u32, u32, f32, u64, u64, u64, vp, P(u64), P(Timing), vp]
+    L.nlp_predict_device_async.argtypes = [vp, i32, u32, u32, f32, u64, u64, u64, vp, vp]
+    L.nlp_sync.argtypes = [vp, P(u64), P(Timing)]
     L.nlp_select_edges_device.argtypes = [vp, vp, u64, u64, vp, P(u64), vp]
     L.nlp_merge_blocks_device.argtypes = [vp, vp, u64, u32, u64, vp, P(u64), vp]
     L.nlp_set_truth.argtypes = [vp, vp, vp, u64]
@@ -102,7 +105,8 @@ def lib(build_if_missing=True):
     L.nlp_metric_name.restype = ctypes.c_char_p
     L.nlp_version.restype = i32
     for f in ("nlp_graph_create", "nlp_graph_create_device", "nlp_graph_info", "nlp_predict", "nlp_predict_ex",
-              "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_select_edges_device",
+              "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_predict_device_async", "nlp_sync",
+              "nlp_select_edges_device",
               "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common"):
         getattr(L, f).restype = i32
     _lib = L
@@ -266,6 +270,29 @@ class Graph:
         t, cnt, rcnt, rt, fn = io
         _check(fn(self._h, _metric(metric), int(hub), int(maxfactor2), float(min_score), int(max_edges), int(u_begin),
                   int(u_end), out.data_ptr(), rcnt, rt, _stream_ptr(stream, out)), "nlp_predict_device_ex")
+        return cnt.value, t.as_dict()
+
+    def predict_device_async(self, metric, hub, max_edges, out, u_begin=0, u_end=UINT64_MAX, min_score=0.0,
+                             stream=None, maxfactor2=0):
+        """nlp_predict_device_async: enqueue predict_device's computation without a
+        host wait (it runs synchronously unless the same call last ran
+        synchronously as one replayed graph); results after sync()."""
+        need = 3 * int(max_edges)
+        memo = (id(out), out.data_ptr(), need)
+        if getattr(self, "_out_ok", None) != memo:
+            _check_tensor(out, "out", _edge_dtypes(), self.device, need)
+            self._out_ok = memo
+        fn = getattr(self, "_afn", None) or lib().nlp_predict_device_async
+        self._afn = fn
+        _check(fn(self._h, _metric(metric), int(hub), int(maxfactor2), float(min_score), int(max_edges), int(u_begin),
+                  int(u_end), out.data_ptr(), _stream_ptr(stream, out)), "nlp_predict_device_async")
+
+    def sync(self):
+        """nlp_sync: wait for the predict_device_async batch; (count, timing) of its
+        last call.  NlpError(NLP_ERR_RETRY = 6) when a call of the batch needs a
+        synchronous redo."""
+        t, cnt = Timing(), ctypes.c_uint64()
+        _check(lib().nlp_sync(self._h, ctypes.byref(cnt), ctypes.byref(t)), "nlp_sync")
         return cnt.value, t.as_dict()
 
     def select_edges_device(self, edges_in, n, max_edges, out, stream=None):

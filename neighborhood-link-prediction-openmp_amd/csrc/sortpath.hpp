@@ -862,6 +862,10 @@ struct GatherOut {
   uint64_t* ctr;   // the call's counters: C_OUT_N is set, all are published to hctr
   uint64_t* hctr;  // host-mapped copy of the counters (read after the call's final event)
   const uint64_t* ts;  // the call's timing stamps, published to hctr[NCTR ..]
+  // device word OR-ed with the call's flags (nlp_predict_device_async: a redo
+  // needed by any call of a batch shows at nlp_sync; the calls of one handle
+  // run in stream order, so a plain read-modify-write is enough)
+  uint64_t* sticky = nullptr;
 };
 
 // Exclusive scan of one value per digit (threads 0-255, 0 elsewhere) over the
@@ -987,6 +991,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
       if (go.hctr) go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
       if (go.hctr && go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
       if (go.hctr && t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();  // the last tile: ~the end
+      if (go.sticky && t == C_FLAGS) *go.sticky |= go.ctr[C_FLAGS];
     }
   };
   if (GATHER && ntiles == 0 && blockIdx.x == 0) publish();
@@ -1382,6 +1387,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__
   if (GATHER && tile == 0 && t < NCTR) {  // every counter is final: published now (also with no tile)
     const uint64_t m = n < go.k ? n : go.k;
     if (t == C_OUT_N) go.ctr[C_OUT_N] = m;
+    if (go.sticky && t == C_FLAGS) *go.sticky |= go.ctr[C_FLAGS];
     if (go.hctr) {
       go.hctr[t] = t == C_OUT_N ? m : go.ctr[t];
       if (go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
@@ -2568,7 +2574,8 @@ __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ i
                                                   uint64_t k, EdgeOut* __restrict__ out,
                                                   uint64_t* __restrict__ ctr, uint64_t* __restrict__ hctr,
                                                   const uint64_t* __restrict__ ts,
-                                                  uint32_t* __restrict__ clean_desc = nullptr, uint32_t clean_nb = 0) {
+                                                  uint32_t* __restrict__ clean_desc = nullptr, uint32_t clean_nb = 0,
+                                                  uint64_t* __restrict__ sticky = nullptr) {
   const uint64_t m = std::min<uint64_t>(ctr[C_C], k);
   if (clean_desc) {  // the last ordering pass's descriptor rows (clean_nb words each) back to zero (see k_sp_pass)
     const uint64_t words = (ctr[C_C] + OS2_TILE - 1) / OS2_TILE * clean_nb;
@@ -2577,6 +2584,7 @@ __global__ __launch_bounds__(NT) void k_sp_gather(const uint32_t* __restrict__ i
   }
   if (blockIdx.x == 0) {
     if (threadIdx.x == 0) ctr[C_OUT_N] = m;
+    if (sticky && threadIdx.x == C_FLAGS) *sticky |= ctr[C_FLAGS];  // see GatherOut::sticky
     if (hctr && threadIdx.x < NCTR) hctr[threadIdx.x] = threadIdx.x == C_OUT_N ? m : ctr[threadIdx.x];
     if (hctr && ts && threadIdx.x >= NCTR && threadIdx.x < NCTR + TS_END) hctr[threadIdx.x] = ts[threadIdx.x - NCTR];
     if (hctr) __threadfence_system();

@@ -744,3 +744,43 @@ def test_gpu_counted_passes_tiles_and_redo(gpu, oracle, n, avg, H, env):
         with gpu.Graph(off, keys) as G:
             u, w, s, _ = G.predict(1, H, k)
             assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_async_batch_equals_sync(gpu, oracle):
+    """nlp_predict_device_async / nlp_sync: a call with no synchronous
+    predecessor runs synchronously; after a synchronous call with the same
+    arguments the calls are only enqueued; a batch mixing both ends with the
+    last call's count and output; nlp_sync with nothing pending is refused."""
+    import torch
+    off, keys = random_csr(20000, 12, 31)
+    k = 4000
+    st = torch.cuda.current_stream()
+    with gpu.Graph(off, keys) as G:
+        with pytest.raises(gpu.NlpError) as e:
+            G.sync()
+        assert e.value.status == 1
+        ref = {}
+        for m, H in ((1, 4), (0, 8), (7, 4)):
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            ref[(m, H)] = (eu, ew, es)
+        outs = {mh: torch.zeros((k, 3), dtype=torch.int32, device="cuda") for mh in ref}
+        for rnd in range(3):  # 0: nothing replayable yet; later rounds replay
+            for (m, H), out in outs.items():
+                out.zero_()
+                for _ in range(4):
+                    G.predict_device_async(m, H, k, out, stream=st)
+                cnt, t = G.sync()
+                eu, ew, es = ref[(m, H)]
+                assert cnt == len(eu) and t["candidates"] >= cnt
+                a = out[:cnt].cpu().numpy()
+                assert_canonical_equal(eu, ew, es, a[:, 0].view(np.uint32), a[:, 1].view(np.uint32),
+                                       a[:, 2].view(np.float32))
+                G.predict_device(m, H, k, out, stream=st)  # makes the next round's calls replayable
+        # a batch that ends with a different (synchronous) call reports that call
+        (m1, H1), (m2, H2) = list(outs)[:2]
+        G.predict_device(m1, H1, k, outs[(m1, H1)], stream=st)
+        for _ in range(3):
+            G.predict_device_async(m1, H1, k, outs[(m1, H1)], stream=st)
+        G.predict_device_async(m2, H2, k, outs[(m2, H2)], u_begin=0, u_end=gpu.UINT64_MAX - 1, stream=st)
+        cnt, _ = G.sync()
+        assert cnt == len(ref[(m2, H2)][0])
