@@ -2122,11 +2122,11 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.counted && ps == 0) {  // bucket groups of k_sp_grouprun's candidates (it counted digit 0 per group)
-        hipLaunchKernelGGL(k_sp_cpass0, dim3(cp_groups), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
+      if (f.counted && ps == 0) {  // dense tiles of k_sp_grouprun's candidates (it counted digit 0 per bucket group)
+        hipLaunchKernelGGL(k_sp_cpass0, dim3(CP_MAXT), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
                            (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
-                           cp_g, f.caplog, (const uint32_t*)cmat, cmat + CP_M, f.ok1, (uint64_t*)f.rk0, f.ov1, ctr,
-                           ts + TS_HOT_OUT, hot == s ? g->d_stamp : nullptr);
+                           (uint32_t)nb_used, cp_g, cp_groups, f.caplog, (const uint32_t*)cmat, cmat + CP_M, f.ok1,
+                           (uint64_t*)f.rk0, f.ov1, ctr, ts + TS_HOT_OUT, hot == s ? g->d_stamp : nullptr);
       } else if (f.counted) {  // pass ps from matrix ps; cleans matrix ps - 1
         const uint32_t* m_in = cmat + (uint64_t)ps * CP_M;
         uint32_t* const m_old = cmat + (uint64_t)(ps - 1) * CP_M;

@@ -1154,8 +1154,9 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
 // wait on nothing, so any grid size and dispatch order works.
 //
 //   k_sp_grouprun   counts digit 0 per bucket group into m0
-//   k_sp_cpass0     tile = a group of G consecutive buckets (their slots, in bucket
-//                   order = (u, w) order); counts digit 1 per output tile (m1)
+//   k_sp_cpass0     tile = 4096 consecutive keys of the concatenated buckets
+//                   (their slots, in bucket order = (u, w) order); counts digit
+//                   1 per output tile (m1)
 //   k_sp_cpass x3   tile = OS2_TILE consecutive keys; passes 1 and 2 count the
 //                   next digit per output tile (m2, m3); pass 3 writes the
 //                   caller's edges (GATHER) and publishes the counters
@@ -1170,7 +1171,6 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
 // before any early exit); m3 -- read by every tile of the last pass -- is
 // zeroed by pass 1 of the next call (all CP_MAXT rows), before pass 2 counts
 // into it.
-constexpr int CP_MAXG = 32;  // buckets per group (DX_MAXB / CP_MAXT)
 
 // Digit bases of tile `tile` of `ntiles` from the count matrix m: s_base[d] =
 // (totals of the digits below d) + (digit d in tiles < tile); returns the key
@@ -1267,62 +1267,109 @@ __device__ __forceinline__ void cp_flush_next(const uint32_t* s_th, uint32_t nti
   }
 }
 
-// Pass 0: tile = bucket group `blockIdx` (buckets [G blockIdx, G blockIdx +
-// G), gridDim = groups <= CP_MAXT, G <= CP_MAXG; the host spreads the groups
-// over the buckets that can hold keys); its keys in chunks of OS2_TILE, each
-// chunk ranked and placed behind the previous one (stable).  The candidate
-// count (the matrix total) goes to ctr[C_C].
+// Pass 0: tile = OS2_TILE consecutive keys of the concatenated buckets (dense
+// position P = bucket prefix + slot), gridDim >= tiles.  m0 holds digit 0 per
+// bucket GROUP (G consecutive buckets, counted by k_sp_grouprun), so the digit
+// bases of tile j at P_j = j OS2_TILE are (totals of the lower digits) + (m0
+// rows of the groups before P_j's group) + (the digit's count among that
+// group's keys before P_j, counted here from the keys themselves).  Every tile
+// holds exactly OS2_TILE keys (the last one fewer): no imbalance between tiles
+// whatever the bucket sizes.  The candidate count (the matrix total) goes to
+// ctr[C_C].
 __global__ __launch_bounds__(OS_NT) void k_sp_cpass0(const uint32_t* __restrict__ okey, const uint32_t* __restrict__ cu,
                                                      const uint32_t* __restrict__ cw, const float* __restrict__ cs,
-                                                     const uint32_t* __restrict__ kcnt, uint32_t G, int caplog,
-                                                     const uint32_t* __restrict__ m0, uint32_t* __restrict__ m1,
-                                                     uint32_t* __restrict__ kout, uint64_t* __restrict__ uwout,
-                                                     uint32_t* __restrict__ sout, uint64_t* __restrict__ ctr,
-                                                     uint64_t* __restrict__ end_mark, uint64_t* __restrict__ stamp) {
+                                                     const uint32_t* __restrict__ kcnt, uint32_t nb, uint32_t G,
+                                                     uint32_t ngroups, int caplog, const uint32_t* __restrict__ m0,
+                                                     uint32_t* __restrict__ m1, uint32_t* __restrict__ kout,
+                                                     uint64_t* __restrict__ uwout, uint32_t* __restrict__ sout,
+                                                     uint64_t* __restrict__ ctr, uint64_t* __restrict__ end_mark,
+                                                     uint64_t* __restrict__ stamp) {
   constexpr int IPT = OS2_IPT, WT = 64 * IPT, TILE = OS2_TILE;
+  constexpr uint32_t Q = OS_NT / RS_BINS, R = CP_MAXT / Q, PER = DX_MAXB / OS_NT;
   __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
-  __shared__ uint32_t s_part[2][OS_NT / RS_BINS][RS_BINS];
+  __shared__ uint32_t s_pre[DX_MAXB + 1];  // exclusive prefix of the bucket counts
+  __shared__ uint32_t s_part[2][Q][RS_BINS];
+  __shared__ uint32_t s_lead[RS_BINS];     // digit counts of P_j's group before P_j
   __shared__ uint32_t s_base[RS_BINS];
   __shared__ uint32_t s_w[OS_NW];
-  __shared__ uint32_t s_gp[CP_MAXG + 1];
   __shared__ uint32_t s_th[CP_THW];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint32_t group = blockIdx.x;
+  const uint32_t tile = blockIdx.x, P = tile * TILE;
   ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel)
   sp_stamp(stamp, true, 7);
-  if (wv == 0) {  // the group's bucket counts, prefix-summed (G <= 64)
-    const uint32_t c = (uint32_t)lane < G ? kcnt[group * G + lane] : 0u;
-    uint32_t inc = c;
+  // the m0 rows (all in flight while the bucket prefix is formed)
+  const uint32_t d = (uint32_t)t % RS_BINS, q = (uint32_t)t / RS_BINS;
+  uint32_t c[R];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    if ((uint32_t)lane <= G && lane <= CP_MAXG) s_gp[lane] = inc - c;
+  for (uint32_t i = 0; i < R; ++i) {
+    const uint32_t r = q + i * Q;
+    c[i] = m0[(r < ngroups ? r : 0u) * RS_BINS + d];
   }
-  const uint64_t n = cp_bases(m0, gridDim.x, group, s_part, s_base, s_w);  // syncs (s_gp too)
-  sp_stamp(stamp, true, 0);
-  if (group == 0 && t == 0) ctr[C_C] = n;
-  const uint32_t nout = (uint32_t)((n + TILE - 1) / TILE);
-  if (nout > (uint32_t)CP_MAXT) {  // beyond the counted passes: redone with look-back passes
-    if (group == 0 && t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], (unsigned long long)F_CPASS);
+  {  // bucket prefix: thread t sums buckets [PER t, PER t + PER)
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) {
+      const uint32_t b = (uint32_t)t * PER + i;
+      v[i] = b < nb ? kcnt[b] : 0u;
+      sum += v[i];
+    }
+    uint64_t tot;
+    uint32_t run = os_block_scan(sum, s_w, &tot);  // syncs
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) {
+      const uint32_t b = (uint32_t)t * PER + i;
+      if (b < nb) s_pre[b] = run;
+      run += v[i];
+    }
+    if (t == 0) s_pre[nb] = (uint32_t)tot;
+    if (t < RS_BINS) s_lead[t] = 0;
+  }
+  for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t n = s_pre[nb];
+  if (tile == 0 && t == 0) ctr[C_C] = n;
+  const uint32_t ntiles = (n + TILE - 1) / TILE;
+  if (ntiles > (uint32_t)CP_MAXT) {  // beyond the counted passes: redone with look-back passes
+    if (tile == 0 && t == 0) atomicOr((unsigned long long*)&ctr[C_FLAGS], (unsigned long long)F_CPASS);
     return;
   }
-  for (uint32_t i = t; i < nout * (RS_BINS / 2); i += OS_NT) s_th[i] = 0;
-  const uint32_t ng = s_gp[G];
-  for (uint32_t c0 = 0; c0 < ng; c0 += TILE) {
-    for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-    uint32_t k[IPT], uu[IPT], ww[IPT], ss[IPT], dg[IPT], rk[IPT];
-    bool ok[IPT];
-    uint32_t bi = 0;  // bucket of the wave's current key (keys ascend: a short walk)
+  if (tile >= ntiles) return;
+  // bucket of a dense position: last b with s_pre[b] <= x (a uniform search)
+  auto bucket_of = [&](uint32_t x) {
+    uint32_t lo = 0, hi = nb;  // s_pre[lo] <= x < s_pre[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_pre[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const uint32_t bj = bucket_of(P), gj = bj / G, gp = s_pre[gj * G];  // P_j's group and its dense start
+  {
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < R; ++i) {
+      const uint32_t r = q + i * Q;
+      total += r < ngroups ? c[i] : 0u;
+      before += r < gj ? c[i] : 0u;
+    }
+    s_part[0][q][d] = before;
+    s_part[1][q][d] = total;
+  }
+  for (uint32_t i = t; i < ntiles * (RS_BINS / 2); i += OS_NT) s_th[i] = 0;
+  // the tile's keys and payload: wave wv's keys from one search, then short walks
+  uint32_t k[IPT], uu[IPT], ww[IPT], ss[IPT], dg[IPT], rk[IPT];
+  bool ok[IPT];
+  {
+    const uint32_t j0 = P + (uint32_t)wv * WT;
+    uint32_t b = bucket_of(j0 < n ? j0 : 0u);
 #pragma unroll
     for (int i = 0; i < IPT; ++i) {
-      const uint32_t j = c0 + (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-      ok[i] = j < ng;
+      const uint32_t j = j0 + (uint32_t)i * 64 + (uint32_t)lane;
+      ok[i] = j < n && j < P + TILE;
       if (ok[i]) {
-        while (bi + 1 < G && s_gp[bi + 1] <= j) ++bi;
-        const uint64_t slot = ((uint64_t)(group * G + bi) << caplog) + (j - s_gp[bi]);
+        while (s_pre[b + 1] <= j) ++b;
+        const uint64_t slot = ((uint64_t)b << caplog) + (j - s_pre[b]);
         k[i] = okey[slot];
         uu[i] = cu[slot];
         ww[i] = cw[slot];
@@ -1331,27 +1378,60 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass0(const uint32_t* __restrict_
         k[i] = uu[i] = ww[i] = ss[i] = 0u;
       }
     }
-    cp_rank<IPT>(k, ok, 0, dg, rk, s_wcnt);
-    __syncthreads();
-    sp_stamp(stamp, c0 == 0, 2);
-    uint32_t cnt = 0;
-    if (t < RS_BINS) cnt = cp_wave_prefix(s_wcnt, t);
-    __syncthreads();
+  }
+  {  // the digit counts of the group's keys in [gp, P) (in LDS), LP keys per thread per round with all
+     // loads in flight together
+    constexpr int LP = 8;
+    for (uint32_t x0 = gp; x0 < P; x0 += LP * OS_NT) {
+      uint32_t kk[LP];
+      uint32_t b = bucket_of(x0 + (uint32_t)t < P ? x0 + (uint32_t)t : x0);
 #pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (ok[i]) {
-        const uint32_t pos = s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
-        kout[pos] = k[i];
-        uwout[pos] = ((uint64_t)uu[i] << 32) | ww[i];
-        sout[pos] = ss[i];
-        cp_count_next(s_th, pos, k[i], 8);
+      for (int i = 0; i < LP; ++i) {
+        const uint32_t x = x0 + (uint32_t)t + (uint32_t)i * OS_NT;
+        kk[i] = 0u;
+        if (x < P) {
+          while (s_pre[b + 1] <= x) ++b;
+          kk[i] = okey[((uint64_t)b << caplog) + (x - s_pre[b])];
+        }
       }
+#pragma unroll
+      for (int i = 0; i < LP; ++i)
+        if (x0 + (uint32_t)t + (uint32_t)i * OS_NT < P) atomicAdd(&s_lead[kk[i] & 255u], 1u);
     }
-    __syncthreads();
-    if (t < RS_BINS) s_base[t] += cnt;  // the next chunk lands behind this one
+  }
+  __syncthreads();  // s_part, s_lead
+  {
+    uint32_t before = 0, total = 0;
+    if (t < RS_BINS) {
+#pragma unroll
+      for (uint32_t i = 0; i < Q; ++i) {
+        before += s_part[0][i][t];
+        total += s_part[1][i][t];
+      }
+      before += s_lead[t];
+    }
+    uint64_t tot;
+    const uint32_t dbase = os_digit_scan(total, s_w, &tot);  // syncs
+    if (t < RS_BINS) s_base[t] = dbase + before;
+  }
+  sp_stamp(stamp, true, 0);
+  cp_rank<IPT>(k, ok, 0, dg, rk, s_wcnt);
+  __syncthreads();
+  sp_stamp(stamp, true, 2);
+  if (t < RS_BINS) cp_wave_prefix(s_wcnt, t);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    if (ok[i]) {
+      const uint32_t pos = s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
+      kout[pos] = k[i];
+      uwout[pos] = ((uint64_t)uu[i] << 32) | ww[i];
+      sout[pos] = ss[i];
+      cp_count_next(s_th, pos, k[i], 8);
+    }
   }
   __syncthreads();
-  cp_flush_next(s_th, nout, m1);
+  cp_flush_next(s_th, ntiles, m1);
   sp_stamp(stamp, true, 4);
 }
 
