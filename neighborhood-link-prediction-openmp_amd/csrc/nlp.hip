@@ -2131,6 +2131,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
         const uint32_t* m_in = cmat + (uint64_t)ps * CP_M;
         uint32_t* const m_old = cmat + (uint64_t)(ps - 1) * CP_M;
         const uint32_t rows_old = ps == 1 ? cp_groups : 0u;  // matrix 0 has a row per bucket group
+        const uint32_t words_old = ps == 1 ? RS_BINS : RS_BINS / 2;  // u32 counts; matrices 1-3 u16 pairs
         // matrix 3 (read by every tile of the last pass, so not cleaned there) is zeroed by pass 1
         uint32_t* const m_last = ps == 1 ? cmat + 3 * CP_M : nullptr;
         // payload ping-pong: A = (ok1, rk0, ov1) after passes 0 and 2, B = (ok0, rk1, ov0) after pass 1
@@ -2138,16 +2139,16 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
         if (ps == 1)
           hipLaunchKernelGGL(k_sp_cpass<true>, dim3(CP_MAXT), dim3(OS_NT), 0, st, kA, uwA, sA, f.ok0,
                              (uint64_t*)f.rk1, f.ov0, (const uint64_t*)&ctr[C_C], 8, m_in, cmat + 2 * CP_M, m_old,
-                             rows_old, hot == s ? g->d_stamp : nullptr, GatherOut{}, m_last);
+                             rows_old, words_old, hot == s ? g->d_stamp : nullptr, GatherOut{}, m_last);
         else if (ps == 2)
           hipLaunchKernelGGL(k_sp_cpass<true>, dim3(CP_MAXT), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
                              (const uint64_t*)f.rk1, (const uint32_t*)f.ov0, f.ok1, (uint64_t*)f.rk0, f.ov1,
-                             (const uint64_t*)&ctr[C_C], 16, m_in, cmat + 3 * CP_M, m_old, rows_old,
+                             (const uint64_t*)&ctr[C_C], 16, m_in, cmat + 3 * CP_M, m_old, rows_old, words_old,
                              hot == s ? g->d_stamp : nullptr, GatherOut{});
         else  // the last pass writes the caller's edges and publishes the counters
           hipLaunchKernelGGL((k_sp_cpass<false, true>), dim3(CP_MAXT), dim3(OS_NT), 0, st, kA, uwA, sA,
                              (uint32_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr, (const uint64_t*)&ctr[C_C], 24,
-                             m_in, (uint32_t*)nullptr, m_old, rows_old, hot == s ? g->d_stamp : nullptr,
+                             m_in, (uint32_t*)nullptr, m_old, rows_old, words_old, hot == s ? g->d_stamp : nullptr,
                              GatherOut{nullptr, nullptr, nullptr, p.max_edges, out, ctr, g->host_ctr_dev, ts, g->d_sticky});
       } else if (f.fused && !f.ord11 && ps == 0)  // k_sp_grouprun's per-bucket candidates (it counted digit 0); this pass counts 1-3
         hipLaunchKernelGGL((k_sp_pass<uint32_t, OS2_IPT, false, true, GAP_BUCKETS>), grid(tO, g->occ_p32),

@@ -1175,11 +1175,14 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
 // Digit bases of tile `tile` of `ntiles` from the count matrix m: s_base[d] =
 // (totals of the digits below d) + (digit d in tiles < tile); returns the key
 // total n.  All threads of an OS_NT workgroup; ends with a barrier.
-__device__ __forceinline__ uint64_t cp_bases(const uint32_t* __restrict__ m, uint32_t ntiles, uint32_t tile,
+// m: packed u16 pairs (bin 2i in the low half of word i) -- the matrices the
+// passes count into; a bin holds at most OS2_TILE keys.
+__device__ __forceinline__ uint64_t cp_bases(const uint32_t* __restrict__ m32, uint32_t ntiles, uint32_t tile,
                                              uint32_t (&s_part)[2][OS_NT / RS_BINS][RS_BINS], uint32_t* s_base,
                                              uint32_t* s_w) {
   constexpr uint32_t Q = OS_NT / RS_BINS;
   const int t = threadIdx.x;
+  const uint16_t* m = (const uint16_t*)m32;
   {  // thread t: digit t % 256 over the tiles r = t / 256 (mod Q), all loads in one round trip
     constexpr int R = CP_MAXT / Q;
     const uint32_t d = (uint32_t)t % RS_BINS, q = (uint32_t)t / RS_BINS;
@@ -1259,11 +1262,12 @@ __device__ __forceinline__ void cp_count_next(uint32_t* s_th, uint32_t pos, uint
   const uint32_t bin = (pos / OS2_TILE) * RS_BINS + ((key >> nshift) & 255u);
   atomicAdd(&s_th[bin >> 1], 1u << ((bin & 1u) * 16));  // a bin holds <= OS2_TILE keys: no carry
 }
+// The output matrix keeps the LDS layout (u16 pairs): one atomic per non-zero
+// pair, no carry between the halves (a bin holds at most OS2_TILE keys).
 __device__ __forceinline__ void cp_flush_next(const uint32_t* s_th, uint32_t ntiles, uint32_t* __restrict__ hout) {
   for (uint32_t i = threadIdx.x; i < ntiles * (RS_BINS / 2); i += OS_NT) {
     const uint32_t c = s_th[i];
-    if (c & 0xffffu) atomicAdd(&hout[2 * i], c & 0xffffu);
-    if (c >> 16) atomicAdd(&hout[2 * i + 1], c >> 16);
+    if (c) atomicAdd(&hout[i], c);
   }
 }
 
@@ -1448,7 +1452,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__
                                                     const uint64_t* __restrict__ d_n, int shift,
                                                     const uint32_t* __restrict__ hin, uint32_t* __restrict__ hout,
                                                     uint32_t* __restrict__ clean, uint32_t clean_rows,
-                                                    uint64_t* __restrict__ stamp, GatherOut go,
+                                                    uint32_t clean_words, uint64_t* __restrict__ stamp, GatherOut go,
                                                     uint32_t* __restrict__ clean_all = nullptr) {
   constexpr int IPT = OS2_IPT, WT = 64 * IPT, TILE = OS2_TILE;
   __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
@@ -1460,10 +1464,10 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__
   const uint64_t n = *d_n;
   const uint32_t ntiles = (uint32_t)((n + TILE - 1) / TILE);
   const uint32_t tile = blockIdx.x;
-  if (clean && tile < (clean_rows ? clean_rows : ntiles))
-    for (int i = t; i < RS_BINS; i += OS_NT) clean[(uint64_t)tile * RS_BINS + i] = 0u;
-  if (clean_all)  // every row (gridDim = CP_MAXT): a matrix of the previous call, whatever its tile count
-    for (int i = t; i < RS_BINS; i += OS_NT) clean_all[(uint64_t)tile * RS_BINS + i] = 0u;
+  if (clean && tile < (clean_rows ? clean_rows : ntiles))  // rows of clean_words words
+    for (uint32_t i = t; i < clean_words; i += OS_NT) clean[(uint64_t)tile * clean_words + i] = 0u;
+  if (clean_all)  // every packed row (gridDim = CP_MAXT): a matrix of the previous call, whatever its tile count
+    for (int i = t; i < RS_BINS / 2; i += OS_NT) clean_all[(uint64_t)tile * (RS_BINS / 2) + i] = 0u;
   if (GATHER && tile == 0 && t < NCTR) {  // every counter is final: published now (also with no tile)
     const uint64_t m = n < go.k ? n : go.k;
     if (t == C_OUT_N) go.ctr[C_OUT_N] = m;
