@@ -187,6 +187,7 @@ struct nlp_graph {
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   int gr_nt = GR_NT;                           // k_sp_grouprun threads per bucket (NLP_GR_NT=512)
   bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
+  bool async_direct = true;                    // asynchronous calls launched kernel by kernel (NLP_ASYNC_GRAPH=1: graphs)
   int exb_spt = 2;                             // k_sp_exbucket: survivors per thread (NLP_EXB_SPT 1, 2, 4)
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
   double dx_target = 256;                      // direct buckets: mean records per bucket (NLP_DX_TARGET)
@@ -555,6 +556,9 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* dl = getenv("NLP_DIRECT_LAUNCH")) {
     g->direct_launch = dl[0] == '1';
     if (g->direct_launch) g->use_graphs = false;
+  }
+  if (const char* ag = getenv("NLP_ASYNC_GRAPH")) {
+    g->async_direct = ag[0] != '1';
   }
   if (const char* gt = getenv("NLP_GR_NT")) g->gr_nt = atoi(gt) == 512 ? 512 : GR_NT;
   if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
@@ -2487,7 +2491,14 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     // 0.117 -> 0.111 ms each on C2, the event node costing GPU time per graph.
     static const bool stream_wait = !(getenv("NLP_STREAM_WAIT") && getenv("NLP_STREAM_WAIT")[0] == '0');
     const bool gseq = stream_wait && sorted;
-    if (sorted)
+    // asynchronous stamp-timed calls are launched kernel by kernel (below): the
+    // host's ~40 us of launches hide behind the previous call's kernels, and
+    // back-to-back graph launches leave ~10 us between graphs on the GPU
+    // (C2: 0.101 vs 0.109 ms per call)
+    const bool async_direct = async && stamps && g->async_direct;
+    if (sorted && async_direct)
+      replayed = false;
+    else if (sorted)
       s = run_graph(g, p, out, st, (msd ? 1 + sp.msd_passes : 1) + (sp.counted ? 16 : 0), sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps,
                     stamps && gseq);
@@ -2498,9 +2509,9 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     // NLP_DIRECT_LAUNCH=1 (stamp-timed sort path): kernels launched one by one,
     // no graph and no events -- the GPU starts after the first launch and the
     // later launches overlap the running kernels
-    const bool direct_nomark = stamps && g->direct_launch;
+    const bool direct_nomark = stamps && (g->direct_launch || async_direct);
     if (!replayed) {
-      if (async) return NLP_ERR_DEVICE;  // unreachable: async calls follow a replayed one
+      if (async && !direct_nomark) return NLP_ERR_DEVICE;  // unreachable: async calls follow a replayed one
       s = sorted ? launch_sp(g, p, sp, out, st, direct_nomark ? -2 : -1) : launch_fast(g, p, f, out, st, -1);
       if (s != NLP_OK) return s;
     }
@@ -2621,7 +2632,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if ((h[C_FLAGS] & F_TOOBIG) || h[C_W] > g->wedge_budget) return NLP_OK;
     *out_count = h[C_OUT_N];
     // the same call may be replayed without a wait next time (nlp_predict_device_async)
-    g->async_ok = sorted && attempt == 0 && replayed && g->last_single && stamps;
+    g->async_ok = sorted && attempt == 0 && ((replayed && g->last_single && stamps) || direct_nomark);
     if (g->async_ok) {
       async_key_of(p, g->async_key);
       g->async_out = out;

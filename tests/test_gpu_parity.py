@@ -746,16 +746,18 @@ def test_gpu_counted_passes_tiles_and_redo(gpu, oracle, n, avg, H, env):
             assert_canonical_equal(eu, ew, es, u, w, s)
 
 
-def test_gpu_async_batch_equals_sync(gpu, oracle):
+@pytest.mark.parametrize("env", [{}, dict(NLP_ASYNC_GRAPH="1")])
+def test_gpu_async_batch_equals_sync(gpu, oracle, env):
     """nlp_predict_device_async / nlp_sync: a call with no synchronous
     predecessor runs synchronously; after a synchronous call with the same
-    arguments the calls are only enqueued; a batch mixing both ends with the
-    last call's count and output; nlp_sync with nothing pending is refused."""
+    arguments the calls are only enqueued (kernel by kernel, or as replayed
+    graphs with NLP_ASYNC_GRAPH=1); a batch mixing both ends with the last
+    call's count and output; nlp_sync with nothing pending is refused."""
     import torch
     off, keys = random_csr(20000, 12, 31)
     k = 4000
     st = torch.cuda.current_stream()
-    with gpu.Graph(off, keys) as G:
+    with _env(**env), gpu.Graph(off, keys) as G:
         with pytest.raises(gpu.NlpError) as e:
             G.sync()
         assert e.value.status == 1
