@@ -55,7 +55,7 @@ def f1_on_device(G, out, n, du, dw):
     return p, r, (0.0 if p + r == 0 else 2 * p * r / (p + r))
 
 
-def cpu_baseline(off, keys, metric, hub, k, ncand):
+def cpu_baseline(off, keys, metric, hub, k, ncand, threads=None):
     """The reference's own OpenMP path (oracle/_ref/ref_driver, compiled from
     /root/reference/inc by oracle/Makefile) on this host's cores, same graph.
     maxEdges is capped at the candidate count: above it the reference's
@@ -66,6 +66,8 @@ def cpu_baseline(off, keys, metric, hub, k, ncand):
     except AttributeError:
         cores = os.cpu_count() or 1
     cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    if threads:
+        cores = threads
     metric_id = ["CN", "JAC", "SOR", "SAL", "HPI", "HDI", "LHN", "AA", "RA"].index(metric)
     me = min(k, ncand) if ncand else k
     with tempfile.TemporaryDirectory() as tmp:
@@ -266,6 +268,9 @@ def main():
                        "n": spec[0], "m": spec[1], "alpha": alpha, "M": ginfo["nnz"], "k": k,
                        "deletion_fraction": d, "parallelism": "source-range shards x%d" % world},
             "predicted": cnt,
+            # the reference's README quotes "edges/s" without a definition,
+            # so the graph's adjacency entries per second of prediction are reported too
+            "graph_entries_per_s": ginfo["nnz"] / (ms_per_step * 1e-3),
             "f1": f1, "precision": p, "recall": r,
             "score_ms": score_ms, "select_ms": select_ms,
             "host_overhead_ms": ms_per_step - score_ms - select_ms,
@@ -285,8 +290,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(off.cpu().numpy(), keys.cpu().numpy().view(np.uint32), metric,
-                                                    hub, k, cands)
+                h_off, h_keys = off.cpu().numpy(), keys.cpu().numpy().view(np.uint32)
+                line["cpu_baseline"] = cpu_baseline(h_off, h_keys, metric, hub, k, cands)
+                # the 1-thread time beside the all-cores one
+                line["cpu_baseline_1thread"] = cpu_baseline(h_off, h_keys, metric, hub, k, cands, threads=1)
             except Exception as e:  # report, never hide
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
