@@ -168,10 +168,12 @@ nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_m
  * wait, no counterpart in the reference).  Enqueues the same computation as
  * nlp_predict_device_ex on `stream` and returns at once when this handle's
  * last synchronous call had the same arguments and output array and ran as
- * one replayed graph; otherwise the call runs synchronously.  All calls of a
- * batch use one stream.  Results (d_out of each call, the last call's count
- * and timing) are valid after nlp_sync.  Not thread-safe with other calls on
- * the handle. */
+ * one replayed graph and `stream` is a caller stream (NULL: the call runs
+ * synchronously, ordered after all device work); otherwise the call runs
+ * synchronously.  All calls of a batch use one stream.  Results (d_out of each
+ * call, the last call's count and timing) are valid after nlp_sync; until then
+ * the synchronous predict entry points return NLP_ERR_INVALID.  Not
+ * thread-safe with other calls on the handle. */
 nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
                                     float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end,
                                     nlp_edge* d_out, void* stream);

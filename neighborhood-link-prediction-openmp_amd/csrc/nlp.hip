@@ -2862,6 +2862,7 @@ nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_m
                                  float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end, nlp_edge* d_out,
                                  uint64_t* out_count, nlp_timing* t, void* stream) {
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
+  if (g->async_pending) return NLP_ERR_INVALID;  // an asynchronous batch is in flight: nlp_sync first
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
   // the graph's own stream does not order after other streams: with no caller
@@ -2901,7 +2902,8 @@ nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hu
   async_key_of(p, key);
   g->last_out = nullptr;
   g->last_n = 0;
-  if (g->async_ok && g->async_out == (const void*)d_out && memcmp(key, g->async_key, sizeof key) == 0) {
+  // replayed only on a caller stream (the graph's own stream would need a device-wide wait first)
+  if (stream && g->async_ok && g->async_out == (const void*)d_out && memcmp(key, g->async_key, sizeof key) == 0) {
     bool handled = false;
     uint64_t cnt = 0;
     // a batch starts with a clean flag word (a synchronous call's own redos are no failure)
@@ -2981,6 +2983,7 @@ nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degr
                           float min_score, uint64_t max_edges, int repeat, nlp_edge* out, uint64_t* out_count,
                           nlp_timing* t) {
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8) return NLP_ERR_INVALID;
+  if (g->async_pending) return NLP_ERR_INVALID;  // an asynchronous batch is in flight: nlp_sync first
   if (repeat < 1) repeat = 1;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = g->stream;

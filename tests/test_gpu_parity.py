@@ -771,6 +771,9 @@ def test_gpu_async_batch_equals_sync(gpu, oracle, env):
                 out.zero_()
                 for _ in range(4):
                     G.predict_device_async(m, H, k, out, stream=st)
+                with pytest.raises(gpu.NlpError) as e:  # a batch is pending: synchronous calls are refused
+                    G.predict_device(m, H, k, out, stream=st)
+                assert e.value.status == 1
                 cnt, t = G.sync()
                 eu, ew, es = ref[(m, H)]
                 assert cnt == len(eu) and t["candidates"] >= cnt
