@@ -94,12 +94,6 @@ __global__ __launch_bounds__(256) void k_etab_build(const uint64_t* __restrict__
   }
 }
 
-// w in N(u)?  (u < w; the table when there is one, else a search of N(u))
-__device__ __forceinline__ bool first_order(const GraphView& g, uint32_t u, uint32_t w) {
-  if (g.etab) return et_has(g.etab, g.etbits, u, w);
-  return contains_u32(g.keys + g.off[u], g.deg[u], w);
-}
-
 // The reference's MAXFACTOR2 filter on second-hop keys (predict.hxx:221,295):
 // ft(w) = w > u && deg(u) <= F deg(u) && deg(w) <= F deg(u), size_t products.
 // Its first clause holds for F >= 1; the second is a per-(u, w) predicate, so a
@@ -118,6 +112,20 @@ __device__ __forceinline__ uint64_t edge_slot(uint32_t u, uint32_t w, uint32_t b
   x *= 0xc4ceb9fe1a85ec53ull;
   x ^= x >> 33;
   return x >> (64 - bits);
+}
+
+// w in N(u)?  (u < w; the table when there is one -- behind the edge filter
+// when both exist (NLP_EDGE_FILTER=2): a clear bit proves absence -- else a
+// search of N(u))
+__device__ __forceinline__ bool first_order(const GraphView& g, uint32_t u, uint32_t w) {
+  if (g.etab) {
+    if (g.efbits) {
+      const uint64_t h = edge_slot(u, w, g.efbits);
+      if (!((g.efilt[h >> 5] >> (h & 31)) & 1u)) return false;
+    }
+    return et_has(g.etab, g.etbits, u, w);
+  }
+  return contains_u32(g.keys + g.off[u], g.deg[u], w);
 }
 
 // One wave per row u: set the filter bit of every (u, w), w in N(u).

@@ -510,9 +510,10 @@ nlp_status finish_graph(nlp_graph* g) {
   // NLP_EDGE_FILTER=0 disables it.
   {
     const char* ef = getenv("NLP_EDGE_FILTER");
-    if (M > 0 && !g->etab && !(ef && ef[0] == '0')) {
+    const bool both = ef && ef[0] == '2';  // also in front of the table (8 slots per entry, ~128 MB on C2)
+    if (M > 0 && (!g->etab || both) && !(ef && ef[0] == '0')) {
       uint32_t bits = 20;
-      while (bits < 33 && (1ull << bits) < 16 * M) ++bits;
+      while (bits < 33 && (1ull << bits) < (both ? 8 : 16) * M) ++bits;
       size_t fr = 0, tot = 0;
       TRY(hipMemGetInfo(&fr, &tot));
       if ((1ull << bits) / 8 < fr / 16) {

@@ -703,7 +703,8 @@ def test_gpu_exclusion_without_edge_table(gpu, oracle):
 @pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"), dict(NLP_DIRECT="0"),
                                  dict(NLP_MSD_PASSES="2"), dict(NLP_FUSE_RUNS="0"), dict(NLP_DX_BITS="1"),
                                  dict(NLP_DX_BITS="2"), dict(NLP_DX_BITS="3"), dict(NLP_DX_BITS="12"),
-                                 dict(NLP_ORD11="1"), dict(NLP_GR_NT="512"), dict(NLP_COUNTED="0")])
+                                 dict(NLP_ORD11="1"), dict(NLP_GR_NT="512"), dict(NLP_COUNTED="0"),
+                                 dict(NLP_EDGE_FILTER="2")])
 def test_gpu_sort_path_variants_equal(gpu, oracle, env):
     """Sort-path build variants (fused output gather, several survivors per
     expansion thread, two MSD passes + group sort, separate grouping and
