@@ -53,6 +53,10 @@ def test_invalid_arguments_rejected_without_device(nlp):
     assert L.nlp_graph_create(None, None, 0, 0, ctypes.byref(h)) == 1
     cnt = ctypes.c_uint64()
     assert L.nlp_predict(None, 0, 4, 0.0, 10, 1, None, ctypes.byref(cnt), None) == 1
+    # the asynchronous pair: no handle, nothing pending
+    assert L.nlp_predict_device_async(None, 1, 4, 0, 0.0, 10, 0, 2**64 - 1, None, None) == 1
+    assert L.nlp_sync(None, ctypes.byref(cnt), None) == 1
+    assert L.nlp_status_string(6) == b"an asynchronous prediction needs a synchronous redo"
 
 
 def test_no_silent_cpu_fallback(nlp):
