@@ -168,9 +168,8 @@ nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_m
  * wait, no counterpart in the reference).  Enqueues the same computation as
  * nlp_predict_device_ex on `stream` and returns at once when this handle's
  * last synchronous call had the same arguments and output array and ran as
- * one replayed graph and `stream` is a caller stream (NULL: the call runs
- * synchronously, ordered after all device work); otherwise the call runs
- * synchronously.  All calls of a batch use one stream.  Results (d_out of each
+ * one replayed graph (`stream` NULL = the device's default stream); otherwise
+ * the call runs synchronously.  All calls of a batch use one stream.  Results (d_out of each
  * call, the last call's count and timing) are valid after nlp_sync; until then
  * the synchronous predict entry points return NLP_ERR_INVALID.  Not
  * thread-safe with other calls on the handle. */

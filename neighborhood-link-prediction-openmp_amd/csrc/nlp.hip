@@ -2896,15 +2896,16 @@ nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hu
                                     nlp_edge* d_out, void* stream) {
   if (!g || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
-  hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+  // NULL: the device's default stream (ordered after the caller's default-stream work without a
+  // device-wide wait; the synchronous entry points use the handle's own stream and a device sync)
+  hipStream_t st = (hipStream_t)stream;
   if (g->async_pending && st != g->async_stream) return NLP_ERR_INVALID;  // one stream per batch
   Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span), max_factor2};
   uint64_t key[6];
   async_key_of(p, key);
   g->last_out = nullptr;
   g->last_n = 0;
-  // replayed only on a caller stream (the graph's own stream would need a device-wide wait first)
-  if (stream && g->async_ok && g->async_out == (const void*)d_out && memcmp(key, g->async_key, sizeof key) == 0) {
+  if (g->async_ok && g->async_out == (const void*)d_out && memcmp(key, g->async_key, sizeof key) == 0) {
     bool handled = false;
     uint64_t cnt = 0;
     // a batch starts with a clean flag word (a synchronous call's own redos are no failure)
@@ -2929,7 +2930,6 @@ nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hu
   uint64_t cnt = 0;
   nlp_timing tt;
   memset(&tt, 0, sizeof(tt));
-  if (!stream && hipDeviceSynchronize() != hipSuccess) return NLP_ERR_DEVICE;
   nlp_status s = predict_impl(g, p, (EdgeOut*)d_out, &cnt, &tt, st, nullptr);
   if (s != NLP_OK) return s;
   ++g->async_pending;
