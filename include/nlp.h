@@ -180,9 +180,11 @@ nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hu
 /* Wait for the batch of nlp_predict_device_async calls: *out_count and t of
  * the last one.  NLP_ERR_RETRY when any call of the batch hit a condition the
  * synchronous path handles by redoing the call (a bucket or buffer overflow,
- * more candidate tiles than the counted passes hold): its output is not
- * valid, the caller redoes it with nlp_predict_device_ex.  NLP_ERR_INVALID
- * when nothing is pending. */
+ * more candidate tiles than the counted passes hold).  Which call failed is
+ * not known, and the calls after it ran on scratch state the failed call left
+ * behind: EVERY output of the batch is invalid, and the caller redoes every
+ * call of the batch with nlp_predict_device_ex.  NLP_ERR_INVALID when nothing
+ * is pending. */
 nlp_status nlp_sync(nlp_graph* g, uint64_t* out_count, nlp_timing* t);
 
 /* Merge step of the multi-GPU path: given `n` device-resident edges that are the

@@ -259,7 +259,7 @@ class Graph:
         # the per-call Python is part of every step: the output tensor's checks
         # are remembered for the same tensor and size, the result structs reused
         need = 3 * int(max_edges)
-        memo = (id(out), out.data_ptr(), need)
+        memo = (id(out), out.data_ptr(), need, out.dtype, out.is_contiguous(), out.numel())
         if getattr(self, "_out_ok", None) != memo:
             _check_tensor(out, "out", _edge_dtypes(), self.device, need)
             self._out_ok = memo
@@ -278,7 +278,7 @@ class Graph:
         host wait (it runs synchronously unless the same call last ran
         synchronously as one replayed graph); results after sync()."""
         need = 3 * int(max_edges)
-        memo = (id(out), out.data_ptr(), need)
+        memo = (id(out), out.data_ptr(), need, out.dtype, out.is_contiguous(), out.numel())
         if getattr(self, "_out_ok", None) != memo:
             _check_tensor(out, "out", _edge_dtypes(), self.device, need)
             self._out_ok = memo

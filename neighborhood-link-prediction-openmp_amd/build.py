@@ -14,8 +14,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libnlp.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("nlp.hip",)]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in ("prims.hpp", "kernels.hpp", "lookback.hpp", "group.hpp", "select.hpp", "sortpath.hpp")] + \
-    [os.path.join(ROOT, "include", "nlp.h")]
+
+
+def deps():
+    """Every file the library is built from: the sources, every header under
+    csrc/ (globbed, so a new header is never missed) and the C-ABI header."""
+    import glob
+    return SOURCES + sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp"))) + [os.path.join(ROOT, "include", "nlp.h")]
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -35,7 +40,7 @@ def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(d) > t for d in DEPS if os.path.exists(d))
+    return any(os.path.getmtime(d) > t for d in deps() if os.path.exists(d))
 
 
 CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "predict_main.cxx")

@@ -1895,9 +1895,13 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
   f.arena_words = f.d_cm + 4 * (uint64_t)CP_MAXT * RS_BINS / 2;
   TRY(wsget(ws, B_SP_ARENA, f.arena_words, &f.arena));
   f.zero = ArenaZero{{0, 0, 0}, {f.arena_words, 0, 0}};
-  if (f.fused) f.zero = ArenaZero{{0, SP_HORD, 0}, {SP_HREC, f.d_surv, 0}};
+  // without the degree-class index k_sp_survivors runs: its look-back
+  // descriptors [d_surv, d_exp) are reset with the counters (an earlier call
+  // with another survivor set, or a new arena, leaves them dirty)
+  const uint64_t zend = f.dindex ? f.d_surv : f.d_exp;
+  if (f.fused) f.zero = ArenaZero{{0, SP_HORD, 0}, {SP_HREC, zend, 0}};
   // counted passes: no score-digit histogram copies to reset (the tickets: the survivor scan's)
-  if (f.counted) f.zero = ArenaZero{{0, SP_DESC, 0}, {SP_HREC, f.d_surv, 0}};
+  if (f.counted) f.zero = ArenaZero{{0, SP_DESC, 0}, {SP_HREC, zend, 0}};
   return NLP_OK;
 }
 
@@ -2709,6 +2713,10 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   // Adamic-Adar / Resource-Allocation stay on the sort paths unless forced: their
   // ordered sums of three or more contributions re-walk intersections in path 4
   const bool custom = p.metric == M_AA || p.metric == M_RA;
+  // a synchronous call may change what an asynchronous replay would rebuild
+  // (capacities, the grouping memo, the range index): only the call that ends
+  // eligible below may be replayed
+  g->async_ok = false;
   const bool use_hash = !g->force_radix && p.max_edges > 0 &&
                         (g->hash_mode > 0 ||
                          (g->hash_mode == 0 && !custom && hp_estimate(g, p) > (double)g->hp_min_wedges));

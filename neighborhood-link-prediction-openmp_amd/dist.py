@@ -1,5 +1,5 @@
 """Multi-GPU link prediction: one process per GPU, source-vertex range shards,
-one exchange step over RCCL (torch.distributed backend "nccl" on ROCm).
+one selection exchange over RCCL (torch.distributed backend "nccl" on ROCm).
 
 SURVEY.md §8(e).  The reference has a single OpenMP team over source vertices
 (predict.hxx:287, schedule(dynamic, 2048)) and merges per-thread heaps serially
@@ -8,19 +8,26 @@ SURVEY.md §8(e).  The reference has a single OpenMP team over source vertices
   1. every rank holds a full CSR replica (second-hop lists are arbitrary, so
      the adjacency cannot be partitioned) and predicts the canonical top-k of
      its own contiguous source range [u_begin, u_end)  -> nlp_predict_device;
-  2. ONE all_gather over xGMI of fixed-stride blocks: entry 0 of a rank's
-     block is a header with its count, entries 1..n its top-k list.  The
-     stride is learnt once per job (one extra all_gather of the counts on the
-     first call) and kept; a block that outgrows it is seen by every rank in
-     the gathered headers, and all ranks regather with a larger stride;
-  3. every rank merges in one kernel: block order is u order, so ranking each
+     the ranges balance the per-source wedge estimate (source_weights);
+  2. histogram-first selection (select_quota): every rank histograms the top
+     16 bits of its result's score keys, one all_reduce(sum) gives the global
+     histogram and the bin of the k-th key; a second all_reduce of the low 16
+     bits inside that bin gives the k-th key itself.  Every rank then knows how
+     many of its links rank above it; one all_gather of two counts per rank
+     hands out the tie quota in rank (= u) order, the canonical tie rule.  A
+     rank's share of the global top-k is a PREFIX of its canonical list;
+  3. ONE all_gather of exactly those prefixes (block stride = the largest
+     share + 1 header entry): about 12 k bytes in total instead of every
+     rank's whole local top-k;
+  4. every rank merges in one kernel: block order is u order, so ranking each
      entry against the other blocks by score (ties: lower block first) gives
      exactly the single-GPU canonical result        -> nlp_merge_blocks_device.
 
 Every rank ends with the identical global result (so rank 0 can report it
 and any rank can evaluate F1).  The local predictor and the merge are
 injectable so that the same orchestration runs under gloo on the CPU in the
-tests (with the oracle standing in for the device kernels there).
+tests (with the oracle standing in for the device kernels there); with the
+gloo backend the collectives run on CPU copies of the small tensors.
 """
 import torch
 import torch.distributed as dist
@@ -76,7 +83,8 @@ BLOCK_MAGIC = 0x4E4C5042  # nlp.h NLP_BLOCK_MAGIC
 
 class BlockOverflow(RuntimeError):
     """A gathered block held more entries than the exchange stride (count = the
-    largest block count); the exchange regathers with a larger stride."""
+    largest block count).  With the quota exchange the stride is exact, so this
+    means the blocks were corrupted in transit."""
 
     def __init__(self, count):
         super().__init__("block count %d exceeds the exchange stride" % count)
@@ -84,17 +92,11 @@ class BlockOverflow(RuntimeError):
 
 
 class Exchange:
-    """Exchange state of one sharded job.  `cap` (entries per gathered block,
-    header excluded) is identical on every rank: it is set from gathered data
-    only, so every rank takes the same branch."""
+    """Exchange state of one sharded job: the shard bounds (the weights' prefix
+    sum is O(span), computed once)."""
 
     def __init__(self):
-        self.cap = None
-        self.ranges = None  # shard bounds, computed once (the weights' prefix sum is O(span))
-
-
-def _grow(mx, max_edges):
-    return int(min(max_edges, max(1024, mx + mx // 16)))
+        self.ranges = None
 
 
 def write_header(block, n):
@@ -110,14 +112,76 @@ def block_counts(blocks):
     return [int(lo) | (int(hi) << 32) for lo, hi in h.tolist()]
 
 
-def gather_blocks(block, cap, group=None):
-    """One all_gather of every rank's first cap + 1 entries (header + result)
-    into [world, cap + 1, 3]."""
+def _coll(t, group=None):
+    """The tensor the collective runs on: gloo takes CPU tensors."""
+    return t.cpu() if dist.get_backend(group) == "gloo" and t.is_cuda else t
+
+
+def score_keys(edges, n):
+    """Order-preserving uint32 keys (as int64) of the scores in edges[:n, 2]
+    (int32 bit patterns): larger score -> larger key, -0 == +0, NaN -> 0 --
+    the library's score_key (kernels.hpp) and the oracle's nlpo_score_key."""
+    b = edges[:n, 2].to(torch.int64) & 0xFFFFFFFF
+    b = torch.where(b == 0x80000000, torch.zeros_like(b), b)  # -0.0 -> +0.0
+    neg = (b & 0x80000000) != 0
+    k = torch.where(neg, (~b) & 0xFFFFFFFF, b | 0x80000000)
+    nan = ((b & 0x7F800000) == 0x7F800000) & ((b & 0x007FFFFF) != 0)
+    return torch.where(nan, torch.zeros_like(k), k)
+
+
+def select_quota(edges, n, max_edges, group=None):
+    """Histogram-first global selection.  `edges[:n]` is this
+    rank's canonical list (score key desc, then u, then w).  Returns (share,
+    shares): how many leading entries of this rank's list belong to the
+    canonical global top max_edges, and every rank's share (rank order)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    keys = score_keys(edges, n)
+    hi = torch.bincount(keys >> 16, minlength=1 << 16) if n else torch.zeros(1 << 16, dtype=torch.int64,
+                                                                             device=edges.device)
+    hi = _coll(hi, group)
+    dist.all_reduce(hi, group=group)  # the one histogram exchange for the top 16 bits
+    total = int(hi.sum())
+    take = min(int(max_edges), total)
+    if take == total:  # every candidate is kept: no boundary key
+        kth, above_all = -1, 0
+    else:
+        from_top = torch.cumsum(hi.flip(0), 0)
+        b = (1 << 16) - 1 - int(torch.searchsorted(from_top, torch.tensor(take, dtype=from_top.dtype)))
+        above_all = int(hi[b + 1:].sum())
+        sel = keys[(keys >> 16) == b]
+        lo = torch.bincount(sel & 0xFFFF, minlength=1 << 16) if sel.numel() else \
+            torch.zeros(1 << 16, dtype=torch.int64, device=edges.device)
+        lo = _coll(lo, group)
+        dist.all_reduce(lo, group=group)
+        from_top = torch.cumsum(lo.flip(0), 0)
+        l = (1 << 16) - 1 - int(torch.searchsorted(from_top, torch.tensor(take - above_all, dtype=from_top.dtype)))
+        above_all += int(lo[l + 1:].sum())
+        kth = (b << 16) | l
+    if kth < 0:
+        mine = torch.tensor([n, 0], dtype=torch.int64)
+    else:
+        mine = torch.stack([(keys > kth).sum(), (keys == kth).sum()]).cpu()
+    both = torch.empty(2 * world, dtype=torch.int64)
+    mine, both = _coll(mine.to(edges.device), group), _coll(both.to(edges.device), group)
+    dist.all_gather_into_tensor(both, mine, group=group)
+    both = both.cpu().view(world, 2).tolist()
+    quota = take - above_all
+    shares = []
+    for a, t in both:
+        q = min(t, max(quota, 0))
+        quota -= q
+        shares.append(a + q)
+    return shares[rank], shares
+
+
+def gather_blocks(block, stride, group=None):
+    """One all_gather of every rank's first `stride` entries (header + its
+    share) into [world, stride, 3]."""
     world = dist.get_world_size(group)
-    stride = cap + 1
-    recv = torch.empty((world * stride, 3), dtype=block.dtype, device=block.device)
-    dist.all_gather_into_tensor(recv, block[:stride].contiguous(), group=group)
-    return recv.view(world, stride, 3)
+    send = _coll(block[:stride].contiguous(), group)
+    recv = torch.empty((world * stride, 3), dtype=block.dtype, device=send.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return recv.to(block.device).view(world, stride, 3)
 
 
 def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=None, state=None):
@@ -125,10 +189,8 @@ def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=N
 
     local_predict(u_begin, u_end) -> (block [>= max_edges + 1, 3] int32 tensor
         whose entries 1..n hold the shard's canonical result, n, info)
-    merge(blocks [world, stride, 3], max_edges) -> (edges [>= k, 3], k); raises
-        BlockOverflow when a header count exceeds stride - 1
-    state: an Exchange kept across calls (the stride learnt by the first call);
-        a fresh one costs one extra all_gather of the counts.
+    merge(blocks [world, stride, 3], max_edges) -> (edges [>= k, 3], k)
+    state: an Exchange kept across calls (the shard bounds).
     Returns (edges, k, info) -- identical on every rank."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     state = state if state is not None else Exchange()
@@ -136,22 +198,13 @@ def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=N
         state.ranges = shard_ranges(span, world, weights)
     ub, ue = state.ranges[rank]
     block, n, info = local_predict(ub, ue)
-    if block.shape[0] < max_edges + 1:
-        raise ValueError("local block must hold max_edges + 1 entries")
-    write_header(block, n)
-    if state.cap is None:
-        cnt = torch.tensor([n], dtype=torch.int64, device=block.device)
-        counts = torch.empty(world, dtype=torch.int64, device=block.device)
-        dist.all_gather_into_tensor(counts, cnt, group=group)
-        state.cap = _grow(int(counts.max()), max_edges)
-    while True:
-        blocks = gather_blocks(block, state.cap, group)
-        try:
-            out, k = merge(blocks, max_edges)
-            break
-        except BlockOverflow as e:  # every rank sees the same headers, so all regather
-            state.cap = _grow(e.count, max_edges)
-    info = dict(info or {}, shard=(ub, ue), blocks=blocks, stride=state.cap + 1)
+    if block.shape[0] < min(n, max_edges) + 1:
+        raise ValueError("local block must hold the result + 1 header entry")
+    share, shares = select_quota(block[1:], n, max_edges, group)
+    write_header(block, share)
+    blocks = gather_blocks(block, max(shares) + 1, group)
+    out, k = merge(blocks, max_edges)
+    info = dict(info or {}, shard=(ub, ue), blocks=blocks, stride=max(shares) + 1, shares=shares, local_count=n)
     return out, k, info
 
 

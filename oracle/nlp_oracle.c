@@ -121,70 +121,112 @@ static int cmp_cand(const void *x, const void *y) {
   return 0;
 }
 
+/* Per-source scratch of the reference's loop (predict.hxx:280-283): the dense
+ * counter table veout (count or float accumulator) and the touched list vedgs. */
+typedef struct {
+  uint32_t *cnt;
+  float *acc;
+  uint32_t *touched;
+} tables_t;
+
+static int tables_alloc(tables_t *t, uint64_t span, int custom) {
+  t->cnt = (uint32_t *)calloc(span ? span : 1, sizeof(uint32_t));
+  t->acc = custom ? (float *)calloc(span ? span : 1, sizeof(float)) : NULL;
+  t->touched = (uint32_t *)malloc((span ? span : 1) * sizeof(uint32_t));
+  return (!t->cnt || !t->touched || (custom && !t->acc)) ? -1 : 0;
+}
+
+static void tables_free(tables_t *t) {
+  free(t->cnt); free(t->acc); free(t->touched);
+  t->cnt = NULL; t->acc = NULL; t->touched = NULL;
+}
+
+typedef int (*emit_fn)(void *arg, uint32_t u, uint32_t w, float s, uint32_t key);
+
+/*
+ * One source u of predictLinksWithIntersectionLoopU (predict.hxx:214-265):
+ * emits every candidate (u, w, score) with score > min_score (or NaN) in
+ * ascending w.  Adds the wedges the reference scans (SURVEY §8(d) W_H) and
+ * those with w > u (the wedges that reach the counter table).
+ */
+static int scan_source(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                       int metric, uint32_t hub, uint32_t maxf2, float min_score, uint64_t u,
+                       tables_t *tb, emit_fn emit, void *arg, uint64_t *wedges, uint64_t *wedges_gt) {
+  int custom = (metric == NLPO_AA || metric == NLPO_RA);
+  uint32_t *cnt = tb->cnt, *touched = tb->touched;
+  float *acc = tb->acc;
+  size_t nt = 0;
+  uint64_t du = off[u + 1] - off[u];
+  /* wedge scan: predict.hxx:224-230 -> 153-179 */
+  for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
+    uint32_t v = keys[i];
+    uint64_t dv = v < span ? off[v + 1] - off[v] : 0;
+    if (hub && dv > hub) continue;                /* predict.hxx:227 */
+    double c = custom ? contrib(metric, dv) : 0.0;
+    for (uint64_t j = off[v]; j < off[v + 1]; ++j) {
+      uint32_t w = keys[j];
+      ++*wedges;
+      if (!(w > u)) continue;                      /* ft: predict.hxx:221 */
+      ++*wedges_gt;
+      if (maxf2 && (w < span ? off[w + 1] - off[w] : 0) > (uint64_t)maxf2 * du)
+        continue;                                  /* ft, MAXFACTOR2 clause */
+      if (custom) {
+        if (!acc[w]) touched[nt++] = w;            /* predict.hxx:176 */
+        acc[w] = (float)((double)acc[w] + c);      /* fu: entry += 1.0/..  */
+      } else {
+        if (!cnt[w]) touched[nt++] = w;            /* predict.hxx:157 */
+        ++cnt[w];
+      }
+    }
+  }
+  /* first-order exclusion, predict.hxx:232-233 */
+  if (custom) acc[u] = 0.0f; else cnt[u] = 0;
+  for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
+    if (custom) acc[keys[i]] = 0.0f; else cnt[keys[i]] = 0;
+  }
+  /* canonical w order inside u (the reference scores in first-touch order,
+     which only matters for ties, A.1) */
+  qsort(touched, nt, sizeof(uint32_t), cmp_u32);
+  int rc = 0;
+  for (size_t t = 0; t < nt; ++t) {
+    uint32_t w = touched[t];
+    float s;
+    if (custom) s = acc[w];                        /* fs = W(Nuv) */
+    else {
+      uint64_t dw = w < span ? off[w + 1] - off[w] : 0;
+      s = score_basic(metric, cnt[w], du, dw);
+    }
+    if (custom) acc[w] = 0.0f; else cnt[w] = 0;    /* predictClearScanW 187-192 */
+    if (s <= min_score) continue;                  /* predict.hxx:237 (NaN passes) */
+    if (!rc && emit(arg, (uint32_t)u, w, s, nlpo_score_key(s))) rc = -1;
+  }
+  return rc;
+}
+
+static int emit_push(void *arg, uint32_t u, uint32_t w, float s, uint32_t key) {
+  cand_t cd = {u, w, s, key};
+  return cvec_push((cvec_t *)arg, cd);
+}
+
 /*
  * Enumerate every candidate (u, w, score) with score > min_score (or NaN) for
  * u in [u_begin, u_end), in (u asc, w asc) order.  Returns 0 on success.
- * Also reports the wedge count the reference scans (SURVEY §8(d) W_H) and
- * the number of those with w > u (the wedges that reach the counter table).
  */
 static int enumerate(const uint64_t *off, const uint32_t *keys, uint64_t span,
                      int metric, uint32_t hub, uint32_t maxf2, float min_score,
                      uint64_t u_begin, uint64_t u_end, cvec_t *out,
                      uint64_t *wedges_out, uint64_t *wedges_gt_out) {
   int custom = (metric == NLPO_AA || metric == NLPO_RA);
-  uint32_t *cnt = (uint32_t *)calloc(span ? span : 1, sizeof(uint32_t));
-  float *acc = custom ? (float *)calloc(span ? span : 1, sizeof(float)) : NULL;
-  uint32_t *touched = (uint32_t *)malloc((span ? span : 1) * sizeof(uint32_t));
+  tables_t tb;
   uint64_t wedges = 0, wedges_gt = 0;
-  if (!cnt || !touched || (custom && !acc)) { free(cnt); free(acc); free(touched); return -1; }
+  if (tables_alloc(&tb, span, custom)) { tables_free(&tb); return -1; }
   for (uint64_t u = u_begin; u < u_end && u < span; ++u) {
-    size_t nt = 0;
-    uint64_t du = off[u + 1] - off[u];
-    /* wedge scan: predict.hxx:224-230 -> 153-179 */
-    for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
-      uint32_t v = keys[i];
-      uint64_t dv = v < span ? off[v + 1] - off[v] : 0;
-      if (hub && dv > hub) continue;                /* predict.hxx:227 */
-      double c = custom ? contrib(metric, dv) : 0.0;
-      for (uint64_t j = off[v]; j < off[v + 1]; ++j) {
-        uint32_t w = keys[j];
-        ++wedges;
-        if (!(w > u)) continue;                      /* ft: predict.hxx:221 */
-        ++wedges_gt;
-        if (maxf2 && (w < span ? off[w + 1] - off[w] : 0) > (uint64_t)maxf2 * du)
-          continue;                                  /* ft, MAXFACTOR2 clause */
-        if (custom) {
-          if (!acc[w]) touched[nt++] = w;            /* predict.hxx:176 */
-          acc[w] = (float)((double)acc[w] + c);      /* fu: entry += 1.0/..  */
-        } else {
-          if (!cnt[w]) touched[nt++] = w;            /* predict.hxx:157 */
-          ++cnt[w];
-        }
-      }
-    }
-    /* first-order exclusion, predict.hxx:232-233 */
-    if (custom) acc[u] = 0.0f; else cnt[u] = 0;
-    for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
-      if (custom) acc[keys[i]] = 0.0f; else cnt[keys[i]] = 0;
-    }
-    /* canonical w order inside u (the reference scores in first-touch order,
-       which only matters for ties, A.1) */
-    qsort(touched, nt, sizeof(uint32_t), cmp_u32);
-    for (size_t t = 0; t < nt; ++t) {
-      uint32_t w = touched[t];
-      float s;
-      if (custom) s = acc[w];                        /* fs = W(Nuv) */
-      else {
-        uint64_t dw = w < span ? off[w + 1] - off[w] : 0;
-        s = score_basic(metric, cnt[w], du, dw);
-      }
-      if (custom) acc[w] = 0.0f; else cnt[w] = 0;    /* predictClearScanW 187-192 */
-      if (s <= min_score) continue;                  /* predict.hxx:237 (NaN passes) */
-      cand_t cd = {(uint32_t)u, w, s, nlpo_score_key(s)};
-      if (cvec_push(out, cd)) { free(cnt); free(acc); free(touched); return -1; }
+    if (scan_source(off, keys, span, metric, hub, maxf2, min_score, u, &tb, emit_push, out, &wedges, &wedges_gt)) {
+      tables_free(&tb);
+      return -1;
     }
   }
-  free(cnt); free(acc); free(touched);
+  tables_free(&tb);
   if (wedges_out) *wedges_out = wedges;
   if (wedges_gt_out) *wedges_gt_out = wedges_gt;
   return 0;
@@ -272,4 +314,277 @@ int nlpo_count_candidates(const uint64_t *off, const uint32_t *keys, uint64_t sp
                           uint64_t *n_candidates, uint64_t *n_wedges) {
   return nlpo_predict(off, keys, span, metric, hub, min_score, 0, NULL, NULL, NULL,
                       NULL, n_candidates, NULL, n_wedges);
+}
+
+/* ------------------------------------------------------------------------
+ * Parallel restatement for the full-size configs.
+ *
+ * The same per-source scan (scan_source, predict.hxx:214-265) over the source
+ * range cut into chunks of consecutive u, run by OpenMP threads with one set
+ * of tables each -- the reference's own parallelisation (predict.hxx:284-339,
+ * one table per thread), without its per-thread heaps.  Candidates are never
+ * all stored; four passes over the sources:
+ *   A  count the candidates, histogram of key >> 16     -> take = min(k, C)
+ *   B  histogram of key & 0xffff inside the boundary bin -> k-th key, tie quota
+ *   C  per chunk: candidates above the k-th key, ties at it
+ *   D  per chunk: write the kept ones (all above, ties while the chunk's share
+ *      of the quota lasts -- chunks ascend in u, so this is the canonical
+ *      (u asc, w asc) tie fill) at the chunk's prefix offset
+ * then a stable LSD radix sort by descending key puts the kept set in the
+ * canonical order (score desc, u asc, w asc).  The digest (sum and xor of
+ * nlpo_edge_hash over the kept set) is order-free, for checks that do not
+ * copy the result.
+ * ------------------------------------------------------------------------ */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* splitmix64 finaliser */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* Hash of one predicted link: (u, w) and the score bits (NaN canonicalised). */
+uint64_t nlpo_edge_hash(uint32_t u, uint32_t w, float s) {
+  uint32_t b;
+  if (s != s) b = 0x7fc00000u;
+  else memcpy(&b, &s, 4);
+  return mix64((((uint64_t)u << 32) | w) ^ ((uint64_t)b * 0x9E3779B97F4A7C15ull));
+}
+
+typedef struct {
+  uint64_t *hist;       /* pass A: 65536 bins of key >> 16; pass B: of key & 0xffff */
+  uint32_t hi;          /* pass B: the boundary bin */
+  uint32_t kth;         /* passes C, D */
+  uint64_t above, ties; /* pass C: this chunk's counts */
+  uint64_t ncand, nnan;
+  cand_t *dst;          /* pass D: the chunk's slice */
+  uint64_t quota;       /* pass D: ties this chunk keeps */
+  uint64_t n;           /* pass D: written */
+  uint64_t dsum, dxor;
+  int all;              /* pass D: keep every candidate */
+} pass_t;
+
+static int emit_a(void *arg, uint32_t u, uint32_t w, float s, uint32_t key) {
+  pass_t *p = (pass_t *)arg;
+  (void)u; (void)w; (void)s;
+  p->hist[key >> 16]++;
+  p->ncand++;
+  p->nnan += (key == 0);
+  return 0;
+}
+
+static int emit_b(void *arg, uint32_t u, uint32_t w, float s, uint32_t key) {
+  pass_t *p = (pass_t *)arg;
+  (void)u; (void)w; (void)s;
+  if ((key >> 16) == p->hi) p->hist[key & 0xffff]++;
+  return 0;
+}
+
+static int emit_c(void *arg, uint32_t u, uint32_t w, float s, uint32_t key) {
+  pass_t *p = (pass_t *)arg;
+  (void)u; (void)w; (void)s;
+  if (key > p->kth) p->above++;
+  else if (key == p->kth) p->ties++;
+  return 0;
+}
+
+static int emit_d(void *arg, uint32_t u, uint32_t w, float s, uint32_t key) {
+  pass_t *p = (pass_t *)arg;
+  if (p->all || key > p->kth || (key == p->kth && p->quota)) {
+    if (!p->all && key == p->kth) p->quota--;
+    cand_t c = {u, w, s, key};
+    p->dst[p->n++] = c;
+    uint64_t h = nlpo_edge_hash(u, w, s);
+    p->dsum += h;
+    p->dxor ^= h;
+  }
+  return 0;
+}
+
+/* Stable LSD radix sort by descending key (the input is in (u, w) order). */
+static int sort_desc(cand_t *a, uint64_t n) {
+  if (n < 2) return 0;
+  cand_t *tmp = (cand_t *)malloc(n * sizeof(cand_t));
+  if (!tmp) return -1;
+  cand_t *src = a, *dst = tmp;
+  for (int sh = 0; sh < 32; sh += 8) {
+    uint64_t cnt[257];
+    memset(cnt, 0, sizeof cnt);
+    for (uint64_t i = 0; i < n; ++i) cnt[((~src[i].key) >> sh & 255) + 1]++;
+    for (int b = 0; b < 256; ++b) cnt[b + 1] += cnt[b];
+    for (uint64_t i = 0; i < n; ++i) dst[cnt[(~src[i].key) >> sh & 255]++] = src[i];
+    cand_t *t = src; src = dst; dst = t;
+  }
+  /* four passes: the result is back in a */
+  free(tmp);
+  return 0;
+}
+
+/*
+ * nlpo_predict_par: canonical top max_edges of [u_begin, u_end) with `threads`
+ * OpenMP threads (0 = the OpenMP default).  out_u/out_w/out_score (nullable)
+ * receive the result in canonical order.  stats[0..7] = out_count,
+ * candidates, NaN candidates, wedges, wedges (w > u), k-th key, digest sum,
+ * digest xor.  Returns 0, or -1 on allocation failure.
+ */
+int nlpo_predict_par(const uint64_t *off, const uint32_t *keys, uint64_t span,
+                     int metric, uint32_t hub, uint32_t maxf2, float min_score, uint64_t max_edges,
+                     uint64_t u_begin, uint64_t u_end, int threads,
+                     uint32_t *out_u, uint32_t *out_w, float *out_score, uint64_t *stats) {
+  int custom = (metric == NLPO_AA || metric == NLPO_RA);
+  if (u_end > span) u_end = span;
+  if (u_begin > u_end) u_begin = u_end;
+  for (int i = 0; i < 8; ++i) stats[i] = 0;
+  int T = 1;
+#ifdef _OPENMP
+  T = threads > 0 ? threads : omp_get_max_threads();
+#else
+  (void)threads;
+#endif
+  const uint64_t nu = u_end - u_begin;
+  const uint64_t nch = nu == 0 ? 1 : (nu < 16384 ? nu : 16384);
+  uint64_t *above = (uint64_t *)calloc(nch, 8), *ties = (uint64_t *)calloc(nch, 8);
+  uint64_t *hist = (uint64_t *)calloc((size_t)T * 65536, 8);
+  tables_t *tb = (tables_t *)calloc(T, sizeof(tables_t));
+  int fail = !above || !ties || !hist || !tb;
+  for (int t = 0; t < T && !fail; ++t) fail = tables_alloc(&tb[t], span, custom);
+  uint64_t wedges = 0, wedges_gt = 0, ncand = 0, nnan = 0;
+  cand_t *kept = NULL;
+#define CHUNK_LO(c) (u_begin + nu * (uint64_t)(c) / nch)
+#define CHUNK_HI(c) (u_begin + nu * (uint64_t)((c) + 1) / nch)
+  /* pass A */
+  if (!fail) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T) reduction(+ : wedges, wedges_gt, ncand, nnan)
+    for (int64_t c = 0; c < (int64_t)nch; ++c) {
+      int t = 0;
+#ifdef _OPENMP
+      t = omp_get_thread_num();
+#endif
+      pass_t p;
+      memset(&p, 0, sizeof p);
+      p.hist = hist + (size_t)t * 65536;
+      for (uint64_t u = CHUNK_LO(c); u < CHUNK_HI(c); ++u)
+        scan_source(off, keys, span, metric, hub, maxf2, min_score, u, &tb[t], emit_a, &p, &wedges, &wedges_gt);
+      above[c] = p.ncand;  /* all kept when take == ncand: pass C is skipped */
+      ncand += p.ncand;
+      nnan += p.nnan;
+    }
+  }
+  uint64_t take = ncand < max_edges ? ncand : max_edges;
+  uint32_t kth = 0;
+  uint64_t quota = 0;
+  if (!fail && take > 0 && take < ncand) {
+    uint64_t acc = 0;
+    int b = 65535;
+    for (; b >= 0; --b) {
+      uint64_t h = 0;
+      for (int t = 0; t < T; ++t) h += hist[(size_t)t * 65536 + b];
+      if (acc + h >= take) break;
+      acc += h;
+    }
+    memset(hist, 0, (size_t)T * 65536 * 8);
+    uint64_t dummy0 = 0, dummy1 = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T) reduction(+ : dummy0, dummy1)
+    for (int64_t c = 0; c < (int64_t)nch; ++c) {
+      int t = 0;
+#ifdef _OPENMP
+      t = omp_get_thread_num();
+#endif
+      pass_t p;
+      memset(&p, 0, sizeof p);
+      p.hist = hist + (size_t)t * 65536;
+      p.hi = (uint32_t)b;
+      for (uint64_t u = CHUNK_LO(c); u < CHUNK_HI(c); ++u)
+        scan_source(off, keys, span, metric, hub, maxf2, min_score, u, &tb[t], emit_b, &p, &dummy0, &dummy1);
+    }
+    int l = 65535;
+    for (; l >= 0; --l) {
+      uint64_t h = 0;
+      for (int t = 0; t < T; ++t) h += hist[(size_t)t * 65536 + l];
+      if (acc + h >= take) break;
+      acc += h;
+    }
+    kth = ((uint32_t)b << 16) | (uint32_t)l;
+    quota = take - acc;
+  }
+  /* passes C and D (with take == ncand every candidate is kept: kth = 0 and
+     all ties -- key 0 = NaN -- fit the quota) */
+  if (!fail && take > 0) {
+    if (take == ncand) quota = 0;  /* above[c] (pass A) already counts every candidate, NaN included */
+    uint64_t dummy0 = 0, dummy1 = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T) reduction(+ : dummy0, dummy1)
+    for (int64_t c = 0; c < (int64_t)(take < ncand ? nch : 0); ++c) {
+      int t = 0;
+#ifdef _OPENMP
+      t = omp_get_thread_num();
+#endif
+      pass_t p;
+      memset(&p, 0, sizeof p);
+      p.kth = kth;
+      for (uint64_t u = CHUNK_LO(c); u < CHUNK_HI(c); ++u)
+        scan_source(off, keys, span, metric, hub, maxf2, min_score, u, &tb[t], emit_c, &p, &dummy0, &dummy1);
+      above[c] = p.above;
+      ties[c] = p.ties;
+    }
+    kept = (cand_t *)malloc((take ? take : 1) * sizeof(cand_t));
+    fail = !kept;
+  }
+  uint64_t dsum = 0, dxor = 0;
+  if (!fail && take > 0) {
+    /* each chunk's slice and tie share, in chunk (= u) order */
+    uint64_t *base = (uint64_t *)malloc(nch * 8), *share = (uint64_t *)malloc(nch * 8);
+    fail = !base || !share;
+    if (!fail) {
+      uint64_t pos = 0, q = quota;
+      for (uint64_t c = 0; c < nch; ++c) {
+        share[c] = ties[c] < q ? ties[c] : q;
+        q -= share[c];
+        base[c] = pos;
+        pos += above[c] + share[c];
+      }
+      uint64_t dummy0 = 0, dummy1 = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(T) reduction(+ : dummy0, dummy1, dsum) reduction(^ : dxor)
+      for (int64_t c = 0; c < (int64_t)nch; ++c) {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        pass_t p;
+        memset(&p, 0, sizeof p);
+        p.kth = kth;
+        p.quota = share[c];
+        p.all = take == ncand;
+        p.dst = kept + base[c];
+        for (uint64_t u = CHUNK_LO(c); u < CHUNK_HI(c); ++u)
+          scan_source(off, keys, span, metric, hub, maxf2, min_score, u, &tb[t], emit_d, &p, &dummy0, &dummy1);
+        dsum += p.dsum;
+        dxor ^= p.dxor;
+      }
+      if (out_u || out_w || out_score) fail = sort_desc(kept, take);
+      for (uint64_t i = 0; i < take && !fail; ++i) {
+        if (out_u) out_u[i] = kept[i].u;
+        if (out_w) out_w[i] = kept[i].w;
+        if (out_score) out_score[i] = kept[i].score;
+      }
+    }
+    free(base);
+    free(share);
+  }
+#undef CHUNK_LO
+#undef CHUNK_HI
+  for (int t = 0; tb && t < T; ++t) tables_free(&tb[t]);
+  free(tb); free(hist); free(above); free(ties); free(kept);
+  if (fail) return -1;
+  stats[0] = take;
+  stats[1] = ncand;
+  stats[2] = nnan;
+  stats[3] = wedges;
+  stats[4] = wedges_gt;
+  stats[5] = kth;
+  stats[6] = dsum;
+  stats[7] = dxor;
+  return 0;
 }

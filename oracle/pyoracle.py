@@ -41,6 +41,13 @@ def lib():
             ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p, u64p, u64p, u64p, u64p]
         L.nlpo_predict_range2.restype = ctypes.c_int
+        L.nlpo_predict_par.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+            ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.nlpo_predict_par.restype = ctypes.c_int
+        L.nlpo_edge_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float]
+        L.nlpo_edge_hash.restype = ctypes.c_uint64
         L.nlpo_score_key.argtypes = [ctypes.c_float]
         L.nlpo_score_key.restype = ctypes.c_uint32
         _lib = L
@@ -84,6 +91,70 @@ def predict(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0
     n = cnt.value
     info = dict(candidates=ncand.value, nan=nnan.value, wedges=nw.value, wedges_gt=nwg.value)
     return ou[:n].copy(), ow[:n].copy(), os_[:n].copy(), info
+
+
+def predict_par(offsets, keys, metric, hub, max_edges=None, min_score=0.0, u_begin=0, u_end=None, maxfactor2=0,
+                threads=0, arrays=True):
+    """The same canonical top-k as predict(), computed by nlpo_predict_par (OpenMP
+    over source chunks, four passes, nothing stored beyond the kept set): for
+    the full-size configs.  arrays=False returns no edges, only the counts and
+    the order-free digest of the kept set (info["digest"] = (sum, xor) of
+    nlpo_edge_hash, compare with edge_digest())."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    keys = np.ascontiguousarray(keys, dtype=np.uint32)
+    span = len(offsets) - 1
+    if u_end is None:
+        u_end = span
+    if isinstance(metric, str):
+        metric = METRICS.index(metric)
+    me = (1 << 64) - 1 if max_edges is None else int(max_edges)
+    L = lib()
+    stats = np.zeros(8, np.uint64)
+    if arrays:
+        if max_edges is None:  # size the buffers from a counting run
+            rc = L.nlpo_predict_par(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, maxfactor2,
+                                    min_score, 0, u_begin, u_end, threads, None, None, None, stats.ctypes.data)
+            if rc:
+                raise MemoryError("oracle allocation failed")
+            me = int(stats[1])
+        cap = max(me, 1)
+        ou, ow, os_ = np.empty(cap, np.uint32), np.empty(cap, np.uint32), np.empty(cap, np.float32)
+        ptrs = (ou.ctypes.data, ow.ctypes.data, os_.ctypes.data)
+    else:
+        ptrs = (None, None, None)
+    rc = L.nlpo_predict_par(offsets.ctypes.data, keys.ctypes.data, span, metric, hub, maxfactor2, min_score, me,
+                            u_begin, u_end, threads, *ptrs, stats.ctypes.data)
+    if rc:
+        raise MemoryError("oracle allocation failed")
+    n = int(stats[0])
+    info = dict(candidates=int(stats[1]), nan=int(stats[2]), wedges=int(stats[3]), wedges_gt=int(stats[4]),
+                kth_key=int(stats[5]), digest=(int(stats[6]), int(stats[7])), count=n)
+    if not arrays:
+        return None, None, None, info
+    return ou[:n].copy(), ow[:n].copy(), os_[:n].copy(), info
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def edge_digest(u, w, s, chunk=1 << 24):
+    """(sum, xor) of nlpo_edge_hash over the links (u, w, score): the order-free
+    digest predict_par reports (uint64 wrapping arithmetic)."""
+    tot, x = np.uint64(0), np.uint64(0)
+    with np.errstate(over="ignore"):
+        for i in range(0, len(u), chunk):
+            uu = np.asarray(u[i:i + chunk], np.uint64)
+            ww = np.asarray(w[i:i + chunk], np.uint64)
+            ss = np.asarray(s[i:i + chunk], np.float32)
+            b = ss.view(np.uint32).astype(np.uint64)
+            b[np.isnan(ss)] = np.uint64(0x7fc00000)
+            h = _mix64(((uu << np.uint64(32)) | ww) ^ (b * np.uint64(0x9E3779B97F4A7C15)))
+            tot = tot + h.sum(dtype=np.uint64)
+            x = x ^ np.bitwise_xor.reduce(h) if len(h) else x
+    return int(tot), int(x)
 
 
 def score_keys(scores):

@@ -82,3 +82,26 @@ def test_cpp_header_compiles(tmp_path):
     src.write_text('#include "nlp/predict.hxx"\nint main(){return 0;}\n')
     subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
                    check=True)
+
+
+def test_every_included_header_is_a_build_dependency(nlp):
+    """build.py's dependency list covers every header nlp.hip includes (a stale
+    libnlp.so after a header-only edit would travel to the GPU box): touching
+    any of them makes needs_build() true."""
+    from nlp_amd import build as b
+    src = open(os.path.join(os.path.dirname(b.__file__), "csrc", "nlp.hip")).read()
+    included = re.findall(r'#include\s+"([^"]+\.hpp)"', src)
+    deps = {os.path.basename(d) for d in b.deps()}
+    assert included and set(included) <= deps, set(included) - deps
+    b.build(verbose=False)
+    assert not b.needs_build()
+    for h in included:
+        path = os.path.join(os.path.dirname(b.__file__), "csrc", h)
+        st = os.stat(path)
+        lib_t = os.path.getmtime(b.LIB)
+        try:
+            os.utime(path, (st.st_atime, lib_t + 10))
+            assert b.needs_build(), h
+        finally:
+            os.utime(path, (st.st_atime, st.st_mtime))
+    assert not b.needs_build()

@@ -1,8 +1,10 @@
-"""The multi-GPU orchestration (dist.py) with world_size 2 over gloo on the
-CPU.  The per-rank device predictor is replaced by the oracle here (there is no
-GPU in this container); the shard ranges, the padded all_gather, the rank-order
-concatenation and the stable merge are the production code.  The result must
-equal the single-process canonical top-k exactly."""
+"""The multi-GPU orchestration (dist.py) with world_size 2 and 3 over gloo on
+the CPU.  The per-rank device predictor is replaced by the oracle here (there is
+no GPU in this container; tests/test_gpu_dist.py runs the same chain with the
+HIP predictor and merge on the GPU box); the shard ranges, the histogram-first
+quota selection, the all_gather of the shares and the rank-order merge rule are
+the production code.  The result must equal the single-process canonical top-k
+exactly."""
 import os
 import socket
 import sys
@@ -54,7 +56,7 @@ def _canonical_merge(blocks, k):
     return torch.from_numpy(a[order].copy()), len(order)
 
 
-def _worker(rank, world, port, name, metric, hub, q, cap0=None):
+def _worker(rank, world, port, name, metric, hub, q, k_override=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -64,7 +66,8 @@ def _worker(rank, world, port, name, metric, hub, q, cap0=None):
         import pyoracle
         dmod = nlp_loader.load_sub("dist")
         g = dict(np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"), allow_pickle=False))
-        off, keys, k = g["offsets"], g["keys"], int(g["k"][0])
+        off, keys = g["offsets"], g["keys"]
+        k = int(g["k"][0]) if k_override is None else k_override
 
         def local(ub, ue):
             u, w, s, info = pyoracle.predict(off, keys, metric, hub, max_edges=k, u_begin=ub, u_end=ue)
@@ -73,25 +76,24 @@ def _worker(rank, world, port, name, metric, hub, q, cap0=None):
             return block, len(u), info
 
         state = dmod.Exchange()
-        state.cap = cap0  # None: learnt from a counts all_gather; small: forces the regather path
         outs = []
-        for _ in range(2):  # the second call reuses the learnt stride
+        for _ in range(2):  # the second call reuses the shard bounds
             out, n, info = dmod.predict_sharded(local, _canonical_merge, len(off) - 1, k, state=state)
             outs.append(out[:n].numpy().copy())
         assert np.array_equal(outs[0], outs[1])
-        q.put((rank, outs[1], info["shard"], dmod.block_counts(info["blocks"])))
+        q.put((rank, outs[1], info["shard"], dmod.block_counts(info["blocks"]), info["shares"], info["local_count"]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,metric,hub,cap0", [("g3k", 1, 4, None), ("g3k", 7, 8, None), ("g300", 0, 0, None),
-                                                  ("g3k", 1, 4, 1)])
-def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub, cap0):
-    world = 2
+@pytest.mark.parametrize("name,metric,hub,k,world", [("g3k", 1, 4, None, 2), ("g3k", 7, 8, None, 2),
+                                                     ("g300", 0, 0, None, 2), ("g3k", 1, 4, 50, 2),
+                                                     ("g3k", 0, 0, 333, 3), ("g300", 1, 4, 10 ** 6, 3)])
+def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub, k, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, metric, hub, q, cap0)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, metric, hub, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -100,11 +102,13 @@ def test_sharded_predict_equals_single_process(oracle, golden, name, metric, hub
         assert p.exitcode == 0
     res.sort(key=lambda x: x[0])
     g = golden[name]
-    k = int(g["k"][0])
+    k = int(g["k"][0]) if k is None else k
     eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], metric, hub, max_edges=k)
-    for rank, a, shard, counts in res:
+    for rank, a, shard, counts, shares, local in res:
         assert np.array_equal(a[:, 0].view(np.uint32), eu)
         assert np.array_equal(a[:, 1].view(np.uint32), ew)
         assert np.array_equal(a[:, 2].view(np.uint32), es.view(np.uint32))
-    assert res[0][2][1] == res[1][2][0]  # contiguous shards
-    assert sum(res[0][3]) >= len(eu)
+        assert counts == shares  # the gathered blocks hold exactly the quota shares
+    assert all(res[i][2][1] == res[i + 1][2][0] for i in range(world - 1))  # contiguous shards
+    assert sum(res[0][4]) == len(eu)  # the shares add up to the global top-k: nothing else crossed the wire
+    assert all(res[r][4][r] <= res[r][5] for r in range(world))

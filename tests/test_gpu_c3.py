@@ -1,0 +1,59 @@
+"""BASELINE configs[2] / SURVEY §8(d) C3: the uk-2005-shaped stand-in
+(n = 39.5 M, M = 1.7e9) -- the "HBM-roofline run".  LHub Adamic-Adar (the
+config's metric) and Jaccard at H = 4 (path 1) and H = 16 (Jaccard on path 4,
+the hash accumulation; Adamic-Adar on path 2, the chunked sort -- k = 8.7e7 of
+9.6e8 candidates), exact against the parallel oracle, order included."""
+import numpy as np
+import pytest
+
+from bigconf import ORACLE_THREADS, Config
+from parity import assert_canonical_equal, assert_canonical_order
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c3(nlp):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = Config(nlp, "C3-uk-2005")
+    yield c
+    c.close()
+
+
+def _check(c, oracle, metric, H, path=None):
+    out = c.out()
+    n, t = c.G.predict_device(metric, H, c.k, out)
+    if path is not None:
+        assert t["path"] == path, t
+    u, w, s = c.nlp.edges_from_tensor(out, n)
+    del out
+    eu, ew, es, oi = oracle.predict_par(c.off, c.keys, metric, H, max_edges=c.k, threads=ORACLE_THREADS)
+    assert_canonical_equal(eu, ew, es, u, w, s)
+    assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
+    assert t["nan_candidates"] == oi["nan"]
+    assert_canonical_order(u, w, s)
+    return n, t
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c3_adamic_adar_h4(c3, oracle):
+    _check(c3, oracle, 7, 4, path=1)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c3_jaccard_h4(c3, oracle):
+    _check(c3, oracle, 1, 4, path=1)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c3_jaccard_h16_hash_path(c3, oracle):
+    n, t = _check(c3, oracle, 1, 16, path=4)
+    assert n == c3.k and t["chunks"] >= 1
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c3_adamic_adar_h16(c3, oracle):
+    n, t = _check(c3, oracle, 7, 16)
+    assert n == c3.k

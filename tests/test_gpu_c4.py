@@ -1,0 +1,71 @@
+"""BASELINE configs[3] / SURVEY §8(d) C4: the sk-2005-shaped stand-in
+(n = 50.6 M, M = 3.53e9 adjacency entries after symmetrize and 0.1|E|
+deletion -- beyond 2^31, so every signed 32-bit index in the kernels would
+show here) through the HIP path, checked exactly (order included) against the
+parallel oracle for the bench call (LHub-4 Jaccard, main.cxx:50) and its
+neighbours in the MINDEGREE1 sweep (main.cxx:67-80)."""
+import numpy as np
+import pytest
+
+from bigconf import ORACLE_THREADS, Config
+from parity import assert_canonical_equal, assert_canonical_order
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c4(nlp):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = Config(nlp, "C4-sk-2005")
+    yield c
+    c.close()
+
+
+def _check(c, oracle, metric, H):
+    out = c.out()
+    n, t = c.G.predict_device(metric, H, c.k, out)
+    u, w, s = c.nlp.edges_from_tensor(out, n)
+    eu, ew, es, oi = oracle.predict_par(c.off, c.keys, metric, H, max_edges=c.k, threads=ORACLE_THREADS)
+    assert_canonical_equal(eu, ew, es, u, w, s)
+    assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
+    assert t["nan_candidates"] == oi["nan"]
+    assert_canonical_order(u, w, s)
+    return n, t
+
+
+def test_gpu_c4_shape(c4):
+    info = c4.G.info()
+    assert info["nnz"] == c4.info["M"] == len(c4.keys)
+    assert info["nnz"] > (1 << 31), "C4 must exercise adjacency offsets beyond 2^31"
+    assert info["span"] == 50_636_155 and c4.k == len(c4.del_u) // 2
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_jaccard_h4_bench_call(c4, oracle):
+    n, t = _check(c4, oracle, 1, 4)
+    assert n == t["candidates"] > 0  # fewer candidates than k: all of them
+    # idempotent: the second call returns the identical list
+    out2 = c4.out()
+    n2, _ = c4.G.predict_device(1, 4, c4.k, out2)
+    assert n2 == n
+    import torch
+    out1 = c4.out()
+    c4.G.predict_device(1, 4, c4.k, out1)
+    assert torch.equal(out1[:n], out2[:n])
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_jaccard_h8(c4, oracle):
+    _check(c4, oracle, 1, 8)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_common_neighbors_h8(c4, oracle):
+    _check(c4, oracle, 0, 8)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_adamic_adar_h4(c4, oracle):
+    _check(c4, oracle, 7, 4)

@@ -1,0 +1,87 @@
+"""The multi-GPU chain end to end with the HIP predictor: dist.predict_sharded
+(wedge-balanced source ranges, histogram-first quota selection, all_gather of
+the shares, nlp_merge_blocks_device) in 2 and 3 processes on the one GPU of
+the box.  RCCL refuses two ranks on one device, so the collectives run over
+gloo on CPU copies of the small tensors (dist._coll); the local predictions
+and the merge are the library's, on cuda:0.  Every rank's result must equal
+the single-process prediction bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cases, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import nlp_loader
+        from test_gpu_parity import random_csr
+        nlp = nlp_loader.load()
+        dmod = nlp_loader.load_sub("dist")
+        torch.cuda.set_device(0)
+        off, keys = random_csr(30000, 10, 5)
+        res = []
+        with nlp.Graph(off, keys, device=0) as G:
+            off_t = torch.from_numpy(off.astype(np.int64))
+            keys_t = torch.from_numpy(keys.view(np.int32))
+            for metric, hub, k in cases:
+                block = torch.empty((k + 1, 3), dtype=torch.int32, device="cuda")
+                out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+                st = dmod.Exchange()
+                w = dmod.source_weights(off_t, keys_t, hub)
+                edges, n, info = dmod.predict_sharded(dmod.hip_local_predict(G, metric, hub, k, block),
+                                                      dmod.hip_merge(G, out), len(off) - 1, k, state=st, weights=w)
+                res.append((edges[:n].cpu().numpy().copy(), info["shares"]))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_equals_single_gpu(nlp, world):
+    import torch
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_gpu_parity import random_csr
+    cases = [(1, 4, 2000), (7, 8, 5000), (0, 0, 3000), (1, 16, 10 ** 6)]
+    off, keys = random_csr(30000, 10, 5)
+    want = []
+    with nlp.Graph(off, keys) as G:
+        for metric, hub, k in cases:
+            out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+            n, _ = G.predict_device(metric, hub, k, out)
+            want.append(out[:n].cpu().numpy().copy())
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in got:
+        for (a, shares), b, (metric, hub, k) in zip(res, want, cases):
+            assert np.array_equal(a, b), (rank, metric, hub)
+            assert sum(shares) == len(b)

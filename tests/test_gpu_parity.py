@@ -790,3 +790,19 @@ def test_gpu_async_batch_equals_sync(gpu, oracle, env):
         G.predict_device_async(m2, H2, k, outs[(m2, H2)], u_begin=0, u_end=gpu.UINT64_MAX - 1, stream=st)
         cnt, _ = G.sync()
         assert cnt == len(ref[(m2, H2)][0])
+
+
+def test_gpu_survivor_scan_after_other_survivor_set(gpu, oracle):
+    """the fused/counted paths must reset k_sp_survivors'
+    look-back descriptors when that scan runs (no degree-class index: H = 0,
+    H > 1024).  A graph of > 32768 vertices (several survivor tiles), an
+    Adamic-Adar call (ordered survivor scan, other survivor set) first, then
+    count-metric calls without the index on the same handle, each exact."""
+    off, keys = random_csr(100000, 6, 11)
+    k = 20000
+    with gpu.Graph(off, keys) as G:
+        for m, H in ((7, 4), (1, 0), (7, 8), (1, 2048), (0, 0), (8, 3), (1, 0)):
+            u, w, s, t = G.predict(m, H, k)
+            eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+            assert t["wedges"] == info["wedges_gt"]
