@@ -248,7 +248,7 @@ def main():
         step()  # leave the synchronous result in `out`
 
     sweep = []
-    if world == 1 and args.sweep:
+    if world == 1 and args.sweep not in ("", "none", "="):
         # the reference's MINDEGREE1 sweep (main.cxx:67-80) for the bench metric; one warm call each,
         # then the bench call again so `out` holds the line's result for F1
         out_s = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")

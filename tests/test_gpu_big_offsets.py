@@ -93,4 +93,11 @@ def test_gpu_offsets_beyond_2e32(big, nlp, oracle, metric, H):
     assert_canonical_equal(eu, ew, es, u, w, s)
     assert_canonical_order(u, w, s)
     assert t["candidates"] == oi["candidates"] and t["wedges"] == oi["wedges_gt"]
-    assert np.any(u >= big["mid"] + 64), "the checked links must include rows beyond the 2^32 offset"
+    # the sources whose rows lie beyond the 2^32 offset, as a range of their own
+    ua = big["mid"] + 64
+    n, t = G.predict_device(metric, H, k, out, ua, big["span"])
+    u, w, s = nlp.edges_from_tensor(out, n)
+    eu, ew, es, oi = oracle.predict(big["off_r"], big["keys_r"], metric, H, max_edges=k, u_begin=ua)
+    assert n > 0 and np.all(u >= ua)
+    assert_canonical_equal(eu, ew, es, u, w, s)
+    assert t["candidates"] == oi["candidates"] and t["wedges"] == oi["wedges_gt"]
