@@ -114,6 +114,33 @@ nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint6
 nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_keys, uint64_t span,
                                    uint64_t nnz, int device, void* stream, nlp_graph** out);
 
+/* Multi-device graph: the reference's one OpenMP team over all source vertices
+ * (predict.hxx:284-339, omp_get_max_threads() threads, predict.hxx:413) becomes
+ * `ndev` partitions of the source range, partition p on HIP device devices[p]
+ * (a device may appear several times: logical partitions sharing its
+ * replica).  Every distinct device keeps a full replica of the graph (second-
+ * hop lists are arbitrary).  The partitions are balanced by the wedge work of
+ * the call's hub threshold (computed once per threshold).  A predict call runs
+ * every partition's canonical top-k on its device (one host thread per
+ * device), then selects the global top-k histogram-first (key histograms of
+ * the partitions' lists give the k-th key and each partition's share, a prefix
+ * of its list), copies only the shares to devices[0] (peer copies over xGMI)
+ * and merges them there in one kernel -- the same result, bit for bit and in
+ * the same order, as a single-device handle.  Device outputs (d_out of
+ * nlp_predict_device*) live on devices[0].  nlp_predict_device_async is not
+ * available on a multi-device handle (NLP_ERR_INVALID).  ndev <= NLP_MAX_PARTS. */
+#define NLP_MAX_PARTS 64
+nlp_status nlp_graph_create_multi(const uint64_t* offsets, const uint32_t* keys, uint64_t span,
+                                  const int* devices, int ndev, nlp_graph** out);
+
+/* Number of visible gfx950 devices (the C++ header's default device set). */
+int nlp_device_count(void);
+
+/* Partitions of a handle: *nparts (1 for a single-device handle) and, when
+ * `bounds` is not NULL, the nparts + 1 source bounds used by the last
+ * prediction (NLP_ERR_INVALID before the first prediction of a group). */
+nlp_status nlp_graph_parts(const nlp_graph* g, int* nparts, uint64_t* bounds);
+
 void nlp_graph_destroy(nlp_graph* g);
 
 /* Graph properties: span (S), nnz (M), maximum degree, symmetric flag. */

@@ -64,7 +64,7 @@ EXPORTS = [
     "nlp_predict_ex", "nlp_copy_last", "nlp_predict_device", "nlp_predict_device_ex", "nlp_predict_device_async",
     "nlp_sync", "nlp_select_edges_device",
     "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
-    "nlp_metric_name", "nlp_version",
+    "nlp_metric_name", "nlp_version", "nlp_graph_create_multi", "nlp_device_count", "nlp_graph_parts",
 ]
 
 _lib = None
@@ -84,6 +84,11 @@ def lib(build_if_missing=True):
     P = ctypes.POINTER
     L.nlp_graph_create.argtypes = [vp, vp, u64, i32, P(vp)]
     L.nlp_graph_create_device.argtypes = [vp, vp, u64, u64, i32, vp, P(vp)]
+    L.nlp_graph_create_multi.argtypes = [vp, vp, u64, vp, i32, P(vp)]
+    L.nlp_graph_create_multi.restype = i32
+    L.nlp_device_count.restype = i32
+    L.nlp_graph_parts.argtypes = [vp, P(i32), vp]
+    L.nlp_graph_parts.restype = i32
     L.nlp_graph_destroy.argtypes = [vp]
     L.nlp_graph_destroy.restype = None
     L.nlp_graph_info.argtypes = [vp, P(u64), P(u64), P(u32), P(i32)]
@@ -191,17 +196,37 @@ class Graph:
     offsets: u64[span+1], keys: u32[nnz]; rows sorted ascending, duplicates
     allowed (the reference's LazyBitset multiset semantics)."""
 
-    def __init__(self, offsets, keys, device=0):
+    def __init__(self, offsets, keys, device=0, devices=None):
+        """devices: a list of HIP ordinals, one per source partition (repeats =
+        logical partitions on one device) -> nlp_graph_create_multi; results
+        are identical to a single-device graph and device outputs live on
+        devices[0]."""
         L = lib()
         self._off = np.ascontiguousarray(offsets, dtype=np.uint64)
         self._keys = np.ascontiguousarray(keys, dtype=np.uint32)
         span = len(self._off) - 1
         h = ctypes.c_void_p()
-        _check(L.nlp_graph_create(self._off.ctypes.data, self._keys.ctypes.data if len(self._keys) else None,
-                                  span, int(device), ctypes.byref(h)), "nlp_graph_create")
+        kp = self._keys.ctypes.data if len(self._keys) else None
+        if devices is not None:
+            devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
+            _check(L.nlp_graph_create_multi(self._off.ctypes.data, kp, span, devs.ctypes.data, len(devs),
+                                            ctypes.byref(h)), "nlp_graph_create_multi")
+            device = int(devs[0]) if len(devs) else 0
+        else:
+            _check(L.nlp_graph_create(self._off.ctypes.data, kp, span, int(device), ctypes.byref(h)),
+                   "nlp_graph_create")
         self._h = h
         self.device = int(device)
         del self._off, self._keys
+
+    def parts(self):
+        """(number of partitions, their source bounds of the last prediction or None)."""
+        L = lib()
+        n = ctypes.c_int()
+        _check(L.nlp_graph_parts(self._h, ctypes.byref(n), None), "nlp_graph_parts")
+        b = np.zeros(n.value + 1, np.uint64)
+        st = L.nlp_graph_parts(self._h, ctypes.byref(n), b.ctypes.data)
+        return n.value, (b if st == 0 else None)
 
     @classmethod
     def from_device(cls, offsets, keys, device=None, stream=None):

@@ -14,6 +14,7 @@
 #include <string>
 #include <chrono>
 #include <algorithm>
+#include <thread>
 
 #include "../../include/nlp.h"
 #include "prims.hpp"
@@ -23,6 +24,7 @@
 #include "select.hpp"
 #include "sortpath.hpp"
 #include "hashpath.hpp"
+#include "multi.hpp"
 
 using namespace nlp;
 
@@ -242,6 +244,19 @@ struct nlp_graph {
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
   uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
+  // multi-device group (nlp_graph_create_multi; SURVEY §8(b) devices[], ndev): no CSR of its own
+  bool is_group = false;
+  std::vector<nlp_graph*> members;             // one full graph per distinct device, members[0] on devices[0]
+  std::vector<int> part_member;                // member of each logical partition p (= devices[p])
+  std::vector<uint64_t> part_bounds;           // P + 1 source bounds, balanced for the hub threshold part_H
+  int64_t part_H = -1;
+  std::vector<EdgeOut*> part_buf;              // per partition, on its member's device: header + its list
+  std::vector<uint64_t> part_cap;
+  std::vector<uint64_t*> part_hist;            // per partition: first / last run bounds of 65536 key bins
+  EdgeOut* gather_buf = nullptr;               // on members[0]: the partitions' shares, one block each
+  uint64_t gather_cap = 0;
+  EdgeOut* group_out = nullptr;                // on members[0]: the merged result of a host-output call
+  uint64_t group_out_cap = 0;
 };
 
 namespace {
@@ -303,6 +318,19 @@ hipError_t read_small(nlp_graph* g, const uint64_t* d, int n, hipStream_t st) {
 
 void destroy_graph(nlp_graph* g) {
   if (!g) return;
+  if (g->is_group) {
+    for (size_t q = 0; q < g->part_buf.size(); ++q) {
+      (void)hipSetDevice(g->members[g->part_member[q]]->device);
+      if (g->part_buf[q]) (void)hipFree(g->part_buf[q]);
+      if (q < g->part_hist.size() && g->part_hist[q]) (void)hipFree(g->part_hist[q]);
+    }
+    if (!g->members.empty()) (void)hipSetDevice(g->members[0]->device);
+    if (g->gather_buf) (void)hipFree(g->gather_buf);
+    if (g->group_out) (void)hipFree(g->group_out);
+    for (nlp_graph* m : g->members) destroy_graph(m);
+    delete g;
+    return;
+  }
   (void)hipSetDevice(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   for (auto& c : g->graphs)
@@ -2794,6 +2822,256 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   return NLP_OK;
 }
 
+
+// ================================================================ multi-device group
+// nlp_graph_create_multi: a handle over P logical partitions of the source
+// range, partition p on device devices[p] (a device may hold several).  Each
+// distinct device keeps one full replica of the graph (second-hop lists are
+// arbitrary); partitions run concurrently across devices, one
+// host thread per device, and sequentially on a device.
+
+// Partition bounds balanced by the wedge work of hub threshold H, computed
+// once per H on the first device (k_hp_work_edges, k_part_weight, a scan and
+// P - 1 binary searches).
+nlp_status group_bounds(nlp_graph* g, uint32_t H) {
+  if (g->part_H == (int64_t)H) return NLP_OK;
+  nlp_graph* m = g->members[0];
+  TRY(hipSetDevice(m->device));
+  hipStream_t st = m->stream;
+  const uint64_t S = m->span, M = m->nnz;
+  const uint32_t P = (uint32_t)g->part_member.size();
+  std::vector<uint64_t> b(P + 1, 0);
+  b[P] = S;
+  if (P > 1) {
+    unsigned long long* wu = nullptr;
+    uint64_t *w = nullptr, *pre = nullptr, *scr = nullptr, *bd = nullptr;
+    hipError_t e = hipMalloc(&wu, (S + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&w, (S + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&pre, (S + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&scr, (scan_scratch_words(S) + 16) * 8);
+    if (e == hipSuccess) e = hipMalloc(&bd, P * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(wu, 0, (S + 1) * 8, st);
+    if (e == hipSuccess && M) {
+      hipLaunchKernelGGL(k_hp_work_edges, dim3((unsigned)std::min<uint64_t>((M + NT * HP_WR - 1) / (NT * HP_WR) + 1, 8192)),
+                         dim3(NT), 0, st, view_of(m, M_CN), H, (uint64_t)0, S, (uint64_t)0, M,
+                         (const uint32_t*)m->tile_row, wu);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+      LAUNCH(k_part_weight, S, st, (const unsigned long long*)wu, S, w);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = scan_excl_u64<uint64_t>(w, S, pre, pre + S, scr, st);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_split_points, dim3(1), dim3(std::max<uint32_t>(P, 64)), 0, st, (const uint64_t*)pre, S, P, bd);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(b.data() + 1, bd, (P - 1) * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    for (void* x : {(void*)wu, (void*)w, (void*)pre, (void*)scr, (void*)bd})
+      if (x) (void)hipFree(x);
+    TRY(e);
+    for (uint32_t r = 1; r <= P; ++r) b[r] = std::min(std::max(b[r], b[r - 1]), S);
+  }
+  g->part_bounds = b;
+  g->part_H = H;
+  return NLP_OK;
+}
+
+// A device buffer of the group, on member `mi`'s device, grown to `n` entries.
+template <typename T>
+hipError_t group_buf(nlp_graph* g, int mi, T** buf, uint64_t* cap, uint64_t n) {
+  if (*cap >= n && *buf) return hipSuccess;
+  NLP_HIP(hipSetDevice(g->members[mi]->device));
+  if (*buf) NLP_HIP(hipFree(*buf));
+  *buf = nullptr;
+  *cap = 0;
+  NLP_HIP(hipMalloc(buf, std::max<uint64_t>(n, 1) * sizeof(T)));
+  *cap = n;
+  return hipSuccess;
+}
+
+// Key histogram (level 0: key >> 16; level 1: key & 0xffff inside bin `hi`) of
+// every partition's list -> per partition 65536 counts.
+nlp_status group_hist(nlp_graph* g, const std::vector<uint64_t>& n, int level, uint32_t hi,
+                      std::vector<std::vector<uint64_t>>& cnt) {
+  const size_t P = g->part_member.size();
+  std::vector<std::vector<uint64_t>> fl(P, std::vector<uint64_t>(2 * 65536));
+  for (size_t q = 0; q < P; ++q) {
+    nlp_graph* m = g->members[g->part_member[q]];
+    TRY(hipSetDevice(m->device));
+    if (!g->part_hist[q]) TRY(hipMalloc(&g->part_hist[q], 2 * 65536 * 8));
+    TRY(hipMemsetAsync(g->part_hist[q], 0, 2 * 65536 * 8, m->stream));
+    if (n[q])
+      LAUNCH(k_sorted_hist, n[q], m->stream, (const EdgeOut*)(g->part_buf[q] + 1), n[q], level, hi, g->part_hist[q],
+             g->part_hist[q] + 65536);
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(fl[q].data(), g->part_hist[q], 2 * 65536 * 8, hipMemcpyDeviceToHost, m->stream));
+  }
+  cnt.assign(P, std::vector<uint64_t>(65536, 0));
+  for (size_t q = 0; q < P; ++q) {
+    nlp_graph* m = g->members[g->part_member[q]];
+    TRY(hipSetDevice(m->device));
+    TRY(hipStreamSynchronize(m->stream));
+    for (int b = 0; b < 65536; ++b)
+      if (fl[q][b]) cnt[q][b] = fl[q][65536 + b] - fl[q][b] + 1;
+  }
+  return NLP_OK;
+}
+
+// predictLinks<Metric>Omp over the group: every partition's canonical top-k,
+// then the histogram-first selection and one merge on the first device.
+// d_out (on devices[0]) may be NULL: the result then stays in group_out.
+nlp_status predict_group(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
+                         EdgeOut** result) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t P = g->part_member.size();
+  nlp_graph* m0 = g->members[0];
+  *out_count = 0;
+  nlp_status s = group_bounds(g, p.H);
+  if (s != NLP_OK) return s;
+  std::vector<uint64_t> n(P, 0);
+  std::vector<nlp_timing> tp(P);
+  std::vector<nlp_status> sm(g->members.size(), NLP_OK);
+  const bool bounded = p.max_edges != UINT64_MAX;
+  // 1. the partitions' lists (entries 1..n of part_buf), one host thread per device
+  auto run_member = [&](size_t mi) {
+    nlp_graph* m = g->members[mi];
+    if (hipSetDevice(m->device) != hipSuccess) { sm[mi] = NLP_ERR_DEVICE; return; }
+    for (size_t q = 0; q < P; ++q) {
+      if ((size_t)g->part_member[q] != mi) continue;
+      Params pq = p;
+      pq.ua = std::max(p.ua, g->part_bounds[q]);
+      pq.ub = std::min(p.ub, g->part_bounds[q + 1]);
+      memset(&tp[q], 0, sizeof(nlp_timing));
+      if (pq.ua >= pq.ub || p.max_edges == 0) continue;
+      nlp_status r;
+      if (bounded) {
+        if (group_buf(g, (int)mi, &g->part_buf[q], &g->part_cap[q], p.max_edges + 1) != hipSuccess) {
+          sm[mi] = NLP_ERR_NOMEM;
+          return;
+        }
+        r = predict_impl(m, pq, g->part_buf[q] + 1, &n[q], &tp[q], m->stream, nullptr);
+      } else {  // all candidates: kept in the member's workspace, then copied behind the header slot
+        EdgeOut* res = nullptr;
+        r = predict_impl(m, pq, nullptr, &n[q], &tp[q], m->stream, &res);
+        if (r == NLP_OK && group_buf(g, (int)mi, &g->part_buf[q], &g->part_cap[q], n[q] + 1) != hipSuccess)
+          r = NLP_ERR_NOMEM;
+        if (r == NLP_OK && n[q] &&
+            hipMemcpyAsync(g->part_buf[q] + 1, res, n[q] * sizeof(EdgeOut), hipMemcpyDeviceToDevice, m->stream) !=
+                hipSuccess)
+          r = NLP_ERR_DEVICE;
+      }
+      if (r == NLP_OK && hipStreamSynchronize(m->stream) != hipSuccess) r = NLP_ERR_DEVICE;
+      if (r != NLP_OK) { sm[mi] = r; return; }
+    }
+  };
+  if (g->members.size() == 1) {
+    run_member(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t mi = 0; mi < g->members.size(); ++mi) th.emplace_back(run_member, mi);
+    for (auto& x : th) x.join();
+  }
+  for (nlp_status r : sm)
+    if (r != NLP_OK) return r;
+  const auto t1 = std::chrono::steady_clock::now();
+  // 2. histogram-first selection: the k-th key, every partition's share
+  uint64_t total = 0;
+  for (uint64_t x : n) total += x;
+  const uint64_t take = std::min(p.max_edges, total);
+  std::vector<uint64_t> share(P, 0);
+  if (take == total) {
+    share = n;
+  } else if (take > 0) {
+    std::vector<std::vector<uint64_t>> hc, lc;
+    s = group_hist(g, n, 0, 0, hc);
+    if (s != NLP_OK) return s;
+    uint64_t acc = 0;
+    int b = 65535;
+    for (; b >= 0; --b) {
+      uint64_t h = 0;
+      for (size_t q = 0; q < P; ++q) h += hc[q][b];
+      if (acc + h >= take) break;
+      acc += h;
+    }
+    s = group_hist(g, n, 1, (uint32_t)b, lc);
+    if (s != NLP_OK) return s;
+    int l = 65535;
+    for (; l >= 0; --l) {
+      uint64_t h = 0;
+      for (size_t q = 0; q < P; ++q) h += lc[q][l];
+      if (acc + h >= take) break;
+      acc += h;
+    }
+    uint64_t quota = take - acc;  // ties at the k-th key, handed out in partition (= u) order
+    for (size_t q = 0; q < P; ++q) {
+      uint64_t above = 0;
+      for (int x = b + 1; x < 65536; ++x) above += hc[q][x];
+      for (int x = l + 1; x < 65536; ++x) above += lc[q][x];
+      const uint64_t tq = std::min(lc[q][l], quota);
+      quota -= tq;
+      share[q] = above + tq;
+    }
+  }
+  // 3. headers, then the shares to the first device (peer copies over xGMI
+  //    between devices, device copies within one)
+  uint64_t stride = 1;
+  for (uint64_t x : share) stride = std::max(stride, x + 1);
+  std::vector<uint32_t> hdr(3 * P);
+  for (size_t q = 0; q < P; ++q) {
+    hdr[3 * q] = (uint32_t)(share[q] & 0xffffffffu);
+    hdr[3 * q + 1] = (uint32_t)(share[q] >> 32);
+    hdr[3 * q + 2] = NLP_BLOCK_MAGIC;
+  }
+  TRY(group_buf(g, 0, &g->gather_buf, &g->gather_cap, stride * P));
+  TRY(hipSetDevice(m0->device));
+  for (size_t q = 0; q < P; ++q) {
+    nlp_graph* m = g->members[g->part_member[q]];
+    EdgeOut* dst = g->gather_buf + q * stride;
+    TRY(hipMemcpyAsync(dst, &hdr[3 * q], sizeof(EdgeOut), hipMemcpyHostToDevice, m0->stream));
+    if (!share[q]) continue;
+    if (m->device == m0->device)
+      TRY(hipMemcpyAsync(dst + 1, g->part_buf[q] + 1, share[q] * sizeof(EdgeOut), hipMemcpyDeviceToDevice,
+                         m0->stream));
+    else
+      TRY(hipMemcpyPeerAsync(dst + 1, m0->device, g->part_buf[q] + 1, m->device, share[q] * sizeof(EdgeOut),
+                             m0->stream));
+  }
+  // 4. one merge (select.hpp) in canonical order: score desc, then partition = u order
+  EdgeOut* out = d_out;
+  if (!out) {
+    TRY(group_buf(g, 0, &g->group_out, &g->group_out_cap, std::max<uint64_t>(take, 1)));
+    TRY(hipSetDevice(m0->device));
+    out = g->group_out;
+  }
+  uint64_t cnt = 0;
+  if (take > 0) {
+    s = nlp_merge_blocks_device(m0, (const nlp_edge*)g->gather_buf, stride, (uint32_t)P, take, (nlp_edge*)out, &cnt,
+                                m0->stream);
+    if (s != NLP_OK) return s;
+  }
+  TRY(hipStreamSynchronize(m0->stream));
+  *out_count = cnt;
+  if (result) *result = out;
+  if (t) {
+    memset(t, 0, sizeof(*t));
+    const double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double sc = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t->score_ms = (float)sc;
+    t->select_ms = (float)(tot - sc);
+    t->total_ms = (float)tot;
+    for (size_t q = 0; q < P; ++q) {
+      t->wedges += tp[q].wedges;
+      t->candidates += tp[q].candidates;
+      t->nan_candidates += tp[q].nan_candidates;
+      t->path = std::max(t->path, tp[q].path);
+      t->chunks += tp[q].chunks;
+    }
+  }
+  return NLP_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C-ABI
@@ -2856,6 +3134,76 @@ nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_
   return NLP_OK;
 }
 
+nlp_status nlp_graph_create_multi(const uint64_t* offsets, const uint32_t* keys, uint64_t span, const int* devices,
+                                  int ndev, nlp_graph** out) {
+  if (!out || !offsets || !devices || ndev < 1 || ndev > NLP_MAX_PARTS || span == 0 || span > 0xffffffffull)
+    return NLP_ERR_INVALID;
+  *out = nullptr;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0) return NLP_ERR_NODEVICE;
+  for (int i = 0; i < ndev; ++i) {
+    nlp_status s = check_device(devices[i]);
+    if (s != NLP_OK) return s;
+  }
+  nlp_graph* g = new (std::nothrow) nlp_graph();
+  if (!g) return NLP_ERR_NOMEM;
+  g->is_group = true;
+  g->device = devices[0];
+  std::vector<int> devs;  // distinct devices, in order of first appearance
+  for (int i = 0; i < ndev; ++i) {
+    int mi = (int)(std::find(devs.begin(), devs.end(), devices[i]) - devs.begin());
+    if (mi == (int)devs.size()) devs.push_back(devices[i]);
+    g->part_member.push_back(mi);
+  }
+  for (int d : devs) {
+    nlp_graph* m = nullptr;
+    nlp_status s = nlp_graph_create(offsets, keys, span, d, &m);
+    if (s != NLP_OK) { destroy_graph(g); return s; }
+    g->members.push_back(m);
+  }
+  for (size_t a = 0; a < devs.size(); ++a)  // peer access for the share copies (xGMI); copies work without it
+    for (size_t b = 0; b < devs.size(); ++b)
+      if (a != b && hipSetDevice(devs[a]) == hipSuccess) {
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, devs[a], devs[b]) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(devs[b], 0);
+        (void)hipGetLastError();
+      }
+  g->part_buf.assign(ndev, nullptr);
+  g->part_cap.assign(ndev, 0);
+  g->part_hist.assign(ndev, nullptr);
+  g->span = span;
+  g->nnz = g->members[0]->nnz;
+  g->maxdeg = g->members[0]->maxdeg;
+  g->symmetric = g->members[0]->symmetric;
+  g->last_stream = g->members[0]->stream;
+  *out = g;
+  return NLP_OK;
+}
+
+int nlp_device_count(void) {
+  int n = 0, c = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  for (int d = 0; d < n; ++d)
+    if (check_device(d) == NLP_OK) ++c;
+  return c;
+}
+
+nlp_status nlp_graph_parts(const nlp_graph* g, int* nparts, uint64_t* bounds) {
+  if (!g || !nparts) return NLP_ERR_INVALID;
+  *nparts = g->is_group ? (int)g->part_member.size() : 1;
+  if (bounds) {
+    if (g->is_group && g->part_H >= 0)
+      for (size_t i = 0; i < g->part_bounds.size(); ++i) bounds[i] = g->part_bounds[i];
+    else if (g->is_group)
+      return NLP_ERR_INVALID;  // no prediction yet: the bounds depend on the hub threshold
+    else {
+      bounds[0] = 0;
+      bounds[1] = g->span;
+    }
+  }
+  return NLP_OK;
+}
+
 void nlp_graph_destroy(nlp_graph* g) { destroy_graph(g); }
 
 nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uint32_t* max_degree, int* symmetric) {
@@ -2873,6 +3221,24 @@ nlp_status nlp_predict_device_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_m
   if (!g || !out_count || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (g->async_pending) return NLP_ERR_INVALID;  // an asynchronous batch is in flight: nlp_sync first
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
+  if (g->is_group) {  // every partition on its device, the merged result into d_out (on devices[0])
+    if ((stream ? hipStreamSynchronize((hipStream_t)stream) : hipDeviceSynchronize()) != hipSuccess)
+      return NLP_ERR_DEVICE;
+    Params p{(int)metric, hub_max_degree, min_score, max_edges, u_begin, std::min<uint64_t>(u_end, g->span),
+             max_factor2};
+    nlp_timing tt;
+    memset(&tt, 0, sizeof(tt));
+    g->last_out = nullptr;
+    g->last_n = 0;
+    nlp_status s = predict_group(g, p, (EdgeOut*)d_out, out_count, &tt, nullptr);
+    if (t) *t = tt;
+    if (s == NLP_OK) {
+      g->last_out = (const EdgeOut*)d_out;
+      g->last_n = *out_count;
+      g->last_stream = g->members[0]->stream;
+    }
+    return s;
+  }
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
   // the graph's own stream does not order after other streams: with no caller
   // stream, wait for all prior device work (inputs/outputs may come from it)
@@ -2902,7 +3268,7 @@ nlp_status nlp_predict_device(nlp_graph* g, nlp_metric metric, uint32_t hub_max_
 nlp_status nlp_predict_device_async(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degree, uint32_t max_factor2,
                                     float min_score, uint64_t max_edges, uint64_t u_begin, uint64_t u_end,
                                     nlp_edge* d_out, void* stream) {
-  if (!g || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out)) return NLP_ERR_INVALID;
+  if (!g || (int)metric < 0 || (int)metric > 8 || (max_edges && !d_out) || g->is_group) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   // NULL: the device's default stream (ordered after the caller's default-stream work without a
   // device-wide wait; the synchronous entry points use the handle's own stream and a device sync)
@@ -3006,8 +3372,11 @@ nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degr
   uint64_t n = 0;
   g->last_out = nullptr;
   g->last_n = 0;
+  if (g->is_group) st = g->members[0]->stream;
   for (int r = 0; r < repeat; ++r) {
-    nlp_status s = predict_impl(g, p, nullptr, &n, &last, st, &d_res);
+    nlp_status s = g->is_group ? predict_group(g, p, nullptr, &n, &last, &d_res)
+                               : predict_impl(g, p, nullptr, &n, &last, st, &d_res);
+    if (s == NLP_OK && g->is_group) TRY(hipSetDevice(g->device));
     if (s != NLP_OK) return s;
     score_sum += last.score_ms;
     select_sum += last.select_ms;
@@ -3015,7 +3384,12 @@ nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degr
   last.score_ms = score_sum / repeat;
   last.select_ms = select_sum / repeat;
   last.total_ms = last.score_ms + last.select_ms;
-  if (out && n) {
+  if (out && n && g->is_group) {
+    const auto c0 = std::chrono::steady_clock::now();
+    TRY(hipMemcpyAsync(out, d_res, n * sizeof(EdgeOut), hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    last.copy_ms = (float)std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count();
+  } else if (out && n) {
     TRY(hipEventRecord(g->ev[0], st));
     TRY(hipMemcpyAsync(out, d_res, n * sizeof(EdgeOut), hipMemcpyDeviceToHost, st));
     TRY(hipEventRecord(g->ev[1], st));
@@ -3049,6 +3423,7 @@ nlp_status nlp_copy_last(nlp_graph* g, nlp_edge* out, uint64_t n, uint64_t* copi
 }
 
 nlp_status nlp_set_truth(nlp_graph* g, const uint32_t* u, const uint32_t* v, uint64_t n) {
+  if (g && g->is_group) return nlp_set_truth(g->members[0], u, v, n);
   if (!g || (n && (!u || !v))) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   std::vector<uint64_t> k(n);
@@ -3065,6 +3440,7 @@ nlp_status nlp_set_truth(nlp_graph* g, const uint32_t* u, const uint32_t* v, uin
 
 nlp_status nlp_count_common_device(nlp_graph* g, const nlp_edge* d_edges, uint64_t n, uint64_t* common,
                                    void* stream) {
+  if (g && g->is_group) return nlp_count_common_device(g->members[0], d_edges, n, common, stream);
   if (!g || !common || (n && !d_edges)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
@@ -3090,6 +3466,7 @@ nlp_status nlp_last_common(nlp_graph* g, uint64_t* common) {
 
 nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t n, uint64_t max_edges,
                                    nlp_edge* d_out, uint64_t* out_count, void* stream) {
+  if (g && g->is_group) return nlp_select_edges_device(g->members[0], d_in, n, max_edges, d_out, out_count, stream);
   if (!g || !out_count || (n && !d_in) || (max_edges && !d_out)) return NLP_ERR_INVALID;
   if (hipSetDevice(g->device) != hipSuccess) return NLP_ERR_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : g->stream;
@@ -3117,6 +3494,8 @@ nlp_status nlp_select_edges_device(nlp_graph* g, const nlp_edge* d_in, uint64_t 
 
 nlp_status nlp_merge_blocks_device(nlp_graph* g, const nlp_edge* d_blocks, uint64_t stride, uint32_t nblocks,
                                    uint64_t max_edges, nlp_edge* d_out, uint64_t* out_count, void* stream) {
+  if (g && g->is_group)
+    return nlp_merge_blocks_device(g->members[0], d_blocks, stride, nblocks, max_edges, d_out, out_count, stream);
   if (!g || !out_count || !d_blocks || stride < 1 || nblocks < 1 || nblocks > 65535 || (max_edges && !d_out) ||
       (uint64_t)nblocks * stride >= (1ull << 32))  // merge ranks are 32-bit
     return NLP_ERR_INVALID;

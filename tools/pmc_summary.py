@@ -1,6 +1,7 @@
 """Summarise tools/gpu_pmc.sh's counter passes into profiles/pmc_traffic.json.
 
-    python tools/pmc_summary.py gpurun_out/pmc <round-tag> [--config C2-soc-LiveJournal1] [--hot k_sp_grouprun]
+    python tools/pmc_summary.py gpurun_out/pmc <round-tag> [--config C4-sk-2005] [--hot k_sp_grouprun]
+        [--fetch DIR --write DIR] [--metric JAC --hub 4]
 
 HBM bytes per launch, following MI355X_MICROARCH.md ("HBM [CDNA4]"):
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes (they do not fit one
@@ -17,15 +18,13 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_sp_grouprun", "k_sp_exbucket", "k_sp_gather", "k_sp_arena_init", "k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
+KERNELS = ["k_sp_cpass0", "k_sp_cpass", "k_sp_grouprun", "k_sp_exbucket", "k_sp_gather", "k_sp_arena_init", "k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
            "k_desc_keys_sel", "k_sel_hist"]
 
 
 def short(name):
-    for k in KERNELS:
-        if k in name:
-            return k
-    return None
+    hits = [k for k in KERNELS if k + "(" in name or k + "<" in name or name.endswith(k)]
+    return max(hits, key=len) if hits else None
 
 
 def per_kernel(path, counter):
@@ -44,17 +43,19 @@ def per_kernel(path, counter):
 def main():
     src = sys.argv[1]
     tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
-    config = "C2-soc-LiveJournal1"
-    if "--config" in sys.argv:
-        config = sys.argv[sys.argv.index("--config") + 1]
-    fetch = per_kernel(os.path.join(src, "p1"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "p2"), "WRITE_SIZE")
+    def opt(name, default):
+        return sys.argv[sys.argv.index(name) + 1] if name in sys.argv else default
+    config = opt("--config", "C4-sk-2005")
+    fetch = per_kernel(opt("--fetch", os.path.join(src, "p1")), "FETCH_SIZE")
+    write = per_kernel(opt("--write", os.path.join(src, "p2")), "WRITE_SIZE")
     hot = "k_sp_grouprun"
     if "--hot" in sys.argv:
         hot = sys.argv[sys.argv.index("--hot") + 1]
-    out = {"config": config, "n_gpus": 1, "metric": "JAC", "hub": 4, "hot_kernel": hot,
-           "source": "profiles/%s_pmc (rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE, "
-                     "bench.py --steps 5 --warmup 2); traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024" % tag,
+    out = {"config": config, "n_gpus": 1, "metric": opt("--metric", "JAC"), "hub": int(opt("--hub", "4")),
+           "hot_kernel": hot,
+           "source": "profiles/%s (rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE in separate passes, "
+                     "bench.py --steps 5 --warmup 2 --no-cpu-baseline --sweep =); traffic = (2*FETCH_SIZE + "
+                     "WRITE_SIZE) KiB * 1024 per dispatch" % tag,
            "kernels": {}}
     for k in KERNELS:
         if k not in fetch or k not in write:
