@@ -30,14 +30,18 @@
 //
 // Graph input: any type with the reference's graph concept (Graph.hxx):
 // key_type, span(), hasVertex(u), forEachEdgeKey(u, fn) -- DiGraph and
-// DiGraphCsr both qualify.  It is converted to a CSR with identity vertex ids
-// (absent vertices get empty rows) and uploaded on every call; keep a
-// nlp::HipGraph to upload once and call many times (main.cxx runs 99
-// predictions per graph).
+// DiGraphCsr both qualify (a DiGraphCsr's arrays are read directly).  It is
+// converted to a CSR with identity vertex ids (absent vertices get empty rows)
+// and uploaded once per distinct graph (detail::cachedGraph: the 99 calls
+// main.cxx makes per graph reuse one resident copy); a nlp::HipGraph keeps a
+// graph resident explicitly.  Devices: NLP_DEVICES or every gfx950 device
+// (defaultDevices(), the analogue of the reference's OpenMP team).
 #pragma once
 #include <cstdint>
 #include <cstddef>
+#include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -71,6 +75,9 @@ struct PredictLinkResult {
   PredictLinkResult() : edges(), time(), scoringTime() {}
   PredictLinkResult(std::vector<std::tuple<K, K, W>>&& edges, float time = 0, float scoringTime = 0)
       : edges(std::move(edges)), time(time), scoringTime(scoringTime) {}
+  /** From an lvalue list, which is moved from (predict.hxx:99-100). */
+  PredictLinkResult(std::vector<std::tuple<K, K, W>>& edges, float time = 0, float scoringTime = 0)
+      : edges(std::move(edges)), time(time), scoringTime(scoringTime) {}
 };
 #pragma endregion
 
@@ -80,19 +87,68 @@ inline void check(nlp_status s, const char* what) {
   if (s != NLP_OK) throw std::runtime_error(std::string(what) + ": " + nlp_status_string(s));
 }
 
+namespace detail {
+// A CSR graph type with the reference's DiGraphCsr data members (Graph.hxx:396-406:
+// offsets, degrees, edgeKeys) -- read directly instead of through forEachEdgeKey.
+template <class G, class = void>
+struct has_csr_members : std::false_type {};
+template <class G>
+struct has_csr_members<G, std::void_t<decltype(std::declval<const G&>().offsets[0]),
+                                      decltype(std::declval<const G&>().degrees[0]),
+                                      decltype(std::declval<const G&>().edgeKeys[0])>> : std::true_type {};
+}  // namespace detail
+
 /** Build the identity-id CSR of any graph concept G (csr.hxx:106-222 layout,
- *  without the dense renumbering so vertex ids are preserved). */
+ *  without the dense renumbering so vertex ids are preserved): span(),
+ *  hasVertex(u), forEachEdgeKey(u, fn) (Graph.hxx:59-169, DiGraph), or the
+ *  offsets / degrees / edgeKeys arrays of a DiGraphCsr (Graph.hxx:383-639). */
 template <class G>
 inline void graphToCsr(const G& x, std::vector<uint64_t>& offsets, std::vector<uint32_t>& keys) {
   const size_t S = x.span();
   offsets.assign(S + 1, 0);
   keys.clear();
-  for (size_t u = 0; u < S; ++u) {
-    offsets[u] = keys.size();
-    if (!x.hasVertex(typename G::key_type(u))) continue;
-    x.forEachEdgeKey(typename G::key_type(u), [&](auto v) { keys.push_back(uint32_t(v)); });
+  if constexpr (detail::has_csr_members<G>::value) {
+    size_t M = 0;
+    for (size_t u = 0; u < S; ++u) M += size_t(x.degrees[u]);
+    keys.reserve(M);
+    for (size_t u = 0; u < S; ++u) {  // row u: degrees[u] keys from offsets[u] (rows may leave gaps)
+      offsets[u] = keys.size();
+      const size_t o = size_t(x.offsets[u]), d = size_t(x.degrees[u]);
+      for (size_t i = 0; i < d; ++i) keys.push_back(uint32_t(x.edgeKeys[o + i]));
+    }
+  } else {
+    for (size_t u = 0; u < S; ++u) {
+      offsets[u] = keys.size();
+      if (!x.hasVertex(typename G::key_type(u))) continue;
+      x.forEachEdgeKey(typename G::key_type(u), [&](auto v) { keys.push_back(uint32_t(v)); });
+    }
   }
   offsets[S] = keys.size();
+}
+
+/** The devices a graph handle uses by default -- the analogue of the
+ *  reference's omp_get_max_threads() team (predict.hxx:413): NLP_DEVICES
+ *  (comma-separated HIP ordinals; repeats = logical partitions on one device),
+ *  else every visible gfx950 device. */
+inline std::vector<int> defaultDevices() {
+  std::vector<int> d;
+  if (const char* e = std::getenv("NLP_DEVICES")) {
+    std::string s(e), x;
+    for (size_t i = 0; i <= s.size(); ++i) {
+      if (i == s.size() || s[i] == ',') {
+        if (!x.empty()) d.push_back(std::atoi(x.c_str()));
+        x.clear();
+      } else {
+        x += s[i];
+      }
+    }
+  }
+  if (d.empty()) {
+    const int n = nlp_device_count();
+    for (int i = 0; i < n; ++i) d.push_back(i);
+  }
+  if (d.empty()) d.push_back(0);  // no device: nlp_graph_create reports NLP_ERR_NODEVICE
+  return d;
 }
 
 /** A graph resident in HBM (one nlp_graph handle). */
@@ -103,13 +159,26 @@ class HipGraph {
   HipGraph(const uint64_t* offsets, const uint32_t* keys, uint64_t span, int device = 0) {
     check(nlp_graph_create(offsets, keys, span, device, &g_), "nlp_graph_create");
   }
+  /** One partition per entry of `devices` (nlp_graph_create_multi); a single
+   *  entry is a single-device handle. */
+  HipGraph(const uint64_t* offsets, const uint32_t* keys, uint64_t span, const std::vector<int>& devices) {
+    create(offsets, keys, span, devices);
+  }
   template <class G>
-  explicit HipGraph(const G& x, int device = 0) {
+  explicit HipGraph(const G& x, int device) {
     std::vector<uint64_t> off;
     std::vector<uint32_t> keys;
     graphToCsr(x, off, keys);
     check(nlp_graph_create(off.data(), keys.empty() ? nullptr : keys.data(), off.size() - 1, device, &g_),
           "nlp_graph_create");
+  }
+  /** On the default devices (defaultDevices()), or on `devices`. */
+  template <class G>
+  explicit HipGraph(const G& x, const std::vector<int>& devices = defaultDevices()) {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> keys;
+    graphToCsr(x, off, keys);
+    create(off.data(), keys.empty() ? nullptr : keys.data(), off.size() - 1, devices);
   }
   HipGraph(const HipGraph&) = delete;
   HipGraph& operator=(const HipGraph&) = delete;
@@ -124,6 +193,14 @@ class HipGraph {
     g_ = nullptr;
   }
   nlp_graph* get() const { return g_; }
+  void create(const uint64_t* offsets, const uint32_t* keys, uint64_t span, const std::vector<int>& devices) {
+    reset();
+    if (devices.size() <= 1)
+      check(nlp_graph_create(offsets, keys, span, devices.empty() ? 0 : devices[0], &g_), "nlp_graph_create");
+    else
+      check(nlp_graph_create_multi(offsets, keys, span, devices.data(), int(devices.size()), &g_),
+            "nlp_graph_create_multi");
+  }
   size_t span() const {
     uint64_t s = 0;
     nlp_graph_info(g_, &s, nullptr, nullptr, nullptr);
@@ -161,13 +238,42 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
   return PredictLinkResult<K, W>(std::move(a), t.total_ms, t.score_ms);
 }
 
+namespace detail {
+// The graph handle of the last graph predicted on from this thread.  main.cxx
+// runs 99 predictions per graph (PREDICT_LINKS_ALL, main.cxx:67-80, 212-220)
+// on the same object: the CSR is rebuilt on the host each call (O(M), like
+// the reference's own pass over the graph) and compared with the resident
+// one, so the graph is uploaded and prepared (degrees, index, membership
+// table) once per distinct graph.
+struct GraphCache {
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> keys;
+  std::vector<int> devices;
+  HipGraph g;
+};
+template <class G>
+inline const HipGraph& cachedGraph(const G& x) {
+  static thread_local GraphCache c;
+  std::vector<uint64_t> off;
+  std::vector<uint32_t> keys;
+  graphToCsr(x, off, keys);
+  std::vector<int> devs = defaultDevices();
+  if (!c.g.get() || devs != c.devices || off != c.off || keys != c.keys) {
+    c.g.create(off.data(), keys.empty() ? nullptr : keys.data(), off.size() - 1, devs);
+    c.devices = devs;
+    c.off.swap(off);
+    c.keys.swap(keys);
+  }
+  return c.g;
+}
+}  // namespace detail
+
 template <class G, class W>
 inline PredictLinkResult<typename G::key_type, W> predictLinksHipAny(const G& x, nlp_metric metric,
                                                                      uint32_t mindegree1,
                                                                      const PredictLinkOptions<W>& o,
                                                                      uint32_t maxfactor2 = 0) {
-  HipGraph g(x);
-  return predictLinksHip<typename G::key_type, W>(g, metric, mindegree1, o, maxfactor2);
+  return predictLinksHip<typename G::key_type, W>(detail::cachedGraph(x), metric, mindegree1, o, maxfactor2);
 }
 
 template <class W>

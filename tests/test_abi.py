@@ -105,3 +105,33 @@ def test_every_included_header_is_a_build_dependency(nlp):
         finally:
             os.utime(path, (st.st_atime, st.st_mtime))
     assert not b.needs_build()
+
+
+def test_reference_main_compiles_against_the_dropin_header(tmp_path):
+    """The reference's own main.cxx, unmodified, compiled with inc/predict.hxx
+    swapped for include/nlp/predict.hxx (oracle/Makefile _ref/main_dropin,
+    main.sh:29-42's macros) and linked to libnlp.so: it loads and ingests an
+    MTX with the reference's code, and without a GPU its first prediction
+    fails loudly with the library's NODEVICE status (no CPU fallback)."""
+    if not os.path.exists("/root/reference/main.cxx"):
+        pytest.skip("reference not present (GPU box): the prebuilt binary is run by tests/test_gpu_dropin.py")
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present: tests/test_gpu_dropin.py runs it")
+    except ImportError:
+        pass
+    import sys
+    from nlp_amd import build as b
+    b.build(verbose=False)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_ref/main_dropin"], check=True)
+    exe = os.path.join(ROOT, "oracle", "_ref", "main_dropin")
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import chung_lu_mtx
+    mtx = str(tmp_path / "g.mtx")
+    chung_lu_mtx(mtx, 300, 1200, 0.6, 1)
+    r = subprocess.run([exe, mtx, "0", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "nlp_graph_create: no gfx950 device" in r.stderr
+    syms = subprocess.run(["nm", "-D", exe], capture_output=True, text=True).stdout
+    assert "nlp_predict_ex" in syms and "nlp_graph_create" in syms
