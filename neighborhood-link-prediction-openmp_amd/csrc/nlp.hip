@@ -186,6 +186,10 @@ struct nlp_graph {
   bool counted_force = false;
   bool counted = true;                         // fused path: ordering passes 2-4 from per-tile digit counts (k_sp_cpass,
                                                // no look-back) when the candidates fit CP_MAXT tiles (NLP_COUNTED=0: off)
+  bool small_order = true;                     // fused path: one workgroup orders <= SO_MAX candidates
+                                               // (k_sp_order_small; NLP_SMALL_ORDER=0: off)
+  double small_off_w = 0;                      // wedge estimate of the last call whose candidates did not fit it
+  bool small_force = false;
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   int gr_nt = GR_NT;                           // k_sp_grouprun threads per bucket (NLP_GR_NT=512)
   bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
@@ -595,6 +599,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* cp = getenv("NLP_COUNTED")) {  // 0: off, 2: whatever the estimate (tests the F_CPASS redo)
     g->counted = cp[0] != '0';
     g->counted_force = cp[0] == '2';
+  }
+  if (const char* so = getenv("NLP_SMALL_ORDER")) {  // 0: off, 2: whatever the estimate (tests the F_SMALL redo)
+    g->small_order = so[0] != '0';
+    g->small_force = so[0] == '2';
   }
   if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
@@ -1765,6 +1773,7 @@ struct SpBufs {
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   uint64_t ostride11;                           // the same for 11-bit digits (the fused path's three passes)
   bool ord11;                                   // fused path: three 11-bit passes
+  bool small;                                   // fused path: k_sp_order_small orders all candidates (one launch)
   bool counted;                                 // fused path: passes 2-4 are k_sp_cpass (tile digit counts from the
                                                 // pass before, count matrix p at d_cm; the last pass gathers)
   int wbits, passes;
@@ -1908,6 +1917,11 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
     const double est = hp_estimate(g, p), cap = (double)CP_MAXT * OS2_TILE;
     f.counted = f.fused && !f.ord11 && g->counted && (g->counted_force || est < 4.0 * cap) &&
                 !(g->cp_off_w > 0 && est > 0.5 * g->cp_off_w);
+    // small calls: one workgroup orders every candidate (k_sp_order_small) when the estimate -- at least
+    // the wedges w > u, so at least the candidates -- fits it, unless a similar call did not (F_SMALL)
+    f.small = f.fused && !f.ord11 && g->small_order && !g->counted_force &&
+              (g->small_force || est <= (double)SO_MAX) && !(g->small_off_w > 0 && est > 0.5 * g->small_off_w);
+    if (f.small) f.counted = false;
   }
   f.ostride11 = tO * 2048;
   f.d_tick = SP_DESC;
@@ -2159,7 +2173,14 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.counted && ps == 0) {  // dense tiles of k_sp_grouprun's candidates (it counted digit 0 per bucket group)
+      if (f.small) {  // all four passes and the output in one workgroup
+        if (ps != 0) return NLP_OK;
+        hipLaunchKernelGGL(k_sp_order_small, dim3(1), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
+                           (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
+                           (uint32_t)nb_used, f.caplog,
+                           GatherOut{nullptr, nullptr, nullptr, p.max_edges, out, ctr, g->host_ctr_dev, ts, g->d_sticky},
+                           ts + TS_HOT_OUT);
+      } else if (f.counted && ps == 0) {  // dense tiles of k_sp_grouprun's candidates (it counted digit 0 per bucket group)
         hipLaunchKernelGGL(k_sp_cpass0, dim3(CP_MAXT), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
                            (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
                            (uint32_t)nb_used, cp_g, cp_groups, f.caplog, (const uint32_t*)cmat, cmat + CP_M, f.ok1,
@@ -2237,7 +2258,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)nullptr, (uint64_t*)nullptr, (const uint64_t*)nullptr, 0u, 0,
                            (uint64_t*)nullptr, f.fused ? dord + (uint64_t)(ps - 1) * f.ostride : (uint32_t*)nullptr);
     } else {
-      if ((g->fuse_gather && !f.fused) || f.counted) return NLP_OK;  // done by the last ordering pass
+      if ((g->fuse_gather && !f.fused) || f.counted || f.small) return NLP_OK;  // done by the last ordering pass
       const uint64_t m = std::min<uint64_t>(p.max_edges, capW);
       // one workgroup per CU at most: the last one to finish is found with one atomic each
       hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)std::min<uint64_t>(256, std::max<uint64_t>(1, (m + NT - 1) / NT))),
@@ -2532,7 +2553,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (sorted && async_direct)
       replayed = false;
     else if (sorted)
-      s = run_graph(g, p, out, st, (msd ? 1 + sp.msd_passes : 1) + (sp.counted ? 16 : 0), sp.arena, &replayed,
+      s = run_graph(g, p, out, st, (msd ? 1 + sp.msd_passes : 1) + (sp.counted ? 16 : 0) + (sp.small ? 32 : 0), sp.arena, &replayed,
                     [&](hipStream_t gs, int seg) { return launch_sp(g, p, sp, out, gs, seg); }, stamps,
                     stamps && gseq);
     else
@@ -2653,6 +2674,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     }
     if (sorted && sp.counted && (h[C_FLAGS] & F_CPASS)) {  // more than CP_MAXT candidate tiles: look-back passes
       g->cp_off_w = est_w;
+      continue;
+    }
+    if (sorted && sp.small && (h[C_FLAGS] & F_SMALL)) {  // more than SO_MAX candidates: the counted passes
+      g->small_off_w = std::max(est_w, 1.0);
       continue;
     }
     if (sorted && sp.fused && !(h[C_FLAGS] >> 32)) g->ord_clean = sp.arena;  // self-cleaned (or never written)
@@ -3328,7 +3353,7 @@ nlp_status nlp_sync(nlp_graph* g, uint64_t* out_count, nlp_timing* t) {
   }
   f |= g->async_fail;
   g->async_fail = 0;
-  if ((f & (F_OVERFLOW | F_TOOBIG | F_CPASS)) || (f >> 32)) {  // some call of the batch needs a redo
+  if ((f & (F_OVERFLOW | F_TOOBIG | F_CPASS | F_SMALL)) || (f >> 32)) {  // some call of the batch needs a redo
     g->ord_clean = nullptr;
     g->async_ok = false;
     return NLP_ERR_RETRY;

@@ -806,3 +806,34 @@ def test_gpu_survivor_scan_after_other_survivor_set(gpu, oracle):
             eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k)
             assert_canonical_equal(eu, ew, es, u, w, s)
             assert t["wedges"] == info["wedges_gt"]
+
+
+@pytest.mark.parametrize("n,avg,H", [(30000, 6, 2), (30000, 6, 3), (100000, 8, 4), (150000, 6, 6)])
+def test_gpu_small_order_equals_counted_passes(gpu, oracle, n, avg, H):
+    """k_sp_order_small (one workgroup orders all candidates of a small fused
+    call) against the counted passes (NLP_SMALL_ORDER=0) and the oracle, below
+    and above its SO_MAX = 16384 candidates; NLP_SMALL_ORDER=2 forces it
+    whatever the estimate, so calls beyond SO_MAX take the F_SMALL redo."""
+    off, keys = random_csr(n, avg, 21 + H)
+    k_list = (50, 7000, 10 ** 6)
+    res = {}
+    for env in ("1", "0", "2"):
+        os.environ["NLP_SMALL_ORDER"] = env
+        try:
+            with gpu.Graph(off, keys) as G:
+                for m in (1, 0, 6):
+                    for k in k_list:
+                        u, w, s, t = G.predict(m, H, k)
+                        res[(env, m, k)] = (u, w, s, t["candidates"])
+                        if k == 10 ** 6:
+                            u2, w2, s2, t2 = G.predict(m, H, k)  # the memo after a redo
+                            assert np.array_equal(u, u2) and np.array_equal(w, w2)
+        finally:
+            del os.environ["NLP_SMALL_ORDER"]
+    for m in (1, 0, 6):
+        for k in k_list:
+            eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k)
+            for env in ("1", "0", "2"):
+                u, w, s, c = res[(env, m, k)]
+                assert_canonical_equal(eu, ew, es, u, w, s)
+                assert c == info["candidates"]
