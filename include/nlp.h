@@ -250,6 +250,41 @@ nlp_status nlp_count_common_device(nlp_graph* g, const nlp_edge* d_edges, uint64
                                    void* stream);
 nlp_status nlp_last_common(nlp_graph* g, uint64_t* common);
 
+/* SURVEY §8(f) N1 on the device: the reference's ingest (main.cxx:241-245)
+ * from the MatrixMarket file's directed pairs (1-based ids <= n, any order;
+ * a symmetric-header file listed in both directions, as readMtxOmpW adds
+ * them): every row sorted and deduplicated (readMtxOmpW), then, unless
+ * `symmetric_input`, symmetrizeOmp with set_union_last_inplace's duplicate
+ * rule (symmetrize.hxx:72-82, _algorithm.hxx:176-214, SURVEY A.3: a key of
+ * both the row and its reverse edges is kept twice when it lies above the
+ * first reverse key missing from the row), then removeSelfLoopsOmpU (one
+ * (u, u) per row).  d_src / d_dst: m device ids; d_off: device array of
+ * n + 2 offsets (span = n + 1, row 0 empty); d_keys: device array of
+ * keys_cap entries (2 m always suffices).  *nnz = the entries;
+ * NLP_ERR_CAPACITY (with *nnz set) when keys_cap is too small.  Ids < 2^31.
+ * Synchronous; `stream` orders the work (NULL = the default stream). */
+nlp_status nlp_ingest_device(const uint32_t* d_src, const uint32_t* d_dst, uint64_t m, uint64_t n,
+                             int symmetric_input, uint64_t* d_off, uint32_t* d_keys, uint64_t keys_cap,
+                             uint64_t* nnz, int device, void* stream);
+
+/* SURVEY §8(f) N2 on the device: one deletion batch as main.cxx:164-169 makes
+ * it -- generateEdgeDeletions(rnd, y, batch, 1, span - 1, true) (batch.hxx:
+ * 29-112: per deletion up to 5 draws of u, then the floor(U deg u)-th entry of
+ * N(u), both directions), tidyBatchUpdateU (keep existing, sort, unique) and
+ * applyBatchUpdateOmpU (one occurrence of each deletion leaves its row).  rnd
+ * is std::default_random_engine (minstd_rand0) whose state is *rng_state: pass
+ * the seed for a fresh engine (default_random_engine rnd(seed)); on return it
+ * holds the engine's state, so consecutive calls continue one engine like
+ * main.cxx's.  The draws are made on the host (sequential by definition), the
+ * entries they name, the tidy and the compaction on the device.  Inputs: the
+ * CSR (d_off: span + 1, d_keys); outputs (caller's device arrays): d_off2
+ * (span + 1), d_keys2 (nnz entries suffice), *nnz2, and the directed
+ * deletions, sorted and unique (main.cxx `deletions0`), in d_del_u / d_del_v
+ * (2 batch entries suffice), *ndel.  Synchronous. */
+nlp_status nlp_delete_edges_device(const uint64_t* d_off, const uint32_t* d_keys, uint64_t span, uint64_t batch,
+                                   uint32_t* rng_state, uint64_t* d_off2, uint32_t* d_keys2, uint64_t* nnz2,
+                                   uint32_t* d_del_u, uint32_t* d_del_v, uint64_t* ndel, int device, void* stream);
+
 const char* nlp_status_string(nlp_status s);
 const char* nlp_metric_name(nlp_metric m);
 

@@ -65,6 +65,7 @@ EXPORTS = [
     "nlp_sync", "nlp_select_edges_device",
     "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
     "nlp_metric_name", "nlp_version", "nlp_graph_create_multi", "nlp_device_count", "nlp_graph_parts",
+    "nlp_ingest_device", "nlp_delete_edges_device",
 ]
 
 _lib = None
@@ -89,6 +90,10 @@ def lib(build_if_missing=True):
     L.nlp_device_count.restype = i32
     L.nlp_graph_parts.argtypes = [vp, P(i32), vp]
     L.nlp_graph_parts.restype = i32
+    L.nlp_ingest_device.argtypes = [vp, vp, u64, u64, i32, vp, vp, u64, P(u64), i32, vp]
+    L.nlp_ingest_device.restype = i32
+    L.nlp_delete_edges_device.argtypes = [vp, vp, u64, u64, P(u32), vp, vp, P(u64), vp, vp, P(u64), i32, vp]
+    L.nlp_delete_edges_device.restype = i32
     L.nlp_graph_destroy.argtypes = [vp]
     L.nlp_graph_destroy.restype = None
     L.nlp_graph_info.argtypes = [vp, P(u64), P(u64), P(u32), P(i32)]
@@ -383,6 +388,49 @@ class Graph:
 
     def __exit__(self, *a):
         self.close()
+
+
+def ingest_device(src, dst, n, symmetric_input=False, stream=None):
+    """SURVEY §8(f) N1 on the device (nlp_ingest_device): the reference's
+    readMtx rows, symmetrize (duplicate rule included) and self-loop removal
+    from the file's directed pairs (torch int32 device tensors, 1-based ids
+    <= n).  Returns (offsets int64 [n + 2], keys int32 [nnz]) on the device."""
+    import torch
+    dev = src.device.index or 0
+    _check_tensor(src, "src", (torch.int32,), dev)
+    _check_tensor(dst, "dst", (torch.int32,), dev, src.numel())
+    m = src.numel()
+    off = torch.empty(n + 2, dtype=torch.int64, device=src.device)
+    keys = torch.empty(max(2 * m, 1), dtype=torch.int32, device=src.device)
+    nnz = ctypes.c_uint64()
+    _check(lib().nlp_ingest_device(src.data_ptr() if m else None, dst.data_ptr() if m else None, m, int(n),
+                                   int(bool(symmetric_input)), off.data_ptr(), keys.data_ptr(), keys.numel(),
+                                   ctypes.byref(nnz), dev, _stream_ptr(stream, src)), "nlp_ingest_device")
+    return off, keys[:nnz.value].clone()
+
+
+def delete_edges_device(offsets, keys, batch, rng_state, stream=None):
+    """SURVEY §8(f) N2 on the device (nlp_delete_edges_device): one deletion
+    batch drawn by std::default_random_engine at `rng_state` (the seed of a
+    fresh engine, or the state a previous call returned), tidied and applied.
+    Returns (offsets', keys', del_u, del_v, rng_state') -- the deletions
+    directed, sorted, unique (main.cxx deletions0)."""
+    import torch
+    dev = offsets.device.index or 0
+    _check_tensor(offsets, "offsets", (torch.int64,), dev, 1)
+    _check_tensor(keys, "keys", (torch.int32,), dev)
+    span = offsets.numel() - 1
+    off2 = torch.empty_like(offsets)
+    keys2 = torch.empty(max(keys.numel(), 1), dtype=torch.int32, device=keys.device)
+    du = torch.empty(max(2 * int(batch), 1), dtype=torch.int32, device=keys.device)
+    dv = torch.empty_like(du)
+    st = ctypes.c_uint32(int(rng_state) & 0xFFFFFFFF)
+    n2, nd = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().nlp_delete_edges_device(offsets.data_ptr(), keys.data_ptr() if keys.numel() else None, span,
+                                         int(batch), ctypes.byref(st), off2.data_ptr(), keys2.data_ptr(),
+                                         ctypes.byref(n2), du.data_ptr(), dv.data_ptr(), ctypes.byref(nd), dev,
+                                         _stream_ptr(stream, offsets)), "nlp_delete_edges_device")
+    return off2, keys2[:n2.value].clone(), du[:nd.value].clone(), dv[:nd.value].clone(), st.value
 
 
 def _make_predictor(metric):

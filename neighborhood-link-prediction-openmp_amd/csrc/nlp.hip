@@ -25,6 +25,8 @@
 #include "sortpath.hpp"
 #include "hashpath.hpp"
 #include "multi.hpp"
+#include "ingest.hpp"
+#include "../../include/nlp/random.hxx"
 
 using namespace nlp;
 
@@ -3096,6 +3098,241 @@ nlp_status predict_group(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t
   }
   return NLP_OK;
 }
+
+
+// ================================================================ N1 / N2 on the device
+// (csrc/ingest.hpp; SURVEY §8(f): the reference's ingest and deletion batch)
+
+struct DevTmp {  // device scratch of one call, freed on every exit
+  std::vector<void*> p;
+  ~DevTmp() {
+    for (void* x : p)
+      if (x) (void)hipFree(x);
+  }
+  template <typename T>
+  hipError_t get(T** out, uint64_t n) {
+    void* x = nullptr;
+    hipError_t e = hipMalloc(&x, std::max<uint64_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) p.push_back(x);
+    *out = (T*)x;
+    return e;
+  }
+};
+
+// stable LSD sort of u64 keys on the given byte shifts; the sorted keys end in *k
+hipError_t sort_u64_keys(uint64_t** k, uint64_t** k2, uint64_t n, const int* shifts, int np, DevTmp& tmp,
+                         hipStream_t st) {
+  if (n <= 1) return hipSuccess;
+  const uint64_t nb = rs_blocks(n);
+  uint32_t* hist;
+  uint64_t *hoff, *scan;
+  NLP_HIP(tmp.get(&hist, (uint64_t)RS_BINS * nb));
+  NLP_HIP(tmp.get(&hoff, (uint64_t)RS_BINS * nb));
+  NLP_HIP(tmp.get(&scan, scan_scratch_words((uint64_t)RS_BINS * nb) + 16));
+  SortScratch sc{hist, hoff, scan, nb};
+  int which = 0;
+  NLP_HIP(sort_pairs_u64(*k, nullptr, *k2, nullptr, n, shifts, np, sc, &which, st));
+  if (which) std::swap(*k, *k2);
+  return hipSuccess;
+}
+
+// the byte shifts covering a u64 key whose high word holds hbits bits above bit `hi`
+// and whose low part holds lbits bits
+int key_shifts(int lbits, int hi, int hbits, int* shifts) {
+  int np = 0;
+  for (int b = 0; b < lbits; b += 8) shifts[np++] = b;
+  for (int b = hi; b < hi + hbits; b += 8) shifts[np++] = b;
+  return np;
+}
+
+// sorted unique keys: compact in place into *out (count in *n_out)
+nlp_status unique_keys(const uint64_t* k, uint64_t n, uint64_t* out, uint64_t* n_out, DevTmp& tmp, hipStream_t st) {
+  uint8_t* flag;
+  uint64_t *pos, *scan;
+  TRY(tmp.get(&flag, n));
+  TRY(tmp.get(&pos, n + 1));
+  TRY(tmp.get(&scan, scan_scratch_words(n) + 16));
+  LAUNCH(k_in_first, n, st, k, n, flag);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint8_t>(flag, n, pos, pos + n, scan, st));
+  LAUNCH(k_in_compact<uint64_t>, n, st, k, (const uint8_t*)flag, (const uint64_t*)pos, n, out);
+  TRY(hipGetLastError());
+  TRY(hipMemcpyAsync(n_out, pos + n, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  return NLP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+nlp_status nlp_ingest_device(const uint32_t* d_src, const uint32_t* d_dst, uint64_t m, uint64_t n,
+                             int symmetric_input, uint64_t* d_off, uint32_t* d_keys, uint64_t keys_cap,
+                             uint64_t* nnz, int device, void* stream) {
+  if (!nnz || !d_off || (m && (!d_src || !d_dst)) || n >= (1ull << 31)) return NLP_ERR_INVALID;
+  *nnz = 0;
+  nlp_status s = check_device(device);
+  if (s != NLP_OK) return s;
+  TRY(hipSetDevice(device));
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t span = n + 1;
+  DevTmp tmp;
+  const int vb = std::max(1, bits_for(n));
+  uint64_t ne = 0;
+  uint64_t *e = nullptr, *e2 = nullptr;
+  if (m) {  // readMtxOmpW: every row sorted and unique
+    TRY(tmp.get(&e, m));
+    TRY(tmp.get(&e2, m));
+    LAUNCH(k_in_pairs, m, st, d_src, d_dst, m, e);
+    TRY(hipGetLastError());
+    int shifts[16];
+    const int np = key_shifts(vb, 32, vb, shifts);
+    TRY(sort_u64_keys(&e, &e2, m, shifts, np, tmp, st));
+    s = unique_keys(e, m, e2, &ne, tmp, st);
+    if (s != NLP_OK) return s;
+    std::swap(e, e2);  // the distinct pairs, sorted
+  }
+  // the union entries (row << 33 | key << 1 | tag), sorted
+  const uint64_t nent = symmetric_input ? ne : 2 * ne;
+  uint64_t *ent = nullptr, *ent2 = nullptr;
+  TRY(tmp.get(&ent, nent));
+  if (ne && symmetric_input) {  // the rows as read: tag-0 entries, already in (row, key) order
+    LAUNCH(k_in_row_entries, ne, st, (const uint64_t*)e, ne, ent);
+    TRY(hipGetLastError());
+  } else if (ne) {  // symmetrizeOmp's entries: both directions, sorted by (row, key, tag)
+    TRY(tmp.get(&ent2, nent));
+    LAUNCH(k_in_sym_entries, ne, st, (const uint64_t*)e, ne, ent);
+    TRY(hipGetLastError());
+    int shifts[16];
+    const int np = key_shifts(std::min(64, 1 + vb), 33, vb, shifts);
+    TRY(sort_u64_keys(&ent, &ent2, nent, shifts, np, tmp, st));
+  }
+  // t_v (symmetrize) and the keep flags of the union and of removeSelfLoops
+  uint32_t* t;
+  uint8_t* keep;
+  uint64_t *pos, *scan;
+  TRY(tmp.get(&t, span));
+  TRY(tmp.get(&keep, nent));
+  TRY(tmp.get(&pos, nent + 1));
+  TRY(tmp.get(&scan, scan_scratch_words(nent) + 16));
+  TRY(hipMemsetAsync(t, 0xff, span * 4, st));
+  if (nent) {
+    if (!symmetric_input) LAUNCH(k_in_first_absent, nent, st, (const uint64_t*)ent, nent, t);
+    LAUNCH(k_in_keep, nent, st, (const uint64_t*)ent, nent, (const uint32_t*)t, symmetric_input ? 0 : 1, keep);
+    TRY(hipGetLastError());
+  }
+  TRY(scan_excl_u64<uint8_t>(keep, nent, pos, pos + nent, scan, st));
+  uint64_t total = 0;
+  TRY(hipMemcpyAsync(&total, pos + nent, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  *nnz = total;
+  if (total > keys_cap || (total && !d_keys)) return NLP_ERR_CAPACITY;
+  if (nent) {
+    LAUNCH(k_in_scatter_keys, nent, st, (const uint64_t*)ent, (const uint8_t*)keep, (const uint64_t*)pos, nent, d_keys);
+    TRY(hipGetLastError());
+  }
+  LAUNCH(k_in_offsets, span + 1, st, (const uint64_t*)ent, nent, (const uint64_t*)pos, span, d_off);
+  TRY(hipGetLastError());
+  TRY(hipStreamSynchronize(st));
+  return NLP_OK;
+}
+
+nlp_status nlp_delete_edges_device(const uint64_t* d_off, const uint32_t* d_keys, uint64_t span, uint64_t batch,
+                                   uint32_t* rng_state, uint64_t* d_off2, uint32_t* d_keys2, uint64_t* nnz2,
+                                   uint32_t* d_del_u, uint32_t* d_del_v, uint64_t* ndel, int device, void* stream) {
+  if (!d_off || !rng_state || !d_off2 || !nnz2 || !ndel || span == 0 || span > 0xffffffffull ||
+      (batch && (!d_del_u || !d_del_v)))
+    return NLP_ERR_INVALID;
+  *nnz2 = 0;
+  *ndel = 0;
+  nlp_status s = check_device(device);
+  if (s != NLP_OK) return s;
+  TRY(hipSetDevice(device));
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<uint64_t> off(span + 1);
+  TRY(hipMemcpyAsync(off.data(), d_off, (span + 1) * 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t M = off[span];
+  if (M && !d_keys2) return NLP_ERR_INVALID;
+  // generateEdgeDeletions(rnd, y, batch, 1, span - 1, true) (batch.hxx:99-112, 29-58): per deletion up
+  // to 5 attempts (retry, _utility.hxx:199-203), u = K(1 + (span - 1) U), then K(U deg u) -- the draws
+  std::vector<uint32_t> du, di;
+  du.reserve(batch);
+  di.reserve(batch);
+  nlp::Minstd0 rnd(*rng_state);  // a seed, or a state in [1, 2^31 - 2] (which seeds to itself)
+  const size_t i0 = 1, n0 = span - 1;
+  for (uint64_t l = 0; l < batch; ++l) {
+    for (int attempt = 0; attempt < 5; ++attempt) {
+      const uint32_t u = (uint32_t)(i0 + n0 * nlp::canonical01(rnd));
+      const uint64_t d = u < span ? off[u + 1] - off[u] : 0;
+      if (d == 0) continue;
+      du.push_back(u);
+      di.push_back((uint32_t)(nlp::canonical01(rnd) * d));
+      break;
+    }
+  }
+  *rng_state = rnd.x;
+  const uint64_t nd = du.size();
+  DevTmp tmp;
+  uint64_t nt = 0;
+  uint64_t *dk = nullptr, *dk2 = nullptr;
+  const int vb = std::max(1, bits_for(span - 1));
+  if (nd) {
+    uint32_t *ddu, *ddi;
+    TRY(tmp.get(&ddu, nd));
+    TRY(tmp.get(&ddi, nd));
+    TRY(hipMemcpyAsync(ddu, du.data(), nd * 4, hipMemcpyHostToDevice, st));
+    TRY(hipMemcpyAsync(ddi, di.data(), nd * 4, hipMemcpyHostToDevice, st));
+    TRY(tmp.get(&dk, 2 * nd));
+    TRY(tmp.get(&dk2, 2 * nd));
+    LAUNCH(k_del_pick, nd, st, (const uint32_t*)ddu, (const uint32_t*)ddi, nd, d_off, d_keys, dk);
+    TRY(hipGetLastError());
+    // tidyBatchUpdateU (batch.hxx:152-208): keep existing, sort, unique
+    int shifts[16];
+    const int np = key_shifts(vb, 32, vb, shifts);
+    TRY(sort_u64_keys(&dk, &dk2, 2 * nd, shifts, np, tmp, st));
+    uint8_t* f;
+    uint64_t *pos, *scan;
+    TRY(tmp.get(&f, 2 * nd));
+    TRY(tmp.get(&pos, 2 * nd + 1));
+    TRY(tmp.get(&scan, scan_scratch_words(2 * nd) + 16));
+    LAUNCH(k_del_tidy, 2 * nd, st, (const uint64_t*)dk, 2 * nd, d_off, d_keys, span, f);
+    TRY(hipGetLastError());
+    TRY(scan_excl_u64<uint8_t>(f, 2 * nd, pos, pos + 2 * nd, scan, st));
+    LAUNCH(k_in_compact<uint64_t>, 2 * nd, st, (const uint64_t*)dk, (const uint8_t*)f, (const uint64_t*)pos, 2 * nd,
+           dk2);
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(&nt, pos + 2 * nd, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    std::swap(dk, dk2);
+  }
+  // applyBatchUpdateOmpU (batch.hxx:239-247): one occurrence per deletion leaves its row
+  uint8_t *gone, *keep;
+  uint64_t *pos, *scan;
+  TRY(tmp.get(&gone, M));
+  TRY(tmp.get(&keep, M));
+  TRY(tmp.get(&pos, M + 1));
+  TRY(tmp.get(&scan, scan_scratch_words(M) + 16));
+  TRY(hipMemsetAsync(gone, 0, std::max<uint64_t>(M, 1), st));
+  if (nt) LAUNCH(k_del_mark, nt, st, (const uint64_t*)dk, nt, d_off, d_keys, span, gone);
+  if (M) LAUNCH(k_del_keepflag, M, st, (const uint8_t*)gone, M, keep);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint8_t>(keep, M, pos, pos + M, scan, st));
+  if (M) LAUNCH(k_in_compact<uint32_t>, M, st, d_keys, (const uint8_t*)keep, (const uint64_t*)pos, M, d_keys2);
+  LAUNCH(k_del_offsets, span + 1, st, d_off, span, (const uint64_t*)pos, d_off2);
+  if (nt) LAUNCH(k_del_split, nt, st, (const uint64_t*)dk, nt, d_del_u, d_del_v);
+  TRY(hipGetLastError());
+  uint64_t m2 = 0;
+  TRY(hipMemcpyAsync(&m2, pos + M, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  *nnz2 = m2;
+  *ndel = nt;
+  return NLP_OK;
+}
+
+}  // extern "C"
+
+namespace {
 
 }  // namespace
 

@@ -1,0 +1,77 @@
+"""SURVEY §8(f) N1 + N2 on the device (nlp_ingest_device,
+nlp_delete_edges_device) bit-exact against the reference's own ingest:
+tests/golden/ingest_*.npz (and the prediction fixtures g300 / g3k) were made by
+oracle/_ref/ref_driver -- readMtxOmpW -> symmetrizeOmp -> removeSelfLoopsOmpU ->
+generateEdgeDeletions(default_random_engine(seed)) -> tidyBatchUpdateU ->
+applyBatchUpdateOmpU (main.cxx:164-169, 241-245) -- so the CSR after the
+deletions (duplicate entries of the symmetrize quirk included) and the
+directed deletion list must match byte for byte."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from mtx import parse_mtx
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gpu(nlp):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return nlp
+
+
+def ingest(nlp, text, seed, d):
+    import torch
+    u, v, n, _ = parse_mtx(text)
+    src = torch.from_numpy(u.view(np.int32)).cuda()
+    dst = torch.from_numpy(v.view(np.int32)).cuda()
+    off, keys = nlp.ingest_device(src, dst, n)  # ref_driver ingest symmetrizes every input
+    batch = int(d * keys.numel() / 2)  # size_t(d * x.size()/2), main.cxx:166
+    off2, keys2, du, dv, state = nlp.delete_edges_device(off, keys, batch, seed)
+    return (off2.cpu().numpy().astype(np.uint64), keys2.cpu().numpy().view(np.uint32),
+            du.cpu().numpy().view(np.uint32), dv.cpu().numpy().view(np.uint32), state)
+
+
+@pytest.mark.parametrize("name", ["general", "sym", "d0"])
+def test_gpu_ingest_matches_reference_fixtures(gpu, name):
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "ingest_%s.npz" % name), allow_pickle=False))
+    off, keys, du, dv, _ = ingest(gpu, g["mtx"].tobytes(), int(g["seed"][0]), float(g["d"][0]))
+    assert np.array_equal(off, g["offsets"]), "offsets differ"
+    assert np.array_equal(keys, g["keys"]), "adjacency differs"
+    assert np.array_equal(du, g["del_u"]) and np.array_equal(dv, g["del_w"]), "deletions differ"
+
+
+@pytest.mark.parametrize("name,params", [("g300", (300, 1200, 0.6, 1)), ("g3k", (3000, 20000, 0.6, 7))])
+def test_gpu_ingest_reproduces_prediction_fixtures(gpu, tmp_path, name, params):
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import chung_lu_mtx
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"), allow_pickle=False))
+    mtx = str(tmp_path / "in.mtx")
+    chung_lu_mtx(mtx, *params)
+    off, keys, du, dv, _ = ingest(gpu, open(mtx, "rb").read(), 42, 0.1)
+    assert np.array_equal(off, g["offsets"]) and np.array_equal(keys, g["keys"])
+    assert np.array_equal(du, g["del_u"]) and np.array_equal(dv, g["del_w"])
+    if name == "g3k":  # the symmetrize duplicates are there
+        assert int(np.sum(np.diff(keys.astype(np.int64)) == 0)) > 0
+
+
+def test_gpu_rng_state_continues_one_engine(gpu):
+    """Two batches from one engine (main.cxx keeps one default_random_engine):
+    the second call, started from the state the first returned, draws what a
+    single engine draws next -- the same as deleting twice on the host."""
+    import torch
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "ingest_general.npz"), allow_pickle=False))
+    u, v, n, _ = parse_mtx(g["mtx"].tobytes())
+    off, keys = gpu.ingest_device(torch.from_numpy(u.view(np.int32)).cuda(), torch.from_numpy(v.view(np.int32)).cuda(), n)
+    a = gpu.delete_edges_device(off, keys, 200, 7)
+    b = gpu.delete_edges_device(off, keys, 200, a[4])
+    c = gpu.delete_edges_device(off, keys, 400, 7)  # the same 400 draws in one call
+    pairs = lambda r: set(zip(r[2].cpu().tolist(), r[3].cpu().tolist()))
+    assert pairs(a) | pairs(b) == pairs(c)
+    assert b[4] == c[4]

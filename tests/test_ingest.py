@@ -78,3 +78,29 @@ def test_ingest_matches_live_reference(ingest_bin, tmp_path):
         du, dw = O.read_deletions(pre + ".del")
         got = run_ingest(ingest_bin, mtx, seed, d, str(tmp_path / "out"))
         assert_same(got, dict(offsets=off, keys=keys, del_u=du, del_w=dw))
+
+
+def test_minstd0_canonical_matches_libstdcxx(tmp_path):
+    """include/nlp/random.hxx (the engine the device ingest draws from, its
+    state exposed) equals std::default_random_engine +
+    uniform_real_distribution<double>(0, 1) draw for draw."""
+    src = tmp_path / "rt.cxx"
+    src.write_text(r'''
+#include "nlp/random.hxx"
+#include <random>
+#include <cstdio>
+int main() {
+  for (unsigned seed : {0u, 1u, 42u, 123456789u, 2147483647u, 4294967295u}) {
+    std::default_random_engine a(seed);
+    nlp::Minstd0 b(seed);
+    std::uniform_real_distribution<> d(0.0, 1.0);
+    for (int i = 0; i < 3000000; ++i)
+      if (d(a) != nlp::canonical01(b)) { printf("differ: seed %u draw %d\n", seed, i); return 1; }
+    if (a() != b()) return 2;
+  }
+  return 0;
+}''')
+    exe = str(tmp_path / "rt")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
