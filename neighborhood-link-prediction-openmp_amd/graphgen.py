@@ -13,6 +13,10 @@ shape of each BASELINE.json config:
 Vertex ids are 1..n and row 0 is empty, as in the reference's DiGraph
 (mtx.hxx reads 1-based ids; Graph.hxx span() = n+1).
 
+On a GPU the pairs go through the reference's own ingest and deletion batch
+on the device instead (make_workload's ingest="reference"); the host-side
+construction below is the "simple" variant the CPU tests use.
+
 Deletions follow the reference's sampling shape (batch.hxx:29-58, 99-112):
 a uniformly random vertex u in [1, n] (retried up to 5 times when deg(u)=0,
 _utility.hxx:432), then a uniformly random entry of N(u); both directions are
@@ -235,18 +239,43 @@ def delete_edges(offsets, keys, frac, seed, n=None):
     return off2, keys2, (pairs // span).to(torch.int32), (pairs % span).to(torch.int32)
 
 
-def make_workload(name_or_spec, device="cpu", scale=1.0):
+def make_workload(name_or_spec, device="cpu", scale=1.0, ingest=None):
     """Build (offsets, keys, del_u, del_w, spec) for a CONFIGS entry.
 
-    `scale` shrinks n and m proportionally (tests use small scales)."""
+    `scale` shrinks n and m proportionally (tests use small scales).
+
+    ingest = "reference" (the default on a GPU): the Chung-Lu pairs are the
+    MatrixMarket file's lines and go through the reference's own ingest and
+    deletion batch on the device (nlp_ingest_device / nlp_delete_edges_device,
+    SURVEY §8(f) N1 + N2): symmetrize with its duplicate rule (the graph keeps
+    the duplicate entries main.cxx's graph has), then generateEdgeDeletions
+    with std::default_random_engine(seed + 1000) and batch size
+    size_t(d |E| / 2) (main.cxx:164-169), tidied and applied one occurrence at
+    a time.  ingest = "simple" (the default on the CPU): the deduplicated
+    symmetric graph and the counter-based deletions above, for host tests."""
     spec = CONFIGS[name_or_spec] if isinstance(name_or_spec, str) else name_or_spec
     n, m, alpha, seed, d, metric, hub = spec
     n = max(16, int(math.ceil(n * scale)))
     m = max(16, int(math.ceil(m * scale)))
+    if ingest is None:
+        ingest = "reference" if str(device).startswith("cuda") else "simple"
     src, dst = chung_lu_edges(n, m, alpha, seed, device)
-    off, keys = symmetric_csr(n, src, dst)
-    del src, dst
-    off2, keys2, du, dw = delete_edges(off, keys, d, seed + 1000, n=n)
+    if ingest == "reference":
+        import nlp_amd
+        src, dst = src.to(torch.int32), dst.to(torch.int32)
+        if src.is_cuda:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()  # the library allocates its scratch with hipMalloc
+        off, keys = nlp_amd.ingest_device(src, dst, n)
+        del src, dst
+        if off.is_cuda:
+            torch.cuda.empty_cache()
+        batch = int(d * keys.numel() / 2)  # size_t(d * x.size()/2), main.cxx:166
+        off2, keys2, du, dw, _ = nlp_amd.delete_edges_device(off, keys, batch, seed + 1000)
+    else:
+        off, keys = symmetric_csr(n, src, dst)
+        del src, dst
+        off2, keys2, du, dw = delete_edges(off, keys, d, seed + 1000, n=n)
     return off2, keys2, du, dw, dict(n=n, m=m, alpha=alpha, seed=seed, d=d, metric=metric, hub=hub,
                                      M_before=int(keys.numel()), M=int(keys2.numel()),
-                                     k=int(du.numel()) // 2)
+                                     k=int(du.numel()) // 2, ingest=ingest)

@@ -75,3 +75,34 @@ def test_gpu_rng_state_continues_one_engine(gpu):
     pairs = lambda r: set(zip(r[2].cpu().tolist(), r[3].cpu().tolist()))
     assert pairs(a) | pairs(b) == pairs(c)
     assert b[4] == c[4]
+
+
+def test_gpu_workload_uses_the_reference_ingest(gpu, tmp_path):
+    """graphgen's GPU workload (the bench / config graphs) = the host
+    restatement of the reference's ingest (include/nlp/ingest.hxx, itself
+    bit-exact against the reference) run on the same pairs written as a
+    MatrixMarket file, with the same seed and deletion fraction."""
+    import subprocess
+    import torch
+    import nlp_loader
+    gg = nlp_loader.load_sub("graphgen")
+    spec = gg.CONFIGS["C2-soc-LiveJournal1"]
+    off, keys, du, dw, info = gg.make_workload(spec, "cuda", scale=0.002)
+    assert info["ingest"] == "reference"
+    n, m, alpha, seed, d = info["n"], info["m"], spec[2], spec[3], spec[4]
+    src, dst = gg.chung_lu_edges(n, m, alpha, seed, "cpu")  # counter-based: the same pairs as on the device
+    mtx = str(tmp_path / "w.mtx")
+    with open(mtx, "w") as f:
+        f.write("%%%%MatrixMarket matrix coordinate pattern general\n%d %d %d\n" % (n, n, src.numel()))
+        f.write("\n".join("%d %d" % (a, b) for a, b in zip(src.tolist(), dst.tolist())) + "\n")
+    exe = str(tmp_path / "ingest_main")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-fopenmp", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "ingest_main.cxx"), "-o", exe], check=True)
+    subprocess.run([exe, mtx, str(seed + 1000), repr(d), str(tmp_path / "h")], check=True, capture_output=True)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    hoff, hkeys = pyoracle.read_csr(str(tmp_path / "h.csr"))
+    hu, hw = pyoracle.read_deletions(str(tmp_path / "h.del"))
+    assert np.array_equal(off.cpu().numpy().astype(np.uint64), hoff)
+    assert np.array_equal(keys.cpu().numpy().view(np.uint32), hkeys)
+    assert np.array_equal(du.cpu().numpy().view(np.uint32), hu) and np.array_equal(dw.cpu().numpy().view(np.uint32), hw)
