@@ -288,6 +288,92 @@ __device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t
   }
 }
 
+// ---------------------------------------------------------------- latency batching
+// Every loop below does a dependent global load per item (a key of N(v), a
+// degree, a scratch word) and then LDS work on it.  Issued one item at a time
+// a lane waits a full memory round trip per item; here each lane first issues
+// the loads of HP_UN items (their addresses from LDS searches, which do not
+// wait on the outstanding global loads: separate counters), then consumes them.
+constexpr int HP_UN = 4;
+
+// The wedges of one block of first-hop entries: wedge j belongs to the entry
+// whose inclusive length prefix s_incl first exceeds j (NS entries, searched in
+// LDS); f(w, v) for every wedge, HP_UN per lane in flight.  stride = the
+// threads sharing the block (64: a wave; HP_BNT: a workgroup), t = this
+// thread's index among them.
+template <int NS, typename IT, typename F>
+__device__ __forceinline__ void hp_wedges(uint64_t total, uint32_t t, uint32_t stride, const IT* s_incl,
+                                          const uint64_t* s_start, const uint32_t* s_iv, const uint32_t* keys, F f) {
+  for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)stride * HP_UN) {
+    uint32_t w[HP_UN], v[HP_UN];
+    bool ok[HP_UN];
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * stride + t;
+      ok[q] = j < total;
+      uint32_t lo = 0, hi = NS - 1;  // first entry o with s_incl[o] > j
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((uint64_t)s_incl[m] > j) hi = m; else lo = m + 1;
+      }
+      const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
+      v[q] = s_iv[lo];
+      w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
+    }
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q)
+      if (ok[q]) f(w[q], v[q]);
+  }
+}
+
+// n consecutive words src[0..n): f(x) for each, HP_UN per lane in flight
+template <typename F>
+__device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint32_t t, uint32_t stride, F f) {
+  for (uint64_t i0 = 0; i0 < n; i0 += (uint64_t)stride * HP_UN) {
+    uint32_t x[HP_UN];
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q) {
+      const uint64_t i = i0 + (uint64_t)q * stride + t;
+      x[q] = src[i < n ? i : 0ull];
+    }
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q)
+      if (i0 + (uint64_t)q * stride + t < n) f(x[q]);
+  }
+}
+
+// Take, score and emit every entry of a table of T slots (T a multiple of
+// 64): the slots of HP_UN rounds first (LDS or slab), then their degree loads
+// (count metrics) in flight together, then the scores; every thread of the
+// caller runs every round (hp_emit ballots per wave).
+template <bool GLOBAL, bool CUSTOM>
+__device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
+                                         const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
+  for (uint32_t i0 = 0; i0 < T; i0 += stride * HP_UN) {
+    uint32_t w[HP_UN], c[HP_UN], v0[HP_UN], v1[HP_UN], dw[HP_UN];
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q) {
+      const uint32_t i = i0 + (uint32_t)q * stride + t;
+      c[q] = v0[q] = v1[q] = 0;
+      w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+    }
+    if (!CUSTOM) {
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) dw[q] = a.g.deg[w[q] != HP_EMPTY ? w[q] : 0u];
+    }
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q) {
+      const bool valid = w[q] != HP_EMPTY;
+      float s = 0.0f;
+      if (valid) {
+        if (CUSTOM) s = hp_score<true>(a, u, du, w[q], c[q], v0[q], v1[q]);
+        else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & HP_CMASK), du, (uint64_t)dw[q]);
+      }
+      hp_emit(sg, a, valid, s, u, w[q], tau);
+    }
+  }
+}
+
 __global__ void k_sum_deg2_above(const uint32_t* __restrict__ deg, uint64_t S, uint32_t above,
                                  unsigned long long* __restrict__ out) {
   unsigned long long s = 0;
@@ -377,6 +463,25 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
+}
+
+// The same W(u) from the survivors' side, for small H: the surviving
+// intermediates are a prefix of the degree-class index (vbydeg, degrees 1..H),
+// and every entry u of I(v) (the transposed multiset: one per occurrence of v
+// in N(u)) adds deg v to W(u) -- P_H = sum of their degrees atomics instead of
+// a pass over all M entries with a random degree gather each (C4 at H = 16:
+// ~1e7 in-edges instead of 3.5e9 entries).
+__global__ __launch_bounds__(NT) void k_hp_work_surv(GraphView g, const uint32_t* __restrict__ surv, uint64_t nsurv,
+                                                     uint64_t ua, uint64_t ub, unsigned long long* __restrict__ wu) {
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < nsurv; i += (uint64_t)gridDim.x * NT) {
+    const uint32_t v = surv[i];
+    const unsigned long long d = g.deg[v];
+    const uint64_t a = g.toff[v], b = g.toff[v + 1];
+    for (uint64_t e = a; e < b; ++e) {
+      const uint64_t u = g.tkeys[e];
+      if (u >= ua && u < ub) atomicAdd(&wu[u - ua], d);
+    }
   }
 }
 
@@ -558,33 +663,21 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       s_iv[wv][lane] = v;
       wave_sync_lds();
       const uint32_t total = __shfl(incl, 63, 64);
-      for (uint32_t j = lane; j < total; j += 64) {
-        uint32_t lo = 0, hi = 63;  // first o with incl[o] > j
-        while (lo < hi) {
-          const uint32_t m = (lo + hi) >> 1;
-          if (s_incl[wv][m] > j) hi = m; else lo = m + 1;
-        }
-        const uint32_t ex = lo ? s_incl[wv][lo - 1] : 0u;
-        const uint32_t w = a.g.keys[s_start[wv][lo] + (j - ex)];
-        if (w > u) {
-          ++wedges;
-          hp_insert<false, CUSTOM>(tb, mask, shift, w, s_iv[wv][lo], &a.ctr[HPC_ERR]);
-        }
-      }
+      hp_wedges<64>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                    [&](uint32_t w, uint32_t v) {
+                      if (w > u) {
+                        ++wedges;
+                        hp_insert<false, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
+                      }
+                    });
       wave_sync_lds();
     }
-    for (uint64_t i = lane; i < du; i += 64) {  // first-order exclusion (predict.hxx:306-307)
-      const uint32_t x = a.g.keys[o0 + i];
+    // first-order exclusion (predict.hxx:306-307)
+    hp_stream(a.g.keys + o0, du, (uint32_t)lane, 64u, [&](uint32_t x) {
       if (x > u) hp_mark<false>(tb, mask, shift, x);
-    }
+    });
     wave_sync_lds();
-    for (uint32_t i = lane; i < T; i += 64) {
-      uint32_t c = 0, v0 = 0, v1 = 0;
-      const uint32_t w = hp_take<false, CUSTOM>(tb, i, &c, &v0, &v1);
-      const bool valid = w != HP_EMPTY;
-      const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
-      hp_emit(sg, a, valid, s, u, w, tau);
-    }
+    hp_drain<false, CUSTOM>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -707,34 +800,21 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
         if (t == HP_BNT - 1) s_tot = incl;
         hp_sync<GLOBAL>();
         const uint64_t total = s_tot;
-        for (uint64_t j = t; j < total; j += HP_BNT) {
-          uint32_t lo = 0, hi = HP_BNT - 1;
-          while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (s_incl[m] > j) hi = m; else lo = m + 1;
-          }
-          const uint64_t ex = lo ? s_incl[lo - 1] : 0ull;
-          const uint32_t w = a.g.keys[s_start[lo] + (j - ex)];
-          if (w > u) {
-            if (p == 0) ++wedges;
-            if ((uint64_t)w >= wlo && (uint64_t)w < whi)
-              hp_insert<GLOBAL, CUSTOM>(tb, mask, shift, w, s_iv[lo], &a.ctr[HPC_ERR]);
-          }
-        }
+        hp_wedges<HP_BNT>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
+                          [&](uint32_t w, uint32_t v) {
+                            if (w > u) {
+                              if (p == 0) ++wedges;
+                              if ((uint64_t)w >= wlo && (uint64_t)w < whi)
+                                hp_insert<GLOBAL, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
+                            }
+                          });
         hp_sync<GLOBAL>();
       }
-      for (uint64_t i = t; i < du; i += HP_BNT) {
-        const uint32_t x = a.g.keys[o0 + i];
+      hp_stream(a.g.keys + o0, du, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
         if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
-      }
+      });
       hp_sync<GLOBAL>();
-      for (uint32_t i = t; i < T; i += HP_BNT) {
-        uint32_t c = 0, v0 = 0, v1 = 0;
-        const uint32_t w = hp_take<GLOBAL, CUSTOM>(tb, i, &c, &v0, &v1);
-        const bool valid = w != HP_EMPTY;
-        const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
-        hp_emit(sg, a, valid, s, u, w, tau);
-      }
+      hp_drain<GLOBAL, CUSTOM>(tb, T, (uint32_t)t, (uint32_t)HP_BNT, sg, a, u, du, tau);
       hp_sync<GLOBAL>();
     }
   }
@@ -753,6 +833,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
 // single bucket beyond the scratch is accumulated directly from the row
 // enumeration (rare: hub-hub concentrations).
 constexpr int HP_PMAX = 4096;
+constexpr uint64_t HP_PART_W = 2048;  // wedges per w-bucket (at most LT / 2 distinct w fill its table)
 
 // Row expansion shared by the passes: calls f(w, v) for every wedge (u, v, w)
 // with w > u, v surviving; every thread of the workgroup must call it.
@@ -798,16 +879,10 @@ __device__ __forceinline__ void hp_enum_row(const HpArgs& a, uint32_t u, uint64_
     if (t == HP_BNT - 1) *s_tot = incl;
     __syncthreads();
     const uint64_t total = *s_tot;
-    for (uint64_t j = t; j < total; j += HP_BNT) {
-      uint32_t lo = 0, hi = HP_BNT - 1;
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (s_incl[m] > j) hi = m; else lo = m + 1;
-      }
-      const uint64_t ex = lo ? s_incl[lo - 1] : 0ull;
-      const uint32_t w = a.g.keys[s_start[lo] + (j - ex)];
-      if (w > u) f(w, s_iv[lo]);
-    }
+    hp_wedges<HP_BNT>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
+                      [&](uint32_t w, uint32_t v) {
+                        if (w > u) f(w, v);
+                      });
     __syncthreads();
   }
 }
@@ -892,8 +967,8 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
     const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
     const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
     if (span_w == 0) continue;
-    // buckets: about 1024 wedges each, never narrower than needed
-    uint64_t pd = (W + 1023) / 1024;
+    // buckets: about HP_PART_W wedges each, never narrower than needed
+    uint64_t pd = (W + HP_PART_W - 1) / HP_PART_W;
     const uint64_t pspan = (span_w + (LT / 2) - 1) / (LT / 2);
     if (pd > pspan) pd = pspan;
     if (a.one_bucket) pd = 1;  // test hook: one bucket per row (sub-range passes)
@@ -975,10 +1050,21 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
           const uint64_t slo = lo + q * sw_w;
           const uint64_t shi = slo + sw_w < hi ? slo + sw_w : hi;
           if (!direct) {
-            for (uint32_t i = t; i < nb; i += HP_BNT) {
-              const uint32_t w = sw[off + i];
-              if (sub == 1 || ((uint64_t)w >= slo && (uint64_t)w < shi))
-                hp_insert<false, CUSTOM>(tb, mask, hs, w, CUSTOM ? sv[off + i] : 0u, &a.ctr[HPC_ERR]);
+            for (uint32_t i0 = 0; i0 < nb; i0 += HP_BNT * HP_UN) {  // HP_UN scratch words per lane in flight
+              uint32_t wq[HP_UN], vq[HP_UN];
+#pragma unroll
+              for (int r = 0; r < HP_UN; ++r) {
+                const uint32_t i = i0 + (uint32_t)r * HP_BNT + (uint32_t)t;
+                const uint32_t ii = i < nb ? i : 0u;
+                wq[r] = sw[off + ii];
+                vq[r] = CUSTOM ? sv[off + ii] : 0u;
+              }
+#pragma unroll
+              for (int r = 0; r < HP_UN; ++r) {
+                const uint32_t i = i0 + (uint32_t)r * HP_BNT + (uint32_t)t;
+                if (i < nb && (sub == 1 || ((uint64_t)wq[r] >= slo && (uint64_t)wq[r] < shi)))
+                  hp_insert<false, CUSTOM>(tb, mask, hs, wq[r], vq[r], &a.ctr[HPC_ERR]);
+              }
             }
             __syncthreads();
           } else {
@@ -1007,13 +1093,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
             if (adv < HP_BNT) break;
           }
           __syncthreads();
-          for (uint32_t i = t; i < T; i += HP_BNT) {
-            uint32_t c = 0, v0 = 0, v1 = 0;
-            const uint32_t w = hp_take<false, CUSTOM>(tb, i, &c, &v0, &v1);
-            const bool valid = w != HP_EMPTY;
-            const float s = valid ? hp_score<CUSTOM>(a, u, du, w, c, v0, v1) : 0.0f;
-            hp_emit(sg, a, valid, s, u, w, tau);
-          }
+          hp_drain<false, CUSTOM>(tb, T, (uint32_t)t, (uint32_t)HP_BNT, sg, a, u, du, tau);
           __syncthreads();
         }
       }

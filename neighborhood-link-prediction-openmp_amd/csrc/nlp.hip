@@ -246,6 +246,7 @@ struct nlp_graph {
   uint64_t hp_emit = 0;
   int hp_minbin = 0, hp_one_bucket = 0;
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
+  bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
@@ -625,6 +626,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hc = getenv("NLP_HASH_SCAP")) g->hp_scap_force = std::max<uint64_t>(64, strtoull(hc, nullptr, 10));
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
+  if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
@@ -1422,7 +1424,18 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipStreamSynchronize(st));
     const uint64_t e0 = g->host_small[8], e1 = g->host_small[9];
     const uint64_t b1max = custom ? HP_BT / 4 : HP_B1_MAX;
-    if (e1 > e0)
+    // small H: W(u) from the survivors' in-edges (P_H atomics) when that is well below the range's entries
+    uint64_t p_h = ~0ull;
+    if (p.H >= 1 && p.H <= DCAP && g->vbydeg && !g->deg_hist.empty()) {
+      p_h = 0;
+      for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
+    }
+    if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
+      const uint64_t ns = g->dstart[p.H + 1];
+      if (ns)
+        hipLaunchKernelGGL(k_hp_work_surv, dim3(grid_full(ns)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg, ns,
+                           ua, ub, (unsigned long long*)wu);
+    } else if (e1 > e0)
       hipLaunchKernelGGL(k_hp_work_edges,
                          dim3((unsigned)std::min<uint64_t>((e1 - e0 + NT * HP_WR - 1) / (NT * HP_WR) + 1, 8192)),
                          dim3(NT), 0, st, gv, p.H, ua, nU, e0, e1, (const uint32_t*)g->tile_row,

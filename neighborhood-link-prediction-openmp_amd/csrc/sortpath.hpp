@@ -1591,7 +1591,8 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_small(const uint32_t* __rest
     if (n > SO_MAX) atomicOr((unsigned long long*)&ctr[C_FLAGS], (unsigned long long)F_SMALL);
   }
   const bool fits = n <= SO_MAX;
-  // this thread's keys: position j = wv WT + i 64 + lane (a wave owns WT consecutive positions)
+  // this thread's keys: position j = wv WT + i 64 + lane (a wave owns WT consecutive positions);
+  // the slots first (LDS searches), then all IPT key loads in flight together
   uint32_t k[IPT], sl[IPT], dg[IPT], rk[IPT];
   bool ok[IPT];
   uint32_t kor = 0u, kand = 0xffffffffu;
@@ -1599,19 +1600,20 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_small(const uint32_t* __rest
   for (int i = 0; i < IPT; ++i) {
     const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
     ok[i] = fits && j < n;
-    k[i] = 0u;
-    sl[i] = 0u;
-    if (ok[i]) {
-      uint32_t lo = 0, hi = nb;  // the bucket of j: s_pre[lo] <= j < s_pre[hi]
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre[mid] <= j) lo = mid; else hi = mid;
-      }
-      sl[i] = (lo << caplog) + (j - s_pre[lo]);
-      k[i] = okey[sl[i]];
-      kor |= k[i];
-      kand &= k[i];
+    uint32_t lo = 0, hi = nb;  // the bucket of j: s_pre[lo] <= j < s_pre[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_pre[mid] <= j) lo = mid; else hi = mid;
     }
+    sl[i] = ok[i] ? (lo << caplog) + (j - s_pre[lo]) : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) k[i] = okey[sl[i]];  // slot 0 always exists
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    if (!ok[i]) k[i] = 0u;
+    kor |= ok[i] ? k[i] : 0u;
+    kand &= ok[i] ? k[i] : 0xffffffffu;
   }
   // the key bytes that vary (OR ^ AND over all keys): only those are sorted
 #pragma unroll
@@ -1655,12 +1657,25 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_small(const uint32_t* __rest
       }
     }
   }
-  // the caller's edges: sorted position j < k
+  // the caller's edges: sorted position j < k (all 3 IPT column loads in flight, then the stores)
   const uint64_t m = fits ? (n < go.k ? (uint64_t)n : go.k) : 0ull;
+  uint32_t eu[IPT], ew[IPT];
+  float es[IPT];
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
     const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-    if (ok[i] && j < m) go.out[j] = EdgeOut{cu[sl[i]], cw[sl[i]], cs[sl[i]]};
+    if (!(ok[i] && j < m)) sl[i] = 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    eu[i] = cu[sl[i]];
+    ew[i] = cw[sl[i]];
+    es[i] = cs[sl[i]];
+  }
+#pragma unroll
+  for (int i = 0; i < IPT; ++i) {
+    const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
+    if (ok[i] && j < m) go.out[j] = EdgeOut{eu[i], ew[i], es[i]};
   }
   __syncthreads();  // ctr[C_C] and the flags are final
   if (t < NCTR) {

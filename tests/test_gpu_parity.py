@@ -410,7 +410,7 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_TIERS="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_SLICES="7"),
-                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3")]
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3"), dict(NLP_HASH_WORK_SURV="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
