@@ -37,9 +37,12 @@
 // graph resident explicitly.  Devices: NLP_DEVICES or every gfx950 device
 // (defaultDevices(), the analogue of the reference's OpenMP team).
 #pragma once
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstddef>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -283,6 +286,93 @@ inline PredictLinkResult<uint32_t, W> predictLinksHipAny(const HipGraph& g, nlp_
 }
 
 }  // namespace nlp
+
+namespace nlp {
+namespace detail {
+// canonical order of a generic result: score desc (bit-pattern key of float /
+// double, NaN last), then u asc, then v asc -- the order of the built-in metrics
+template <class W>
+inline uint64_t scoreKey(W s) {
+  const double d = double(s);
+  if (d != d) return 0;
+  uint64_t b;
+  const double z = d == 0.0 ? 0.0 : d;
+  std::memcpy(&b, &z, 8);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+}  // namespace detail
+
+/**
+ * predictLinksWithIntersectionBasic[Omp] (predict.hxx:387-407, 480-490) with a
+ * user score lambda fs(u, v, N): the GPU finds every candidate (u, w > u)
+ * reached by a wedge through a surviving intermediate, with N = |N(u) ∩ N(w)|
+ * over the survivors (0 for first-order neighbours, which the reference zeroes
+ * but keeps in its touched list, predict.hxx:306-307) -- one common-neighbours
+ * call with minScore -1 and no maxEdges limit; fs runs on the host for each,
+ * `score <= minScore` is skipped (predict.hxx:311) and the top maxEdges are
+ * kept in the canonical order.  N travels as a float (exact below 2^24).
+ */
+template <int MINDEGREE1, int MAXFACTOR2, class V, class G, class W, class FS>
+inline auto predictLinksWithIntersectionHipBasic(const G& x, const PredictLinkOptions<W>& o, FS fs) {
+  using K = typename G::key_type;
+  const HipGraph& g = detail::cachedGraph(x);
+  std::vector<std::tuple<K, K, W>> a;
+  nlp_timing t{};
+  float host_ms = 0;
+  if (o.maxEdges > 0) {
+    uint64_t n = 0;
+    check(nlp_predict_ex(g.get(), NLP_CN, uint32_t(MINDEGREE1), uint32_t(MAXFACTOR2), -1.0f, UINT64_MAX, o.repeat,
+                         nullptr, &n, &t),
+          "nlp_predict_ex");
+    std::vector<nlp_edge> buf(n);
+    uint64_t got = 0;
+    check(nlp_copy_last(g.get(), buf.data(), n, &got), "nlp_copy_last");
+    const auto h0 = std::chrono::steady_clock::now();
+    a.reserve(got);
+    for (uint64_t i = 0; i < got; ++i) {
+      if (!(buf[i].score < 16777216.0f)) throw std::runtime_error("predictLinksWithIntersectionBasic: count >= 2^24");
+      const W s = fs(K(buf[i].u), K(buf[i].v), V(buf[i].score));
+      if (s <= o.minScore) continue;
+      a.emplace_back(K(buf[i].u), K(buf[i].v), s);
+    }
+    auto lt = [](const std::tuple<K, K, W>& p, const std::tuple<K, K, W>& q) {
+      const uint64_t kp = detail::scoreKey(std::get<2>(p)), kq = detail::scoreKey(std::get<2>(q));
+      if (kp != kq) return kp > kq;
+      if (std::get<0>(p) != std::get<0>(q)) return std::get<0>(p) < std::get<0>(q);
+      return std::get<1>(p) < std::get<1>(q);
+    };
+    if (a.size() > o.maxEdges) {
+      std::nth_element(a.begin(), a.begin() + o.maxEdges, a.end(), lt);
+      a.resize(o.maxEdges);
+    }
+    std::sort(a.begin(), a.end(), lt);
+    host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - h0).count();
+  }
+  return PredictLinkResult<K, W>(std::move(a), t.total_ms + host_ms, t.score_ms + host_ms);
+}
+}  // namespace nlp
+
+// The generic entry points (predict.hxx:358-490).  CUSTOMVALUE = false is the
+// count scan (fu is never called, predict.hxx:228-229); a custom per-wedge
+// update lambda fu (CUSTOMVALUE = true) runs inside the reference's wedge loop
+// and cannot be offloaded -- it is refused at compile time rather than run on
+// the CPU.
+#define NLP_DEFINE_GENERIC(SUFFIX)                                                                          \
+  template <int MINDEGREE1 = 4, int MAXFACTOR2 = 0, bool FORCEHEAP = false, bool CUSTOMVALUE = false, class G, \
+            class V, class W, class FS, class FU>                                                           \
+  inline auto predictLinksWithIntersection##SUFFIX(const G& x, const PredictLinkOptions<W>& o, V, FS fs, FU) { \
+    static_assert(!CUSTOMVALUE, "custom per-wedge update lambdas (CUSTOMVALUE) are not offloadable; use a "    \
+                                "built-in metric or a count-based score lambda");                            \
+    return nlp::predictLinksWithIntersectionHipBasic<MINDEGREE1, MAXFACTOR2, V>(x, o, fs);                   \
+  }                                                                                                           \
+  template <int MINDEGREE1 = 4, int MAXFACTOR2 = 0, bool FORCEHEAP = false, class G, class W, class FS>      \
+  inline auto predictLinksWithIntersectionBasic##SUFFIX(const G& x, const PredictLinkOptions<W>& o, FS fs) {   \
+    return nlp::predictLinksWithIntersectionHipBasic<MINDEGREE1, MAXFACTOR2, typename G::key_type>(x, o, fs); \
+  }
+NLP_DEFINE_GENERIC()
+NLP_DEFINE_GENERIC(Omp)
+NLP_DEFINE_GENERIC(Hip)
+#undef NLP_DEFINE_GENERIC
 
 // The 27 entry points: predictLinks<Metric>, predictLinks<Metric>Omp, predictLinks<Metric>Hip.
 #define NLP_DEFINE_PREDICTOR(NAME, METRIC)                                                                 \

@@ -42,7 +42,7 @@ enum {
 constexpr uint64_t F_OVERFLOW = 1, F_TOOBIG = 2;
 // the counted ordering passes (k_sp_cpass) got more than CP_MAXT tiles: the call is redone with look-back passes
 constexpr uint64_t F_CPASS = 4;
-constexpr uint64_t F_SMALL = 8;  // k_sp_order_small: more candidates than one workgroup orders (redo without it)
+constexpr uint64_t F_SMALL = 8;  // k_sp_order_rank: more candidates than SO_MAX (redo with the counted passes)
 
 struct GraphView {
   const uint64_t* off;

@@ -63,7 +63,26 @@ struct HpArgs {
   const int64_t* tau; // emit only key > *tau
   unsigned long long* ctr;
   int one_bucket;     // test hook (k_hp_part): one w-bucket per row
+  // small H: the surviving first hops of every source of the range (S(u) =
+  // {v in N(u) : deg v <= H}, multiplicities kept, any order), so a row walks
+  // S(u) instead of all of N(u) with a degree gather per entry (null: N(u))
+  const uint64_t* soff;  // [nU + 1], indexed by u - sua
+  const uint32_t* skeys;
+  uint64_t sua;
 };
+
+// A row's first-hop list: S(u) when the survivor lists exist, else N(u).
+__device__ __forceinline__ void hp_first_hops(const HpArgs& a, uint32_t u, uint64_t o0, uint64_t du,
+                                              const uint32_t** list, uint64_t* n) {
+  if (a.soff) {
+    const uint64_t s0 = a.soff[u - a.sua];
+    *list = a.skeys + s0;
+    *n = a.soff[u - a.sua + 1] - s0;
+  } else {
+    *list = a.g.keys + o0;
+    *n = du;
+  }
+}
 
 __device__ __forceinline__ bool hp_surv(uint32_t d, uint32_t H) { return d > 0 && (H == 0 || d <= H); }
 
@@ -294,7 +313,7 @@ __device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t
 // a lane waits a full memory round trip per item; here each lane first issues
 // the loads of HP_UN items (their addresses from LDS searches, which do not
 // wait on the outstanding global loads: separate counters), then consumes them.
-constexpr int HP_UN = 4;
+constexpr int HP_UN = 2;
 
 // The wedges of one block of first-hop entries: wedge j belongs to the entry
 // whose inclusive length prefix s_incl first exceeds j (NS entries, searched in
@@ -471,16 +490,29 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
 // and every entry u of I(v) (the transposed multiset: one per occurrence of v
 // in N(u)) adds deg v to W(u) -- P_H = sum of their degrees atomics instead of
 // a pass over all M entries with a random degree gather each (C4 at H = 16:
-// ~1e7 in-edges instead of 3.5e9 entries).
-__global__ __launch_bounds__(NT) void k_hp_work_surv(GraphView g, const uint32_t* __restrict__ surv, uint64_t nsurv,
-                                                     uint64_t ua, uint64_t ub, unsigned long long* __restrict__ wu) {
+// ~1e7 in-edges instead of 3.5e9 entries).  The same walk builds the
+// survivor lists S(u) the row kernels then use instead of N(u).
+// The survivor lists S(u) of a range: count per source (and W(u) with it),
+// then, after a scan of the counts, fill (slots by a per-source cursor).
+template <bool FILL>
+__global__ __launch_bounds__(NT) void k_hp_surv_lists(GraphView g, const uint32_t* __restrict__ surv, uint64_t nsurv,
+                                                      uint64_t ua, uint64_t ub, unsigned long long* __restrict__ wu,
+                                                      uint32_t* __restrict__ cnt, const uint64_t* __restrict__ soff,
+                                                      uint32_t* __restrict__ skeys) {
   for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < nsurv; i += (uint64_t)gridDim.x * NT) {
     const uint32_t v = surv[i];
     const unsigned long long d = g.deg[v];
     const uint64_t a = g.toff[v], b = g.toff[v + 1];
     for (uint64_t e = a; e < b; ++e) {
       const uint64_t u = g.tkeys[e];
-      if (u >= ua && u < ub) atomicAdd(&wu[u - ua], d);
+      if (u < ua || u >= ub) continue;
+      if (FILL) {
+        const uint32_t p = atomicAdd(&cnt[u - ua], 1u);
+        skeys[soff[u - ua] + p] = v;
+      } else {
+        atomicAdd(&wu[u - ua], d);
+        atomicAdd(&cnt[u - ua], 1u);
+      }
     }
   }
 }
@@ -645,12 +677,15 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
     const int shift = 32 - lg;
     const uint64_t o0 = a.g.off[u], o1 = a.g.off[u + 1];
     const uint64_t du = o1 - o0;
-    for (uint64_t base = 0; base < du; base += 64) {
+    const uint32_t* fh;
+    uint64_t nf;
+    hp_first_hops(a, u, o0, du, &fh, &nf);
+    for (uint64_t base = 0; base < nf; base += 64) {
       const uint64_t i = base + lane;
       uint32_t len = 0, v = 0;
       uint64_t st = 0;
-      if (i < du) {
-        v = a.g.keys[o0 + i];
+      if (i < nf) {
+        v = fh[i];
         const uint32_t d = a.g.deg[v];
         if (hp_surv(d, a.H)) {
           len = d;
@@ -781,12 +816,15 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
     for (uint64_t p = 0; p < passes; ++p) {
       const uint64_t wlo = (uint64_t)u + 1 + p * rw;
       const uint64_t whi = wlo + rw < a.S ? wlo + rw : a.S;
-      for (uint64_t base = 0; base < du; base += HP_BNT) {
+      const uint32_t* fh;
+      uint64_t nf;
+      hp_first_hops(a, u, o0, du, &fh, &nf);
+      for (uint64_t base = 0; base < nf; base += HP_BNT) {
         const uint64_t i = base + t;
         uint32_t v = 0;
         uint64_t len = 0, st = 0;
-        if (i < du) {
-          v = a.g.keys[o0 + i];
+        if (i < nf) {
+          v = fh[i];
           const uint32_t d = a.g.deg[v];
           if (hp_surv(d, a.H)) {
             len = d;
@@ -833,7 +871,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
 // single bucket beyond the scratch is accumulated directly from the row
 // enumeration (rare: hub-hub concentrations).
 constexpr int HP_PMAX = 4096;
-constexpr uint64_t HP_PART_W = 2048;  // wedges per w-bucket (at most LT / 2 distinct w fill its table)
+constexpr uint64_t HP_PART_W = 1024;  // wedges per w-bucket
 
 // Row expansion shared by the passes: calls f(w, v) for every wedge (u, v, w)
 // with w > u, v surviving; every thread of the workgroup must call it.
@@ -845,12 +883,15 @@ __device__ __forceinline__ void hp_enum_row(const HpArgs& a, uint32_t u, uint64_
                                             uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f,
                                             uint64_t wlo = 0, uint64_t whi = 0) {
   const int t = threadIdx.x;
-  for (uint64_t base = 0; base < du; base += HP_BNT) {
+  const uint32_t* fh;
+  uint64_t nf;
+  hp_first_hops(a, u, o0, du, &fh, &nf);
+  for (uint64_t base = 0; base < nf; base += HP_BNT) {
     const uint64_t i = base + t;
     uint32_t v = 0;
     uint64_t len = 0, st = 0;
-    if (i < du) {
-      v = a.g.keys[o0 + i];
+    if (i < nf) {
+      v = fh[i];
       const uint32_t d = a.g.deg[v];
       if (hp_surv(d, a.H)) {
         len = d;

@@ -226,15 +226,31 @@ __global__ void k_p1_inedges(const uint64_t* __restrict__ ioff, uint64_t span, c
 }
 
 // ---------------------------------------------------------------- path 2: source-centric
+// The row of adjacency entry e: the per-graph tile table (tile_row[t] = the
+// row of entry t * tile, hashpath.hpp k_hp_tile_rows) bounds it to the rows
+// between two table entries, a few probes instead of a search of all offsets.
+__device__ __forceinline__ uint64_t row_of_entry(const uint64_t* __restrict__ off, const uint32_t* __restrict__ tile_row,
+                                                 uint64_t tile, uint64_t M, uint64_t span, uint64_t e) {
+  const uint64_t t = e / tile;
+  uint64_t lo = tile_row[t];                                       // off[lo] <= e
+  uint64_t hi = (t + 1) * tile < M ? (uint64_t)tile_row[t + 1] + 1 : span;  // off[hi] > e
+  while (hi - lo > 1) {  // largest u with off[u] <= e
+    const uint64_t mid = (lo + hi) >> 1;
+    if (off[mid] <= e) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 // One thread per edge e in [e0, e1) (relative index e - e0).
 __global__ void k_p2_edges(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
                            const uint32_t* __restrict__ deg, uint64_t span, uint64_t e0, uint64_t e1, uint32_t H,
                            uint32_t* __restrict__ ev, uint32_t* __restrict__ eu, uint32_t* __restrict__ ewc,
-                           uint32_t* __restrict__ efirst) {
+                           uint32_t* __restrict__ efirst, const uint32_t* __restrict__ tile_row, uint64_t tile,
+                           uint64_t M) {
   const uint64_t n = e1 - e0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t e = e0 + i;
-    uint32_t u = (uint32_t)lbs_find(off, span + 1, e);
+    uint32_t u = (uint32_t)row_of_entry(off, tile_row, tile, M, span, e);
     uint32_t v = keys[e];
     uint32_t d = deg[v];
     bool surv = (H == 0) || (d <= H);                     // predict.hxx:301

@@ -72,7 +72,7 @@ enum Buf {
   B_SP_OK0, B_SP_OK1, B_SP_OV0, B_SP_OV1, B_SP_ARENA, B_SP_SEGCNT, B_SP_BKT,
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
-  B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER,
+  B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   NBUF
 };
 
@@ -188,8 +188,8 @@ struct nlp_graph {
   bool counted_force = false;
   bool counted = true;                         // fused path: ordering passes 2-4 from per-tile digit counts (k_sp_cpass,
                                                // no look-back) when the candidates fit CP_MAXT tiles (NLP_COUNTED=0: off)
-  bool small_order = true;                     // fused path: one workgroup orders <= SO_MAX candidates
-                                               // (k_sp_order_small; NLP_SMALL_ORDER=0: off)
+  bool small_order = true;                     // fused path: one launch ranks <= SO_MAX candidates
+                                               // (k_sp_order_rank; NLP_SMALL_ORDER=0: off)
   double small_off_w = 0;                      // wedge estimate of the last call whose candidates did not fit it
   bool small_force = false;
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
@@ -1178,7 +1178,8 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   TRY(wsget(ws, B_WOFF, E + 1, &woff));
   TRY(wsget(ws, B_SCAN, scan_scratch_words(E + 1) + 16, &scan));
   TRY(wsget(ws, B_CNT, 8, &cnt));
-  LAUNCH(k_p2_edges, E, st, g->off, g->keys, g->deg, S, e0, e1, p.H, ev, eu, ewc, efirst);
+  LAUNCH(k_p2_edges, E, st, g->off, g->keys, g->deg, S, e0, e1, p.H, ev, eu, ewc, efirst, (const uint32_t*)g->tile_row,
+         (uint64_t)HP_WTILE, g->nnz);
   TRY(hipGetLastError());
   TRY(scan_excl_u64<uint32_t>(ewc, E, woff, cnt + 1, scan, st));
   TRY(hipMemcpyAsync(woff + E, cnt + 1, 8, hipMemcpyDeviceToDevice, st));  // woff[E] = W
@@ -1417,6 +1418,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
   // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
   const GraphView gv = view_of(g, p.metric, p.maxf2);
+  uint64_t* s_soff = nullptr;  // survivor lists S(u) of the range (small H), see k_hp_surv_lists
+  uint32_t* s_skeys = nullptr;
   {
     TRY(hipMemsetAsync(wu, 0, nU * 8, st));
     TRY(hipMemcpyAsync(&g->host_small[8], g->off + ua, 8, hipMemcpyDeviceToHost, st));
@@ -1431,10 +1434,25 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
     if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
+      // the survivor lists S(u) of the range, and W(u) with them: the row kernels walk S(u), not N(u)
       const uint64_t ns = g->dstart[p.H + 1];
+      uint32_t* scnt;
+      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
+      TRY(wsget(ws, B_HP_SOFF, nU + 1, &s_soff));
+      TRY(hipMemsetAsync(scnt, 0, nU * 4, st));
       if (ns)
-        hipLaunchKernelGGL(k_hp_work_surv, dim3(grid_full(ns)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg, ns,
-                           ua, ub, (unsigned long long*)wu);
+        hipLaunchKernelGGL(k_hp_surv_lists<false>, dim3(grid_full(ns)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg,
+                           ns, ua, ub, (unsigned long long*)wu, scnt, (const uint64_t*)nullptr, (uint32_t*)nullptr);
+      TRY(hipGetLastError());
+      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
+      TRY(hipMemsetAsync(scnt, 0, nU * 4, st));
+      if (ns)
+        hipLaunchKernelGGL(k_hp_surv_lists<true>, dim3(grid_full(ns)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg,
+                           ns, ua, ub, (unsigned long long*)wu, scnt, (const uint64_t*)s_soff, s_skeys);
+      TRY(hipGetLastError());
     } else if (e1 > e0)
       hipLaunchKernelGGL(k_hp_work_edges,
                          dim3((unsigned)std::min<uint64_t>((e1 - e0 + NT * HP_WR - 1) / (NT * HP_WR) + 1, 8192)),
@@ -1505,6 +1523,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.tau = (const int64_t*)(small + 8);
     a.ctr = (unsigned long long*)small;
     a.one_bucket = g->hp_one_bucket;
+    a.soff = s_skeys ? s_soff : nullptr;
+    a.skeys = s_skeys;
+    a.sua = ua;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     if (n0 && g->hp_tiers) {
       // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
@@ -1788,7 +1809,7 @@ struct SpBufs {
   uint64_t ostride;                             // u32 onesweep descriptors per pass
   uint64_t ostride11;                           // the same for 11-bit digits (the fused path's three passes)
   bool ord11;                                   // fused path: three 11-bit passes
-  bool small;                                   // fused path: k_sp_order_small orders all candidates (one launch)
+  bool small;                                   // fused path: k_sp_order_rank orders all candidates (one launch)
   bool counted;                                 // fused path: passes 2-4 are k_sp_cpass (tile digit counts from the
                                                 // pass before, count matrix p at d_cm; the last pass gathers)
   int wbits, passes;
@@ -1932,7 +1953,7 @@ nlp_status prepare_sp(nlp_graph* g, const Params& p, SpBufs& f, bool msd, int ms
     const double est = hp_estimate(g, p), cap = (double)CP_MAXT * OS2_TILE;
     f.counted = f.fused && !f.ord11 && g->counted && (g->counted_force || est < 4.0 * cap) &&
                 !(g->cp_off_w > 0 && est > 0.5 * g->cp_off_w);
-    // small calls: one workgroup orders every candidate (k_sp_order_small) when the estimate -- at least
+    // small calls: one launch ranks every candidate (k_sp_order_rank) when the estimate -- at least
     // the wedges w > u, so at least the candidates -- fits it, unless a similar call did not (F_SMALL)
     f.small = f.fused && !f.ord11 && g->small_order && !g->counted_force &&
               (g->small_force || est <= (double)SO_MAX) && !(g->small_off_w > 0 && est > 0.5 * g->small_off_w);
@@ -2188,9 +2209,9 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
     } else if (s < s_runs + 6) {
       const int ps = s - (s_runs + 2);
       const bool odd = ps & 1;
-      if (f.small) {  // all four passes and the output in one workgroup
+      if (f.small) {  // all four passes and the output in one launch (rank by counting)
         if (ps != 0) return NLP_OK;
-        hipLaunchKernelGGL(k_sp_order_small, dim3(1), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
+        hipLaunchKernelGGL(k_sp_order_rank, dim3(SR_GRID), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
                            (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
                            (uint32_t)nb_used, f.caplog,
                            GatherOut{nullptr, nullptr, nullptr, p.max_edges, out, ctr, g->host_ctr_dev, ts, g->d_sticky},

@@ -1528,37 +1528,36 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__
   if (GATHER && go.hctr && tile == ntiles - 1 && t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
 }
 
-// ---------------------------------------------------------------- small calls: one-workgroup ordering
+// ---------------------------------------------------------------- small calls: ordering by rank
 // When the candidates of a fused call fit SO_MAX keys (the LHub-4 calls of the
 // large configs: C4 predicts ~1e4 links), the four counted passes -- four
-// launches, each waiting for the previous one's keys to land in HBM -- are
-// replaced by ONE workgroup that keeps all keys on chip: the keys of the
-// concatenated buckets ((u, w) order) are loaded once with their slot, sorted
-// by four stable 8-bit LSD passes (the counted passes' ballot ranking per wave,
-// one block scan of the digit counts, placement through LDS), passes whose
-// digit is the same for every key skipped, and the first min(k, C) edges
-// gathered from the candidate columns.  The order key is ~score_key, so the
-// result is score descending, then (u, w) ascending -- the canonical order.
-// More than SO_MAX candidates raise F_SMALL and the host redoes the call with
-// the counted passes.  Publishes the counters like the last counted pass.
-constexpr int SO_IPT = 16;
-constexpr uint32_t SO_MAX = OS_NT * SO_IPT;  // 16384 keys: 128 KiB of keys and slots in LDS
+// launches, each waiting for the previous one's keys to land -- are replaced
+// by ONE launch that ranks every candidate directly: workgroup b owns the
+// SR_ELEMS candidates at positions [b SR_ELEMS, (b + 1) SR_ELEMS) of the
+// concatenated buckets ((u, w) order), loads ALL n order keys into LDS, and
+// each wave counts, for its candidates, the keys that precede them:
+//   rank(e) = #{j : key_j < key_e} + #{j < e : key_j == key_e},
+// i.e. the position in the stable sort by ~score_key -- score descending, then
+// (u, w) ascending, the canonical order.  n^2 / 64 LDS reads per wave, spread
+// over up to SO_MAX / SR_ELEMS workgroups; then each ranked candidate below k
+// is gathered from the candidate columns to the caller's edges.  More than
+// SO_MAX candidates raise F_SMALL and the host redoes the call with the
+// counted passes.  Workgroup 0 publishes the counters like the last counted pass.
+constexpr uint32_t SO_MAX = 16384;   // candidates at most (64 KiB of keys in LDS per workgroup)
+constexpr uint32_t SR_ELEMS = 64;    // candidates ranked per workgroup (4 per wave)
+constexpr uint32_t SR_GRID = SO_MAX / SR_ELEMS;
 
-__global__ __launch_bounds__(OS_NT) void k_sp_order_small(const uint32_t* __restrict__ okey,
-                                                          const uint32_t* __restrict__ cu,
-                                                          const uint32_t* __restrict__ cw,
-                                                          const float* __restrict__ cs,
-                                                          const uint32_t* __restrict__ kcnt, uint32_t nb, int caplog,
-                                                          GatherOut go, uint64_t* __restrict__ end_mark) {
-  constexpr int IPT = SO_IPT, WT = 64 * IPT;
+__global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restrict__ okey,
+                                                         const uint32_t* __restrict__ cu,
+                                                         const uint32_t* __restrict__ cw,
+                                                         const float* __restrict__ cs,
+                                                         const uint32_t* __restrict__ kcnt, uint32_t nb, int caplog,
+                                                         GatherOut go, uint64_t* __restrict__ end_mark) {
   constexpr uint32_t PER = (DX_MAXB + OS_NT - 1) / OS_NT;
+  constexpr int LD = (int)(SO_MAX / OS_NT);  // key loads per thread in flight
   __shared__ uint32_t s_key[SO_MAX];
-  __shared__ uint32_t s_slot[SO_MAX];  // first the bucket prefix (DX_MAXB + 1 <= SO_MAX entries)
-  __shared__ uint32_t s_wcnt[OS_NW][RS_BINS];
-  __shared__ uint32_t s_base[RS_BINS];
+  __shared__ uint32_t s_pre[DX_MAXB + 1];
   __shared__ uint32_t s_w[OS_NW];
-  __shared__ uint32_t s_bits[2];
-  uint32_t* s_pre = s_slot;
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel)
   {  // bucket prefix: thread t sums buckets [PER t, PER t + PER)
@@ -1577,115 +1576,81 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_small(const uint32_t* __rest
       if (b < nb) s_pre[b] = run;
       run += v[i];
     }
-    if (t == 0) {
-      s_pre[nb] = (uint32_t)tot;
-      s_bits[0] = 0u;           // OR of the keys
-      s_bits[1] = 0xffffffffu;  // AND of the keys
-    }
+    if (t == 0) s_pre[nb] = (uint32_t)tot;
   }
   __syncthreads();
   const uint32_t n = s_pre[nb];
   uint64_t* ctr = go.ctr;
-  if (t == 0) {
-    ctr[C_C] = n;
-    if (n > SO_MAX) atomicOr((unsigned long long*)&ctr[C_FLAGS], (unsigned long long)F_SMALL);
-  }
   const bool fits = n <= SO_MAX;
-  // this thread's keys: position j = wv WT + i 64 + lane (a wave owns WT consecutive positions);
-  // the slots first (LDS searches), then all IPT key loads in flight together
-  uint32_t k[IPT], sl[IPT], dg[IPT], rk[IPT];
-  bool ok[IPT];
-  uint32_t kor = 0u, kand = 0xffffffffu;
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-    ok[i] = fits && j < n;
-    uint32_t lo = 0, hi = nb;  // the bucket of j: s_pre[lo] <= j < s_pre[hi]
+  auto slot_of = [&](uint32_t j) {  // the bucket slot of position j: s_pre[lo] <= j < s_pre[lo + 1]
+    uint32_t lo = 0, hi = nb;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (s_pre[mid] <= j) lo = mid; else hi = mid;
     }
-    sl[i] = ok[i] ? (lo << caplog) + (j - s_pre[lo]) : 0u;
-  }
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) k[i] = okey[sl[i]];  // slot 0 always exists
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    if (!ok[i]) k[i] = 0u;
-    kor |= ok[i] ? k[i] : 0u;
-    kand &= ok[i] ? k[i] : 0xffffffffu;
-  }
-  // the key bytes that vary (OR ^ AND over all keys): only those are sorted
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    kor |= __shfl_xor(kor, o, 64);
-    kand &= __shfl_xor(kand, o, 64);
-  }
-  if (lane == 0) {
-    atomicOr(&s_bits[0], kor);
-    atomicAnd(&s_bits[1], kand);
-  }
-  __syncthreads();  // s_pre (s_slot) is free again
-  const uint32_t vary = s_bits[0] ^ s_bits[1];
-  for (int shift = 0; shift < 32 && fits; shift += 8) {
-    if (!((vary >> shift) & 255u)) continue;
-    for (int i = t; i < OS_NW * RS_BINS; i += OS_NT) (&s_wcnt[0][0])[i] = 0;
-    __syncthreads();
-    cp_rank<IPT>(k, ok, shift, dg, rk, s_wcnt);
-    __syncthreads();
-    uint32_t tot = 0;
-    if (t < RS_BINS) tot = cp_wave_prefix(s_wcnt, t);
-    uint64_t all;
-    const uint32_t dbase = os_digit_scan(t < RS_BINS ? tot : 0u, s_w, &all);  // syncs
-    if (t < RS_BINS) s_base[t] = dbase;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (ok[i]) {
-        const uint32_t pos = s_base[dg[i]] + s_wcnt[wv][dg[i]] + rk[i];
-        s_key[pos] = k[i];
-        s_slot[pos] = sl[i];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-      if (ok[i]) {
-        k[i] = s_key[j];
-        sl[i] = s_slot[j];
-      }
-    }
-  }
-  // the caller's edges: sorted position j < k (all 3 IPT column loads in flight, then the stores)
+    return (lo << caplog) + (j - s_pre[lo]);
+  };
+  const uint32_t e0 = blockIdx.x * SR_ELEMS;
   const uint64_t m = fits ? (n < go.k ? (uint64_t)n : go.k) : 0ull;
-  uint32_t eu[IPT], ew[IPT];
-  float es[IPT];
+  if (fits && e0 < n) {
+    {  // every key, in position order (LD loads per thread in flight)
+      uint32_t sl[LD], kk[LD];
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-    if (!(ok[i] && j < m)) sl[i] = 0u;
-  }
+      for (int i = 0; i < LD; ++i) {
+        const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+        sl[i] = j < n ? slot_of(j) : 0u;
+      }
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    eu[i] = cu[sl[i]];
-    ew[i] = cw[sl[i]];
-    es[i] = cs[sl[i]];
-  }
+      for (int i = 0; i < LD; ++i) kk[i] = okey[sl[i]];  // slot 0 always exists
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const uint32_t j = (uint32_t)wv * WT + (uint32_t)i * 64 + (uint32_t)lane;
-    if (ok[i] && j < m) go.out[j] = EdgeOut{eu[i], ew[i], es[i]};
+      for (int i = 0; i < LD; ++i) {
+        const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+        if (j < n) s_key[j] = kk[i];
+      }
+    }
+    __syncthreads();
+    // each wave ranks SR_ELEMS / OS_NW candidates
+    constexpr int PW = (int)(SR_ELEMS / OS_NW);
+    uint32_t rank[PW], me[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      me[q] = e0 + (uint32_t)wv * PW + (uint32_t)q;
+      const uint32_t e = me[q] < n ? me[q] : 0u;
+      const uint32_t ke = s_key[e];
+      uint32_t c = 0;
+      for (uint32_t j = (uint32_t)lane; j < n; j += 64) {
+        const uint32_t kj = s_key[j];
+        c += (kj < ke || (kj == ke && j < e)) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      rank[q] = c;
+    }
+    if (lane < PW) {  // lane q gathers and writes candidate q of the wave
+      uint32_t r = 0, e = 0;
+#pragma unroll
+      for (int q = 0; q < PW; ++q)
+        if (lane == q) { r = rank[q]; e = me[q]; }
+      if (e < n && r < m) {
+        const uint32_t s = slot_of(e);
+        go.out[r] = EdgeOut{cu[s], cw[s], cs[s]};
+      }
+    }
   }
-  __syncthreads();  // ctr[C_C] and the flags are final
-  if (t < NCTR) {
-    if (t == C_OUT_N) ctr[C_OUT_N] = m;
-    if (go.sticky && t == C_FLAGS) *go.sticky |= ctr[C_FLAGS];
-    if (go.hctr) {
-      go.hctr[t] = t == C_OUT_N ? m : ctr[t];
-      if (go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
-      if (t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
-      __threadfence_system();
+  if (blockIdx.x == 0 && t < NCTR) {  // counters: final once this call's kernels before this one are done
+    uint64_t x = ctr[t];
+    if (t == C_C) x = n;
+    if (t == C_FLAGS && !fits) x |= F_SMALL;
+    if (t == C_OUT_N) x = m;
+    if (t == C_C || t == C_FLAGS || t == C_OUT_N) ctr[t] = x;
+    if (go.sticky && t == C_FLAGS) *go.sticky |= x;
+    {
+      if (go.hctr) {
+        go.hctr[t] = x;
+        if (go.ts && t < TS_END) go.hctr[NCTR + t] = go.ts[t];
+        if (t == 0) go.hctr[NCTR + TS_END] = __builtin_amdgcn_s_memrealtime();
+        __threadfence_system();
+      }
     }
   }
 }

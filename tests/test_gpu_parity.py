@@ -810,8 +810,8 @@ def test_gpu_survivor_scan_after_other_survivor_set(gpu, oracle):
 
 @pytest.mark.parametrize("n,avg,H", [(30000, 6, 2), (30000, 6, 3), (100000, 8, 4), (150000, 6, 6)])
 def test_gpu_small_order_equals_counted_passes(gpu, oracle, n, avg, H):
-    """k_sp_order_small (one workgroup orders all candidates of a small fused
-    call) against the counted passes (NLP_SMALL_ORDER=0) and the oracle, below
+    """k_sp_order_rank (one launch ranks all candidates of a small fused call)
+    against the counted passes (NLP_SMALL_ORDER=0) and the oracle, below
     and above its SO_MAX = 16384 candidates; NLP_SMALL_ORDER=2 forces it
     whatever the estimate, so calls beyond SO_MAX take the F_SMALL redo."""
     off, keys = random_csr(n, avg, 21 + H)
@@ -837,3 +837,41 @@ def test_gpu_small_order_equals_counted_passes(gpu, oracle, n, avg, H):
                 u, w, s, c = res[(env, m, k)]
                 assert_canonical_equal(eu, ew, es, u, w, s)
                 assert c == info["candidates"]
+
+
+def test_gpu_generic_score_lambdas(gpu, golden, oracle, tmp_path):
+    """The generic predictLinksWithIntersectionBasicOmp / ...Omp<CUSTOMVALUE =
+    false> with user score lambdas (tests/cpp/generic_main.cxx): the
+    reference's own Jaccard lambda (predict.hxx:557-559) through the generic
+    entry equals the built-in metric bit for bit, and a count-based lambda
+    equals its host recomputation from the oracle's intersection counts, in
+    the canonical order."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "generic_main")
+    lib = os.path.join(root, "neighborhood-link-prediction-openmp_amd")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "generic_main.cxx"), "-L", lib, "-lnlp", "-Wl,-rpath," + lib,
+                    "-o", exe], check=True)
+    g = golden["g3k"]
+    k = int(g["k"][0])
+    csr = str(tmp_path / "g.csr")
+    oracle.write_csr(csr, g["offsets"], g["keys"])
+    for H in (0, 4, 8):
+        pre = str(tmp_path / ("o%d" % H))
+        subprocess.run([exe, csr, str(H), str(k), pre], check=True, timeout=300)
+        a = oracle.read_edges(pre + ".jac_generic")
+        b = oracle.read_edges(pre + ".jac_builtin")
+        assert all(np.array_equal(x.view(np.uint32), y.view(np.uint32)) for x, y in zip(a, b))
+        eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], 1, H, max_edges=k)
+        assert_canonical_equal(eu, ew, es, *a)
+        # the custom lambda from the oracle's counts (CN with minScore -1: every touched w, count 0 included)
+        cu_, cw_, cn_, _ = oracle.predict(g["offsets"], g["keys"], 0, H, max_edges=None, min_score=-1.0)
+        sc = cn_.astype(np.float32) * np.float32(0.5) + np.float32(1.0) / (cu_ % 7 + 1).astype(np.float32)
+        keep = sc > 0
+        from parity import keys_of
+        kk = keys_of(sc[keep]).astype(np.int64)
+        order = np.lexsort((cw_[keep], cu_[keep], -kk))[:k]
+        u, w, s = oracle.read_edges(pre + ".custom")
+        assert np.array_equal(u, cu_[keep][order]) and np.array_equal(w, cw_[keep][order])
+        assert np.array_equal(s.view(np.uint32), sc[keep][order].view(np.uint32))

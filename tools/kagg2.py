@@ -6,7 +6,7 @@ import glob
 import os
 import sys
 
-GRAPH = ("k_degrees", "k_check_keys", "k_count_cols", "k_transpose_keys", "k_etab_build", "k_edge_filter",
+GRAPH = ("k_in_", "k_del_", "k_degrees", "k_check_keys", "k_count_cols", "k_transpose_keys", "k_etab_build", "k_edge_filter",
          "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_diff_", "k_low32", "k_sum_deg2")
 path = sys.argv[1]
 if os.path.isdir(path):
