@@ -166,7 +166,8 @@ struct nlp_graph {
   bool sort_lsd = false;                       // NLP_GROUPING=lsd: full LSD record sort (no MSD buckets)
   // degree-class index (sortpath.hpp): vertices of degree 1..DCAP grouped by degree
   uint32_t* vbydeg = nullptr;
-  uint64_t* sv_pack = nullptr;  // symmetric graphs: (deg v << 48 | off v) per vbydeg entry (k_sv_pack)
+  uint64_t* sv_pack = nullptr;     // (deg v << 48 | off v) per vbydeg entry (k_sv_pack)
+  uint64_t* sv_pack_in = nullptr;  // asymmetric graphs: (|I(v)| << 48 | toff v) per vbydeg entry
   std::vector<uint64_t> dstart;                // class d occupies [dstart[d], dstart[d + 1]) (class 1 at 0)
   bool use_dindex = true;                      // NLP_NO_DINDEX=1: always scan deg[] for survivors
   // the same index restricted to a source range (k_range_index; multi-GPU shards)
@@ -246,6 +247,8 @@ struct nlp_graph {
   uint64_t hp_emit = 0;
   int hp_minbin = 0, hp_one_bucket = 0;
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
+  bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
+  bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
   uint64_t hp_scap_force = 0;
@@ -358,6 +361,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->deg) (void)hipFree(g->deg);
   if (g->vbydeg) (void)hipFree(g->vbydeg);
   if (g->sv_pack) (void)hipFree(g->sv_pack);
+  if (g->sv_pack_in) (void)hipFree(g->sv_pack_in);
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   if (g->efilt) (void)hipFree(g->efilt);
@@ -494,11 +498,29 @@ nlp_status finish_graph(nlp_graph* g) {
     hipLaunchKernelGGL(k_deg_class_scatter, dim3(grid_for(S)), dim3(NT), 0, st, (const uint32_t*)g->deg, S, cur,
                        g->vbydeg);
     TRY(hipGetLastError());
-    if (g->symmetric && nv > 0 && g->nnz < (1ull << SV_PACK_SHIFT)) {
+    if (const char* sp = getenv("NLP_SV_PACK")) g->sv_pack_on = sp[0] != '0';
+    if (nv > 0 && g->nnz < (1ull << SV_PACK_SHIFT) && g->sv_pack_on) {
       TRY(hipMalloc(&g->sv_pack, nv * 8));
+      uint32_t* flag = nullptr;
+      if (!g->symmetric) {
+        TRY(hipMalloc(&g->sv_pack_in, nv * 8));
+        TRY(wsget(g->ws, B_HP_SMALL, 8, &flag));
+        TRY(hipMemsetAsync(flag, 0, 4, st));
+      }
       hipLaunchKernelGGL(k_sv_pack, dim3(grid_for(nv)), dim3(NT), 0, st, (const uint32_t*)g->vbydeg, nv,
-                         (const uint64_t*)g->off, (const uint32_t*)g->deg, g->sv_pack);
+                         (const uint64_t*)g->off, (const uint32_t*)g->deg, g->sv_pack, (const uint64_t*)g->toff,
+                         g->sv_pack_in, flag);
       TRY(hipGetLastError());
+      if (flag) {
+        uint32_t hf = 0;
+        TRY(hipMemcpyAsync(&hf, flag, 4, hipMemcpyDeviceToHost, st));
+        TRY(hipStreamSynchronize(st));
+        if (hf) {  // an in-degree beyond the pack's 16 bits: the unpacked loads
+          (void)hipFree(g->sv_pack);
+          (void)hipFree(g->sv_pack_in);
+          g->sv_pack = g->sv_pack_in = nullptr;
+        }
+      }
     }
     TRY(hipStreamSynchronize(st));
   }
@@ -627,6 +649,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
   if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
+  if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
@@ -1473,6 +1496,31 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     LAUNCH(k_hp_scatter, nU, st, flags + (uint64_t)b * nU, pos, nU, ua, lists[b]);
     TRY(hipGetLastError());
   }
+  if (g->hp_stats) {  // diagnostic: rows and wedge bounds per bin, W(u) by power of two
+    std::vector<uint64_t> hw(nU);
+    std::vector<uint8_t> hf((size_t)HP_NBINS * nU);
+    TRY(hipMemcpyAsync(hw.data(), wu, nU * 8, hipMemcpyDeviceToHost, st));
+    TRY(hipMemcpyAsync(hf.data(), flags, (uint64_t)HP_NBINS * nU, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    uint64_t rows[HP_NBINS] = {}, wsum[HP_NBINS] = {}, lr[40] = {}, lw[40] = {};
+    for (uint64_t i = 0; i < nU; ++i)
+      for (int b = 0; b < HP_NBINS; ++b)
+        if (hf[(size_t)b * nU + i]) {
+          ++rows[b];
+          wsum[b] += hw[i];
+          int l = 0;
+          while ((1ull << l) < hw[i] && l < 39) ++l;
+          ++lr[l];
+          lw[l] += hw[i];
+        }
+    for (int b = 0; b < HP_NBINS; ++b)
+      fprintf(stderr, "[hash-stats] bin %d: rows %llu, W %llu\n", b, (unsigned long long)rows[b],
+              (unsigned long long)wsum[b]);
+    for (int l = 0; l < 40; ++l)
+      if (lr[l])
+        fprintf(stderr, "[hash-stats] W <= 2^%d: rows %llu, W %llu\n", l, (unsigned long long)lr[l],
+                (unsigned long long)lw[l]);
+  }
   // row prefix of W(u) (wu[nU] = total)
   TRY(scan_excl_u64<uint64_t>(wu, nU, pos, small + 16, scan, st));
   TRY(hipMemcpyAsync(pos + nU, small + 16, 8, hipMemcpyDeviceToDevice, st));
@@ -1576,6 +1624,11 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
+    if (g->hp_stats)
+      fprintf(stderr, "[hash-stats] chunk rows [%llu, %llu) bins %llu %llu %llu %llu W %llu emitted %llu cand %llu tau %lld\n",
+              (unsigned long long)r0, (unsigned long long)r1, (unsigned long long)n0, (unsigned long long)n1,
+              (unsigned long long)(q1[2] - q0[2]), (unsigned long long)(q1[3] - q0[3]), (unsigned long long)wchunk,
+              (unsigned long long)emitted, (unsigned long long)g->host_small[HPC_CAND], (long long)tau);
     if (g->host_small[HPC_ERR]) return NLP_ERR_DEVICE;
     if (emitted > a.cap) {
       // overflow: nothing of this chunk is kept; prune what is held and retry a smaller chunk
@@ -2067,7 +2120,8 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                      dim3(NT), 0, st, gv, ua, ub, f.wbits, f.survivors, f.dshift, f.dbits, f.caplog, f.bkt,     \
                      (uint32_t*)(f.arena + f.d_bcur), ctr, f.arena + f.d_wsum, ts,                             \
                      (const uint64_t*)(f.survivors == g->vbydeg ? g->sv_pack : nullptr),                         \
-                     hot == s ? g->d_stamp : nullptr)
+                     hot == s ? g->d_stamp : nullptr,                                                           \
+                     (const uint64_t*)(f.survivors == g->vbydeg ? g->sv_pack_in : nullptr))
         if (spt >= 4) NLP_EXBUCKET(4);
         else if (spt == 2) NLP_EXBUCKET(2);
         else NLP_EXBUCKET(1);

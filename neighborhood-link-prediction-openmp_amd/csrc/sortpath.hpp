@@ -446,30 +446,46 @@ __device__ __forceinline__ uint64_t ex_count(const GraphView& g, const ExSurv& x
   return c;
 }
 
-// Symmetric graphs: the degree-class index's (deg v << 48 | off v) words
-// (k_sv_pack, built once per graph) give a survivor's row in the same round
-// trip as its id, and I(v) = N(v).
+// The degree-class index's (deg v << 48 | off v) words (k_sv_pack, built once
+// per graph) give a survivor's row in the same round trip as its id.
+// Symmetric graphs: I(v) = N(v).  Asymmetric graphs (the reference's ingest
+// keeps duplicate entries, and a deletion removes one occurrence per row): a
+// second word (|I(v)| << 48 | toff v) per entry, unless some in-degree reaches
+// 2^16 (flag[0] set; the host then drops both packs).
 constexpr int SV_PACK_SHIFT = 48;
 __global__ void k_sv_pack(const uint32_t* __restrict__ vbydeg, uint64_t n, const uint64_t* __restrict__ off,
-                          const uint32_t* __restrict__ deg, uint64_t* __restrict__ pack) {
+                          const uint32_t* __restrict__ deg, uint64_t* __restrict__ pack,
+                          const uint64_t* __restrict__ toff = nullptr, uint64_t* __restrict__ pack_in = nullptr,
+                          uint32_t* __restrict__ flag = nullptr) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t v = vbydeg[i];
     pack[i] = ((uint64_t)deg[v] << SV_PACK_SHIFT) | off[v];
+    if (pack_in) {
+      const uint64_t a = toff[v], nin = toff[v + 1] - a;
+      if (nin >= (1ull << (64 - SV_PACK_SHIFT))) flag[0] = 1u;
+      pack_in[i] = (nin << SV_PACK_SHIFT) | a;
+    }
   }
 }
 
-__device__ __forceinline__ void ex_load_packed(const GraphView& g, uint32_t v, uint64_t pk, ExSurv& x) {
+__device__ __forceinline__ void ex_load_packed(const GraphView& g, uint32_t v, uint64_t pk, ExSurv& x,
+                                               const uint64_t* pk_in = nullptr) {
   x.v = v;
   x.d = (uint32_t)(pk >> SV_PACK_SHIFT);
-  x.a = pk & ((1ull << SV_PACK_SHIFT) - 1);
-  x.nin = x.d;
-  x.nv = g.keys + x.a;
-  x.reg = x.d <= EX_REG;
+  x.nv = g.keys + (pk & ((1ull << SV_PACK_SHIFT) - 1));
+  if (pk_in) {
+    x.nin = (uint32_t)(*pk_in >> SV_PACK_SHIFT);
+    x.a = *pk_in & ((1ull << SV_PACK_SHIFT) - 1);
+  } else {
+    x.nin = x.d;
+    x.a = pk & ((1ull << SV_PACK_SHIFT) - 1);
+  }
+  x.reg = x.d <= EX_REG && x.nin <= EX_REG;
   if (x.reg) {
 #pragma unroll
     for (int q = 0; q < EX_REG; ++q) {
       x.N[q] = q < (int)x.d ? x.nv[q] : 0u;
-      x.I[q] = x.N[q];
+      x.I[q] = pk_in ? (q < (int)x.nin ? g.tkeys[x.a + q] : 0u) : x.N[q];
     }
   }
 }
@@ -1532,20 +1548,25 @@ __global__ __launch_bounds__(OS_NT) void k_sp_cpass(const uint32_t* __restrict__
 // When the candidates of a fused call fit SO_MAX keys (the LHub-4 calls of the
 // large configs: C4 predicts ~1e4 links), the four counted passes -- four
 // launches, each waiting for the previous one's keys to land -- are replaced
-// by ONE launch that ranks every candidate directly: workgroup b owns the
-// SR_ELEMS candidates at positions [b SR_ELEMS, (b + 1) SR_ELEMS) of the
-// concatenated buckets ((u, w) order), loads ALL n order keys into LDS, and
-// each wave counts, for its candidates, the keys that precede them:
-//   rank(e) = #{j : key_j < key_e} + #{j < e : key_j == key_e},
-// i.e. the position in the stable sort by ~score_key -- score descending, then
-// (u, w) ascending, the canonical order.  n^2 / 64 LDS reads per wave, spread
-// over up to SO_MAX / SR_ELEMS workgroups; then each ranked candidate below k
-// is gathered from the candidate columns to the caller's edges.  More than
-// SO_MAX candidates raise F_SMALL and the host redoes the call with the
-// counted passes.  Workgroup 0 publishes the counters like the last counted pass.
-constexpr uint32_t SO_MAX = 16384;   // candidates at most (64 KiB of keys in LDS per workgroup)
-constexpr uint32_t SR_ELEMS = 64;    // candidates ranked per workgroup (4 per wave)
-constexpr uint32_t SR_GRID = SO_MAX / SR_ELEMS;
+// by ONE launch that ranks every candidate directly.  Every workgroup loads
+// all n order keys (thread t: positions i OS_NT + t of the concatenated
+// buckets, (u, w) order) and groups them in LDS by bin = (key - kmin) >> sh,
+// with sh the smallest shift that leaves 2^14 bins over the call's key range;
+// the rest of the key and the position fit one 32-bit composite
+// ((key - kmin) mod 2^sh) << 14 | position, unique within a bin.  The rank of
+// candidate e in the stable sort by key (score descending, then (u, w)
+// ascending -- the canonical order) is then
+//   rank(e) = start(bin(e)) + #{j in bin(e) : composite_j < composite_e},
+// one comparison per member of its own bin instead of per candidate (the
+// n^2 / 64 comparisons of counting against every key were the whole cost).
+// Workgroup g ranks the positions [g Q, (g + 1) Q), Q = ceil(n / gridDim), on
+// the threads that loaded them (key, bin and slot already in registers) and
+// gathers each one below k to the caller's edges.  More than SO_MAX
+// candidates raise F_SMALL and the host redoes the call with the counted
+// passes.  Workgroup 0 publishes the counters like the last counted pass.
+constexpr uint32_t SO_MAX = 16384;  // candidates at most (positions: 14 bits)
+constexpr int SR_BITS = 14;         // bins over the key range
+constexpr uint32_t SR_GRID = 256;   // one workgroup per CU (LDS: ~144 KiB)
 
 __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restrict__ okey,
                                                          const uint32_t* __restrict__ cu,
@@ -1554,12 +1575,18 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
                                                          const uint32_t* __restrict__ kcnt, uint32_t nb, int caplog,
                                                          GatherOut go, uint64_t* __restrict__ end_mark) {
   constexpr uint32_t PER = (DX_MAXB + OS_NT - 1) / OS_NT;
-  constexpr int LD = (int)(SO_MAX / OS_NT);  // key loads per thread in flight
-  __shared__ uint32_t s_key[SO_MAX];
+  constexpr int LD = (int)(SO_MAX / OS_NT);  // positions per thread
+  constexpr uint32_t NBIN = 1u << SR_BITS;
+  constexpr int BPT = (int)(NBIN / OS_NT);   // bins per thread in the scan
+  static_assert(SO_MAX <= (1u << SR_BITS) && BPT % 4 == 0, "order_rank layout");
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[NBIN];  // counts, then starts, then ends
+  __shared__ __attribute__((aligned(16))) uint32_t s_list[SO_MAX + 16];  // the composites, grouped by bin
   __shared__ uint32_t s_pre[DX_MAXB + 1];
   __shared__ uint32_t s_w[OS_NW];
-  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  __shared__ uint32_t s_mm[2];
+  const int t = threadIdx.x;
   ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel)
+  if (t == 0) { s_mm[0] = 0xffffffffu; s_mm[1] = 0u; }
   {  // bucket prefix: thread t sums buckets [PER t, PER t + PER)
     uint32_t v[PER], sum = 0;
 #pragma unroll
@@ -1582,57 +1609,107 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
   const uint32_t n = s_pre[nb];
   uint64_t* ctr = go.ctr;
   const bool fits = n <= SO_MAX;
-  auto slot_of = [&](uint32_t j) {  // the bucket slot of position j: s_pre[lo] <= j < s_pre[lo + 1]
-    uint32_t lo = 0, hi = nb;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_pre[mid] <= j) lo = mid; else hi = mid;
-    }
-    return (lo << caplog) + (j - s_pre[lo]);
-  };
-  const uint32_t e0 = blockIdx.x * SR_ELEMS;
   const uint64_t m = fits ? (n < go.k ? (uint64_t)n : go.k) : 0ull;
-  if (fits && e0 < n) {
-    {  // every key, in position order (LD loads per thread in flight)
-      uint32_t sl[LD], kk[LD];
+  const uint32_t Q = (n + gridDim.x - 1) / gridDim.x;
+  const uint32_t q0 = blockIdx.x * Q;
+  if (fits && q0 < n) {
+    uint32_t sl[LD], kk[LD];
 #pragma unroll
-      for (int i = 0; i < LD; ++i) {
-        const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
-        sl[i] = j < n ? slot_of(j) : 0u;
+    for (int i = 0; i < LD; ++i) {  // the bucket slot of each position (LDS searches, independent chains)
+      const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+      uint32_t lo = 0, hi = nb;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_pre[mid] <= j) lo = mid; else hi = mid;
+      }
+      sl[i] = j < n ? (lo << caplog) + (j - s_pre[lo]) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < LD; ++i) kk[i] = okey[sl[i]];  // slot 0 always exists
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int i = 0; i < LD; ++i)
+      if ((uint32_t)i * OS_NT + (uint32_t)t < n) {
+        kmin = min(kmin, kk[i]);
+        kmax = max(kmax, kk[i]);
       }
 #pragma unroll
-      for (int i = 0; i < LD; ++i) kk[i] = okey[sl[i]];  // slot 0 always exists
+    for (int o = 32; o > 0; o >>= 1) {
+      kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+      kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    }
+    if (lane_id() == 0) {
+      atomicMin(&s_mm[0], kmin);
+      atomicMax(&s_mm[1], kmax);
+    }
+    for (uint32_t i = t; i < NBIN; i += OS_NT) s_bin[i] = 0u;
+    __syncthreads();
+    kmin = s_mm[0];
+    const uint32_t span = s_mm[1] - kmin;
+    const int lb = span ? 32 - __clz(span) : 0;
+    const int sh = lb > SR_BITS ? lb - SR_BITS : 0;
+    uint32_t bn[LD];
 #pragma unroll
-      for (int i = 0; i < LD; ++i) {
-        const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
-        if (j < n) s_key[j] = kk[i];
+    for (int i = 0; i < LD; ++i) {
+      bn[i] = (kk[i] - kmin) >> sh;
+      if ((uint32_t)i * OS_NT + (uint32_t)t < n) atomicAdd(&s_bin[bn[i]], 1u);
+    }
+    __syncthreads();
+    {  // exclusive starts: thread t owns bins [BPT t, BPT t + BPT)
+      uint32_t c[BPT], sum = 0;
+      const uint4* p = reinterpret_cast<const uint4*>(s_bin + (uint32_t)t * BPT);
+#pragma unroll
+      for (int i = 0; i < BPT / 4; ++i) {
+        const uint4 x = p[i];
+        c[4 * i] = x.x; c[4 * i + 1] = x.y; c[4 * i + 2] = x.z; c[4 * i + 3] = x.w;
+      }
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) sum += c[i];
+      uint64_t tot;
+      uint32_t run = os_block_scan(sum, s_w, &tot);  // syncs (every read above is done)
+      uint4* w = reinterpret_cast<uint4*>(s_bin + (uint32_t)t * BPT);
+#pragma unroll
+      for (int i = 0; i < BPT / 4; ++i) {
+        uint4 x;
+        x.x = run; run += c[4 * i];
+        x.y = run; run += c[4 * i + 1];
+        x.z = run; run += c[4 * i + 2];
+        x.w = run; run += c[4 * i + 3];
+        w[i] = x;
       }
     }
     __syncthreads();
-    // each wave ranks SR_ELEMS / OS_NW candidates
-    constexpr int PW = (int)(SR_ELEMS / OS_NW);
-    uint32_t rank[PW], me[PW];
+    const uint32_t lowmask = sh ? (1u << sh) - 1u : 0u;
+    uint32_t cp[LD];
 #pragma unroll
-    for (int q = 0; q < PW; ++q) {
-      me[q] = e0 + (uint32_t)wv * PW + (uint32_t)q;
-      const uint32_t e = me[q] < n ? me[q] : 0u;
-      const uint32_t ke = s_key[e];
-      uint32_t c = 0;
-      for (uint32_t j = (uint32_t)lane; j < n; j += 64) {
-        const uint32_t kj = s_key[j];
-        c += (kj < ke || (kj == ke && j < e)) ? 1u : 0u;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-      rank[q] = c;
+    for (int i = 0; i < LD; ++i) {  // group: s_bin[b] advances from the start of bin b to its end
+      const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+      cp[i] = (((kk[i] - kmin) & lowmask) << SR_BITS) | j;
+      if (j < n) s_list[atomicAdd(&s_bin[bn[i]], 1u)] = cp[i];
     }
-    if (lane < PW) {  // lane q gathers and writes candidate q of the wave
-      uint32_t r = 0, e = 0;
+    __syncthreads();
 #pragma unroll
-      for (int q = 0; q < PW; ++q)
-        if (lane == q) { r = rank[q]; e = me[q]; }
-      if (e < n && r < m) {
-        const uint32_t s = slot_of(e);
+    for (int i = 0; i < LD; ++i) {  // this workgroup's positions: rank within the bin, gather
+      const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+      if (j < q0 || j >= q0 + Q || j >= n) continue;
+      const uint32_t b = bn[i];
+      const uint32_t bs = b ? s_bin[b - 1] : 0u, be = s_bin[b];
+      uint32_t r = bs;
+      for (uint32_t x = bs & ~3u; x < be; x += 16) {  // 16 members per round of LDS reads (4 x 16 B)
+        uint4 q[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) q[h] = *reinterpret_cast<const uint4*>(s_list + x + 4 * h);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t y = x + 4 * h;
+          r += (y >= bs && y < be && q[h].x < cp[i]) ? 1u : 0u;
+          r += (y + 1 >= bs && y + 1 < be && q[h].y < cp[i]) ? 1u : 0u;
+          r += (y + 2 >= bs && y + 2 < be && q[h].z < cp[i]) ? 1u : 0u;
+          r += (y + 3 >= bs && y + 3 < be && q[h].w < cp[i]) ? 1u : 0u;
+        }
+      }
+      if (r < m) {
+        const uint32_t s = sl[i];
         go.out[r] = EdgeOut{cu[s], cw[s], cs[s]};
       }
     }
@@ -2222,7 +2299,8 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
                                                     uint32_t* __restrict__ bcnt, uint64_t* __restrict__ ctr,
                                                     uint64_t* __restrict__ wsum, uint64_t* __restrict__ ts,
                                                     const uint64_t* __restrict__ pack,
-                                                    uint64_t* __restrict__ stamp = nullptr) {
+                                                    uint64_t* __restrict__ stamp = nullptr,
+                                                    const uint64_t* __restrict__ pack_in = nullptr) {
   ts_enter(ts, TS_FIRST);
   sp_stamp(stamp, true, 0);
   __shared__ uint32_t s_h[DX_MAXB];
@@ -2238,7 +2316,7 @@ __global__ __launch_bounds__(NT) void k_sp_exbucket(GraphView g, uint64_t ua, ui
   for (int p = 0; p < SPT; ++p) {
     const uint64_t i = ((uint64_t)blockIdx.x * SPT + p) * NT + t;
     if (i >= n) ex_empty(g, x[p]);
-    else if (pack) ex_load_packed(g, surv[i], pack[i], x[p]);
+    else if (pack) ex_load_packed(g, surv[i], pack[i], x[p], pack_in ? pack_in + i : nullptr);
     else ex_load(g, surv[i], x[p]);
   }
   uint64_t c = 0;

@@ -704,7 +704,7 @@ def test_gpu_exclusion_without_edge_table(gpu, oracle):
                                  dict(NLP_MSD_PASSES="2"), dict(NLP_FUSE_RUNS="0"), dict(NLP_DX_BITS="1"),
                                  dict(NLP_DX_BITS="2"), dict(NLP_DX_BITS="3"), dict(NLP_DX_BITS="12"),
                                  dict(NLP_ORD11="1"), dict(NLP_GR_NT="512"), dict(NLP_COUNTED="0"),
-                                 dict(NLP_EDGE_FILTER="2")])
+                                 dict(NLP_EDGE_FILTER="2"), dict(NLP_SV_PACK="0")])
 def test_gpu_sort_path_variants_equal(gpu, oracle, env):
     """Sort-path build variants (fused output gather, several survivors per
     expansion thread, two MSD passes + group sort, separate grouping and
