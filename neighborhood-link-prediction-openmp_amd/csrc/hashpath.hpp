@@ -503,15 +503,32 @@ __global__ __launch_bounds__(NT) void k_hp_surv_lists(GraphView g, const uint32_
     const uint32_t v = surv[i];
     const unsigned long long d = g.deg[v];
     const uint64_t a = g.toff[v], b = g.toff[v + 1];
-    for (uint64_t e = a; e < b; ++e) {
-      const uint64_t u = g.tkeys[e];
-      if (u < ua || u >= ub) continue;
+    for (uint64_t e0 = a; e0 < b; e0 += 8) {  // 8 in-edges in flight: keys, then the atomics, then the stores
+      uint64_t u[8];
+      bool in[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        u[q] = e0 + q < b ? g.tkeys[e0 + q] : 0ull;
+        in[q] = e0 + q < b && u[q] >= ua && u[q] < ub;
+      }
       if (FILL) {
-        const uint32_t p = atomicAdd(&cnt[u - ua], 1u);
-        skeys[soff[u - ua] + p] = v;
+        uint32_t p[8];
+        uint64_t o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          p[q] = in[q] ? atomicAdd(&cnt[u[q] - ua], 1u) : 0u;
+          o[q] = in[q] ? soff[u[q] - ua] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (in[q]) skeys[o[q] + p[q]] = v;
       } else {
-        atomicAdd(&wu[u - ua], d);
-        atomicAdd(&cnt[u - ua], 1u);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (in[q]) {
+            atomicAdd(&wu[u[q] - ua], d);
+            atomicAdd(&cnt[u[q] - ua], 1u);
+          }
       }
     }
   }
@@ -713,6 +730,242 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
     });
     wave_sync_lds();
     hp_drain<false, CUSTOM>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
+    wave_sync_lds();
+  }
+  hp_finish(sg, a, wedges);
+}
+
+// ---------------------------------------------------------------- bin 0: row batches
+// A wave per row leaves most of a small row's lanes idle and pays the row's
+// chain of dependent graph reads (row bounds -> S(u) -> deg/off of v -> N(v)
+// -> deg w -> emission) once per row.  With the survivor lists S(u) (small H)
+// the rows of a tier are instead taken in batches: consecutive rows of the
+// list while sum (W(u) + HB_ROWCOST) stays within TW / 4 (tiers 0 and 1:
+// W(u) <= TW / 4 each), so a batch has
+// at most TW / 20 < 64 rows and at most TW / 2 wedges.  One wave accumulates a
+// whole batch in one LDS table keyed (slot << wbits | w), slot = the row's
+// index in the batch, and pays the chain once per batch.  Exclusion marks
+// (slot, x) for x in N(u); the drain decodes the slot back to (u, deg u).
+// Needs S <= 2^(32 - 6) (six slot bits above w).
+constexpr uint64_t HB_ROWCOST = 5;  // budget units per row besides its wedges (bounds the rows per batch)
+
+// The rows of tiers tlo..thi: a contiguous region of the tier list.
+__device__ __forceinline__ void hb_region(const uint32_t* tcnt, int tlo, int thi, uint32_t* base, uint32_t* cnt) {
+  uint32_t b = 0, c = 0;
+  for (int r = 0; r < tlo; ++r) b += tcnt[r];
+  for (int r = tlo; r <= thi; ++r) c += tcnt[r];
+  *base = b;
+  *cnt = c;
+}
+
+// bw[i] = W(u_i) + HB_ROWCOST for the rows of tiers tlo..thi of the tier list, 0 beyond
+__global__ void k_hp_batch_w(const uint32_t* __restrict__ tl, uint64_t n0, const uint32_t* __restrict__ tcnt,
+                             int tlo, int thi, const uint64_t* __restrict__ wu, uint64_t ua, uint64_t* __restrict__ bw) {
+  uint32_t base, cnt;
+  hb_region(tcnt, tlo, thi, &base, &cnt);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0; i += (uint64_t)gridDim.x * blockDim.x)
+    bw[i] = i < cnt ? wu[tl[base + i] - ua] + HB_ROWCOST : 0ull;
+}
+
+// bstart[b] = the first row whose budget prefix reaches b * BW (batch b = rows
+// [bstart[b], bstart[b + 1])); *nbatch = the number of batches (zeroed first).
+__global__ void k_hp_batch_starts(const uint64_t* __restrict__ bpre, const uint32_t* __restrict__ tcnt, int tlo,
+                                  int thi, uint64_t bwid, uint32_t* __restrict__ bstart, uint32_t* __restrict__ nbatch) {
+  uint32_t base, cnt;
+  hb_region(tcnt, tlo, thi, &base, &cnt);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = bpre[i] / bwid;
+    const uint64_t b0 = i ? bpre[i - 1] / bwid + 1 : 0;  // batches without a row start of their own begin here
+    for (uint64_t q = b0; q <= b; ++q) bstart[q] = (uint32_t)i;
+    if (i + 1 == cnt) {
+      bstart[b + 1] = (uint32_t)cnt;
+      *nbatch = (uint32_t)(b + 1);
+    }
+  }
+}
+
+// hp_wedges with the first-hop entry's index: f(w, v, entry)
+template <typename IT, typename F>
+__device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* s_incl, const uint64_t* s_start,
+                                          const uint32_t* s_iv, const uint32_t* keys, F f) {
+  for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * HP_UN) {
+    uint32_t w[HP_UN], v[HP_UN], e[HP_UN];
+    bool ok[HP_UN];
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * 64 + t;
+      ok[q] = j < total;
+      uint32_t lo = 0, hi = 63;
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((uint64_t)s_incl[m] > j) hi = m; else lo = m + 1;
+      }
+      const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
+      v[q] = s_iv[lo];
+      e[q] = lo;
+      w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
+    }
+#pragma unroll
+    for (int q = 0; q < HP_UN; ++q)
+      if (ok[q]) f(w[q], v[q], e[q]);
+  }
+}
+
+// the batch slot of flattened item j: the first r with incl[r] > j (nr <= 64 entries)
+__device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t nr, uint32_t j) {
+  uint32_t lo = 0, hi = nr - 1;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (incl[m] > j) hi = m; else lo = m + 1;
+  }
+  return lo;
+}
+
+template <bool CUSTOM, int TW, int STG = HP_STG>
+__global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __restrict__ tl,
+                                                 const uint32_t* __restrict__ tcnt, int tlo, int thi,
+                                                 const uint32_t* __restrict__ bstart,
+                                                 const uint32_t* __restrict__ nbatch, const uint64_t* __restrict__ wu,
+                                                 uint64_t ua, int wbits) {
+  constexpr int VT = CUSTOM ? TW : 1;
+  __shared__ uint32_t s_k[NWAVE][TW];
+  __shared__ uint32_t s_c[NWAVE][TW];
+  __shared__ uint32_t s_v0[NWAVE][VT];
+  __shared__ uint32_t s_v1[NWAVE][VT];
+  __shared__ uint32_t s_incl[NWAVE][64];   // first-hop block: inclusive prefix of the lengths
+  __shared__ uint64_t s_start[NWAVE][64];
+  __shared__ uint32_t s_iv[NWAVE][64];
+  __shared__ uint32_t s_islot[NWAVE][64];
+  __shared__ uint32_t s_u[NWAVE][64];      // batch rows: u, deg u, S(u) / N(u) starts, inclusive prefixes
+  __shared__ uint32_t s_du[NWAVE][64];
+  __shared__ uint64_t s_s0[NWAVE][64];
+  __shared__ uint64_t s_o0[NWAVE][64];
+  __shared__ uint32_t s_sp[NWAVE][64];
+  __shared__ uint32_t s_np[NWAVE][64];
+  __shared__ uint32_t s_gu[NWAVE][STG], s_gw[NWAVE][STG];
+  __shared__ float s_gs[NWAVE][STG];
+  const int lane = lane_id(), wv = wave_id();
+  uint32_t base, cnt;
+  hb_region(tcnt, tlo, thi, &base, &cnt);
+  const uint32_t* rows = tl + base;
+  const uint32_t nb = *nbatch;
+  const uint32_t wmask = (1u << wbits) - 1u;
+  const HpTable tb{s_k[wv], s_c[wv], s_v0[wv], s_v1[wv]};
+  for (int i = lane; i < TW; i += 64) {
+    s_k[wv][i] = HP_EMPTY;
+    s_c[wv][i] = 0;
+    if (CUSTOM) { s_v0[wv][i] = HP_EMPTY; s_v1[wv][i] = 0; }
+  }
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  wave_sync_lds();
+  for (uint32_t b = blockIdx.x * NWAVE + wv; b < nb; b += gridDim.x * NWAVE) {
+    const uint32_t r0 = bstart[b], nr = bstart[b + 1] - r0;  // nr < 64 by the budget
+    if (nr == 0) continue;
+    uint32_t u = 0, ns = 0, du = 0;
+    uint64_t s0 = 0, o0 = 0, W = 0;
+    if ((uint32_t)lane < nr) {
+      u = rows[r0 + lane];
+      W = wu[u - ua];
+      s0 = a.soff[u - a.sua];
+      ns = (uint32_t)(a.soff[u - a.sua + 1] - s0);
+      o0 = a.g.off[u];
+      du = (uint32_t)(a.g.off[u + 1] - o0);
+    }
+    const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(du);
+    s_u[wv][lane] = u;
+    s_du[wv][lane] = du;
+    s_s0[wv][lane] = s0;
+    s_o0[wv][lane] = o0;
+    s_sp[wv][lane] = sp;
+    s_np[wv][lane] = np;
+    wave_sync_lds();
+    const uint32_t NS = __shfl(sp, (int)nr - 1, 64), NN = __shfl(np, (int)nr - 1, 64);
+    const uint64_t Wb = wave_sum(W);
+    const int lg = max(6, log2_ceil(2 * Wb));
+    const uint32_t T = 1u << lg, mask = T - 1;
+    if (T > (uint32_t)TW) {  // a batch beyond the budget (a partition bug): fail the call, never overrun LDS
+      if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+      continue;
+    }
+    const int shift = 32 - lg;
+    // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
+    for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
+      const uint32_t e = e0 + (uint32_t)lane;
+      uint32_t len = 0, v = 0, slot = 0;
+      uint64_t st = 0;
+      if (e < NS) {
+        slot = hb_slot(s_sp[wv], nr, e);
+        const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
+        v = a.skeys[s_s0[wv][slot] + (e - ex)];
+        const uint32_t d = a.g.deg[v];
+        if (hp_surv(d, a.H)) {
+          len = d;
+          st = a.g.off[v];
+        }
+      }
+      const uint32_t incl = (uint32_t)wave_incl_scan(len);
+      s_incl[wv][lane] = incl;
+      s_start[wv][lane] = st;
+      s_iv[wv][lane] = v;
+      s_islot[wv][lane] = slot;
+      wave_sync_lds();
+      const uint32_t total = __shfl(incl, 63, 64);
+      hb_wedges(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                [&](uint32_t w, uint32_t vv, uint32_t ent) {
+                  const uint32_t sl = s_islot[wv][ent];
+                  if (w > s_u[wv][sl]) {
+                    ++wedges;
+                    hp_insert<false, CUSTOM>(tb, mask, shift, (sl << wbits) | w, vv, &a.ctr[HPC_ERR]);
+                  }
+                });
+      wave_sync_lds();
+    }
+    // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
+    for (uint32_t x0 = 0; x0 < NN; x0 += 64 * HP_UN) {
+      uint32_t key[HP_UN], sl[HP_UN];
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
+        sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
+        const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
+        key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
+        if (x < NN && key[q] > s_u[wv][sl[q]]) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
+      }
+    }
+    wave_sync_lds();
+    // drain: every entry scored for its own row
+    for (uint32_t i0 = 0; i0 < T; i0 += 64 * HP_UN) {
+      uint32_t kq[HP_UN], c[HP_UN], v0[HP_UN], v1[HP_UN], dw[HP_UN];
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
+        c[q] = v0[q] = v1[q] = 0;
+        kq[q] = i < T ? hp_take<false, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+      }
+      if (!CUSTOM) {
+#pragma unroll
+        for (int q = 0; q < HP_UN; ++q) dw[q] = a.g.deg[kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u];
+      }
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const bool valid = kq[q] != HP_EMPTY;
+        const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
+        const uint32_t uu = s_u[wv][sl];
+        const uint64_t du2 = s_du[wv][sl];
+        float s = 0.0f;
+        if (valid) {
+          if (CUSTOM) s = hp_score<true>(a, uu, du2, w, c[q], v0[q], v1[q]);
+          else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & HP_CMASK), du2, (uint64_t)dw[q]);
+        }
+        hp_emit(sg, a, valid, s, uu, w, tau);
+      }
+    }
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -1141,6 +1394,377 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
       b0 = b1;
     }
     __syncthreads();  // the next row rewrites s_bc / s_xcur
+  }
+  hp_finish(sg, a, wedges);
+}
+
+// ---------------------------------------------------------------- bins 2-3: the hub pass
+// k_hp_part works a hub row's w-buckets one after another on one workgroup
+// (the few largest rows of a chunk then run on a handful of CUs), and a sliced
+// row makes every slice walk the whole first-hop list.  The hub pass instead
+// spreads both halves of the work over the chip:
+//   k_hh_rows     per hub row: its w-bucket width (about HH_BW of W(u) per
+//                 bucket, at most HH_PMAX buckets) and its enumeration items
+//                 (HH_EC first hops each);
+//   k_hh_maps     bucket -> row, item -> row, and every bucket's first entry of
+//                 N(u) (the exclusion slice, one binary search per bucket);
+//   k_hh_enum     one workgroup per item: its wedges counted per bucket in LDS
+//                 and added to the global bucket counts (COUNT); then, after a
+//                 scan, counted again, reserved with one atomic per used bucket
+//                 and written to the bucket's contiguous scratch (SCATTER: w,
+//                 and v for AA / RA);
+//   k_hh_accum    one workgroup per bucket (work queue): its wedges into an
+//                 LDS table, the exclusion slice of N(u) marked, every entry
+//                 scored and emitted -- buckets of different rows in parallel.
+// A bucket whose distinct-w bound exceeds the table is accumulated in w-range
+// sub-passes over its scratch.  When a chunk's hub wedges exceed the scratch
+// the host keeps k_hp_part for that chunk.
+constexpr uint64_t HH_BW = 1024;    // W(u) per w-bucket (W counts every w, so buckets hold at most about this)
+constexpr uint32_t HH_PMAX = 8192;  // buckets per row at most
+constexpr uint64_t HH_EC = 4096;    // first hops per enumeration item
+constexpr int HH_NT = 256;          // threads of the enumeration and accumulation workgroups
+constexpr int HH_NW = HH_NT / 64;
+constexpr int HH_TL = 13;           // accumulation table: 2^13 LDS entries (2^12 for AA / RA)
+
+__device__ __forceinline__ uint32_t hh_row_u(const uint32_t* l2, uint64_t n2, const uint32_t* l3, uint64_t r) {
+  return r < n2 ? l2[r] : l3[r - n2];
+}
+
+__global__ void k_hh_rows(HpArgs a, const uint32_t* __restrict__ l2, uint64_t n2, const uint32_t* __restrict__ l3,
+                          uint64_t n3, const uint64_t* __restrict__ wu, uint64_t ua, uint32_t* __restrict__ hr_u,
+                          uint32_t* __restrict__ hr_shift, uint32_t* __restrict__ hr_p, uint32_t* __restrict__ hr_items,
+                          uint64_t bw = HH_BW) {
+  const uint64_t nh = n2 + n3;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = hh_row_u(l2, n2, l3, r);
+    const uint64_t W = wu[u - ua];
+    const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
+    uint32_t P = 0, shift = 0, items = 0;
+    if (span_w > 0) {
+      uint64_t pd = (W + bw - 1) / bw;
+      if (pd < 1) pd = 1;
+      if (pd > HH_PMAX) pd = HH_PMAX;
+      shift = (uint32_t)log2_ceil((span_w + pd - 1) / pd);
+      P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
+      uint64_t nf;
+      if (a.soff) nf = a.soff[u - a.sua + 1] - a.soff[u - a.sua];
+      else nf = a.g.off[u + 1] - a.g.off[u];
+      items = (uint32_t)((nf + HH_EC - 1) / HH_EC);
+      if (items == 0) P = 0;  // no first hop: no wedge, no candidate
+    }
+    hr_u[r] = u;
+    hr_shift[r] = shift;
+    hr_p[r] = P;
+    hr_items[r] = items;
+  }
+}
+
+// brow[bucket] = row, irow[item] = row, xs[bucket] = the first entry of N(u)
+// at or above the bucket's w-range start (absolute index into keys)
+__global__ void k_hh_maps(HpArgs a, uint64_t nh, const uint32_t* __restrict__ hr_u,
+                          const uint32_t* __restrict__ hr_shift, const uint32_t* __restrict__ hr_p,
+                          const uint64_t* __restrict__ bbase, const uint32_t* __restrict__ hr_items,
+                          const uint64_t* __restrict__ ibase, uint32_t* __restrict__ brow, uint32_t* __restrict__ irow) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b0 = bbase[r], i0 = ibase[r];
+    for (uint32_t b = 0; b < hr_p[r]; ++b) brow[b0 + b] = (uint32_t)r;
+    for (uint32_t i = 0; i < hr_items[r]; ++i) irow[i0 + i] = (uint32_t)r;
+  }
+}
+
+__global__ void k_hh_xstart(HpArgs a, uint64_t nb, const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
+                            const uint32_t* __restrict__ hr_shift, const uint64_t* __restrict__ bbase,
+                            uint64_t* __restrict__ xs) {
+  for (uint64_t gb = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gb < nb; gb += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = brow[gb];
+    const uint32_t u = hr_u[r];
+    const uint64_t b = gb - bbase[r];
+    const uint64_t x0 = (uint64_t)u + 1 + (b << hr_shift[r]);
+    const uint64_t o0 = a.g.off[u];
+    uint32_t n = (uint32_t)(a.g.off[u + 1] - o0);
+    xs[gb] = o0 + (x0 > 0xffffffffull ? n : upper_bound_u32(a.g.keys + o0, n, (uint32_t)(x0 - 1)));
+  }
+}
+
+// The wedges (w > u) of item `item`'s first hops: f(w, v) on every thread of the workgroup.
+template <typename F>
+__device__ __forceinline__ void hh_enum_item(const HpArgs& a, uint32_t u, uint64_t f0, uint64_t f1, uint64_t* s_incl,
+                                             uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f) {
+  const int t = threadIdx.x;
+  const uint32_t* fh;
+  uint64_t nf;
+  hp_first_hops(a, u, a.g.off[u], a.g.off[u + 1] - a.g.off[u], &fh, &nf);
+  if (f1 > nf) f1 = nf;
+  for (uint64_t base = f0; base < f1; base += HH_NT) {
+    const uint64_t i = base + t;
+    uint32_t v = 0;
+    uint64_t len = 0, st = 0;
+    if (i < f1) {
+      v = fh[i];
+      const uint32_t d = a.g.deg[v];
+      if (hp_surv(d, a.H)) {
+        len = d;
+        st = a.g.off[v];
+      }
+    }
+    const uint64_t incl = block_incl_scan_1024(len, s_w);
+    s_incl[t] = incl;
+    s_start[t] = st;
+    s_iv[t] = v;
+    if (t == HH_NT - 1) *s_tot = incl;
+    __syncthreads();
+    const uint64_t total = *s_tot;
+    hp_wedges<HH_NT>(total, (uint32_t)t, (uint32_t)HH_NT, s_incl, s_start, s_iv, a.g.keys, [&](uint32_t w, uint32_t vv) {
+      if (w > u) f(w, vv);
+    });
+    __syncthreads();
+  }
+}
+
+template <bool SCATTER, bool CUSTOM>
+__global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, const uint32_t* __restrict__ irow,
+                                                   const uint32_t* __restrict__ hr_u,
+                                                   const uint32_t* __restrict__ hr_shift,
+                                                   const uint32_t* __restrict__ hr_p, const uint64_t* __restrict__ bbase,
+                                                   const uint64_t* __restrict__ ibase, uint32_t* __restrict__ bcnt,
+                                                   const uint64_t* __restrict__ boff, uint32_t* __restrict__ bcur,
+                                                   uint32_t* __restrict__ sw, uint32_t* __restrict__ sv) {
+  __shared__ uint32_t s_h[HH_PMAX];
+  __shared__ uint64_t s_incl[HH_NT], s_start[HH_NT];
+  __shared__ uint32_t s_iv[HH_NT];
+  __shared__ uint64_t s_w[HH_NW];
+  __shared__ uint64_t s_tot;
+  const int t = threadIdx.x;
+  const uint64_t item = blockIdx.x;
+  const uint32_t r = irow[item];
+  const uint32_t u = hr_u[r], shift = hr_shift[r], P = hr_p[r];
+  const uint64_t bb = bbase[r];
+  const uint64_t f0 = (item - ibase[r]) * HH_EC, f1 = f0 + HH_EC;
+  for (uint32_t b = t; b < P; b += HH_NT) s_h[b] = 0;
+  __syncthreads();
+  hh_enum_item(a, u, f0, f1, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t) {
+    atomicAdd(&s_h[(w - u - 1) >> shift], 1u);
+  });
+  if (!SCATTER) {
+    for (uint32_t b = t; b < P; b += HH_NT)
+      if (s_h[b]) atomicAdd(&bcnt[bb + b], s_h[b]);
+    return;
+  }
+  for (uint32_t b = t; b < P; b += HH_NT) {  // reserve: s_h[b] = this item's first scratch word in bucket b
+    const uint32_t h = s_h[b];
+    s_h[b] = h ? (uint32_t)boff[bb + b] + atomicAdd(&bcur[bb + b], h) : 0u;
+  }
+  __syncthreads();
+  hh_enum_item(a, u, f0, f1, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t v) {
+    const uint32_t p = atomicAdd(&s_h[(w - u - 1) >> shift], 1u);
+    sw[p] = w;
+    if (CUSTOM) sv[p] = v;
+  });
+}
+
+// Accumulation items {bucket, w-range [slo, shi), distinct bound}.  A bucket
+// whose distinct-w bound 2 min(n, width) fits the table is one item
+// (k_hh_plan).  A heavier one -- a hub row's wedges are skewed towards low
+// ids, so its first buckets can hold most of them -- is cut by k_hh_split: a
+// histogram of its scratch over HH_FINE equal w-ranges, grouped greedily into
+// consecutive ranges of at most T / 2 wedges (a single fine range beyond that
+// is bounded by its width instead).  The items of a heavy bucket run on
+// different workgroups, each streaming the bucket's scratch and keeping its
+// own w-range.
+struct HhItem {
+  uint32_t gb, cnt;   // bucket, distinct-w bound of the range
+  uint64_t slo, shi;  // w-range
+};
+constexpr uint32_t HH_FINE = 4096;
+
+__device__ __forceinline__ uint64_t hh_bucket_range(const HpArgs& a, uint32_t u, uint32_t shift, uint64_t b,
+                                                    uint64_t* lo) {
+  *lo = (uint64_t)u + 1 + (b << shift);
+  const uint64_t hi = *lo + (1ull << shift) < a.S ? *lo + (1ull << shift) : a.S;
+  return hi - *lo;
+}
+
+// append with one atomic per wave (a single counter shared by the whole chip)
+__device__ __forceinline__ uint32_t hh_wave_append(bool want, uint32_t* ctr) {
+  const uint64_t m = __ballot(want);
+  if (!m) return 0;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
+}
+
+__global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
+                          const uint32_t* __restrict__ hr_shift, const uint64_t* __restrict__ bbase,
+                          const uint32_t* __restrict__ bcnt, int tl, HhItem* __restrict__ items,
+                          uint32_t* __restrict__ nitems, uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy) {
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t gb = b0 + threadIdx.x;
+    uint32_t n = 0;
+    uint64_t lo = 0, width = 0;
+    if (gb < nb) {
+      n = bcnt[gb];
+      const uint32_t r = brow[gb];
+      width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
+    }
+    const uint64_t dist = (uint64_t)n < width ? (uint64_t)n : width;
+    const bool simple = n > 0 && 2 * dist <= (1ull << tl), hv = n > 0 && !simple;
+    const uint32_t i = hh_wave_append(simple, nitems);
+    if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};
+    const uint32_t j = hh_wave_append(hv, nheavy);
+    if (hv) heavy[j] = (uint32_t)gb;
+  }
+}
+
+__global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __restrict__ heavy,
+                                                    const uint32_t* __restrict__ nheavy,
+                                                    const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
+                                                    const uint32_t* __restrict__ hr_shift,
+                                                    const uint64_t* __restrict__ bbase, const uint32_t* __restrict__ bcnt,
+                                                    const uint64_t* __restrict__ boff, const uint32_t* __restrict__ sw,
+                                                    int tl, HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
+                                                    uint64_t cap) {
+  __shared__ uint32_t s_h[HH_FINE];
+  const int t = threadIdx.x;
+  const uint32_t nh = *nheavy;
+  const uint64_t half = 1ull << (tl - 1);
+  for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+    const uint32_t gb = heavy[hi];
+    const uint32_t n = bcnt[gb];
+    const uint64_t off = boff[gb];
+    const uint32_t r = brow[gb];
+    uint64_t lo;
+    const uint64_t width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
+    const uint64_t fw = (width + HH_FINE - 1) / HH_FINE;
+    for (uint32_t f = t; f < HH_FINE; f += HH_NT) s_h[f] = 0;
+    __syncthreads();
+    hp_stream(sw + off, n, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t w) { atomicAdd(&s_h[(w - lo) / fw], 1u); });
+    __syncthreads();
+    if (t == 0) {  // greedy grouping of consecutive fine ranges (a few thousand LDS reads)
+      auto emit = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
+        const uint64_t slo = lo + f0 * fw, shi = lo + f1 * fw < lo + width ? lo + f1 * fw : lo + width;
+        if (slo >= shi) return;
+        const uint64_t span = shi - slo;
+        const uint64_t dist = cnt < span ? cnt : span;
+        if (2 * dist <= 2 * half) {
+          const uint32_t i = atomicAdd(nitems, 1u);
+          if (i < cap) items[i] = HhItem{gb, (uint32_t)dist, slo, shi};
+          else atomicOr(&a.ctr[HPC_ERR], 4ull);
+          return;
+        }
+        for (uint64_t x = slo; x < shi; x += half) {  // one fine range beyond the table: by width
+          const uint64_t x1 = x + half < shi ? x + half : shi;
+          const uint32_t i = atomicAdd(nitems, 1u);
+          if (i < cap) items[i] = HhItem{gb, (uint32_t)(x1 - x), x, x1};
+          else atomicOr(&a.ctr[HPC_ERR], 4ull);
+        }
+      };
+      uint64_t acc = 0, g0 = 0;
+      for (uint32_t f = 0; f < HH_FINE; ++f) {
+        const uint64_t c = s_h[f];
+        if (c > half) {
+          if (acc) emit(g0, f, acc);
+          emit(f, f + 1, c);
+          acc = 0;
+          g0 = f + 1;
+        } else if (acc + c > half) {
+          emit(g0, f, acc);
+          acc = c;
+          g0 = f;
+        } else {
+          if (!acc && !c) g0 = f + 1;
+          acc += c;
+        }
+      }
+      if (acc) emit(g0, HH_FINE, acc);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool CUSTOM>
+__global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __restrict__ items,
+                                                    const uint32_t* __restrict__ nitems,
+                                                    const uint32_t* __restrict__ brow,
+                                                    const uint32_t* __restrict__ hr_u,
+                                                    const uint32_t* __restrict__ hr_shift,
+                                                    const uint32_t* __restrict__ hr_p,
+                                                    const uint64_t* __restrict__ bbase,
+                                                    const uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
+                                                    const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw,
+                                                    const uint32_t* __restrict__ sv, uint32_t* __restrict__ queue) {
+  constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
+  constexpr int LT = 1 << TL;
+  constexpr int VT = CUSTOM ? LT : 1;
+  __shared__ uint32_t s_k[LT];
+  __shared__ uint32_t s_c[LT];
+  __shared__ uint32_t s_v0[VT];
+  __shared__ uint32_t s_v1[VT];
+  __shared__ uint32_t s_gu[HH_NW][HP_BSTG], s_gw[HH_NW][HP_BSTG];
+  __shared__ float s_gs[HH_NW][HP_BSTG];
+  __shared__ uint64_t s_it;
+  const int t = threadIdx.x, wv = wave_id();
+  const HpTable tb{s_k, s_c, s_v0, s_v1};
+  for (int i = t; i < LT; i += HH_NT) {
+    s_k[i] = HP_EMPTY;
+    s_c[i] = 0;
+    if (CUSTOM) { s_v0[i] = HP_EMPTY; s_v1[i] = 0; }
+  }
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  const uint32_t ni = *nitems;
+  uint64_t wedges = 0;
+  __syncthreads();
+  for (;;) {
+    if (t == 0) s_it = atomicAdd(queue, 1u);
+    __syncthreads();
+    const uint64_t it = s_it;
+    __syncthreads();
+    if (it >= ni) break;
+    const HhItem item = items[it];
+    const uint32_t gb = item.gb;
+    const uint32_t n = bcnt[gb];
+    const uint32_t r = brow[gb];
+    const uint32_t u = hr_u[r];
+    const uint64_t b = gb - bbase[r];
+    const uint64_t off = boff[gb];
+    uint64_t lo;
+    const uint64_t width = hh_bucket_range(a, u, hr_shift[r], b, &lo);
+    const bool whole = item.slo == lo && item.shi == lo + width;
+    const uint64_t slo = item.slo, shi = item.shi;
+    const uint64_t o1 = a.g.off[u + 1];
+    const uint64_t du = o1 - a.g.off[u];
+    const uint64_t x0 = xs[gb], x1 = b + 1 < hr_p[r] ? xs[gb + 1] : o1;  // N(u) entries in the bucket
+    const int lg = max(6, log2_ceil(2 * (uint64_t)item.cnt));
+    const uint32_t T = 1u << (lg < TL ? lg : TL), mask = T - 1;
+    const int hs = 32 - (lg < TL ? lg : TL);
+    for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+      uint32_t wq[HP_UN], vq[HP_UN];
+#pragma unroll
+      for (int k = 0; k < HP_UN; ++k) {
+        const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+        const uint64_t p = off + (i < n ? i : 0u);
+        wq[k] = sw[p];
+        vq[k] = CUSTOM ? sv[p] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < HP_UN; ++k) {
+        const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+        if (i < n && (whole || ((uint64_t)wq[k] >= slo && (uint64_t)wq[k] < shi))) {
+          ++wedges;
+          hp_insert<false, CUSTOM>(tb, mask, hs, wq[k], vq[k], &a.ctr[HPC_ERR]);
+        }
+      }
+    }
+    __syncthreads();
+    // first-order exclusion: the entries of N(u) in [slo, shi)
+    hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
+      if ((uint64_t)x >= slo && (uint64_t)x < shi) hp_mark<false>(tb, mask, hs, x);
+    });
+    __syncthreads();
+    hp_drain<false, CUSTOM>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
+    __syncthreads();
   }
   hp_finish(sg, a, wedges);
 }

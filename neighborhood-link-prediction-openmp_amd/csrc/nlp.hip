@@ -73,6 +73,7 @@ enum Buf {
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
   NBUF
 };
 
@@ -195,7 +196,9 @@ struct nlp_graph {
   bool small_force = false;
   uint64_t* ord_clean = nullptr;               // the sort-path arena whose ordering descriptors are all zero
   int gr_nt = GR_NT;                           // k_sp_grouprun threads per bucket (NLP_GR_NT=512)
-  bool direct_launch = false;                  // sort path: kernels launched directly, no graph (NLP_DIRECT_LAUNCH=1)
+  bool direct_launch = false;                  // no graphs anywhere (NLP_DIRECT_LAUNCH=1)
+  bool sync_direct = true;                     // stamp-timed sort path: kernels launched one by one, also for
+                                               // synchronous calls (NLP_DIRECT_LAUNCH=0: one replayed hipGraph)
   bool async_direct = true;                    // asynchronous calls launched kernel by kernel (NLP_ASYNC_GRAPH=1: graphs)
   int exb_spt = 2;                             // k_sp_exbucket: survivors per thread (NLP_EXB_SPT 1, 2, 4)
   bool fuse_runs = true;                       // direct emission: grouping + scoring in one kernel (NLP_FUSE_RUNS=0: off)
@@ -248,6 +251,10 @@ struct nlp_graph {
   int hp_minbin = 0, hp_one_bucket = 0;
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
+  int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
+  uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
+  bool hp_hub = true;        // path 4: bins 2 / 3 by the hub pass (k_hh_*; NLP_HASH_HUB=0: k_hp_part)
+  bool hp_batch = true;      // path 4: bin-0 tiers 0 / 1 in row batches (k_hp_batch; NLP_HASH_BATCH=0: a wave per row)
   bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
@@ -613,6 +620,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
   if (const char* dl = getenv("NLP_DIRECT_LAUNCH")) {
     g->direct_launch = dl[0] == '1';
+    g->sync_direct = dl[0] != '0';
     if (g->direct_launch) g->use_graphs = false;
   }
   if (const char* ag = getenv("NLP_ASYNC_GRAPH")) {
@@ -650,6 +658,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
   if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
   if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
+  if (const char* hb = getenv("NLP_HASH_BATCH")) g->hp_batch = hb[0] != '0';
+  if (const char* hh = getenv("NLP_HASH_HUB")) g->hp_hub = hh[0] != '0';
+  if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
+  if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
@@ -1422,6 +1434,110 @@ double hp_estimate(const nlp_graph* g, const Params& p) {
   return S ? 0.5 * w * (double)(ub - ua) / (double)S : 0.0;
 }
 
+// The hub pass over a chunk's bin-2 and bin-3 rows (hashpath.hpp, k_hh_*).
+// *done = false: the chunk's hub wedges exceed the scratch (the caller runs
+// k_hp_part instead; nothing was emitted).
+nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n2, const uint32_t* l3, uint64_t n3,
+                   const uint64_t* wu, uint64_t ua, bool custom, uint64_t* scan, uint32_t* queue, bool* done,
+                   hipStream_t st) {
+  Workspace& ws = g->ws;
+  *done = false;
+  const uint64_t nh = n2 + n3;
+  uint32_t* hr;    // u, shift, P, items: 4 x nh
+  uint64_t* pre;   // bucket prefix [nh + 1], item prefix [nh + 1]
+  TRY(wsget(ws, B_HH_ROWS, 4 * nh, &hr));
+  TRY(wsget(ws, B_HH_PRE, 2 * (nh + 1), &pre));
+  uint32_t *hr_u = hr, *hr_shift = hr + nh, *hr_p = hr + 2 * nh, *hr_items = hr + 3 * nh;
+  uint64_t *bbase = pre, *ibase = pre + nh + 1;
+  LAUNCH(k_hh_rows, nh, st, a, l2, n2, l3, n3, wu, ua, hr_u, hr_shift, hr_p, hr_items, g->hh_bw);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(hr_p, nh, bbase, bbase + nh, scan, st));
+  TRY(scan_excl_u64<uint32_t>(hr_items, nh, ibase, ibase + nh, scan, st));
+  TRY(hipMemcpyAsync(&g->host_small[48], bbase + nh, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(&g->host_small[49], ibase + nh, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t NB = g->host_small[48], NI = g->host_small[49];
+  if (NB == 0 || NI == 0) {
+    *done = true;
+    return NLP_OK;
+  }
+  if (NI > 0x7fffffffull) return NLP_OK;
+  uint32_t* maps;  // brow [NB], irow [NI]
+  uint32_t* bc;    // bcnt [NB], bcur [NB]
+  uint64_t *boff, *xs;
+  TRY(wsget(ws, B_HH_MAPS, NB + NI, &maps));
+  TRY(wsget(ws, B_HH_BCNT, 2 * NB, &bc));
+  TRY(wsget(ws, B_HH_BOFF, NB + 1, &boff));
+  TRY(wsget(ws, B_HH_XS, NB, &xs));
+  uint32_t *brow = maps, *irow = maps + NB, *bcnt = bc, *bcur = bc + NB;
+  TRY(hipMemsetAsync(bc, 0, 2 * NB * 4, st));
+  LAUNCH(k_hh_maps, nh, st, a, nh, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p,
+         (const uint64_t*)bbase, (const uint32_t*)hr_items, (const uint64_t*)ibase, brow, irow);
+  LAUNCH(k_hh_xstart, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
+         (const uint64_t*)bbase, xs);
+  TRY(hipGetLastError());
+  if (custom)
+    hipLaunchKernelGGL((k_hh_enum<false, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint64_t*)ibase, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr);
+  else
+    hipLaunchKernelGGL((k_hh_enum<false, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint64_t*)ibase, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr);
+  TRY(hipGetLastError());
+  TRY(scan_excl_u64<uint32_t>(bcnt, NB, boff, boff + NB, scan, st));
+  TRY(hipMemcpyAsync(&g->host_small[50], boff + NB, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t tot = g->host_small[50];
+  TRY(hipMemsetAsync(bcur, 0, NB * 4, st));
+  const uint64_t words = (uint64_t)g->hp_gp * g->hp_scap * 2;  // u32 words of the k_hp_part scratch
+  const uint64_t capw = custom ? words / 2 : words;
+  if (tot > capw || tot > 0xffffffffull) return NLP_OK;  // k_hp_part for this chunk
+  uint32_t* sw = g->hp_scratch;
+  uint32_t* sv = custom ? g->hp_scratch + capw : nullptr;
+  if (custom)
+    hipLaunchKernelGGL((k_hh_enum<true, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint64_t*)ibase, bcnt, (const uint64_t*)boff, bcur, sw, sv);
+  else
+    hipLaunchKernelGGL((k_hh_enum<true, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint64_t*)ibase, bcnt, (const uint64_t*)boff, bcur, sw, sv);
+  TRY(hipGetLastError());
+  // accumulation items (k_hh_plan, k_hh_split): a bucket, or a w-range of a heavy bucket
+  const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
+  const uint64_t cap = NB + 3 * (tot >> (tl - 2)) + 1024;
+  HhItem* items;
+  uint32_t* heavy = bcur;  // the cursors are done with
+  uint32_t* nitems = queue + 1;  // and queue + 2: the heavy count
+  TRY(wsget(ws, B_HH_SITEM, cap * sizeof(HhItem) / 8 + 1, (uint64_t**)&items));
+  TRY(hipMemsetAsync(queue, 0, 12, st));
+  LAUNCH(k_hh_plan, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
+         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, queue + 2);
+  hipLaunchKernelGGL(k_hh_split, dim3(512), dim3(HH_NT), 0, st, a, (const uint32_t*)heavy, (const uint32_t*)(queue + 2),
+                     (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint64_t*)bbase,
+                     (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint32_t*)sw, tl, items, nitems, cap);
+  TRY(hipGetLastError());
+  const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
+  if (custom)
+    hipLaunchKernelGGL((k_hh_accum<true>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
+                       (const uint32_t*)nitems, (const uint32_t*)brow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
+                       (const uint32_t*)sv, queue);
+  else
+    hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
+                       (const uint32_t*)nitems, (const uint32_t*)brow,
+                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
+                       (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
+                       (const uint32_t*)sv, queue);
+  TRY(hipGetLastError());
+  *done = true;
+  return NLP_OK;
+}
+
 nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks, hipStream_t st) {
   Workspace& ws = g->ws;
   const uint64_t S = g->span;
@@ -1587,7 +1703,27 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
       const uint32_t* tl = tlist;
       const uint32_t* tc = tcnt;
-      if (custom) {
+      const int wbits = bits_for(S - 1);
+      if (g->hp_batch && s_skeys && wbits <= 26) {
+        // tiers 0 and 1 in row batches (hashpath.hpp:k_hp_batch), tier 2 a wave per row
+        uint64_t *bw, *bpre;
+        uint32_t* bst;
+        TRY(wsget(ws, B_HB_W, n0, &bw));
+        TRY(wsget(ws, B_HB_PRE, n0 + 1, &bpre));
+        TRY(wsget(ws, B_HB_START, (wchunk + HB_ROWCOST * n0) / 256 + 8, &bst));
+        uint32_t* nbat = tcnt + 10;
+        const uint64_t bwid = 256;  // tiers 0 and 1 (W <= 256) together, 1024-entry tables
+        LAUNCH(k_hp_batch_w, n0, st, (const uint32_t*)tl, n0, tc, 0, 1, (const uint64_t*)wu, ua, bw);
+        TRY(scan_excl_u64<uint64_t>(bw, n0, bpre, bpre + n0, scan, st));
+        TRY(hipMemsetAsync(nbat, 0, 4, st));
+        LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
+        TRY(hipGetLastError());
+        if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        TRY(hipGetLastError());
+        if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
+        else hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
+      } else if (custom) {
         hipLaunchKernelGGL((k_hp_wave<true, 256, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 0);
         hipLaunchKernelGGL((k_hp_wave<true, 512, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 1);
         hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
@@ -1610,7 +1746,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
       TRY(hipGetLastError());
     }
-    for (int b = 2; b < HP_NBINS; ++b) {  // rows beyond an LDS table: w-bucket partitioning
+    bool hub_done = false;
+    if (g->hp_hub && (q1[2] - q0[2]) + (q1[3] - q0[3]) > 0) {
+      nlp_status sh = run_hub(g, a, lists[2] + q0[2], q1[2] - q0[2], lists[3] + q0[3], q1[3] - q0[3], wu, ua, custom,
+                              scan, tcnt + 11, &hub_done, st);  // tcnt[11, 14): queue, item and heavy counts
+      if (sh != NLP_OK) return sh;
+    }
+    for (int b = 2; b < HP_NBINS && !hub_done; ++b) {  // rows beyond an LDS table: w-bucket partitioning
       const uint64_t nb = q1[b] - q0[b];
       if (!nb) continue;
       // fewer rows than workgroups: slice each row's w-buckets over several workgroups
@@ -2639,7 +2781,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     // host's ~40 us of launches hide behind the previous call's kernels, and
     // back-to-back graph launches leave ~10 us between graphs on the GPU
     // (C2: 0.101 vs 0.109 ms per call)
-    const bool async_direct = async && stamps && g->async_direct;
+    const bool async_direct = stamps && ((async && g->async_direct) || (!async && g->sync_direct));
     if (sorted && async_direct)
       replayed = false;
     else if (sorted)

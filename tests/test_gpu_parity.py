@@ -335,10 +335,17 @@ def test_gpu_cpp_dropin_header(gpu, golden, oracle, tmp_path):
 def test_gpu_graph_replay_equals_direct_launch(gpu, oracle):
     """The sync-free path is captured once per (metric, H, k, range, buffers)
     and replayed as hipGraphs; replays must equal the directly launched run and
-    the oracle, across interleaved cache entries and a capacity regrow."""
+    the oracle, across interleaved cache entries and a capacity regrow.
+    (Synchronous stamp-timed calls launch kernel by kernel by default;
+    NLP_DIRECT_LAUNCH=0 selects the single replayed graph.)"""
     off, keys = random_csr(6000, 14, 5)
     runs = [(1, 4, 400), (7, 4, 400), (1, 4, 400), (0, 8, 50), (7, 4, 400), (1, 4, 400)]
-    with gpu.Graph(off, keys) as G:
+    with gpu.Graph(off, keys) as G:  # default: direct launches
+        for m, H, k in runs[:3]:
+            u, w, s, t = G.predict(m, H, k)
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
+    with _env(NLP_DIRECT_LAUNCH="0"), gpu.Graph(off, keys) as G:
         seen = {}
         for m, H, k in runs:
             u, w, s, t = G.predict(m, H, k)
@@ -401,16 +408,22 @@ class _env:
                 os.environ[k] = v
 
 
-# path 4 (hash accumulation) with every kernel forced: 0 wave/LDS, 1 workgroup/LDS,
-# 2 w-bucket partitioning, 3 partitioning with a tiny scratch (bucket groups and
-# direct accumulation), 4 one bucket per row (sub-range passes), 5 bin 0 as one
-# 1024-entry launch (no table-size tiers), 6/7 partitioned rows sliced over
-# several workgroups (bucket slices, exclusion cursor per slice)
+# path 4 (hash accumulation) with every kernel forced: 0 default (bin-0 row
+# batches, hub pass), 1 workgroup/LDS, 2 hub pass for every row, 3 k_hp_part
+# over a tiny scratch (bucket groups and direct accumulation), 4 k_hp_part with one bucket per row (sub-range passes), 5 bin
+# 0 as one 1024-entry launch (no table-size tiers), 6/7 k_hp_part rows sliced
+# over several workgroups (bucket slices, exclusion cursor per slice), 8 the
+# edge-parallel work estimate, 9 a wave per bin-0 row, 10 k_hp_part for every row,
+# 11 hub pass with one w-bucket per row, 12 the same with 128-entry item
+# tables (heavy buckets split into w-range items by their fine histogram)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
-                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_TIERS="0"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_SLICES="7"),
-                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3"), dict(NLP_HASH_WORK_SURV="0")]
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_SLICES="7", NLP_HASH_HUB="0"),
+                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3", NLP_HASH_HUB="0"),
+                 dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
