@@ -365,23 +365,23 @@ __device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint3
 // 64): the slots of HP_UN rounds first (LDS or slab), then their degree loads
 // (count metrics) in flight together, then the scores; every thread of the
 // caller runs every round (hp_emit ballots per wave).
-template <bool GLOBAL, bool CUSTOM>
+template <bool GLOBAL, bool CUSTOM, int UN = HP_UN>
 __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
                                          const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
-  for (uint32_t i0 = 0; i0 < T; i0 += stride * HP_UN) {
-    uint32_t w[HP_UN], c[HP_UN], v0[HP_UN], v1[HP_UN], dw[HP_UN];
+  for (uint32_t i0 = 0; i0 < T; i0 += stride * UN) {
+    uint32_t w[UN], c[UN], v0[UN], v1[UN], dw[UN];
 #pragma unroll
-    for (int q = 0; q < HP_UN; ++q) {
+    for (int q = 0; q < UN; ++q) {
       const uint32_t i = i0 + (uint32_t)q * stride + t;
       c[q] = v0[q] = v1[q] = 0;
       w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
     }
     if (!CUSTOM) {
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) dw[q] = a.g.deg[w[q] != HP_EMPTY ? w[q] : 0u];
+      for (int q = 0; q < UN; ++q) dw[q] = a.g.deg[w[q] != HP_EMPTY ? w[q] : 0u];
     }
 #pragma unroll
-    for (int q = 0; q < HP_UN; ++q) {
+    for (int q = 0; q < UN; ++q) {
       const bool valid = w[q] != HP_EMPTY;
       float s = 0.0f;
       if (valid) {
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       if (x > u) hp_mark<false>(tb, mask, shift, x);
     });
     wave_sync_lds();
-    hp_drain<false, CUSTOM>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
+    hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -748,6 +748,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
 // (slot, x) for x in N(u); the drain decodes the slot back to (u, deg u).
 // Needs S <= 2^(32 - 6) (six slot bits above w).
 constexpr uint64_t HB_ROWCOST = 5;  // budget units per row besides its wedges (bounds the rows per batch)
+constexpr int HB_UN = 8;            // loads per lane in flight in the batch loops (a batch is a few round trips)
 
 // The rows of tiers tlo..thi: a contiguous region of the tier list.
 __device__ __forceinline__ void hb_region(const uint32_t* tcnt, int tlo, int thi, uint32_t* base, uint32_t* cnt) {
@@ -784,15 +785,15 @@ __global__ void k_hp_batch_starts(const uint64_t* __restrict__ bpre, const uint3
   }
 }
 
-// hp_wedges with the first-hop entry's index: f(w, v, entry)
-template <typename IT, typename F>
+// hp_wedges with the first-hop entry's index: f(w, v, entry), UN keys per lane in flight
+template <int UN, typename IT, typename F>
 __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* s_incl, const uint64_t* s_start,
                                           const uint32_t* s_iv, const uint32_t* keys, F f) {
-  for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * HP_UN) {
-    uint32_t w[HP_UN], v[HP_UN], e[HP_UN];
-    bool ok[HP_UN];
+  for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * UN) {
+    uint32_t w[UN], v[UN], e[UN];
+    bool ok[UN];
 #pragma unroll
-    for (int q = 0; q < HP_UN; ++q) {
+    for (int q = 0; q < UN; ++q) {
       const uint64_t j = j0 + (uint64_t)q * 64 + t;
       ok[q] = j < total;
       uint32_t lo = 0, hi = 63;
@@ -806,7 +807,7 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
       w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
     }
 #pragma unroll
-    for (int q = 0; q < HP_UN; ++q)
+    for (int q = 0; q < UN; ++q)
       if (ok[q]) f(w[q], v[q], e[q]);
   }
 }
@@ -860,19 +861,47 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   wave_sync_lds();
-  for (uint32_t b = blockIdx.x * NWAVE + wv; b < nb; b += gridDim.x * NWAVE) {
-    const uint32_t r0 = bstart[b], nr = bstart[b + 1] - r0;  // nr < 64 by the budget
-    if (nr == 0) continue;
-    uint32_t u = 0, ns = 0, du = 0;
-    uint64_t s0 = 0, o0 = 0, W = 0;
-    if ((uint32_t)lane < nr) {
-      u = rows[r0 + lane];
-      W = wu[u - ua];
-      s0 = a.soff[u - a.sua];
-      ns = (uint32_t)(a.soff[u - a.sua + 1] - s0);
-      o0 = a.g.off[u];
-      du = (uint32_t)(a.g.off[u + 1] - o0);
+  // The next batch's bounds, rows and row data are loaded while this batch
+  // works (bounds during the first hops, rows during the exclusion, row data
+  // before the drain), so a batch pays only its own chain of graph reads.
+  const uint32_t stride = gridDim.x * NWAVE;
+  uint32_t b = blockIdx.x * NWAVE + wv;
+  uint32_t r0 = 0, nr = 0, u = 0, ns = 0, du = 0;
+  uint64_t s0 = 0, o0 = 0, W = 0;
+  auto fetch_bounds = [&](uint32_t bb, uint32_t* q0, uint32_t* qn) {
+    *q0 = bb < nb ? bstart[bb] : 0u;
+    *qn = bb < nb ? bstart[bb + 1] - *q0 : 0u;  // < 64 by the budget
+  };
+  auto fetch_info = [&](uint32_t n, uint32_t uu, uint64_t* pW, uint64_t* ps0, uint32_t* pns, uint64_t* po0,
+                        uint32_t* pdu) {
+    if ((uint32_t)lane < n) {
+      *pW = wu[uu - ua];
+      *ps0 = a.soff[uu - a.sua];
+      *pns = (uint32_t)(a.soff[uu - a.sua + 1] - *ps0);
+      *po0 = a.g.off[uu];
+      *pdu = (uint32_t)(a.g.off[uu + 1] - *po0);
+    } else {
+      *pW = 0;
+      *ps0 = 0;
+      *pns = 0;
+      *po0 = 0;
+      *pdu = 0;
     }
+  };
+  fetch_bounds(b, &r0, &nr);
+  u = (uint32_t)lane < nr ? rows[r0 + lane] : 0u;
+  fetch_info(nr, u, &W, &s0, &ns, &o0, &du);
+  for (; b < nb;) {
+    const uint32_t bn = b + stride;
+    uint32_t pr0, pnr, pu = 0;
+    if (nr == 0) {  // an empty batch (a row wider than the budget window skipped it)
+      fetch_bounds(bn, &r0, &nr);
+      u = (uint32_t)lane < nr ? rows[r0 + lane] : 0u;
+      fetch_info(nr, u, &W, &s0, &ns, &o0, &du);
+      b = bn;
+      continue;
+    }
+    fetch_bounds(bn, &pr0, &pnr);
     const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(du);
     s_u[wv][lane] = u;
     s_du[wv][lane] = du;
@@ -887,6 +916,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     const uint32_t T = 1u << lg, mask = T - 1;
     if (T > (uint32_t)TW) {  // a batch beyond the budget (a partition bug): fail the call, never overrun LDS
       if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+      nr = 0;  // skip it; the next batch is fetched at the loop top
       continue;
     }
     const int shift = 32 - lg;
@@ -912,7 +942,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       s_islot[wv][lane] = slot;
       wave_sync_lds();
       const uint32_t total = __shfl(incl, 63, 64);
-      hb_wedges(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+      hb_wedges<HB_UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                 [&](uint32_t w, uint32_t vv, uint32_t ent) {
                   const uint32_t sl = s_islot[wv][ent];
                   if (w > s_u[wv][sl]) {
@@ -922,38 +952,43 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
                 });
       wave_sync_lds();
     }
+    pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
     // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
-    for (uint32_t x0 = 0; x0 < NN; x0 += 64 * HP_UN) {
-      uint32_t key[HP_UN], sl[HP_UN];
+    // (marking from N(u) measured faster here than a membership-table line per entry)
+    for (uint32_t x0 = 0; x0 < NN; x0 += 64 * HB_UN) {
+      uint32_t key[HB_UN], sl[HB_UN];
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) {
+      for (int q = 0; q < HB_UN; ++q) {
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
         const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
         key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) {
+      for (int q = 0; q < HB_UN; ++q) {
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         if (x < NN && key[q] > s_u[wv][sl[q]]) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
       }
     }
     wave_sync_lds();
+    uint64_t pW, ps0, po0;
+    uint32_t pns, pdu;
+    fetch_info(pnr, pu, &pW, &ps0, &pns, &po0, &pdu);  // the next batch's row data, in flight during the drain
     // drain: every entry scored for its own row
-    for (uint32_t i0 = 0; i0 < T; i0 += 64 * HP_UN) {
-      uint32_t kq[HP_UN], c[HP_UN], v0[HP_UN], v1[HP_UN], dw[HP_UN];
+    for (uint32_t i0 = 0; i0 < T; i0 += 64 * HB_UN) {
+      uint32_t kq[HB_UN], c[HB_UN], v0[HB_UN], v1[HB_UN], dw[HB_UN];
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) {
+      for (int q = 0; q < HB_UN; ++q) {
         const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
         c[q] = v0[q] = v1[q] = 0;
         kq[q] = i < T ? hp_take<false, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
       }
       if (!CUSTOM) {
 #pragma unroll
-        for (int q = 0; q < HP_UN; ++q) dw[q] = a.g.deg[kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u];
+        for (int q = 0; q < HB_UN; ++q) dw[q] = a.g.deg[kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u];
       }
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) {
+      for (int q = 0; q < HB_UN; ++q) {
         const bool valid = kq[q] != HP_EMPTY;
         const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
         const uint32_t uu = s_u[wv][sl];
@@ -967,6 +1002,15 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
     }
     wave_sync_lds();
+    r0 = pr0;
+    nr = pnr;
+    u = pu;
+    W = pW;
+    s0 = ps0;
+    ns = pns;
+    o0 = po0;
+    du = pdu;
+    b = bn;
   }
   hp_finish(sg, a, wedges);
 }
@@ -1763,7 +1807,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       if ((uint64_t)x >= slo && (uint64_t)x < shi) hp_mark<false>(tb, mask, hs, x);
     });
     __syncthreads();
-    hp_drain<false, CUSTOM>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
+    hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
     __syncthreads();
   }
   hp_finish(sg, a, wedges);
@@ -1842,9 +1886,9 @@ __global__ void k_hp_take(const uint32_t* __restrict__ idx, uint64_t take, uint6
 
 // (u << 32 | w) + identity index, for the canonical (u, w) order before the final sort
 __global__ void k_hp_uwkeys(const uint32_t* __restrict__ u, const uint32_t* __restrict__ w, uint64_t n,
-                            uint64_t* __restrict__ k, uint32_t* __restrict__ idx) {
+                            uint64_t* __restrict__ k, uint32_t* __restrict__ idx, int vb) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    k[i] = ((uint64_t)u[i] << 32) | w[i];
+    k[i] = ((uint64_t)u[i] << vb) | w[i];
     idx[i] = (uint32_t)i;
   }
 }

@@ -62,6 +62,7 @@ enum Buf {
   B_TKEY, B_TU, B_TW, B_TS,           // compaction target
   B_TIE, B_TRANK, B_KEEP, B_KPOS,
   B_SK0, B_SK1, B_SV0, B_SV1,         // final sort
+  B_OSORT,                            // sort_pairs_os: n, ticket, error, digit histograms, descriptors
   B_HIST, B_HOFF, B_SCAN, B_SCAN2, B_SELHIST, B_SEL, B_CNT, B_EDGES,
   // v1 pipeline
   B_ARENA, B_ARENA2, B_VLIST, B_VIOFF, B_UCNT, B_UOFF, B_IEU, B_IEV, B_IEF, B_IEP, B_BUCKET,
@@ -253,8 +254,12 @@ struct nlp_graph {
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
+  int hp_hub_min = 2;        // lowest bin the hub pass takes (NLP_HASH_HUB_MIN=1: bin 1 too)
   bool hp_hub = true;        // path 4: bins 2 / 3 by the hub pass (k_hh_*; NLP_HASH_HUB=0: k_hp_part)
   bool hp_batch = true;      // path 4: bin-0 tiers 0 / 1 in row batches (k_hp_batch; NLP_HASH_BATCH=0: a wave per row)
+  // (u64, u32) sorts of paths 2 / 4 by onesweep passes (NLP_OS_SORT=1); the default hist / scan / scatter
+  // passes measured faster at these sizes (C4 JAC H=16 ordering: 22 vs 77 ms; C3 AA H=16 path 2: 122 vs 418 ms)
+  bool os_sort = false;
   bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
@@ -658,8 +663,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
   if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
   if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
+  if (const char* os = getenv("NLP_OS_SORT")) g->os_sort = os[0] == '1';
   if (const char* hb = getenv("NLP_HASH_BATCH")) g->hp_batch = hb[0] != '0';
   if (const char* hh = getenv("NLP_HASH_HUB")) g->hp_hub = hh[0] != '0';
+  if (const char* hm = getenv("NLP_HASH_HUB_MIN")) g->hp_hub_min = std::max(1, std::min(2, atoi(hm)));
   if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
@@ -750,31 +757,90 @@ struct Cands {
 
 // Group the W wedges of one generator pass, score them and append the
 // surviving candidates to the candidate buffer.
+__global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
+
+// Stable LSD sort of (u64 key, u32 value) pairs (values may be null) by the
+// 8-bit digits at `shifts` (multiples of 8, least significant first), with the
+// onesweep pass of the sort path (sortpath.hpp k_sp_pass<u64>): one read builds
+// every digit histogram, then one kernel per digit -- no per-pass histogram
+// and scan launches, and a pass writes each key once.  Descriptors of two
+// alternate buffers clean themselves (each pass zeroes the previous pass's).
+// Beyond SP_MAX_N (30-bit descriptor counts) or without NLP_OS_SORT=1: the
+// hist / scan / scatter passes of prims.hpp.
+nlp_status sort_pairs_os(nlp_graph* g, uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n,
+                         const int* shifts, int np, int* which, hipStream_t st) {
+  *which = 0;
+  if (n <= 1 || np == 0) return NLP_OK;
+  Workspace& ws = g->ws;
+  if (n > SP_MAX_N || !g->os_sort) {
+    uint64_t *hoff, *scan;
+    uint32_t* hist;
+    const uint64_t nb = rs_blocks(n);
+    TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+    TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+    TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(n, RS_BINS * nb)) + 16, &scan));
+    SortScratch sc{hist, hoff, scan, nb};
+    TRY(sort_pairs_u64(k0, v0, k1, v1, n, shifts, np, sc, which, st));
+    return NLP_OK;
+  }
+  const uint64_t ntiles = (n + OS2_TILE - 1) / OS2_TILE;
+  const uint64_t hwords = (uint64_t)HCOPIES * HSTRIDE / 2, dwords = ntiles * RS_BINS / 2;  // u64 words
+  uint64_t* b;
+  TRY(wsget(ws, B_OSORT, 8 + hwords + 2 * dwords, &b));
+  TRY(hipMemsetAsync(b, 0, (8 + hwords + 2 * dwords) * 8, st));
+  uint64_t* d_n = b;
+  uint32_t* tick = (uint32_t*)(b + 1);  // 8 tickets
+  uint32_t* err = (uint32_t*)(b + 5);
+  uint32_t* ghist = (uint32_t*)(b + 8);
+  uint32_t* desc[2] = {(uint32_t*)(b + 8 + hwords), (uint32_t*)(b + 8 + hwords + dwords)};
+  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_n, n);
+  hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(256), dim3(NT), 0, st, (const uint64_t*)k0, (const uint64_t*)d_n, n, 0, 8,
+                     ghist, (uint64_t*)nullptr, (uint64_t*)nullptr);
+  TRY(hipGetLastError());
+  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_p64));
+  uint64_t* ka = k0;
+  uint64_t* kb = k1;
+  uint32_t* va = v0;
+  uint32_t* vb = v1;
+  for (int p = 0; p < np && p < 8; ++p) {
+    hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), dim3(gr), dim3(OS_NT), 0, st, (const uint64_t*)ka,
+                       (const uint32_t*)va, kb, vb, (const uint64_t*)d_n, shifts[p],
+                       (const uint32_t*)(ghist + (shifts[p] / 8) * RS_BINS), desc[p & 1], tick + p, err,
+                       (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint64_t*)nullptr,
+                       (const uint64_t*)nullptr, 0u, 0, (uint64_t*)nullptr, p ? desc[(p - 1) & 1] : (uint32_t*)nullptr);
+    TRY(hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+    *which ^= 1;
+  }
+  TRY(hipMemcpyAsync(&g->host_small[60], err, 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  if (g->host_small[60] & 0xffffffffull) return NLP_ERR_DEVICE;  // a look-back gave up (never expected)
+  return NLP_OK;
+}
+
 nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* wk, uint32_t* wv, Cands& C,
                            hipStream_t st) {
   Workspace& ws = g->ws;
   const bool custom = p.metric == M_AA || p.metric == M_RA;
   if (W == 0) return NLP_OK;
-  uint64_t *wk1, *hoff, *scan, *rid, *rstart, *rpos, *cnt;
-  uint32_t *wv1 = nullptr, *hist, *rflag, *rkey, *ru, *rw, *rfl;
+  uint64_t *wk1, *scan, *rid, *rstart, *rpos, *cnt;
+  uint32_t *wv1 = nullptr, *rflag, *rkey, *ru, *rw, *rfl;
   float* rs;
   TRY(wsget(ws, B_WKEY1, W, &wk1));
   if (custom) TRY(wsget(ws, B_WVAL1, W, &wv1));
-  uint64_t nb = rs_blocks(W);
-  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
-  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
-  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(W, RS_BINS * nb)) + 16, &scan));
   TRY(wsget(ws, B_CNT, 8, &cnt));
   // 1. stable sort by (u, w): bytes of w then bytes of u
   int vb = bits_for(g->span - 1);
   int shifts[8], np = 0;
   for (int b = 0; b < vb; b += 8) shifts[np++] = b;
   for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
-  SortScratch sc{hist, hoff, scan, nb};
   int which = 0;
-  TRY(sort_pairs_u64(wk, custom ? wv : nullptr, wk1, custom ? wv1 : nullptr, W, shifts, np, sc, &which, st));
+  { nlp_status so = sort_pairs_os(g, wk, custom ? wv : nullptr, wk1, custom ? wv1 : nullptr, W, shifts, np, &which, st);
+    if (so != NLP_OK) return so; }
   uint64_t* sk = which ? wk1 : wk;
   uint32_t* sv = which ? wv1 : wv;
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(W) + 16, &scan));  // after the sort (its fallback regrows B_SCAN2)
   // 2. runs of equal (u, w)
   TRY(wsget(ws, B_RFLAG, W, &rflag));
   TRY(wsget(ws, B_RID, W, &rid));
@@ -899,22 +965,17 @@ nlp_status prune_to(nlp_graph* g, Cands& C, uint64_t k, hipStream_t st) {
 nlp_status order_into(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   if (C.n == 0) return NLP_OK;
   Workspace& ws = g->ws;
-  uint64_t *k0, *k1, *hoff, *scan;
-  uint32_t *v0, *v1, *hist;
+  uint64_t *k0, *k1;
+  uint32_t *v0, *v1;
   TRY(wsget(ws, B_SK0, C.n, &k0));
   TRY(wsget(ws, B_SK1, C.n, &k1));
   TRY(wsget(ws, B_SV0, C.n, &v0));
   TRY(wsget(ws, B_SV1, C.n, &v1));
-  uint64_t nb = rs_blocks(C.n);
-  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
-  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
-  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(C.n, RS_BINS * nb)) + 16, &scan));
   LAUNCH(k_desc_keys, C.n, st, (const uint32_t*)ws.p[B_CKEY], C.n, k0, v0);
   TRY(hipGetLastError());
   int shifts[4] = {0, 8, 16, 24};
-  SortScratch sc{hist, hoff, scan, nb};
   int which = 0;
-  TRY(sort_pairs_u64(k0, v0, k1, v1, C.n, shifts, 4, sc, &which, st));
+  { nlp_status so = sort_pairs_os(g, k0, v0, k1, v1, C.n, shifts, 4, &which, st); if (so != NLP_OK) return so; }
   LAUNCH(k_gather_edges, C.n, st, which ? v1 : v0, C.n, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW],
          (const float*)ws.p[B_CS], d_out);
   TRY(hipGetLastError());
@@ -1129,7 +1190,9 @@ nlp_status order_v1(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   uint32_t* err = (uint32_t*)&ctr[1];
   LAUNCH(k_desc_keys32, C.n, st, (const uint32_t*)ws.p[B_CKEY], C.n, k0, v0);
   TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_os_hist, dim3(std::min<uint64_t>(64, grid_for(C.n))), dim3(NT), 0, st, k0, ctr, ghist);
+  // 4 workgroups per CU: the score keys' high digits are few (ties), and 64
+  // workgroups serialised on their LDS atomics (C4 JAC H=16: 4.8 ms for 1.9e8 keys)
+  hipLaunchKernelGGL(k_os_hist, dim3(std::min<uint64_t>(1024, grid_for(C.n))), dim3(NT), 0, st, k0, ctr, ghist);
   TRY(hipGetLastError());
   uint32_t *ka = k0, *va = v0, *kb = k1, *vb = v1;
   for (int pass = 0; pass < 4; ++pass) {
@@ -1356,19 +1419,12 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
     // canonical tie order: (u asc, w asc)
     TRY(wsget(ws, B_HP_TIEK1, ties, &tk1));
     TRY(wsget(ws, B_HP_TIEI1, ties, &ti1));
-    uint64_t nb = rs_blocks(ties);
-    uint32_t* hist;
-    uint64_t *hoff, *scan;
-    TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
-    TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
-    TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(ties, RS_BINS * nb)) + 16, &scan));
     const int vb = bits_for(g->span - 1);
     int shifts[8], np = 0;
     for (int b = 0; b < vb; b += 8) shifts[np++] = b;
     for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
-    SortScratch sc{hist, hoff, scan, nb};
     int which = 0;
-    TRY(sort_pairs_u64(tk0, ti0, tk1, ti1, ties, shifts, np, sc, &which, st));
+    { nlp_status so = sort_pairs_os(g, tk0, ti0, tk1, ti1, ties, shifts, np, &which, st); if (so != NLP_OK) return so; }
     take_idx = which ? ti1 : ti0;
   }
   if (quota)
@@ -1387,25 +1443,20 @@ nlp_status hp_uw_order(nlp_graph* g, Cands& C, hipStream_t st) {
   if (C.n <= 1) return NLP_OK;
   Workspace& ws = g->ws;
   const uint64_t n = C.n;
-  uint64_t *k0, *k1, *hoff, *scan;
-  uint32_t *v0, *v1, *hist;
+  uint64_t *k0, *k1;
+  uint32_t *v0, *v1;
   TRY(wsget(ws, B_SK0, n, &k0));
   TRY(wsget(ws, B_SK1, n, &k1));
   TRY(wsget(ws, B_SV0, n, &v0));
   TRY(wsget(ws, B_SV1, n, &v1));
-  uint64_t nb = rs_blocks(n);
-  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
-  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
-  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(n, RS_BINS * nb)) + 16, &scan));
-  LAUNCH(k_hp_uwkeys, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], n, k0, v0);
-  TRY(hipGetLastError());
+  // keys (u << vb | w): 2 vb bits, so 7 byte passes instead of 8 at vb = 26
   const int vb = bits_for(g->span - 1);
+  LAUNCH(k_hp_uwkeys, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], n, k0, v0, vb);
+  TRY(hipGetLastError());
   int shifts[8], np = 0;
-  for (int b = 0; b < vb; b += 8) shifts[np++] = b;
-  for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
-  SortScratch sc{hist, hoff, scan, nb};
+  for (int b = 0; b < 2 * vb; b += 8) shifts[np++] = b;
   int which = 0;
-  TRY(sort_pairs_u64(k0, v0, k1, v1, n, shifts, np, sc, &which, st));
+  { nlp_status so = sort_pairs_os(g, k0, v0, k1, v1, n, shifts, np, &which, st); if (so != NLP_OK) return so; }
   uint32_t *nk, *nu, *nw;
   float* ns;
   TRY(wsget(ws, B_TKEY, n, &nk));
@@ -1740,7 +1791,12 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
     }
     TRY(hipMemsetAsync(tcnt + 6, 0, 3 * sizeof(uint32_t), st));  // work queues of bins 2, 3 and 1
-    if (n1) {
+    bool b1_done = false;
+    if (n1 && g->hp_hub && g->hp_hub_min == 1) {
+      nlp_status sh = run_hub(g, a, lists[1] + q0[1], n1, nullptr, 0, wu, ua, custom, scan, tcnt + 11, &b1_done, st);
+      if (sh != NLP_OK) return sh;
+    }
+    if (n1 && !b1_done) {
       const unsigned gr = (unsigned)std::min<uint64_t>(n1, 2048);
       if (custom) hipLaunchKernelGGL((k_hp_block<true, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
       else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
@@ -2411,7 +2467,7 @@ nlp_status launch_sp(nlp_graph* g, const Params& p, const SpBufs& f, EdgeOut* ou
                            (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,
                            (uint32_t)nb_used, f.caplog,
                            GatherOut{nullptr, nullptr, nullptr, p.max_edges, out, ctr, g->host_ctr_dev, ts, g->d_sticky},
-                           ts + TS_HOT_OUT);
+                           ts + TS_HOT_OUT, hot == s ? g->d_stamp : nullptr);
       } else if (f.counted && ps == 0) {  // dense tiles of k_sp_grouprun's candidates (it counted digit 0 per bucket group)
         hipLaunchKernelGGL(k_sp_cpass0, dim3(CP_MAXT), dim3(OS_NT), 0, st, (const uint32_t*)f.ok0,
                            (const uint32_t*)f.cu, (const uint32_t*)f.cw, (const float*)f.cs, (const uint32_t*)f.segcnt,

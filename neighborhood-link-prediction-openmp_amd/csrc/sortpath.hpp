@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
         }
       }
       k[i] = ok[i] ? kin[sj] : (K)0;
-      v[i] = ok[i] ? vin[sj] : 0u;
+      v[i] = ok[i] && vin ? vin[sj] : 0u;  // vin null: keys only
     }
     EdgeOut eo[GATHER ? IPT : 1];
     if (GATHER) {  // the output columns are fetched now, in flight during ranking and look-back
@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_pass(const K* __restrict__ kin, co
           if (pos < go.k) go.out[pos] = eo[i];
         } else {
           kout[pos] = k[i];
-          vout[pos] = v[i];
+          if (vout) vout[pos] = v[i];
         }
         if (NEXT_HIST) {
 #pragma unroll
@@ -1573,7 +1573,8 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
                                                          const uint32_t* __restrict__ cw,
                                                          const float* __restrict__ cs,
                                                          const uint32_t* __restrict__ kcnt, uint32_t nb, int caplog,
-                                                         GatherOut go, uint64_t* __restrict__ end_mark) {
+                                                         GatherOut go, uint64_t* __restrict__ end_mark,
+                                                         uint64_t* __restrict__ stamp = nullptr) {
   constexpr uint32_t PER = (DX_MAXB + OS_NT - 1) / OS_NT;
   constexpr int LD = (int)(SO_MAX / OS_NT);  // positions per thread
   constexpr uint32_t NBIN = 1u << SR_BITS;
@@ -1586,6 +1587,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
   __shared__ uint32_t s_mm[2];
   const int t = threadIdx.x;
   ts_mark_end(end_mark);  // the end of the kernel before (the hot kernel)
+  sp_stamp(stamp, true, 7);
   if (t == 0) { s_mm[0] = 0xffffffffu; s_mm[1] = 0u; }
   {  // bucket prefix: thread t sums buckets [PER t, PER t + PER)
     uint32_t v[PER], sum = 0;
@@ -1612,6 +1614,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
   const uint64_t m = fits ? (n < go.k ? (uint64_t)n : go.k) : 0ull;
   const uint32_t Q = (n + gridDim.x - 1) / gridDim.x;
   const uint32_t q0 = blockIdx.x * Q;
+  sp_stamp(stamp, true, 0);
   if (fits && q0 < n) {
     uint32_t sl[LD], kk[LD];
 #pragma unroll
@@ -1627,6 +1630,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
 #pragma unroll
     for (int i = 0; i < LD; ++i) kk[i] = okey[sl[i]];  // slot 0 always exists
     uint32_t kmin = 0xffffffffu, kmax = 0u;
+    sp_stamp(stamp, true, 1);
 #pragma unroll
     for (int i = 0; i < LD; ++i)
       if ((uint32_t)i * OS_NT + (uint32_t)t < n) {
@@ -1644,6 +1648,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
     }
     for (uint32_t i = t; i < NBIN; i += OS_NT) s_bin[i] = 0u;
     __syncthreads();
+    sp_stamp(stamp, true, 2);
     kmin = s_mm[0];
     const uint32_t span = s_mm[1] - kmin;
     const int lb = span ? 32 - __clz(span) : 0;
@@ -1655,6 +1660,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
       if ((uint32_t)i * OS_NT + (uint32_t)t < n) atomicAdd(&s_bin[bn[i]], 1u);
     }
     __syncthreads();
+    sp_stamp(stamp, true, 3);
     {  // exclusive starts: thread t owns bins [BPT t, BPT t + BPT)
       uint32_t c[BPT], sum = 0;
       const uint4* p = reinterpret_cast<const uint4*>(s_bin + (uint32_t)t * BPT);
@@ -1688,6 +1694,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
       if (j < n) s_list[atomicAdd(&s_bin[bn[i]], 1u)] = cp[i];
     }
     __syncthreads();
+    sp_stamp(stamp, true, 4);
 #pragma unroll
     for (int i = 0; i < LD; ++i) {  // this workgroup's positions: rank within the bin, gather
       const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
@@ -1714,6 +1721,7 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
       }
     }
   }
+  sp_stamp(stamp, true, 5);
   if (blockIdx.x == 0 && t < NCTR) {  // counters: final once this call's kernels before this one are done
     uint64_t x = ctr[t];
     if (t == C_C) x = n;

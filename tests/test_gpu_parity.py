@@ -415,7 +415,9 @@ class _env:
 # over several workgroups (bucket slices, exclusion cursor per slice), 8 the
 # edge-parallel work estimate, 9 a wave per bin-0 row, 10 k_hp_part for every row,
 # 11 hub pass with one w-bucket per row, 12 the same with 128-entry item
-# tables (heavy buckets split into w-range items by their fine histogram)
+# tables (heavy buckets split into w-range items by their fine histogram),
+# 13 the ordering sorts by onesweep passes instead of hist / scan / scatter,
+# 14 bin-1 rows by the hub pass
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -423,7 +425,8 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7")]
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7"), dict(NLP_OS_SORT="1"),
+                 dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
