@@ -796,11 +796,10 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
     for (int q = 0; q < UN; ++q) {
       const uint64_t j = j0 + (uint64_t)q * 64 + t;
       ok[q] = j < total;
-      uint32_t lo = 0, hi = 63;
-      while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if ((uint64_t)s_incl[m] > j) hi = m; else lo = m + 1;
-      }
+      uint32_t lo = 0;  // the first entry with s_incl > j (six fixed steps, see hb_slot)
+#pragma unroll
+      for (uint32_t bit = 32; bit > 0; bit >>= 1) lo += (uint64_t)s_incl[lo + bit - 1] <= j ? bit : 0u;
+      if (lo > 63) lo = 63;
       const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
       v[q] = s_iv[lo];
       e[q] = lo;
@@ -812,13 +811,15 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
   }
 }
 
-// the batch slot of flattened item j: the first r with incl[r] > j (nr <= 64 entries)
-__device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t nr, uint32_t j) {
-  uint32_t lo = 0, hi = nr - 1;
-  while (lo < hi) {
-    const uint32_t m = (lo + hi) >> 1;
-    if (incl[m] > j) hi = m; else lo = m + 1;
-  }
+// the batch slot of flattened item j < incl[63]: the first r with incl[r] > j
+// (64 non-decreasing inclusive prefixes; lanes past the batch's rows repeat
+// the total).  Six fixed steps, no loop: the search runs for every item and a
+// data-dependent loop costs more in branch and exec-mask instructions than the
+// compares themselves.
+__device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t, uint32_t j) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t bit = 32; bit > 0; bit >>= 1) lo += incl[lo + bit - 1] <= j ? bit : 0u;
   return lo;
 }
 
@@ -974,7 +975,9 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     uint64_t pW, ps0, po0;
     uint32_t pns, pdu;
     fetch_info(pnr, pu, &pW, &ps0, &pns, &po0, &pdu);  // the next batch's row data, in flight during the drain
-    // drain: every entry scored for its own row
+    // drain: every entry scored for its own row (a list of the claimed slots
+    // instead of this scan measured slower: the claims cost more in the insert
+    // loop than the scan of empty slots)
     for (uint32_t i0 = 0; i0 < T; i0 += 64 * HB_UN) {
       uint32_t kq[HB_UN], c[HB_UN], v0[HB_UN], v1[HB_UN], dw[HB_UN];
 #pragma unroll

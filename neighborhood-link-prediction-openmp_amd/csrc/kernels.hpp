@@ -276,22 +276,88 @@ __global__ void k_find_chunk_end(const uint64_t* __restrict__ woff, uint64_t E, 
 }
 
 // ---------------------------------------------------------------- common: wedge materialisation
-// One thread per wedge slot i < W; slot order = (edge slot, w index) so the
-// generator's order is preserved.  val = deg(v) for AA/RA (contribution table).
+// Wedge slot i < W (slot order = (edge slot, w index), the generator's order)
+// -> key (u - ubase) << wb | w, and for AA/RA val = deg(v) (contribution
+// table).  A workgroup takes WG_TILE consecutive slots: two searches of the
+// edge offsets find its window of edges, which is staged in LDS when it fits
+// WG_WIN entries, so each slot's edge is an LDS search instead of ~30
+// dependent global loads (edges without wedges can widen a window beyond
+// WG_WIN: then the global search).
+constexpr int WG_IPT = 8;
+constexpr uint32_t WG_TILE = NT * WG_IPT;
+constexpr uint32_t WG_WIN = 2048;
+
 template <bool VAL>
-__global__ void k_wedges(const uint64_t* __restrict__ woff, uint64_t E, const uint64_t* __restrict__ d_W,
-                         uint64_t wbase, const uint32_t* __restrict__ ev, const uint32_t* __restrict__ eu,
-                         const uint32_t* __restrict__ efirst, const uint64_t* __restrict__ off,
-                         const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg,
-                         uint64_t* __restrict__ wkey, uint32_t* __restrict__ wval) {
+__global__ __launch_bounds__(NT) void k_wedges(const uint64_t* __restrict__ woff, uint64_t E,
+                                               const uint64_t* __restrict__ d_W, uint64_t wbase,
+                                               const uint32_t* __restrict__ ev, const uint32_t* __restrict__ eu,
+                                               const uint32_t* __restrict__ efirst, const uint64_t* __restrict__ off,
+                                               const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg,
+                                               uint64_t* __restrict__ wkey, uint32_t* __restrict__ wval, uint32_t ubase,
+                                               int wb) {
+  __shared__ uint64_t s_wo[WG_WIN + 1];
+  __shared__ uint32_t s_v[WG_WIN], s_u[WG_WIN], s_f[WG_WIN];
+  __shared__ uint64_t s_e[2];
   const uint64_t W = *d_W - wbase;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < W; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t s = wbase + i;
-    uint64_t e = lbs_find(woff, E, s);
-    uint32_t v = ev[e];
-    uint32_t w = keys[off[v] + efirst[e] + (s - woff[e])];
-    wkey[i] = ((uint64_t)eu[e] << 32) | w;
-    if (VAL) wval[i] = deg[v];
+  const int t = threadIdx.x;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * WG_TILE; t0 < W; t0 += (uint64_t)gridDim.x * WG_TILE) {
+    const uint64_t t1 = t0 + WG_TILE < W ? t0 + WG_TILE : W;
+    if (t < 2) s_e[t] = lbs_find(woff, E, wbase + (t == 0 ? t0 : t1 - 1));
+    __syncthreads();
+    const uint64_t e_lo = s_e[0], e_hi = s_e[1];
+    const uint64_t nw = e_hi - e_lo + 1;
+    const bool staged = nw <= WG_WIN;
+    if (staged)
+      for (uint32_t i = t; i <= nw; i += NT) {
+        s_wo[i] = i < nw ? woff[e_lo + i] : (e_lo + nw < E ? woff[e_lo + nw] : ~0ull);
+        if (i < nw) {
+          s_v[i] = ev[e_lo + i];
+          s_u[i] = eu[e_lo + i];
+          s_f[i] = efirst[e_lo + i];
+        }
+      }
+    __syncthreads();
+    uint32_t v[WG_IPT], u[WG_IPT];
+    uint64_t pos[WG_IPT];
+    bool ok[WG_IPT];
+#pragma unroll
+    for (int q = 0; q < WG_IPT; ++q) {
+      const uint64_t i = t0 + (uint64_t)q * NT + t;
+      ok[q] = i < t1;
+      const uint64_t sl = wbase + (ok[q] ? i : t0);
+      if (staged) {
+        uint32_t lo = 0, hi = (uint32_t)nw;  // last window edge with s_wo <= sl
+        while (hi - lo > 1) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (s_wo[m] <= sl) lo = m; else hi = m;
+        }
+        v[q] = s_v[lo];
+        u[q] = s_u[lo];
+        pos[q] = (uint64_t)s_f[lo] + (sl - s_wo[lo]);
+      } else {
+        const uint64_t e = lbs_find(woff, E, sl);
+        v[q] = ev[e];
+        u[q] = eu[e];
+        pos[q] = (uint64_t)efirst[e] + (sl - woff[e]);
+      }
+    }
+    uint64_t ov[WG_IPT];
+#pragma unroll
+    for (int q = 0; q < WG_IPT; ++q) ov[q] = off[v[q]];  // in flight together
+    uint32_t w[WG_IPT], d[WG_IPT];
+#pragma unroll
+    for (int q = 0; q < WG_IPT; ++q) {
+      w[q] = keys[ov[q] + pos[q]];
+      d[q] = VAL ? deg[v[q]] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < WG_IPT; ++q) {
+      if (!ok[q]) continue;
+      const uint64_t i = t0 + (uint64_t)q * NT + t;
+      wkey[i] = ((uint64_t)(u[q] - ubase) << wb) | w[q];  // (u - ubase, w) packed: fewer sort digits
+      if (VAL) wval[i] = d[q];
+    }
+    __syncthreads();
   }
 }
 
@@ -316,12 +382,13 @@ __global__ void k_score(const uint64_t* __restrict__ rstart, const uint64_t* __r
                         const uint32_t* __restrict__ deg, const double* __restrict__ ctab, int metric,
                         float min_score, uint32_t* __restrict__ ckey, uint32_t* __restrict__ cu,
                         uint32_t* __restrict__ cw, float* __restrict__ cs, uint32_t* __restrict__ cflag,
-                        uint32_t maxf2, const uint64_t* __restrict__ etab, uint32_t etbits) {
+                        uint32_t maxf2, const uint64_t* __restrict__ etab, uint32_t etbits, uint32_t ubase,
+                        int wb) {
   const uint64_t R = *d_R;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t s = rstart[r], e = rstart[r + 1];
     uint64_t k = wkey[s];
-    uint32_t u = (uint32_t)(k >> 32), w = (uint32_t)k;
+    uint32_t u = (uint32_t)(k >> wb) + ubase, w = (uint32_t)(k & ((1ull << wb) - 1));
     bool excl = etab ? et_has(etab, etbits, u, w) : contains_u32(keys + off[u], deg[u], w);
     float sc;
     if (CUSTOM) {

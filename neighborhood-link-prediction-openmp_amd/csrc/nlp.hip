@@ -819,8 +819,9 @@ nlp_status sort_pairs_os(nlp_graph* g, uint64_t* k0, uint32_t* v0, uint64_t* k1,
   return NLP_OK;
 }
 
+// Records: key (u - ubase) << wb | w with u - ubase < 2^ubits (k_wedges), value deg v (AA / RA).
 nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* wk, uint32_t* wv, Cands& C,
-                           hipStream_t st) {
+                           hipStream_t st, uint32_t ubase, int ubits, int wb) {
   Workspace& ws = g->ws;
   const bool custom = p.metric == M_AA || p.metric == M_RA;
   if (W == 0) return NLP_OK;
@@ -830,11 +831,9 @@ nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* 
   TRY(wsget(ws, B_WKEY1, W, &wk1));
   if (custom) TRY(wsget(ws, B_WVAL1, W, &wv1));
   TRY(wsget(ws, B_CNT, 8, &cnt));
-  // 1. stable sort by (u, w): bytes of w then bytes of u
-  int vb = bits_for(g->span - 1);
+  // 1. stable sort by (u, w): the bytes of the packed key
   int shifts[8], np = 0;
-  for (int b = 0; b < vb; b += 8) shifts[np++] = b;
-  for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;
+  for (int b = 0; b < ubits + wb && np < 8; b += 8) shifts[np++] = b;
   int which = 0;
   { nlp_status so = sort_pairs_os(g, wk, custom ? wv : nullptr, wk1, custom ? wv1 : nullptr, W, shifts, np, &which, st);
     if (so != NLP_OK) return so; }
@@ -862,10 +861,10 @@ nlp_status group_and_score(nlp_graph* g, const Params& p, uint64_t W, uint64_t* 
   const double* ctab = p.metric == M_AA ? g->ctab_aa : g->ctab_ra;
   if (custom)
     LAUNCH(k_score<true>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru, rw,
-           rs, rfl, p.maxf2, g->etab, g->etbits);
+           rs, rfl, p.maxf2, g->etab, g->etbits, ubase, wb);
   else
     LAUNCH(k_score<false>, R, st, rstart, cnt, sk, sv, g->off, g->keys, g->deg, ctab, p.metric, p.min_score, rkey, ru,
-           rw, rs, rfl, p.maxf2, g->etab, g->etbits);
+           rw, rs, rfl, p.maxf2, g->etab, g->etbits, ubase, wb);
   TRY(hipGetLastError());
   // 4. append flagged candidates
   TRY(scan_excl_u64<uint32_t>(rfl, R, rpos, cnt + 1, scan, st));
@@ -1243,12 +1242,16 @@ nlp_status run_path1(nlp_graph* g, const Params& p, Cands& C, bool* fits, hipStr
   const bool custom = p.metric == M_AA || p.metric == M_RA;
   TRY(wsget(ws, B_WKEY0, W, &wk));
   if (custom) TRY(wsget(ws, B_WVAL0, W, &wv));
+  const uint64_t ua1 = std::min(p.ua, S), ub1 = std::min(p.ub, S);
+  const int wb1 = bits_for(S - 1), ubits1 = bits_for(ub1 > ua1 ? ub1 - ua1 - 1 : 0);
   if (custom)
-    LAUNCH(k_wedges<true>, W, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+    hipLaunchKernelGGL(k_wedges<true>, dim3((unsigned)std::min<uint64_t>((W + WG_TILE - 1) / WG_TILE, 65535)), dim3(NT), 0, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv,
+           (uint32_t)ua1, wb1);
   else
-    LAUNCH(k_wedges<false>, W, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+    hipLaunchKernelGGL(k_wedges<false>, dim3((unsigned)std::min<uint64_t>((W + WG_TILE - 1) / WG_TILE, 65535)), dim3(NT), 0, st, woff, E, cnt + 1, (uint64_t)0, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv,
+           (uint32_t)ua1, wb1);
   TRY(hipGetLastError());
-  return group_and_score(g, p, W, wk, wv, C, st);
+  return group_and_score(g, p, W, wk, wv, C, st, (uint32_t)ua1, ubits1, wb1);
 }
 
 // Path 2 generator: source range [ua, ub) in chunks of <= wedge_budget wedges
@@ -1329,12 +1332,15 @@ nlp_status run_path2(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       // cnt[3] = wb for the grid-stride bound
       g->host_small[21] = wb;
       TRY(hipMemcpyAsync(cnt + 3, &g->host_small[21], 8, hipMemcpyHostToDevice, st));
+      const int wb2 = bits_for(S - 1), ubits2 = bits_for(ub > ua ? ub - ua - 1 : 0);
       if (custom)
-        LAUNCH(k_wedges<true>, W, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+        hipLaunchKernelGGL(k_wedges<true>, dim3((unsigned)std::min<uint64_t>((W + WG_TILE - 1) / WG_TILE, 65535)), dim3(NT), 0, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv,
+               (uint32_t)ua, wb2);
       else
-        LAUNCH(k_wedges<false>, W, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv);
+        hipLaunchKernelGGL(k_wedges<false>, dim3((unsigned)std::min<uint64_t>((W + WG_TILE - 1) / WG_TILE, 65535)), dim3(NT), 0, st, woff, E, cnt + 3, wa, ev, eu, efirst, g->off, g->keys, g->deg, wk, wv,
+               (uint32_t)ua, wb2);
       TRY(hipGetLastError());
-      nlp_status s = group_and_score(g, p, W, wk, wv, C, st);
+      nlp_status s = group_and_score(g, p, W, wk, wv, C, st, (uint32_t)ua, ubits2, wb2);
       if (s != NLP_OK) return s;
       if (C.n > 2 * p.max_edges + (1u << 20)) {
         s = prune_to(g, C, p.max_edges, st);

@@ -1616,19 +1616,37 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
   const uint32_t q0 = blockIdx.x * Q;
   sp_stamp(stamp, true, 0);
   if (fits && q0 < n) {
-    uint32_t sl[LD], kk[LD];
-#pragma unroll
-    for (int i = 0; i < LD; ++i) {  // the bucket slot of each position (LDS searches, independent chains)
-      const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
-      uint32_t lo = 0, hi = nb;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_pre[mid] <= j) lo = mid; else hi = mid;
+    // keys in position order: thread t owns positions [LD t, LD t + LD) (one
+    // search for its first bucket, then a walk over the bucket starts), stores
+    // them in LDS (s_list, free until the scatter), then reads back its
+    // strided positions i OS_NT + t
+    {
+      const uint32_t p0 = (uint32_t)t * LD;
+      uint32_t b = 0, hi = nb;  // last b with s_pre[b] <= p0
+      while (hi - b > 1) {
+        const uint32_t mid = (b + hi) >> 1;
+        if (s_pre[mid] <= p0) b = mid; else hi = mid;
       }
-      sl[i] = j < n ? (lo << caplog) + (j - s_pre[lo]) : 0u;
-    }
+      uint32_t sl[LD], kb[LD];
 #pragma unroll
-    for (int i = 0; i < LD; ++i) kk[i] = okey[sl[i]];  // slot 0 always exists
+      for (int i = 0; i < LD; ++i) {
+        const uint32_t p = p0 + (uint32_t)i;
+        while (b + 1 < nb && s_pre[b + 1] <= p) ++b;
+        sl[i] = p < n ? (b << caplog) + (p - s_pre[b]) : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < LD; ++i) kb[i] = okey[sl[i]];  // slot 0 always exists
+#pragma unroll
+      for (int i = 0; i < LD; ++i)
+        if (p0 + (uint32_t)i < n) s_list[p0 + i] = kb[i];
+    }
+    __syncthreads();
+    uint32_t kk[LD];
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const uint32_t j = (uint32_t)i * OS_NT + (uint32_t)t;
+      kk[i] = j < n ? s_list[j] : 0u;
+    }
     uint32_t kmin = 0xffffffffu, kmax = 0u;
     sp_stamp(stamp, true, 1);
 #pragma unroll
@@ -1715,8 +1733,13 @@ __global__ __launch_bounds__(OS_NT) void k_sp_order_rank(const uint32_t* __restr
           r += (y + 3 >= bs && y + 3 < be && q[h].w < cp[i]) ? 1u : 0u;
         }
       }
-      if (r < m) {
-        const uint32_t s = sl[i];
+      if (r < m) {  // the bucket slot of position j (a few per workgroup: one search each)
+        uint32_t lo = 0, hi = nb;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_pre[mid] <= j) lo = mid; else hi = mid;
+        }
+        const uint32_t s = (lo << caplog) + (j - s_pre[lo]);
         go.out[r] = EdgeOut{cu[s], cw[s], cs[s]};
       }
     }
