@@ -227,6 +227,132 @@ __device__ __forceinline__ float hp_score(const HpArgs& a, uint32_t u, uint64_t 
   return hp_ordered_sum(a, u, w, n);
 }
 
+// ---------------------------------------------------------------- ordered AA / RA accumulation
+// The row kernels of bins 0 and 1 (k_hp_batch, k_hp_wave, k_hp_block) add the
+// Adamic-Adar / Resource-Allocation contributions in the reference's order
+// instead of re-walking intersections.  With a row's first hops in ascending v
+// (N(u) is sorted; the survivor lists S(u) are sorted in LDS first), the
+// flattened wedge index j runs in the order of predict.hxx:153-179 (v ascending
+// over N(u), then N(v)) for every w.  Wedges are taken in steps of one per
+// thread, j ascending with the thread index, steps one after another; within
+// a step, threads that hit the same entry add in thread order: each pending
+// thread posts a token (round << TB | reversed thread index) to the entry's
+// owner word with atomicMax, the winner -- the lowest pending thread of that
+// entry -- adds (float)((double)acc + c_v), the others retry in the next round
+// (one round unless a step holds the same w twice).  The table's count word
+// holds the float accumulator (the sign bit, HP_EXCL, is the exclusion mark: an
+// accumulator is never negative) and vmin the owner tokens (0 when free).
+__device__ __forceinline__ uint32_t ho_find(const HpTable& t, uint32_t mask, int shift, uint32_t key,
+                                            unsigned long long* err) {
+  uint32_t h = hp_hash(key, shift);
+  for (uint32_t probe = 0;; ++probe) {
+    if (probe > mask) { atomicOr(err, 1ull); return 0u; }
+    uint32_t cur = *(volatile uint32_t*)&t.k[h];
+    if (cur == HP_EMPTY) {
+      cur = atomicCAS(&t.k[h], HP_EMPTY, key);
+      if (cur == HP_EMPTY) cur = key;
+    }
+    if (cur == key) return h;
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ void ho_apply(const HpTable& t, uint32_t h, double c) {
+  const float a = __uint_as_float(*(volatile uint32_t*)&t.c[h]);
+  *(volatile uint32_t*)&t.c[h] = __float_as_uint((float)((double)a + c));
+}
+
+// one wave's step (every lane calls it; pend = this lane has a wedge)
+__device__ __forceinline__ void ho_add_wave(const HpTable& t, bool pend, uint32_t h, double c, uint32_t* round) {
+  const uint32_t lane = (uint32_t)lane_id();
+  while (__ballot(pend)) {
+    const uint32_t tok = (*round << 6) | (63u - lane);
+    if (pend) atomicMax(&t.vmin[h], tok);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    if (pend && *(volatile uint32_t*)&t.vmin[h] == tok) {
+      ho_apply(t, h, c);
+      pend = false;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    ++*round;
+  }
+}
+
+// one workgroup's step (HP_BNT = 1024 threads, every thread calls it)
+__device__ __forceinline__ void ho_add_block(const HpTable& t, bool pend, uint32_t h, double c, uint32_t* round) {
+  const uint32_t tid = threadIdx.x;
+  while (__syncthreads_or(pend)) {
+    const uint32_t tok = (*round << 10) | (1023u - tid);
+    if (pend) atomicMax(&t.vmin[h], tok);
+    __syncthreads();
+    if (pend && *(volatile uint32_t*)&t.vmin[h] == tok) {
+      ho_apply(t, h, c);
+      pend = false;
+    }
+    ++*round;
+  }
+}
+
+// Read entry i and reset it (key, accumulator, owner).
+__device__ __forceinline__ uint32_t ho_take(const HpTable& t, uint32_t i, uint32_t* c) {
+  const uint32_t w = *(volatile uint32_t*)&t.k[i];
+  if (w != HP_EMPTY) {
+    *c = *(volatile uint32_t*)&t.c[i];
+    *(volatile uint32_t*)&t.k[i] = HP_EMPTY;
+    *(volatile uint32_t*)&t.c[i] = 0u;
+    *(volatile uint32_t*)&t.vmin[i] = 0u;
+  }
+  return w;
+}
+
+// score of an ordered entry: 0 when w is in N(u) (predict.hxx:306-307), else the sum
+__device__ __forceinline__ float ho_score(uint32_t c) { return (c & HP_EXCL) ? 0.0f : __uint_as_float(c); }
+
+// Ascending bitonic sort of n (a power of two, >= 2) words in LDS by one wave.
+__device__ __forceinline__ void wave_bitonic_u32(uint32_t* s, uint32_t n) {
+  const uint32_t lane = (uint32_t)lane_id();
+  for (uint32_t k = 2; k <= n; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = lane; i < n / 2; i += 64) {
+        const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+        const uint32_t x = s[lo], y = s[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          s[lo] = y;
+          s[hi] = x;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+}
+
+// The same over a workgroup of HP_BNT threads.
+__device__ __forceinline__ void block_bitonic_u32(uint32_t* s, uint32_t n) {
+  for (uint32_t k = 2; k <= n; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n / 2; i += blockDim.x) {
+        const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+        const uint32_t x = s[lo], y = s[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          s[lo] = y;
+          s[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint32_t pow2_at_least(uint32_t n) {
+  uint32_t p = 2;
+  while (p < n) p <<= 1;
+  return p;
+}
+
 // ---------------------------------------------------------------- emission
 // Per-wave staging of emitted candidates in LDS: one global atomic per
 // HP_STG candidates instead of one per wave and iteration (a single counter
@@ -320,7 +446,8 @@ constexpr int HP_UN = 2;
 // LDS); f(w, v) for every wedge, HP_UN per lane in flight.  stride = the
 // threads sharing the block (64: a wave; HP_BNT: a workgroup), t = this
 // thread's index among them.
-template <int NS, typename IT, typename F>
+// ALL: f(ok, w, entry) on every thread (convergent; entry = the first-hop index).
+template <int NS, bool ALL = false, typename IT, typename F>
 __device__ __forceinline__ void hp_wedges(uint64_t total, uint32_t t, uint32_t stride, const IT* s_incl,
                                           const uint64_t* s_start, const uint32_t* s_iv, const uint32_t* keys, F f) {
   for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)stride * HP_UN) {
@@ -336,12 +463,14 @@ __device__ __forceinline__ void hp_wedges(uint64_t total, uint32_t t, uint32_t s
         if ((uint64_t)s_incl[m] > j) hi = m; else lo = m + 1;
       }
       const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
-      v[q] = s_iv[lo];
+      v[q] = ALL ? lo : s_iv[lo];
       w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
     }
 #pragma unroll
-    for (int q = 0; q < HP_UN; ++q)
-      if (ok[q]) f(w[q], v[q]);
+    for (int q = 0; q < HP_UN; ++q) {
+      if constexpr (ALL) f(ok[q], w[q], v[q]);
+      else if (ok[q]) f(w[q], v[q]);
+    }
   }
 }
 
@@ -365,7 +494,8 @@ __device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint3
 // 64): the slots of HP_UN rounds first (LDS or slab), then their degree loads
 // (count metrics) in flight together, then the scores; every thread of the
 // caller runs every round (hp_emit ballots per wave).
-template <bool GLOBAL, bool CUSTOM, int UN = HP_UN>
+// ORD: an ordered AA / RA table (LDS only, see ho_add_wave).
+template <bool GLOBAL, bool CUSTOM, int UN = HP_UN, bool ORD = false>
 __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
                                          const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
   for (uint32_t i0 = 0; i0 < T; i0 += stride * UN) {
@@ -374,7 +504,13 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
     for (int q = 0; q < UN; ++q) {
       const uint32_t i = i0 + (uint32_t)q * stride + t;
       c[q] = v0[q] = v1[q] = 0;
-      w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+      if (ORD) w[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
+      else w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+    }
+    if (ORD) {
+#pragma unroll
+      for (int q = 0; q < UN; ++q) hp_emit(sg, a, w[q] != HP_EMPTY, ho_score(c[q]), u, w[q], tau);
+      continue;
     }
     if (!CUSTOM) {
 #pragma unroll
@@ -665,6 +801,9 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
   __shared__ uint32_t s_iv[NWAVE][64];
   __shared__ uint32_t s_gu[NWAVE][STG], s_gw[NWAVE][STG];
   __shared__ float s_gs[NWAVE][STG];
+  constexpr int SK = CUSTOM ? TW / 2 : 1;  // AA / RA: S(u) sorted (|S(u)| <= W(u) <= TW / 2)
+  __shared__ uint32_t s_sk[NWAVE][SK];
+  __shared__ double s_ic[NWAVE][CUSTOM ? 64 : 1];
   const int lane = lane_id(), wv = wave_id();
   if (tcnt) {  // tier slice of the partitioned list
     uint32_t base = 0;
@@ -676,7 +815,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
   for (int i = lane; i < TW; i += 64) {
     s_k[wv][i] = HP_EMPTY;
     s_c[wv][i] = 0;
-    if (CUSTOM) { s_v0[wv][i] = HP_EMPTY; s_v1[wv][i] = 0; }
+    if (CUSTOM) s_v0[wv][i] = 0;  // owner tokens (ordered accumulation)
   }
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
   const int64_t tau = *a.tau;
@@ -697,31 +836,59 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
     const uint32_t* fh;
     uint64_t nf;
     hp_first_hops(a, u, o0, du, &fh, &nf);
+    if (CUSTOM && a.soff) {  // S(u) is unordered: sort it (N(u) already is)
+      if (nf > (uint64_t)SK) {
+        if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+        continue;
+      }
+      const uint32_t n2 = pow2_at_least((uint32_t)nf);
+      for (uint32_t e = (uint32_t)lane; e < n2; e += 64) s_sk[wv][e] = e < nf ? fh[e] : 0xffffffffu;
+      wave_sync_lds();
+      wave_bitonic_u32(s_sk[wv], n2);
+      fh = s_sk[wv];
+    }
+    uint32_t round = 0;
     for (uint64_t base = 0; base < nf; base += 64) {
       const uint64_t i = base + lane;
       uint32_t len = 0, v = 0;
       uint64_t st = 0;
+      double cv = 0.0;
       if (i < nf) {
         v = fh[i];
         const uint32_t d = a.g.deg[v];
         if (hp_surv(d, a.H)) {
           len = d;
           st = a.g.off[v];
+          if (CUSTOM) cv = a.g.ctab[d];
         }
       }
       const uint32_t incl = (uint32_t)wave_incl_scan(len);
       s_incl[wv][lane] = incl;
       s_start[wv][lane] = st;
       s_iv[wv][lane] = v;
+      if (CUSTOM) s_ic[wv][lane] = cv;
       wave_sync_lds();
       const uint32_t total = __shfl(incl, 63, 64);
-      hp_wedges<64>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
-                    [&](uint32_t w, uint32_t v) {
-                      if (w > u) {
-                        ++wedges;
-                        hp_insert<false, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
-                      }
-                    });
+      if constexpr (CUSTOM) {
+        hp_wedges<64, true>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                            [&](bool ok, uint32_t w, uint32_t ent) {
+                              const bool in = ok && w > u;
+                              uint32_t h = 0;
+                              if (in) {
+                                ++wedges;
+                                h = ho_find(tb, mask, shift, w, &a.ctr[HPC_ERR]);
+                              }
+                              ho_add_wave(tb, in, h, s_ic[wv][ent], &round);
+                            });
+      } else {
+        hp_wedges<64>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                      [&](uint32_t w, uint32_t v) {
+                        if (w > u) {
+                          ++wedges;
+                          hp_insert<false, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
+                        }
+                      });
+      }
       wave_sync_lds();
     }
     // first-order exclusion (predict.hxx:306-307)
@@ -729,7 +896,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       if (x > u) hp_mark<false>(tb, mask, shift, x);
     });
     wave_sync_lds();
-    hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
+    hp_drain<false, CUSTOM, 8, CUSTOM>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -786,7 +953,8 @@ __global__ void k_hp_batch_starts(const uint64_t* __restrict__ bpre, const uint3
 }
 
 // hp_wedges with the first-hop entry's index: f(w, v, entry), UN keys per lane in flight
-template <int UN, typename IT, typename F>
+// (ALL: f(ok, w, v, entry) on every lane, wave-convergent, for the ordered accumulation)
+template <int UN, bool ALL = false, typename IT, typename F>
 __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* s_incl, const uint64_t* s_start,
                                           const uint32_t* s_iv, const uint32_t* keys, F f) {
   for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * UN) {
@@ -806,8 +974,10 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
       w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
     }
 #pragma unroll
-    for (int q = 0; q < UN; ++q)
-      if (ok[q]) f(w[q], v[q], e[q]);
+    for (int q = 0; q < UN; ++q) {
+      if constexpr (ALL) f(ok[q], w[q], v[q], e[q]);
+      else if (ok[q]) f(w[q], v[q], e[q]);
+    }
   }
 }
 
@@ -846,6 +1016,9 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
   __shared__ uint32_t s_np[NWAVE][64];
   __shared__ uint32_t s_gu[NWAVE][STG], s_gw[NWAVE][STG];
   __shared__ float s_gs[NWAVE][STG];
+  constexpr int SK = CUSTOM ? TW / 2 : 1;  // AA / RA: the batch's first hops (slot << wbits | v), sorted
+  __shared__ uint32_t s_sk[NWAVE][SK];
+  __shared__ double s_ic[NWAVE][CUSTOM ? 64 : 1];
   const int lane = lane_id(), wv = wave_id();
   uint32_t base, cnt;
   hb_region(tcnt, tlo, thi, &base, &cnt);
@@ -856,8 +1029,9 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
   for (int i = lane; i < TW; i += 64) {
     s_k[wv][i] = HP_EMPTY;
     s_c[wv][i] = 0;
-    if (CUSTOM) { s_v0[wv][i] = HP_EMPTY; s_v1[wv][i] = 0; }
+    if (CUSTOM) s_v0[wv][i] = 0;  // owner tokens
   }
+  uint32_t round = 0;
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
@@ -921,19 +1095,48 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       continue;
     }
     const int shift = 32 - lg;
+    if (CUSTOM) {
+      // AA / RA: the batch's first hops sorted by (slot, v) -- S(u) is unordered
+      // -- so that the wedge steps run in the reference's order of additions
+      if (NS > (uint32_t)SK) {  // more first hops than wedges (a budget bug): fail the call
+        if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+        nr = 0;
+        continue;
+      }
+      const uint32_t n2 = pow2_at_least(NS);
+      for (uint32_t e = (uint32_t)lane; e < n2; e += 64) {
+        uint32_t key = 0xffffffffu;
+        if (e < NS) {
+          const uint32_t slot = hb_slot(s_sp[wv], nr, e);
+          const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
+          key = (slot << wbits) | a.skeys[s_s0[wv][slot] + (e - ex)];
+        }
+        s_sk[wv][e] = key;
+      }
+      wave_sync_lds();
+      wave_bitonic_u32(s_sk[wv], n2);
+    }
     // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
     for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
       const uint32_t e = e0 + (uint32_t)lane;
       uint32_t len = 0, v = 0, slot = 0;
       uint64_t st = 0;
+      double cv = 0.0;
       if (e < NS) {
-        slot = hb_slot(s_sp[wv], nr, e);
-        const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
-        v = a.skeys[s_s0[wv][slot] + (e - ex)];
+        if (CUSTOM) {
+          const uint32_t key = s_sk[wv][e];
+          slot = key >> wbits;
+          v = key & wmask;
+        } else {
+          slot = hb_slot(s_sp[wv], nr, e);
+          const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
+          v = a.skeys[s_s0[wv][slot] + (e - ex)];
+        }
         const uint32_t d = a.g.deg[v];
         if (hp_surv(d, a.H)) {
           len = d;
           st = a.g.off[v];
+          if (CUSTOM) cv = a.g.ctab[d];
         }
       }
       const uint32_t incl = (uint32_t)wave_incl_scan(len);
@@ -941,16 +1144,31 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       s_start[wv][lane] = st;
       s_iv[wv][lane] = v;
       s_islot[wv][lane] = slot;
+      if (CUSTOM) s_ic[wv][lane] = cv;
       wave_sync_lds();
       const uint32_t total = __shfl(incl, 63, 64);
-      hb_wedges<HB_UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
-                [&](uint32_t w, uint32_t vv, uint32_t ent) {
-                  const uint32_t sl = s_islot[wv][ent];
-                  if (w > s_u[wv][sl]) {
-                    ++wedges;
-                    hp_insert<false, CUSTOM>(tb, mask, shift, (sl << wbits) | w, vv, &a.ctr[HPC_ERR]);
-                  }
-                });
+      if constexpr (CUSTOM) {
+        hb_wedges<HB_UN, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                               [&](bool ok, uint32_t w, uint32_t, uint32_t ent) {
+                                 const uint32_t sl = s_islot[wv][ent];
+                                 const bool in = ok && w > s_u[wv][sl];
+                                 uint32_t h = 0;
+                                 if (in) {
+                                   ++wedges;
+                                   h = ho_find(tb, mask, shift, (sl << wbits) | w, &a.ctr[HPC_ERR]);
+                                 }
+                                 ho_add_wave(tb, in, h, s_ic[wv][ent], &round);
+                               });
+      } else {
+        hb_wedges<HB_UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                         [&](uint32_t w, uint32_t vv, uint32_t ent) {
+                           const uint32_t sl = s_islot[wv][ent];
+                           if (w > s_u[wv][sl]) {
+                             ++wedges;
+                             hp_insert<false, CUSTOM>(tb, mask, shift, (sl << wbits) | w, vv, &a.ctr[HPC_ERR]);
+                           }
+                         });
+      }
       wave_sync_lds();
     }
     pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
@@ -984,7 +1202,8 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       for (int q = 0; q < HB_UN; ++q) {
         const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
         c[q] = v0[q] = v1[q] = 0;
-        kq[q] = i < T ? hp_take<false, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+        if (CUSTOM) kq[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
+        else kq[q] = i < T ? hp_take<false, false>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
       }
       if (!CUSTOM) {
 #pragma unroll
@@ -998,13 +1217,14 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
         const uint64_t du2 = s_du[wv][sl];
         float s = 0.0f;
         if (valid) {
-          if (CUSTOM) s = hp_score<true>(a, uu, du2, w, c[q], v0[q], v1[q]);
+          if (CUSTOM) s = ho_score(c[q]);
           else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & HP_CMASK), du2, (uint64_t)dw[q]);
         }
         hp_emit(sg, a, valid, s, uu, w, tau);
       }
     }
     wave_sync_lds();
+    round = 0;  // every owner word of the batch is free again
     r0 = pr0;
     nr = pnr;
     u = pu;
@@ -1066,6 +1286,11 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
   __shared__ uint64_t s_it;
+  // AA / RA in LDS: ordered accumulation (see ho_add_block) over S(u) sorted here
+  constexpr bool ORD = CUSTOM && !GLOBAL;
+  constexpr int SK = ORD ? LT / 2 : 1;
+  __shared__ uint32_t s_sk[SK];
+  __shared__ double s_ic[ORD ? HP_BNT : 1];
   const int t = threadIdx.x, wv = wave_id();
   const uint64_t tmax = GLOBAL ? (1ull << tlog) : (uint64_t)LT;
   HpTable tb;
@@ -1079,7 +1304,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
     for (int i = t; i < LT; i += HP_BNT) {
       s_k[i] = HP_EMPTY;
       s_c[i] = 0;
-      if (CUSTOM) { s_v0[i] = HP_EMPTY; s_v1[i] = 0; }
+      if (CUSTOM) s_v0[i] = 0;  // owner tokens
     }
   }
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
@@ -1113,47 +1338,74 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
     const uint32_t T = 1u << lg, mask = T - 1;
     const int shift = 32 - lg;
     const uint64_t rw = (span_w + passes - 1) / passes;
+    const uint32_t* fh;
+    uint64_t nf;
+    hp_first_hops(a, u, o0, du, &fh, &nf);
+    if (ORD && a.soff) {  // S(u) is unordered: sort it (N(u) already is)
+      if (nf > (uint64_t)SK) {
+        if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+        continue;  // uniform: nf is the workgroup's row
+      }
+      const uint32_t n2 = pow2_at_least((uint32_t)nf);
+      for (uint32_t e = (uint32_t)t; e < n2; e += HP_BNT) s_sk[e] = e < nf ? fh[e] : 0xffffffffu;
+      __syncthreads();
+      block_bitonic_u32(s_sk, n2);
+      fh = s_sk;
+    }
+    uint32_t round = 0;
     for (uint64_t p = 0; p < passes; ++p) {
       const uint64_t wlo = (uint64_t)u + 1 + p * rw;
       const uint64_t whi = wlo + rw < a.S ? wlo + rw : a.S;
-      const uint32_t* fh;
-      uint64_t nf;
-      hp_first_hops(a, u, o0, du, &fh, &nf);
       for (uint64_t base = 0; base < nf; base += HP_BNT) {
         const uint64_t i = base + t;
         uint32_t v = 0;
         uint64_t len = 0, st = 0;
+        double cv = 0.0;
         if (i < nf) {
           v = fh[i];
           const uint32_t d = a.g.deg[v];
           if (hp_surv(d, a.H)) {
             len = d;
             st = a.g.off[v];
+            if (ORD) cv = a.g.ctab[d];
           }
         }
         const uint64_t incl = block_incl_scan_1024(len, s_w);
         s_incl[t] = incl;
         s_start[t] = st;
         s_iv[t] = v;
+        if (ORD) s_ic[t] = cv;
         if (t == HP_BNT - 1) s_tot = incl;
         hp_sync<GLOBAL>();
         const uint64_t total = s_tot;
-        hp_wedges<HP_BNT>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
-                          [&](uint32_t w, uint32_t v) {
-                            if (w > u) {
-                              if (p == 0) ++wedges;
-                              if ((uint64_t)w >= wlo && (uint64_t)w < whi)
-                                hp_insert<GLOBAL, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
-                            }
-                          });
+        if constexpr (ORD) {
+          hp_wedges<HP_BNT, true>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
+                                  [&](bool ok, uint32_t w, uint32_t ent) {
+                                    const bool in = ok && w > u && (uint64_t)w >= wlo && (uint64_t)w < whi;
+                                    if (ok && w > u && p == 0) ++wedges;
+                                    uint32_t h = 0;
+                                    if (in) h = ho_find(tb, mask, shift, w, &a.ctr[HPC_ERR]);
+                                    ho_add_block(tb, in, h, s_ic[ent], &round);
+                                  });
+        } else {
+          hp_wedges<HP_BNT>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
+                            [&](uint32_t w, uint32_t v) {
+                              if (w > u) {
+                                if (p == 0) ++wedges;
+                                if ((uint64_t)w >= wlo && (uint64_t)w < whi)
+                                  hp_insert<GLOBAL, CUSTOM>(tb, mask, shift, w, v, &a.ctr[HPC_ERR]);
+                              }
+                            });
+        }
         hp_sync<GLOBAL>();
       }
       hp_stream(a.g.keys + o0, du, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
         if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
       });
       hp_sync<GLOBAL>();
-      hp_drain<GLOBAL, CUSTOM>(tb, T, (uint32_t)t, (uint32_t)HP_BNT, sg, a, u, du, tau);
+      hp_drain<GLOBAL, CUSTOM, HP_UN, ORD>(tb, T, (uint32_t)t, (uint32_t)HP_BNT, sg, a, u, du, tau);
       hp_sync<GLOBAL>();
+      round = 0;
     }
   }
   hp_finish(sg, a, wedges);
