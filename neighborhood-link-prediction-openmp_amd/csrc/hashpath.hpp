@@ -69,6 +69,7 @@ struct HpArgs {
   const uint64_t* soff;  // [nU + 1], indexed by u - sua
   const uint32_t* skeys;
   uint64_t sua;
+  int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
 };
 
 // A row's first-hop list: S(u) when the survivor lists exist, else N(u).
@@ -621,6 +622,124 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
   }
 }
 
+// ---------------------------------------------------------------- survivor lists by degree classes
+// Per graph: dcls[e] = min(deg keys[e], 255).  For H <= HP_DCLS_MAX the
+// survivor lists S(u) = {v in N(u): 1 <= deg v <= H} of a range are the stream
+// compaction of its entries by dcls -- coalesced bytes, no atomics, and S(u)
+// keeps N(u)'s ascending order (the AA / RA row kernels then need no sort).
+//   k_hp_dcls_rows: per row (cnt << 40 | W) packed into wu, per tile its count
+//   k_hp_unpack:    wu -> W(u), cnt -> |S(u)| (scanned into soff by the caller)
+//   k_hp_dcls_fill: per tile, the surviving keys at the scanned tile offsets
+// (deg u < 2^24 is required at graph build, so the packed count cannot carry
+// into W's 40 bits: W <= 254 deg u).
+constexpr uint32_t HP_DCLS_MAX = 254;
+
+__global__ void k_hp_dcls(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg, uint64_t M,
+                          uint8_t* __restrict__ out) {
+  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = deg[keys[e]];
+    out[e] = (uint8_t)(d < 255u ? d : 255u);
+  }
+}
+
+__device__ __forceinline__ bool hp_dsurv(uint32_t c, uint32_t H) { return c >= 1 && c <= H; }
+
+__global__ __launch_bounds__(NT) void k_hp_dcls_rows(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                     uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                     const uint32_t* __restrict__ tile_row,
+                                                     unsigned long long* __restrict__ wu, uint32_t* __restrict__ tcnt) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  s_acc[wv][lane] = 0;
+  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t tr = tile_row[tile];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;  // first row of the tile inside the range
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < nU ? g.off[ua + rl + 1] : ~0ull;  // end of row r0 + lane
+    const uint64_t last_end = __shfl(rend, 63, 64);
+    uint32_t c[HP_WR];
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      c[i] = e >= e0 && e < e1 ? (uint32_t)dcls[e] : 0u;
+      c[i] = hp_dsurv(c[i], H) ? c[i] : 0u;
+    }
+    uint32_t tc = 0;
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      tc += (uint32_t)__popcll(__ballot(c[i] != 0));
+      int lo = 0, hi = 64;  // local row: the number of the 64 row ends <= e
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        const uint64_t v = __shfl(rend, m, 64);
+        if (v <= e) lo = m + 1; else hi = m;
+      }
+      if (c[i] == 0) continue;
+      const unsigned long long add = (1ull << 40) | c[i];
+      if (e < last_end) {
+        atomicAdd(&s_acc[wv][lo], add);
+      } else {  // more than 64 rows in this tile: search the offsets
+        uint64_t a = r0, b = nU;
+        while (b - a > 1) {
+          const uint64_t m = (a + b) >> 1;
+          if (g.off[ua + m] <= e) a = m; else b = m;
+        }
+        atomicAdd(&wu[a], add);
+      }
+    }
+    if (lane == 0) tcnt[tile - t0] = tc;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const unsigned long long v = s_acc[wv][lane];
+    if (v) {
+      atomicAdd(&wu[rl], v);
+      s_acc[wv][lane] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  }
+}
+
+__global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __restrict__ cnt, uint64_t nU) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nU; r += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long x = wu[r];
+    cnt[r] = (uint32_t)(x >> 40);
+    wu[r] = x & ((1ull << 40) - 1);
+  }
+}
+
+// tpre: exclusive prefix of the tile counts (tile - t0 indexed)
+__global__ __launch_bounds__(NT) void k_hp_dcls_fill(const uint32_t* __restrict__ keys,
+                                                     const uint8_t* __restrict__ dcls, uint32_t H, uint64_t e0,
+                                                     uint64_t e1, const uint64_t* __restrict__ tpre,
+                                                     uint32_t* __restrict__ skeys) {
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    uint64_t pos = tpre[tile - t0];
+    uint32_t c[HP_WR];
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      c[i] = e >= e0 && e < e1 ? (uint32_t)dcls[e] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      const bool s = hp_dsurv(c[i], H);
+      const uint64_t m = __ballot(s);
+      if (s) skeys[pos + (uint64_t)__popcll(m & ((1ull << lane) - 1))] = keys[e];
+      pos += (uint64_t)__popcll(m);
+    }
+  }
+}
+
 // The same W(u) from the survivors' side, for small H: the surviving
 // intermediates are a prefix of the degree-class index (vbydeg, degrees 1..H),
 // and every entry u of I(v) (the transposed multiset: one per occurrence of v
@@ -836,7 +955,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
     const uint32_t* fh;
     uint64_t nf;
     hp_first_hops(a, u, o0, du, &fh, &nf);
-    if (CUSTOM && a.soff) {  // S(u) is unordered: sort it (N(u) already is)
+    if (CUSTOM && a.soff && !a.ssorted) {  // S(u) from in-edge atomics is unordered: sort it
       if (nf > (uint64_t)SK) {
         if (lane == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
         continue;
@@ -1114,7 +1233,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
         s_sk[wv][e] = key;
       }
       wave_sync_lds();
-      wave_bitonic_u32(s_sk[wv], n2);
+      if (!a.ssorted) wave_bitonic_u32(s_sk[wv], n2);
     }
     // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
     for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
@@ -1341,7 +1460,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
     const uint32_t* fh;
     uint64_t nf;
     hp_first_hops(a, u, o0, du, &fh, &nf);
-    if (ORD && a.soff) {  // S(u) is unordered: sort it (N(u) already is)
+    if (ORD && a.soff && !a.ssorted) {  // S(u) from in-edge atomics is unordered: sort it
       if (nf > (uint64_t)SK) {
         if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
         continue;  // uniform: nf is the workgroup's row
@@ -1870,11 +1989,17 @@ __global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, const uint32_t* __r
 // is bounded by its width instead).  The items of a heavy bucket run on
 // different workgroups, each streaming the bucket's scratch and keeping its
 // own w-range.
+// AA / RA sort mode (wcap = HH_SCAP): items hold at most HH_SCAP wedges, which
+// k_hh_accum sorts by (w, v) in LDS and sums run by run in ascending v; a single
+// fine range beyond HH_SCAP wedges is cut by width and flagged HH_BIG (hash
+// table with the ordered re-walk of hp_ordered_sum).
 struct HhItem {
-  uint32_t gb, cnt;   // bucket, distinct-w bound of the range
+  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG)
   uint64_t slo, shi;  // w-range
 };
 constexpr uint32_t HH_FINE = 4096;
+constexpr uint32_t HH_SCAP = 4096;         // sort-mode wedges per item (32 KB of u64 keys)
+constexpr uint32_t HH_BIG = 0x80000000u;
 
 __device__ __forceinline__ uint64_t hh_bucket_range(const HpArgs& a, uint32_t u, uint32_t shift, uint64_t b,
                                                     uint64_t* lo) {
@@ -1894,10 +2019,13 @@ __device__ __forceinline__ uint32_t hh_wave_append(bool want, uint32_t* ctr) {
   return base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
 }
 
+// wcap > 0 (AA / RA sort mode, see k_hh_accum): items are bounded by their
+// wedge count (<= wcap) instead of their distinct-w bound.
 __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
                           const uint32_t* __restrict__ hr_shift, const uint64_t* __restrict__ bbase,
                           const uint32_t* __restrict__ bcnt, int tl, HhItem* __restrict__ items,
-                          uint32_t* __restrict__ nitems, uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy) {
+                          uint32_t* __restrict__ nitems, uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy,
+                          uint32_t wcap) {
   for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t gb = b0 + threadIdx.x;
     uint32_t n = 0;
@@ -1908,7 +2036,7 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
       width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
     }
     const uint64_t dist = (uint64_t)n < width ? (uint64_t)n : width;
-    const bool simple = n > 0 && 2 * dist <= (1ull << tl), hv = n > 0 && !simple;
+    const bool simple = n > 0 && (wcap ? n <= wcap : 2 * dist <= (1ull << tl)), hv = n > 0 && !simple;
     const uint32_t i = hh_wave_append(simple, nitems);
     if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};
     const uint32_t j = hh_wave_append(hv, nheavy);
@@ -1923,11 +2051,12 @@ __global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __
                                                     const uint64_t* __restrict__ bbase, const uint32_t* __restrict__ bcnt,
                                                     const uint64_t* __restrict__ boff, const uint32_t* __restrict__ sw,
                                                     int tl, HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
-                                                    uint64_t cap) {
+                                                    uint64_t cap, uint32_t wcap) {
   __shared__ uint32_t s_h[HH_FINE];
   const int t = threadIdx.x;
   const uint32_t nh = *nheavy;
-  const uint64_t half = 1ull << (tl - 1);
+  const uint64_t th = 1ull << (tl - 1);        // distinct w per table
+  const uint64_t half = wcap ? wcap : th;      // wedges per group
   for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
     const uint32_t gb = heavy[hi];
     const uint32_t n = bcnt[gb];
@@ -1946,16 +2075,16 @@ __global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __
         if (slo >= shi) return;
         const uint64_t span = shi - slo;
         const uint64_t dist = cnt < span ? cnt : span;
-        if (2 * dist <= 2 * half) {
+        if (wcap ? cnt <= wcap : dist <= th) {
           const uint32_t i = atomicAdd(nitems, 1u);
           if (i < cap) items[i] = HhItem{gb, (uint32_t)dist, slo, shi};
           else atomicOr(&a.ctr[HPC_ERR], 4ull);
           return;
         }
-        for (uint64_t x = slo; x < shi; x += half) {  // one fine range beyond the table: by width
-          const uint64_t x1 = x + half < shi ? x + half : shi;
+        for (uint64_t x = slo; x < shi; x += th) {  // one fine range beyond the table: by width
+          const uint64_t x1 = x + th < shi ? x + th : shi;
           const uint32_t i = atomicAdd(nitems, 1u);
-          if (i < cap) items[i] = HhItem{gb, (uint32_t)(x1 - x), x, x1};
+          if (i < cap) items[i] = HhItem{gb, (uint32_t)(x1 - x) | (wcap ? HH_BIG : 0u), x, x1};
           else atomicOr(&a.ctr[HPC_ERR], 4ull);
         }
       };
@@ -1982,6 +2111,32 @@ __global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __
   }
 }
 
+// Ascending bitonic sort of n (a power of two, >= 2) u64 keys in LDS by the workgroup.
+template <int NTH>
+__device__ __forceinline__ void block_bitonic_u64(uint64_t* s, uint32_t n) {
+  for (uint32_t k = 2; k <= n; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n / 2; i += NTH) {
+        const uint32_t lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+        const uint64_t x = s[lo], y = s[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          s[lo] = y;
+          s[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// Sort-mode keys: (w - slo) << 38 | v << 12 | min(deg v, 4095) (w - slo, v < 2^26)
+constexpr int HS_WSH = 38;
+constexpr uint32_t HS_DMAX = 4095;
+
+// sortmode (AA / RA, items of at most HH_SCAP wedges unless flagged HH_BIG): an
+// item's wedges are loaded as (w, v, deg v) keys into LDS (over the vmin / vmax
+// words of the hash table), sorted, and every run of equal w summed by its
+// first thread in ascending v -- the additions of predict.hxx:788 / 828 in the
+// reference's order; the exclusion marks the run of each x in N(u).
 template <bool CUSTOM>
 __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __restrict__ items,
                                                     const uint32_t* __restrict__ nitems,
@@ -1992,18 +2147,23 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
                                                     const uint64_t* __restrict__ bbase,
                                                     const uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
                                                     const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw,
-                                                    const uint32_t* __restrict__ sv, uint32_t* __restrict__ queue) {
+                                                    const uint32_t* __restrict__ sv, uint32_t* __restrict__ queue,
+                                                    int sortmode) {
   constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
   constexpr int LT = 1 << TL;
   constexpr int VT = CUSTOM ? LT : 1;
+  static_assert(!CUSTOM || LT >= (int)HH_SCAP, "the sort buffer overlays the vmin / vmax words");
   __shared__ uint32_t s_k[LT];
   __shared__ uint32_t s_c[LT];
-  __shared__ uint32_t s_v0[VT];
-  __shared__ uint32_t s_v1[VT];
+  __shared__ uint64_t s_vv[VT];  // vmin | vmax (2 x LT u32), or the sort-mode keys (LT u64)
+  __shared__ uint8_t s_ex[CUSTOM ? HH_SCAP : 1];
   __shared__ uint32_t s_gu[HH_NW][HP_BSTG], s_gw[HH_NW][HP_BSTG];
   __shared__ float s_gs[HH_NW][HP_BSTG];
   __shared__ uint64_t s_it;
+  __shared__ uint32_t s_n;
   const int t = threadIdx.x, wv = wave_id();
+  uint32_t* const s_v0 = (uint32_t*)s_vv;
+  uint32_t* const s_v1 = (uint32_t*)s_vv + (CUSTOM ? LT : 0);
   const HpTable tb{s_k, s_c, s_v0, s_v1};
   for (int i = t; i < LT; i += HH_NT) {
     s_k[i] = HP_EMPTY;
@@ -2035,7 +2195,87 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     const uint64_t o1 = a.g.off[u + 1];
     const uint64_t du = o1 - a.g.off[u];
     const uint64_t x0 = xs[gb], x1 = b + 1 < hr_p[r] ? xs[gb + 1] : o1;  // N(u) entries in the bucket
-    const int lg = max(6, log2_ceil(2 * (uint64_t)item.cnt));
+    if (CUSTOM && sortmode && !(item.cnt & HH_BIG)) {
+      uint64_t* const sk = s_vv;
+      if (t == 0) s_n = 0;
+      __syncthreads();
+      for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+        uint32_t wq[HP_UN], vq[HP_UN], dq[HP_UN];
+        bool in[HP_UN];
+#pragma unroll
+        for (int k = 0; k < HP_UN; ++k) {
+          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+          const uint64_t p = off + (i < n ? i : 0u);
+          wq[k] = sw[p];
+          vq[k] = sv[p];
+        }
+#pragma unroll
+        for (int k = 0; k < HP_UN; ++k) {
+          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+          in[k] = i < n && (whole || ((uint64_t)wq[k] >= slo && (uint64_t)wq[k] < shi));
+          dq[k] = in[k] ? a.g.deg[vq[k]] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < HP_UN; ++k) {
+          const uint32_t pos = hh_wave_append(in[k], &s_n);  // one LDS atomic per wave
+          if (in[k]) {
+            ++wedges;
+            if (pos < HH_SCAP)
+              sk[pos] = ((uint64_t)wq[k] - slo) << HS_WSH | (uint64_t)vq[k] << 12 |
+                        (dq[k] < HS_DMAX ? dq[k] : HS_DMAX);
+            else
+              atomicOr(&a.ctr[HPC_ERR], 8ull);
+          }
+        }
+      }
+      __syncthreads();
+      const uint32_t m = s_n < HH_SCAP ? s_n : HH_SCAP;
+      const uint32_t m2 = pow2_at_least(m);
+      for (uint32_t i = m + t; i < m2; i += HH_NT) sk[i] = ~0ull;
+      for (uint32_t i = t; i < m2; i += HH_NT) s_ex[i] = 0;
+      __syncthreads();
+      block_bitonic_u64<HH_NT>(sk, m2);
+      // first-order exclusion: the run of every x in N(u) within [slo, shi)
+      hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
+        if ((uint64_t)x >= slo && (uint64_t)x < shi) {
+          const uint64_t xl = (uint64_t)x - slo;
+          uint32_t l = 0, h = m;
+          while (l < h) {
+            const uint32_t md = (l + h) >> 1;
+            if ((sk[md] >> HS_WSH) < xl) l = md + 1; else h = md;
+          }
+          if (l < m && (sk[l] >> HS_WSH) == xl) s_ex[l] = 1;
+        }
+      });
+      __syncthreads();
+      for (uint32_t i0 = 0; i0 < m2; i0 += HH_NT) {
+        const uint32_t i = i0 + (uint32_t)t;
+        const bool start = i < m && (i == 0 || (sk[i] >> HS_WSH) != (sk[i - 1] >> HS_WSH));
+        float s = 0.0f;
+        uint32_t w = 0;
+        if (start) {
+          const uint64_t wl = sk[i] >> HS_WSH;
+          float acc = 0.0f;
+          for (uint32_t j = i; j < m && (sk[j] >> HS_WSH) == wl; ++j) {
+            uint32_t d = (uint32_t)(sk[j] & 0xfffu);
+            if (d == HS_DMAX) d = a.g.deg[(uint32_t)(sk[j] >> 12) & 0x3ffffffu];
+            acc = (float)((double)acc + a.g.ctab[d]);
+          }
+          s = s_ex[i] ? 0.0f : acc;
+          w = (uint32_t)(slo + wl);
+        }
+        hp_emit(sg, a, start, s, u, w, tau);
+      }
+      __syncthreads();
+      for (int i = t; i < LT; i += HH_NT) {  // the hash-table words under the buffer
+        s_v0[i] = HP_EMPTY;
+        s_v1[i] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t dcnt = item.cnt & ~HH_BIG;
+    const int lg = max(6, log2_ceil(2 * (uint64_t)dcnt));
     const uint32_t T = 1u << (lg < TL ? lg : TL), mask = T - 1;
     const int hs = 32 - (lg < TL ? lg : TL);
     for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {

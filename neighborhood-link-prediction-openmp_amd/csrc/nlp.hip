@@ -74,6 +74,7 @@ enum Buf {
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
+  B_HP_TCNT, B_HP_TPRE,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
   NBUF
 };
@@ -236,6 +237,7 @@ struct nlp_graph {
   // hash path: per-workgroup global tables of bins 2 and 3 (kept clean between calls)
   uint32_t* hp_scratch = nullptr;              // k_hp_part: per-workgroup wedge scratch (w and v)
   uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
+  uint8_t* dcls = nullptr;                     // min(deg keys[e], 255) per adjacency entry (path 4's survivor lists)
   // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
   uint64_t* truth = nullptr;
   uint64_t ntruth = 0;
@@ -253,6 +255,8 @@ struct nlp_graph {
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
+  bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
+  uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
   int hp_hub_min = 2;        // lowest bin the hub pass takes (NLP_HASH_HUB_MIN=1: bin 1 too)
   bool hp_hub = true;        // path 4: bins 2 / 3 by the hub pass (k_hh_*; NLP_HASH_HUB=0: k_hp_part)
@@ -262,6 +266,7 @@ struct nlp_graph {
   bool os_sort = false;
   bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
+  bool hp_dcls = true;       // survivor lists by filtering N(u) with the degree classes (NLP_HASH_DCLS=0: in-edge atomics)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
@@ -362,6 +367,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->d_stamp) (void)hipFree(g->d_stamp);
   if (g->hp_scratch) (void)hipFree(g->hp_scratch);
   if (g->tile_row) (void)hipFree(g->tile_row);
+  if (g->dcls) (void)hipFree(g->dcls);
   if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
@@ -541,6 +547,18 @@ nlp_status finish_graph(nlp_graph* g) {
   TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
   LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
   TRY(hipGetLastError());
+  // degree class of every adjacency entry: path 4 filters N(u) by it (coalesced
+  // bytes instead of a degree gather per entry) to build the survivor lists S(u)
+  const char* hdc = getenv("NLP_HASH_DCLS");
+  if (M > 0 && !(hdc && hdc[0] == '0') && g->maxdeg < (1u << 24)) {
+    if (hipMalloc(&g->dcls, M) == hipSuccess) {
+      LAUNCH(k_hp_dcls, M, st, (const uint32_t*)g->keys, (const uint32_t*)g->deg, M, g->dcls);
+      TRY(hipGetLastError());
+    } else {
+      (void)hipGetLastError();
+      g->dcls = nullptr;
+    }
+  }
   // Exact membership table of the entries w > u for the first-order exclusion
   // (kernels.hpp et_has): one 64-byte bucket read per candidate instead of a
   // search of N(u).  At most half full; skipped (NLP_ETAB=0, or when it would
@@ -662,6 +680,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
   if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
   if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
+  if (const char* hd = getenv("NLP_HASH_DCLS")) g->hp_dcls = hd[0] != '0';
   if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
   if (const char* os = getenv("NLP_OS_SORT")) g->os_sort = os[0] == '1';
   if (const char* hb = getenv("NLP_HASH_BATCH")) g->hp_batch = hb[0] != '0';
@@ -669,6 +688,9 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hm = getenv("NLP_HASH_HUB_MIN")) g->hp_hub_min = std::max(1, std::min(2, atoi(hm)));
   if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
+  if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
+  if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
+    g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
   if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
@@ -1565,17 +1587,19 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   TRY(hipGetLastError());
   // accumulation items (k_hh_plan, k_hh_split): a bucket, or a w-range of a heavy bucket
   const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
-  const uint64_t cap = NB + 3 * (tot >> (tl - 2)) + 1024;
+  // AA / RA: sort-mode items (at most HH_SCAP wedges each, keys need w, v < 2^26)
+  const uint32_t wcap = custom && g->hh_sort && g->span <= (1ull << 26) ? g->hh_scap : 0u;
+  const uint64_t cap = 2 * NB + 3 * (tot >> (tl - 2)) + 1024;
   HhItem* items;
   uint32_t* heavy = bcur;  // the cursors are done with
   uint32_t* nitems = queue + 1;  // and queue + 2: the heavy count
   TRY(wsget(ws, B_HH_SITEM, cap * sizeof(HhItem) / 8 + 1, (uint64_t**)&items));
   TRY(hipMemsetAsync(queue, 0, 12, st));
   LAUNCH(k_hh_plan, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
-         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, queue + 2);
+         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, queue + 2, wcap);
   hipLaunchKernelGGL(k_hh_split, dim3(512), dim3(HH_NT), 0, st, a, (const uint32_t*)heavy, (const uint32_t*)(queue + 2),
                      (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint64_t*)bbase,
-                     (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint32_t*)sw, tl, items, nitems, cap);
+                     (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint32_t*)sw, tl, items, nitems, cap, wcap);
   TRY(hipGetLastError());
   const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
   if (custom)
@@ -1583,13 +1607,13 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue);
+                       (const uint32_t*)sv, queue, (int)(wcap != 0));
   else
     hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue);
+                       (const uint32_t*)sv, queue, 0);
   TRY(hipGetLastError());
   *done = true;
   return NLP_OK;
@@ -1614,8 +1638,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
   // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
   const GraphView gv = view_of(g, p.metric, p.maxf2);
-  uint64_t* s_soff = nullptr;  // survivor lists S(u) of the range (small H), see k_hp_surv_lists
+  uint64_t* s_soff = nullptr;  // survivor lists S(u) of the range (small H), see k_hp_surv_lists / k_hp_dcls_*
   uint32_t* s_skeys = nullptr;
+  bool s_sorted = false;       // S(u) in N(u)'s order (degree-class compaction)
+  uint64_t* scan2 = nullptr;
   {
     TRY(hipMemsetAsync(wu, 0, nU * 8, st));
     TRY(hipMemcpyAsync(&g->host_small[8], g->off + ua, 8, hipMemcpyDeviceToHost, st));
@@ -1629,7 +1655,33 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       p_h = 0;
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
-    if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
+    if (g->dcls && g->hp_dcls && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
+      // the survivor lists S(u) as the compaction of the range's entries by
+      // degree class (sorted, no atomics; hashpath.hpp k_hp_dcls_*)
+      const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
+      uint32_t *scnt, *tcn;
+      uint64_t* tpre;
+      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
+      TRY(wsget(ws, B_HP_SOFF, nU + 1, &s_soff));
+      TRY(wsget(ws, B_HP_TCNT, nt, &tcn));
+      TRY(wsget(ws, B_HP_TPRE, nt + 1, &tpre));
+      const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
+      hipLaunchKernelGGL(k_hp_dcls_rows, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                         (const uint32_t*)g->tile_row, (unsigned long long*)wu, tcn);
+      TRY(hipGetLastError());
+      LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
+      TRY(hipGetLastError());
+      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(wsget(ws, B_SCAN2, scan_scratch_words(nt) + 16, &scan2));
+      TRY(scan_excl_u64<uint32_t>(tcn, nt, tpre, tpre + nt, scan2, st));
+      TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
+      hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, (const uint32_t*)g->keys, (const uint8_t*)g->dcls,
+                         p.H, e0, e1, (const uint64_t*)tpre, s_skeys);
+      TRY(hipGetLastError());
+      s_sorted = true;
+    } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
       // the survivor lists S(u) of the range, and W(u) with them: the row kernels walk S(u), not N(u)
       const uint64_t ns = g->dstart[p.H + 1];
       uint32_t* scnt;
@@ -1746,6 +1798,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.one_bucket = g->hp_one_bucket;
     a.soff = s_skeys ? s_soff : nullptr;
     a.skeys = s_skeys;
+    a.ssorted = s_sorted ? 1 : 0;
     a.sua = ua;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     if (n0 && g->hp_tiers) {

@@ -417,7 +417,9 @@ class _env:
 # 11 hub pass with one w-bucket per row, 12 the same with 128-entry item
 # tables (heavy buckets split into w-range items by their fine histogram),
 # 13 the ordering sorts by onesweep passes instead of hist / scan / scatter,
-# 14 bin-1 rows by the hub pass
+# 14 bin-1 rows by the hub pass, 15 the hub pass's AA / RA items by the ordered
+# re-walk instead of sort mode, 16/17 sort-mode items of at most 16 / 40 wedges
+# (heavy buckets split, single fine ranges beyond flagged HH_BIG)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -426,7 +428,10 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7"), dict(NLP_OS_SORT="1"),
-                 dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1")]
+                 dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SORT="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))

@@ -7,7 +7,7 @@ cd "$REPO"
 TAG=${TAG:-r03j}
 OUT=$REPO/gpurun_out/$TAG
 mkdir -p $OUT
-if [ -n "${PYTEST_K:-}" ]; then
+if [ -n "${PYTEST_K:-}" ] && [ -z "${NO_PYTEST:-}" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
     --maxfail=3 -k "$PYTEST_K" > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" $OUT/pytest_gpu.log | tail -12
