@@ -70,6 +70,7 @@ struct HpArgs {
   const uint32_t* skeys;
   uint64_t sua;
   int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
+  const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
 };
 
 // A row's first-hop list: S(u) when the survivor lists exist, else N(u).
@@ -226,6 +227,38 @@ __device__ __forceinline__ float hp_score(const HpArgs& a, uint32_t u, uint64_t 
     return acc;
   }
   return hp_ordered_sum(a, u, w, n);
+}
+
+// Count tables that also hold the second hop's degree (KD row kernels): count
+// in bits [0, CB), min(deg w, 2^(31 - CB) - 1) above it (added once, by the
+// thread whose CAS creates the entry), HP_EXCL on top.  A saturated degree is
+// gathered at the drain.
+template <int CB>
+__device__ __forceinline__ void hp_insert_kd(const HpTable& t, uint32_t mask, int shift, uint32_t key, uint32_t dw,
+                                             unsigned long long* err) {
+  constexpr uint32_t DSAT = (1u << (31 - CB)) - 1u;
+  uint32_t h = hp_hash(key, shift);
+  for (uint32_t probe = 0;; ++probe) {
+    if (probe > mask) { atomicOr(err, 1ull); return; }
+    uint32_t cur = *(volatile uint32_t*)&t.k[h];
+    bool mine = false;
+    if (cur == HP_EMPTY) {
+      cur = atomicCAS(&t.k[h], HP_EMPTY, key);
+      if (cur == HP_EMPTY) { cur = key; mine = true; }
+    }
+    if (cur == key) {
+      atomicAdd(&t.c[h], 1u + (mine ? (dw < DSAT ? dw : DSAT) << CB : 0u));
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+template <int CB>
+__device__ __forceinline__ uint32_t hp_kd_deg(const GraphView& g, uint32_t c, uint32_t w) {
+  constexpr uint32_t DSAT = (1u << (31 - CB)) - 1u;
+  const uint32_t d = (c & HP_CMASK) >> CB;
+  return d < DSAT ? d : g.deg[w];
 }
 
 // ---------------------------------------------------------------- ordered AA / RA accumulation
@@ -448,11 +481,13 @@ constexpr int HP_UN = 2;
 // threads sharing the block (64: a wave; HP_BNT: a workgroup), t = this
 // thread's index among them.
 // ALL: f(ok, w, entry) on every thread (convergent; entry = the first-hop index).
-template <int NS, bool ALL = false, typename IT, typename F>
+// KD: f(w, v, deg w) with the degree loaded beside the key from kd[].
+template <int NS, bool ALL = false, bool KD = false, typename IT, typename F>
 __device__ __forceinline__ void hp_wedges(uint64_t total, uint32_t t, uint32_t stride, const IT* s_incl,
-                                          const uint64_t* s_start, const uint32_t* s_iv, const uint32_t* keys, F f) {
+                                          const uint64_t* s_start, const uint32_t* s_iv, const uint32_t* keys, F f,
+                                          const uint32_t* kd = nullptr) {
   for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)stride * HP_UN) {
-    uint32_t w[HP_UN], v[HP_UN];
+    uint32_t w[HP_UN], v[HP_UN], dw[HP_UN];
     bool ok[HP_UN];
 #pragma unroll
     for (int q = 0; q < HP_UN; ++q) {
@@ -465,11 +500,14 @@ __device__ __forceinline__ void hp_wedges(uint64_t total, uint32_t t, uint32_t s
       }
       const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
       v[q] = ALL ? lo : s_iv[lo];
-      w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
+      const uint64_t at = ok[q] ? s_start[lo] + (j - ex) : 0ull;
+      w[q] = keys[at];
+      if constexpr (KD) dw[q] = kd[at];
     }
 #pragma unroll
     for (int q = 0; q < HP_UN; ++q) {
       if constexpr (ALL) f(ok[q], w[q], v[q]);
+      else if constexpr (KD) { if (ok[q]) f(w[q], v[q], dw[q]); }
       else if (ok[q]) f(w[q], v[q]);
     }
   }
@@ -495,8 +533,9 @@ __device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint3
 // 64): the slots of HP_UN rounds first (LDS or slab), then their degree loads
 // (count metrics) in flight together, then the scores; every thread of the
 // caller runs every round (hp_emit ballots per wave).
-// ORD: an ordered AA / RA table (LDS only, see ho_add_wave).
-template <bool GLOBAL, bool CUSTOM, int UN = HP_UN, bool ORD = false>
+// ORD: an ordered AA / RA table (LDS only, see ho_add_wave).  KCB > 0: a KD
+// count table (hp_insert_kd<KCB>: deg w in the count word).
+template <bool GLOBAL, bool CUSTOM, int UN = HP_UN, bool ORD = false, int KCB = 0>
 __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
                                          const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
   for (uint32_t i0 = 0; i0 < T; i0 += stride * UN) {
@@ -515,15 +554,20 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
     }
     if (!CUSTOM) {
 #pragma unroll
-      for (int q = 0; q < UN; ++q) dw[q] = a.g.deg[w[q] != HP_EMPTY ? w[q] : 0u];
+      for (int q = 0; q < UN; ++q) {
+        const uint32_t wq = w[q] != HP_EMPTY ? w[q] : 0u;
+        if constexpr (KCB > 0) dw[q] = hp_kd_deg<KCB>(a.g, c[q], wq);
+        else dw[q] = a.g.deg[wq];
+      }
     }
+    constexpr uint32_t CM = KCB > 0 ? (1u << KCB) - 1u : HP_CMASK;
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
       const bool valid = w[q] != HP_EMPTY;
       float s = 0.0f;
       if (valid) {
         if (CUSTOM) s = hp_score<true>(a, u, du, w[q], c[q], v0[q], v1[q]);
-        else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & HP_CMASK), du, (uint64_t)dw[q]);
+        else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & CM), du, (uint64_t)dw[q]);
       }
       hp_emit(sg, a, valid, s, u, w[q], tau);
     }
@@ -634,11 +678,13 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
 // into W's 40 bits: W <= 254 deg u).
 constexpr uint32_t HP_DCLS_MAX = 254;
 
+// (and, when kd is given, the entry degrees themselves: kd[e] = deg keys[e])
 __global__ void k_hp_dcls(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg, uint64_t M,
-                          uint8_t* __restrict__ out) {
+                          uint8_t* __restrict__ out, uint32_t* __restrict__ kd) {
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t d = deg[keys[e]];
     out[e] = (uint8_t)(d < 255u ? d : 255u);
+    if (kd) kd[e] = d;
   }
 }
 
@@ -906,7 +952,7 @@ __global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ row
   }
 }
 
-template <bool CUSTOM, int TW = HP_WT, int STG = HP_STG>
+template <bool CUSTOM, int TW = HP_WT, int STG = HP_STG, bool KD = false>
 __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
                                                 const uint64_t* __restrict__ wu, uint64_t ua,
                                                 const uint32_t* __restrict__ tcnt = nullptr, int tier = 0) {
@@ -999,6 +1045,14 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
                               }
                               ho_add_wave(tb, in, h, s_ic[wv][ent], &round);
                             });
+      } else if constexpr (KD) {  // TW <= 1024: at most 512 wedges per row, counts in 10 bits
+        hp_wedges<64, false, true>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                                   [&](uint32_t w, uint32_t, uint32_t dw) {
+                                     if (w > u) {
+                                       ++wedges;
+                                       hp_insert_kd<10>(tb, mask, shift, w, dw, &a.ctr[HPC_ERR]);
+                                     }
+                                   }, a.kdeg);
       } else {
         hp_wedges<64>(total, (uint32_t)lane, 64u, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                       [&](uint32_t w, uint32_t v) {
@@ -1015,7 +1069,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       if (x > u) hp_mark<false>(tb, mask, shift, x);
     });
     wave_sync_lds();
-    hp_drain<false, CUSTOM, 8, CUSTOM>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
+    hp_drain<false, CUSTOM, 8, CUSTOM, KD ? 10 : 0>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -1073,11 +1127,14 @@ __global__ void k_hp_batch_starts(const uint64_t* __restrict__ bpre, const uint3
 
 // hp_wedges with the first-hop entry's index: f(w, v, entry), UN keys per lane in flight
 // (ALL: f(ok, w, v, entry) on every lane, wave-convergent, for the ordered accumulation)
-template <int UN, bool ALL = false, typename IT, typename F>
+// (KD: also the degree of every second hop, kd[] = the graph's entry degrees,
+// loaded beside the key: f(w, v, entry, deg w))
+template <int UN, bool ALL = false, bool KD = false, typename IT, typename F>
 __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* s_incl, const uint64_t* s_start,
-                                          const uint32_t* s_iv, const uint32_t* keys, F f) {
+                                          const uint32_t* s_iv, const uint32_t* keys, F f,
+                                          const uint32_t* kd = nullptr) {
   for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * UN) {
-    uint32_t w[UN], v[UN], e[UN];
+    uint32_t w[UN], v[UN], e[UN], dw[UN];
     bool ok[UN];
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
@@ -1090,15 +1147,19 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
       const uint64_t ex = lo ? (uint64_t)s_incl[lo - 1] : 0ull;
       v[q] = s_iv[lo];
       e[q] = lo;
-      w[q] = keys[ok[q] ? s_start[lo] + (j - ex) : 0ull];
+      const uint64_t at = ok[q] ? s_start[lo] + (j - ex) : 0ull;
+      w[q] = keys[at];
+      if constexpr (KD) dw[q] = kd[at];
     }
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
       if constexpr (ALL) f(ok[q], w[q], v[q], e[q]);
+      else if constexpr (KD) { if (ok[q]) f(w[q], v[q], e[q], dw[q]); }
       else if (ok[q]) f(w[q], v[q], e[q]);
     }
   }
 }
+
 
 // the batch slot of flattened item j < incl[63]: the first r with incl[r] > j
 // (64 non-decreasing inclusive prefixes; lanes past the batch's rows repeat
@@ -1112,7 +1173,9 @@ __device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t, uint
   return lo;
 }
 
-template <bool CUSTOM, int TW, int STG = HP_STG>
+// KD (count metrics, with the graph's entry degrees): deg w rides in the table
+// (hp_insert_kd<10>: a batch holds at most 512 wedges), no gather at the drain.
+template <bool CUSTOM, int TW, int STG = HP_STG, bool KD = false>
 __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __restrict__ tl,
                                                  const uint32_t* __restrict__ tcnt, int tlo, int thi,
                                                  const uint32_t* __restrict__ bstart,
@@ -1278,6 +1341,15 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
                                  }
                                  ho_add_wave(tb, in, h, s_ic[wv][ent], &round);
                                });
+      } else if constexpr (KD) {
+        hb_wedges<HB_UN, false, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+                                      [&](uint32_t w, uint32_t, uint32_t ent, uint32_t dw) {
+                                        const uint32_t sl = s_islot[wv][ent];
+                                        if (w > s_u[wv][sl]) {
+                                          ++wedges;
+                                          hp_insert_kd<10>(tb, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
+                                        }
+                                      }, a.kdeg);
       } else {
         hb_wedges<HB_UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                          [&](uint32_t w, uint32_t vv, uint32_t ent) {
@@ -1326,7 +1398,10 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
       if (!CUSTOM) {
 #pragma unroll
-        for (int q = 0; q < HB_UN; ++q) dw[q] = a.g.deg[kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u];
+        for (int q = 0; q < HB_UN; ++q) {
+          const uint32_t w = kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u;
+          dw[q] = KD ? hp_kd_deg<10>(a.g, c[q], w) : a.g.deg[w];
+        }
       }
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
@@ -1337,7 +1412,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
         float s = 0.0f;
         if (valid) {
           if (CUSTOM) s = ho_score(c[q]);
-          else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & HP_CMASK), du2, (uint64_t)dw[q]);
+          else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & (KD ? 1023u : HP_CMASK)), du2, (uint64_t)dw[q]);
         }
         hp_emit(sg, a, valid, s, uu, w, tau);
       }
@@ -1385,7 +1460,7 @@ __device__ __forceinline__ void hp_sync() {
   if (GLOBAL) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
-template <bool CUSTOM, bool GLOBAL>
+template <bool CUSTOM, bool GLOBAL, bool KD = false>
 __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* __restrict__ rows, uint64_t nrows,
                                                      const uint64_t* __restrict__ wu, uint64_t ua,
                                                      uint32_t* __restrict__ slab, int tlog,
@@ -1506,6 +1581,15 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
                                     if (in) h = ho_find(tb, mask, shift, w, &a.ctr[HPC_ERR]);
                                     ho_add_block(tb, in, h, s_ic[ent], &round);
                                   });
+        } else if constexpr (KD && !GLOBAL && !CUSTOM) {  // bin 1: W <= 4096, counts in 13 bits
+          hp_wedges<HP_BNT, false, true>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
+                                         [&](uint32_t w, uint32_t, uint32_t dw) {
+                                           if (w > u) {
+                                             if (p == 0) ++wedges;
+                                             if ((uint64_t)w >= wlo && (uint64_t)w < whi)
+                                               hp_insert_kd<13>(tb, mask, shift, w, dw, &a.ctr[HPC_ERR]);
+                                           }
+                                         }, a.kdeg);
         } else {
           hp_wedges<HP_BNT>(total, (uint32_t)t, (uint32_t)HP_BNT, s_incl, s_start, s_iv, a.g.keys,
                             [&](uint32_t w, uint32_t v) {
@@ -1522,7 +1606,8 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
         if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
       });
       hp_sync<GLOBAL>();
-      hp_drain<GLOBAL, CUSTOM, HP_UN, ORD>(tb, T, (uint32_t)t, (uint32_t)HP_BNT, sg, a, u, du, tau);
+      hp_drain<GLOBAL, CUSTOM, HP_UN, ORD, (KD && !GLOBAL && !CUSTOM) ? 13 : 0>(tb, T, (uint32_t)t, (uint32_t)HP_BNT,
+                                                                              sg, a, u, du, tau);
       hp_sync<GLOBAL>();
       round = 0;
     }
@@ -2038,7 +2123,7 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
     const uint64_t dist = (uint64_t)n < width ? (uint64_t)n : width;
     const bool simple = n > 0 && (wcap ? n <= wcap : 2 * dist <= (1ull << tl)), hv = n > 0 && !simple;
     const uint32_t i = hh_wave_append(simple, nitems);
-    if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};
+    if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};  // i < nb <= the item capacity
     const uint32_t j = hh_wave_append(hv, nheavy);
     if (hv) heavy[j] = (uint32_t)gb;
   }
@@ -2148,7 +2233,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
                                                     const uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
                                                     const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw,
                                                     const uint32_t* __restrict__ sv, uint32_t* __restrict__ queue,
-                                                    int sortmode) {
+                                                    int sortmode, uint64_t cap) {
   constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
   constexpr int LT = 1 << TL;
   constexpr int VT = CUSTOM ? LT : 1;
@@ -2172,7 +2257,9 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   }
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
-  const uint32_t ni = *nitems;
+  // k_hh_split counts past `cap` when the item array overflows (and raises
+  // HPC_ERR): never read beyond it
+  const uint32_t ni = (uint32_t)min((uint64_t)*nitems, cap);
   uint64_t wedges = 0;
   __syncthreads();
   for (;;) {

@@ -238,6 +238,7 @@ struct nlp_graph {
   uint32_t* hp_scratch = nullptr;              // k_hp_part: per-workgroup wedge scratch (w and v)
   uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
   uint8_t* dcls = nullptr;                     // min(deg keys[e], 255) per adjacency entry (path 4's survivor lists)
+  uint32_t* kdeg = nullptr;                    // deg keys[e] per adjacency entry (path 4's count-metric row kernels)
   // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
   uint64_t* truth = nullptr;
   uint64_t ntruth = 0;
@@ -255,6 +256,7 @@ struct nlp_graph {
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
+  bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
@@ -368,6 +370,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->hp_scratch) (void)hipFree(g->hp_scratch);
   if (g->tile_row) (void)hipFree(g->tile_row);
   if (g->dcls) (void)hipFree(g->dcls);
+  if (g->kdeg) (void)hipFree(g->kdeg);
   if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
@@ -552,7 +555,13 @@ nlp_status finish_graph(nlp_graph* g) {
   const char* hdc = getenv("NLP_HASH_DCLS");
   if (M > 0 && !(hdc && hdc[0] == '0') && g->maxdeg < (1u << 24)) {
     if (hipMalloc(&g->dcls, M) == hipSuccess) {
-      LAUNCH(k_hp_dcls, M, st, (const uint32_t*)g->keys, (const uint32_t*)g->deg, M, g->dcls);
+      // and the entry degrees (the count-metric row kernels carry deg w in their tables)
+      const char* hkd = getenv("NLP_HASH_KDEG");
+      if (!(hkd && hkd[0] == '0') && hipMalloc(&g->kdeg, M * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        g->kdeg = nullptr;
+      }
+      LAUNCH(k_hp_dcls, M, st, (const uint32_t*)g->keys, (const uint32_t*)g->deg, M, g->dcls, g->kdeg);
       TRY(hipGetLastError());
     } else {
       (void)hipGetLastError();
@@ -689,6 +698,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
+  if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
     g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
@@ -1589,7 +1599,10 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
   // AA / RA: sort-mode items (at most HH_SCAP wedges each, keys need w, v < 2^26)
   const uint32_t wcap = custom && g->hh_sort && g->span <= (1ull << 26) ? g->hh_scap : 0u;
-  const uint64_t cap = 2 * NB + 3 * (tot >> (tl - 2)) + 1024;
+  // items: at most NB whole buckets, per heavy bucket 2 n / half + 1 groups, and
+  // per fine range beyond half at most 8 width pieces (fine width <= 2^26 / 4096)
+  const uint64_t half = wcap ? wcap : (1ull << (tl - 1));
+  const uint64_t cap = 3 * NB + 10 * (tot / half) + 1024;
   HhItem* items;
   uint32_t* heavy = bcur;  // the cursors are done with
   uint32_t* nitems = queue + 1;  // and queue + 2: the heavy count
@@ -1607,13 +1620,13 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue, (int)(wcap != 0));
+                       (const uint32_t*)sv, queue, (int)(wcap != 0), cap);
   else
     hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue, 0);
+                       (const uint32_t*)sv, queue, 0, cap);
   TRY(hipGetLastError());
   *done = true;
   return NLP_OK;
@@ -1799,6 +1812,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.soff = s_skeys ? s_soff : nullptr;
     a.skeys = s_skeys;
     a.ssorted = s_sorted ? 1 : 0;
+    a.kdeg = g->kdeg;
     a.sua = ua;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     if (n0 && g->hp_tiers) {
@@ -1829,9 +1843,11 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
         if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());
         if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
+        else if (a.kdeg) hipLaunchKernelGGL((k_hp_wave<false, HP_WT, HP_STG, true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
       } else if (custom) {
         hipLaunchKernelGGL((k_hp_wave<true, 256, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 0);
@@ -1858,6 +1874,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     if (n1 && !b1_done) {
       const unsigned gr = (unsigned)std::min<uint64_t>(n1, 2048);
       if (custom) hipLaunchKernelGGL((k_hp_block<true, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
+      else if (a.kdeg) hipLaunchKernelGGL((k_hp_block<false, false, true>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
       else hipLaunchKernelGGL((k_hp_block<false, false>), dim3(gr), dim3(HP_BNT), 0, st, a, lists[1] + q0[1], n1, wu, ua, (uint32_t*)nullptr, 13, tcnt + 8);
       TRY(hipGetLastError());
     }
@@ -3109,9 +3126,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
 nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result) {
   // path 3 (hash accumulation) once the wedge count is large: bounded memory,
-  // no wedge materialisation (NLP_HASH=1 forces it, NLP_HASH=0 disables it)
-  // Adamic-Adar / Resource-Allocation stay on the sort paths unless forced: their
-  // ordered sums of three or more contributions re-walk intersections in path 4
+  // no wedge materialisation (NLP_HASH=1 forces it, NLP_HASH=0 disables it).
+  // Adamic-Adar / Resource-Allocation too: their ordered sums are the row
+  // kernels' ordered accumulation and the hub pass's sort-mode items
+  // (NLP_HASH_AA=0 keeps them on the sort paths, as before round 3)
   const bool custom = p.metric == M_AA || p.metric == M_RA;
   // a synchronous call may change what an asynchronous replay would rebuild
   // (capacities, the grouping memo, the range index): only the call that ends
@@ -3119,7 +3137,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   g->async_ok = false;
   const bool use_hash = !g->force_radix && p.max_edges > 0 &&
                         (g->hash_mode > 0 ||
-                         (g->hash_mode == 0 && !custom && hp_estimate(g, p) > (double)g->hp_min_wedges));
+                         (g->hash_mode == 0 && (!custom || g->hp_aa) && hp_estimate(g, p) > (double)g->hp_min_wedges));
   if (!use_hash && (p.H > 0 || g->sort_grouping) && !g->force_radix && p.max_edges > 0 && p.ua < p.ub && p.ua < g->span) {
     bool handled = false;
     nlp_status s = predict_fast(g, p, d_out, out_count, t, st, result, &handled);

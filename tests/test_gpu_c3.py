@@ -1,8 +1,9 @@
 """BASELINE configs[2] / SURVEY §8(d) C3: the uk-2005-shaped stand-in
 (n = 39.5 M, M = 1.7e9) -- the "HBM-roofline run".  LHub Adamic-Adar (the
 config's metric) and Jaccard at H = 4 (path 1) and H = 16 (Jaccard on path 4,
-the hash accumulation; Adamic-Adar on path 2, the chunked sort -- k = 8.7e7 of
-9.6e8 candidates), exact against the parallel oracle, order included."""
+the hash accumulation, Adamic-Adar too: ordered accumulation in the row
+kernels, sort-mode items in the hub pass -- k = 8.7e7 of 9.6e8 candidates),
+exact against the parallel oracle, order included."""
 import numpy as np
 import pytest
 
@@ -55,5 +56,5 @@ def test_gpu_c3_jaccard_h16_hash_path(c3, oracle):
 
 @pytest.mark.timeout(300)
 def test_gpu_c3_adamic_adar_h16(c3, oracle):
-    n, t = _check(c3, oracle, 7, 16)
+    n, t = _check(c3, oracle, 7, 16, path=4)
     assert n == c3.k

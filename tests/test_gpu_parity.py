@@ -502,7 +502,7 @@ def test_gpu_hash_routing_and_shards(gpu, oracle):
         with gpu.Graph(off, keys) as G:
             for m, H in ((1, 16), (7, 0), (0, 32), (2, 0)):
                 u, w, s, t = G.predict(m, H, k)
-                assert t["path"] == (4 if m != 7 else 1)  # AA / RA stay on the sort paths unless forced
+                assert t["path"] == 4  # AA / RA too (ordered accumulation, hub sort mode)
                 eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
                 assert_canonical_equal(eu, ew, es, u, w, s)
                 parts = []
@@ -521,25 +521,28 @@ def test_gpu_hash_routing_and_shards(gpu, oracle):
 
 
 def test_gpu_full_size_c2_large_hub_threshold(gpu, oracle, nlp):
-    """C2 stand-in at H = 16 (1.6e8 wedges) against the oracle: Jaccard on path 4
-    (automatic routing), Adamic-Adar on the sort path (persistent scans over
-    many tiles)."""
+    """C2 stand-in at H = 16 (1.6e8 wedges) against the oracle: Jaccard and
+    Adamic-Adar on path 4 (automatic routing), and Adamic-Adar on the sort path
+    (NLP_HASH_AA=0: persistent scans over many tiles)."""
     import torch
     import nlp_loader
     gg = nlp_loader.load_sub("graphgen")
     off_t, keys_t, du, dw, info = gg.make_workload("C2-soc-LiveJournal1", "cuda")
-    with gpu.Graph.from_device(off_t, keys_t) as G:
-        off = off_t.cpu().numpy().astype(np.uint64)
-        keys = keys_t.cpu().numpy().view(np.uint32)
-        k = info["k"]
-        out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
-        for m in (1, 7):
-            n, t = G.predict_device(m, 16, k, out)
-            assert t["path"] == (4 if m == 1 else 1)
-            u, w, s = gpu.edges_from_tensor(out, n)
-            eu, ew, es, oi = oracle.predict(off, keys, m, 16, max_edges=k)
-            assert_canonical_equal(eu, ew, es, u, w, s)
-            assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
+    off = off_t.cpu().numpy().astype(np.uint64)
+    keys = keys_t.cpu().numpy().view(np.uint32)
+    k = info["k"]
+    out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+    ref = {m: oracle.predict(off, keys, m, 16, max_edges=k) for m in (1, 7)}
+    for env, cases in ((dict(), ((1, 4), (7, 4))), (dict(NLP_HASH_AA="0"), ((7, 1),))):
+        with _env(**env):
+            with gpu.Graph.from_device(off_t, keys_t) as G:
+                for m, path in cases:
+                    n, t = G.predict_device(m, 16, k, out)
+                    assert t["path"] == path
+                    u, w, s = gpu.edges_from_tensor(out, n)
+                    eu, ew, es, oi = ref[m]
+                    assert_canonical_equal(eu, ew, es, u, w, s)
+                    assert t["wedges"] == oi["wedges_gt"] and t["candidates"] == oi["candidates"]
 
 
 def test_gpu_device_evaluation_matches_host(gpu, golden):
