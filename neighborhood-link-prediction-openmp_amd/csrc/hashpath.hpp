@@ -71,7 +71,9 @@ struct HpArgs {
   uint64_t sua;
   int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
   const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
+  const uint64_t* sdo;   // S(u) entries packed deg v << HP_SDO_SH | off[v] (degree-class lists; null: none)
 };
+constexpr int HP_SDO_SH = 40;  // offsets < 2^40 (guarded at the list build)
 
 // A row's first-hop list: S(u) when the survivor lists exist, else N(u).
 __device__ __forceinline__ void hp_first_hops(const HpArgs& a, uint32_t u, uint64_t o0, uint64_t du,
@@ -760,10 +762,13 @@ __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __res
 }
 
 // tpre: exclusive prefix of the tile counts (tile - t0 indexed)
+// (sdo: also deg v << HP_SDO_SH | off[v] per entry, so that the row batches
+// skip the gather of v's row bounds; the class is the exact degree here)
 __global__ __launch_bounds__(NT) void k_hp_dcls_fill(const uint32_t* __restrict__ keys,
                                                      const uint8_t* __restrict__ dcls, uint32_t H, uint64_t e0,
                                                      uint64_t e1, const uint64_t* __restrict__ tpre,
-                                                     uint32_t* __restrict__ skeys) {
+                                                     uint32_t* __restrict__ skeys, const uint64_t* __restrict__ off,
+                                                     uint64_t* __restrict__ sdo) {
   const int lane = lane_id(), wv = wave_id();
   const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
   for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
@@ -780,7 +785,12 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill(const uint32_t* __restrict_
       const uint64_t e = base + (uint64_t)i * 64 + lane;
       const bool s = hp_dsurv(c[i], H);
       const uint64_t m = __ballot(s);
-      if (s) skeys[pos + (uint64_t)__popcll(m & ((1ull << lane) - 1))] = keys[e];
+      if (s) {
+        const uint64_t q = pos + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+        const uint32_t v = keys[e];
+        skeys[q] = v;
+        if (sdo) sdo[q] = (uint64_t)c[i] << HP_SDO_SH | off[v];
+      }
       pos += (uint64_t)__popcll(m);
     }
   }
@@ -1277,7 +1287,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       continue;
     }
     const int shift = 32 - lg;
-    if (CUSTOM) {
+    if (CUSTOM && !a.sdo) {
       // AA / RA: the batch's first hops sorted by (slot, v) -- S(u) is unordered
       // -- so that the wedge steps run in the reference's order of additions
       if (NS > (uint32_t)SK) {  // more first hops than wedges (a budget bug): fail the call
@@ -1305,20 +1315,29 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       uint64_t st = 0;
       double cv = 0.0;
       if (e < NS) {
-        if (CUSTOM) {
-          const uint32_t key = s_sk[wv][e];
-          slot = key >> wbits;
-          v = key & wmask;
-        } else {
+        if (a.sdo) {  // packed survivor entries: no degree / offset gather (every entry survives)
           slot = hb_slot(s_sp[wv], nr, e);
           const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
-          v = a.skeys[s_s0[wv][slot] + (e - ex)];
-        }
-        const uint32_t d = a.g.deg[v];
-        if (hp_surv(d, a.H)) {
-          len = d;
-          st = a.g.off[v];
-          if (CUSTOM) cv = a.g.ctab[d];
+          const uint64_t x = a.sdo[s_s0[wv][slot] + (e - ex)];
+          len = (uint32_t)(x >> HP_SDO_SH);
+          st = x & ((1ull << HP_SDO_SH) - 1);
+          if (CUSTOM) cv = a.g.ctab[len];
+        } else {
+          if (CUSTOM) {
+            const uint32_t key = s_sk[wv][e];
+            slot = key >> wbits;
+            v = key & wmask;
+          } else {
+            slot = hb_slot(s_sp[wv], nr, e);
+            const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
+            v = a.skeys[s_s0[wv][slot] + (e - ex)];
+          }
+          const uint32_t d = a.g.deg[v];
+          if (hp_surv(d, a.H)) {
+            len = d;
+            st = a.g.off[v];
+            if (CUSTOM) cv = a.g.ctab[d];
+          }
         }
       }
       const uint32_t incl = (uint32_t)wave_incl_scan(len);
@@ -2399,21 +2418,26 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
 // Split the candidate buffer around the k-th key (sel[3] from the radix
 // select): keys above go to the target columns (unordered), ties to a list of
 // (u << 32 | w) records with their index, to be ordered canonically.
-constexpr int HP_SPLIT_IPL = 16;  // elements per lane: one wave-tile = 1024 candidates, two atomics
+constexpr int HP_SPLIT_IPL = 16;  // elements per lane: a wave-tile = 1024 candidates, a workgroup tile 4 of them
 
+// One pair of reservations (above, ties) per workgroup tile of 4096
+// candidates: a chip-wide stream of atomics on two words serialises at their
+// L2 channel, so the four waves' counts meet in LDS first.
 __global__ __launch_bounds__(NT) void k_hp_split(const uint32_t* __restrict__ key, const uint32_t* __restrict__ u,
                                                  const uint32_t* __restrict__ w, const float* __restrict__ s, uint64_t n,
                                                  const uint64_t* __restrict__ sel, uint32_t* __restrict__ okey,
                                                  uint32_t* __restrict__ ou, uint32_t* __restrict__ ow,
                                                  float* __restrict__ os, uint64_t* __restrict__ tie_k,
                                                  uint32_t* __restrict__ tie_i, unsigned long long* __restrict__ cnt) {
-  constexpr uint64_t WT = 64 * HP_SPLIT_IPL;
+  constexpr uint64_t WT = 64 * HP_SPLIT_IPL, BT = WT * NWAVE;
+  __shared__ uint32_t s_na[NWAVE], s_nt[NWAVE];
+  __shared__ unsigned long long s_base[2];
   const uint32_t kth = (uint32_t)sel[3];
-  const int lane = lane_id();
+  const int lane = lane_id(), wv = wave_id();
   const uint64_t below = (1ull << lane) - 1;
-  const uint64_t nwt = (n + WT - 1) / WT;
-  for (uint64_t wt = (uint64_t)blockIdx.x * NWAVE + wave_id(); wt < nwt; wt += (uint64_t)gridDim.x * NWAVE) {
-    const uint64_t base = wt * WT;
+  const uint64_t nbt = (n + BT - 1) / BT;
+  for (uint64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
+    const uint64_t base = bt * BT + (uint64_t)wv * WT;
     uint32_t k[HP_SPLIT_IPL];
     uint32_t na = 0, nt = 0;
 #pragma unroll
@@ -2423,13 +2447,27 @@ __global__ __launch_bounds__(NT) void k_hp_split(const uint32_t* __restrict__ ke
       na += (uint32_t)__popcll(__ballot(i < n && k[r] > kth));
       nt += (uint32_t)__popcll(__ballot(i < n && k[r] == kth));
     }
-    unsigned long long pa = 0, pt = 0;
     if (lane == 0) {
-      if (na) pa = atomicAdd(&cnt[0], (unsigned long long)na);
-      if (nt) pt = atomicAdd(&cnt[1], (unsigned long long)nt);
+      s_na[wv] = na;
+      s_nt[wv] = nt;
     }
-    pa = __shfl(pa, 0, 64);
-    pt = __shfl(pt, 0, 64);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t ta = 0, tt = 0;
+      for (int q = 0; q < NWAVE; ++q) {
+        ta += s_na[q];
+        tt += s_nt[q];
+      }
+      s_base[0] = ta ? atomicAdd(&cnt[0], (unsigned long long)ta) : 0ull;
+      s_base[1] = tt ? atomicAdd(&cnt[1], (unsigned long long)tt) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long pa = s_base[0], pt = s_base[1];
+    for (int q = 0; q < wv; ++q) {
+      pa += s_na[q];
+      pt += s_nt[q];
+    }
+    __syncthreads();  // s_na / s_nt / s_base are rewritten by the next tile
 #pragma unroll
     for (int r = 0; r < HP_SPLIT_IPL; ++r) {
       const uint64_t i = base + (uint64_t)r * 64 + lane;
@@ -2472,6 +2510,43 @@ __global__ void k_hp_uwkeys(const uint32_t* __restrict__ u, const uint32_t* __re
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     k[i] = ((uint64_t)u[i] << vb) | w[i];
     idx[i] = (uint32_t)i;
+  }
+}
+
+// Final order of path 4 (hp_final_order): (u << vb | w) keys with the score
+// key as value, sorted; then 64-bit keys (~score key << 32 | uw position),
+// sorted on their high half (stable: equal scores keep (u, w) order) -- the
+// output's (u, w) come from the uw position, the score from the key (NaN keys
+// are 0: a NaN of some payload comes back, compared by NaN-ness).
+__global__ void k_hp_uwkeys2(const uint32_t* __restrict__ u, const uint32_t* __restrict__ w,
+                             const uint32_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ k,
+                             uint32_t* __restrict__ val, int vb) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    k[i] = ((uint64_t)u[i] << vb) | w[i];
+    val[i] = key[i];
+  }
+}
+
+__global__ void k_hp_skeys(const uint32_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ k) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    k[i] = ((uint64_t)(~key[i]) << 32) | i;
+}
+
+__device__ __forceinline__ float score_of_key(uint32_t key) {
+  return __uint_as_float((key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
+}
+
+__global__ void k_hp_final_edges(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ uw, uint64_t n,
+                                 int vb, EdgeOut* __restrict__ out) {
+  const uint64_t wm = (1ull << vb) - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = sk[i];
+    const uint64_t y = uw[x & 0xffffffffull];
+    EdgeOut o;
+    o.u = (uint32_t)(y >> vb);
+    o.v = (uint32_t)(y & wm);
+    o.score = score_of_key(~(uint32_t)(x >> 32));
+    out[i] = o;
   }
 }
 

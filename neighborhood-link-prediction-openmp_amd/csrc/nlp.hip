@@ -74,7 +74,7 @@ enum Buf {
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
-  B_HP_TCNT, B_HP_TPRE,
+  B_HP_TCNT, B_HP_TPRE, B_HP_SDO,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
   NBUF
 };
@@ -256,6 +256,8 @@ struct nlp_graph {
   int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
+  bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
+  bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
@@ -699,6 +701,8 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
+  if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
+  if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
     g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
   if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
@@ -1442,7 +1446,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   TRY(wsget(ws, B_TS, std::max<uint64_t>(cap, 1), &ns));
   TRY(wsget(ws, B_HP_TIEK0, n, &tk0));
   TRY(wsget(ws, B_HP_TIEI0, n, &ti0));
-  hipLaunchKernelGGL(k_hp_split, dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>(n / (NT * HP_SPLIT_IPL), 1), 4096)),
+  hipLaunchKernelGGL(k_hp_split, dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>(n / (NT * HP_SPLIT_IPL), 1), 2048)),
                      dim3(NT), 0, st, ckey, cu, cw, cs, n, sel, nk, nu, nw, ns, tk0, ti0,
                      (unsigned long long*)(small + 40));
   TRY(hipGetLastError());
@@ -1508,6 +1512,43 @@ nlp_status hp_uw_order(nlp_graph* g, Cands& C, hipStream_t st) {
   std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
   std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
   std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  return NLP_OK;
+}
+
+// The held candidates straight to the caller's edges in the canonical order
+// (score key desc, u asc, w asc): two sorts and one gather of 8 bytes per edge
+// (k_hp_final_edges) instead of hp_uw_order's permutation, order_v1's score
+// sort and its three-column gather.
+nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
+  const uint64_t n = C.n;
+  if (n == 0) return NLP_OK;
+  if (n > 0xffffffffull) return NLP_ERR_INVALID;
+  Workspace& ws = g->ws;
+  uint64_t *k0, *k1, *s0, *s1;
+  uint32_t *v0, *v1;
+  TRY(wsget(ws, B_SK0, n, &k0));
+  TRY(wsget(ws, B_SK1, n, &k1));
+  TRY(wsget(ws, B_SV0, n, &v0));
+  TRY(wsget(ws, B_SV1, n, &v1));
+  const int vb = bits_for(g->span - 1);
+  LAUNCH(k_hp_uwkeys2, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const uint32_t*)ws.p[B_CKEY],
+         n, k0, v0, vb);
+  TRY(hipGetLastError());
+  int shifts[8], np = 0;
+  for (int b = 0; b < 2 * vb && np < 8; b += 8) shifts[np++] = b;
+  int which = 0;
+  { nlp_status so = sort_pairs_os(g, k0, v0, k1, v1, n, shifts, np, &which, st); if (so != NLP_OK) return so; }
+  const uint64_t* uw = which ? k1 : k0;
+  const uint32_t* sv = which ? v1 : v0;
+  TRY(wsget(ws, B_HP_TIEK0, n, &s0));
+  TRY(wsget(ws, B_HP_TIEK1, n, &s1));
+  LAUNCH(k_hp_skeys, n, st, sv, n, s0);
+  TRY(hipGetLastError());
+  const int hs[4] = {32, 40, 48, 56};
+  int w2 = 0;
+  { nlp_status so = sort_pairs_os(g, s0, nullptr, s1, nullptr, n, hs, 4, &w2, st); if (so != NLP_OK) return so; }
+  LAUNCH(k_hp_final_edges, n, st, (const uint64_t*)(w2 ? s1 : s0), uw, n, vb, d_out);
+  TRY(hipGetLastError());
   return NLP_OK;
 }
 
@@ -1654,6 +1695,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t* s_soff = nullptr;  // survivor lists S(u) of the range (small H), see k_hp_surv_lists / k_hp_dcls_*
   uint32_t* s_skeys = nullptr;
   bool s_sorted = false;       // S(u) in N(u)'s order (degree-class compaction)
+  uint64_t* s_sdo = nullptr;   // packed S(u) entries (deg v, off[v]) of the degree-class lists
   uint64_t* scan2 = nullptr;
   {
     TRY(hipMemsetAsync(wu, 0, nU * 8, st));
@@ -1668,7 +1710,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       p_h = 0;
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
-    if (g->dcls && g->hp_dcls && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
+    if (g->dcls && g->hp_dcls && g->hp_work_surv && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
       // the survivor lists S(u) as the compaction of the range's entries by
       // degree class (sorted, no atomics; hashpath.hpp k_hp_dcls_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
@@ -1690,8 +1732,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
+      if (g->hp_sdo && g->nnz < (1ull << HP_SDO_SH))
+        TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(g->host_small[10], 1), &s_sdo));
       hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, (const uint32_t*)g->keys, (const uint8_t*)g->dcls,
-                         p.H, e0, e1, (const uint64_t*)tpre, s_skeys);
+                         p.H, e0, e1, (const uint64_t*)tpre, s_skeys, (const uint64_t*)g->off, s_sdo);
       TRY(hipGetLastError());
       s_sorted = true;
     } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
@@ -1813,6 +1857,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.skeys = s_skeys;
     a.ssorted = s_sorted ? 1 : 0;
     a.kdeg = g->kdeg;
+    a.sdo = s_sdo;
     a.sua = ua;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     if (n0 && g->hp_tiers) {
@@ -1945,7 +1990,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     if (!full && target > free_slots) target = free_slots;  // no threshold yet: emissions <= W(u)
     if (target == 0) target = 1;
   }
-  return hp_uw_order(g, C, st);
+  // held candidates are unordered: the caller orders them (hp_final_order,
+  // or hp_uw_order + order_v1 with NLP_HASH_FINAL=0)
+  if (!g->hp_final) return hp_uw_order(g, C, st);
+  return NLP_OK;
 }
 
 // ================================================================ fast path
@@ -3190,7 +3238,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   nlp_status s = prune_to(g, C, p.max_edges, st);
   if (s != NLP_OK) return s;
   if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.n, 1), &d_out));
-  s = order_v1(g, C, d_out, st);
+  s = path == 4 && g->hp_final ? hp_final_order(g, C, d_out, st) : order_v1(g, C, d_out, st);
   if (s != NLP_OK) return s;
   TRY(hipEventRecord(g->ev[2], st));
   TRY(hipEventSynchronize(g->ev[2]));

@@ -419,7 +419,11 @@ class _env:
 # 13 the ordering sorts by onesweep passes instead of hist / scan / scatter,
 # 14 bin-1 rows by the hub pass, 15 the hub pass's AA / RA items by the ordered
 # re-walk instead of sort mode, 16/17 sort-mode items of at most 16 / 40 wedges
-# (heavy buckets split, single fine ranges beyond flagged HH_BIG)
+# (heavy buckets split, single fine ranges beyond flagged HH_BIG), 18 survivor
+# lists from in-edge atomics (unordered: the AA / RA row kernels sort them), 19
+# no entry-degree tables (deg w gathered at the drain), 20 = 18 with bin-1 rows,
+# 21 the held candidates ordered by (u, w) permutation + order_v1 (before hp_final_order),
+# 22 row batches gathering deg / off of every first hop (no packed survivor entries)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -431,7 +435,9 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SORT="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000")]
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
+                 dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
+                 dict(NLP_HASH_FINAL="0"), dict(NLP_HASH_SDO="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
