@@ -540,10 +540,13 @@ __device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint3
 template <bool GLOBAL, bool CUSTOM, int UN = HP_UN, bool ORD = false, int KCB = 0>
 __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
                                          const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
+  T = __builtin_amdgcn_readfirstlane(T);
   for (uint32_t i0 = 0; i0 < T; i0 += stride * UN) {
     uint32_t w[UN], c[UN], v0[UN], v1[UN], dw[UN];
+    const uint32_t nq = min((uint32_t)UN, (T - i0 + stride - 1) / stride);  // steps inside the table (uniform)
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
+      if ((uint32_t)q >= nq) break;
       const uint32_t i = i0 + (uint32_t)q * stride + t;
       c[q] = v0[q] = v1[q] = 0;
       if (ORD) w[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
@@ -551,12 +554,16 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
     }
     if (ORD) {
 #pragma unroll
-      for (int q = 0; q < UN; ++q) hp_emit(sg, a, w[q] != HP_EMPTY, ho_score(c[q]), u, w[q], tau);
+      for (int q = 0; q < UN; ++q) {
+        if ((uint32_t)q >= nq) break;
+        hp_emit(sg, a, w[q] != HP_EMPTY, ho_score(c[q]), u, w[q], tau);
+      }
       continue;
     }
     if (!CUSTOM) {
 #pragma unroll
       for (int q = 0; q < UN; ++q) {
+        if ((uint32_t)q >= nq) break;
         const uint32_t wq = w[q] != HP_EMPTY ? w[q] : 0u;
         if constexpr (KCB > 0) dw[q] = hp_kd_deg<KCB>(a.g, c[q], wq);
         else dw[q] = a.g.deg[wq];
@@ -565,6 +572,7 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
     constexpr uint32_t CM = KCB > 0 ? (1u << KCB) - 1u : HP_CMASK;
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
+      if ((uint32_t)q >= nq) break;
       const bool valid = w[q] != HP_EMPTY;
       float s = 0.0f;
       if (valid) {
@@ -1143,11 +1151,16 @@ template <int UN, bool ALL = false, bool KD = false, typename IT, typename F>
 __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* s_incl, const uint64_t* s_start,
                                           const uint32_t* s_iv, const uint32_t* keys, F f,
                                           const uint32_t* kd = nullptr) {
-  for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)64 * UN) {
+  // the steps past the batch's wedges are skipped wave-uniformly (a batch often
+  // holds fewer than 64 * UN wedges: their searches and loads would be issued anyway)
+  const uint32_t tot = __builtin_amdgcn_readfirstlane((uint32_t)total);
+  for (uint64_t j0 = 0; j0 < tot; j0 += (uint64_t)64 * UN) {
     uint32_t w[UN], v[UN], e[UN], dw[UN];
     bool ok[UN];
+    const uint32_t nq = (uint32_t)min((uint64_t)UN, (tot - j0 + 63) / 64);
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
+      if ((uint32_t)q >= nq) break;
       const uint64_t j = j0 + (uint64_t)q * 64 + t;
       ok[q] = j < total;
       uint32_t lo = 0;  // the first entry with s_incl > j (six fixed steps, see hb_slot)
@@ -1163,6 +1176,7 @@ __device__ __forceinline__ void hb_wedges(uint64_t total, uint32_t t, const IT* 
     }
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
+      if ((uint32_t)q >= nq) break;
       if constexpr (ALL) f(ok[q], w[q], v[q], e[q]);
       else if constexpr (KD) { if (ok[q]) f(w[q], v[q], e[q], dw[q]); }
       else if (ok[q]) f(w[q], v[q], e[q]);
@@ -1384,10 +1398,13 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
     // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
     // (marking from N(u) measured faster here than a membership-table line per entry)
-    for (uint32_t x0 = 0; x0 < NN; x0 += 64 * HB_UN) {
+    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
+    for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * HB_UN) {
       uint32_t key[HB_UN], sl[HB_UN];
+      const uint32_t nq = min((uint32_t)HB_UN, (NNs - x0 + 63) / 64);
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
+        if ((uint32_t)q >= nq) break;
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
         const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
@@ -1395,6 +1412,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
+        if ((uint32_t)q >= nq) break;
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         if (x < NN && key[q] > s_u[wv][sl[q]]) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
       }
@@ -1406,24 +1424,29 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     // drain: every entry scored for its own row (a list of the claimed slots
     // instead of this scan measured slower: the claims cost more in the insert
     // loop than the scan of empty slots)
-    for (uint32_t i0 = 0; i0 < T; i0 += 64 * HB_UN) {
+    const uint32_t Ts = __builtin_amdgcn_readfirstlane(T);
+    for (uint32_t i0 = 0; i0 < Ts; i0 += 64 * HB_UN) {
       uint32_t kq[HB_UN], c[HB_UN], v0[HB_UN], v1[HB_UN], dw[HB_UN];
+      const uint32_t nq = min((uint32_t)HB_UN, (Ts - i0) / 64);  // T: a power of two >= 64
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
+        if ((uint32_t)q >= nq) break;
         const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
         c[q] = v0[q] = v1[q] = 0;
-        if (CUSTOM) kq[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
-        else kq[q] = i < T ? hp_take<false, false>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+        if (CUSTOM) kq[q] = ho_take(tb, i, &c[q]);
+        else kq[q] = hp_take<false, false>(tb, i, &c[q], &v0[q], &v1[q]);
       }
       if (!CUSTOM) {
 #pragma unroll
         for (int q = 0; q < HB_UN; ++q) {
+          if ((uint32_t)q >= nq) break;
           const uint32_t w = kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u;
           dw[q] = KD ? hp_kd_deg<10>(a.g, c[q], w) : a.g.deg[w];
         }
       }
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
+        if ((uint32_t)q >= nq) break;
         const bool valid = kq[q] != HP_EMPTY;
         const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
         const uint32_t uu = s_u[wv][sl];
@@ -2486,6 +2509,114 @@ __global__ __launch_bounds__(NT) void k_hp_split(const uint32_t* __restrict__ ke
       }
       pa += __popcll(ma);
       pt += __popcll(mt);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- tie selection (hp_prune)
+// The first `quota` ties of the k-th key in (u, w) order, by a radix select
+// over the packed keys (u << vb | w) -- four 13-bit digits from the top,
+// ascending -- instead of sorting every tie: the kept set is all that the
+// prune needs (the final order sorts it).  Needs 2 vb <= 52.
+constexpr int TS_BITS = 13, TS_BINS = 1 << TS_BITS;
+__device__ __forceinline__ uint64_t ts_key(uint64_t k, int vb) { return (k >> 32) << vb | (k & 0xffffffffull); }
+
+// st: [0] prefix (the digits fixed so far), [1] remaining rank (1-based)
+__global__ __launch_bounds__(NT) void k_ts_hist(const uint64_t* __restrict__ tk, uint64_t n, int vb, int shift,
+                                                const uint64_t* __restrict__ st, uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t h[TS_BINS];
+  for (int i = threadIdx.x; i < TS_BINS; i += NT) h[i] = 0;
+  __syncthreads();
+  const uint64_t prefix = st[0];
+  const int ps = shift + TS_BITS;
+  for (uint64_t j = (uint64_t)blockIdx.x * NT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * NT) {
+    const uint64_t k = ts_key(tk[j], vb);
+    if ((k >> ps) == prefix) atomicAdd(&h[(k >> shift) & (TS_BINS - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TS_BINS; i += NT)
+    if (h[i]) atomicAdd(&ghist[i], h[i]);
+}
+
+// One workgroup: the digit whose cumulative count (ascending) reaches the rank.
+__global__ __launch_bounds__(NT) void k_ts_pick(uint32_t* __restrict__ ghist, uint64_t* __restrict__ st) {
+  constexpr int PER = TS_BINS / NT;  // 32 bins per thread
+  __shared__ uint64_t s_w[NWAVE];
+  const int t = threadIdx.x;
+  uint64_t mine = 0;
+  for (int i = 0; i < PER; ++i) mine += ghist[t * PER + i];
+  const uint64_t inc = wave_incl_scan(mine);
+  if (lane_id() == 63) s_w[wave_id()] = inc;
+  __syncthreads();
+  uint64_t pre = 0;
+  for (int q = 0; q < wave_id(); ++q) pre += s_w[q];
+  const uint64_t excl = pre + inc - mine, rank = st[1];
+  __syncthreads();
+  if (excl < rank && rank <= excl + mine) {  // exactly one thread
+    uint64_t rem = rank - excl;
+    int d = t * PER;
+    for (; d < t * PER + PER - 1; ++d) {
+      const uint64_t c = ghist[d];
+      if (c >= rem) break;
+      rem -= c;
+    }
+    st[0] = (st[0] << TS_BITS) | (uint64_t)d;
+    st[1] = rem;
+  }
+  __syncthreads();
+  for (int i = t; i < TS_BINS; i += NT) ghist[i] = 0;  // ready for the next pass
+}
+
+// The ties with packed key <= st[0] (exactly the quota: keys are unique)
+// behind the `above` entries, in any order; one reservation per workgroup tile.
+__global__ __launch_bounds__(NT) void k_ts_take(const uint64_t* __restrict__ tk, const uint32_t* __restrict__ ti,
+                                                uint64_t n, int vb, const uint64_t* __restrict__ st, uint64_t above,
+                                                const uint32_t* __restrict__ key, const uint32_t* __restrict__ u,
+                                                const uint32_t* __restrict__ w, const float* __restrict__ s,
+                                                uint32_t* __restrict__ okey, uint32_t* __restrict__ ou,
+                                                uint32_t* __restrict__ ow, float* __restrict__ os,
+                                                unsigned long long* __restrict__ cnt) {
+  constexpr int IPL = 8;
+  constexpr uint64_t WT = 64 * IPL, BT = WT * NWAVE;
+  __shared__ uint32_t s_n[NWAVE];
+  __shared__ unsigned long long s_base;
+  const uint64_t thr = st[0];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t below = (1ull << lane) - 1;
+  const uint64_t nbt = (n + BT - 1) / BT;
+  for (uint64_t bt = blockIdx.x; bt < nbt; bt += gridDim.x) {
+    const uint64_t base = bt * BT + (uint64_t)wv * WT;
+    bool sel[IPL];
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < IPL; ++r) {
+      const uint64_t j = base + (uint64_t)r * 64 + lane;
+      sel[r] = j < n && ts_key(tk[j], vb) <= thr;
+      c += (uint32_t)__popcll(__ballot(sel[r]));
+    }
+    if (lane == 0) s_n[wv] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (int q = 0; q < NWAVE; ++q) tot += s_n[q];
+      s_base = tot ? atomicAdd(cnt, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long p = s_base;
+    for (int q = 0; q < wv; ++q) p += s_n[q];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < IPL; ++r) {
+      const uint64_t m = __ballot(sel[r]);
+      if (sel[r]) {
+        const uint64_t q = above + p + __popcll(m & below);
+        const uint32_t i = ti[base + (uint64_t)r * 64 + lane];
+        okey[q] = key[i];
+        ou[q] = u[i];
+        ow[q] = w[i];
+        os[q] = s[i];
+      }
+      p += __popcll(m);
     }
   }
 }

@@ -74,7 +74,7 @@ enum Buf {
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
-  B_HP_TCNT, B_HP_TPRE, B_HP_SDO,
+  B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
   NBUF
 };
@@ -257,6 +257,7 @@ struct nlp_graph {
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
+  bool hp_tie_select = true; // prune: the kept ties by radix select, not a sort (NLP_HASH_TIE_SORT=1 sorts)
   bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
@@ -702,6 +703,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
+  if (const char* ht = getenv("NLP_HASH_TIE_SORT")) g->hp_tie_select = ht[0] != '1';
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
     g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
@@ -1457,7 +1459,33 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   *kth = (uint32_t)h[19];
   if (above != h[20] || quota > ties || above + quota != k) return NLP_ERR_DEVICE;
   const uint32_t* take_idx = ti0;
-  if (ties > quota) {
+  const int svb = bits_for(g->span - 1);
+  if (ties > quota && quota > 0 && g->hp_tie_select && 2 * svb <= 4 * TS_BITS) {
+    // the quota smallest ties in (u, w) order by radix select (k_ts_*), in any order
+    uint32_t* th;
+    uint64_t* tst;
+    TRY(wsget(ws, B_TSHIST, TS_BINS, &th));  // zeroed here, then by every k_ts_pick
+    TRY(hipMemsetAsync(th, 0, TS_BINS * 4, st));
+    tst = small + 48;  // [48] prefix, [49] rank, [50] placed count
+    h[24] = 0;
+    h[25] = quota;
+    h[26] = 0;
+    TRY(hipMemcpyAsync(tst, &h[24], 24, hipMemcpyHostToDevice, st));
+    const unsigned gh = (unsigned)std::min<uint64_t>(std::max<uint64_t>(ties / (NT * 16), 1), 1024);
+    for (int d = 3; d >= 0; --d) {
+      hipLaunchKernelGGL(k_ts_hist, dim3(gh), dim3(NT), 0, st, (const uint64_t*)tk0, ties, svb, d * TS_BITS,
+                         (const uint64_t*)tst, th);
+      hipLaunchKernelGGL(k_ts_pick, dim3(1), dim3(NT), 0, st, th, tst);
+      TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_ts_take, dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>(ties / (NT * 8), 1), 2048)),
+                       dim3(NT), 0, st, (const uint64_t*)tk0, (const uint32_t*)ti0, ties, svb, (const uint64_t*)tst,
+                       above, ckey, cu, cw, cs, nk, nu, nw, ns, (unsigned long long*)(tst + 2));
+    TRY(hipGetLastError());
+    TRY(hipMemcpyAsync(&h[27], tst + 2, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (h[27] != quota) return NLP_ERR_DEVICE;
+  } else if (ties > quota) {
     // canonical tie order: (u asc, w asc)
     TRY(wsget(ws, B_HP_TIEK1, ties, &tk1));
     TRY(wsget(ws, B_HP_TIEI1, ties, &ti1));
@@ -1469,7 +1497,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
     { nlp_status so = sort_pairs_os(g, tk0, ti0, tk1, ti1, ties, shifts, np, &which, st); if (so != NLP_OK) return so; }
     take_idx = which ? ti1 : ti0;
   }
-  if (quota)
+  if (quota && !(ties > quota && g->hp_tie_select && 2 * svb <= 4 * TS_BITS))
     LAUNCH(k_hp_take, quota, st, take_idx, quota, above, ckey, cu, cw, cs, nk, nu, nw, ns);
   TRY(hipGetLastError());
   std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
