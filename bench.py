@@ -42,7 +42,7 @@ import nlp_loader  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 HOT_KERNELS = {1: "k_sp_bucket", 2: "k_sp_scan<F_Runs>", 3: "k_group_tiles", 4: "k_sp_survivors",
                5: "k_sp_expand", 6: "k_sp_pass", 7: "k_sp_runs", 8: "k_sp_group",
-               9: "k_sp_grouprun"}
+               9: "k_sp_grouprun", 10: "k_sp_exbucket"}
 METRIC_NAMES = {"CN": "CommonNeighbors", "JAC": "JaccardCoefficient", "SOR": "SorensenIndex",
                 "SAL": "SaltonCosineSimilarity", "HPI": "HubPromoted", "HDI": "HubDepressed",
                 "LHN": "LeichtHolmeNermanScore", "AA": "AdamicAdarCoefficient", "RA": "ResourceAllocationScore"}

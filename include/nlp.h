@@ -96,7 +96,7 @@ typedef struct {
   uint64_t hot_bytes;       /* algorithmic bytes of that launch */
   uint32_t hot_kernel;      /* which kernel hot_ms times: 1 k_sp_bucket, 2 k_sp_scan<F_Runs>,
                                3 k_group_tiles, 4 k_sp_survivors, 5 k_sp_expand, 6 k_sp_pass,
-                               7 k_sp_runs, 8 k_sp_group, 9 k_sp_grouprun; 0 none */
+                               7 k_sp_runs, 8 k_sp_group, 9 k_sp_grouprun, 10 k_sp_exbucket; 0 none */
 } nlp_timing;
 
 typedef struct nlp_graph nlp_graph;

@@ -71,7 +71,7 @@ struct HpArgs {
   uint64_t sua;
   int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
   const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
-  const uint64_t* sdo;   // S(u) entries packed deg v << HP_SDO_SH | off[v] (degree-class lists; null: none)
+  const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
 };
 constexpr int HP_SDO_SH = 40;  // offsets < 2^40 (guarded at the list build)
 
@@ -770,18 +770,29 @@ __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __res
 }
 
 // tpre: exclusive prefix of the tile counts (tile - t0 indexed)
-// (sdo: also deg v << HP_SDO_SH | off[v] per entry, so that the row batches
-// skip the gather of v's row bounds; the class is the exact degree here)
-__global__ __launch_bounds__(NT) void k_hp_dcls_fill(const uint32_t* __restrict__ keys,
-                                                     const uint8_t* __restrict__ dcls, uint32_t H, uint64_t e0,
-                                                     uint64_t e1, const uint64_t* __restrict__ tpre,
-                                                     uint32_t* __restrict__ skeys, const uint64_t* __restrict__ off,
-                                                     uint64_t* __restrict__ sdo) {
+// (sdo: also the entry packed for the row batches, deg v << 48 | n << 40 | o,
+// where [o, o + n) is the part of N(v) above the entry's row u -- found here
+// by a binary search of v's short list (deg v <= 254) -- so that the batches
+// enumerate only the wedges w > u and skip the gather of v's row bounds; and
+// W+(u) = the sum of n over S(u), accumulated into wu (zeroed by the caller):
+// a tighter bound than W(u) for the bins, the tables and the batch budget)
+__global__ __launch_bounds__(NT) void k_hp_dcls_fill(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                     uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                     const uint32_t* __restrict__ tile_row,
+                                                     const uint64_t* __restrict__ tpre, uint32_t* __restrict__ skeys,
+                                                     uint64_t* __restrict__ sdo, unsigned long long* __restrict__ wu) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
   const int lane = lane_id(), wv = wave_id();
   const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  s_acc[wv][lane] = 0;
   for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
     const uint64_t base = tile * HP_WTILE;
     uint64_t pos = tpre[tile - t0];
+    const uint64_t tr = tile_row[tile];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;  // first row of the tile inside the range
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < nU ? g.off[ua + rl + 1] : ~0ull;
+    const uint64_t last_end = __shfl(rend, 63, 64);
     uint32_t c[HP_WR];
 #pragma unroll
     for (int i = 0; i < HP_WR; ++i) {
@@ -791,15 +802,68 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill(const uint32_t* __restrict_
 #pragma unroll
     for (int i = 0; i < HP_WR; ++i) {
       const uint64_t e = base + (uint64_t)i * 64 + lane;
-      const bool s = hp_dsurv(c[i], H);
-      const uint64_t m = __ballot(s);
-      if (s) {
-        const uint64_t q = pos + (uint64_t)__popcll(m & ((1ull << lane) - 1));
-        const uint32_t v = keys[e];
-        skeys[q] = v;
-        if (sdo) sdo[q] = (uint64_t)c[i] << HP_SDO_SH | off[v];
+      const bool sv = hp_dsurv(c[i], H);
+      const uint64_t m = __ballot(sv);
+      if (m) {
+        int lo = 0, hi = 64;  // local row of e
+        while (lo < hi) {
+          const int md = (lo + hi) >> 1;
+          const uint64_t x = __shfl(rend, md, 64);
+          if (x <= e) lo = md + 1; else hi = md;
+        }
+        if (sv) {
+          const uint64_t q = pos + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+          const uint32_t v = g.keys[e];
+          skeys[q] = v;
+          if (sdo) {
+            uint64_t r = r0 + lo;
+            if (e >= last_end) {  // more than 64 rows in this tile: search the offsets
+              uint64_t a = r0, b = nU;
+              while (b - a > 1) {
+                const uint64_t md = (a + b) >> 1;
+                if (g.off[ua + md] <= e) a = md; else b = md;
+              }
+              r = a;
+            }
+            const uint32_t u = (uint32_t)(ua + r);
+            const uint64_t o = g.off[v];
+            uint32_t l = 0;  // the first entry of N(v) above u
+            if (c[i] <= 16) {  // short lists: count the entries <= u with independent loads (one round trip)
+              uint32_t kk[16];
+#pragma unroll
+              for (int q = 0; q < 16; ++q) kk[q] = (uint32_t)q < c[i] ? g.keys[o + q] : 0xffffffffu;
+#pragma unroll
+              for (int q = 0; q < 16; ++q) l += kk[q] <= u ? 1u : 0u;
+            } else {
+              uint32_t h = c[i];
+              while (l < h) {
+                const uint32_t md = (l + h) >> 1;
+                if (g.keys[o + md] <= u) l = md + 1; else h = md;
+              }
+            }
+            const uint32_t n = c[i] - l;
+            sdo[q] = (uint64_t)c[i] << 48 | (uint64_t)n << HP_SDO_SH | (o + l);
+            if (n) {
+              if (e < last_end) atomicAdd(&s_acc[wv][lo], (unsigned long long)n);
+              else atomicAdd(&wu[r], (unsigned long long)n);
+            }
+          }
+        }
       }
       pos += (uint64_t)__popcll(m);
+    }
+    if (sdo) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      const unsigned long long x = s_acc[wv][lane];
+      if (x) {
+        atomicAdd(&wu[rl], x);
+        s_acc[wv][lane] = 0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     }
   }
 }
@@ -1031,18 +1095,27 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       fh = s_sk[wv];
     }
     uint32_t round = 0;
+    // packed survivor entries (the part of N(v) above u, no row-bound gather)
+    const uint64_t* fd = a.sdo && fh != s_sk[wv] && a.soff ? a.sdo + (fh - a.skeys) : nullptr;
     for (uint64_t base = 0; base < nf; base += 64) {
       const uint64_t i = base + lane;
       uint32_t len = 0, v = 0;
       uint64_t st = 0;
       double cv = 0.0;
       if (i < nf) {
-        v = fh[i];
-        const uint32_t d = a.g.deg[v];
-        if (hp_surv(d, a.H)) {
-          len = d;
-          st = a.g.off[v];
-          if (CUSTOM) cv = a.g.ctab[d];
+        if (fd) {
+          const uint64_t x = fd[i];
+          len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+          st = x & ((1ull << HP_SDO_SH) - 1);
+          if (CUSTOM) cv = a.g.ctab[x >> 48];
+        } else {
+          v = fh[i];
+          const uint32_t d = a.g.deg[v];
+          if (hp_surv(d, a.H)) {
+            len = d;
+            st = a.g.off[v];
+            if (CUSTOM) cv = a.g.ctab[d];
+          }
         }
       }
       const uint32_t incl = (uint32_t)wave_incl_scan(len);
@@ -1333,9 +1406,9 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
           slot = hb_slot(s_sp[wv], nr, e);
           const uint32_t ex = slot ? s_sp[wv][slot - 1] : 0u;
           const uint64_t x = a.sdo[s_s0[wv][slot] + (e - ex)];
-          len = (uint32_t)(x >> HP_SDO_SH);
+          len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;  // the part of N(v) above u
           st = x & ((1ull << HP_SDO_SH) - 1);
-          if (CUSTOM) cv = a.g.ctab[len];
+          if (CUSTOM) cv = a.g.ctab[x >> 48];
         } else {
           if (CUSTOM) {
             const uint32_t key = s_sk[wv][e];
@@ -1589,6 +1662,8 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
       fh = s_sk;
     }
     uint32_t round = 0;
+    // packed survivor entries (the part of N(v) above u, no row-bound gather)
+    const uint64_t* fd = a.sdo && a.soff && fh != (const uint32_t*)s_sk ? a.sdo + (fh - a.skeys) : nullptr;
     for (uint64_t p = 0; p < passes; ++p) {
       const uint64_t wlo = (uint64_t)u + 1 + p * rw;
       const uint64_t whi = wlo + rw < a.S ? wlo + rw : a.S;
@@ -1598,12 +1673,19 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
         uint64_t len = 0, st = 0;
         double cv = 0.0;
         if (i < nf) {
-          v = fh[i];
-          const uint32_t d = a.g.deg[v];
-          if (hp_surv(d, a.H)) {
-            len = d;
-            st = a.g.off[v];
-            if (ORD) cv = a.g.ctab[d];
+          if (fd) {
+            const uint64_t x = fd[i];
+            len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+            st = x & ((1ull << HP_SDO_SH) - 1);
+            if (ORD) cv = a.g.ctab[x >> 48];
+          } else {
+            v = fh[i];
+            const uint32_t d = a.g.deg[v];
+            if (hp_surv(d, a.H)) {
+              len = d;
+              st = a.g.off[v];
+              if (ORD) cv = a.g.ctab[d];
+            }
           }
         }
         const uint64_t incl = block_incl_scan_1024(len, s_w);
@@ -2039,6 +2121,7 @@ __device__ __forceinline__ void hh_enum_item(const HpArgs& a, uint32_t u, uint64
   const uint32_t* fh;
   uint64_t nf;
   hp_first_hops(a, u, a.g.off[u], a.g.off[u + 1] - a.g.off[u], &fh, &nf);
+  const uint64_t* fd = a.sdo && a.soff ? a.sdo + (fh - a.skeys) : nullptr;  // packed: N(v) above u
   if (f1 > nf) f1 = nf;
   for (uint64_t base = f0; base < f1; base += HH_NT) {
     const uint64_t i = base + t;
@@ -2046,10 +2129,16 @@ __device__ __forceinline__ void hh_enum_item(const HpArgs& a, uint32_t u, uint64
     uint64_t len = 0, st = 0;
     if (i < f1) {
       v = fh[i];
-      const uint32_t d = a.g.deg[v];
-      if (hp_surv(d, a.H)) {
-        len = d;
-        st = a.g.off[v];
+      if (fd) {
+        const uint64_t x = fd[i];
+        len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+        st = x & ((1ull << HP_SDO_SH) - 1);
+      } else {
+        const uint32_t d = a.g.deg[v];
+        if (hp_surv(d, a.H)) {
+          len = d;
+          st = a.g.off[v];
+        }
       }
     }
     const uint64_t incl = block_incl_scan_1024(len, s_w);

@@ -1760,10 +1760,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
-      if (g->hp_sdo && g->nnz < (1ull << HP_SDO_SH))
+      if (g->hp_sdo && g->nnz < (1ull << HP_SDO_SH)) {
         TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(g->host_small[10], 1), &s_sdo));
-      hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, (const uint32_t*)g->keys, (const uint8_t*)g->dcls,
-                         p.H, e0, e1, (const uint64_t*)tpre, s_skeys, (const uint64_t*)g->off, s_sdo);
+        TRY(hipMemsetAsync(wu, 0, nU * 8, st));  // W+(u), accumulated by the fill
+      }
+      hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                         (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
+                         (unsigned long long*)wu);
       TRY(hipGetLastError());
       s_sorted = true;
     } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
@@ -2394,9 +2397,18 @@ int sp_hot_default(const SpBufs& f) {
 
 // Algorithmic bytes of one launch of sort-path stage `s`,
 // from the call's own counters (host copy of the arena counters).
-uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64_t* h) {
+uint64_t sp_stage_bytes(const nlp_graph* g, const SpBufs& f, int s, const uint64_t* h, uint32_t H) {
   const uint64_t S = g->span, V = h[C_NV], W = h[C_W], C = h[C_C];
   if (s == 1) return 4 * S + 4 * V;             // deg read, survivor ids written
+  if (s == 2 && f.fused && f.dindex && g->sv_pack) {
+    // k_sp_exbucket over the degree-class index: survivor id + packed row (and
+    // in-row when asymmetric) per survivor, the survivors' lists (P_H =
+    // sum of d n_d over 1 <= d <= H; in-lists counted alike), 8-byte records
+    uint64_t P = 0;
+    for (uint64_t d = 1; d <= H && d < g->deg_hist.size(); ++d) P += d * g->deg_hist[d];
+    const uint64_t asym = g->sv_pack_in ? 1 : 0;
+    return (12 + 8 * asym) * V + 4 * (1 + asym) * P + 8 * W;
+  }
   if (s == 2) return 4 * V + 4 * V + 16 * V + 8 * V + 4 * W + 12 * W;  // ids, deg, toff pair, off, keys, records
   const int P = f.msd ? f.msd_passes : f.passes;
   if (s >= 4 && s < 4 + P) return 24 * W;  // records in + out
@@ -3161,11 +3173,11 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       if (sorted) {
         const int s_runs = 4 + (sp.msd ? sp.msd_passes : sp.passes) + (sp.split ? 1 : 0);
         const int hs = g->hot_stage < 0 ? sp_hot_default(sp) : std::min(std::max(g->hot_stage, 1), s_runs);
-        t->hot_bytes = sp_stage_bytes(g, sp, hs, h);
+        t->hot_bytes = sp_stage_bytes(g, sp, hs, h, p.H);
         t->hot_kernel = (sp.fused && hs == s_runs - 1) ? 9u
                         : hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
                         : (sp.split && hs == s_runs - 1) ? (sp.msd_passes == 1 && g->group_sort != 1 && !sp.direct ? 1u : 8u)
-                        : hs == 1 ? 4u : hs == 2 ? 5u : hs >= 4 ? 6u : 0u;
+                        : hs == 1 ? 4u : hs == 2 ? (sp.fused ? 10u : 5u) : hs >= 4 ? 6u : 0u;
       } else {
         // k_group_tiles: bucket counts, records, flags, runs
         t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];

@@ -3,7 +3,7 @@
 deletion -- beyond 2^31, so every signed 32-bit index in the kernels would
 show here) through the HIP path, checked exactly (order included) against the
 parallel oracle for the bench call (LHub-4 Jaccard, main.cxx:50) and its
-neighbours in the MINDEGREE1 sweep (main.cxx:67-80)."""
+neighbours in the MINDEGREE1 sweep (main.cxx:67-80), including H = 16 on path 4."""
 import numpy as np
 import pytest
 
@@ -69,3 +69,19 @@ def test_gpu_c4_common_neighbors_h8(c4, oracle):
 @pytest.mark.timeout(300)
 def test_gpu_c4_adamic_adar_h4(c4, oracle):
     _check(c4, oracle, 7, 4)
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_jaccard_h16_hash_path(c4, oracle):
+    """The hash accumulation (path 4: degree-class survivor lists with packed
+    above-u suffixes, row batches, hub pass, radix-selected ties, fused final
+    order) over offsets beyond 2^32; k = 1.9e8 of 2.8e8 candidates."""
+    n, t = _check(c4, oracle, 1, 16)
+    assert t["path"] == 4 and n == c4.k
+
+
+@pytest.mark.timeout(300)
+def test_gpu_c4_adamic_adar_h16_hash_path(c4, oracle):
+    """Adamic-Adar on path 4 at the same size (ordered accumulation, hub sort mode)."""
+    n, t = _check(c4, oracle, 7, 16)
+    assert t["path"] == 4 and n == c4.k
