@@ -770,6 +770,55 @@ __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __res
 }
 
 // tpre: exclusive prefix of the tile counts (tile - t0 indexed)
+// Per graph: for every entry e = (u -> v) with deg v <= 254, the number of
+// entries of N(v) at or below u (its rank there; u8) -- the survivor lists'
+// fill reads it instead of searching N(v) on every call.
+__global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __restrict__ dcls, uint64_t S,
+                                                 uint64_t M, const uint32_t* __restrict__ tile_row,
+                                                 uint8_t* __restrict__ out) {
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t nt = (M + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t tile = (uint64_t)blockIdx.x * NWAVE + wv; tile < nt; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t r0 = tile_row[tile];
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < S ? g.off[rl + 1] : ~0ull;
+    const uint64_t last_end = __shfl(rend, 63, 64);
+#pragma unroll 1
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      const uint32_t c = e < M ? (uint32_t)dcls[e] : 0u;
+      int lo = 0, hi = 64;
+      while (lo < hi) {
+        const int md = (lo + hi) >> 1;
+        const uint64_t x = __shfl(rend, md, 64);
+        if (x <= e) lo = md + 1; else hi = md;
+      }
+      if (c == 0 || c > HP_DCLS_MAX) {
+        if (e < M) out[e] = 0;
+        continue;
+      }
+      uint64_t r = r0 + lo;
+      if (e >= last_end) {
+        uint64_t a = r0, b = S;
+        while (b - a > 1) {
+          const uint64_t md = (a + b) >> 1;
+          if (g.off[md] <= e) a = md; else b = md;
+        }
+        r = a;
+      }
+      const uint32_t u = (uint32_t)r, v = g.keys[e];
+      const uint64_t o = g.off[v];
+      uint32_t l = 0, h = c;
+      while (l < h) {
+        const uint32_t md = (l + h) >> 1;
+        if (g.keys[o + md] <= u) l = md + 1; else h = md;
+      }
+      out[e] = (uint8_t)l;
+    }
+  }
+}
+
 // (sdo: also the entry packed for the row batches, deg v << 48 | n << 40 | o,
 // where [o, o + n) is the part of N(v) above the entry's row u -- found here
 // by a binary search of v's short list (deg v <= 254) -- so that the batches
@@ -780,7 +829,8 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill(GraphView g, const uint8_t*
                                                      uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
                                                      const uint32_t* __restrict__ tile_row,
                                                      const uint64_t* __restrict__ tpre, uint32_t* __restrict__ skeys,
-                                                     uint64_t* __restrict__ sdo, unsigned long long* __restrict__ wu) {
+                                                     uint64_t* __restrict__ sdo, unsigned long long* __restrict__ wu,
+                                                     const uint8_t* __restrict__ drank) {
   __shared__ unsigned long long s_acc[NWAVE][64];
   const int lane = lane_id(), wv = wave_id();
   const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
@@ -828,7 +878,9 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill(GraphView g, const uint8_t*
             const uint32_t u = (uint32_t)(ua + r);
             const uint64_t o = g.off[v];
             uint32_t l = 0;  // the first entry of N(v) above u
-            if (c[i] <= 16) {  // short lists: count the entries <= u with independent loads (one round trip)
+            if (drank) {
+              l = drank[e];
+            } else if (c[i] <= 16) {  // short lists: count the entries <= u with independent loads (one round trip)
               uint32_t kk[16];
 #pragma unroll
               for (int q = 0; q < 16; ++q) kk[q] = (uint32_t)q < c[i] ? g.keys[o + q] : 0xffffffffu;
@@ -1395,6 +1447,24 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       wave_sync_lds();
       if (!a.ssorted) wave_bitonic_u32(s_sk[wv], n2);
     }
+    // the first exclusion block's keys of N(u), issued now: in flight during the
+    // wedge phase instead of a round trip of their own after it
+    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
+    uint32_t xkey[HB_UN], xsl[HB_UN];
+    {
+      const uint32_t nq = min((uint32_t)HB_UN, (NNs + 63) / 64);
+#pragma unroll
+      for (int q = 0; q < HB_UN; ++q) {
+        xkey[q] = 0u;
+        xsl[q] = 0u;
+        if ((uint32_t)q < nq) {
+          const uint32_t x = (uint32_t)q * 64 + (uint32_t)lane;
+          xsl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
+          const uint32_t ex = xsl[q] ? s_np[wv][xsl[q] - 1] : 0u;
+          xkey[q] = x < NN ? a.g.keys[s_o0[wv][xsl[q]] + (x - ex)] : 0u;
+        }
+      }
+    }
     // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
     for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
       const uint32_t e = e0 + (uint32_t)lane;
@@ -1471,17 +1541,24 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
     // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
     // (marking from N(u) measured faster here than a membership-table line per entry)
-    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
     for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * HB_UN) {
       uint32_t key[HB_UN], sl[HB_UN];
       const uint32_t nq = min((uint32_t)HB_UN, (NNs - x0 + 63) / 64);
+      if (x0 == 0) {
 #pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
-        if ((uint32_t)q >= nq) break;
-        const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
-        sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
-        const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
-        key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
+        for (int q = 0; q < HB_UN; ++q) {
+          key[q] = xkey[q];
+          sl[q] = xsl[q];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < HB_UN; ++q) {
+          if ((uint32_t)q >= nq) break;
+          const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
+          sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
+          const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
+          key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
+        }
       }
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {

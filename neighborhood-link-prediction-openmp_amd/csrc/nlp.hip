@@ -239,6 +239,7 @@ struct nlp_graph {
   uint32_t* tile_row = nullptr;                // row of the first entry of every HP_WTILE-entry tile
   uint8_t* dcls = nullptr;                     // min(deg keys[e], 255) per adjacency entry (path 4's survivor lists)
   uint32_t* kdeg = nullptr;                    // deg keys[e] per adjacency entry (path 4's count-metric row kernels)
+  uint8_t* drank = nullptr;                    // entries with deg v <= 254: the row's rank in N(v) (survivor suffixes)
   // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
   uint64_t* truth = nullptr;
   uint64_t ntruth = 0;
@@ -374,6 +375,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->tile_row) (void)hipFree(g->tile_row);
   if (g->dcls) (void)hipFree(g->dcls);
   if (g->kdeg) (void)hipFree(g->kdeg);
+  if (g->drank) (void)hipFree(g->drank);
   if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
@@ -566,6 +568,23 @@ nlp_status finish_graph(nlp_graph* g) {
       }
       LAUNCH(k_hp_dcls, M, st, (const uint32_t*)g->keys, (const uint32_t*)g->deg, M, g->dcls, g->kdeg);
       TRY(hipGetLastError());
+      // and the rank of every short-list entry's row in the list (k_hp_drank)
+      const char* hdr = getenv("NLP_HASH_DRANK");
+      if (!(hdr && hdr[0] == '0')) {
+        if (hipMalloc(&g->drank, M) == hipSuccess) {
+          GraphView gv0{};
+          gv0.off = g->off;
+          gv0.keys = g->keys;
+          gv0.deg = g->deg;
+          const unsigned gd = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 16384);
+          hipLaunchKernelGGL(k_hp_drank, dim3(gd), dim3(NT), 0, st, gv0, (const uint8_t*)g->dcls, S, M,
+                             (const uint32_t*)g->tile_row, g->drank);
+          TRY(hipGetLastError());
+        } else {
+          (void)hipGetLastError();
+          g->drank = nullptr;
+        }
+      }
     } else {
       (void)hipGetLastError();
       g->dcls = nullptr;
@@ -1766,7 +1785,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       }
       hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
                          (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
-                         (unsigned long long*)wu);
+                         (unsigned long long*)wu, (const uint8_t*)g->drank);
       TRY(hipGetLastError());
       s_sorted = true;
     } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
