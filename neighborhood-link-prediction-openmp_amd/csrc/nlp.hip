@@ -74,7 +74,7 @@ enum Buf {
   // hash path (hashpath.hpp)
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
-  B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST,
+  B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
   NBUF
 };
@@ -1664,7 +1664,11 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint64_t*)ibase, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
                        (uint32_t*)nullptr);
   TRY(hipGetLastError());
-  TRY(scan_excl_u64<uint32_t>(bcnt, NB, boff, boff + NB, scan, st));
+  // the buckets can outnumber the chunk's rows (the caller's scan scratch is
+  // sized for those): a scratch of their own
+  uint64_t* bscan;
+  TRY(wsget(ws, B_HH_SCAN, scan_scratch_words(NB + 1) + 16, &bscan));
+  TRY(scan_excl_u64<uint32_t>(bcnt, NB, boff, boff + NB, bscan, st));
   TRY(hipMemcpyAsync(&g->host_small[50], boff + NB, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
   const uint64_t tot = g->host_small[50];

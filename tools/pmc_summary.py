@@ -18,7 +18,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_sp_cpass0", "k_sp_cpass", "k_sp_grouprun", "k_sp_exbucket", "k_sp_gather", "k_sp_arena_init", "k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
+KERNELS = ["k_sp_order_rank", "k_sp_cpass0", "k_sp_cpass", "k_sp_grouprun", "k_sp_exbucket", "k_sp_gather", "k_sp_arena_init", "k_sp_runs", "k_sp_bucket", "k_sp_survivors", "k_sp_expand", "k_sp_pass", "k_group_tiles", "k_p1_pass", "k_rts_scan", "k_rts_reduce", "k_os_pass", "k_score_runs", "k_gather_sel",
            "k_desc_keys_sel", "k_sel_hist"]
 
 
