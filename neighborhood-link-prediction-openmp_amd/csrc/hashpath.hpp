@@ -1447,24 +1447,6 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       wave_sync_lds();
       if (!a.ssorted) wave_bitonic_u32(s_sk[wv], n2);
     }
-    // the first exclusion block's keys of N(u), issued now: in flight during the
-    // wedge phase instead of a round trip of their own after it
-    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
-    uint32_t xkey[HB_UN], xsl[HB_UN];
-    {
-      const uint32_t nq = min((uint32_t)HB_UN, (NNs + 63) / 64);
-#pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
-        xkey[q] = 0u;
-        xsl[q] = 0u;
-        if ((uint32_t)q < nq) {
-          const uint32_t x = (uint32_t)q * 64 + (uint32_t)lane;
-          xsl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
-          const uint32_t ex = xsl[q] ? s_np[wv][xsl[q] - 1] : 0u;
-          xkey[q] = x < NN ? a.g.keys[s_o0[wv][xsl[q]] + (x - ex)] : 0u;
-        }
-      }
-    }
     // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
     for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
       const uint32_t e = e0 + (uint32_t)lane;
@@ -1541,24 +1523,19 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
     // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
     // (marking from N(u) measured faster here than a membership-table line per entry)
+    // (prefetching the first block of these keys during the wedge phase measured
+    // slower: 46.6 -> 52.7 ms on C3 JAC H=16)
+    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
     for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * HB_UN) {
       uint32_t key[HB_UN], sl[HB_UN];
       const uint32_t nq = min((uint32_t)HB_UN, (NNs - x0 + 63) / 64);
-      if (x0 == 0) {
 #pragma unroll
-        for (int q = 0; q < HB_UN; ++q) {
-          key[q] = xkey[q];
-          sl[q] = xsl[q];
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < HB_UN; ++q) {
-          if ((uint32_t)q >= nq) break;
-          const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
-          sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
-          const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
-          key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
-        }
+      for (int q = 0; q < HB_UN; ++q) {
+        if ((uint32_t)q >= nq) break;
+        const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
+        sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
+        const uint32_t ex = sl[q] ? s_np[wv][sl[q] - 1] : 0u;
+        key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
       }
 #pragma unroll
       for (int q = 0; q < HB_UN; ++q) {
