@@ -761,6 +761,74 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_rows(GraphView g, const uint8_t*
   }
 }
 
+// The same per-row (count, W) and tile counts with eight consecutive entries
+// per lane (one 8-byte load of classes): a lane finds the row of its first
+// entry once (six LDS steps) and walks forward over the row ends, adding runs
+// of one row with one LDS atomic, instead of a search per entry.
+__global__ __launch_bounds__(NT) void k_hp_dcls_rows8(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                      uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                      const uint32_t* __restrict__ tile_row,
+                                                      unsigned long long* __restrict__ wu, uint32_t* __restrict__ tcnt) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
+  __shared__ uint64_t s_end[NWAVE][64];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  s_acc[wv][lane] = 0;
+  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t tr = tile_row[tile];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;
+    const uint64_t rl = r0 + lane;
+    s_end[wv][lane] = rl < nU ? g.off[ua + rl + 1] : ~0ull;
+    wave_sync_lds();
+    const uint64_t last_end = s_end[wv][63];
+    const uint64_t eb = base + (uint64_t)lane * 8;  // this lane's 8 entries
+    uint64_t word = 0;
+    if (eb + 8 <= e1 && eb >= e0) word = *(const uint64_t*)(dcls + eb);
+    else
+      for (int q = 0; q < 8; ++q)
+        if (eb + q >= e0 && eb + q < e1) word |= (uint64_t)dcls[eb + q] << (8 * q);
+    uint32_t tc = 0;
+    int idx = 0;  // local row of the current entry: the number of row ends <= e
+#pragma unroll
+    for (uint32_t bit = 32; bit > 0; bit >>= 1) idx += s_end[wv][idx + bit - 1] <= eb ? (int)bit : 0;
+    unsigned long long run = 0;
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t e = eb + q;
+      const uint32_t c = (uint32_t)(word >> (8 * q)) & 0xffu;
+      const bool sv = e >= e0 && e < e1 && hp_dsurv(c, H);
+      while (idx < 64 && s_end[wv][idx] <= e) {  // the entry starts a later row: flush the run
+        if (run) atomicAdd(&s_acc[wv][idx], run);
+        run = 0;
+        ++idx;
+      }
+      if (!sv) continue;
+      ++tc;
+      const unsigned long long add = (1ull << 40) | c;
+      if (e < last_end) {
+        run += add;
+      } else {  // more than 64 rows in this tile: search the offsets
+        uint64_t a = r0, b = nU;
+        while (b - a > 1) {
+          const uint64_t md = (a + b) >> 1;
+          if (g.off[ua + md] <= e) a = md; else b = md;
+        }
+        atomicAdd(&wu[a], add);
+      }
+    }
+    if (run && idx < 64) atomicAdd(&s_acc[wv][idx], run);
+    tc = (uint32_t)wave_sum((uint64_t)tc);
+    if (lane == 0) tcnt[tile - t0] = tc;
+    wave_sync_lds();
+    const unsigned long long v = s_acc[wv][lane];
+    if (v) {
+      atomicAdd(&wu[rl], v);
+      s_acc[wv][lane] = 0;
+    }
+    wave_sync_lds();
+  }
+}
+
 __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __restrict__ cnt, uint64_t nU) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nU; r += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long x = wu[r];

@@ -425,7 +425,8 @@ class _env:
 # 21 the held candidates ordered by (u, w) permutation + order_v1 (before hp_final_order),
 # 22 row batches gathering deg / off of every first hop (no packed survivor entries),
 # 23 the prune's kept ties by a full (u, w) sort instead of the radix select,
-# 24 survivor suffixes searched per call (no per-graph rank bytes)
+# 24 survivor suffixes searched per call (no per-graph rank bytes), 25 survivor
+# counts with eight consecutive entries per lane (k_hp_dcls_rows8)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -440,7 +441,7 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_FINAL="0"), dict(NLP_HASH_SDO="0"), dict(NLP_HASH_TIE_SORT="1"),
-                 dict(NLP_HASH_DRANK="0")]
+                 dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ROWS8="1")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
