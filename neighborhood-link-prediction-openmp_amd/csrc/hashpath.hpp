@@ -988,6 +988,93 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill(GraphView g, const uint8_t*
   }
 }
 
+// k_hp_dcls_fill with eight consecutive entries per lane (the layout of
+// k_hp_dcls_rows8): one 8-byte load of classes and of ranks, the lane's
+// survivors placed at a wave scan of the per-lane counts, the row of the
+// lane's first entry found once and walked forward.  Needs sdo and drank.
+__global__ __launch_bounds__(NT) void k_hp_dcls_fill8(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                      uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                      const uint32_t* __restrict__ tile_row,
+                                                      const uint64_t* __restrict__ tpre, uint32_t* __restrict__ skeys,
+                                                      uint64_t* __restrict__ sdo, unsigned long long* __restrict__ wu,
+                                                      const uint8_t* __restrict__ drank) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
+  __shared__ uint64_t s_end[NWAVE][64];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  s_acc[wv][lane] = 0;
+  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t tr = tile_row[tile];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;
+    const uint64_t rl = r0 + lane;
+    s_end[wv][lane] = rl < nU ? g.off[ua + rl + 1] : ~0ull;
+    wave_sync_lds();
+    const uint64_t last_end = s_end[wv][63];
+    const uint64_t eb = base + (uint64_t)lane * 8;
+    uint64_t word = 0, rk = 0;
+    if (eb + 8 <= e1 && eb >= e0) {
+      word = *(const uint64_t*)(dcls + eb);
+      rk = *(const uint64_t*)(drank + eb);
+    } else {
+      for (int q = 0; q < 8; ++q)
+        if (eb + q >= e0 && eb + q < e1) {
+          word |= (uint64_t)dcls[eb + q] << (8 * q);
+          rk |= (uint64_t)drank[eb + q] << (8 * q);
+        }
+    }
+    uint32_t mine = 0;  // survivors among this lane's entries (in range)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t e = eb + q;
+      mine += (e >= e0 && e < e1 && hp_dsurv((uint32_t)(word >> (8 * q)) & 0xffu, H)) ? 1u : 0u;
+    }
+    uint64_t pos = tpre[tile - t0] + wave_incl_scan((uint64_t)mine) - mine;
+    int idx = 0;
+#pragma unroll
+    for (uint32_t bit = 32; bit > 0; bit >>= 1) idx += s_end[wv][idx + bit - 1] <= eb ? (int)bit : 0;
+    unsigned long long run = 0;
+    for (int q = 0; q < 8; ++q) {
+      const uint64_t e = eb + q;
+      const uint32_t c = (uint32_t)(word >> (8 * q)) & 0xffu;
+      while (idx < 64 && s_end[wv][idx] <= e) {
+        if (run) atomicAdd(&s_acc[wv][idx], run);
+        run = 0;
+        ++idx;
+      }
+      if (!(e >= e0 && e < e1 && hp_dsurv(c, H))) continue;
+      uint64_t r = r0 + (uint64_t)idx;
+      if (e >= last_end) {
+        uint64_t a = r0, b = nU;
+        while (b - a > 1) {
+          const uint64_t md = (a + b) >> 1;
+          if (g.off[ua + md] <= e) a = md; else b = md;
+        }
+        r = a;
+      }
+      const uint32_t v = g.keys[e];
+      const uint32_t l = (uint32_t)(rk >> (8 * q)) & 0xffu;
+      const uint64_t o = g.off[v];
+      const uint32_t n = c - l;
+      skeys[pos] = v;
+      sdo[pos] = (uint64_t)c << 48 | (uint64_t)n << HP_SDO_SH | (o + l);
+      ++pos;
+      if (n) {
+        if (e < last_end) run += n;
+        else atomicAdd(&wu[r], (unsigned long long)n);
+      }
+    }
+    if (run && idx < 64) atomicAdd(&s_acc[wv][idx], run);
+    wave_sync_lds();
+    const unsigned long long x = s_acc[wv][lane];
+    if (x) {
+      atomicAdd(&wu[rl], x);
+      s_acc[wv][lane] = 0;
+    }
+    wave_sync_lds();
+  }
+}
+
 // The same W(u) from the survivors' side, for small H: the surviving
 // intermediates are a prefix of the degree-class index (vbydeg, degrees 1..H),
 // and every entry u of I(v) (the transposed multiset: one per occurrence of v

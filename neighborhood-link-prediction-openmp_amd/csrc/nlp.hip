@@ -1793,9 +1793,14 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(g->host_small[10], 1), &s_sdo));
         TRY(hipMemsetAsync(wu, 0, nU * 8, st));  // W+(u), accumulated by the fill
       }
-      hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
-                         (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
-                         (unsigned long long*)wu, (const uint8_t*)g->drank);
+      if (g->hp_rows8 && s_sdo && g->drank)
+        hipLaunchKernelGGL(k_hp_dcls_fill8, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0,
+                           e1, (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
+                           (unsigned long long*)wu, (const uint8_t*)g->drank);
+      else
+        hipLaunchKernelGGL(k_hp_dcls_fill, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                           (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
+                           (unsigned long long*)wu, (const uint8_t*)g->drank);
       TRY(hipGetLastError());
       s_sorted = true;
     } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
