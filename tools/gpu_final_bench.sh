@@ -19,6 +19,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
   python3 $REPO/bench.py --steps 20 --warmup 3 --no-cpu-baseline --sweep = > $OUT/prof_bench.json 2> $OUT/prof_bench.err
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit $rc
 python3 $REPO/tools/prof_summary.py $OUT/prof/bench_kernel_trace.csv > $OUT/step_timeline.txt; cat $OUT/step_timeline.txt
+mkdir -p $OUT/pmc
 i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
