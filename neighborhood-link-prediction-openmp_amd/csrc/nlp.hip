@@ -259,7 +259,7 @@ struct nlp_graph {
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
   bool hp_tie_select = true; // prune: the kept ties by radix select, not a sort (NLP_HASH_TIE_SORT=1 sorts)
-  bool hp_rows8 = false;     // survivor counts with 8 consecutive entries per lane (NLP_HASH_ROWS8=1)
+  bool hp_rows8 = true;      // survivor count / fill with 8 consecutive entries per lane (NLP_HASH_ROWS8=0: one per lane)
   bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
@@ -723,7 +723,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
-  if (const char* hr = getenv("NLP_HASH_ROWS8")) g->hp_rows8 = hr[0] == '1';
+  if (const char* hr = getenv("NLP_HASH_ROWS8")) g->hp_rows8 = hr[0] != '0';
   if (const char* ht = getenv("NLP_HASH_TIE_SORT")) g->hp_tie_select = ht[0] != '1';
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
