@@ -42,7 +42,8 @@ import nlp_loader  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 HOT_KERNELS = {1: "k_sp_bucket", 2: "k_sp_scan<F_Runs>", 3: "k_group_tiles", 4: "k_sp_survivors",
                5: "k_sp_expand", 6: "k_sp_pass", 7: "k_sp_runs", 8: "k_sp_group",
-               9: "k_sp_grouprun", 10: "k_sp_exbucket"}
+               9: "k_sp_grouprun", 10: "k_sp_exbucket", 11: "k_hp_batch"}
+CALLS_PER_GRAPH = 99  # main.cxx:67-80,212-220: 9 metrics x 11 hub thresholds per batch graph
 METRIC_NAMES = {"CN": "CommonNeighbors", "JAC": "JaccardCoefficient", "SOR": "SorensenIndex",
                 "SAL": "SaltonCosineSimilarity", "HPI": "HubPromoted", "HDI": "HubDepressed",
                 "LHN": "LeichtHolmeNermanScore", "AA": "AdamicAdarCoefficient", "RA": "ResourceAllocationScore"}
@@ -64,11 +65,45 @@ def f1_on_device(G, out, n, du, dw):
 
 
 def host_cores():
+    """Threads for the reference's OpenMP run: every core this process may run
+    on, unless OMP_NUM_THREADS says fewer (the GPU box sets it to the box's CPU
+    share and asks that it be left as is)."""
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+
+
+def host_info():
+    """the host the CPU baseline ran on -- nproc, the affinity
+    set, OMP_NUM_THREADS and the CPU model (lscpu)."""
+    model = None
+    try:
+        r = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10)
+        for ln in r.stdout.splitlines():
+            if ln.startswith("Model name:"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpu_model": model}
+
+
+def b_alg(off, H, kout):
+    """SURVEY §8(d) whole-call algorithmic bytes of the reference's wedge scan:
+    B_alg(H) = 8 (S+1) + 4 M (first hops) + 4 M (their degrees) + 8 P_H + 4 W_H
+    + 12 k_out, P_H = sum of deg v and W_H = sum of deg v^2 over the surviving
+    intermediates (1 <= deg v <= H, or all for H = 0)."""
+    deg = (off[1:] - off[:-1]).to(torch.float64)
+    sv = deg[(deg > 0) & (deg <= H)] if H > 0 else deg[deg > 0]
+    S, M = off.numel() - 1, int(off[-1])
+    return 8.0 * (S + 1) + 8.0 * M + 8.0 * float(sv.sum()) + 4.0 * float((sv * sv).sum()) + 12.0 * kout
 
 
 def ref_time(path, metric, hub, me, threads, timeout):
@@ -87,61 +122,144 @@ def ref_time(path, metric, hub, me, threads, timeout):
     return float(t_ms), float(ts_ms), int(n), wall
 
 
-def cpu_baseline(off, keys, metric, hub, k, ncand, budget_s=240.0):
+def write_csr(off, keys):
+    """The CSR as ref_driver reads it ([span, nnz] u64, offsets u64, keys u32),
+    in /dev/shm when present.  Returns (path, tmpdir object)."""
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    tmp = tempfile.TemporaryDirectory(dir=shm)
+    path = os.path.join(tmp.name, "g.csr")
+    with open(path, "wb") as f:
+        np.array([len(off) - 1, len(keys)], np.uint64).tofile(f)
+        off.astype(np.uint64).tofile(f)
+        keys.tofile(f)
+    return path, tmp
+
+
+def cpu_baseline(path, metric, hub, k, ncand, budget_s=240.0, one_thread=True):
     """The reference's own OpenMP path on this host's cores, same graph, same
     call (repeat 1), then the same on ONE thread when the all-cores time says
     it fits the budget.  maxEdges is capped at the candidate count: above it
     the reference's OpenMP merge reads past its per-thread lists (SURVEY
-    Appendix A.2).  The CSR goes through /dev/shm (the driver reads a file).
-    Returns (all-cores dict, 1-thread dict)."""
+    Appendix A.2).  `path`: the CSR file (write_csr).  Returns (all-cores
+    dict, 1-thread dict or None)."""
     drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     if not os.path.exists(drv):
         return {"error": "oracle/_ref/ref_driver not built"}, None
     cores = host_cores()
     me = min(k, ncand) if ncand else k
-    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
-    with tempfile.TemporaryDirectory(dir=shm) as tmp:
-        path = os.path.join(tmp, "g.csr")
-        with open(path, "wb") as f:
-            np.array([len(off) - 1, len(keys)], np.uint64).tofile(f)
-            off.astype(np.uint64).tofile(f)
-            keys.tofile(f)
-        t0 = time.perf_counter()
-        t_ms, ts_ms, n, wall = ref_time(path, metric, hub, me, cores, timeout=budget_s)
-        sample = "full workload: predictLinks%sOmp<%d>(G, {repeat 1, maxEdges %d}), DiGraphCsr of the same CSR" % (
-            METRIC_NAMES[metric], hub, me)
-        full = dict(value=n / (t_ms / 1e3) if t_ms > 0 else None, unit="predicted edges/s", cores=cores,
-                    kind="reference", time_ms=t_ms, scoring_ms=ts_ms, predicted=n, sample=sample,
-                    driver_wall_s=wall)
-        one = None
-        left = budget_s - (time.perf_counter() - t0)
-        est = t_ms / 1e3 * cores * 1.3 + (wall - t_ms / 1e3)  # linear in the cores, plus the CSR load
-        if est < left:
-            t1, ts1, n1, wall1 = ref_time(path, metric, hub, me, 1, timeout=left)
-            one = dict(value=n1 / (t1 / 1e3) if t1 > 0 else None, unit="predicted edges/s", cores=1,
-                       kind="reference", time_ms=t1, scoring_ms=ts1, predicted=n1, sample=sample)
-        else:
-            one = {"skipped": "estimated %.0f s on one thread > the %.0f s left of the baseline budget" % (est, left)}
+    t0 = time.perf_counter()
+    t_ms, ts_ms, n, wall = ref_time(path, metric, hub, me, cores, timeout=budget_s)
+    sample = "full workload: predictLinks%sOmp<%d>(G, {repeat 1, maxEdges %d}), DiGraphCsr of the same CSR" % (
+        METRIC_NAMES[metric], hub, me)
+    full = dict(value=n / (t_ms / 1e3) if t_ms > 0 else None, unit="predicted edges/s", cores=cores,
+                kind="reference", time_ms=t_ms, scoring_ms=ts_ms, predicted=n, sample=sample,
+                driver_wall_s=wall, host=host_info())
+    if not one_thread:
+        return full, None
+    left = budget_s - (time.perf_counter() - t0)
+    est = t_ms / 1e3 * cores * 1.3 + (wall - t_ms / 1e3)  # linear in the cores, plus the CSR load
+    if est < left:
+        t1, ts1, n1, wall1 = ref_time(path, metric, hub, me, 1, timeout=left)
+        one = dict(value=n1 / (t1 / 1e3) if t1 > 0 else None, unit="predicted edges/s", cores=1,
+                   kind="reference", time_ms=t1, scoring_ms=ts1, predicted=n1, sample=sample)
+    else:
+        one = {"skipped": "estimated %.0f s on one thread > the %.0f s left of the baseline budget" % (est, left)}
     return full, one
 
 
 def pmc_traffic(config, world, metric, hub, kernel):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (tools/pmc_summary.py over tools/gpu_pmc.sh's separate FETCH_SIZE /
+    """HBM bytes per launch of a kernel from the committed PMC summaries
+    (profiles/pmc_traffic.json: tools/pmc_summary.py over separate FETCH_SIZE /
     WRITE_SIZE passes of this same bench command, corrected as
-    MI355X_MICROARCH.md's HBM section prescribes).  None when absent or for
-    another workload."""
+    MI355X_MICROARCH.md's HBM section prescribes).  The file holds one record
+    per (config, n_gpus, metric, hub); None when this workload has none."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("config") != config or d.get("n_gpus") != world or d.get("metric") != metric or d.get("hub") != hub:
-        return None
-    if kernel not in d.get("kernels", {}):
-        return None
-    return {"bytes_per_launch": d["kernels"][kernel]["traffic_bytes"], "source": d.get("source"), "kernel": kernel}
+    for rec in d.get("records", [d]):
+        if (rec.get("config"), rec.get("n_gpus"), rec.get("metric"), rec.get("hub")) != (config, world, metric, hub):
+            continue
+        if kernel in rec.get("kernels", {}):
+            kr = rec["kernels"][kernel]
+            return {"bytes_per_launch": kr["traffic_bytes"], "source": rec.get("source"), "kernel": kernel,
+                    "launches_per_call": kr.get("launches_per_call")}
+    return None
+
+
+class Runner:
+    """One predict call of the bench on this rank: world 1 = the library call
+    (nlp_predict_device, result in HBM); world > 1 = the rank's shard plus the
+    histogram-quota exchange and the merge (dist.py)."""
+
+    def __init__(self, nlp, dmod, G, off, keys, span, k, world, stream):
+        self.nlp, self.dmod, self.G, self.span, self.k, self.world, self.stream = nlp, dmod, G, span, k, world, stream
+        self.off, self.keys = off, keys
+        self.out_local = torch.empty((k + 1, 3), dtype=torch.int32, device="cuda") if world > 1 else None
+        self.out = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+        self.states = {}
+
+    def __call__(self, mid, hub):
+        if self.world == 1:
+            cnt, t = self.G.predict_device(mid, hub, self.k, self.out, stream=self.stream)
+            return cnt, dict(t)
+        if hub not in self.states:  # shard bounds balanced by the per-source wedge estimate (SURVEY §8(e)), per H
+            st = self.dmod.Exchange()
+            st.weights = self.dmod.source_weights(self.off, self.keys, hub)
+            self.states[hub] = st
+        st = self.states[hub]
+        res, cnt, inf = self.dmod.predict_sharded(
+            self.dmod.hip_local_predict(self.G, mid, hub, self.k, self.out_local, self.stream),
+            self.dmod.hip_merge(self.G, self.out, self.stream), self.span, self.k, state=st, weights=st.weights)
+        return cnt, dict(inf)
+
+
+def timed(run, mid, hub, steps, warmup, world):
+    """W untimed calls, then exactly `steps` calls between barrier +
+    synchronize on both sides; the max over ranks.  Returns (ms per call,
+    last count, per-call sums of the library's timing fields)."""
+    for _ in range(warmup):
+        run(mid, hub)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    acc = dict(score_ms=0.0, select_ms=0.0, hot_ms=0.0, hot_bytes=0)
+    last = {}
+    cnt = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cnt, last = run(mid, hub)
+        for key in acc:
+            acc[key] += last.get(key, 0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms = float(el.item()) / steps * 1e3
+    for key in acc:
+        acc[key] = acc[key] / steps
+    return ms, cnt, acc, last
+
+
+def roofline_of(acc, last, config, world, metric, hub):
+    """roofline of the call's dominant kernel: its algorithmic bytes per call
+    (counted by the library) over its device time per call (HIP
+    events / the kernel's own stamps on the stream it runs on), averaged over
+    the timed calls; traffic = the committed PMC HBM bytes of the same kernel
+    on the same workload (rocprofv3, profiles/)."""
+    hot_ms, hot_bytes = acc["hot_ms"], int(acc["hot_bytes"])
+    achieved = hot_bytes / (hot_ms * 1e-3) / 1e9 if hot_ms > 0 else None
+    kname = HOT_KERNELS.get(int(last.get("hot_kernel", 0)), "?")
+    traffic = pmc_traffic(config, world, metric, hub, kname)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "kernel": kname, "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
+            "traffic_source": traffic["source"] if traffic else None}
 
 
 def main():
@@ -155,6 +273,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", default="2,8,16,32",
                     help="N = 1: hub thresholds (main.cxx:67-80) timed once each after the timed region; '' = none")
+    ap.add_argument("--work-point", default="auto",
+                    help="hub threshold of the work point: 'auto' = the first of 8,16,32,64,128 whose call "
+                         "predicts all k links; an integer; 'none'")
+    ap.add_argument("--wp-steps", type=int, default=5)
+    ap.add_argument("--wp-warmup", type=int, default=1)
+    ap.add_argument("--wp-cpu-budget", type=float, default=300.0,
+                    help="seconds allowed for the reference's all-cores run at the work point")
     ap.add_argument("--pipelined", action="store_true",
                     help="N = 1: also time the same calls enqueued back to back (nlp_predict_device_async)")
     args = ap.parse_args()
@@ -187,96 +312,65 @@ def main():
     span = ginfo["span"]
     k = info["k"]
     stream = torch.cuda.current_stream()
-    out_local = torch.empty((k + 1, 3), dtype=torch.int32, device="cuda")  # block: header + local top-k
-    out = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
     mid = nlp.METRICS.index(metric)
-    last = {}
-    xstate = dmod.Exchange()
-    # shard bounds balanced by the per-source wedge estimate, once per graph
-    weights = dmod.source_weights(off, keys, hub) if world > 1 else None
+    run = Runner(nlp, dmod, G, off, keys, span, k, world, stream)
+    amort = create_s * 1e3 / CALLS_PER_GRAPH
 
-    def step():
-        if world == 1:
-            cnt, t = G.predict_device(mid, hub, k, out, stream=stream)
-            last.clear()
-            last.update(t)
-            return cnt
-        res, cnt, inf = dmod.predict_sharded(dmod.hip_local_predict(G, mid, hub, k, out_local, stream),
-                                             dmod.hip_merge(G, out, stream), span, k, state=xstate,
-                                             weights=weights)
-        last.clear()
-        last.update(inf)
-        return cnt
-
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    score_ms = select_ms = hot_ms = 0.0
-    hot_bytes = replays = 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cnt = step()
-        score_ms += last.get("score_ms", 0.0)
-        select_ms += last.get("select_ms", 0.0)
-        hot_ms += last.get("hot_ms", 0.0)
-        hot_bytes += int(last.get("hot_bytes", 0))
-        replays += int(last.get("graph_replay", 0))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    ms_per_step = elapsed / args.steps * 1e3
-    value = cnt / (elapsed / args.steps)
-    timing = dict(last)
+    ms_per_step, cnt, acc, timing = timed(run, mid, hub, args.steps, args.warmup, world)
+    value = cnt / (ms_per_step * 1e-3)
 
     pipelined_ms = None
     if world == 1 and args.pipelined:  # serving loop: the same calls without a host wait (outside the line's value)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            G.predict_device_async(mid, hub, k, out, stream=stream)
+            G.predict_device_async(mid, hub, k, run.out, stream=stream)
         try:
             G.sync()
             pipelined_ms = (time.perf_counter() - t1) / args.steps * 1e3
         except nlp.NlpError as e:
             log("bench: asynchronous batch needs a redo (%s)" % e)
-        step()  # leave the synchronous result in `out`
 
     sweep = []
     if world == 1 and args.sweep not in ("", "none", "="):
-        # the reference's MINDEGREE1 sweep (main.cxx:67-80) for the bench metric; one warm call each,
-        # then the bench call again so `out` holds the line's result for F1
-        out_s = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+        # the reference's MINDEGREE1 sweep (main.cxx:67-80) for the bench metric; one warm call each
         for h in (int(x) for x in args.sweep.split(",") if x):
-            G.predict_device(mid, h, k, out_s, stream=stream)
+            run(mid, h)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            c, t = G.predict_device(mid, h, k, out_s, stream=stream)
+            c, t = run(mid, h)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t1) * 1e3
-            sweep.append(dict(H=h, ms=ms, predicted=c, predicted_per_s=c / (ms * 1e-3), wedges=t["wedges"],
-                              candidates=t["candidates"], path=t["path"], chunks=t["chunks"]))
-        del out_s
-        cnt = step()
+            sweep.append(dict(H=h, ms=ms, predicted=c, predicted_per_s=c / (ms * 1e-3), wedges=t.get("wedges"),
+                              candidates=t.get("candidates"), path=t.get("path"), chunks=t.get("chunks")))
+
+    # The work point: the first hub threshold whose call fills
+    # all k = |del|/2 links -- where the bytes are -- timed like the headline,
+    # with the roofline of its dominant kernel and the reference at the same H.
+    wp = None
+    if args.work_point not in ("", "none"):
+        cands = [8, 16, 32, 64, 128] if args.work_point == "auto" else [int(args.work_point)]
+        wp_h = None
+        for h in cands:
+            c, _ = run(mid, h)
+            if c == k or args.work_point != "auto":
+                wp_h = h
+                break
+        if wp_h is not None:
+            wms, wcnt, wacc, wlast = timed(run, mid, wp_h, args.wp_steps, args.wp_warmup, world)
+            balg = b_alg(off, wp_h, wcnt)
+            wp = {"H": wp_h, "metric": metric, "ms": wms, "predicted": wcnt, "predicted_per_s": wcnt / (wms * 1e-3),
+                  "amortized_ms_per_call": wms + amort, "steps": args.wp_steps,
+                  "wedges": int(wlast.get("wedges", 0)), "candidates": int(wlast.get("candidates", 0)),
+                  "path": wlast.get("path"), "chunks": wlast.get("chunks"),
+                  "score_ms": wacc["score_ms"], "select_ms": wacc["select_ms"],
+                  "call_alg_bytes": balg, "call_frac": balg / (wms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                  "roofline": roofline_of(wacc, wlast, args.config, world, metric, wp_h) if world == 1 else None,
+                  "cpu_baseline": None}
+    cnt, _ = run(mid, hub)  # leave the headline call's result in `out` for F1
+
     if rank == 0:
-        p, r, f1 = f1_on_device(G, out, cnt, du, dw)
-        score_ms /= args.steps
-        select_ms /= args.steps
-        # Roofline of the dominant kernel of the step: its
-        # algorithmic bytes per launch (from the call's own counters) over its
-        # device time (the kernel's own s_memrealtime stamps on the stream it
-        # runs on; rocprofv3 kernel trace of the same command in profiles/r03/),
-        # averaged over the timed steps.
-        hot_ms /= args.steps
-        hot_bytes //= args.steps
-        achieved = hot_bytes / (hot_ms * 1e-3) / 1e9 if hot_ms > 0 else None
-        kname = HOT_KERNELS.get(int(timing.get("hot_kernel", 0)), "?")
-        traffic = pmc_traffic(args.config, world, metric, hub, kname)
+        p, r, f1 = f1_on_device(G, run.out, cnt, du, dw)
         line = {
             "metric": "predicted edges/sec + F1, LHub Jaccard, 0.1|E| removed",
             "value": value,
@@ -290,7 +384,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u32/f32",
             "data": "synthetic (Chung-Lu stand-in of %s, generated on device; SURVEY §8(d))" % args.config,
-            "config": {"workload": "%s x%d: predictLinks%sOmp<%d>(G, {1, k = |del|/2}), synchronous drop-in call"
+            "config": {"workload": "%s x%d: predictLinks%sOmp<%d>(G, {1, k = |del|/2}) through the C-ABI "
+                                   "(nlp_predict_device via ctypes: graph resident, links left in HBM)"
                                    % (args.config, world, METRIC_NAMES[metric], hub),
                        "n": spec[0], "m": spec[1], "alpha": alpha, "M": ginfo["nnz"], "k": k,
                        "deletion_fraction": d,
@@ -301,33 +396,41 @@ def main():
             # so the graph's adjacency entries per second of prediction are reported too
             "graph_entries_per_s": ginfo["nnz"] / (ms_per_step * 1e-3),
             "f1": f1, "precision": p, "recall": r,
-            "score_ms": score_ms, "select_ms": select_ms,
-            "host_overhead_ms": ms_per_step - score_ms - select_ms if world == 1 else None,
+            "score_ms": acc["score_ms"], "select_ms": acc["select_ms"],
+            "host_overhead_ms": ms_per_step - acc["score_ms"] - acc["select_ms"] if world == 1 else None,
             "wedges": int(timing.get("wedges", 0)), "candidates": int(timing.get("candidates", 0)),
             "path": timing.get("path"),
             "graph_gen_s": gen_s,
             "graph_create_s": create_s,
+            # graph_create amortised over main.cxx's 99 calls per batch graph
+            "amortized_ms_per_call": ms_per_step + amort,
             "untimed_per_graph": "degrees, degree-class index, transposed CSR (if asymmetric), edge-membership "
-                                 "table, AA/RA tables: built once in nlp_graph_create (graph_create_s)",
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic["bytes_per_launch"] if traffic else None,
-                         "kernel": kname, "algorithmic_bytes": hot_bytes, "kernel_ms": hot_ms,
-                         "traffic_source": traffic["source"] if traffic else None} if world == 1 else None,
-            "graph_replay": replays == args.steps if world == 1 else None,
+                                 "table, AA/RA tables: built once in nlp_graph_create (graph_create_s; "
+                                 "amortized_ms_per_call adds graph_create_s / %d)" % CALLS_PER_GRAPH,
+            "roofline": roofline_of(acc, timing, args.config, world, metric, hub) if world == 1 else None,
             "pipelined_ms_per_step": pipelined_ms,
             "hub_sweep": sweep,
+            "work_point": wp,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
+            csr = tmpd = None
             try:
-                h_off, h_keys = off.cpu().numpy(), keys.cpu().numpy().view(np.uint32)
-                full, one = cpu_baseline(h_off, h_keys, metric, hub, k, int(timing.get("candidates", 0)))
+                csr, tmpd = write_csr(off.cpu().numpy(), keys.cpu().numpy().view(np.uint32))
+                full, one = cpu_baseline(csr, metric, hub, k, int(timing.get("candidates", 0)))
                 line["cpu_baseline"] = full
                 line["cpu_baseline_1thread"] = one  # the 1-thread time beside the all-cores one
-                del h_off, h_keys
             except Exception as e:  # report, never hide
                 line["cpu_baseline"] = {"error": repr(e)}
+            if wp is not None and csr is not None:
+                try:
+                    full, _ = cpu_baseline(csr, metric, wp["H"], k, wp["candidates"], budget_s=args.wp_cpu_budget,
+                                           one_thread=False)
+                    wp["cpu_baseline"] = full
+                except Exception as e:
+                    wp["cpu_baseline"] = {"error": repr(e)}
+            if tmpd is not None:
+                tmpd.cleanup()
         print(json.dumps(line), flush=True)
     G.close()
     if world > 1:

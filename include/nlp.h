@@ -96,7 +96,9 @@ typedef struct {
   uint64_t hot_bytes;       /* algorithmic bytes of that launch */
   uint32_t hot_kernel;      /* which kernel hot_ms times: 1 k_sp_bucket, 2 k_sp_scan<F_Runs>,
                                3 k_group_tiles, 4 k_sp_survivors, 5 k_sp_expand, 6 k_sp_pass,
-                               7 k_sp_runs, 8 k_sp_group, 9 k_sp_grouprun, 10 k_sp_exbucket; 0 none */
+                               7 k_sp_runs, 8 k_sp_group, 9 k_sp_grouprun, 10 k_sp_exbucket,
+                               11 k_hp_batch (path 4: all its launches of the call, times and bytes
+                               summed); 0 none */
 } nlp_timing;
 
 typedef struct nlp_graph nlp_graph;
@@ -261,6 +263,7 @@ nlp_status nlp_last_common(nlp_graph* g, uint64_t* common);
  * (u, u) per row).  d_src / d_dst: m device ids; d_off: device array of
  * n + 2 offsets (span = n + 1, row 0 empty); d_keys: device array of
  * keys_cap entries (2 m always suffices).  *nnz = the entries;
+ * NLP_ERR_INVALID (nothing written) when an id exceeds n;
  * NLP_ERR_CAPACITY (with *nnz set) when keys_cap is too small.  Ids < 2^31.
  * Synchronous; `stream` orders the work (NULL = the default stream). */
 nlp_status nlp_ingest_device(const uint32_t* d_src, const uint32_t* d_dst, uint64_t m, uint64_t n,

@@ -46,7 +46,8 @@ constexpr uint64_t HP_B2_MAX = 1ull << 19;  // bin 2: W(u) <= 2^19, bin 3: the r
 constexpr int HP_NBINS = 4;
 
 // per-chunk counters (u64)
-enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_NCTR = 8 };
+// HPC_HOTB: algorithmic bytes of the chunk's k_hp_batch launch, counted by the kernel
+enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_HOTB = 5, HPC_NCTR = 8 };
 
 struct HpArgs {
   GraphView g;
@@ -403,6 +404,7 @@ struct HpStage {
   uint32_t cap;   // entries per array
   uint32_t n;     // wave-uniform fill
   uint64_t cand, nan;
+  uint64_t out;   // candidates written (wave-uniform; the batch kernel's algorithmic bytes)
 };
 
 // Orders one wave's LDS accesses across lanes (staging, scan arrays, LDS
@@ -434,6 +436,7 @@ __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
     }
   }
   wave_sync_lds();
+  st.out += st.n;
   st.n = 0;
 }
 
@@ -1521,6 +1524,8 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
+  uint64_t abytes = 0;  // algorithmic bytes (wave-uniform): rows, entries, exclusion keys
+  uint64_t drained = 0;  // per lane: table entries whose deg w is gathered (count metrics without KD)
   wave_sync_lds();
   // The next batch's bounds, rows and row data are loaded while this batch
   // works (bounds during the first hops, rows during the exclusion, row data
@@ -1572,6 +1577,9 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     s_np[wv][lane] = np;
     wave_sync_lds();
     const uint32_t NS = __shfl(sp, (int)nr - 1, 64), NN = __shfl(np, (int)nr - 1, 64);
+    // per batch: its bounds (8); per row: list entry, W+(u), S(u) and N(u) bounds (28); per
+    // survivor entry 8 (packed) or 12 (key, deg, off); per exclusion key 4
+    abytes += 8 + 28ull * nr + (a.sdo ? 8ull : 12ull) * NS + 4ull * NN;
     const uint64_t Wb = wave_sum(W);
     const int lg = max(6, log2_ceil(2 * Wb));
     const uint32_t T = 1u << lg, mask = T - 1;
@@ -1730,6 +1738,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       for (int q = 0; q < HB_UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const bool valid = kq[q] != HP_EMPTY;
+        if (!CUSTOM && !KD) drained += valid ? 1 : 0;  // deg w gathered for it
         const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
         const uint32_t uu = s_u[wv][sl];
         const uint64_t du2 = s_du[wv][sl];
@@ -1754,6 +1763,10 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     b = bn;
   }
   hp_finish(sg, a, wedges);
+  // + per wedge its key (and its degree for KD), per emitted candidate 16 (key, u, w, score)
+  const uint64_t wsum = wave_sum(wedges);
+  abytes += (KD ? 8ull : 4ull) * wsum + 16ull * sg.out + 4ull * wave_sum(drained);
+  if (lane == 0 && abytes) atomicAdd(&a.ctr[HPC_HOTB], (unsigned long long)abytes);
 }
 
 // ---------------------------------------------------------------- bins 1-3: workgroup per row

@@ -27,10 +27,18 @@
 namespace nlp {
 
 // (src << 32 | dst) of the file's directed pairs
+// Also flags an id above n (*bad = 1): the rows are indexed by id further on
+// (k_in_first_absent's t[row], the radix passes cover bits_for(n) bits), so
+// one out-of-range id in the file would write past t[] or mis-sort silently.
 __global__ void k_in_pairs(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst, uint64_t m,
-                           uint64_t* __restrict__ out) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = ((uint64_t)src[i] << 32) | dst[i];
+                           uint64_t n, uint64_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  bool oob = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = src[i], b = dst[i];
+    oob |= a > n || b > n;
+    out[i] = ((uint64_t)a << 32) | b;
+  }
+  if (__ballot(oob) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
 }
 
 // flag[i] = 1 when sorted key i differs from key i - 1 (unique)

@@ -812,6 +812,9 @@ struct Cands {
   uint64_t nan = 0;
   uint64_t total = 0; // candidates produced (before pruning)
   uint64_t wedges = 0;
+  double hot_ms = 0;       // path 4: device time of the k_hp_batch launches (HIP events around each)
+  uint64_t hot_bytes = 0;  // and their algorithmic bytes (counted by the kernel, HPC_HOTB)
+  uint32_t hot_launches = 0;
 };
 
 // Group the W wedges of one generator pass, score them and append the
@@ -1925,6 +1928,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.sdo = s_sdo;
     a.sua = ua;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
+    bool batch_timed = false;
     if (n0 && g->hp_tiers) {
       // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
       TRY(hipMemsetAsync(tcnt, 0, 8 * sizeof(uint32_t), st));
@@ -1952,10 +1956,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(hipMemsetAsync(nbat, 0, 4, st));
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
+        TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
         if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());
+        TRY(hipEventRecord(g->ev[6], st));
+        batch_timed = true;
         if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_wave<false, HP_WT, HP_STG, true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
@@ -2008,6 +2015,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
+    if (batch_timed) {
+      float ms = 0;
+      TRY(hipEventElapsedTime(&ms, g->ev[5], g->ev[6]));
+      C.hot_ms += ms;
+      C.hot_bytes += g->host_small[HPC_HOTB];
+      ++C.hot_launches;
+    }
     if (g->hp_stats)
       fprintf(stderr, "[hash-stats] chunk rows [%llu, %llu) bins %llu %llu %llu %llu W %llu emitted %llu cand %llu tau %lld\n",
               (unsigned long long)r0, (unsigned long long)r1, (unsigned long long)n0, (unsigned long long)n1,
@@ -3330,6 +3344,10 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     t->nan_candidates = nan;
     t->path = path;
     t->chunks = chunks;
+    t->hot_ms = (float)C.hot_ms;
+    t->hot_bytes = C.hot_bytes;
+    t->hot_kernel = C.hot_launches ? 11u : 0u;
+    t->graph_replay = 0;
   }
   return NLP_OK;
 }
@@ -3668,8 +3686,15 @@ nlp_status nlp_ingest_device(const uint32_t* d_src, const uint32_t* d_dst, uint6
   if (m) {  // readMtxOmpW: every row sorted and unique
     TRY(tmp.get(&e, m));
     TRY(tmp.get(&e2, m));
-    LAUNCH(k_in_pairs, m, st, d_src, d_dst, m, e);
+    uint32_t* bad;
+    TRY(tmp.get(&bad, 1));
+    TRY(hipMemsetAsync(bad, 0, 4, st));
+    LAUNCH(k_in_pairs, m, st, d_src, d_dst, m, n, e, bad);
     TRY(hipGetLastError());
+    uint32_t hbad = 0;
+    TRY(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (hbad) return NLP_ERR_INVALID;  // an id above n: nothing is written
     int shifts[16];
     const int np = key_shifts(vb, 32, vb, shifts);
     TRY(sort_u64_keys(&e, &e2, m, shifts, np, tmp, st));

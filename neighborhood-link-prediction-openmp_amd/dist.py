@@ -129,56 +129,85 @@ def score_keys(edges, n):
     return torch.where(nan, torch.zeros_like(k), k)
 
 
+HBINS = 1 << 16
+
+
+def _hist16(idx, valid, device):
+    """Counts of the 16-bit values idx[valid] (int64 [HBINS]) without a host
+    sync: index_add_ into a fixed-size tensor (torch.bincount sizes its output
+    from the data's maximum, which reads it back to the host)."""
+    h = torch.zeros(HBINS + 1, dtype=torch.int64, device=device)
+    if idx.numel():
+        h.index_add_(0, torch.where(valid, idx, torch.full_like(idx, HBINS)), torch.ones_like(idx))
+    return h[:HBINS]
+
+
+def _all_gather_rows(x, group=None):
+    """[world, len(x)] on x's device: one all_gather (gloo: on CPU copies)."""
+    world = dist.get_world_size(group)
+    send = _coll(x.contiguous(), group)
+    recv = torch.empty(world * x.numel(), dtype=x.dtype, device=send.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return recv.to(x.device).view(world, x.numel())
+
+
+def _kth_bin(per_rank, need):
+    """Per-rank histograms [world, HBINS] and the number `need` (>= 1, device
+    scalar) of entries wanted from the top: the bin holding the need-th largest
+    entry over all ranks, and per rank the entries in bins above it."""
+    from_top = torch.cumsum(per_rank.flip(1), 1)          # per rank, bins HBINS-1 .. 0
+    tot_top = from_top.sum(0)
+    j = torch.searchsorted(tot_top, need.view(1)).clamp_(max=HBINS - 1)  # first from-top bin reaching need
+    above = torch.where(j > 0, from_top[:, (j - 1).clamp(min=0)].squeeze(1), torch.zeros_like(from_top[:, 0]))
+    return (HBINS - 1 - j).squeeze(0), above
+
+
 def select_quota(edges, n, max_edges, group=None):
     """Histogram-first global selection.  `edges[:n]` is this
     rank's canonical list (score key desc, then u, then w).  Returns (share,
     shares): how many leading entries of this rank's list belong to the
-    canonical global top max_edges, and every rank's share (rank order)."""
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    canonical global top max_edges, and every rank's share (rank order).
+
+    Two collectives and one host read: an all_gather of every rank's histogram
+    of the top 16 key bits gives every rank the bin b of the k-th key and each
+    rank's count above b; an all_gather of the histograms of the low 16 bits
+    inside b gives the k-th key itself, each rank's count above it and its tie
+    count, from which the tie quota is handed out in rank (= u) order -- the
+    canonical tie rule.  Everything stays on the list's device until the shares
+    (world integers) are read back to size the block exchange."""
+    rank = dist.get_rank(group)
+    dev = edges.device
     keys = score_keys(edges, n)
-    hi = torch.bincount(keys >> 16, minlength=1 << 16) if n else torch.zeros(1 << 16, dtype=torch.int64,
-                                                                             device=edges.device)
-    hi = _coll(hi, group)
-    dist.all_reduce(hi, group=group)  # the one histogram exchange for the top 16 bits
-    total = int(hi.sum())
-    take = min(int(max_edges), total)
-    if take == total:  # every candidate is kept: no boundary key
-        kth, above_all = -1, 0
-    else:
-        from_top = torch.cumsum(hi.flip(0), 0)
-        b = (1 << 16) - 1 - int(torch.searchsorted(from_top, torch.tensor(take, dtype=from_top.dtype)))
-        above_all = int(hi[b + 1:].sum())
-        sel = keys[(keys >> 16) == b]
-        lo = torch.bincount(sel & 0xFFFF, minlength=1 << 16) if sel.numel() else \
-            torch.zeros(1 << 16, dtype=torch.int64, device=edges.device)
-        lo = _coll(lo, group)
-        dist.all_reduce(lo, group=group)
-        from_top = torch.cumsum(lo.flip(0), 0)
-        l = (1 << 16) - 1 - int(torch.searchsorted(from_top, torch.tensor(take - above_all, dtype=from_top.dtype)))
-        above_all += int(lo[l + 1:].sum())
-        kth = (b << 16) | l
-    if kth < 0:
-        mine = torch.tensor([n, 0], dtype=torch.int64)
-    else:
-        mine = torch.stack([(keys > kth).sum(), (keys == kth).sum()]).cpu()
-    both = torch.empty(2 * world, dtype=torch.int64)
-    mine, both = _coll(mine.to(edges.device), group), _coll(both.to(edges.device), group)
-    dist.all_gather_into_tensor(both, mine, group=group)
-    both = both.cpu().view(world, 2).tolist()
-    quota = take - above_all
-    shares = []
-    for a, t in both:
-        q = min(t, max(quota, 0))
-        quota -= q
-        shares.append(a + q)
+    ones = torch.ones_like(keys, dtype=torch.bool)
+    hi = _all_gather_rows(_hist16(keys >> 16, ones, dev), group)          # [world, HBINS]
+    counts = hi.sum(1)                                                     # per-rank list lengths
+    total = counts.sum()
+    take = torch.clamp(total, max=int(max_edges))
+    b, above_hi = _kth_bin(hi, take.clamp(min=1))
+    lo = _all_gather_rows(_hist16(keys & 0xFFFF, (keys >> 16) == b, dev), group)
+    l, above_lo = _kth_bin(lo, (take - above_hi.sum()).clamp(min=1))
+    above = above_hi + above_lo                                            # per rank: keys > the k-th key
+    ties = lo[:, l]                                                        # per rank: keys == the k-th key
+    quota = take - above.sum()
+    before = torch.cumsum(ties, 0) - ties                                  # ties of the ranks before
+    shares = above + torch.minimum(ties, (quota - before).clamp(min=0))
+    shares = torch.where(take == total, counts, shares)                    # everything kept: no boundary key
+    shares = [int(x) for x in shares.cpu().tolist()]
     return shares[rank], shares
 
 
 def gather_blocks(block, stride, group=None):
     """One all_gather of every rank's first `stride` entries (header + its
-    share) into [world, stride, 3]."""
+    share) into [world, stride, 3].  A block shorter than the stride (a rank
+    sized to its own smaller result) is padded, so every rank sends the same
+    number of entries."""
     world = dist.get_world_size(group)
-    send = _coll(block[:stride].contiguous(), group)
+    send = block[:stride]
+    if send.shape[0] < stride:
+        pad = torch.zeros((stride, 3), dtype=block.dtype, device=block.device)
+        pad[:send.shape[0]] = send
+        send = pad
+    send = _coll(send.contiguous(), group)
     recv = torch.empty((world * stride, 3), dtype=block.dtype, device=send.device)
     dist.all_gather_into_tensor(recv, send, group=group)
     return recv.to(block.device).view(world, stride, 3)

@@ -24,20 +24,26 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cases, q):
+GRAPHS = {"small": (30000, 10, 5), "1M": (1_000_000, 12, 9)}
+
+
+def _worker(rank, world, port, cases, q, backend="gloo", graph="small"):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import nlp_loader
         from test_gpu_parity import random_csr
         nlp = nlp_loader.load()
         dmod = nlp_loader.load_sub("dist")
-        torch.cuda.set_device(0)
-        off, keys = random_csr(30000, 10, 5)
+        off, keys = random_csr(*GRAPHS[graph])
         res = []
         with nlp.Graph(off, keys, device=0) as G:
             off_t = torch.from_numpy(off.astype(np.int64))
@@ -55,16 +61,13 @@ def _worker(rank, world, port, cases, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_sharded_chain_equals_single_gpu(nlp, world):
+def _run_chain(nlp, world, cases, backend="gloo", graph="small"):
     import torch
     import torch.multiprocessing as mp
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from test_gpu_parity import random_csr
-    cases = [(1, 4, 2000), (7, 8, 5000), (0, 0, 3000), (1, 16, 10 ** 6)]
-    off, keys = random_csr(30000, 10, 5)
+    off, keys = random_csr(*GRAPHS[graph])
     want = []
     with nlp.Graph(off, keys) as G:
         for metric, hub, k in cases:
@@ -74,7 +77,7 @@ def test_gpu_sharded_chain_equals_single_gpu(nlp, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, backend, graph)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in range(world)]
@@ -85,3 +88,23 @@ def test_gpu_sharded_chain_equals_single_gpu(nlp, world):
         for (a, shares), b, (metric, hub, k) in zip(res, want, cases):
             assert np.array_equal(a, b), (rank, metric, hub)
             assert sum(shares) == len(b)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_sharded_chain_equals_single_gpu(nlp, world):
+    _run_chain(nlp, world, [(1, 4, 2000), (7, 8, 5000), (0, 0, 3000), (1, 16, 10 ** 6)])
+
+
+@pytest.mark.timeout(300)
+def test_gpu_sharded_chain_h16_1m_vertices(nlp):
+    """H = 16 on a 1 M-vertex graph (k-filling: more candidates than k), 2 ranks."""
+    _run_chain(nlp, 2, [(1, 16, 400_000), (7, 16, 300_000)], graph="1M")
+
+
+@pytest.mark.timeout(300)
+def test_gpu_sharded_chain_nccl_world1(nlp):
+    """The production backend: RCCL ("nccl") with the tensors on cuda:0 -- the
+    histogram all_gathers, the quota and the block exchange never leave the
+    device except for the shares (one rank: RCCL refuses two ranks on one GPU)."""
+    _run_chain(nlp, 1, [(1, 4, 2000), (1, 16, 400_000)], backend="nccl", graph="1M")

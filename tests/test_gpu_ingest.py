@@ -106,3 +106,16 @@ def test_gpu_workload_uses_the_reference_ingest(gpu, tmp_path):
     assert np.array_equal(off.cpu().numpy().astype(np.uint64), hoff)
     assert np.array_equal(keys.cpu().numpy().view(np.uint32), hkeys)
     assert np.array_equal(du.cpu().numpy().view(np.uint32), hu) and np.array_equal(dw.cpu().numpy().view(np.uint32), hw)
+
+
+def test_ingest_rejects_id_above_n(gpu):
+    """One id above n in the pairs: NLP_ERR_INVALID, nothing indexed by it
+    (the rows are addressed by id on the device)."""
+    import torch
+    src = torch.tensor([1, 2, 3, 9], dtype=torch.int32, device="cuda")
+    dst = torch.tensor([2, 3, 1, 1], dtype=torch.int32, device="cuda")
+    with pytest.raises(gpu.NlpError) as e:
+        gpu.ingest_device(src, dst, 5)
+    assert e.value.status == 1
+    off, keys = gpu.ingest_device(src, dst, 9)  # the same pairs with n large enough
+    assert int(off[-1]) == keys.numel() == 8
