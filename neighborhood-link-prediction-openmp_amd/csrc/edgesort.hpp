@@ -1,0 +1,245 @@
+// edgesort.hpp -- the canonical order of a call's links as ONE stable LSD sort
+// of 12-byte edge records (gfx950 onesweep passes).
+//
+// The reference leaves its result in heap-merge order (predict.hxx:431-460)
+// and its ties schedule-dependent; the build returns the
+// canonical order: score key descending, then u ascending, then w ascending
+// (DESIGN.md §2).  That is the ascending order of the composite
+//
+//     K = (~score_key(s)) << 2vb | u << vb | w          (32 + 2 vb bits)
+//
+// computed from the record itself, so a record carries no separate key: each
+// pass reads (u, w, s), takes its 8-bit digit of K, and writes the record to
+// its stable position; the last pass writes the caller's edge array.  The
+// round-3 order (two sorts: (u, w) with the key as payload in 7 counted
+// passes, then the key in 4, then a gather; C4 JAC H=16: 33.9 ms) moved 8-byte
+// keys + payloads through separate histogram and scatter kernels.
+//
+//   k_es_hist   one read of the records: the 256-bin histogram of every
+//               digit (wave-aggregated LDS counts); a digit whose histogram
+//               has one bin holding every record is a pass not run
+//   k_es_pass   one pass: 4096-record tiles claimed by an ordered ticket; a
+//               wave ranks its 512 consecutive records in 8 ballot-multisplit
+//               substeps; per digit the tile's count is published, the
+//               exclusive prefix over earlier tiles is found by decoupled
+//               look-back (u64 descriptors {epoch, status, count}: a pass
+//               never clears the previous pass's descriptors, it ignores
+//               another epoch); the tile is reordered by digit in LDS and
+//               written out in digit runs (consecutive lanes, consecutive
+//               12-byte records: coalesced stores)
+#pragma once
+#include "kernels.hpp"
+#include "prims.hpp"
+
+namespace nlp {
+
+constexpr int ES_NT = 512;                 // threads per tile
+constexpr int ES_NW = ES_NT / 64;          // 8 waves
+constexpr int ES_IPT = 8;                  // records per thread
+constexpr int ES_WCH = 64 * ES_IPT;        // 512 consecutive records per wave
+constexpr int ES_TILE = ES_NT * ES_IPT;    // 4096 records per tile
+constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
+constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
+constexpr uint32_t ES_SPIN_LIMIT = 1u << 26;
+
+// 8-bit digit `shift` (bit offset) of K; `bits` < 8 for the top digit
+__device__ __forceinline__ uint32_t es_digit(uint32_t u, uint32_t w, float s, int vb, int shift) {
+  const int lob = 2 * vb;
+  const uint32_t hk = ~score_key(s);
+  if (shift >= lob) return (hk >> (shift - lob)) & 0xffu;
+  const uint64_t lo = ((uint64_t)u << vb) | w;
+  uint32_t d = (uint32_t)(lo >> shift);
+  if (shift + 8 > lob) d |= hk << (lob - shift);
+  return d & 0xffu;
+}
+
+// peers of this lane in the wave: the lanes holding the same 8-bit value
+__device__ __forceinline__ uint64_t es_peers(uint32_t d, bool ok) {
+  uint64_t peers = __ballot(ok);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint64_t bb = __ballot((d >> b) & 1u);
+    peers &= ((d >> b) & 1u) ? bb : ~bb;
+  }
+  return peers;
+}
+
+// ghist[p * 256 + d]: records whose digit p (bits 8p..8p+7 of K) is d
+__global__ __launch_bounds__(ES_NT) void k_es_hist(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+                                                   const float* __restrict__ cs, uint64_t n, int vb, int npass,
+                                                   uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t h[ES_MAXP][256];
+  for (int i = threadIdx.x; i < ES_MAXP * 256; i += ES_NT) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t lt = (1ull << lane_id()) - 1ull;
+  const uint64_t stride = (uint64_t)gridDim.x * ES_NT;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT; j0 < n; j0 += stride) {  // uniform per wave: ballots below
+    const uint64_t j = j0 + threadIdx.x;
+    const bool ok = j < n;
+    const uint32_t u = ok ? cu[j] : 0u, w = ok ? cw[j] : 0u;
+    const float s = ok ? cs[j] : 0.0f;
+    for (int p = 0; p < npass; ++p) {
+      const uint32_t d = es_digit(u, w, s, vb, 8 * p);
+      const uint64_t peers = es_peers(d, ok);
+      if (ok && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < npass * 256; i += ES_NT) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&ghist[i], c);
+  }
+}
+
+__device__ __forceinline__ void es_publish(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t es_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// FIRST: the input is the candidate columns (cu, cw, cs); else records `in`.
+// The output is always records (`out`: the caller's edges on the last pass).
+template <bool FIRST>
+__global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+                                                   const float* __restrict__ cs, const EdgeOut* __restrict__ in,
+                                                   EdgeOut* __restrict__ out, uint64_t n, int vb, int shift,
+                                                   const uint32_t* __restrict__ ghist, uint64_t* __restrict__ desc,
+                                                   uint32_t* __restrict__ ticket, uint64_t epoch,
+                                                   uint32_t* __restrict__ err) {
+  __shared__ uint32_t s_u[ES_TILE], s_w[ES_TILE], s_s[ES_TILE];
+  __shared__ uint32_t s_wc[ES_NW][256];   // per wave: running digit counts, then wave prefixes
+  __shared__ uint64_t s_gofs[256];        // global position of the tile's first record of each digit
+  __shared__ uint32_t s_lofs[256];        // tile position of the first record of each digit
+  __shared__ uint32_t s_scan[8];
+  __shared__ uint32_t s_tile;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t ntiles = (n + ES_TILE - 1) / ES_TILE;
+  const uint64_t ep = epoch << 48;
+  while (true) {
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+    for (int i = t; i < ES_NW * 256; i += ES_NT) (&s_wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    if (tile >= ntiles) break;  // uniform: every wave leaves
+    const uint64_t base = tile * ES_TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - base);
+    // records of this wave: base + wv * 512 + i * 64 + lane (item order = (wave, substep, lane))
+    uint32_t ru[ES_IPT], rw[ES_IPT], rs[ES_IPT], rk[ES_IPT], dg[ES_IPT];
+#pragma unroll
+    for (int i = 0; i < ES_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      const bool ok = q < tn;
+      const uint64_t j = base + q;
+      if (FIRST) {
+        ru[i] = ok ? cu[j] : 0u;
+        rw[i] = ok ? cw[j] : 0u;
+        rs[i] = ok ? __float_as_uint(cs[j]) : 0u;
+      } else {
+        EdgeOut e{0u, 0u, 0.0f};
+        if (ok) e = in[j];
+        ru[i] = e.u;
+        rw[i] = e.v;
+        rs[i] = __float_as_uint(e.score);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ES_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      const bool ok = q < tn;
+      dg[i] = es_digit(ru[i], rw[i], __uint_as_float(rs[i]), vb, shift);
+      const uint64_t peers = es_peers(dg[i], ok);
+      const uint64_t below = peers & ((1ull << lane) - 1ull);
+      rk[i] = ok ? s_wc[wv][dg[i]] + (uint32_t)__popcll(below) : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      if (ok && below == 0) s_wc[wv][dg[i]] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+    __syncthreads();
+    // threads 0-255 own digit t: wave prefixes, the tile count, look-back, global base
+    uint32_t cnt = 0, gh = 0;
+    if (t < 256) {
+#pragma unroll
+      for (int w = 0; w < ES_NW; ++w) {
+        const uint32_t c = s_wc[w][t];
+        s_wc[w][t] = cnt;
+        cnt += c;
+      }
+      gh = ghist[t];
+      uint64_t* my = desc + tile * 256 + t;
+      es_publish(my, ep | (tile == 0 ? ES_PFX : ES_AGG) | (uint64_t)cnt);
+    }
+    // exclusive scans over the 256 digits (threads 0-255; waves 0-3): tile counts and the pass histogram
+    uint32_t lof = 0, gb = 0;
+    {
+      uint32_t a = cnt, b = gh;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ya = __shfl_up(a, o, 64), yb = __shfl_up(b, o, 64);
+        if (lane >= o) { a += ya; b += yb; }
+      }
+      if (lane == 63 && wv < 4) { s_scan[wv] = a; s_scan[4 + wv] = b; }
+      __syncthreads();
+      uint32_t pa = 0, pb = 0;
+      for (int w = 0; w < wv && w < 4; ++w) { pa += s_scan[w]; pb += s_scan[4 + w]; }
+      lof = pa + a - cnt;
+      gb = pb + b - gh;
+    }
+    if (t < 256) {
+      uint64_t excl = 0;
+      if (tile > 0) {
+        int64_t j = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        while (j >= 0) {
+          const uint64_t x = es_load(desc + (uint64_t)j * 256 + t);
+          const uint64_t st = (x >> 46) & 3ull;
+          if ((x >> 48) != epoch || st == 0) {
+            if (++spins > ES_SPIN_LIMIT) { atomicOr(err, 1u); break; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          excl += x & ES_VAL;
+          if (st == 2) break;
+          --j;
+        }
+        es_publish(desc + tile * 256 + t, ep | ES_PFX | (excl + cnt));
+      }
+      s_gofs[t] = (uint64_t)gb + excl;
+      s_lofs[t] = lof;
+    }
+    __syncthreads();
+    // reorder the tile by digit in LDS
+#pragma unroll
+    for (int i = 0; i < ES_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      if (q < tn) {
+        const uint32_t p = s_lofs[dg[i]] + s_wc[wv][dg[i]] + rk[i];
+        s_u[p] = ru[i];
+        s_w[p] = rw[i];
+        s_s[p] = rs[i];
+      }
+    }
+    __syncthreads();
+    // write the digit runs: consecutive tile positions -> consecutive output records
+    for (uint32_t p = (uint32_t)t; p < tn; p += ES_NT) {
+      const uint32_t u = s_u[p], w = s_w[p], sb = s_s[p];
+      const uint32_t d = es_digit(u, w, __uint_as_float(sb), vb, shift);
+      const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);
+      out[pos] = EdgeOut{u, w, __uint_as_float(sb)};
+    }
+    __syncthreads();
+  }
+}
+
+// n <= 1 or every digit constant: the candidate columns as records, in place order
+__global__ void k_es_copy(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+                          const float* __restrict__ cs, uint64_t n, EdgeOut* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = EdgeOut{cu[i], cw[i], cs[i]};
+}
+
+}  // namespace nlp

@@ -26,6 +26,7 @@
 #include "hashpath.hpp"
 #include "multi.hpp"
 #include "ingest.hpp"
+#include "edgesort.hpp"
 #include "../../include/nlp/random.hxx"
 
 using namespace nlp;
@@ -76,6 +77,7 @@ enum Buf {
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
+  B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
 
@@ -261,6 +263,10 @@ struct nlp_graph {
   bool hp_tie_select = true; // prune: the kept ties by radix select, not a sort (NLP_HASH_TIE_SORT=1 sorts)
   bool hp_rows8 = true;      // survivor count / fill with 8 consecutive entries per lane (NLP_HASH_ROWS8=0: one per lane)
   bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
+  bool es_final = true;      // path 4's final order as one record sort (edgesort.hpp; NLP_ES_FINAL=0: two key sorts)
+  unsigned occ_es = 256;     // resident k_es_pass workgroups
+  uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
+  size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
@@ -723,6 +729,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
+  if (const char* ef = getenv("NLP_ES_FINAL")) g->es_final = ef[0] != '0';
   if (const char* hr = getenv("NLP_HASH_ROWS8")) g->hp_rows8 = hr[0] != '0';
   if (const char* ht = getenv("NLP_HASH_TIE_SORT")) g->hp_tie_select = ht[0] != '1';
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
@@ -752,6 +759,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_survivors, &g->occ_surv));
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
+    TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
     unsigned a = 0, b = 0;
@@ -1571,9 +1579,75 @@ nlp_status hp_uw_order(nlp_graph* g, Cands& C, hipStream_t st) {
 // (score key desc, u asc, w asc): two sorts and one gather of 8 bytes per edge
 // (k_hp_final_edges) instead of hp_uw_order's permutation, order_v1's score
 // sort and its three-column gather.
+// The canonical order of n links given as columns (u, w, score) written to
+// `out` as records: one stable LSD sort of the records by
+// (~score_key, u, w) (edgesort.hpp).  Digits that are the same for every
+// record are skipped (one histogram read decides, read back with one sync).
+nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
+                   hipStream_t st) {
+  if (n == 0) return NLP_OK;
+  Workspace& ws = g->ws;
+  const int vb = std::max(1, bits_for(g->span - 1));
+  const int npass = (32 + 2 * vb + 7) / 8;
+  if (npass > ES_MAXP || n >= ES_AGG) return NLP_ERR_INVALID;
+  uint32_t* hw;  // [npass * 256] histograms, [ES_MAXP] tickets, error word
+  TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
+  uint32_t* tick = hw + ES_MAXP * 256;
+  uint32_t* err = tick + ES_MAXP;
+  TRY(hipMemsetAsync(hw, 0, ((uint64_t)ES_MAXP * 256 + ES_MAXP + 4) * 4, st));
+  hipLaunchKernelGGL(k_es_hist, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
+                     cu, cw, cs, n, vb, npass, hw);
+  TRY(hipGetLastError());
+  std::vector<uint32_t> h((size_t)npass * 256);
+  TRY(hipMemcpyAsync(h.data(), hw, h.size() * 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  int run[ES_MAXP], P = 0;
+  for (int p = 0; p < npass; ++p) {
+    uint32_t mx = 0;
+    for (int d = 0; d < 256; ++d) mx = std::max(mx, h[(size_t)p * 256 + d]);
+    if (mx < n) run[P++] = p;
+  }
+  if (P == 0) {
+    LAUNCH(k_es_copy, n, st, cu, cw, cs, n, out);
+    return hipGetLastError() == hipSuccess ? NLP_OK : NLP_ERR_DEVICE;
+  }
+  const uint64_t ntiles = (n + ES_TILE - 1) / ES_TILE;
+  uint64_t* desc;
+  EdgeOut* tmp = nullptr;
+  TRY(wsget(ws, B_ES_DESC, ntiles * 256, &desc));
+  if (P > 1) TRY(wsget(ws, B_ES_TMP, n, &tmp));
+  if (ws.bytes[B_ES_DESC] != g->es_desc_bytes || g->es_epoch + P >= 0xffffull) {
+    TRY(hipMemsetAsync(desc, 0, ws.bytes[B_ES_DESC], st));  // no stale descriptor can carry a live epoch
+    g->es_desc_bytes = ws.bytes[B_ES_DESC];
+    g->es_epoch = 0;
+  }
+  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es));
+  const EdgeOut* src = nullptr;
+  for (int r = 0; r < P; ++r) {
+    EdgeOut* dst = ((P - 1 - r) & 1) ? tmp : out;  // the last pass writes `out`
+    const uint64_t ep = ++g->es_epoch;
+    if (r == 0)
+      hipLaunchKernelGGL(k_es_pass<true>, dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst, n, vb,
+                         8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+    else
+      hipLaunchKernelGGL(k_es_pass<false>, dim3(gr), dim3(ES_NT), 0, st, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, (const float*)nullptr, src, dst, n, vb, 8 * run[r],
+                         (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+    TRY(hipGetLastError());
+    src = dst;
+  }
+  uint32_t herr = 0;
+  TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  return herr ? NLP_ERR_DEVICE : NLP_OK;  // a look-back gave up (never expected)
+}
+
 nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   const uint64_t n = C.n;
   if (n == 0) return NLP_OK;
+  if (g->es_final)
+    return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], n,
+                   d_out, st);
   if (n > 0xffffffffull) return NLP_ERR_INVALID;
   Workspace& ws = g->ws;
   uint64_t *k0, *k1, *s0, *s1;

@@ -7,6 +7,7 @@
 #   c5prof  -- kernel trace + stats of tools/range_call.py (C5 IHub range)
 #   c5pmc   -- FETCH_SIZE / WRITE_SIZE passes of that range call
 #   sweep   -- tools/sweep.py SWEEP_ARGS
+#   sweepprof -- the same under rocprofv3 --kernel-trace --stats
 # Output in gpurun_out/$TAG.  Every GPU step has its own time limit and the
 # script stops at the first failure.
 set -u
@@ -46,6 +47,8 @@ for s in ${STEPS//,/ }; do
                 -d "$OUT/c5pmc_$c" -o pmc -- $C5_CMD) || exit 1
            done ;;
     sweep) run sweep 900 python3 tools/sweep.py ${SWEEP_ARGS:-} ;;
+    sweepprof) (cd /tmp && export TMPDIR=/tmp && run sweepprof 900 rocprofv3 --kernel-trace --stats --output-format csv \
+                  -d "$OUT/sweepprof" -o sweep -- python3 $REPO/tools/sweep.py ${SWEEP_ARGS:-}) || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
