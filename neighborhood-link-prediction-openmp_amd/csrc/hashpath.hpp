@@ -1078,6 +1078,164 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill8(GraphView g, const uint8_t
   }
 }
 
+// ---------------------------------------------------------------- survivor lists in one pass
+// k_hp_dcls_rows8 + scan + k_hp_dcls_fill8 read the range's degree classes
+// twice (C4 H=16: 3.3 + 8.5 ms).  Here one pass does both: tiles of
+// HD_TILE entries (every wave takes HD_SUB consecutive 512-entry wave tiles,
+// one 8-byte class word per lane each, kept in registers), the survivors of a
+// tile counted, the tile's output offset found by decoupled look-back on one
+// u64 descriptor per tile (ordered tile tickets, so a tile only waits on tiles
+// already claimed), then the survivors written in entry order -- S(u) stays
+// sorted -- with their packed entries; per row (count << 40 | W+) by
+// LDS-aggregated runs as in k_hp_dcls_fill8 (unpacked and scanned into soff
+// afterwards: the lists are the entry-order compaction, so the rows' counts
+// give their starts).  The rank bytes are read only for words holding a
+// survivor.  Output capacity `cap` (from the degree histogram); more survivors
+// raise err bit 1 (the caller falls back to the two-kernel build).
+constexpr int HD_SUB = 8;                                   // wave tiles per wave per tile
+constexpr uint64_t HD_TILE = (uint64_t)NWAVE * HD_SUB * HP_WTILE;  // 16384 entries
+constexpr uint64_t HD_AGG = 1ull << 62, HD_PFX = 2ull << 62, HD_VAL = HD_AGG - 1;
+
+__global__ __launch_bounds__(NT) void k_hp_dcls_one(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                    uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                    const uint32_t* __restrict__ tile_row, uint32_t* __restrict__ skeys,
+                                                    uint64_t* __restrict__ sdo, uint64_t cap,
+                                                    unsigned long long* __restrict__ wu,
+                                                    const uint8_t* __restrict__ drank, uint64_t* __restrict__ desc,
+                                                    uint32_t* __restrict__ ticket, uint32_t* __restrict__ err) {
+  __shared__ unsigned long long s_acc[NWAVE][64];
+  __shared__ uint64_t s_end[NWAVE][64];
+  __shared__ uint32_t s_wt[NWAVE][HD_SUB];
+  __shared__ uint64_t s_base;
+  __shared__ uint32_t s_tile;
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t T0 = e0 / HD_TILE, ntiles = (e1 + HD_TILE - 1) / HD_TILE - T0;
+  s_acc[wv][lane] = 0;
+  while (true) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t ti = s_tile;
+    if (ti >= ntiles) break;
+    const uint64_t tile = T0 + ti;
+    // phase 1: class words and survivor counts of this wave's wave tiles
+    uint64_t word[HD_SUB];
+    uint32_t mine[HD_SUB];
+#pragma unroll
+    for (int sb = 0; sb < HD_SUB; ++sb) {
+      const uint64_t eb = (tile * (NWAVE * HD_SUB) + (uint64_t)wv * HD_SUB + sb) * HP_WTILE + (uint64_t)lane * 8;
+      uint64_t w = 0;
+      if (eb >= e0 && eb + 8 <= e1) w = *(const uint64_t*)(dcls + eb);
+      else
+        for (int q = 0; q < 8; ++q)
+          if (eb + q >= e0 && eb + q < e1) w |= (uint64_t)dcls[eb + q] << (8 * q);
+      uint32_t c = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) c += hp_dsurv((uint32_t)(w >> (8 * q)) & 0xffu, H) ? 1u : 0u;  // out of range: 0
+      word[sb] = w;
+      mine[sb] = c;
+      const uint32_t tot = (uint32_t)wave_sum((uint64_t)c);
+      if (lane == 0) s_wt[wv][sb] = tot;
+    }
+    __syncthreads();
+    // phase 2: the tile's offset (thread 0: publish the count, look back, publish the prefix)
+    if (threadIdx.x == 0) {
+      uint64_t cnt = 0;
+      for (int i = 0; i < NWAVE * HD_SUB; ++i) cnt += (&s_wt[0][0])[i];
+      uint64_t excl = 0;
+      if (ti == 0) {
+        __hip_atomic_store(&desc[ti], HD_PFX | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_store(&desc[ti], HD_AGG | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t j = (int64_t)ti - 1;
+        uint32_t spins = 0;
+        while (j >= 0) {
+          const uint64_t x = __hip_atomic_load(&desc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((x >> 62) == 0) {
+            if (++spins > (1u << 26)) { atomicOr(err, 2u); break; }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          excl += x & HD_VAL;
+          if ((x >> 62) == 2) break;
+          --j;
+        }
+        __hip_atomic_store(&desc[ti], HD_PFX | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_base = excl;
+    }
+    __syncthreads();
+    uint64_t wpre = s_base;  // survivors of the tile before this wave's wave tiles
+    for (int i = 0; i < wv * HD_SUB; ++i) wpre += (&s_wt[0][0])[i];
+    // phase 3: per wave tile, the survivors at their positions, the row runs
+    for (int sb = 0; sb < HD_SUB; ++sb) {
+      const uint64_t wt = tile * (NWAVE * HD_SUB) + (uint64_t)wv * HD_SUB + sb;
+      const uint64_t base = wt * HP_WTILE;
+      if (base >= e1) break;  // wave-uniform
+      const uint64_t tr = tile_row[wt];
+      const uint64_t r0 = tr > ua ? tr - ua : 0;
+      const uint64_t rl = r0 + lane;
+      s_end[wv][lane] = rl < nU ? g.off[ua + rl + 1] : ~0ull;
+      wave_sync_lds();
+      const uint64_t last_end = s_end[wv][63];
+      const uint64_t eb = base + (uint64_t)lane * 8;
+      const uint64_t w = word[sb];
+      const uint32_t c8 = mine[sb];
+      uint64_t pos = wpre + wave_incl_scan((uint64_t)c8) - c8;
+      const uint64_t rk = c8 ? (eb + 8 <= e1 && eb >= e0 ? *(const uint64_t*)(drank + eb) : 0ull) : 0ull;
+      uint64_t rkx = rk;
+      if (c8 && !(eb + 8 <= e1 && eb >= e0))
+        for (int q = 0; q < 8; ++q)
+          if (eb + q >= e0 && eb + q < e1) rkx |= (uint64_t)drank[eb + q] << (8 * q);
+      int idx = 0;
+#pragma unroll
+      for (uint32_t bit = 32; bit > 0; bit >>= 1) idx += s_end[wv][idx + bit - 1] <= eb ? (int)bit : 0;
+      unsigned long long run = 0;
+      for (int q = 0; q < 8; ++q) {
+        const uint64_t e = eb + q;
+        const uint32_t c = (uint32_t)(w >> (8 * q)) & 0xffu;
+        while (idx < 64 && s_end[wv][idx] <= e) {
+          if (run) atomicAdd(&s_acc[wv][idx], run);
+          run = 0;
+          ++idx;
+        }
+        if (!hp_dsurv(c, H)) continue;  // (entries outside the range carry class 0)
+        uint64_t r = r0 + (uint64_t)idx;
+        if (e >= last_end) {
+          uint64_t a = r0, b = nU;
+          while (b - a > 1) {
+            const uint64_t md = (a + b) >> 1;
+            if (g.off[ua + md] <= e) a = md; else b = md;
+          }
+          r = a;
+        }
+        const uint32_t v = g.keys[e];
+        const uint32_t l = (uint32_t)(rkx >> (8 * q)) & 0xffu;
+        const uint32_t n = c - l;
+        if (pos < cap) {
+          skeys[pos] = v;
+          sdo[pos] = (uint64_t)c << 48 | (uint64_t)n << HP_SDO_SH | (g.off[v] + l);
+        } else {
+          atomicOr(err, 1u);
+        }
+        ++pos;
+        const unsigned long long add = (1ull << 40) | n;
+        if (e < last_end) run += add;
+        else atomicAdd(&wu[r], add);
+      }
+      if (run && idx < 64) atomicAdd(&s_acc[wv][idx], run);
+      wave_sync_lds();
+      const unsigned long long x = s_acc[wv][lane];
+      if (x) {
+        atomicAdd(&wu[rl], x);
+        s_acc[wv][lane] = 0;
+      }
+      wave_sync_lds();
+      wpre += s_wt[wv][sb];
+    }
+    __syncthreads();
+  }
+}
+
 // The same W(u) from the survivors' side, for small H: the surviving
 // intermediates are a prefix of the degree-class index (vbydeg, degrees 1..H),
 // and every entry u of I(v) (the transposed multiset: one per occurrence of v

@@ -262,6 +262,8 @@ struct nlp_graph {
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
   bool hp_tie_select = true; // prune: the kept ties by radix select, not a sort (NLP_HASH_TIE_SORT=1 sorts)
   bool hp_rows8 = true;      // survivor count / fill with 8 consecutive entries per lane (NLP_HASH_ROWS8=0: one per lane)
+  bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
+  uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
   bool es_final = true;      // path 4's final order as one record sort (edgesort.hpp; NLP_ES_FINAL=0: two key sorts)
   unsigned occ_es = 256;     // resident k_es_pass workgroups
@@ -731,6 +733,8 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
   if (const char* ef = getenv("NLP_ES_FINAL")) g->es_final = ef[0] != '0';
   if (const char* hr = getenv("NLP_HASH_ROWS8")) g->hp_rows8 = hr[0] != '0';
+  if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
+  if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
   if (const char* ht = getenv("NLP_HASH_TIE_SORT")) g->hp_tie_select = ht[0] != '1';
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
@@ -1840,7 +1844,46 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       p_h = 0;
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
-    if (g->dcls && g->hp_dcls && g->hp_work_surv && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
+    bool one_done = false;
+    if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one && g->hp_sdo && g->drank && p.H >= 1 &&
+        p.H <= HP_DCLS_MAX && e1 > e0 && p_h != ~0ull && g->nnz < (1ull << HP_SDO_SH)) {
+      // one pass over the range's classes (hashpath.hpp k_hp_dcls_one); output sized by the
+      // degree histogram's P_H (an asymmetric graph's in-degrees may exceed it: overflow -> two passes)
+      uint64_t cap = std::min<uint64_t>(e1 - e0, p_h + p_h / 8 + 4096);
+      if (g->hp_one_cap) cap = std::min<uint64_t>(cap, g->hp_one_cap);  // test hook: force the overflow fallback
+      const uint64_t ntl = (e1 + HD_TILE - 1) / HD_TILE - e0 / HD_TILE;
+      uint32_t* scnt;
+      uint64_t* hd;  // [0] ticket + error, [1, 1 + ntl) descriptors
+      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
+      TRY(wsget(ws, B_HP_SOFF, nU + 1, &s_soff));
+      TRY(wsget(ws, B_HP_SKEYS, cap, &s_skeys));
+      TRY(wsget(ws, B_HP_SDO, cap, &s_sdo));
+      TRY(wsget(ws, B_HP_TPRE, ntl + 1, &hd));
+      TRY(hipMemsetAsync(hd, 0, (ntl + 1) * 8, st));
+      const unsigned gt = (unsigned)std::min<uint64_t>(ntl, 2048);
+      hipLaunchKernelGGL(k_hp_dcls_one, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                         (const uint32_t*)g->tile_row, s_skeys, s_sdo, cap, (unsigned long long*)wu,
+                         (const uint8_t*)g->drank, hd + 1, (uint32_t*)hd, (uint32_t*)hd + 1);
+      TRY(hipGetLastError());
+      LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
+      TRY(hipGetLastError());
+      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipMemcpyAsync(&g->host_small[11], hd, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      const uint32_t herr = (uint32_t)(g->host_small[11] >> 32);
+      if (herr & 2u) return NLP_ERR_DEVICE;  // a look-back gave up (never expected)
+      if (herr & 1u) {                      // more survivors than the histogram bound: the two-kernel build
+        TRY(hipMemsetAsync(wu, 0, nU * 8, st));
+        s_skeys = nullptr;
+        s_sdo = nullptr;
+      } else {
+        s_sorted = true;
+        one_done = true;
+      }
+    }
+    if (one_done) {
+    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
       // the survivor lists S(u) as the compaction of the range's entries by
       // degree class (sorted, no atomics; hashpath.hpp k_hp_dcls_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;

@@ -426,7 +426,10 @@ class _env:
 # 22 row batches gathering deg / off of every first hop (no packed survivor entries),
 # 23 the prune's kept ties by a full (u, w) sort instead of the radix select,
 # 24 survivor suffixes searched per call (no per-graph rank bytes), 25 survivor
-# counts and fill with one entry per lane (k_hp_dcls_rows / _fill instead of the *8 kernels)
+# counts and fill with one entry per lane (k_hp_dcls_rows / _fill instead of the *8 kernels),
+# 26 survivor counts and fill as two kernels (not k_hp_dcls_one), 27 k_hp_dcls_one's output
+# capacity overflowing (the two-kernel fallback), 28 the final order as two key sorts + gather
+# (not edgesort.hpp)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -441,7 +444,8 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_FINAL="0"), dict(NLP_HASH_SDO="0"), dict(NLP_HASH_TIE_SORT="1"),
-                 dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ROWS8="0")]
+                 dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ROWS8="0"), dict(NLP_HASH_ONE="0"),
+                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_ES_FINAL="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
