@@ -73,7 +73,22 @@ struct HpArgs {
   int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
   const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
   const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
+  const uint32_t* xs;    // per row: entries of N(u) at or below u (null: none; the exclusion starts after them)
 };
+
+// xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
+__global__ void k_hp_xs(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t S,
+                        uint32_t* __restrict__ xs) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < S; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t lo = off[u], hi = off[u + 1];
+    const uint64_t o = lo;
+    while (lo < hi) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (keys[m] <= (uint32_t)u) lo = m + 1; else hi = m;
+    }
+    xs[u] = (uint32_t)(lo - o);
+  }
+}
 constexpr int HP_SDO_SH = 40;  // offsets < 2^40 (guarded at the list build)
 
 // A row's first-hop list: S(u) when the survivor lists exist, else N(u).
@@ -1523,8 +1538,9 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       }
       wave_sync_lds();
     }
-    // first-order exclusion (predict.hxx:306-307)
-    hp_stream(a.g.keys + o0, du, (uint32_t)lane, 64u, [&](uint32_t x) {
+    // first-order exclusion (predict.hxx:306-307): the entries of N(u) above u
+    const uint32_t xu = a.xs ? a.xs[u] : 0u;
+    hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)lane, 64u, [&](uint32_t x) {
       if (x > u) hp_mark<false>(tb, mask, shift, x);
     });
     wave_sync_lds();
@@ -1696,37 +1712,44 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     *q0 = bb < nb ? bstart[bb] : 0u;
     *qn = bb < nb ? bstart[bb + 1] - *q0 : 0u;  // < 64 by the budget
   };
+  // per row: W+(u), S(u) bounds, deg u (the score) and the exclusion slice of
+  // N(u) -- its entries above u, [o0, o0 + dx)
   auto fetch_info = [&](uint32_t n, uint32_t uu, uint64_t* pW, uint64_t* ps0, uint32_t* pns, uint64_t* po0,
-                        uint32_t* pdu) {
+                        uint32_t* pdu, uint32_t* pdx) {
     if ((uint32_t)lane < n) {
       *pW = wu[uu - ua];
       *ps0 = a.soff[uu - a.sua];
       *pns = (uint32_t)(a.soff[uu - a.sua + 1] - *ps0);
-      *po0 = a.g.off[uu];
-      *pdu = (uint32_t)(a.g.off[uu + 1] - *po0);
+      const uint64_t ob = a.g.off[uu];
+      *pdu = (uint32_t)(a.g.off[uu + 1] - ob);
+      const uint32_t xu = a.xs ? a.xs[uu] : 0u;
+      *po0 = ob + xu;
+      *pdx = *pdu - xu;
     } else {
       *pW = 0;
       *ps0 = 0;
       *pns = 0;
       *po0 = 0;
       *pdu = 0;
+      *pdx = 0;
     }
   };
+  uint32_t dx = 0;
   fetch_bounds(b, &r0, &nr);
   u = (uint32_t)lane < nr ? rows[r0 + lane] : 0u;
-  fetch_info(nr, u, &W, &s0, &ns, &o0, &du);
+  fetch_info(nr, u, &W, &s0, &ns, &o0, &du, &dx);
   for (; b < nb;) {
     const uint32_t bn = b + stride;
     uint32_t pr0, pnr, pu = 0;
     if (nr == 0) {  // an empty batch (a row wider than the budget window skipped it)
       fetch_bounds(bn, &r0, &nr);
       u = (uint32_t)lane < nr ? rows[r0 + lane] : 0u;
-      fetch_info(nr, u, &W, &s0, &ns, &o0, &du);
+      fetch_info(nr, u, &W, &s0, &ns, &o0, &du, &dx);
       b = bn;
       continue;
     }
     fetch_bounds(bn, &pr0, &pnr);
-    const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(du);
+    const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(dx);
     s_u[wv][lane] = u;
     s_du[wv][lane] = du;
     s_s0[wv][lane] = s0;
@@ -1867,8 +1890,8 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     }
     wave_sync_lds();
     uint64_t pW, ps0, po0;
-    uint32_t pns, pdu;
-    fetch_info(pnr, pu, &pW, &ps0, &pns, &po0, &pdu);  // the next batch's row data, in flight during the drain
+    uint32_t pns, pdu, pdx;
+    fetch_info(pnr, pu, &pW, &ps0, &pns, &po0, &pdu, &pdx);  // the next batch's row data, in flight during the drain
     // drain: every entry scored for its own row (a list of the claimed slots
     // instead of this scan measured slower: the claims cost more in the insert
     // loop than the scan of empty slots)
@@ -1918,6 +1941,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     ns = pns;
     o0 = po0;
     du = pdu;
+    dx = pdx;
     b = bn;
   }
   hp_finish(sg, a, wedges);
@@ -2106,7 +2130,8 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
         }
         hp_sync<GLOBAL>();
       }
-      hp_stream(a.g.keys + o0, du, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
+      const uint32_t xu = a.xs ? a.xs[u] : 0u;  // the entries of N(u) above u
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
         if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
       });
       hp_sync<GLOBAL>();

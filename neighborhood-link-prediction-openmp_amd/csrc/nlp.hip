@@ -242,6 +242,7 @@ struct nlp_graph {
   uint8_t* dcls = nullptr;                     // min(deg keys[e], 255) per adjacency entry (path 4's survivor lists)
   uint32_t* kdeg = nullptr;                    // deg keys[e] per adjacency entry (path 4's count-metric row kernels)
   uint8_t* drank = nullptr;                    // entries with deg v <= 254: the row's rank in N(v) (survivor suffixes)
+  uint32_t* xs = nullptr;                      // per row: entries of N(u) at or below u (the exclusion walks the rest)
   // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
   uint64_t* truth = nullptr;
   uint64_t ntruth = 0;
@@ -385,6 +386,7 @@ void destroy_graph(nlp_graph* g) {
   if (g->dcls) (void)hipFree(g->dcls);
   if (g->kdeg) (void)hipFree(g->kdeg);
   if (g->drank) (void)hipFree(g->drank);
+  if (g->xs) (void)hipFree(g->xs);
   if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
@@ -558,6 +560,18 @@ nlp_status finish_graph(nlp_graph* g) {
       }
     }
     TRY(hipStreamSynchronize(st));
+  }
+  // per row the entries of N(u) at or below u: the first-order exclusion only
+  // marks x > u (predict.hxx:306-307 zeroes all of N(u), but only w > u are
+  // candidates), so path 4's row kernels walk N(u) from there
+  if (S > 0 && !(getenv("NLP_HASH_XS") && getenv("NLP_HASH_XS")[0] == '0')) {
+    if (hipMalloc(&g->xs, S * 4) == hipSuccess) {
+      LAUNCH(k_hp_xs, S, st, (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->xs);
+      TRY(hipGetLastError());
+    } else {
+      (void)hipGetLastError();
+      g->xs = nullptr;
+    }
   }
   // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
   TRY(hipMalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
@@ -2044,6 +2058,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.kdeg = g->kdeg;
     a.sdo = s_sdo;
     a.sua = ua;
+    a.xs = g->xs;
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0 && g->hp_tiers) {

@@ -429,7 +429,7 @@ class _env:
 # counts and fill with one entry per lane (k_hp_dcls_rows / _fill instead of the *8 kernels),
 # 26 survivor counts and fill as two kernels (not k_hp_dcls_one), 27 k_hp_dcls_one's output
 # capacity overflowing (the two-kernel fallback), 28 the final order as two key sorts + gather
-# (not edgesort.hpp)
+# (not edgesort.hpp), 29 the exclusion walking all of N(u) (no per-row start above u)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -445,7 +445,7 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_FINAL="0"), dict(NLP_HASH_SDO="0"), dict(NLP_HASH_TIE_SORT="1"),
                  dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ROWS8="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_ES_FINAL="0")]
+                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_ES_FINAL="0"), dict(NLP_HASH_XS="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
