@@ -41,6 +41,7 @@ constexpr int ES_TILE = ES_NT * ES_IPT;    // 4096 records per tile
 constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
 constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
 constexpr uint32_t ES_SPIN_LIMIT = 1u << 26;
+constexpr int ES_LBW = 16;                 // predecessors read per look-back round trip
 
 // 8-bit digit `shift` (bit offset) of K; `bits` < 8 for the top digit
 __device__ __forceinline__ uint32_t es_digit(uint32_t u, uint32_t w, float s, int vb, int shift) {
@@ -80,8 +81,12 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist(const uint32_t* __restrict__ 
     const float s = ok ? cs[j] : 0.0f;
     for (int p = 0; p < npass; ++p) {
       const uint32_t d = es_digit(u, w, s, vb, 8 * p);
-      const uint64_t peers = es_peers(d, ok);
-      if (ok && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+      if (8 * p + 8 <= 2 * vb) {  // a digit of (u, w): spread over its bins, one LDS atomic per record
+        if (ok) atomicAdd(&h[p][d], 1u);
+      } else {  // a digit of the score key: few bins, so one atomic per group of equal digits (8 ballots)
+        const uint64_t peers = es_peers(d, ok);
+        if (ok && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+      }
     }
   }
   __syncthreads();
@@ -192,19 +197,37 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
     if (t < 256) {
       uint64_t excl = 0;
       if (tile > 0) {
+        // windowed look-back: ES_LBW predecessors per round trip (the tiles in
+        // flight have published only their counts, so the nearest inclusive
+        // prefix can be hundreds of tiles back), consumed nearest first up to
+        // the first inclusive prefix or the first tile not yet counted
         int64_t j = (int64_t)tile - 1;
         uint32_t spins = 0;
-        while (j >= 0) {
-          const uint64_t x = es_load(desc + (uint64_t)j * 256 + t);
-          const uint64_t st = (x >> 46) & 3ull;
-          if ((x >> 48) != epoch || st == 0) {
+        bool fin = false;
+        while (!fin) {
+          uint64_t x[ES_LBW];
+#pragma unroll
+          for (int r = 0; r < ES_LBW; ++r)
+            x[r] = j - r >= 0 ? es_load(desc + (uint64_t)(j - r) * 256 + t) : (ep | ES_PFX);  // before tile 0: zero
+          int used = 0;
+          bool blocked = false;
+#pragma unroll
+          for (int r = 0; r < ES_LBW; ++r) {
+            if (fin || blocked) continue;
+            const uint64_t st = (x[r] >> 48) == epoch ? (x[r] >> 46) & 3ull : 0ull;
+            if (st == 0) {
+              blocked = true;
+              continue;
+            }
+            excl += x[r] & ES_VAL;
+            ++used;
+            fin = st == 2;
+          }
+          j -= used;
+          if (!fin && used == 0) {
             if (++spins > ES_SPIN_LIMIT) { atomicOr(err, 1u); break; }
             __builtin_amdgcn_s_sleep(1);
-            continue;
           }
-          excl += x & ES_VAL;
-          if (st == 2) break;
-          --j;
         }
         es_publish(desc + tile * 256 + t, ep | ES_PFX | (excl + cnt));
       }
