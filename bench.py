@@ -167,6 +167,32 @@ def cpu_baseline(path, metric, hub, k, ncand, budget_s=240.0, one_thread=True):
     return full, one
 
 
+def dropin_bench(csr, k, hubs, calls=3, timeout=600):
+    """The drop-in header's cost per call (tests/cpp/dropin_bench.cxx): the
+    reference's predictLinksJaccardCoefficientOmp<H>(x, {1, k}) through
+    include/nlp/predict.hxx on a host graph (DiGraphCsr-shaped, the same CSR),
+    as main.cxx:50 makes it -- graph fingerprint, prediction, the links copied
+    to the host as vector<tuple>.  first_call_ms includes the upload and the
+    per-graph build; dropin_ms_per_call is the steady call."""
+    exe = os.path.join(ROOT, "neighborhood-link-prediction-openmp_amd", "dropin_bench")
+    if not os.path.exists(exe):
+        return {"error": "dropin_bench not built"}
+    hs = ",".join(str(h) for h in hubs if h in (4, 8, 16, 32))
+    try:
+        r = subprocess.run([exe, csr, str(k), hs, str(calls)], capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    if r.returncode != 0:
+        return {"error": "rc %d: %s" % (r.returncode, r.stderr[-300:])}
+    try:
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": "unparsed: " + r.stdout[-300:]}
+    d["what"] = ("predictLinksJaccardCoefficientOmp<H>(x, {1, k}) via include/nlp/predict.hxx, host graph "
+                 "(DiGraphCsr arrays), links returned as vector<tuple> (main.cxx:50); wall ms per call")
+    return d
+
+
 def pmc_traffic(config, world, metric, hub, kernel):
     """HBM bytes per launch of a kernel from the committed PMC summaries
     (profiles/pmc_traffic.json: tools/pmc_summary.py over separate FETCH_SIZE /
@@ -280,6 +306,7 @@ def main():
     ap.add_argument("--wp-warmup", type=int, default=1)
     ap.add_argument("--wp-cpu-budget", type=float, default=300.0,
                     help="seconds allowed for the reference's all-cores run at the work point")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the C++ drop-in header timing")
     ap.add_argument("--pipelined", action="store_true",
                     help="N = 1: also time the same calls enqueued back to back (nlp_predict_device_async)")
     args = ap.parse_args()
@@ -429,6 +456,8 @@ def main():
                     wp["cpu_baseline"] = full
                 except Exception as e:
                     wp["cpu_baseline"] = {"error": repr(e)}
+            if csr is not None and not args.no_dropin:
+                line["dropin"] = dropin_bench(csr, k, [hub] + ([wp["H"]] if wp is not None else []))
             if tmpd is not None:
                 tmpd.cleanup()
         print(json.dumps(line), flush=True)

@@ -288,6 +288,26 @@ nlp_status nlp_delete_edges_device(const uint64_t* d_off, const uint32_t* d_keys
                                    uint32_t* rng_state, uint64_t* d_off2, uint32_t* d_keys2, uint64_t* nnz2,
                                    uint32_t* d_del_u, uint32_t* d_del_v, uint64_t* ndel, int device, void* stream);
 
+/* The same N1 / N2 for host callers (nlp_main, C++ drivers): a device-resident
+ * CSR object.  nlp_dcsr_ingest uploads the MatrixMarket file's directed pairs
+ * (host arrays, as nlp::readMtxPairs returns them) and runs nlp_ingest_device;
+ * nlp_dcsr_delete_batch runs nlp_delete_edges_device on it into a new object
+ * and copies the directed deletions (sorted, unique; at most del_cap) to the
+ * host arrays del_u / del_v (either may be NULL); nlp_graph_create_dcsr builds
+ * the graph handle from it without a host round trip.  nlp_dcsr_info also
+ * reports the sizes of the graph after readMtx (distinct pairs) and after
+ * symmetrize (before self-loop removal), the sizes main.cxx prints
+ * (main.cxx:241-245).  Synchronous; the default stream of `device`. */
+typedef struct nlp_dcsr nlp_dcsr;
+nlp_status nlp_dcsr_ingest(const uint32_t* src, const uint32_t* dst, uint64_t m, uint64_t n, int symmetric_input,
+                           int device, nlp_dcsr** out);
+nlp_status nlp_dcsr_delete_batch(const nlp_dcsr* x, uint64_t batch, uint32_t* rng_state, nlp_dcsr** out,
+                                 uint32_t* del_u, uint32_t* del_v, uint64_t del_cap, uint64_t* ndel);
+nlp_status nlp_dcsr_info(const nlp_dcsr* x, uint64_t* span, uint64_t* nnz, uint64_t* read_size, uint64_t* sym_size);
+nlp_status nlp_dcsr_copy(const nlp_dcsr* x, uint64_t* offsets /* span + 1 */, uint32_t* keys /* nnz */);
+void nlp_dcsr_destroy(nlp_dcsr* x);
+nlp_status nlp_graph_create_dcsr(const nlp_dcsr* x, nlp_graph** out);
+
 const char* nlp_status_string(nlp_status s);
 const char* nlp_metric_name(nlp_metric m);
 

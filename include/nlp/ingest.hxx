@@ -36,6 +36,9 @@
 #include <string>
 #include <utility>
 #include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 namespace nlp {
 
@@ -164,26 +167,43 @@ inline bool parseU64(const char*& p, const char* e, uint64_t& v) {
 
 }  // namespace detail
 
+/** The body of a MatrixMarket coordinate file: its order n = max(rows, cols),
+ *  the header's symmetry, and the directed pairs the reference's reader hands
+ *  to its graph (mtx.hxx:119-188: both directions for a symmetric header), in
+ *  file order. */
+struct MtxPairs {
+  uint64_t n = 0;
+  bool coordinate = false;
+  bool symmetric = false;
+  std::vector<uint32_t> src, dst;
+};
+
 /**
- * Read a MatrixMarket coordinate file as the reference does (readMtxOmpW with
- * weighted = false): header "%%MatrixMarket matrix coordinate <field> <sym>",
- * span = max(rows, cols) + 1, 1-based ids, symmetric / skew-symmetric headers
- * add both directions; every row is sorted and deduplicated.  `symmetricHeader`
- * receives whether the header said symmetric.
+ * Parse a MatrixMarket file's pairs on all threads (the reference's
+ * readMtxDoOmp parses 131072-line batches with `#pragma omp parallel for`,
+ * mtx.hxx:152-188): the file is read once, the body cut into one byte range
+ * per thread at line ends, every range parsed into its own pair list, the
+ * lists concatenated in file order.  A line that does not start with two
+ * integers ends the body (mtx.hxx:130); an id beyond n throws.
  */
-inline HostCsr readMtx(const std::string& path, bool* symmetricHeader = nullptr) {
+inline MtxPairs readMtxPairs(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("nlp::readMtx: cannot open " + path);
-  std::string text;
+  std::vector<char> text;
   {
-    std::vector<char> buf(1 << 24);
-    size_t n;
-    while ((n = fread(buf.data(), 1, buf.size(), f)) > 0) text.append(buf.data(), n);
+    fseek(f, 0, SEEK_END);
+    const long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    text.resize(sz > 0 ? (size_t)sz : 0);
+    if (!text.empty() && fread(text.data(), 1, text.size(), f) != text.size()) {
+      fclose(f);
+      throw std::runtime_error("nlp::readMtx: short read of " + path);
+    }
     fclose(f);
   }
   const char* p = text.data();
   const char* e = p + text.size();
-  bool symmetric = false, coordinate = false;
+  MtxPairs out;
   std::string line;
   // comments and the banner (mtx.hxx:42-48)
   while (p < e) {
@@ -195,35 +215,100 @@ inline HostCsr readMtx(const std::string& path, bool* symmetricHeader = nullptr)
     if (line.rfind("%%", 0) != 0) continue;
     char h[5][64] = {};
     sscanf(line.c_str(), "%63s %63s %63s %63s %63s", h[0], h[1], h[2], h[3], h[4]);
-    coordinate = strcmp(h[1], "matrix") == 0 && strcmp(h[2], "coordinate") == 0;
-    symmetric = strcmp(h[4], "symmetric") == 0 || strcmp(h[4], "skew-symmetric") == 0;
+    out.coordinate = strcmp(h[1], "matrix") == 0 && strcmp(h[2], "coordinate") == 0;
+    out.symmetric = strcmp(h[4], "symmetric") == 0 || strcmp(h[4], "skew-symmetric") == 0;
   }
-  if (symmetricHeader) *symmetricHeader = symmetric;
-  if (!coordinate) return HostCsr();  // the reference reads nothing (mtx.hxx:49)
+  if (!out.coordinate) return out;  // the reference reads nothing (mtx.hxx:49)
   unsigned long long rows = 0, cols = 0, size = 0;
   sscanf(line.c_str(), "%llu %llu %llu", &rows, &cols, &size);
-  const uint64_t n = std::max(rows, cols);
+  out.n = std::max(rows, cols);
+  if (out.n == 0) return out;
+  const uint64_t n = out.n;
+  const bool sym = out.symmetric;
+  // one byte range per thread, starting after a line end
+  int T = 1;
+#ifdef _OPENMP
+  T = omp_get_max_threads();
+#endif
+  const size_t body = (size_t)(e - p);
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, body / 4096 + 1));
+  std::vector<const char*> cut(T + 1);
+  cut[0] = p;
+  cut[T] = e;
+  for (int t = 1; t < T; ++t) {
+    const char* c = p + body * t / T;
+    const char* nl = c > p ? (const char*)memchr(c - 1, '\n', e - (c - 1)) : c;
+    cut[t] = nl ? std::max(cut[t - 1], nl + 1) : e;
+  }
+  std::vector<std::vector<uint32_t>> ps(T), pd(T);
+  std::vector<char> bad(T, 0), oob(T, 0);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t < T; ++t) {
+    const char* a = cut[t];
+    const char* z = cut[t + 1];
+    auto& su = ps[t];
+    auto& sv = pd[t];
+    su.reserve((size_t)(z - a) / 8 * (sym ? 2 : 1));
+    sv.reserve(su.capacity());
+    while (a < z) {
+      uint64_t u, v;
+      const char* q = a;
+      if (!detail::parseU64(q, z, u) || !detail::parseU64(q, z, v)) {
+        bad[t] = 1;  // the body ends here (mtx.hxx:130)
+        break;
+      }
+      const char* nl = (const char*)memchr(q, '\n', z - q);
+      a = nl ? nl + 1 : z;
+      if (u > n || v > n) {
+        oob[t] = 1;
+        break;
+      }
+      su.push_back((uint32_t)u);
+      sv.push_back((uint32_t)v);
+      if (sym) {
+        su.push_back((uint32_t)v);
+        sv.push_back((uint32_t)u);
+      }
+    }
+  }
+  // file order: the ranges up to the first one that ended the body
+  int last = T - 1;
+  for (int t = 0; t < T; ++t)
+    if (bad[t] || oob[t]) {
+      last = t;
+      break;
+    }
+  for (int t = 0; t <= last; ++t)
+    if (oob[t]) throw std::runtime_error("nlp::readMtx: vertex id beyond the header's order");
+  std::vector<size_t> at(last + 2, 0);
+  for (int t = 0; t <= last; ++t) at[t + 1] = at[t] + ps[t].size();
+  out.src.resize(at[last + 1]);
+  out.dst.resize(at[last + 1]);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t <= last; ++t) {
+    std::copy(ps[t].begin(), ps[t].end(), out.src.begin() + at[t]);
+    std::copy(pd[t].begin(), pd[t].end(), out.dst.begin() + at[t]);
+  }
+  return out;
+}
+
+/**
+ * Read a MatrixMarket coordinate file as the reference does (readMtxOmpW with
+ * weighted = false): header "%%MatrixMarket matrix coordinate <field> <sym>",
+ * span = max(rows, cols) + 1, 1-based ids, symmetric / skew-symmetric headers
+ * add both directions; every row is sorted and deduplicated.  `symmetricHeader`
+ * receives whether the header said symmetric.
+ */
+inline HostCsr readMtx(const std::string& path, bool* symmetricHeader = nullptr) {
+  MtxPairs mp = readMtxPairs(path);
+  if (symmetricHeader) *symmetricHeader = mp.symmetric;
+  if (!mp.coordinate) return HostCsr();
+  const uint64_t n = mp.n;
   HostCsr g;
   g.off.assign(n + 2, 0);
   if (n == 0) return g;
-  // edges in file order (rows keep arrival order until the update sorts them)
-  std::vector<uint32_t> eu, ev;
-  eu.reserve(symmetric ? 2 * size : size);
-  ev.reserve(symmetric ? 2 * size : size);
-  while (p < e) {
-    uint64_t u, v;
-    const char* q = p;
-    if (!detail::parseU64(q, e, u) || !detail::parseU64(q, e, v)) break;  // mtx.hxx:130
-    const char* nl = (const char*)memchr(q, '\n', e - q);
-    p = nl ? nl + 1 : e;
-    if (u > n || v > n) throw std::runtime_error("nlp::readMtx: vertex id beyond the header's order");
-    eu.push_back((uint32_t)u);
-    ev.push_back((uint32_t)v);
-    if (symmetric) {
-      eu.push_back((uint32_t)v);
-      ev.push_back((uint32_t)u);
-    }
-  }
+  const std::vector<uint32_t>& eu = mp.src;
+  const std::vector<uint32_t>& ev = mp.dst;
   // counting sort by source, stable (file order inside a row)
   for (size_t i = 0; i < eu.size(); ++i) ++g.off[eu[i] + 1];
   for (size_t u = 1; u < g.off.size(); ++u) g.off[u] += g.off[u - 1];

@@ -34,7 +34,7 @@
 // converted to a CSR with identity vertex ids (absent vertices get empty rows)
 // and uploaded once per distinct graph (detail::cachedGraph: the 99 calls
 // main.cxx makes per graph reuse one resident copy); a nlp::HipGraph keeps a
-// graph resident explicitly.  Devices: NLP_DEVICES or every gfx950 device
+// graph resident explicitly.  Devices: NLP_DEVICES or device 0
 // (defaultDevices(), the analogue of the reference's OpenMP team).
 #pragma once
 #include <algorithm>
@@ -101,38 +101,96 @@ struct has_csr_members<G, std::void_t<decltype(std::declval<const G&>().offsets[
                                       decltype(std::declval<const G&>().edgeKeys[0])>> : std::true_type {};
 }  // namespace detail
 
-/** Build the identity-id CSR of any graph concept G (csr.hxx:106-222 layout,
- *  without the dense renumbering so vertex ids are preserved): span(),
- *  hasVertex(u), forEachEdgeKey(u, fn) (Graph.hxx:59-169, DiGraph), or the
- *  offsets / degrees / edgeKeys arrays of a DiGraphCsr (Graph.hxx:383-639). */
+namespace detail {
+template <class G, class = void>
+struct has_degree : std::false_type {};
 template <class G>
-inline void graphToCsr(const G& x, std::vector<uint64_t>& offsets, std::vector<uint32_t>& keys) {
-  const size_t S = x.span();
-  offsets.assign(S + 1, 0);
-  keys.clear();
-  if constexpr (detail::has_csr_members<G>::value) {
-    size_t M = 0;
-    for (size_t u = 0; u < S; ++u) M += size_t(x.degrees[u]);
-    keys.reserve(M);
-    for (size_t u = 0; u < S; ++u) {  // row u: degrees[u] keys from offsets[u] (rows may leave gaps)
-      offsets[u] = keys.size();
-      const size_t o = size_t(x.offsets[u]), d = size_t(x.degrees[u]);
-      for (size_t i = 0; i < d; ++i) keys.push_back(uint32_t(x.edgeKeys[o + i]));
-    }
+struct has_degree<G, std::void_t<decltype(std::declval<const G&>().degree(typename G::key_type()))>> : std::true_type {};
+
+// row u's entry count: DiGraphCsr degrees[], the concept's degree(u) (Graph.hxx:167), else counted
+template <class G>
+inline size_t rowDegree(const G& x, size_t u) {
+  if constexpr (has_csr_members<G>::value) {
+    return size_t(x.degrees[u]);
   } else {
-    for (size_t u = 0; u < S; ++u) {
-      offsets[u] = keys.size();
-      if (!x.hasVertex(typename G::key_type(u))) continue;
-      x.forEachEdgeKey(typename G::key_type(u), [&](auto v) { keys.push_back(uint32_t(v)); });
+    if (!x.hasVertex(typename G::key_type(u))) return 0;
+    if constexpr (has_degree<G>::value) {
+      return size_t(x.degree(typename G::key_type(u)));
+    } else {
+      size_t d = 0;
+      x.forEachEdgeKey(typename G::key_type(u), [&](auto) { ++d; });
+      return d;
     }
   }
-  offsets[S] = keys.size();
+}
+
+// f(i, key) for the entries of row u in order
+template <class G, class F>
+inline void forRow(const G& x, size_t u, F f) {
+  if constexpr (has_csr_members<G>::value) {
+    const size_t o = size_t(x.offsets[u]), d = size_t(x.degrees[u]);
+    for (size_t i = 0; i < d; ++i) f(i, uint32_t(x.edgeKeys[o + i]));
+  } else {
+    if (!x.hasVertex(typename G::key_type(u))) return;
+    size_t i = 0;
+    x.forEachEdgeKey(typename G::key_type(u), [&](auto v) { f(i++, uint32_t(v)); });
+  }
+}
+
+inline uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+}  // namespace detail
+
+/** Build the identity-id CSR of any graph concept G (csr.hxx:106-222 layout,
+ *  without the dense renumbering so vertex ids are preserved): span(),
+ *  hasVertex(u), degree(u), forEachEdgeKey(u, fn) (Graph.hxx:59-169, DiGraph),
+ *  or the offsets / degrees / edgeKeys arrays of a DiGraphCsr (Graph.hxx:383-639).
+ *  Rows are counted, scanned and filled in parallel (OpenMP when the caller
+ *  compiles with it, as main.cxx does). */
+template <class G>
+inline void graphToCsr(const G& x, std::vector<uint64_t>& offsets, std::vector<uint32_t>& keys) {
+  const long long S = (long long)x.span();
+  offsets.assign(size_t(S) + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (long long u = 0; u < S; ++u) offsets[size_t(u) + 1] = detail::rowDegree(x, size_t(u));
+  for (long long u = 0; u < S; ++u) offsets[size_t(u) + 1] += offsets[size_t(u)];
+  keys.resize(size_t(offsets[size_t(S)]));
+  uint32_t* k = keys.data();
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (long long u = 0; u < S; ++u) {
+    uint32_t* row = k + offsets[size_t(u)];
+    detail::forRow(x, size_t(u), [&](size_t i, uint32_t v) { row[i] = v; });
+  }
+}
+
+/** 64-bit fingerprint of a graph's adjacency: the span, then per row its id,
+ *  degree and keys in order (a polynomial hash, mixed), summed over the rows --
+ *  one parallel read of the graph, no copy.  `entries` receives the entry count. */
+template <class G>
+inline uint64_t graphFingerprint(const G& x, uint64_t* entries) {
+  const long long S = (long long)x.span();
+  uint64_t h = 0, m = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : h, m)
+  for (long long u = 0; u < S; ++u) {
+    uint64_t r = 0x9E3779B97F4A7C15ull * uint64_t(u + 1), d = 0;
+    detail::forRow(x, size_t(u), [&](size_t, uint32_t v) {
+      r = r * 0x100000001B3ull + v;
+      ++d;
+    });
+    h += detail::mix64(r ^ (d << 40) ^ uint64_t(u));
+    m += d;
+  }
+  if (entries) *entries = m;
+  return detail::mix64(h ^ uint64_t(S));
 }
 
 /** The devices a graph handle uses by default -- the analogue of the
  *  reference's omp_get_max_threads() team (predict.hxx:413): NLP_DEVICES
  *  (comma-separated HIP ordinals; repeats = logical partitions on one device),
- *  else every visible gfx950 device. */
+ *  else device 0. */
 inline std::vector<int> defaultDevices() {
   std::vector<int> d;
   if (const char* e = std::getenv("NLP_DEVICES")) {
@@ -146,10 +204,9 @@ inline std::vector<int> defaultDevices() {
       }
     }
   }
-  if (d.empty()) {
-    const int n = nlp_device_count();
-    for (int i = 0; i < n; ++i) d.push_back(i);
-  }
+  // without NLP_DEVICES: device 0 alone.  The multi-device handle's
+  // cross-device peer copies have been run only with logical partitions on
+  // one GPU, so spreading over every device is opt-in.
   if (d.empty()) d.push_back(0);  // no device: nlp_graph_create reports NLP_ERR_NODEVICE
   return d;
 }
@@ -159,6 +216,8 @@ class HipGraph {
  public:
   using key_type = uint32_t;
   HipGraph() = default;
+  /** Takes ownership of a handle (nlp_graph_create*, nlp_graph_create_dcsr). */
+  explicit HipGraph(nlp_graph* g) : g_(g) {}
   HipGraph(const uint64_t* offsets, const uint32_t* keys, uint64_t span, int device = 0) {
     check(nlp_graph_create(offsets, keys, span, device, &g_), "nlp_graph_create");
   }
@@ -235,37 +294,46 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
                          me ? buf.data() : nullptr, &n, &t),
           "nlp_predict_ex");
   }
-  std::vector<std::tuple<K, K, W>> a;
-  a.reserve(n);
-  for (uint64_t i = 0; i < n; ++i) a.emplace_back(K(buf[i].u), K(buf[i].v), W(buf[i].score));
+  std::vector<std::tuple<K, K, W>> a(n);
+  const nlp_edge* b = buf.data();
+#pragma omp parallel for schedule(static)
+  for (long long i = 0; i < (long long)n; ++i) a[size_t(i)] = std::tuple<K, K, W>(K(b[i].u), K(b[i].v), W(b[i].score));
   return PredictLinkResult<K, W>(std::move(a), t.total_ms, t.score_ms);
 }
 
 namespace detail {
 // The graph handle of the last graph predicted on from this thread.  main.cxx
 // runs 99 predictions per graph (PREDICT_LINKS_ALL, main.cxx:67-80, 212-220)
-// on the same object: the CSR is rebuilt on the host each call (O(M), like
-// the reference's own pass over the graph) and compared with the resident
-// one, so the graph is uploaded and prepared (degrees, index, membership
-// table) once per distinct graph.
+// on the same object, so the graph is uploaded and prepared (degrees, index,
+// membership table) once per distinct graph.  A call recognises the resident
+// graph by the object's address, span and entry count and a 64-bit
+// fingerprint of its adjacency (graphFingerprint: one parallel read, no CSR
+// built, no host copy kept); only a different graph is converted and uploaded.
+// (Two different adjacencies share a fingerprint with probability ~2^-64.)
 struct GraphCache {
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> keys;
+  const void* addr = nullptr;
+  size_t span = 0;
+  uint64_t entries = 0, fp = 0;
   std::vector<int> devices;
   HipGraph g;
 };
 template <class G>
 inline const HipGraph& cachedGraph(const G& x) {
   static thread_local GraphCache c;
-  std::vector<uint64_t> off;
-  std::vector<uint32_t> keys;
-  graphToCsr(x, off, keys);
+  uint64_t m = 0;
+  const uint64_t fp = graphFingerprint(x, &m);
   std::vector<int> devs = defaultDevices();
-  if (!c.g.get() || devs != c.devices || off != c.off || keys != c.keys) {
+  if (!c.g.get() || devs != c.devices || c.addr != (const void*)&x || c.span != size_t(x.span()) ||
+      c.entries != m || c.fp != fp) {
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> keys;
+    graphToCsr(x, off, keys);
     c.g.create(off.data(), keys.empty() ? nullptr : keys.data(), off.size() - 1, devs);
     c.devices = devs;
-    c.off.swap(off);
-    c.keys.swap(keys);
+    c.addr = (const void*)&x;
+    c.span = size_t(x.span());
+    c.entries = m;
+    c.fp = fp;
   }
   return c.g;
 }

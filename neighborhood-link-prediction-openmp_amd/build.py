@@ -78,10 +78,46 @@ def build_main(verbose=True):
     return MAIN_BIN
 
 
+INGEST_SRC = os.path.join(ROOT, "tests", "cpp", "ingest_dev_main.cxx")
+INGEST_BIN = os.path.join(HERE, "ingest_dev_main")
+
+
+def build_ingest_dev(verbose=True):
+    """ingest_dev_main: nlp_main's device ingest route (readMtxPairs + nlp_dcsr_*) for the GPU ingest tests."""
+    deps = [INGEST_SRC, LIB] + [os.path.join(ROOT, "include", "nlp", f) for f in ("predict.hxx", "ingest.hxx")]
+    if os.path.exists(INGEST_BIN) and all(os.path.getmtime(d) <= os.path.getmtime(INGEST_BIN) for d in deps):
+        return INGEST_BIN
+    cmd = ["g++", "-std=c++17", "-O2", "-fopenmp", "-I", os.path.join(ROOT, "include"), INGEST_SRC, "-L", HERE,
+           "-lnlp", "-Wl,-rpath," + HERE, "-o", INGEST_BIN]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return INGEST_BIN
+
+
+BENCH_SRC = os.path.join(ROOT, "tests", "cpp", "dropin_bench.cxx")
+BENCH_BIN = os.path.join(HERE, "dropin_bench")
+
+
+def build_dropin_bench(verbose=True):
+    """dropin_bench: the drop-in header's cost per call (bench.py's dropin object), OpenMP like main.cxx."""
+    deps = [BENCH_SRC, LIB, os.path.join(ROOT, "include", "nlp", "predict.hxx")]
+    if os.path.exists(BENCH_BIN) and all(os.path.getmtime(d) <= os.path.getmtime(BENCH_BIN) for d in deps):
+        return BENCH_BIN
+    cmd = ["g++", "-std=c++17", "-O3", "-fopenmp", "-I", os.path.join(ROOT, "include"), BENCH_SRC, "-L", HERE,
+           "-lnlp", "-Wl,-rpath," + HERE, "-o", BENCH_BIN]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return BENCH_BIN
+
+
 def build(force=False, verbose=True):
     if not force and not needs_build():
         build_cpp_test(verbose)
         build_main(verbose)
+        build_dropin_bench(verbose)
+        build_ingest_dev(verbose)
         return LIB
     cmd = [hipcc()] + HIPCC_FLAGS + [f for f in os.environ.get("NLP_HIPCC_EXTRA", "").split() if f] + SOURCES + \
         ["-o", LIB + ".tmp"]
@@ -91,6 +127,8 @@ def build(force=False, verbose=True):
     os.replace(LIB + ".tmp", LIB)
     build_cpp_test(verbose)
     build_main(verbose)
+    build_dropin_bench(verbose)
+    build_ingest_dev(verbose)
     return LIB
 
 

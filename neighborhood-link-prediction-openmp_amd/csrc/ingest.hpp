@@ -41,6 +41,24 @@ __global__ void k_in_pairs(const uint32_t* __restrict__ src, const uint32_t* __r
   if (__ballot(oob) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
 }
 
+// cnt[0] += distinct keys, cnt[1] += distinct keys with high == low half (self loops) of a sorted array
+__global__ void k_in_count_distinct(const uint64_t* __restrict__ k, uint64_t n, unsigned long long* __restrict__ cnt) {
+  unsigned long long a = 0, b = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (i == 0 || k[i] != k[i - 1]) {
+      ++a;
+      b += (k[i] >> 32) == (k[i] & 0xffffffffull) ? 1 : 0;
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (a) atomicAdd(&cnt[0], a);
+    if (b) atomicAdd(&cnt[1], b);
+  }
+}
+
 // flag[i] = 1 when sorted key i differs from key i - 1 (unique)
 __global__ void k_in_first(const uint64_t* __restrict__ k, uint64_t n, uint8_t* __restrict__ flag) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)

@@ -3974,6 +3974,153 @@ nlp_status nlp_delete_edges_device(const uint64_t* d_off, const uint32_t* d_keys
 
 }  // extern "C"
 
+// ---------------------------------------------------------------- device CSR (N1 / N2 for host callers)
+struct nlp_dcsr {
+  int device = 0;
+  uint64_t span = 0, nnz = 0;
+  uint64_t* off = nullptr;
+  uint32_t* keys = nullptr;
+  uint64_t read_size = 0, sym_size = 0;  // the graph after readMtx and after symmetrize (N1 stages)
+};
+
+namespace {
+void dcsr_free(nlp_dcsr* x) {
+  if (!x) return;
+  (void)hipSetDevice(x->device);
+  if (x->off) (void)hipFree(x->off);
+  if (x->keys) (void)hipFree(x->keys);
+  delete x;
+}
+}  // namespace
+
+extern "C" {
+
+nlp_status nlp_dcsr_ingest(const uint32_t* src, const uint32_t* dst, uint64_t m, uint64_t n, int symmetric_input,
+                           int device, nlp_dcsr** out) {
+  if (!out || (m && (!src || !dst)) || n >= (1ull << 31)) return NLP_ERR_INVALID;
+  *out = nullptr;
+  nlp_status s = check_device(device);
+  if (s != NLP_OK) return s;
+  TRY(hipSetDevice(device));
+  nlp_dcsr* x = new (std::nothrow) nlp_dcsr();
+  if (!x) return NLP_ERR_NOMEM;
+  x->device = device;
+  x->span = n + 1;
+  DevTmp tmp;
+  uint32_t *ds = nullptr, *dd = nullptr;
+  if (tmp.get(&ds, m) != hipSuccess || tmp.get(&dd, m) != hipSuccess ||
+      hipMalloc(&x->off, (n + 2) * 8) != hipSuccess || hipMalloc(&x->keys, std::max<uint64_t>(2 * m, 1) * 4) != hipSuccess) {
+    dcsr_free(x);
+    return NLP_ERR_NOMEM;
+  }
+  if (m && (hipMemcpy(ds, src, m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dd, dst, m * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+    dcsr_free(x);
+    return NLP_ERR_DEVICE;
+  }
+  // the stage sizes main.cxx prints: distinct pairs (readMtx), then + the one
+  // self loop per row that removeSelfLoops takes out again
+  uint64_t* e;
+  uint64_t* cnt;
+  if (tmp.get(&e, std::max<uint64_t>(m, 1)) != hipSuccess || tmp.get(&cnt, 2) != hipSuccess) {
+    dcsr_free(x);
+    return NLP_ERR_NOMEM;
+  }
+  s = nlp_ingest_device(ds, dd, m, n, symmetric_input, x->off, x->keys, std::max<uint64_t>(2 * m, 1), &x->nnz, device,
+                        nullptr);
+  if (s != NLP_OK) {
+    dcsr_free(x);
+    return s;
+  }
+  if (m) {  // distinct pairs and distinct self loops
+    LAUNCH(k_in_pairs, m, nullptr, (const uint32_t*)ds, (const uint32_t*)dd, m, n, e, (uint32_t*)cnt);
+    int shifts[16];
+    const int vb = std::max(1, bits_for(n));
+    const int np = key_shifts(vb, 32, vb, shifts);
+    uint64_t* e2;
+    if (tmp.get(&e2, m) != hipSuccess) {
+      dcsr_free(x);
+      return NLP_ERR_NOMEM;
+    }
+    if (sort_u64_keys(&e, &e2, m, shifts, np, tmp, nullptr) != hipSuccess ||
+        hipMemset(cnt, 0, 16) != hipSuccess) {
+      dcsr_free(x);
+      return NLP_ERR_DEVICE;
+    }
+    LAUNCH(k_in_count_distinct, m, nullptr, (const uint64_t*)e, m, (unsigned long long*)cnt);
+    uint64_t h[2] = {0, 0};
+    if (hipMemcpy(h, cnt, 16, hipMemcpyDeviceToHost) != hipSuccess) {
+      dcsr_free(x);
+      return NLP_ERR_DEVICE;
+    }
+    x->read_size = h[0];
+    x->sym_size = x->nnz + h[1];
+  }
+  *out = x;
+  return NLP_OK;
+}
+
+nlp_status nlp_dcsr_delete_batch(const nlp_dcsr* x, uint64_t batch, uint32_t* rng_state, nlp_dcsr** out,
+                                 uint32_t* del_u, uint32_t* del_v, uint64_t del_cap, uint64_t* ndel) {
+  if (!x || !out || !rng_state || !ndel) return NLP_ERR_INVALID;
+  *out = nullptr;
+  *ndel = 0;
+  TRY(hipSetDevice(x->device));
+  nlp_dcsr* y = new (std::nothrow) nlp_dcsr();
+  if (!y) return NLP_ERR_NOMEM;
+  y->device = x->device;
+  y->span = x->span;
+  DevTmp tmp;
+  uint32_t *du = nullptr, *dv = nullptr;
+  if (hipMalloc(&y->off, (x->span + 1) * 8) != hipSuccess ||
+      hipMalloc(&y->keys, std::max<uint64_t>(x->nnz, 1) * 4) != hipSuccess || tmp.get(&du, 2 * batch) != hipSuccess ||
+      tmp.get(&dv, 2 * batch) != hipSuccess) {
+    dcsr_free(y);
+    return NLP_ERR_NOMEM;
+  }
+  uint64_t nd = 0;
+  nlp_status s = nlp_delete_edges_device(x->off, x->keys, x->span, batch, rng_state, y->off, y->keys, &y->nnz, du, dv,
+                                         &nd, x->device, nullptr);
+  if (s != NLP_OK) {
+    dcsr_free(y);
+    return s;
+  }
+  *ndel = nd;
+  if ((del_u || del_v) && nd > del_cap) {
+    dcsr_free(y);
+    return NLP_ERR_CAPACITY;
+  }
+  if (nd && ((del_u && hipMemcpy(del_u, du, nd * 4, hipMemcpyDeviceToHost) != hipSuccess) ||
+             (del_v && hipMemcpy(del_v, dv, nd * 4, hipMemcpyDeviceToHost) != hipSuccess))) {
+    dcsr_free(y);
+    return NLP_ERR_DEVICE;
+  }
+  y->read_size = y->sym_size = y->nnz;
+  *out = y;
+  return NLP_OK;
+}
+
+nlp_status nlp_dcsr_info(const nlp_dcsr* x, uint64_t* span, uint64_t* nnz, uint64_t* read_size, uint64_t* sym_size) {
+  if (!x) return NLP_ERR_INVALID;
+  if (span) *span = x->span;
+  if (nnz) *nnz = x->nnz;
+  if (read_size) *read_size = x->read_size;
+  if (sym_size) *sym_size = x->sym_size;
+  return NLP_OK;
+}
+
+nlp_status nlp_dcsr_copy(const nlp_dcsr* x, uint64_t* off, uint32_t* keys) {
+  if (!x) return NLP_ERR_INVALID;
+  TRY(hipSetDevice(x->device));
+  if (off) TRY(hipMemcpy(off, x->off, (x->span + 1) * 8, hipMemcpyDeviceToHost));
+  if (keys && x->nnz) TRY(hipMemcpy(keys, x->keys, x->nnz * 4, hipMemcpyDeviceToHost));
+  return NLP_OK;
+}
+
+void nlp_dcsr_destroy(nlp_dcsr* x) { dcsr_free(x); }
+
+}  // extern "C"
+
 namespace {
 
 }  // namespace
@@ -4006,6 +4153,11 @@ nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint6
   if (s != NLP_OK) { destroy_graph(g); return s; }
   *out = g;
   return NLP_OK;
+}
+
+nlp_status nlp_graph_create_dcsr(const nlp_dcsr* x, nlp_graph** out) {
+  if (!x || !out) return NLP_ERR_INVALID;
+  return nlp_graph_create_device(x->off, x->keys, x->span, x->nnz, x->device, nullptr, out);
 }
 
 nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_keys, uint64_t span, uint64_t nnz,

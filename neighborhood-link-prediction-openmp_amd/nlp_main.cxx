@@ -1,6 +1,8 @@
 // nlp_main.cxx -- the reference experiment driver (main.cxx) on the MI355X
-// library: SURVEY.md §8(f) N4, with the N1/N2 host ingest (nlp/ingest.hxx) and
-// the N3 device evaluation (nlp_set_truth / nlp_last_common).
+// library: SURVEY.md §8(f) N4, with N1/N2 on the device (the MatrixMarket
+// pairs parsed on all host threads by nlp::readMtxPairs, then nlp_dcsr_ingest
+// and nlp_dcsr_delete_batch; NLP_HOST_INGEST=1: the host restatement
+// nlp/ingest.hxx) and the N3 device evaluation (nlp_set_truth / nlp_last_common).
 //
 //   nlp_main <graph.mtx> [symmetric=0] [weighted=0]
 //
@@ -92,23 +94,48 @@ int main(int argc, char** argv) {
   const int device = envi("NLP_DEVICE", 0);
   printf("OMP_NUM_THREADS=%d\n", threads);
   printf("Loading graph %s ...\n", file);
+  // N1 / N2 on the device (default): the file's pairs parsed on all host
+  // threads (nlp::readMtxPairs, as readMtxDoOmp), then ingest and every
+  // deletion batch on the GPU (nlp_dcsr_*); NLP_HOST_INGEST=1 keeps the host
+  // restatement (nlp/ingest.hxx) end to end.
+  const bool host = envi("NLP_HOST_INGEST", 0) != 0;
   nlp::HostCsr x;
+  nlp_dcsr* dx = nullptr;
+  size_t xsize = 0;
   try {
-    x = nlp::readMtx(file);
+    if (host) {
+      x = nlp::readMtx(file);
+      printGraph(x, "");
+      if (!symmetric) {
+        x = nlp::symmetrize(x);
+        printGraph(x, " (symmetrize)");
+      }
+      x = nlp::removeSelfLoops(x);
+      printGraph(x, " (removeSelfLoops)");
+      xsize = x.size();
+    } else {
+      nlp::MtxPairs mp = nlp::readMtxPairs(file);
+      nlp::check(nlp_dcsr_ingest(mp.src.empty() ? nullptr : mp.src.data(), mp.dst.empty() ? nullptr : mp.dst.data(),
+                                 mp.src.size(), mp.n, symmetric ? 1 : 0, device, &dx),
+                 "nlp_dcsr_ingest");
+      uint64_t span = 0, nnz = 0, rs = 0, ss = 0;
+      nlp::check(nlp_dcsr_info(dx, &span, &nnz, &rs, &ss), "nlp_dcsr_info");
+      printf("order: %llu size: %llu [directed] {}\n", (unsigned long long)(span - 1), (unsigned long long)rs);
+      if (!symmetric)
+        printf("order: %llu size: %llu [directed] {} (symmetrize)\n", (unsigned long long)(span - 1),
+               (unsigned long long)ss);
+      printf("order: %llu size: %llu [directed] {} (removeSelfLoops)\n", (unsigned long long)(span - 1),
+             (unsigned long long)nnz);
+      xsize = nnz;
+    }
   } catch (const std::exception& e) {
     fprintf(stderr, "nlp_main: %s\n", e.what());
     return 1;
   }
-  printGraph(x, "");
-  if (!symmetric) {
-    x = nlp::symmetrize(x);
-    printGraph(x, " (symmetrize)");
-  }
-  x = nlp::removeSelfLoops(x);
-  printGraph(x, " (removeSelfLoops)");
   std::default_random_engine rnd;
-  if (getenv("NLP_SEED")) rnd.seed((unsigned)strtoul(getenv("NLP_SEED"), nullptr, 10));
-  else rnd.seed(std::random_device()());
+  uint32_t seed = getenv("NLP_SEED") ? (uint32_t)strtoul(getenv("NLP_SEED"), nullptr, 10) : std::random_device()();
+  rnd.seed(seed);
+  uint32_t rng = seed;  // the device deletions continue one minstd_rand0 engine through its state
   std::vector<const Metric*> metrics;
   for (const auto& m : envlist("NLP_METRICS", "CN,JAC,SOR,SAL,HPI,HDI,LHN,AA,RA"))
     for (const auto& mm : METRICS)
@@ -119,16 +146,39 @@ int main(int argc, char** argv) {
   const char* dStep = getenv("BATCH_DELETIONS_STEP");
   for (double d = envd("BATCH_DELETIONS_BEGIN", 0.0001);;) {  // runBatches, main.cxx:157-179
     for (int r = 0; r < repeatBatch; ++r) {
-      nlp::HostCsr y = x;
+      nlp::HostCsr y;
+      if (host) y = x;
+      const nlp_dcsr* cur = dx;  // device route: the batch graph (dx itself before the first batch)
       for (int seq = 0; seq < batchLength; ++seq) {
-        auto del = nlp::generateEdgeDeletions(rnd, y, (size_t)(d * x.size() / 2), 1, x.span() - 1, true);
-        nlp::tidyDeletions(del, y);
-        y = nlp::applyDeletions(y, del);
-        if (del.empty()) continue;  // main.cxx:209
-        std::vector<uint32_t> du(del.size()), dv(del.size());
-        for (size_t i = 0; i < del.size(); ++i) { du[i] = del[i].first; dv[i] = del[i].second; }
-        nlp::HipGraph hg(y.off.data(), y.keys.empty() ? nullptr : y.keys.data(), y.span(), device);
+        const size_t batch = (size_t)(d * xsize / 2);
+        std::vector<uint32_t> du, dv;
+        nlp_graph* gh = nullptr;
+        if (host) {
+          auto del = nlp::generateEdgeDeletions(rnd, y, batch, 1, y.span() - 1, true);
+          nlp::tidyDeletions(del, y);
+          y = nlp::applyDeletions(y, del);
+          du.resize(del.size());
+          dv.resize(del.size());
+          for (size_t i = 0; i < del.size(); ++i) { du[i] = del[i].first; dv[i] = del[i].second; }
+        } else {
+          nlp_dcsr* nx = nullptr;
+          du.resize(2 * batch);
+          dv.resize(2 * batch);
+          uint64_t nd = 0;
+          nlp::check(nlp_dcsr_delete_batch(cur, batch, &rng, &nx, du.data(), dv.data(), du.size(), &nd),
+                     "nlp_dcsr_delete_batch");
+          du.resize(nd);
+          dv.resize(nd);
+          if (cur != dx) nlp_dcsr_destroy(const_cast<nlp_dcsr*>(cur));
+          cur = nx;
+        }
+        if (du.empty()) continue;  // main.cxx:209
+        if (host) nlp::check(nlp_graph_create(y.off.data(), y.keys.empty() ? nullptr : y.keys.data(), y.span(), device, &gh),
+                             "nlp_graph_create");
+        else nlp::check(nlp_graph_create_dcsr(cur, &gh), "nlp_graph_create_dcsr");
+        nlp::HipGraph hg(gh);
         nlp::check(nlp_set_truth(hg.get(), du.data(), dv.data(), du.size()), "nlp_set_truth");
+        struct Del { size_t n; size_t size() const { return n; } } del{du.size()};
         const size_t k = del.size() / 2;  // insertions0.size() / 2 (main.cxx:50)
         for (const Metric* m : metrics) {
           for (uint32_t H : hubs) {
@@ -144,10 +194,12 @@ int main(int argc, char** argv) {
           }
         }
       }
+      if (cur != dx) nlp_dcsr_destroy(const_cast<nlp_dcsr*>(cur));
     }
     if (d >= dEnd) break;
     d = std::min(step(d, dStep), dEnd);
   }
+  if (dx) nlp_dcsr_destroy(dx);
   printf("\n");
   return 0;
 }

@@ -119,3 +119,69 @@ def test_ingest_rejects_id_above_n(gpu):
     assert e.value.status == 1
     off, keys = gpu.ingest_device(src, dst, 9)  # the same pairs with n large enough
     assert int(off[-1]) == keys.numel() == 8
+
+
+def _dev_route(tmp_path, mtx_bytes, seed, d):
+    """nlp_main's ingest route (tests/cpp/ingest_dev_main.cxx: readMtxPairs on all
+    threads, nlp_dcsr_ingest, nlp_dcsr_delete_batch) on a MatrixMarket text."""
+    import json
+    import subprocess
+    from nlp_amd import build as B
+    exe = B.build_ingest_dev(verbose=False)
+    mtx = str(tmp_path / "in.mtx")
+    open(mtx, "wb").write(mtx_bytes)
+    r = subprocess.run([exe, mtx, str(seed), repr(d), str(tmp_path / "dev")], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-1000:]
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    off, keys = pyoracle.read_csr(str(tmp_path / "dev.csr"))
+    du, dw = pyoracle.read_deletions(str(tmp_path / "dev.del"))
+    return off, keys, du, dw, json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("name", ["general", "sym", "d0"])
+def test_gpu_device_route_matches_reference_fixtures(gpu, tmp_path, name):
+    """N1 at the drivers' level: nlp_main's route -- parallel
+    MatrixMarket parse + nlp_dcsr_* -- byte for byte against the reference's ingest."""
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "ingest_%s.npz" % name), allow_pickle=False))
+    off, keys, du, dw, info = _dev_route(tmp_path, g["mtx"].tobytes(), int(g["seed"][0]), float(g["d"][0]))
+    assert np.array_equal(off, g["offsets"]) and np.array_equal(keys, g["keys"])
+    assert np.array_equal(du, g["del_u"]) and np.array_equal(dw, g["del_w"])
+
+
+@pytest.mark.parametrize("name,params", [("g300", (300, 1200, 0.6, 1)), ("g3k", (3000, 20000, 0.6, 7))])
+def test_gpu_device_route_reproduces_prediction_fixtures(gpu, tmp_path, name, params):
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import chung_lu_mtx
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"), allow_pickle=False))
+    mtx = str(tmp_path / "gen.mtx")
+    chung_lu_mtx(mtx, *params)
+    off, keys, du, dw, info = _dev_route(tmp_path, open(mtx, "rb").read(), 42, 0.1)
+    assert np.array_equal(off, g["offsets"]) and np.array_equal(keys, g["keys"])
+    assert np.array_equal(du, g["del_u"]) and np.array_equal(dw, g["del_w"])
+
+
+@pytest.mark.timeout(300)
+def test_gpu_device_route_c2_size_file(gpu, tmp_path):
+    """A generated C2-sized MatrixMarket file (soc-LiveJournal1 shape: 4.85 M
+    vertices, 69 M lines, ~1 GB of text) through nlp_main's route: parsed on
+    all threads and ingested on the device in seconds (times reported)."""
+    import json
+    import subprocess
+    from nlp_amd import build as B
+    exe = B.build_ingest_dev(verbose=False)
+    mtx = str(tmp_path / "c2.mtx")
+    subprocess.run([exe, "gen", mtx, "4847571", "68993773", "0.6", "12"], check=True, timeout=240)
+    r = subprocess.run([exe, mtx, "42", "0.1", str(tmp_path / "c2")], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-1000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(info))
+    d = os.environ.get("NLP_TEST_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "c2_mtx_ingest.json"), "w") as f:
+            json.dump(info, f)
+    assert info["lines"] == 68993773
+    assert info["size"] > 0.9 * 2 * 68993773 * 0.95  # symmetrized, few duplicates / self loops
+    assert info["parse_ms"] + info["ingest_ms"] < 60000

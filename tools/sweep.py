@@ -3,7 +3,7 @@
 For the C2 stand-in (BASELINE.json configs[1]) and each metric / hub threshold
 H, times predictLinks<Metric>Hip<H> on the GPU (graph resident, device output,
 the last of `--reps` calls) and, for a bounded set of H, the reference's own
-OpenMP code (oracle/_ref/ref_driver, all host cores up to 16) on the same CSR.
+OpenMP code (oracle/_ref/ref_driver, all host cores; OMP_NUM_THREADS caps them) on the same CSR.
 One JSON line per (metric, H) on stdout.
 
     python tools/sweep.py [--metrics JAC,CN,AA] [--hubs 0,2,4,...] [--cpu-hubs 2,4,8,16,32,64]
@@ -44,9 +44,10 @@ def main():
     out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
     drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     try:
-        cores = min(16, len(os.sched_getaffinity(0)))
+        cores = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
+        cores = os.cpu_count() or 1
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     cpu_hubs = {int(h) for h in args.cpu_hubs.split(",") if h}
     csr = None
     if cpu_hubs:  # the reference driver reads the CSR from a file
@@ -77,6 +78,7 @@ def main():
             line = {"config": args.config, "metric": metric, "H": H, "k": k, "predicted": cnt,
                     "gpu_ms": wall, "score_ms": t["score_ms"], "select_ms": t["select_ms"], "path": t["path"],
                     "chunks": t["chunks"], "wedges": t["wedges"], "candidates": t["candidates"],
+                    "hot_kernel": t.get("hot_kernel"), "hot_ms": t.get("hot_ms"), "hot_bytes": t.get("hot_bytes"),
                     "gpu_predicted_per_s": cnt / (wall / 1e3), "gpu_wedges_per_s": t["wedges"] / (wall / 1e3),
                     "n": span - 1, "M": nnz}
             ba = b_alg(H, cnt)
