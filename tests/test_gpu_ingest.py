@@ -183,5 +183,5 @@ def test_gpu_device_route_c2_size_file(gpu, tmp_path):
         with open(os.path.join(d, "c2_mtx_ingest.json"), "w") as f:
             json.dump(info, f)
     assert info["lines"] == 68993773
-    assert info["size"] > 0.9 * 2 * 68993773 * 0.95  # symmetrized, few duplicates / self loops
+    assert info["size"] > 68993773  # symmetrized (duplicate pairs and self loops removed)
     assert info["parse_ms"] + info["ingest_ms"] < 60000
