@@ -74,6 +74,7 @@ struct HpArgs {
   const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
   const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
   const uint32_t* xs;    // per row: entries of N(u) at or below u (null: none; the exclusion starts after them)
+  unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -1788,6 +1789,14 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
   fetch_bounds(b, &r0, &nr);
   u = (uint32_t)lane < nr ? rows[r0 + lane] : 0u;
   fetch_info(nr, u, &W, &s0, &ns, &o0, &du, &dx);
+  uint64_t ph_t = a.ph ? __builtin_amdgcn_s_memrealtime() : 0, ph_acc[4] = {0, 0, 0, 0};
+  auto ph_mark = [&](int i) {  // time since the last mark goes to phase i
+    if (a.ph) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      ph_acc[i] += now - ph_t;
+      ph_t = now;
+    }
+  };
   for (; b < nb;) {
     const uint32_t bn = b + stride;
     uint32_t pr0, pnr, pu = 0;
@@ -1841,6 +1850,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       wave_sync_lds();
       if (!a.ssorted) wave_bitonic_u32(s_sk[wv], n2);
     }
+    ph_mark(0);  // batch setup (row data wait, scans, AA order)
     // the batch's surviving first hops, 64 at a time; their wedges (slot, w) into the table
     for (uint32_t e0 = 0; e0 < NS; e0 += 64) {
       const uint32_t e = e0 + (uint32_t)lane;
@@ -1914,6 +1924,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
       wave_sync_lds();
     }
+    ph_mark(1);  // first hops and wedge inserts
     pu = (uint32_t)lane < pnr ? rows[pr0 + lane] : 0u;  // the next batch's rows, in flight during the exclusion
     // first-order exclusion (predict.hxx:306-307): (slot, x) for x in N(u), x > u
     // (marking from N(u) measured faster here than a membership-table line per entry)
@@ -1939,6 +1950,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
     }
     wave_sync_lds();
+    ph_mark(2);  // exclusion
     uint64_t pW, ps0, po0;
     uint32_t pns, pdu, pdx;
     fetch_info(pnr, pu, &pW, &ps0, &pns, &po0, &pdu, &pdx);  // the next batch's row data, in flight during the drain
@@ -1982,6 +1994,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
     }
     wave_sync_lds();
+    ph_mark(3);  // drain, scores, emission
     round = 0;  // every owner word of the batch is free again
     r0 = pr0;
     nr = pnr;
@@ -1995,6 +2008,8 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     b = bn;
   }
   hp_finish(sg, a, wedges);
+  if (a.ph && lane == 0)
+    for (int i = 0; i < 4; ++i) atomicAdd(&a.ph[i], (unsigned long long)ph_acc[i]);
   // + per wedge its key (and its degree for KD), per emitted candidate 16 (key, u, w, score)
   const uint64_t wsum = wave_sum(wedges);
   abytes += (KD ? 8ull : 4ull) * wsum + 16ull * sg.out + 4ull * wave_sum(drained);

@@ -2059,6 +2059,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.sdo = s_sdo;
     a.sua = ua;
     a.xs = g->xs;
+    a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
+    if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0 && g->hp_tiers) {
@@ -2153,6 +2155,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       C.hot_ms += ms;
       C.hot_bytes += g->host_small[HPC_HOTB];
       ++C.hot_launches;
+    }
+    if (g->hp_stats && batch_timed) {
+      uint64_t ph[4];
+      TRY(hipMemcpy(ph, small + 56, 32, hipMemcpyDeviceToHost));
+      const double tot = (double)(ph[0] + ph[1] + ph[2] + ph[3]) + 1e-9;
+      fprintf(stderr, "[hash-stats] k_hp_batch wave time: setup %.1f%% wedges %.1f%% exclusion %.1f%% drain %.1f%% "
+              "(%.3g wave-s)\n", 100 * ph[0] / tot, 100 * ph[1] / tot, 100 * ph[2] / tot, 100 * ph[3] / tot, tot * 1e-8);
     }
     if (g->hp_stats)
       fprintf(stderr, "[hash-stats] chunk rows [%llu, %llu) bins %llu %llu %llu %llu W %llu emitted %llu cand %llu tau %lld\n",
