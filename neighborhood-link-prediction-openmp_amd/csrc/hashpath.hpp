@@ -1707,8 +1707,8 @@ __device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t, uint
 
 // KD (count metrics, with the graph's entry degrees): deg w rides in the table
 // (hp_insert_kd<10>: a batch holds at most 512 wedges), no gather at the drain.
-template <bool CUSTOM, int TW, int STG = HP_STG, bool KD = false>
-__global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __restrict__ tl,
+template <bool CUSTOM, int TW, int STG = HP_STG, bool KD = false, int UN = HB_UN, int MW = 1>
+__global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* __restrict__ tl,
                                                  const uint32_t* __restrict__ tcnt, int tlo, int thi,
                                                  const uint32_t* __restrict__ bstart,
                                                  const uint32_t* __restrict__ nbatch, const uint64_t* __restrict__ wu,
@@ -1892,7 +1892,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       wave_sync_lds();
       const uint32_t total = __shfl(incl, 63, 64);
       if constexpr (CUSTOM) {
-        hb_wedges<HB_UN, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+        hb_wedges<UN, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                                [&](bool ok, uint32_t w, uint32_t, uint32_t ent) {
                                  const uint32_t sl = s_islot[wv][ent];
                                  const bool in = ok && w > s_u[wv][sl];
@@ -1904,7 +1904,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
                                  ho_add_wave(tb, in, h, s_ic[wv][ent], &round);
                                });
       } else if constexpr (KD) {
-        hb_wedges<HB_UN, false, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+        hb_wedges<UN, false, true>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                                       [&](uint32_t w, uint32_t, uint32_t ent, uint32_t dw) {
                                         const uint32_t sl = s_islot[wv][ent];
                                         if (w > s_u[wv][sl]) {
@@ -1913,7 +1913,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
                                         }
                                       }, a.kdeg);
       } else {
-        hb_wedges<HB_UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
+        hb_wedges<UN>(total, (uint32_t)lane, s_incl[wv], s_start[wv], s_iv[wv], a.g.keys,
                          [&](uint32_t w, uint32_t vv, uint32_t ent) {
                            const uint32_t sl = s_islot[wv][ent];
                            if (w > s_u[wv][sl]) {
@@ -1931,11 +1931,11 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     // (prefetching the first block of these keys during the wedge phase measured
     // slower: 46.6 -> 52.7 ms on C3 JAC H=16)
     const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
-    for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * HB_UN) {
-      uint32_t key[HB_UN], sl[HB_UN];
-      const uint32_t nq = min((uint32_t)HB_UN, (NNs - x0 + 63) / 64);
+    for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * UN) {
+      uint32_t key[UN], sl[UN];
+      const uint32_t nq = min((uint32_t)UN, (NNs - x0 + 63) / 64);
 #pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
+      for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         sl[q] = x < NN ? hb_slot(s_np[wv], nr, x) : 0u;
@@ -1943,7 +1943,7 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
         key[q] = x < NN ? a.g.keys[s_o0[wv][sl[q]] + (x - ex)] : 0u;
       }
 #pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
+      for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
         if (x < NN && key[q] > s_u[wv][sl[q]]) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
@@ -1958,11 +1958,11 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
     // instead of this scan measured slower: the claims cost more in the insert
     // loop than the scan of empty slots)
     const uint32_t Ts = __builtin_amdgcn_readfirstlane(T);
-    for (uint32_t i0 = 0; i0 < Ts; i0 += 64 * HB_UN) {
-      uint32_t kq[HB_UN], c[HB_UN], v0[HB_UN], v1[HB_UN], dw[HB_UN];
-      const uint32_t nq = min((uint32_t)HB_UN, (Ts - i0) / 64);  // T: a power of two >= 64
+    for (uint32_t i0 = 0; i0 < Ts; i0 += 64 * UN) {
+      uint32_t kq[UN], c[UN], v0[UN], v1[UN], dw[UN];
+      const uint32_t nq = min((uint32_t)UN, (Ts - i0) / 64);  // T: a power of two >= 64
 #pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
+      for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
         c[q] = v0[q] = v1[q] = 0;
@@ -1971,14 +1971,14 @@ __global__ __launch_bounds__(NT) void k_hp_batch(HpArgs a, const uint32_t* __res
       }
       if (!CUSTOM) {
 #pragma unroll
-        for (int q = 0; q < HB_UN; ++q) {
+        for (int q = 0; q < UN; ++q) {
           if ((uint32_t)q >= nq) break;
           const uint32_t w = kq[q] != HP_EMPTY ? (kq[q] & wmask) : 0u;
           dw[q] = KD ? hp_kd_deg<10>(a.g, c[q], w) : a.g.deg[w];
         }
       }
 #pragma unroll
-      for (int q = 0; q < HB_UN; ++q) {
+      for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const bool valid = kq[q] != HP_EMPTY;
         if (!CUSTOM && !KD) drained += valid ? 1 : 0;  // deg w gathered for it

@@ -261,12 +261,10 @@ struct nlp_graph {
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
-  bool hp_tie_select = true; // prune: the kept ties by radix select, not a sort (NLP_HASH_TIE_SORT=1 sorts)
-  bool hp_rows8 = true;      // survivor count / fill with 8 consecutive entries per lane (NLP_HASH_ROWS8=0: one per lane)
+  int hb_var = 0;            // experiment (NLP_HB_VAR): k_hp_batch KD build -- 0: 8 loads per lane, 1: 4, 2: 4 + 3 waves
+                             // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
   bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
-  bool hp_final = true;      // path 4's held candidates ordered by hp_final_order (NLP_HASH_FINAL=0: uw order + order_v1)
-  bool es_final = true;      // path 4's final order as one record sort (edgesort.hpp; NLP_ES_FINAL=0: two key sorts)
   unsigned occ_es = 256;     // resident k_es_pass workgroups
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
@@ -744,12 +742,9 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
-  if (const char* hf = getenv("NLP_HASH_FINAL")) g->hp_final = hf[0] != '0';
-  if (const char* ef = getenv("NLP_ES_FINAL")) g->es_final = ef[0] != '0';
-  if (const char* hr = getenv("NLP_HASH_ROWS8")) g->hp_rows8 = hr[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
+  if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
   if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
-  if (const char* ht = getenv("NLP_HASH_TIE_SORT")) g->hp_tie_select = ht[0] != '1';
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
     g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
@@ -1510,7 +1505,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   if (above != h[20] || quota > ties || above + quota != k) return NLP_ERR_DEVICE;
   const uint32_t* take_idx = ti0;
   const int svb = bits_for(g->span - 1);
-  if (ties > quota && quota > 0 && g->hp_tie_select && 2 * svb <= 4 * TS_BITS) {
+  if (ties > quota && quota > 0 && 2 * svb <= 4 * TS_BITS) {
     // the quota smallest ties in (u, w) order by radix select (k_ts_*), in any order
     uint32_t* th;
     uint64_t* tst;
@@ -1547,7 +1542,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
     { nlp_status so = sort_pairs_os(g, tk0, ti0, tk1, ti1, ties, shifts, np, &which, st); if (so != NLP_OK) return so; }
     take_idx = which ? ti1 : ti0;
   }
-  if (quota && !(ties > quota && g->hp_tie_select && 2 * svb <= 4 * TS_BITS))
+  if (quota && !(ties > quota && 2 * svb <= 4 * TS_BITS))
     LAUNCH(k_hp_take, quota, st, take_idx, quota, above, ckey, cu, cw, cs, nk, nu, nw, ns);
   TRY(hipGetLastError());
   std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
@@ -1558,45 +1553,8 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   return NLP_OK;
 }
 
-// Put the held candidates in (u asc, w asc) order (the order order_v1 expects).
-nlp_status hp_uw_order(nlp_graph* g, Cands& C, hipStream_t st) {
-  if (C.n <= 1) return NLP_OK;
-  Workspace& ws = g->ws;
-  const uint64_t n = C.n;
-  uint64_t *k0, *k1;
-  uint32_t *v0, *v1;
-  TRY(wsget(ws, B_SK0, n, &k0));
-  TRY(wsget(ws, B_SK1, n, &k1));
-  TRY(wsget(ws, B_SV0, n, &v0));
-  TRY(wsget(ws, B_SV1, n, &v1));
-  // keys (u << vb | w): 2 vb bits, so 7 byte passes instead of 8 at vb = 26
-  const int vb = bits_for(g->span - 1);
-  LAUNCH(k_hp_uwkeys, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], n, k0, v0, vb);
-  TRY(hipGetLastError());
-  int shifts[8], np = 0;
-  for (int b = 0; b < 2 * vb; b += 8) shifts[np++] = b;
-  int which = 0;
-  { nlp_status so = sort_pairs_os(g, k0, v0, k1, v1, n, shifts, np, &which, st); if (so != NLP_OK) return so; }
-  uint32_t *nk, *nu, *nw;
-  float* ns;
-  TRY(wsget(ws, B_TKEY, n, &nk));
-  TRY(wsget(ws, B_TU, n, &nu));
-  TRY(wsget(ws, B_TW, n, &nw));
-  TRY(wsget(ws, B_TS, n, &ns));
-  LAUNCH(k_hp_permute, n, st, which ? v1 : v0, n, (const uint32_t*)ws.p[B_CKEY], (const uint32_t*)ws.p[B_CU],
-         (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], nk, nu, nw, ns);
-  TRY(hipGetLastError());
-  std::swap(ws.p[B_CKEY], ws.p[B_TKEY]); std::swap(ws.bytes[B_CKEY], ws.bytes[B_TKEY]);
-  std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
-  std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
-  std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
-  return NLP_OK;
-}
-
 // The held candidates straight to the caller's edges in the canonical order
-// (score key desc, u asc, w asc): two sorts and one gather of 8 bytes per edge
-// (k_hp_final_edges) instead of hp_uw_order's permutation, order_v1's score
-// sort and its three-column gather.
+// (score key desc, u asc, w asc): one record sort (es_sort).
 // The canonical order of n links given as columns (u, w, score) written to
 // `out` as records: one stable LSD sort of the records by
 // (~score_key, u, w) (edgesort.hpp).  Digits that are the same for every
@@ -1661,39 +1619,9 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
 }
 
 nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
-  const uint64_t n = C.n;
-  if (n == 0) return NLP_OK;
-  if (g->es_final)
-    return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], n,
-                   d_out, st);
-  if (n > 0xffffffffull) return NLP_ERR_INVALID;
-  Workspace& ws = g->ws;
-  uint64_t *k0, *k1, *s0, *s1;
-  uint32_t *v0, *v1;
-  TRY(wsget(ws, B_SK0, n, &k0));
-  TRY(wsget(ws, B_SK1, n, &k1));
-  TRY(wsget(ws, B_SV0, n, &v0));
-  TRY(wsget(ws, B_SV1, n, &v1));
-  const int vb = bits_for(g->span - 1);
-  LAUNCH(k_hp_uwkeys2, n, st, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const uint32_t*)ws.p[B_CKEY],
-         n, k0, v0, vb);
-  TRY(hipGetLastError());
-  int shifts[8], np = 0;
-  for (int b = 0; b < 2 * vb && np < 8; b += 8) shifts[np++] = b;
-  int which = 0;
-  { nlp_status so = sort_pairs_os(g, k0, v0, k1, v1, n, shifts, np, &which, st); if (so != NLP_OK) return so; }
-  const uint64_t* uw = which ? k1 : k0;
-  const uint32_t* sv = which ? v1 : v0;
-  TRY(wsget(ws, B_HP_TIEK0, n, &s0));
-  TRY(wsget(ws, B_HP_TIEK1, n, &s1));
-  LAUNCH(k_hp_skeys, n, st, sv, n, s0);
-  TRY(hipGetLastError());
-  const int hs[4] = {32, 40, 48, 56};
-  int w2 = 0;
-  { nlp_status so = sort_pairs_os(g, s0, nullptr, s1, nullptr, n, hs, 4, &w2, st); if (so != NLP_OK) return so; }
-  LAUNCH(k_hp_final_edges, n, st, (const uint64_t*)(w2 ? s1 : s0), uw, n, vb, d_out);
-  TRY(hipGetLastError());
-  return NLP_OK;
+  if (C.n == 0) return NLP_OK;
+  return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
+                 d_out, st);
 }
 
 // Estimated wedges (w > u) of a call: sum over surviving v of deg(v)^2 / 2,
@@ -2092,6 +2020,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(hipGetLastError());
         TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
         if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 1) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 1>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 2) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 3) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 8, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 4) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 2, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());
@@ -2210,9 +2142,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     if (!full && target > free_slots) target = free_slots;  // no threshold yet: emissions <= W(u)
     if (target == 0) target = 1;
   }
-  // held candidates are unordered: the caller orders them (hp_final_order,
-  // or hp_uw_order + order_v1 with NLP_HASH_FINAL=0)
-  if (!g->hp_final) return hp_uw_order(g, C, st);
+  // held candidates are unordered: the caller orders them (hp_final_order)
   return NLP_OK;
 }
 
@@ -3467,7 +3397,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   nlp_status s = prune_to(g, C, p.max_edges, st);
   if (s != NLP_OK) return s;
   if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.n, 1), &d_out));
-  s = path == 4 && g->hp_final ? hp_final_order(g, C, d_out, st) : order_v1(g, C, d_out, st);
+  s = path == 4 ? hp_final_order(g, C, d_out, st) : order_v1(g, C, d_out, st);
   if (s != NLP_OK) return s;
   TRY(hipEventRecord(g->ev[2], st));
   TRY(hipEventSynchronize(g->ev[2]));

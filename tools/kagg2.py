@@ -7,7 +7,7 @@ import os
 import sys
 
 GRAPH = ("k_in_", "k_del_", "k_degrees", "k_check_keys", "k_count_cols", "k_transpose_keys", "k_etab_build", "k_edge_filter",
-         "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_diff_", "k_low32", "k_sum_deg2", "k_hp_dcls(", "k_hp_drank", "k_etab_build")
+         "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_hp_xs", "k_diff_", "k_low32", "k_sum_deg2", "k_hp_dcls(", "k_hp_drank", "k_etab_build")
 path = sys.argv[1]
 if os.path.isdir(path):
     path = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)[0]

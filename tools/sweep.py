@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--cpu-hubs", default="2,4,8,16,32,64")
     ap.add_argument("--cpu-metrics", default="JAC")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--envs", default="",
+                    help="';'-separated environment settings (A=1,B=2), one graph handle each (the library reads "
+                         "its switches when a handle is created); '' = the current environment")
     args = ap.parse_args()
     nlp = nlp_loader.load()
     gg = nlp_loader.load_sub("graphgen")
@@ -40,7 +43,6 @@ def main():
     torch.cuda.empty_cache()  # hand the generator's cached blocks back: libnlp allocates with hipMalloc
     torch.cuda.synchronize()
     k = info["k"]
-    G = nlp.Graph.from_device(off, keys)
     out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
     drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     try:
@@ -67,6 +69,21 @@ def main():
         sv = degs[(degs > 0) & ((degs <= H) if H > 0 else (degs > 0))]
         return 8 * (span + 1) + 8 * nnz + 8 * float(sv.sum()) + 4 * float((sv * sv).sum()) + 12 * kout
     cpu_metrics = set(args.cpu_metrics.split(","))
+    for envspec in args.envs.split(";"):
+        env = dict(kv.split("=", 1) for kv in envspec.split(",") if "=" in kv)
+        saved = {kk: os.environ.get(kk) for kk in env}
+        os.environ.update(env)
+        G = nlp.Graph.from_device(off, keys)
+        for kk, vv in saved.items():  # the handle has read its switches
+            if vv is None:
+                os.environ.pop(kk, None)
+            else:
+                os.environ[kk] = vv
+        run_sweep(args, nlp, G, out, k, span, nnz, b_alg, csr, cpu_hubs, cpu_metrics, drv, cores, envspec)
+        G.close()
+
+
+def run_sweep(args, nlp, G, out, k, span, nnz, b_alg, csr, cpu_hubs, cpu_metrics, drv, cores, envspec):
     for metric in args.metrics.split(","):
         mid = nlp.METRICS.index(metric)
         for H in (int(h) for h in args.hubs.split(",")):
@@ -75,7 +92,7 @@ def main():
                 cnt, t = G.predict_device(mid, H, k, out)
                 torch.cuda.synchronize()
                 wall = (time.perf_counter() - t0) * 1e3
-            line = {"config": args.config, "metric": metric, "H": H, "k": k, "predicted": cnt,
+            line = {"config": args.config, "env": envspec, "metric": metric, "H": H, "k": k, "predicted": cnt,
                     "gpu_ms": wall, "score_ms": t["score_ms"], "select_ms": t["select_ms"], "path": t["path"],
                     "chunks": t["chunks"], "wedges": t["wedges"], "candidates": t["candidates"],
                     "hot_kernel": t.get("hot_kernel"), "hot_ms": t.get("hot_ms"), "hot_bytes": t.get("hot_bytes"),
@@ -93,7 +110,6 @@ def main():
                     line.update(cpu_ms=float(t_ms), cpu_cores=cores, cpu_kind="reference",
                                 speedup=float(t_ms) / wall)
             print(json.dumps(line), flush=True)
-    G.close()
 
 
 if __name__ == "__main__":
