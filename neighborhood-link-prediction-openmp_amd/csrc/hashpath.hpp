@@ -700,7 +700,7 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
 // survivor lists S(u) = {v in N(u): 1 <= deg v <= H} of a range are the stream
 // compaction of its entries by dcls -- coalesced bytes, no atomics, and S(u)
 // keeps N(u)'s ascending order (the AA / RA row kernels then need no sort).
-//   k_hp_dcls_rows: per row (cnt << 40 | W) packed into wu, per tile its count
+//   k_hp_dcls_rows8: per row (cnt << 40 | W) packed into wu, per tile its count
 //   k_hp_unpack:    wu -> W(u), cnt -> |S(u)| (scanned into soff by the caller)
 //   k_hp_dcls_fill: per tile, the surviving keys at the scanned tile offsets
 // (deg u < 2^24 is required at graph build, so the packed count cannot carry
@@ -718,67 +718,6 @@ __global__ void k_hp_dcls(const uint32_t* __restrict__ keys, const uint32_t* __r
 }
 
 __device__ __forceinline__ bool hp_dsurv(uint32_t c, uint32_t H) { return c >= 1 && c <= H; }
-
-__global__ __launch_bounds__(NT) void k_hp_dcls_rows(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
-                                                     uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
-                                                     const uint32_t* __restrict__ tile_row,
-                                                     unsigned long long* __restrict__ wu, uint32_t* __restrict__ tcnt) {
-  __shared__ unsigned long long s_acc[NWAVE][64];
-  const int lane = lane_id(), wv = wave_id();
-  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
-  s_acc[wv][lane] = 0;
-  for (uint64_t tile = t0 + (uint64_t)blockIdx.x * NWAVE + wv; tile < t1; tile += (uint64_t)gridDim.x * NWAVE) {
-    const uint64_t base = tile * HP_WTILE;
-    const uint64_t tr = tile_row[tile];
-    const uint64_t r0 = tr > ua ? tr - ua : 0;  // first row of the tile inside the range
-    const uint64_t rl = r0 + lane;
-    const uint64_t rend = rl < nU ? g.off[ua + rl + 1] : ~0ull;  // end of row r0 + lane
-    const uint64_t last_end = __shfl(rend, 63, 64);
-    uint32_t c[HP_WR];
-#pragma unroll
-    for (int i = 0; i < HP_WR; ++i) {
-      const uint64_t e = base + (uint64_t)i * 64 + lane;
-      c[i] = e >= e0 && e < e1 ? (uint32_t)dcls[e] : 0u;
-      c[i] = hp_dsurv(c[i], H) ? c[i] : 0u;
-    }
-    uint32_t tc = 0;
-#pragma unroll
-    for (int i = 0; i < HP_WR; ++i) {
-      const uint64_t e = base + (uint64_t)i * 64 + lane;
-      tc += (uint32_t)__popcll(__ballot(c[i] != 0));
-      int lo = 0, hi = 64;  // local row: the number of the 64 row ends <= e
-      while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        const uint64_t v = __shfl(rend, m, 64);
-        if (v <= e) lo = m + 1; else hi = m;
-      }
-      if (c[i] == 0) continue;
-      const unsigned long long add = (1ull << 40) | c[i];
-      if (e < last_end) {
-        atomicAdd(&s_acc[wv][lo], add);
-      } else {  // more than 64 rows in this tile: search the offsets
-        uint64_t a = r0, b = nU;
-        while (b - a > 1) {
-          const uint64_t m = (a + b) >> 1;
-          if (g.off[ua + m] <= e) a = m; else b = m;
-        }
-        atomicAdd(&wu[a], add);
-      }
-    }
-    if (lane == 0) tcnt[tile - t0] = tc;
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    const unsigned long long v = s_acc[wv][lane];
-    if (v) {
-      atomicAdd(&wu[rl], v);
-      s_acc[wv][lane] = 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-  }
-}
 
 // The same per-row (count, W) and tile counts with eight consecutive entries
 // per lane (one 8-byte load of classes): a lane finds the row of its first
@@ -3194,63 +3133,8 @@ __global__ void k_hp_take(const uint32_t* __restrict__ idx, uint64_t take, uint6
   }
 }
 
-// (u << 32 | w) + identity index, for the canonical (u, w) order before the final sort
-__global__ void k_hp_uwkeys(const uint32_t* __restrict__ u, const uint32_t* __restrict__ w, uint64_t n,
-                            uint64_t* __restrict__ k, uint32_t* __restrict__ idx, int vb) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    k[i] = ((uint64_t)u[i] << vb) | w[i];
-    idx[i] = (uint32_t)i;
-  }
-}
-
-// Final order of path 4 (hp_final_order): (u << vb | w) keys with the score
-// key as value, sorted; then 64-bit keys (~score key << 32 | uw position),
-// sorted on their high half (stable: equal scores keep (u, w) order) -- the
-// output's (u, w) come from the uw position, the score from the key (NaN keys
-// are 0: a NaN of some payload comes back, compared by NaN-ness).
-__global__ void k_hp_uwkeys2(const uint32_t* __restrict__ u, const uint32_t* __restrict__ w,
-                             const uint32_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ k,
-                             uint32_t* __restrict__ val, int vb) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    k[i] = ((uint64_t)u[i] << vb) | w[i];
-    val[i] = key[i];
-  }
-}
-
-__global__ void k_hp_skeys(const uint32_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ k) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    k[i] = ((uint64_t)(~key[i]) << 32) | i;
-}
-
 __device__ __forceinline__ float score_of_key(uint32_t key) {
   return __uint_as_float((key & 0x80000000u) ? (key & 0x7fffffffu) : ~key);
-}
-
-__global__ void k_hp_final_edges(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ uw, uint64_t n,
-                                 int vb, EdgeOut* __restrict__ out) {
-  const uint64_t wm = (1ull << vb) - 1;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t x = sk[i];
-    const uint64_t y = uw[x & 0xffffffffull];
-    EdgeOut o;
-    o.u = (uint32_t)(y >> vb);
-    o.v = (uint32_t)(y & wm);
-    o.score = score_of_key(~(uint32_t)(x >> 32));
-    out[i] = o;
-  }
-}
-
-__global__ void k_hp_permute(const uint32_t* __restrict__ idx, uint64_t n, const uint32_t* __restrict__ key,
-                             const uint32_t* __restrict__ u, const uint32_t* __restrict__ w,
-                             const float* __restrict__ s, uint32_t* __restrict__ okey, uint32_t* __restrict__ ou,
-                             uint32_t* __restrict__ ow, float* __restrict__ os) {
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t i = idx[j];
-    okey[j] = key[i];
-    ou[j] = u[i];
-    ow[j] = w[i];
-    os[j] = s[i];
-  }
 }
 
 

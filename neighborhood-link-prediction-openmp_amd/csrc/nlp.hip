@@ -63,7 +63,6 @@ enum Buf {
   B_TKEY, B_TU, B_TW, B_TS,           // compaction target
   B_TIE, B_TRANK, B_KEEP, B_KPOS,
   B_SK0, B_SK1, B_SV0, B_SV1,         // final sort
-  B_OSORT,                            // sort_pairs_os: n, ticket, error, digit histograms, descriptors
   B_HIST, B_HOFF, B_SCAN, B_SCAN2, B_SELHIST, B_SEL, B_CNT, B_EDGES,
   // v1 pipeline
   B_ARENA, B_ARENA2, B_VLIST, B_VIOFF, B_UCNT, B_UOFF, B_IEU, B_IEV, B_IEF, B_IEP, B_BUCKET,
@@ -277,7 +276,6 @@ struct nlp_graph {
   bool hp_batch = true;      // path 4: bin-0 tiers 0 / 1 in row batches (k_hp_batch; NLP_HASH_BATCH=0: a wave per row)
   // (u64, u32) sorts of paths 2 / 4 by onesweep passes (NLP_OS_SORT=1); the default hist / scan / scatter
   // passes measured faster at these sizes (C4 JAC H=16 ordering: 22 vs 77 ms; C3 AA H=16 path 2: 122 vs 418 ms)
-  bool os_sort = false;
   bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   bool hp_dcls = true;       // survivor lists by filtering N(u) with the degree classes (NLP_HASH_DCLS=0: in-edge atomics)
@@ -734,7 +732,6 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
   if (const char* hd = getenv("NLP_HASH_DCLS")) g->hp_dcls = hd[0] != '0';
   if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
-  if (const char* os = getenv("NLP_OS_SORT")) g->os_sort = os[0] == '1';
   if (const char* hb = getenv("NLP_HASH_BATCH")) g->hp_batch = hb[0] != '0';
   if (const char* hh = getenv("NLP_HASH_HUB")) g->hp_hub = hh[0] != '0';
   if (const char* hm = getenv("NLP_HASH_HUB_MIN")) g->hp_hub_min = std::max(1, std::min(2, atoi(hm)));
@@ -843,62 +840,22 @@ struct Cands {
 __global__ void k_set_u64(uint64_t* p, uint64_t v) { *p = v; }
 
 // Stable LSD sort of (u64 key, u32 value) pairs (values may be null) by the
-// 8-bit digits at `shifts` (multiples of 8, least significant first), with the
-// onesweep pass of the sort path (sortpath.hpp k_sp_pass<u64>): one read builds
-// every digit histogram, then one kernel per digit -- no per-pass histogram
-// and scan launches, and a pass writes each key once.  Descriptors of two
-// alternate buffers clean themselves (each pass zeroes the previous pass's).
-// Beyond SP_MAX_N (30-bit descriptor counts) or without NLP_OS_SORT=1: the
-// hist / scan / scatter passes of prims.hpp.
+// 8-bit digits at `shifts` (multiples of 8, least significant first): the
+// hist / scan / scatter passes of prims.hpp (a onesweep variant measured
+// slower here and was removed in round 4).
 nlp_status sort_pairs_os(nlp_graph* g, uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint64_t n,
                          const int* shifts, int np, int* which, hipStream_t st) {
   *which = 0;
   if (n <= 1 || np == 0) return NLP_OK;
   Workspace& ws = g->ws;
-  if (n > SP_MAX_N || !g->os_sort) {
-    uint64_t *hoff, *scan;
-    uint32_t* hist;
-    const uint64_t nb = rs_blocks(n);
-    TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
-    TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
-    TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(n, RS_BINS * nb)) + 16, &scan));
-    SortScratch sc{hist, hoff, scan, nb};
-    TRY(sort_pairs_u64(k0, v0, k1, v1, n, shifts, np, sc, which, st));
-    return NLP_OK;
-  }
-  const uint64_t ntiles = (n + OS2_TILE - 1) / OS2_TILE;
-  const uint64_t hwords = (uint64_t)HCOPIES * HSTRIDE / 2, dwords = ntiles * RS_BINS / 2;  // u64 words
-  uint64_t* b;
-  TRY(wsget(ws, B_OSORT, 8 + hwords + 2 * dwords, &b));
-  TRY(hipMemsetAsync(b, 0, (8 + hwords + 2 * dwords) * 8, st));
-  uint64_t* d_n = b;
-  uint32_t* tick = (uint32_t*)(b + 1);  // 8 tickets
-  uint32_t* err = (uint32_t*)(b + 5);
-  uint32_t* ghist = (uint32_t*)(b + 8);
-  uint32_t* desc[2] = {(uint32_t*)(b + 8 + hwords), (uint32_t*)(b + 8 + hwords + dwords)};
-  hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, st, d_n, n);
-  hipLaunchKernelGGL(k_sp_hist<uint64_t>, dim3(256), dim3(NT), 0, st, (const uint64_t*)k0, (const uint64_t*)d_n, n, 0, 8,
-                     ghist, (uint64_t*)nullptr, (uint64_t*)nullptr);
-  TRY(hipGetLastError());
-  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_p64));
-  uint64_t* ka = k0;
-  uint64_t* kb = k1;
-  uint32_t* va = v0;
-  uint32_t* vb = v1;
-  for (int p = 0; p < np && p < 8; ++p) {
-    hipLaunchKernelGGL((k_sp_pass<uint64_t, OS2_IPT>), dim3(gr), dim3(OS_NT), 0, st, (const uint64_t*)ka,
-                       (const uint32_t*)va, kb, vb, (const uint64_t*)d_n, shifts[p],
-                       (const uint32_t*)(ghist + (shifts[p] / 8) * RS_BINS), desc[p & 1], tick + p, err,
-                       (uint64_t*)nullptr, GatherOut{}, (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint64_t*)nullptr,
-                       (const uint64_t*)nullptr, 0u, 0, (uint64_t*)nullptr, p ? desc[(p - 1) & 1] : (uint32_t*)nullptr);
-    TRY(hipGetLastError());
-    std::swap(ka, kb);
-    std::swap(va, vb);
-    *which ^= 1;
-  }
-  TRY(hipMemcpyAsync(&g->host_small[60], err, 4, hipMemcpyDeviceToHost, st));
-  TRY(hipStreamSynchronize(st));
-  if (g->host_small[60] & 0xffffffffull) return NLP_ERR_DEVICE;  // a look-back gave up (never expected)
+  uint64_t *hoff, *scan;
+  uint32_t* hist;
+  const uint64_t nb = rs_blocks(n);
+  TRY(wsget(ws, B_HIST, RS_BINS * nb, &hist));
+  TRY(wsget(ws, B_HOFF, RS_BINS * nb, &hoff));
+  TRY(wsget(ws, B_SCAN2, scan_scratch_words(std::max<uint64_t>(n, RS_BINS * nb)) + 16, &scan));
+  SortScratch sc{hist, hoff, scan, nb};
+  TRY(sort_pairs_u64(k0, v0, k1, v1, n, shifts, np, sc, which, st));
   return NLP_OK;
 }
 
@@ -1836,12 +1793,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(wsget(ws, B_HP_TCNT, nt, &tcn));
       TRY(wsget(ws, B_HP_TPRE, nt + 1, &tpre));
       const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
-      if (g->hp_rows8)
-        hipLaunchKernelGGL(k_hp_dcls_rows8, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0,
-                           e1, (const uint32_t*)g->tile_row, (unsigned long long*)wu, tcn);
-      else
-        hipLaunchKernelGGL(k_hp_dcls_rows, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
-                           (const uint32_t*)g->tile_row, (unsigned long long*)wu, tcn);
+      hipLaunchKernelGGL(k_hp_dcls_rows8, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                         (const uint32_t*)g->tile_row, (unsigned long long*)wu, tcn);
       TRY(hipGetLastError());
       LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
       TRY(hipGetLastError());
@@ -1855,7 +1808,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(g->host_small[10], 1), &s_sdo));
         TRY(hipMemsetAsync(wu, 0, nU * 8, st));  // W+(u), accumulated by the fill
       }
-      if (g->hp_rows8 && s_sdo && g->drank)
+      if (s_sdo && g->drank)
         hipLaunchKernelGGL(k_hp_dcls_fill8, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0,
                            e1, (const uint32_t*)g->tile_row, (const uint64_t*)tpre, s_skeys, s_sdo,
                            (unsigned long long*)wu, (const uint8_t*)g->drank);

@@ -409,27 +409,25 @@ class _env:
 
 
 # path 4 (hash accumulation) with every kernel forced: 0 default (bin-0 row
-# batches, hub pass), 1 workgroup/LDS, 2 hub pass for every row, 3 k_hp_part
-# over a tiny scratch (bucket groups and direct accumulation), 4 k_hp_part with one bucket per row (sub-range passes), 5 bin
-# 0 as one 1024-entry launch (no table-size tiers), 6/7 k_hp_part rows sliced
-# over several workgroups (bucket slices, exclusion cursor per slice), 8 the
-# edge-parallel work estimate, 9 a wave per bin-0 row, 10 k_hp_part for every row,
-# 11 hub pass with one w-bucket per row, 12 the same with 128-entry item
-# tables (heavy buckets split into w-range items by their fine histogram),
-# 13 the ordering sorts by onesweep passes instead of hist / scan / scatter,
-# 14 bin-1 rows by the hub pass, 15 the hub pass's AA / RA items by the ordered
-# re-walk instead of sort mode, 16/17 sort-mode items of at most 16 / 40 wedges
-# (heavy buckets split, single fine ranges beyond flagged HH_BIG), 18 survivor
-# lists from in-edge atomics (unordered: the AA / RA row kernels sort them), 19
-# no entry-degree tables (deg w gathered at the drain), 20 = 18 with bin-1 rows,
-# 21 the held candidates ordered by (u, w) permutation + order_v1 (before hp_final_order),
-# 22 row batches gathering deg / off of every first hop (no packed survivor entries),
-# 23 the prune's kept ties by a full (u, w) sort instead of the radix select,
-# 24 survivor suffixes searched per call (no per-graph rank bytes), 25 survivor
-# counts and fill with one entry per lane (k_hp_dcls_rows / _fill instead of the *8 kernels),
-# 26 survivor counts and fill as two kernels (not k_hp_dcls_one), 27 k_hp_dcls_one's output
-# capacity overflowing (the two-kernel fallback), 28 the final order as two key sorts + gather
-# (not edgesort.hpp), 29 the exclusion walking all of N(u) (no per-row start above u)
+# batches, hub pass, one-pass survivor lists, record-sort final order), 1
+# workgroup/LDS, 2 hub pass for every row, 3 k_hp_part over a tiny scratch
+# (bucket groups and direct accumulation), 4 k_hp_part with one bucket per row
+# (sub-range passes), 5 bin 0 as one 1024-entry launch (no table-size tiers),
+# 6/7 k_hp_part rows sliced over several workgroups (bucket slices, exclusion
+# cursor per slice), 8 the edge-parallel work estimate, 9 a wave per bin-0 row,
+# 10 k_hp_part for every row, 11 hub pass with one w-bucket per row, 12 the
+# same with 128-entry item tables (heavy buckets split into w-range items by
+# their fine histogram), 13 bin-1 rows by the hub pass, 14 the hub pass's AA /
+# RA items by the ordered re-walk instead of sort mode, 15/16 sort-mode items
+# of at most 16 / 40 wedges (heavy buckets split, single fine ranges beyond
+# flagged HH_BIG), 17 survivor lists from in-edge atomics (unordered: the AA /
+# RA row kernels sort them), 18 no entry-degree tables (deg w gathered at the
+# drain), 19 = 17 with bin-1 rows, 20 row batches gathering deg / off of every
+# first hop (no packed survivor entries), 21 survivor suffixes searched per call
+# (no per-graph rank bytes), 22 survivor counts and fill as two kernels (not
+# k_hp_dcls_one), 23 k_hp_dcls_one's output capacity overflowing (the
+# two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
+# above u), 25 the row batches' 4-loads / 3-waves build
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -437,15 +435,14 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7"), dict(NLP_OS_SORT="1"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SORT="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
-                 dict(NLP_HASH_FINAL="0"), dict(NLP_HASH_SDO="0"), dict(NLP_HASH_TIE_SORT="1"),
-                 dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ROWS8="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_ES_FINAL="0"), dict(NLP_HASH_XS="0")]
+                 dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
+                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
