@@ -75,6 +75,8 @@ struct HpArgs {
   const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
   const uint32_t* xs;    // per row: entries of N(u) at or below u (null: none; the exclusion starts after them)
   unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
+  int xp;                  // experiment (NLP_HB_XP, wrong results): 1 skip k_hp_batch's exclusion, 2 its emission,
+                           // 4 its wedge inserts
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -1848,7 +1850,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
                                         const uint32_t sl = s_islot[wv][ent];
                                         if (w > s_u[wv][sl]) {
                                           ++wedges;
-                                          hp_insert_kd<10>(tb, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
+                                          if (!(a.xp & 4)) hp_insert_kd<10>(tb, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
                                         }
                                       }, a.kdeg);
       } else {
@@ -1869,7 +1871,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     // (marking from N(u) measured faster here than a membership-table line per entry)
     // (prefetching the first block of these keys during the wedge phase measured
     // slower: 46.6 -> 52.7 ms on C3 JAC H=16)
-    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
+    const uint32_t NNs = (a.xp & 1) ? 0u : __builtin_amdgcn_readfirstlane(NN);
     for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * UN) {
       uint32_t key[UN], sl[UN];
       const uint32_t nq = min((uint32_t)UN, (NNs - x0 + 63) / 64);
@@ -1929,7 +1931,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
           if (CUSTOM) s = ho_score(c[q]);
           else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & (KD ? 1023u : HP_CMASK)), du2, (uint64_t)dw[q]);
         }
-        hp_emit(sg, a, valid, s, uu, w, tau);
+        hp_emit(sg, a, valid && !(a.xp & 2), s, uu, w, tau);
       }
     }
     wave_sync_lds();

@@ -262,6 +262,7 @@ struct nlp_graph {
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
   int hb_var = 0;            // experiment (NLP_HB_VAR): k_hp_batch KD build -- 0: 8 loads per lane, 1: 4, 2: 4 + 3 waves
                              // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
+  int hb_xp = 0;             // experiment (NLP_HB_XP): k_hp_batch phases skipped (wrong results; timing only)
   bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
@@ -741,6 +742,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
   if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
+  if (const char* hx = getenv("NLP_HB_XP")) g->hb_xp = atoi(hx);
   if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
@@ -1940,6 +1942,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.sdo = s_sdo;
     a.sua = ua;
     a.xs = g->xs;
+    a.xp = g->hb_xp;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
     if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
