@@ -2443,14 +2443,21 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
 // spreads both halves of the work over the chip:
 //   k_hh_rows     per hub row: its w-bucket width (about HH_BW of W(u) per
 //                 bucket, at most HH_PMAX buckets) and its enumeration items
-//                 (HH_EC first hops each);
-//   k_hh_maps     bucket -> row, item -> row, and every bucket's first entry of
-//                 N(u) (the exclusion slice, one binary search per bucket);
-//   k_hh_enum     one workgroup per item: its wedges counted per bucket in LDS
-//                 and added to the global bucket counts (COUNT); then, after a
-//                 scan, counted again, reserved with one atomic per used bucket
-//                 and written to the bucket's contiguous scratch (SCATTER: w,
-//                 and v for AA / RA);
+//                 (HH_WC wedges of the row's flattened first-hop lists each: a
+//                 row of an IHub call may hold a few first hops with millions
+//                 of wedges -- items by first hops left one workgroup per row);
+//   k_hh_fpre     per hub row the inclusive prefix of its first hops' lengths
+//                 (an item finds its first first hop by binary search);
+//   k_hh_maps     bucket -> row, and every bucket's first entry of N(u) (the
+//                 exclusion slice, one binary search per bucket);
+//   k_hh_enum     one workgroup per item (its row by binary search of the item
+//                 prefix): its wedges counted per bucket in LDS and added to the
+//                 global bucket counts (COUNT); then, after a scan, counted
+//                 again, reserved with one atomic per used bucket and written to
+//                 the bucket's contiguous scratch (SCATTER: w, and v for AA /
+//                 RA).  Consecutive lanes take consecutive entries of a sorted
+//                 list N(v), so equal buckets come in runs: one LDS atomic per
+//                 run of a wave (its head lane), not per wedge;
 //   k_hh_accum    one workgroup per bucket (work queue): its wedges into an
 //                 LDS table, the exclusion slice of N(u) marked, every entry
 //                 scored and emitted -- buckets of different rows in parallel.
@@ -2459,7 +2466,7 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
 // the host keeps k_hp_part for that chunk.
 constexpr uint64_t HH_BW = 1024;    // W(u) per w-bucket (W counts every w, so buckets hold at most about this)
 constexpr uint32_t HH_PMAX = 8192;  // buckets per row at most
-constexpr uint64_t HH_EC = 4096;    // first hops per enumeration item
+constexpr uint64_t HH_WC = 16384;   // wedges (every w of the row's flattened lists) per enumeration item
 constexpr int HH_NT = 256;          // threads of the enumeration and accumulation workgroups
 constexpr int HH_NW = HH_NT / 64;
 constexpr int HH_TL = 13;           // accumulation table: 2^13 LDS entries (2^12 for AA / RA)
@@ -2471,29 +2478,30 @@ __device__ __forceinline__ uint32_t hh_row_u(const uint32_t* l2, uint64_t n2, co
 __global__ void k_hh_rows(HpArgs a, const uint32_t* __restrict__ l2, uint64_t n2, const uint32_t* __restrict__ l3,
                           uint64_t n3, const uint64_t* __restrict__ wu, uint64_t ua, uint32_t* __restrict__ hr_u,
                           uint32_t* __restrict__ hr_shift, uint32_t* __restrict__ hr_p, uint32_t* __restrict__ hr_items,
-                          uint64_t bw = HH_BW) {
+                          uint64_t* __restrict__ hr_nf, uint64_t bw = HH_BW) {
   const uint64_t nh = n2 + n3;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t u = hh_row_u(l2, n2, l3, r);
     const uint64_t W = wu[u - ua];
     const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
     uint32_t P = 0, shift = 0, items = 0;
+    uint64_t nf = 0;
     if (span_w > 0) {
       uint64_t pd = (W + bw - 1) / bw;
       if (pd < 1) pd = 1;
       if (pd > HH_PMAX) pd = HH_PMAX;
       shift = (uint32_t)log2_ceil((span_w + pd - 1) / pd);
       P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
-      uint64_t nf;
       if (a.soff) nf = a.soff[u - a.sua + 1] - a.soff[u - a.sua];
       else nf = a.g.off[u + 1] - a.g.off[u];
-      items = (uint32_t)((nf + HH_EC - 1) / HH_EC);
-      if (items == 0) P = 0;  // no first hop: no wedge, no candidate
+      items = nf ? (uint32_t)std::min<uint64_t>((W + HH_WC - 1) / HH_WC, 0x7fffffffull) : 0u;
+      if (items == 0) P = 0;  // no first hop or no wedge: no candidate
     }
     hr_u[r] = u;
     hr_shift[r] = shift;
     hr_p[r] = P;
     hr_items[r] = items;
+    hr_nf[r] = items ? nf : 0;
   }
 }
 
@@ -2506,7 +2514,7 @@ __global__ void k_hh_maps(HpArgs a, uint64_t nh, const uint32_t* __restrict__ hr
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t b0 = bbase[r], i0 = ibase[r];
     for (uint32_t b = 0; b < hr_p[r]; ++b) brow[b0 + b] = (uint32_t)r;
-    for (uint32_t i = 0; i < hr_items[r]; ++i) irow[i0 + i] = (uint32_t)r;
+    (void)i0;
   }
 }
 
@@ -2524,32 +2532,84 @@ __global__ void k_hh_xstart(HpArgs a, uint64_t nb, const uint32_t* __restrict__ 
   }
 }
 
-// The wedges (w > u) of item `item`'s first hops: f(w, v) on every thread of the workgroup.
-template <typename F>
-__device__ __forceinline__ void hh_enum_item(const HpArgs& a, uint32_t u, uint64_t f0, uint64_t f1, uint64_t* s_incl,
-                                             uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w, uint64_t* s_tot, F f) {
-  const int t = threadIdx.x;
+// The row's first hops and the lengths of their lists in the flattened wedge
+// space: S(u) with the packed entries (the part of N(v) above u), else the
+// first hops with their whole lists when they survive the hub filter.
+struct HhHops {
   const uint32_t* fh;
+  const uint64_t* fd;
   uint64_t nf;
-  hp_first_hops(a, u, a.g.off[u], a.g.off[u + 1] - a.g.off[u], &fh, &nf);
-  const uint64_t* fd = a.sdo && a.soff ? a.sdo + (fh - a.skeys) : nullptr;  // packed: N(v) above u
-  if (f1 > nf) f1 = nf;
-  for (uint64_t base = f0; base < f1; base += HH_NT) {
-    const uint64_t i = base + t;
+};
+__device__ __forceinline__ HhHops hh_hops(const HpArgs& a, uint32_t u) {
+  HhHops h;
+  hp_first_hops(a, u, a.g.off[u], a.g.off[u + 1] - a.g.off[u], &h.fh, &h.nf);
+  h.fd = a.sdo && a.soff ? a.sdo + (h.fh - a.skeys) : nullptr;
+  return h;
+}
+__device__ __forceinline__ void hh_hop(const HpArgs& a, const HhHops& h, uint64_t i, uint32_t* v, uint64_t* st,
+                                       uint64_t* len) {
+  *v = h.fh[i];
+  if (h.fd) {
+    const uint64_t x = h.fd[i];
+    *len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+    *st = x & ((1ull << HP_SDO_SH) - 1);
+  } else {
+    const uint32_t d = a.g.deg[*v];
+    *len = hp_surv(d, a.H) ? d : 0;
+    *st = *len ? a.g.off[*v] : 0;
+  }
+}
+
+// fp[fbase[r] + i] = the inclusive prefix of the list lengths of row r's first hops (one workgroup per row)
+__global__ __launch_bounds__(HH_NT) void k_hh_fpre(HpArgs a, uint64_t nh, const uint32_t* __restrict__ hr_u,
+                                                   const uint64_t* __restrict__ hr_nf, const uint64_t* __restrict__ fbase,
+                                                   uint64_t* __restrict__ fp) {
+  __shared__ uint64_t s_w[HH_NW];
+  __shared__ uint64_t s_tot;
+  const int t = threadIdx.x;
+  for (uint64_t r = blockIdx.x; r < nh; r += gridDim.x) {
+    const uint64_t nf = hr_nf[r];
+    if (nf == 0) continue;  // uniform
+    const HhHops h = hh_hops(a, hr_u[r]);
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < nf; b0 += HH_NT) {
+      const uint64_t i = b0 + t;
+      uint32_t v;
+      uint64_t st, len = 0;
+      if (i < nf) hh_hop(a, h, i, &v, &st, &len);
+      const uint64_t incl = block_incl_scan_1024(len, s_w);
+      if (i < nf) fp[fbase[r] + i] = carry + incl;
+      if (t == HH_NT - 1) s_tot = incl;
+      __syncthreads();
+      carry += s_tot;
+      __syncthreads();
+    }
+  }
+}
+
+// The wedges (w > u) of item `item`: flattened positions [j0, j1) of the row's
+// lists; f(b, w, v) on every thread of the workgroup (wave-convergent), b = the
+// wedge's bucket or HH_NOB (no wedge on this lane).
+constexpr uint32_t HH_NOB = 0xffffffffu;
+constexpr int HH_UN = 4;
+template <typename F>
+__device__ __forceinline__ void hh_enum_range(const HpArgs& a, uint32_t u, uint32_t shift, const HhHops& h,
+                                              const uint64_t* fpr, uint64_t f, uint64_t j0, uint64_t j1,
+                                              uint64_t* s_incl, uint64_t* s_start, uint32_t* s_iv, uint64_t* s_w,
+                                              uint64_t* s_tot, F fn) {
+  const int t = threadIdx.x;
+  for (uint64_t g0 = f; g0 < h.nf; g0 += HH_NT) {
+    const uint64_t i = g0 + t;
     uint32_t v = 0;
-    uint64_t len = 0, st = 0;
-    if (i < f1) {
-      v = fh[i];
-      if (fd) {
-        const uint64_t x = fd[i];
-        len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
-        st = x & ((1ull << HP_SDO_SH) - 1);
-      } else {
-        const uint32_t d = a.g.deg[v];
-        if (hp_surv(d, a.H)) {
-          len = d;
-          st = a.g.off[v];
-        }
+    uint64_t st = 0, len = 0;
+    if (i < h.nf) {
+      const uint64_t e = fpr[i], s0 = i ? fpr[i - 1] : 0ull;
+      const uint64_t lo = s0 > j0 ? s0 : j0, hi = e < j1 ? e : j1;
+      if (hi > lo) {
+        uint64_t full;
+        hh_hop(a, h, i, &v, &st, &full);
+        st += lo - s0;
+        len = hi - lo;
       }
     }
     const uint64_t incl = block_incl_scan_1024(len, s_w);
@@ -2559,52 +2619,118 @@ __device__ __forceinline__ void hh_enum_item(const HpArgs& a, uint32_t u, uint64
     if (t == HH_NT - 1) *s_tot = incl;
     __syncthreads();
     const uint64_t total = *s_tot;
-    hp_wedges<HH_NT>(total, (uint32_t)t, (uint32_t)HH_NT, s_incl, s_start, s_iv, a.g.keys, [&](uint32_t w, uint32_t vv) {
-      if (w > u) f(w, vv);
-    });
+    for (uint64_t jb = 0; jb < total; jb += (uint64_t)HH_NT * HH_UN) {
+      uint32_t w[HH_UN], vv[HH_UN];
+      bool ok[HH_UN];
+#pragma unroll
+      for (int q = 0; q < HH_UN; ++q) {
+        const uint64_t j = jb + (uint64_t)q * HH_NT + t;
+        ok[q] = j < total;
+        uint32_t lo = 0, hi = HH_NT - 1;  // first entry whose inclusive prefix exceeds j
+        while (lo < hi) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (s_incl[m] > j) hi = m; else lo = m + 1;
+        }
+        const uint64_t ex = lo ? s_incl[lo - 1] : 0ull;
+        vv[q] = s_iv[lo];
+        w[q] = ok[q] ? a.g.keys[s_start[lo] + (j - ex)] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < HH_UN; ++q) {
+        const bool in = ok[q] && w[q] > u;
+        fn(in ? (w[q] - u - 1) >> shift : HH_NOB, w[q], vv[q]);
+      }
+    }
     __syncthreads();
+    // done when this block reached the item's end (uniform)
+    if (g0 + HH_NT >= h.nf || fpr[g0 + HH_NT - 1] >= j1) break;
   }
 }
 
 template <bool SCATTER, bool CUSTOM>
-__global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, const uint32_t* __restrict__ irow,
-                                                   const uint32_t* __restrict__ hr_u,
+__global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, uint64_t nh, const uint32_t* __restrict__ hr_u,
                                                    const uint32_t* __restrict__ hr_shift,
                                                    const uint32_t* __restrict__ hr_p, const uint64_t* __restrict__ bbase,
-                                                   const uint64_t* __restrict__ ibase, uint32_t* __restrict__ bcnt,
-                                                   const uint64_t* __restrict__ boff, uint32_t* __restrict__ bcur,
-                                                   uint32_t* __restrict__ sw, uint32_t* __restrict__ sv) {
+                                                   const uint64_t* __restrict__ ibase,
+                                                   const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ fp,
+                                                   uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
+                                                   uint32_t* __restrict__ bcur, uint32_t* __restrict__ sw,
+                                                   uint32_t* __restrict__ sv) {
   __shared__ uint32_t s_h[HH_PMAX];
   __shared__ uint64_t s_incl[HH_NT], s_start[HH_NT];
   __shared__ uint32_t s_iv[HH_NT];
   __shared__ uint64_t s_w[HH_NW];
-  __shared__ uint64_t s_tot;
-  const int t = threadIdx.x;
+  __shared__ uint64_t s_tot, s_f;
+  __shared__ uint32_t s_r;
+  const int t = threadIdx.x, lane = lane_id();
   const uint64_t item = blockIdx.x;
-  const uint32_t r = irow[item];
+  if (t == 0) {  // the item's row: the last r with ibase[r] <= item
+    uint64_t lo = 0, hi = nh;
+    while (hi - lo > 1) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (ibase[m] <= item) lo = m; else hi = m;
+    }
+    s_r = (uint32_t)lo;
+  }
+  __syncthreads();
+  const uint32_t r = s_r;
   const uint32_t u = hr_u[r], shift = hr_shift[r], P = hr_p[r];
   const uint64_t bb = bbase[r];
-  const uint64_t f0 = (item - ibase[r]) * HH_EC, f1 = f0 + HH_EC;
+  const HhHops h = hh_hops(a, u);
+  const uint64_t* fpr = fp + fbase[r];
+  const uint64_t Wr = fpr[h.nf - 1];
+  const uint64_t j0 = (item - ibase[r]) * HH_WC, j1 = j0 + HH_WC < Wr ? j0 + HH_WC : Wr;
+  if (t == 0) {  // the first first hop whose list reaches past j0
+    uint64_t lo = 0, hi = h.nf - 1;
+    while (lo < hi) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (fpr[m] > j0) hi = m; else lo = m + 1;
+    }
+    s_f = lo;
+  }
   for (uint32_t b = t; b < P; b += HH_NT) s_h[b] = 0;
   __syncthreads();
-  hh_enum_item(a, u, f0, f1, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t) {
-    atomicAdd(&s_h[(w - u - 1) >> shift], 1u);
-  });
+  const uint64_t f = s_f;
+  // a run of equal buckets over consecutive lanes: its head adds the run's length
+  auto count = [&](uint32_t b, uint32_t, uint32_t) {
+    const uint32_t pb = __shfl_up(b, 1, 64);
+    const uint64_t ch = __ballot(lane == 0 || pb != b);
+    if (b != HH_NOB && (lane == 0 || pb != b)) {
+      const uint64_t rest = lane < 63 ? ch >> (lane + 1) : 0ull;
+      atomicAdd(&s_h[b], rest ? (uint32_t)__builtin_ctzll(rest) + 1u : 64u - (uint32_t)lane);
+    }
+  };
+  hh_enum_range(a, u, shift, h, fpr, f, j0, j1, s_incl, s_start, s_iv, s_w, &s_tot, count);
   if (!SCATTER) {
     for (uint32_t b = t; b < P; b += HH_NT)
       if (s_h[b]) atomicAdd(&bcnt[bb + b], s_h[b]);
     return;
   }
+  __syncthreads();
   for (uint32_t b = t; b < P; b += HH_NT) {  // reserve: s_h[b] = this item's first scratch word in bucket b
-    const uint32_t h = s_h[b];
-    s_h[b] = h ? (uint32_t)boff[bb + b] + atomicAdd(&bcur[bb + b], h) : 0u;
+    const uint32_t c = s_h[b];
+    s_h[b] = c ? (uint32_t)boff[bb + b] + atomicAdd(&bcur[bb + b], c) : 0u;
   }
   __syncthreads();
-  hh_enum_item(a, u, f0, f1, s_incl, s_start, s_iv, s_w, &s_tot, [&](uint32_t w, uint32_t v) {
-    const uint32_t p = atomicAdd(&s_h[(w - u - 1) >> shift], 1u);
-    sw[p] = w;
-    if (CUSTOM) sv[p] = v;
-  });
+  auto scatter = [&](uint32_t b, uint32_t w, uint32_t v) {
+    const uint32_t pb = __shfl_up(b, 1, 64);
+    const bool head = lane == 0 || pb != b;
+    const uint64_t ch = __ballot(head);
+    uint32_t base = 0;
+    if (b != HH_NOB && head) {
+      const uint64_t rest = lane < 63 ? ch >> (lane + 1) : 0ull;
+      base = atomicAdd(&s_h[b], rest ? (uint32_t)__builtin_ctzll(rest) + 1u : 64u - (uint32_t)lane);
+    }
+    const uint64_t upto = ch & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    const int hl = 63 - __builtin_clzll(upto);  // this lane's run head
+    base = __shfl(base, hl, 64);
+    if (b != HH_NOB) {
+      const uint32_t p = base + (uint32_t)(lane - hl);
+      sw[p] = w;
+      if (CUSTOM) sv[p] = v;
+    }
+  };
+  hh_enum_range(a, u, shift, h, fpr, f, j0, j1, s_incl, s_start, s_iv, s_w, &s_tot, scatter);
 }
 
 // Accumulation items {bucket, w-range [slo, shi), distinct bound}.  A bucket

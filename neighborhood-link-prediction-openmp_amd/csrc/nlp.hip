@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -116,6 +116,17 @@ hipError_t wsget(Workspace& ws, int id, uint64_t count, T** out) {
   hipError_t e = ws.get(id, (size_t)count * sizeof(T), &p);
   *out = (T*)p;
   return e;
+}
+
+// scan_excl_u64 over workspace scratch `id`, checked against the scratch's
+// size first (round 3's C1 IHub fault was a scan of more items than its
+// scratch was sized for): an undersized scratch is a sizing bug, reported as
+// hipErrorInvalidValue instead of an out-of-bounds device write.
+template <typename T>
+hipError_t scan_ws(const Workspace& ws, int id, const T* in, uint64_t n, uint64_t* out, uint64_t* d_total,
+                   hipStream_t st) {
+  if (ws.bytes[id] < scan_scratch_words(n) * 8) return hipErrorInvalidValue;
+  return scan_excl_u64<T>(in, n, out, d_total, (uint64_t*)ws.p[id], st);
 }
 
 }  // namespace
@@ -1605,54 +1616,59 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   *done = false;
   const uint64_t nh = n2 + n3;
   uint32_t* hr;    // u, shift, P, items: 4 x nh
-  uint64_t* pre;   // bucket prefix [nh + 1], item prefix [nh + 1]
+  uint64_t* pre;   // bucket prefix [nh + 1], item prefix [nh + 1], first-hop count [nh], first-hop prefix [nh + 1]
   TRY(wsget(ws, B_HH_ROWS, 4 * nh, &hr));
-  TRY(wsget(ws, B_HH_PRE, 2 * (nh + 1), &pre));
+  TRY(wsget(ws, B_HH_PRE, 4 * (nh + 1), &pre));
   uint32_t *hr_u = hr, *hr_shift = hr + nh, *hr_p = hr + 2 * nh, *hr_items = hr + 3 * nh;
-  uint64_t *bbase = pre, *ibase = pre + nh + 1;
-  LAUNCH(k_hh_rows, nh, st, a, l2, n2, l3, n3, wu, ua, hr_u, hr_shift, hr_p, hr_items, g->hh_bw);
+  uint64_t *bbase = pre, *ibase = pre + nh + 1, *hr_nf = pre + 2 * (nh + 1), *fbase = pre + 3 * (nh + 1);
+  LAUNCH(k_hh_rows, nh, st, a, l2, n2, l3, n3, wu, ua, hr_u, hr_shift, hr_p, hr_items, hr_nf, g->hh_bw);
   TRY(hipGetLastError());
-  TRY(scan_excl_u64<uint32_t>(hr_p, nh, bbase, bbase + nh, scan, st));
-  TRY(scan_excl_u64<uint32_t>(hr_items, nh, ibase, ibase + nh, scan, st));
+  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_p, nh, bbase, bbase + nh, st));
+  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_items, nh, ibase, ibase + nh, st));
+  TRY(scan_ws<uint64_t>(ws, B_SCAN, hr_nf, nh, fbase, fbase + nh, st));
   TRY(hipMemcpyAsync(&g->host_small[48], bbase + nh, 8, hipMemcpyDeviceToHost, st));
   TRY(hipMemcpyAsync(&g->host_small[49], ibase + nh, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(&g->host_small[51], fbase + nh, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
-  const uint64_t NB = g->host_small[48], NI = g->host_small[49];
+  const uint64_t NB = g->host_small[48], NI = g->host_small[49], NF = g->host_small[51];
   if (NB == 0 || NI == 0) {
     *done = true;
     return NLP_OK;
   }
   if (NI > 0x7fffffffull) return NLP_OK;
-  uint32_t* maps;  // brow [NB], irow [NI]
+  uint32_t* maps;  // brow [NB]
   uint32_t* bc;    // bcnt [NB], bcur [NB]
-  uint64_t *boff, *xs;
-  TRY(wsget(ws, B_HH_MAPS, NB + NI, &maps));
+  uint64_t *boff, *xs, *fp;
+  TRY(wsget(ws, B_HH_MAPS, NB, &maps));
   TRY(wsget(ws, B_HH_BCNT, 2 * NB, &bc));
   TRY(wsget(ws, B_HH_BOFF, NB + 1, &boff));
   TRY(wsget(ws, B_HH_XS, NB, &xs));
-  uint32_t *brow = maps, *irow = maps + NB, *bcnt = bc, *bcur = bc + NB;
+  TRY(wsget(ws, B_HH_FP, std::max<uint64_t>(NF, 1), &fp));
+  uint32_t *brow = maps, *bcnt = bc, *bcur = bc + NB;
   TRY(hipMemsetAsync(bc, 0, 2 * NB * 4, st));
   LAUNCH(k_hh_maps, nh, st, a, nh, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p,
-         (const uint64_t*)bbase, (const uint32_t*)hr_items, (const uint64_t*)ibase, brow, irow);
+         (const uint64_t*)bbase, (const uint32_t*)hr_items, (const uint64_t*)ibase, brow, (uint32_t*)nullptr);
   LAUNCH(k_hh_xstart, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
          (const uint64_t*)bbase, xs);
+  hipLaunchKernelGGL(k_hh_fpre, dim3((unsigned)std::min<uint64_t>(nh, 4096)), dim3(HH_NT), 0, st, a, nh,
+                     (const uint32_t*)hr_u, (const uint64_t*)hr_nf, (const uint64_t*)fbase, fp);
   TRY(hipGetLastError());
   if (custom)
-    hipLaunchKernelGGL((k_hh_enum<false, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint64_t*)ibase, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr);
+    hipLaunchKernelGGL((k_hh_enum<false, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, nh, (const uint32_t*)hr_u,
+                       (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)ibase,
+                       (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
   else
-    hipLaunchKernelGGL((k_hh_enum<false, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint64_t*)ibase, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr);
+    hipLaunchKernelGGL((k_hh_enum<false, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, nh, (const uint32_t*)hr_u,
+                       (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)ibase,
+                       (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
   TRY(hipGetLastError());
   // the buckets can outnumber the chunk's rows (the caller's scan scratch is
   // sized for those): a scratch of their own
   uint64_t* bscan;
   TRY(wsget(ws, B_HH_SCAN, scan_scratch_words(NB + 1) + 16, &bscan));
-  TRY(scan_excl_u64<uint32_t>(bcnt, NB, boff, boff + NB, bscan, st));
+  TRY(scan_ws<uint32_t>(ws, B_HH_SCAN, bcnt, NB, boff, boff + NB, st));
   TRY(hipMemcpyAsync(&g->host_small[50], boff + NB, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
   const uint64_t tot = g->host_small[50];
@@ -1663,13 +1679,13 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   uint32_t* sw = g->hp_scratch;
   uint32_t* sv = custom ? g->hp_scratch + capw : nullptr;
   if (custom)
-    hipLaunchKernelGGL((k_hh_enum<true, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint64_t*)ibase, bcnt, (const uint64_t*)boff, bcur, sw, sv);
+    hipLaunchKernelGGL((k_hh_enum<true, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, nh, (const uint32_t*)hr_u,
+                       (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)ibase,
+                       (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)boff, bcur, sw, sv);
   else
-    hipLaunchKernelGGL((k_hh_enum<true, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, (const uint32_t*)irow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint64_t*)ibase, bcnt, (const uint64_t*)boff, bcur, sw, sv);
+    hipLaunchKernelGGL((k_hh_enum<true, false>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, nh, (const uint32_t*)hr_u,
+                       (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)ibase,
+                       (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)boff, bcur, sw, sv);
   TRY(hipGetLastError());
   // accumulation items (k_hh_plan, k_hh_split): a bucket, or a w-range of a heavy bucket
   const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
@@ -1768,7 +1784,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
       LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
       TRY(hipGetLastError());
-      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipMemcpyAsync(&g->host_small[11], hd, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
@@ -1800,9 +1816,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
       LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
       TRY(hipGetLastError());
-      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
       TRY(wsget(ws, B_SCAN2, scan_scratch_words(nt) + 16, &scan2));
-      TRY(scan_excl_u64<uint32_t>(tcn, nt, tpre, tpre + nt, scan2, st));
+      TRY(scan_ws<uint32_t>(ws, B_SCAN2, tcn, nt, tpre, tpre + nt, st));
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
@@ -1831,7 +1847,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         hipLaunchKernelGGL(k_hp_surv_lists<false>, dim3(grid_full(ns)), dim3(NT), 0, st, gv, (const uint32_t*)g->vbydeg,
                            ns, ua, ub, (unsigned long long*)wu, scnt, (const uint64_t*)nullptr, (uint32_t*)nullptr);
       TRY(hipGetLastError());
-      TRY(scan_excl_u64<uint32_t>(scnt, nU, s_soff, s_soff + nU, scan, st));
+      TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
@@ -1856,7 +1872,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
   for (int b = 0; b < HP_NBINS; ++b) {
     TRY(wsget(ws, lb[b], nU, &lists[b]));
-    TRY(scan_excl_u64<uint8_t>(flags + (uint64_t)b * nU, nU, pos, small + 24 + b, scan, st));
+    TRY(scan_ws<uint8_t>(ws, B_SCAN, flags + (uint64_t)b * nU, nU, pos, small + 24 + b, st));
     LAUNCH(k_hp_scatter, nU, st, flags + (uint64_t)b * nU, pos, nU, ua, lists[b]);
     TRY(hipGetLastError());
   }
@@ -1886,7 +1902,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
                 (unsigned long long)lw[l]);
   }
   // row prefix of W(u) (wu[nU] = total)
-  TRY(scan_excl_u64<uint64_t>(wu, nU, pos, small + 16, scan, st));
+  TRY(scan_ws<uint64_t>(ws, B_SCAN, wu, nU, pos, small + 16, st));
   TRY(hipMemcpyAsync(pos + nU, small + 16, 8, hipMemcpyDeviceToDevice, st));
   TRY(hipMemcpyAsync(&g->host_small[8], small + 16, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
@@ -1970,7 +1986,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         uint32_t* nbat = tcnt + 10;
         const uint64_t bwid = 256;  // tiers 0 and 1 (W <= 256) together, 1024-entry tables
         LAUNCH(k_hp_batch_w, n0, st, (const uint32_t*)tl, n0, tc, 0, 1, (const uint64_t*)wu, ua, bw);
-        TRY(scan_excl_u64<uint64_t>(bw, n0, bpre, bpre + n0, scan, st));
+        TRY(scan_ws<uint64_t>(ws, B_SCAN, bw, n0, bpre, bpre + n0, st));
         TRY(hipMemsetAsync(nbat, 0, 4, st));
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
