@@ -46,8 +46,9 @@ constexpr uint64_t HP_B2_MAX = 1ull << 19;  // bin 2: W(u) <= 2^19, bin 3: the r
 constexpr int HP_NBINS = 4;
 
 // per-chunk counters (u64)
-// HPC_HOTB: algorithmic bytes of the chunk's k_hp_batch launch, counted by the kernel
-enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_HOTB = 5, HPC_NCTR = 8 };
+// HPC_HOTB: algorithmic bytes of the chunk's k_hp_batch launch, counted by the kernel;
+// HPC_PAD: padding entries written into the unused tails of emission windows (hp_flush)
+enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_HOTB = 5, HPC_PAD = 6, HPC_NCTR = 8 };
 
 struct HpArgs {
   GraphView g;
@@ -77,6 +78,7 @@ struct HpArgs {
   unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
   int xp;                  // experiment (NLP_HB_XP, wrong results): 1 skip k_hp_batch's exclusion, 2 its emission,
                            // 4 its wedge inserts
+  uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -423,7 +425,21 @@ struct HpStage {
   uint32_t n;     // wave-uniform fill
   uint64_t cand, nan;
   uint64_t out;   // candidates written (wave-uniform; the batch kernel's algorithmic bytes)
+  // emission window (wave-uniform; wend > 0: windowed): slots [wpos, wend)
+  // reserved with one atomic per HP_WIN candidates, the unused tail padded
+  uint64_t wpos, wend;
+  bool win;
+  uint64_t pad;
 };
+// Emission windows.  Every wave of every path-4 kernel reserving each flush
+// on ONE counter serialises at the memory side (C4 JAC H=16: 2.2 M
+// reservations, ~7 ms of the row batches); the row batches' persistent waves
+// reserve a.win slots at a time (sized by the host to a fraction of a wave's
+// expected emissions, at most HP_WIN) and pad what a window does not use with
+// entries that can never be selected (score key 0, u = w = 0xffffffff: last of
+// every tie), counted in HPC_PAD and dropped by the prune.
+constexpr uint64_t HP_WIN = 4096;
+constexpr uint32_t HP_PADID = 0xffffffffu;
 
 // Orders one wave's LDS accesses across lanes (staging, scan arrays, LDS
 // tables).  A wavefront-scope fence emits no instruction and the wave barrier
@@ -436,13 +452,38 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 }
 
+// padding entries in slots [p0, p1) of the chunk's emission region
+__device__ __forceinline__ void hp_pad(const HpArgs& a, uint64_t p0, uint64_t p1) {
+  for (uint64_t p = p0 + lane_id(); p < p1; p += 64)
+    if (p < a.cap) {
+      const uint64_t q = a.base + p;
+      a.ckey[q] = 0u;
+      a.cu[q] = HP_PADID;
+      a.cw[q] = HP_PADID;
+      a.cs[q] = __uint_as_float(0x7fc00000u);
+    }
+}
+
 __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
   if (st.n == 0) return;
   wave_sync_lds();
   const int lane = lane_id();
   unsigned long long pos = 0;
-  if (lane == 0) pos = atomicAdd(&a.ctr[HPC_EMIT], (unsigned long long)st.n);
-  pos = __shfl(pos, 0, 64);
+  if (st.win) {
+    if (st.wpos + st.n > st.wend) {  // a new window; the old one's tail padded
+      hp_pad(a, st.wpos, st.wend);
+      st.pad += st.wend - st.wpos;
+      const uint64_t wsz = (uint64_t)a.win > st.n ? (uint64_t)a.win : st.n;
+      if (lane == 0) pos = atomicAdd(&a.ctr[HPC_EMIT], (unsigned long long)wsz);
+      st.wpos = __shfl(pos, 0, 64);
+      st.wend = st.wpos + wsz;
+    }
+    pos = st.wpos;
+    st.wpos += st.n;
+  } else {
+    if (lane == 0) pos = atomicAdd(&a.ctr[HPC_EMIT], (unsigned long long)st.n);
+    pos = __shfl(pos, 0, 64);
+  }
   for (uint32_t i = lane; i < st.n; i += 64) {
     const uint64_t p = pos + i;
     if (p < a.cap) {
@@ -482,11 +523,17 @@ __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid
 
 __device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t wedges) {
   hp_flush(st, a);
+  if (st.win) {  // the last window's tail
+    hp_pad(a, st.wpos, st.wend);
+    st.pad += st.wend - st.wpos;
+    st.wpos = st.wend;
+  }
   const uint64_t c = wave_sum(st.cand), n = wave_sum(st.nan), wd = wave_sum(wedges);
   if (lane_id() == 0) {
     if (c) atomicAdd(&a.ctr[HPC_CAND], (unsigned long long)c);
     if (n) atomicAdd(&a.ctr[HPC_NAN], (unsigned long long)n);
     if (wd) atomicAdd(&a.ctr[HPC_WEDGE], (unsigned long long)wd);
+    if (st.pad) atomicAdd(&a.ctr[HPC_PAD], (unsigned long long)st.pad);
   }
 }
 
@@ -1646,6 +1693,45 @@ __device__ __forceinline__ uint32_t hb_slot(const uint32_t* incl, uint32_t, uint
   return lo;
 }
 
+// ---------------------------------------------------------------- one-word table entries (count metrics)
+// The row batches' count tables keep an entry as ONE u64 word, key << 32 |
+// count word, so a wedge that creates its entry costs a single LDS
+// compare-and-swap (the two-array table paid a key load, a key CAS and a
+// count add): most wedges of a k-filling call create their entry (C4 JAC
+// H=16: 2.77e8 candidates from 2.80e8 wedges).  The count word is the KD
+// layout (count in the low CB bits, min(deg w, DSAT) above, HP_EXCL on top),
+// so an add of 1 never carries into the key.
+constexpr uint64_t HP_EMPTY64 = (uint64_t)HP_EMPTY << 32;
+
+template <int CB>
+__device__ __forceinline__ void h64_insert(uint64_t* t, uint32_t mask, int shift, uint32_t key, uint32_t dw,
+                                           unsigned long long* err) {
+  constexpr uint32_t DSAT = CB > 0 ? (1u << (31 - CB)) - 1u : 0u;
+  const uint64_t init = (uint64_t)key << 32 | (1u + (CB > 0 ? (dw < DSAT ? dw : DSAT) << CB : 0u));
+  uint32_t h = hp_hash(key, shift);
+  for (uint32_t probe = 0;; ++probe) {
+    if (probe > mask) { atomicOr(err, 1ull); return; }
+    const uint64_t old = atomicCAS((unsigned long long*)&t[h], (unsigned long long)HP_EMPTY64, (unsigned long long)init);
+    if (old == HP_EMPTY64) return;
+    if ((uint32_t)(old >> 32) == key) {
+      atomicAdd((unsigned long long*)&t[h], 1ull);
+      return;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ void h64_mark(uint64_t* t, uint32_t mask, int shift, uint32_t x) {
+  uint32_t h = hp_hash(x, shift);
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint64_t cur = *(volatile uint64_t*)&t[h];
+    const uint32_t k = (uint32_t)(cur >> 32);
+    if (k == x) { atomicOr((unsigned long long*)&t[h], (unsigned long long)HP_EXCL); return; }
+    if (k == HP_EMPTY) return;
+    h = (h + 1) & mask;
+  }
+}
+
 // KD (count metrics, with the graph's entry degrees): deg w rides in the table
 // (hp_insert_kd<10>: a batch holds at most 512 wedges), no gather at the drain.
 template <bool CUSTOM, int TW, int STG = HP_STG, bool KD = false, int UN = HB_UN, int MW = 1>
@@ -1655,8 +1741,10 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
                                                  const uint32_t* __restrict__ nbatch, const uint64_t* __restrict__ wu,
                                                  uint64_t ua, int wbits) {
   constexpr int VT = CUSTOM ? TW : 1;
-  __shared__ uint32_t s_k[NWAVE][TW];
-  __shared__ uint32_t s_c[NWAVE][TW];
+  constexpr int KT = CUSTOM ? TW : 1;      // AA / RA: key and accumulator arrays (ordered tables)
+  __shared__ uint32_t s_k[NWAVE][KT];
+  __shared__ uint32_t s_c[NWAVE][KT];
+  __shared__ uint64_t s_kc[NWAVE][CUSTOM ? 1 : TW];  // count metrics: one-word entries
   __shared__ uint32_t s_v0[NWAVE][VT];
   __shared__ uint32_t s_v1[NWAVE][VT];
   __shared__ uint32_t s_incl[NWAVE][64];   // first-hop block: inclusive prefix of the lengths
@@ -1681,13 +1769,18 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
   const uint32_t nb = *nbatch;
   const uint32_t wmask = (1u << wbits) - 1u;
   const HpTable tb{s_k[wv], s_c[wv], s_v0[wv], s_v1[wv]};
+  uint64_t* const t64 = s_kc[wv];
   for (int i = lane; i < TW; i += 64) {
-    s_k[wv][i] = HP_EMPTY;
-    s_c[wv][i] = 0;
-    if (CUSTOM) s_v0[wv][i] = 0;  // owner tokens
+    if (CUSTOM) {
+      s_k[wv][i] = HP_EMPTY;
+      s_c[wv][i] = 0;
+      s_v0[wv][i] = 0;  // owner tokens
+    } else {
+      t64[i] = HP_EMPTY64;
+    }
   }
   uint32_t round = 0;
-  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0};
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], STG, 0, 0, 0, 0, 0, 0, a.win != 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
   uint64_t abytes = 0;  // algorithmic bytes (wave-uniform): rows, entries, exclusion keys
@@ -1850,7 +1943,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
                                         const uint32_t sl = s_islot[wv][ent];
                                         if (w > s_u[wv][sl]) {
                                           ++wedges;
-                                          if (!(a.xp & 4)) hp_insert_kd<10>(tb, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
+                                          if (!(a.xp & 4)) h64_insert<10>(t64, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
                                         }
                                       }, a.kdeg);
       } else {
@@ -1859,7 +1952,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
                            const uint32_t sl = s_islot[wv][ent];
                            if (w > s_u[wv][sl]) {
                              ++wedges;
-                             hp_insert<false, CUSTOM>(tb, mask, shift, (sl << wbits) | w, vv, &a.ctr[HPC_ERR]);
+                             h64_insert<0>(t64, mask, shift, (sl << wbits) | w, 0u, &a.ctr[HPC_ERR]);
                            }
                          });
       }
@@ -1887,7 +1980,10 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
       for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const uint32_t x = x0 + (uint32_t)q * 64 + (uint32_t)lane;
-        if (x < NN && key[q] > s_u[wv][sl[q]]) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
+        if (x < NN && key[q] > s_u[wv][sl[q]]) {
+          if (CUSTOM) hp_mark<false>(tb, mask, shift, (sl[q] << wbits) | key[q]);
+          else h64_mark(t64, mask, shift, (sl[q] << wbits) | key[q]);
+        }
       }
     }
     wave_sync_lds();
@@ -1907,8 +2003,14 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         if ((uint32_t)q >= nq) break;
         const uint32_t i = i0 + (uint32_t)q * 64 + (uint32_t)lane;
         c[q] = v0[q] = v1[q] = 0;
-        if (CUSTOM) kq[q] = ho_take(tb, i, &c[q]);
-        else kq[q] = hp_take<false, false>(tb, i, &c[q], &v0[q], &v1[q]);
+        if (CUSTOM) {
+          kq[q] = ho_take(tb, i, &c[q]);
+        } else {
+          const uint64_t x = t64[i];
+          kq[q] = (uint32_t)(x >> 32);
+          c[q] = (uint32_t)x;
+          if (kq[q] != HP_EMPTY) t64[i] = HP_EMPTY64;
+        }
       }
       if (!CUSTOM) {
 #pragma unroll

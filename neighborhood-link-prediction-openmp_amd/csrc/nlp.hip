@@ -274,9 +274,11 @@ struct nlp_graph {
   int hb_var = 0;            // experiment (NLP_HB_VAR): k_hp_batch KD build -- 0: 8 loads per lane, 1: 4, 2: 4 + 3 waves
                              // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
   int hb_xp = 0;             // experiment (NLP_HB_XP): k_hp_batch phases skipped (wrong results; timing only)
+  bool hp_win = true;        // k_hp_batch reserves emission windows (NLP_HASH_WIN=0: one reservation per flush)
   bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
+  unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
@@ -754,6 +756,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
   if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
   if (const char* hx = getenv("NLP_HB_XP")) g->hb_xp = atoi(hx);
+  if (const char* hw = getenv("NLP_HASH_WIN")) g->hp_win = hw[0] != '0';
   if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
@@ -783,6 +786,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
+    TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
     unsigned a = 0, b = 0;
@@ -843,6 +847,7 @@ struct Cands {
   uint64_t nan = 0;
   uint64_t total = 0; // candidates produced (before pruning)
   uint64_t wedges = 0;
+  uint64_t pad = 0;        // path 4: padding entries among the n held (emission window tails, hashpath.hpp hp_flush)
   double hot_ms = 0;       // path 4: device time of the k_hp_batch launches (HIP events around each)
   uint64_t hot_bytes = 0;  // and their algorithmic bytes (counted by the kernel, HPC_HOTB)
   uint32_t hot_launches = 0;
@@ -1920,6 +1925,30 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
   bool full = false;  // k candidates held: tau is in force
   uint64_t target = E;
+  // Prune the held candidates: with at least k real ones (padding excluded) to
+  // the canonical top k, and tau = the k-th key from then on; with fewer, only
+  // the padding goes (it ranks below every real candidate: key 0, u and w
+  // 0xffffffff), and no threshold is set.
+  auto prune_held = [&]() -> nlp_status {
+    const uint64_t real = C.n - C.pad;
+    uint32_t kth = 0;
+    if (real >= k) {
+      if (C.n > k) {
+        nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+        if (s != NLP_OK) return s;
+      }
+      C.pad = 0;
+      tau = (int64_t)kth;
+      full = true;
+      g->host_small[8] = (uint64_t)tau;
+      TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
+    } else if (C.pad) {
+      nlp_status s = hp_prune(g, C, real, capC, &kth, st);
+      if (s != NLP_OK) return s;
+      C.pad = 0;
+    }
+    return NLP_OK;
+  };
   while (r0 < nU) {
     hipLaunchKernelGGL(k_hp_bounds, dim3(1), dim3(64), 0, st, (const uint64_t*)pos, nU, r0, target, ua,
                        (const uint32_t*)lists[0], (const uint32_t*)lists[1], (const uint32_t*)lists[2],
@@ -1959,6 +1988,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.sua = ua;
     a.xs = g->xs;
     a.xp = g->hb_xp;
+    a.win = 0;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
     if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
@@ -1990,17 +2020,27 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(hipMemsetAsync(nbat, 0, 4, st));
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
+        unsigned gb = gr;  // row batches
+        if (g->hp_win) {
+          // persistent waves (one resident round) reserving emission windows: about an
+          // eighth of a wave's share of the chunk's wedge bound per window
+          const unsigned grb = std::min<unsigned>(gr, g->occ_hb);
+          const uint64_t per = wchunk / ((uint64_t)grb * NWAVE * 8 + 1);
+          a.win = (uint32_t)std::max<uint64_t>(HP_STG, std::min<uint64_t>(HP_WIN, per));
+          gb = grb;
+        }
         TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
-        if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 1) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 1>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 2) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 3) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 8, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 4) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 2, 3>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gr), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 1) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 1>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 2) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 3) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 8, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg && g->hb_var == 4) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 2, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());
         TRY(hipEventRecord(g->ev[6], st));
         batch_timed = true;
+        a.win = 0;  // the other row kernels reserve per flush
         if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_wave<false, HP_WT, HP_STG, true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
@@ -2077,20 +2117,16 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       // overflow: nothing of this chunk is kept; prune what is held and retry a smaller chunk
       rate = std::max(rate, (double)emitted / (double)std::max<uint64_t>(wchunk, 1));
       target = std::max<uint64_t>(1, wchunk / 4);
-      if (C.n > k) {
-        uint32_t kth = 0;
-        nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+      if (C.n > k || C.pad) {
+        nlp_status s = prune_held();
         if (s != NLP_OK) return s;
-        tau = (int64_t)kth;
-        full = true;
-        g->host_small[8] = (uint64_t)tau;
-        TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
       } else if (r1 == r0 + 1) {
         return NLP_ERR_DEVICE;  // one row cannot exceed E >= S free slots
       }
       continue;
     }
     ++*nchunks;
+    C.pad += g->host_small[HPC_PAD];
     C.n += emitted;
     C.total += g->host_small[HPC_CAND];
     C.nan += g->host_small[HPC_NAN];
@@ -2098,14 +2134,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     rate = (double)emitted / (double)std::max<uint64_t>(wchunk, 1);
     r0 = r1;
     for (int b = 0; b < HP_NBINS; ++b) q0[b] = q1[b];
-    if (C.n > k && (C.n > k + E / 2 || r0 >= nU)) {
-      uint32_t kth = 0;
-      nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+    if ((C.n > k && C.n > k + E / 2) || (r0 >= nU && (C.n > k || C.pad))) {
+      nlp_status s = prune_held();
       if (s != NLP_OK) return s;
-      tau = (int64_t)kth;
-      full = true;
-      g->host_small[8] = (uint64_t)tau;
-      TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
     }
     // next chunk: aim at half of the free buffer at the last emission rate
     const uint64_t free_slots = capC - C.n;

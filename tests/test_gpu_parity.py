@@ -427,7 +427,8 @@ class _env:
 # (no per-graph rank bytes), 22 survivor counts and fill as two kernels (not
 # k_hp_dcls_one), 23 k_hp_dcls_one's output capacity overflowing (the
 # two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
-# above u), 25 the row batches' 4-loads / 3-waves build
+# above u), 25 the row batches' 4-loads / 3-waves build, 26 the row batches
+# reserving every flush (no emission windows, no padding)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -442,7 +443,7 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2")]
+                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"), dict(NLP_HASH_WIN="0")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
