@@ -31,7 +31,7 @@ run() {  # name limit cmd...
 for s in ${STEPS//,/ }; do
   case $s in
     tests) run tests ${TESTS_LIMIT:-600} python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_dist.py tests/test_gpu_ingest.py} \
-             -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+             ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bench) run bench ${BENCH_LIMIT:-900} python3 bench.py $BENCH_ARGS
            grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
