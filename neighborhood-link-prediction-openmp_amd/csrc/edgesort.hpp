@@ -41,7 +41,7 @@ constexpr int ES_TILE = ES_NT * ES_IPT;    // 4096 records per tile
 constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
 constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
 constexpr uint32_t ES_SPIN_LIMIT = 1u << 26;
-constexpr int ES_LBW = 16;                 // predecessors read per look-back round trip
+constexpr int ES_LBW = 8;                  // predecessors read per look-back round trip
 
 // 8-bit digit `shift` (bit offset) of K; `bits` < 8 for the top digit
 __device__ __forceinline__ uint32_t es_digit(uint32_t u, uint32_t w, float s, int vb, int shift) {
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ ticket, uint64_t epoch,
                                                    uint32_t* __restrict__ err) {
   __shared__ uint32_t s_u[ES_TILE], s_w[ES_TILE], s_s[ES_TILE];
+  __shared__ uint8_t s_d[ES_TILE];         // each tile position's digit (the write phase does not recompute it)
   __shared__ uint32_t s_wc[ES_NW][256];   // per wave: running digit counts, then wave prefixes
   __shared__ uint64_t s_gofs[256];        // global position of the tile's first record of each digit
   __shared__ uint32_t s_lofs[256];        // tile position of the first record of each digit
@@ -244,13 +245,14 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
         s_u[p] = ru[i];
         s_w[p] = rw[i];
         s_s[p] = rs[i];
+        s_d[p] = (uint8_t)dg[i];
       }
     }
     __syncthreads();
     // write the digit runs: consecutive tile positions -> consecutive output records
     for (uint32_t p = (uint32_t)t; p < tn; p += ES_NT) {
       const uint32_t u = s_u[p], w = s_w[p], sb = s_s[p];
-      const uint32_t d = es_digit(u, w, __uint_as_float(sb), vb, shift);
+      const uint32_t d = s_d[p];
       const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);
       out[pos] = EdgeOut{u, w, __uint_as_float(sb)};
     }

@@ -1924,6 +1924,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t r0 = 0, q0[HP_NBINS] = {0, 0, 0, 0};
   double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
   bool full = false;  // k candidates held: tau is in force
+  bool retry = false; // the chunk is a retry after an emission overflow
   uint64_t target = E;
   // Prune the held candidates: with at least k real ones (padding excluded) to
   // the canonical top k, and tau = the k-th key from then on; with fewer, only
@@ -2021,13 +2022,18 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
         unsigned gb = gr;  // row batches
-        if (g->hp_win) {
+        if (g->hp_win && !retry) {
           // persistent waves (one resident round) reserving emission windows: about an
-          // eighth of a wave's share of the chunk's wedge bound per window
+          // eighth of a wave's share of the chunk's wedge bound per window, so the
+          // padding stays below an eighth of the chunk's emission bound; a chunk too
+          // small for a window of HP_STG per wave, or the retry of an overflowed
+          // chunk, reserves per flush
           const unsigned grb = std::min<unsigned>(gr, g->occ_hb);
           const uint64_t per = wchunk / ((uint64_t)grb * NWAVE * 8 + 1);
-          a.win = (uint32_t)std::max<uint64_t>(HP_STG, std::min<uint64_t>(HP_WIN, per));
-          gb = grb;
+          if (per >= (uint64_t)HP_STG) {
+            a.win = (uint32_t)std::min<uint64_t>(HP_WIN, per);
+            gb = grb;
+          }
         }
         TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
         if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
@@ -2115,6 +2121,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     if (g->host_small[HPC_ERR]) return NLP_ERR_DEVICE;
     if (emitted > a.cap) {
       // overflow: nothing of this chunk is kept; prune what is held and retry a smaller chunk
+      // (without emission windows: their padding must not keep a retry overflowing)
+      retry = true;
       rate = std::max(rate, (double)emitted / (double)std::max<uint64_t>(wchunk, 1));
       target = std::max<uint64_t>(1, wchunk / 4);
       if (C.n > k || C.pad) {
@@ -2126,6 +2134,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       continue;
     }
     ++*nchunks;
+    retry = false;
     C.pad += g->host_small[HPC_PAD];
     C.n += emitted;
     C.total += g->host_small[HPC_CAND];
