@@ -2838,23 +2838,40 @@ __global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, uint64_t nh, const 
 // Accumulation items {bucket, w-range [slo, shi), distinct bound}.  A bucket
 // whose distinct-w bound 2 min(n, width) fits the table is one item
 // (k_hh_plan).  A heavier one -- a hub row's wedges are skewed towards low
-// ids, so its first buckets can hold most of them -- is cut by k_hh_split: a
-// histogram of its scratch over HH_FINE equal w-ranges, grouped greedily into
-// consecutive ranges of at most T / 2 wedges (a single fine range beyond that
-// is bounded by its width instead).  The items of a heavy bucket run on
-// different workgroups, each streaming the bucket's scratch and keeping its
-// own w-range.
+// ids, so its first buckets can hold most of them -- is cut into consecutive
+// w-ranges from a histogram of its scratch: k_hh_plan lists the heavy buckets
+// with their scratch in segments of HH_SEG wedges (one packed counter gives
+// both the heavy index and the first segment, so segments stay sorted by
+// heavy bucket), k_hh_hist histograms every segment over the bucket's bins
+// (HH_BPS per segment, HH_FINE at most, power-of-two widths) in LDS and adds
+// it to the bucket's global bins, and k_hh_group groups the bins greedily into
+// ranges whose distinct-w bound min(wedges, width) stays within T / 2.  A
+// single bin beyond that is one HH_WIDE item, accumulated in width sub-ranges
+// of T / 2 by k_hh_accum.  The items of a heavy bucket run on different
+// workgroups, each streaming the bucket's scratch and keeping its own w-range.
 // AA / RA sort mode (wcap = HH_SCAP): items hold at most HH_SCAP wedges, which
 // k_hh_accum sorts by (w, v) in LDS and sums run by run in ascending v; a single
-// fine range beyond HH_SCAP wedges is cut by width and flagged HH_BIG (hash
-// table with the ordered re-walk of hp_ordered_sum).
+// bin beyond HH_SCAP wedges is flagged HH_BIG (hash table with the ordered
+// re-walk of hp_ordered_sum).
 struct HhItem {
-  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG)
+  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG | HH_WIDE)
   uint64_t slo, shi;  // w-range
 };
 constexpr uint32_t HH_FINE = 4096;
 constexpr uint32_t HH_SCAP = 4096;         // sort-mode wedges per item (32 KB of u64 keys)
 constexpr uint32_t HH_BIG = 0x80000000u;
+constexpr uint32_t HH_WIDE = 0x40000000u;  // the range is accumulated in sub-ranges of cnt w
+constexpr uint32_t HH_CNT = 0x3fffffffu;
+constexpr uint64_t HH_SEG = 65536;         // heavy scratch wedges per histogram segment
+constexpr uint32_t HH_BPS = 512;           // histogram bins per segment
+constexpr int HH_HSH = 40;                 // packed heavy counter: count << 40 | segments
+
+struct HhHeavy {
+  uint32_t gb, n;     // bucket, its wedges
+  uint32_t nbin, fsh; // bins of width 2^fsh from lo
+  uint64_t seg0;      // first segment (its bins at seg0 * HH_BPS)
+  uint64_t lo, hi;    // the bucket's w-range
+};
 
 __device__ __forceinline__ uint64_t hh_bucket_range(const HpArgs& a, uint32_t u, uint32_t shift, uint64_t b,
                                                     uint64_t* lo) {
@@ -2875,12 +2892,15 @@ __device__ __forceinline__ uint32_t hh_wave_append(bool want, uint32_t* ctr) {
 }
 
 // wcap > 0 (AA / RA sort mode, see k_hh_accum): items are bounded by their
-// wedge count (<= wcap) instead of their distinct-w bound.
+// wedge count (<= wcap) instead of their distinct-w bound.  Heavy buckets go to
+// heavy[] (at most hcap: host bound tot / half + 1) with their bins zeroed.
 __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
                           const uint32_t* __restrict__ hr_shift, const uint64_t* __restrict__ bbase,
                           const uint32_t* __restrict__ bcnt, int tl, HhItem* __restrict__ items,
-                          uint32_t* __restrict__ nitems, uint32_t* __restrict__ heavy, uint32_t* __restrict__ nheavy,
+                          uint32_t* __restrict__ nitems, HhHeavy* __restrict__ heavy,
+                          unsigned long long* __restrict__ hctr, uint64_t hcap, uint32_t* __restrict__ ghist,
                           uint32_t wcap) {
+  const int lane = lane_id();
   for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t gb = b0 + threadIdx.x;
     uint32_t n = 0;
@@ -2894,64 +2914,128 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
     const bool simple = n > 0 && (wcap ? n <= wcap : 2 * dist <= (1ull << tl)), hv = n > 0 && !simple;
     const uint32_t i = hh_wave_append(simple, nitems);
     if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};  // i < nb <= the item capacity
-    const uint32_t j = hh_wave_append(hv, nheavy);
-    if (hv) heavy[j] = (uint32_t)gb;
+    const uint64_t nseg = hv ? (n + HH_SEG - 1) / HH_SEG : 0;
+    const uint64_t pk = hv ? (1ull << HH_HSH) | nseg : 0ull;
+    const uint64_t inc = wave_incl_scan(pk), wt = __shfl(inc, 63, 64);
+    unsigned long long base = 0;
+    if (lane == 63 && wt) base = atomicAdd(hctr, (unsigned long long)wt);
+    base = __shfl(base, 63, 64);
+    if (hv) {
+      const uint64_t ex = base + inc - pk;
+      const uint64_t j = ex >> HH_HSH, s0 = ex & ((1ull << HH_HSH) - 1);
+      const uint32_t nbin = (uint32_t)(nseg * HH_BPS < HH_FINE ? nseg * HH_BPS : HH_FINE);
+      const uint32_t fsh = (uint32_t)log2_ceil((width + nbin - 1) / nbin);
+      if (j < hcap) {
+        heavy[j] = HhHeavy{(uint32_t)gb, n, nbin, fsh, s0, lo, lo + width};
+        uint4* z = (uint4*)(ghist + s0 * HH_BPS);  // 16-byte aligned: HH_BPS words per segment
+        for (uint32_t q = 0; q < nbin / 4; ++q) z[q] = make_uint4(0, 0, 0, 0);
+      } else {
+        atomicOr(&a.ctr[HPC_ERR], 4ull);
+      }
+    }
   }
 }
 
-__global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __restrict__ heavy,
-                                                    const uint32_t* __restrict__ nheavy,
-                                                    const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
-                                                    const uint32_t* __restrict__ hr_shift,
-                                                    const uint64_t* __restrict__ bbase, const uint32_t* __restrict__ bcnt,
-                                                    const uint64_t* __restrict__ boff, const uint32_t* __restrict__ sw,
-                                                    int tl, HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
+// One workgroup per segment (grid-stride): its heavy bucket by binary search of
+// the segments' starts, its wedges binned in LDS, the bins added to the bucket's.
+__global__ __launch_bounds__(HH_NT) void k_hh_hist(HpArgs a, const HhHeavy* __restrict__ heavy,
+                                                   const unsigned long long* __restrict__ hctr, uint64_t hcap,
+                                                   const uint64_t* __restrict__ boff, const uint32_t* __restrict__ sw,
+                                                   uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s_h[HH_FINE];
+  const int t = threadIdx.x, lane = lane_id();
+  const uint64_t pk = *hctr;
+  const uint64_t nh = (pk >> HH_HSH) < hcap ? (pk >> HH_HSH) : hcap, ns = pk & ((1ull << HH_HSH) - 1);
+  for (uint64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    uint64_t lo = 0, hi = nh;  // the last heavy bucket with seg0 <= s (uniform: every thread the same loads)
+    while (hi - lo > 1) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (heavy[m].seg0 <= s) lo = m; else hi = m;
+    }
+    if (nh == 0) break;
+    const HhHeavy hb = heavy[lo];
+    const uint64_t i0 = (s - hb.seg0) * HH_SEG;
+    if (i0 >= hb.n) continue;  // a segment of a bucket past hcap (HPC_ERR raised)
+    const uint64_t i1 = i0 + HH_SEG < hb.n ? i0 + HH_SEG : hb.n;
+    for (uint32_t f = t; f < hb.nbin; f += HH_NT) s_h[f] = 0;
+    __syncthreads();
+    const uint32_t* src = sw + boff[hb.gb];
+    for (uint64_t j0 = i0; j0 < i1; j0 += (uint64_t)HH_NT * HP_UN) {
+      uint32_t x[HP_UN];
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * HH_NT + t;
+        x[q] = src[j < i1 ? j : i0];
+      }
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        // consecutive wedges of a sorted list fall in runs of equal bins: one LDS atomic per run
+        const uint64_t j = j0 + (uint64_t)q * HH_NT + t;
+        const uint32_t b = j < i1 ? (uint32_t)(((uint64_t)x[q] - hb.lo) >> hb.fsh) : HH_NOB;
+        const uint32_t pb = __shfl_up(b, 1, 64);
+        const bool head = lane == 0 || pb != b;
+        const uint64_t ch = __ballot(head);
+        if (b != HH_NOB && head) {
+          const uint64_t rest = lane < 63 ? ch >> (lane + 1) : 0ull;
+          atomicAdd(&s_h[b], rest ? (uint32_t)__builtin_ctzll(rest) + 1u : 64u - (uint32_t)lane);
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t* gh = ghist + hb.seg0 * HH_BPS;
+    for (uint32_t f = t; f < hb.nbin; f += HH_NT)
+      if (s_h[f]) atomicAdd(&gh[f], s_h[f]);
+    __syncthreads();
+  }
+}
+
+// One workgroup per heavy bucket (grid-stride): its bins into LDS, grouped
+// greedily by one thread into ranges of distinct-w bound (wcap: wedges) <= half.
+__global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __restrict__ heavy,
+                                                    const unsigned long long* __restrict__ hctr, uint64_t hcap,
+                                                    const uint32_t* __restrict__ ghist, int tl,
+                                                    HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
                                                     uint64_t cap, uint32_t wcap) {
   __shared__ uint32_t s_h[HH_FINE];
   const int t = threadIdx.x;
-  const uint32_t nh = *nheavy;
-  const uint64_t th = 1ull << (tl - 1);        // distinct w per table
-  const uint64_t half = wcap ? wcap : th;      // wedges per group
-  for (uint32_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
-    const uint32_t gb = heavy[hi];
-    const uint32_t n = bcnt[gb];
-    const uint64_t off = boff[gb];
-    const uint32_t r = brow[gb];
-    uint64_t lo;
-    const uint64_t width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
-    const uint64_t fw = (width + HH_FINE - 1) / HH_FINE;
-    for (uint32_t f = t; f < HH_FINE; f += HH_NT) s_h[f] = 0;
+  const uint64_t pk = *hctr;
+  const uint64_t nh = (pk >> HH_HSH) < hcap ? (pk >> HH_HSH) : hcap;
+  const uint64_t th = 1ull << (tl - 1);    // distinct w per table
+  const uint64_t half = wcap ? wcap : th;  // per group: wedges (sort mode), else the distinct bound
+  for (uint64_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
+    const HhHeavy hb = heavy[hi];
+    const uint32_t* gh = ghist + hb.seg0 * HH_BPS;
+    for (uint32_t f = t; f < hb.nbin; f += HH_NT) s_h[f] = gh[f];
     __syncthreads();
-    hp_stream(sw + off, n, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t w) { atomicAdd(&s_h[(w - lo) / fw], 1u); });
-    __syncthreads();
-    if (t == 0) {  // greedy grouping of consecutive fine ranges (a few thousand LDS reads)
+    if (t == 0) {  // a few thousand LDS reads
+      // bins of width 2^fsh from lo cover the bucket, the last ones clipped to its end
+      const uint64_t lo = hb.lo, end = hb.hi;
+      auto rlo = [&](uint64_t f) { return lo + (f << hb.fsh) < end ? lo + (f << hb.fsh) : end; };
+      auto bound = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
+        const uint64_t span = rlo(f1) - rlo(f0);
+        return wcap ? cnt : (cnt < span ? cnt : span);
+      };
       auto emit = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
-        const uint64_t slo = lo + f0 * fw, shi = lo + f1 * fw < lo + width ? lo + f1 * fw : lo + width;
+        const uint64_t slo = rlo(f0), shi = rlo(f1);
         if (slo >= shi) return;
-        const uint64_t span = shi - slo;
-        const uint64_t dist = cnt < span ? cnt : span;
-        if (wcap ? cnt <= wcap : dist <= th) {
-          const uint32_t i = atomicAdd(nitems, 1u);
-          if (i < cap) items[i] = HhItem{gb, (uint32_t)dist, slo, shi};
-          else atomicOr(&a.ctr[HPC_ERR], 4ull);
-          return;
-        }
-        for (uint64_t x = slo; x < shi; x += th) {  // one fine range beyond the table: by width
-          const uint64_t x1 = x + th < shi ? x + th : shi;
-          const uint32_t i = atomicAdd(nitems, 1u);
-          if (i < cap) items[i] = HhItem{gb, (uint32_t)(x1 - x) | (wcap ? HH_BIG : 0u), x, x1};
-          else atomicOr(&a.ctr[HPC_ERR], 4ull);
-        }
+        const uint64_t span = shi - slo, dist = cnt < span ? cnt : span;
+        uint32_t c;
+        if (wcap ? cnt <= wcap : dist <= th) c = (uint32_t)dist;
+        else if (dist <= th) c = (uint32_t)dist | HH_BIG;                       // sort mode: by hash
+        else c = (uint32_t)th | HH_WIDE | (wcap ? HH_BIG : 0u);                // by width sub-ranges
+        const uint32_t i = atomicAdd(nitems, 1u);
+        if (i < cap) items[i] = HhItem{hb.gb, c, slo, shi};
+        else atomicOr(&a.ctr[HPC_ERR], 4ull);
       };
       uint64_t acc = 0, g0 = 0;
-      for (uint32_t f = 0; f < HH_FINE; ++f) {
+      for (uint32_t f = 0; f < hb.nbin; ++f) {
         const uint64_t c = s_h[f];
-        if (c > half) {
+        if (bound(f, f + 1, c) > half) {  // a bin beyond a group on its own
           if (acc) emit(g0, f, acc);
           emit(f, f + 1, c);
           acc = 0;
           g0 = f + 1;
-        } else if (acc + c > half) {
+        } else if (bound(g0, f + 1, acc + c) > half) {
           emit(g0, f, acc);
           acc = c;
           g0 = f;
@@ -2960,7 +3044,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_split(HpArgs a, const uint32_t* __
           acc += c;
         }
       }
-      if (acc) emit(g0, HH_FINE, acc);
+      if (acc) emit(g0, hb.nbin, acc);
     }
     __syncthreads();
   }
@@ -3131,36 +3215,42 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       __syncthreads();
       continue;
     }
-    const uint32_t dcnt = item.cnt & ~HH_BIG;
+    const uint32_t dcnt = item.cnt & HH_CNT;
     const int lg = max(6, log2_ceil(2 * (uint64_t)dcnt));
     const uint32_t T = 1u << (lg < TL ? lg : TL), mask = T - 1;
     const int hs = 32 - (lg < TL ? lg : TL);
-    for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
-      uint32_t wq[HP_UN], vq[HP_UN];
+    // an HH_WIDE item: sub-ranges of dcnt w, each through the table
+    const uint64_t step = (item.cnt & HH_WIDE) ? dcnt : shi - slo;
+    for (uint64_t xlo = slo; xlo < shi; xlo += step) {
+      const uint64_t xhi = shi - xlo > step ? xlo + step : shi;
+      const bool all = whole && step == shi - slo;
+      for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+        uint32_t wq[HP_UN], vq[HP_UN];
 #pragma unroll
-      for (int k = 0; k < HP_UN; ++k) {
-        const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
-        const uint64_t p = off + (i < n ? i : 0u);
-        wq[k] = sw[p];
-        vq[k] = CUSTOM ? sv[p] : 0u;
-      }
+        for (int k = 0; k < HP_UN; ++k) {
+          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+          const uint64_t p = off + (i < n ? i : 0u);
+          wq[k] = sw[p];
+          vq[k] = CUSTOM ? sv[p] : 0u;
+        }
 #pragma unroll
-      for (int k = 0; k < HP_UN; ++k) {
-        const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
-        if (i < n && (whole || ((uint64_t)wq[k] >= slo && (uint64_t)wq[k] < shi))) {
-          ++wedges;
-          hp_insert<false, CUSTOM>(tb, mask, hs, wq[k], vq[k], &a.ctr[HPC_ERR]);
+        for (int k = 0; k < HP_UN; ++k) {
+          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+          if (i < n && (all || ((uint64_t)wq[k] >= xlo && (uint64_t)wq[k] < xhi))) {
+            ++wedges;
+            hp_insert<false, CUSTOM>(tb, mask, hs, wq[k], vq[k], &a.ctr[HPC_ERR]);
+          }
         }
       }
+      __syncthreads();
+      // first-order exclusion: the entries of N(u) in [xlo, xhi)
+      hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
+        if ((uint64_t)x >= xlo && (uint64_t)x < xhi) hp_mark<false>(tb, mask, hs, x);
+      });
+      __syncthreads();
+      hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
+      __syncthreads();
     }
-    __syncthreads();
-    // first-order exclusion: the entries of N(u) in [slo, shi)
-    hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
-      if ((uint64_t)x >= slo && (uint64_t)x < shi) hp_mark<false>(tb, mask, hs, x);
-    });
-    __syncthreads();
-    hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
-    __syncthreads();
   }
   hp_finish(sg, a, wedges);
 }

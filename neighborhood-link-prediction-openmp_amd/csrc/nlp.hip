@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -283,6 +283,7 @@ struct nlp_graph {
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
+  bool hh_stats = false;     // NLP_HH_STATS=1: per chunk, the hub items' scratch reads on stderr (debug)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
   int hp_hub_min = 2;        // lowest bin the hub pass takes (NLP_HASH_HUB_MIN=1: bin 1 too)
@@ -752,6 +753,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
+  if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
   if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
@@ -1692,24 +1694,36 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)ibase,
                        (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)boff, bcur, sw, sv);
   TRY(hipGetLastError());
-  // accumulation items (k_hh_plan, k_hh_split): a bucket, or a w-range of a heavy bucket
+  // accumulation items (k_hh_plan, k_hh_group): a bucket, or a w-range of a heavy bucket
   const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
   // AA / RA: sort-mode items (at most HH_SCAP wedges each, keys need w, v < 2^26)
   const uint32_t wcap = custom && g->hh_sort && g->span <= (1ull << 26) ? g->hh_scap : 0u;
-  // items: at most NB whole buckets, per heavy bucket 2 n / half + 1 groups, and
-  // per fine range beyond half at most 8 width pieces (fine width <= 2^26 / 4096)
+  // heavy buckets hold more than `half` wedges each; their groups close past
+  // `half` wedges, so a heavy bucket of n wedges gives at most 2 n / half + 2
+  // items (single bins beyond a group included)
   const uint64_t half = wcap ? wcap : (1ull << (tl - 1));
-  const uint64_t cap = 3 * NB + 10 * (tot / half) + 1024;
+  const uint64_t hcap = tot / half + 1;
+  const uint64_t cap = NB + 4 * (tot / half) + 2 * hcap + 1024;
+  const uint64_t gwords = HH_BPS * (tot / HH_SEG + hcap + 1);  // bins: HH_BPS per segment
   HhItem* items;
-  uint32_t* heavy = bcur;  // the cursors are done with
-  uint32_t* nitems = queue + 1;  // and queue + 2: the heavy count
+  uint64_t* hv;  // the packed heavy counter, then the heavy buckets
+  uint64_t* gh;
   TRY(wsget(ws, B_HH_SITEM, cap * sizeof(HhItem) / 8 + 1, (uint64_t**)&items));
-  TRY(hipMemsetAsync(queue, 0, 12, st));
+  TRY(wsget(ws, B_HH_HEAVY, 1 + hcap * sizeof(HhHeavy) / 8, &hv));
+  TRY(wsget(ws, B_HH_GHIST, gwords / 2 + 2, &gh));
+  HhHeavy* heavy = (HhHeavy*)(hv + 1);
+  unsigned long long* hctr = (unsigned long long*)hv;
+  uint32_t* nitems = queue + 1;
+  TRY(hipMemsetAsync(queue, 0, 8, st));
+  TRY(hipMemsetAsync(hv, 0, 8, st));
   LAUNCH(k_hh_plan, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
-         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, queue + 2, wcap);
-  hipLaunchKernelGGL(k_hh_split, dim3(512), dim3(HH_NT), 0, st, a, (const uint32_t*)heavy, (const uint32_t*)(queue + 2),
-                     (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint64_t*)bbase,
-                     (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint32_t*)sw, tl, items, nitems, cap, wcap);
+         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, hctr, hcap, (uint32_t*)gh, wcap);
+  hipLaunchKernelGGL(k_hh_hist, dim3((unsigned)std::min<uint64_t>(tot / HH_SEG + hcap, 4096)), dim3(HH_NT), 0, st, a,
+                     (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint64_t*)boff,
+                     (const uint32_t*)sw, (uint32_t*)gh);
+  hipLaunchKernelGGL(k_hh_group, dim3((unsigned)std::min<uint64_t>(hcap, 1024)), dim3(HH_NT), 0, st, a,
+                     (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint32_t*)gh, tl, items,
+                     nitems, cap, wcap);
   TRY(hipGetLastError());
   const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
   if (custom)
@@ -1725,6 +1739,31 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
                        (const uint32_t*)sv, queue, 0, cap);
   TRY(hipGetLastError());
+  if (g->hh_stats) {  // debug: how often the accumulation items stream their buckets
+    TRY(hipStreamSynchronize(st));
+    uint32_t ni = 0;
+    unsigned long long hc = 0;
+    TRY(hipMemcpy(&ni, nitems, 4, hipMemcpyDeviceToHost));
+    TRY(hipMemcpy(&hc, hctr, 8, hipMemcpyDeviceToHost));
+    ni = (uint32_t)std::min<uint64_t>(ni, cap);
+    std::vector<HhItem> it(ni);
+    std::vector<uint32_t> bn(NB);
+    TRY(hipMemcpy(it.data(), items, ni * sizeof(HhItem), hipMemcpyDeviceToHost));
+    TRY(hipMemcpy(bn.data(), bcnt, NB * 4, hipMemcpyDeviceToHost));
+    uint64_t rd = 0, big = 0, wide = 0, mx = 0, sortw = 0;
+    for (const HhItem& x : it) {
+      rd += bn[x.gb];
+      mx = std::max<uint64_t>(mx, bn[x.gb]);
+      big += (x.cnt & HH_BIG) != 0;
+      wide += (x.cnt & HH_WIDE) != 0;
+      if (!(x.cnt & HH_BIG) && wcap) sortw += bn[x.gb];
+    }
+    fprintf(stderr, "[hh] rows %llu buckets %llu wedges %llu heavy %llu segs %llu items %u (big %llu wide %llu) "
+            "scratch reads %llu (x%.2f) max bucket %llu sort-mode reads %llu\n",
+            (unsigned long long)nh, (unsigned long long)NB, (unsigned long long)tot, hc >> HH_HSH,
+            hc & ((1ull << HH_HSH) - 1), ni, (unsigned long long)big, (unsigned long long)wide,
+            (unsigned long long)rd, tot ? (double)rd / tot : 0.0, (unsigned long long)mx, (unsigned long long)sortw);
+  }
   *done = true;
   return NLP_OK;
 }
@@ -4141,6 +4180,36 @@ nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_
   return NLP_OK;
 }
 
+}  // extern "C"
+
+// A replica of `src`'s CSR on `device`, copied device to device (peer copies
+// over xGMI between GPUs), then the per-graph build of finish_graph.
+static nlp_status graph_create_peer(const nlp_graph* src, int device, nlp_graph** out) {
+  *out = nullptr;
+  nlp_graph* g;
+  nlp_status s = new_graph(device, &g);
+  if (s != NLP_OK) return s;
+  g->span = src->span;
+  g->nnz = src->nnz;
+  if (hipMalloc(&g->off, (g->span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(g->nnz, 1) * 4) != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_NOMEM;
+  }
+  if (hipSetDevice(src->device) != hipSuccess || hipStreamSynchronize(src->stream) != hipSuccess ||
+      hipSetDevice(device) != hipSuccess ||
+      hipMemcpyPeerAsync(g->off, device, src->off, src->device, (g->span + 1) * 8, g->stream) != hipSuccess ||
+      (g->nnz && hipMemcpyPeerAsync(g->keys, device, src->keys, src->device, g->nnz * 4, g->stream) != hipSuccess)) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g);
+  if (s != NLP_OK) { destroy_graph(g); return s; }
+  *out = g;
+  return NLP_OK;
+}
+
+extern "C" {
+
 nlp_status nlp_graph_create_multi(const uint64_t* offsets, const uint32_t* keys, uint64_t span, const int* devices,
                                   int ndev, nlp_graph** out) {
   if (!out || !offsets || !devices || ndev < 1 || ndev > NLP_MAX_PARTS || span == 0 || span > 0xffffffffull)
@@ -4156,25 +4225,32 @@ nlp_status nlp_graph_create_multi(const uint64_t* offsets, const uint32_t* keys,
   if (!g) return NLP_ERR_NOMEM;
   g->is_group = true;
   g->device = devices[0];
-  std::vector<int> devs;  // distinct devices, in order of first appearance
+  // distinct devices, in order of first appearance (NLP_MULTI_EACH=1: one
+  // member per partition even on a repeated device -- exercises the
+  // member-to-member copy on a one-GPU box)
+  const char* each = getenv("NLP_MULTI_EACH");
+  const bool own = each && atoi(each) > 0;
+  std::vector<int> devs;
   for (int i = 0; i < ndev; ++i) {
-    int mi = (int)(std::find(devs.begin(), devs.end(), devices[i]) - devs.begin());
+    int mi = own ? (int)devs.size() : (int)(std::find(devs.begin(), devs.end(), devices[i]) - devs.begin());
     if (mi == (int)devs.size()) devs.push_back(devices[i]);
     g->part_member.push_back(mi);
   }
-  for (int d : devs) {
-    nlp_graph* m = nullptr;
-    nlp_status s = nlp_graph_create(offsets, keys, span, d, &m);
-    if (s != NLP_OK) { destroy_graph(g); return s; }
-    g->members.push_back(m);
-  }
-  for (size_t a = 0; a < devs.size(); ++a)  // peer access for the share copies (xGMI); copies work without it
+  for (size_t a = 0; a < devs.size(); ++a)  // peer access (xGMI) for the replica copies and the share copies
     for (size_t b = 0; b < devs.size(); ++b)
-      if (a != b && hipSetDevice(devs[a]) == hipSuccess) {
+      if (devs[a] != devs[b] && hipSetDevice(devs[a]) == hipSuccess) {
         int can = 0;
         if (hipDeviceCanAccessPeer(&can, devs[a], devs[b]) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(devs[b], 0);
         (void)hipGetLastError();
       }
+  // the host CSR crosses PCIe once, to the first device; the other replicas
+  // are copied device to device from it (xGMI peer copies)
+  for (size_t i = 0; i < devs.size(); ++i) {
+    nlp_graph* m = nullptr;
+    nlp_status s = i == 0 ? nlp_graph_create(offsets, keys, span, devs[0], &m) : graph_create_peer(g->members[0], devs[i], &m);
+    if (s != NLP_OK) { destroy_graph(g); return s; }
+    g->members.push_back(m);
+  }
   g->part_buf.assign(ndev, nullptr);
   g->part_cap.assign(ndev, 0);
   g->part_hist.assign(ndev, nullptr);

@@ -76,3 +76,17 @@ def test_gpu_cpp_header_on_partitions(gpu, golden, oracle, tmp_path):
         u, w, s = oracle.read_edges(pre + "." + str(m))
         eu, ew, es, _ = oracle.predict(g["offsets"], g["keys"], m, 4, max_edges=k)
         assert_canonical_equal(eu, ew, es, u, w, s)
+
+
+def test_gpu_partitions_replicas_copied_device_to_device(gpu, oracle, golden, monkeypatch):
+    """NLP_MULTI_EACH=1: one member graph per partition even on a repeated
+    device, so members 1.. are built from member 0's CSR by the device-to-device
+    (peer) copy that an 8-GPU handle uses instead of one PCIe upload per GPU."""
+    monkeypatch.setenv("NLP_MULTI_EACH", "1")
+    g = golden["g3k"]
+    off, keys, k = g["offsets"], g["keys"], int(g["k"][0])
+    with gpu.Graph(off, keys, devices=[0, 0, 0]) as G:
+        for m, H in ((1, 4), (0, 0), (8, 16)):
+            u, w, s, _ = G.predict(m, H, k)
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
