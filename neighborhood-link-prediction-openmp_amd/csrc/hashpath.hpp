@@ -1994,7 +1994,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     // drain: every entry scored for its own row (a list of the claimed slots
     // instead of this scan measured slower: the claims cost more in the insert
     // loop than the scan of empty slots)
-    const uint32_t Ts = __builtin_amdgcn_readfirstlane(T);
+    const uint32_t Ts = (a.xp & 8) ? 0u : __builtin_amdgcn_readfirstlane(T);  // xp 8 (with 4): no drain scan
     for (uint32_t i0 = 0; i0 < Ts; i0 += 64 * UN) {
       uint32_t kq[UN], c[UN], v0[UN], v1[UN], dw[UN];
       const uint32_t nq = min((uint32_t)UN, (Ts - i0) / 64);  // T: a power of two >= 64
@@ -2849,19 +2849,29 @@ __global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, uint64_t nh, const 
 // single bin beyond that is one HH_WIDE item, accumulated in width sub-ranges
 // of T / 2 by k_hh_accum.  The items of a heavy bucket run on different
 // workgroups, each streaming the bucket's scratch and keeping its own w-range.
+// Counts (every metric but AA / RA): a range no wider than dw (HH_DW) counts
+// directly -- LDS counter [w - lo], one atomic add per wedge, no probing --
+// when dense (wedges >= width / 4) or beyond the table's distinct bound; so a
+// hub row's dense first buckets are single items.
 // AA / RA sort mode (wcap = HH_SCAP): items hold at most HH_SCAP wedges, which
 // k_hh_accum sorts by (w, v) in LDS and sums run by run in ascending v; a single
 // bin beyond HH_SCAP wedges is flagged HH_BIG (hash table with the ordered
 // re-walk of hp_ordered_sum).
 struct HhItem {
-  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG | HH_WIDE)
+  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG | HH_WIDE | HH_DIRECT | HH_PART)
   uint64_t slo, shi;  // w-range
+  uint64_t off;       // HH_PART: the item's wedges in the partitioned scratch [off, off + n)
+  uint32_t n, pad;
 };
 constexpr uint32_t HH_FINE = 4096;
 constexpr uint32_t HH_SCAP = 4096;         // sort-mode wedges per item (32 KB of u64 keys)
 constexpr uint32_t HH_BIG = 0x80000000u;
 constexpr uint32_t HH_WIDE = 0x40000000u;  // the range is accumulated in sub-ranges of cnt w
-constexpr uint32_t HH_CNT = 0x3fffffffu;
+constexpr uint32_t HH_DIRECT = 0x20000000u;  // counts (no AA / RA) indexed by w - lo in LDS, no hashing
+constexpr uint32_t HH_PART = 0x10000000u;    // a heavy bucket's item: its own wedges, partitioned by k_hh_part
+constexpr uint32_t HH_CNT = 0x0fffffffu;
+constexpr uint32_t HH_DW = 16384;          // direct counters per range (the two words of the 8192-entry table)
+constexpr uint32_t HH_DMARK = 0x80000000u;  // direct counter: w is in N(u)
 constexpr uint64_t HH_SEG = 65536;         // heavy scratch wedges per histogram segment
 constexpr uint32_t HH_BPS = 512;           // histogram bins per segment
 constexpr int HH_HSH = 40;                 // packed heavy counter: count << 40 | segments
@@ -2891,6 +2901,15 @@ __device__ __forceinline__ uint32_t hh_wave_append(bool want, uint32_t* ctr) {
   return base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1));
 }
 
+// The item word of a range of `span` w holding `cnt` wedges (counts mode, dw >
+// 0 enables direct counting): 0 when neither the table nor direct counters fit.
+__device__ __forceinline__ uint32_t hh_count_item(uint64_t cnt, uint64_t span, uint64_t th, uint32_t dw) {
+  const uint64_t dist = cnt < span ? cnt : span;
+  if (span <= dw && (dist > th || 4 * cnt >= span)) return (uint32_t)dist | HH_DIRECT;
+  if (dist <= th) return (uint32_t)dist;
+  return 0u;
+}
+
 // wcap > 0 (AA / RA sort mode, see k_hh_accum): items are bounded by their
 // wedge count (<= wcap) instead of their distinct-w bound.  Heavy buckets go to
 // heavy[] (at most hcap: host bound tot / half + 1) with their bins zeroed.
@@ -2899,8 +2918,9 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
                           const uint32_t* __restrict__ bcnt, int tl, HhItem* __restrict__ items,
                           uint32_t* __restrict__ nitems, HhHeavy* __restrict__ heavy,
                           unsigned long long* __restrict__ hctr, uint64_t hcap, uint32_t* __restrict__ ghist,
-                          uint32_t wcap) {
+                          uint32_t wcap, uint32_t dw) {
   const int lane = lane_id();
+  const uint64_t th = 1ull << (tl - 1);
   for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t gb = b0 + threadIdx.x;
     uint32_t n = 0;
@@ -2911,9 +2931,10 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
       width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
     }
     const uint64_t dist = (uint64_t)n < width ? (uint64_t)n : width;
-    const bool simple = n > 0 && (wcap ? n <= wcap : 2 * dist <= (1ull << tl)), hv = n > 0 && !simple;
+    const uint32_t ci = wcap ? (n <= wcap ? (uint32_t)dist : 0u) : hh_count_item(n, width, th, dw);
+    const bool simple = n > 0 && ci != 0, hv = n > 0 && !simple;
     const uint32_t i = hh_wave_append(simple, nitems);
-    if (simple) items[i] = HhItem{(uint32_t)gb, (uint32_t)dist, lo, lo + width};  // i < nb <= the item capacity
+    if (simple) items[i] = HhItem{(uint32_t)gb, ci, lo, lo + width, 0ull, 0u, 0u};  // i < nb <= the item capacity
     const uint64_t nseg = hv ? (n + HH_SEG - 1) / HH_SEG : 0;
     const uint64_t pk = hv ? (1ull << HH_HSH) | nseg : 0ull;
     const uint64_t inc = wave_incl_scan(pk), wt = __shfl(inc, 63, 64);
@@ -2990,61 +3011,152 @@ __global__ __launch_bounds__(HH_NT) void k_hh_hist(HpArgs a, const HhHeavy* __re
 }
 
 // One workgroup per heavy bucket (grid-stride): its bins into LDS, grouped
-// greedily by one thread into ranges of distinct-w bound (wcap: wedges) <= half.
+// greedily by one thread into the widest consecutive ranges that are one item
+// each (wcap: at most wcap wedges; counts: hh_count_item).  A first walk counts
+// the groups, one atomic reserves their items contiguously, a second walk
+// writes them: item g of the bucket holds its wedges at [boff + pre_g, +cnt_g)
+// of the partitioned scratch.  The bins are overwritten by their item index
+// (HH_NOB: none) and the cursors (HH_BPS words per segment past the bins) set
+// to pre_g for k_hh_part.
 __global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __restrict__ heavy,
                                                     const unsigned long long* __restrict__ hctr, uint64_t hcap,
-                                                    const uint32_t* __restrict__ ghist, int tl,
+                                                    uint32_t* __restrict__ ghist, uint32_t* __restrict__ gcur,
+                                                    const uint64_t* __restrict__ boff, int tl,
                                                     HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
-                                                    uint64_t cap, uint32_t wcap) {
+                                                    uint64_t cap, uint32_t wcap, uint32_t dw) {
   __shared__ uint32_t s_h[HH_FINE];
+  __shared__ uint32_t s_base;
   const int t = threadIdx.x;
   const uint64_t pk = *hctr;
   const uint64_t nh = (pk >> HH_HSH) < hcap ? (pk >> HH_HSH) : hcap;
-  const uint64_t th = 1ull << (tl - 1);    // distinct w per table
-  const uint64_t half = wcap ? wcap : th;  // per group: wedges (sort mode), else the distinct bound
+  const uint64_t th = 1ull << (tl - 1);  // distinct w per table
   for (uint64_t hi = blockIdx.x; hi < nh; hi += gridDim.x) {
     const HhHeavy hb = heavy[hi];
-    const uint32_t* gh = ghist + hb.seg0 * HH_BPS;
+    uint32_t* gh = ghist + hb.seg0 * HH_BPS;
+    uint32_t* gc = gcur + hb.seg0 * HH_BPS;
     for (uint32_t f = t; f < hb.nbin; f += HH_NT) s_h[f] = gh[f];
     __syncthreads();
-    if (t == 0) {  // a few thousand LDS reads
+    if (t == 0) {  // a few thousand LDS reads per walk
       // bins of width 2^fsh from lo cover the bucket, the last ones clipped to its end
       const uint64_t lo = hb.lo, end = hb.hi;
       auto rlo = [&](uint64_t f) { return lo + (f << hb.fsh) < end ? lo + (f << hb.fsh) : end; };
-      auto bound = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
-        const uint64_t span = rlo(f1) - rlo(f0);
-        return wcap ? cnt : (cnt < span ? cnt : span);
+      // a range is fine as one item: sort mode by its wedges, counts by hh_count_item
+      auto ok = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
+        return cnt == 0 || (wcap ? cnt <= wcap : hh_count_item(cnt, rlo(f1) - rlo(f0), th, dw) != 0);
       };
-      auto emit = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
-        const uint64_t slo = rlo(f0), shi = rlo(f1);
-        if (slo >= shi) return;
-        const uint64_t span = shi - slo, dist = cnt < span ? cnt : span;
-        uint32_t c;
-        if (wcap ? cnt <= wcap : dist <= th) c = (uint32_t)dist;
-        else if (dist <= th) c = (uint32_t)dist | HH_BIG;                       // sort mode: by hash
-        else c = (uint32_t)th | HH_WIDE | (wcap ? HH_BIG : 0u);                // by width sub-ranges
-        const uint32_t i = atomicAdd(nitems, 1u);
-        if (i < cap) items[i] = HhItem{hb.gb, c, slo, shi};
-        else atomicOr(&a.ctr[HPC_ERR], 4ull);
-      };
-      uint64_t acc = 0, g0 = 0;
-      for (uint32_t f = 0; f < hb.nbin; ++f) {
-        const uint64_t c = s_h[f];
-        if (bound(f, f + 1, c) > half) {  // a bin beyond a group on its own
-          if (acc) emit(g0, f, acc);
-          emit(f, f + 1, c);
-          acc = 0;
-          g0 = f + 1;
-        } else if (bound(g0, f + 1, acc + c) > half) {
-          emit(g0, f, acc);
-          acc = c;
-          g0 = f;
-        } else {
-          if (!acc && !c) g0 = f + 1;
-          acc += c;
+      uint32_t ng = 0;
+      uint64_t pre = 0;
+      // emit=false: count the groups; true: write item base + ng, its bins' map and its cursor
+      auto walk = [&](bool emit) {
+        auto group = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
+          if (emit) {
+            const uint64_t slo = rlo(f0), shi = rlo(f1);
+            const uint64_t span = shi - slo, dist = cnt < span ? cnt : span;
+            uint32_t c;
+            if (wcap) {
+              if (cnt <= wcap) c = (uint32_t)dist;
+              else if (dist <= th) c = (uint32_t)dist | HH_BIG;          // by hash, ordered re-walk
+              else c = (uint32_t)th | HH_WIDE | HH_BIG;                  // by width sub-ranges
+            } else {
+              c = hh_count_item(cnt, span, th, dw);
+              if (!c) c = dw ? dw | HH_WIDE | HH_DIRECT : (uint32_t)th | HH_WIDE;
+            }
+            const uint64_t i = (uint64_t)s_base + ng;
+            if (i < cap) items[i] = HhItem{hb.gb, c | HH_PART, slo, shi, boff[hb.gb] + pre, (uint32_t)cnt, 0u};
+            else atomicOr(&a.ctr[HPC_ERR], 4ull);
+            for (uint64_t f = f0; f < f1; ++f) s_h[f] = ng;  // walked already: the bin's count is consumed
+            gc[ng] = (uint32_t)pre;
+          }
+          pre += cnt;
+          ++ng;
+        };
+        uint64_t acc = 0, g0 = 0;
+        for (uint32_t f = 0; f < hb.nbin; ++f) {
+          const uint64_t c = (emit && f < g0) ? 0 : s_h[f];  // (emit: bins before g0 hold item indices now)
+          if (!ok(f, f + 1, c)) {  // a bin beyond a group on its own
+            if (acc) group(g0, f, acc);
+            group(f, f + 1, c);
+            acc = 0;
+            g0 = f + 1;
+          } else if (!ok(g0, f + 1, acc + c)) {
+            group(g0, f, acc);
+            acc = c;
+            g0 = f;
+          } else {
+            if (!acc && !c) {
+              if (emit) s_h[f] = HH_NOB;  // an empty bin before the group: no wedge maps here
+              g0 = f + 1;
+            }
+            acc += c;
+          }
         }
-      }
-      if (acc) emit(g0, hb.nbin, acc);
+        if (acc) group(g0, hb.nbin, acc);
+      };
+      walk(false);
+      s_base = atomicAdd(nitems, ng);
+      ng = 0;
+      pre = 0;
+      walk(true);
+    }
+    __syncthreads();
+    for (uint32_t f = t; f < hb.nbin; f += HH_NT) gh[f] = s_h[f];  // bin -> the bucket's item
+    __syncthreads();
+  }
+}
+
+// The heavy buckets' wedges partitioned by item (one workgroup per segment,
+// grid-stride): per item the segment's count in LDS, one global atomic per
+// item reserves the segment's run of the item's range, a second read of the
+// segment writes every wedge there (and v for AA / RA).  The order inside an
+// item is free: its wedges are summed per w (counts), sorted (sort mode) or
+// re-walked in N(u) order (HH_BIG).
+__global__ __launch_bounds__(HH_NT) void k_hh_part(HpArgs a, const HhHeavy* __restrict__ heavy,
+                                                   const unsigned long long* __restrict__ hctr, uint64_t hcap,
+                                                   const uint64_t* __restrict__ boff, const uint32_t* __restrict__ sw,
+                                                   const uint32_t* __restrict__ sv, const uint32_t* __restrict__ ghist,
+                                                   uint32_t* __restrict__ gcur, uint32_t* __restrict__ pw,
+                                                   uint32_t* __restrict__ pv) {
+  __shared__ uint32_t s_map[HH_FINE];
+  __shared__ uint32_t s_cnt[HH_FINE];
+  const int t = threadIdx.x;
+  const uint64_t pk = *hctr;
+  const uint64_t nh = (pk >> HH_HSH) < hcap ? (pk >> HH_HSH) : hcap, ns = pk & ((1ull << HH_HSH) - 1);
+  for (uint64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    uint64_t lo = 0, hi = nh;  // the last heavy bucket with seg0 <= s
+    while (hi - lo > 1) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (heavy[m].seg0 <= s) lo = m; else hi = m;
+    }
+    if (nh == 0) break;
+    const HhHeavy hb = heavy[lo];
+    const uint64_t i0 = (s - hb.seg0) * HH_SEG;
+    if (i0 >= hb.n) continue;
+    const uint64_t i1 = i0 + HH_SEG < hb.n ? i0 + HH_SEG : hb.n;
+    const uint32_t* gm = ghist + hb.seg0 * HH_BPS;
+    uint32_t* gc = gcur + hb.seg0 * HH_BPS;
+    for (uint32_t f = t; f < hb.nbin; f += HH_NT) {
+      s_map[f] = gm[f];
+      s_cnt[f] = 0;
+    }
+    __syncthreads();
+    const uint64_t bo = boff[hb.gb];
+    const uint32_t* src = sw + bo;
+    auto item_of = [&](uint32_t w) { return s_map[((uint64_t)w - hb.lo) >> hb.fsh]; };
+    for (uint64_t j = i0 + t; j < i1; j += HH_NT) {
+      const uint32_t g = item_of(src[j]);
+      if (g < hb.nbin) atomicAdd(&s_cnt[g], 1u);
+      else atomicOr(&a.ctr[HPC_ERR], 4ull);  // a wedge outside every item (never expected)
+    }
+    __syncthreads();
+    for (uint32_t g = t; g < hb.nbin; g += HH_NT)  // items <= bins
+      if (s_cnt[g]) s_cnt[g] = atomicAdd(&gc[g], s_cnt[g]);
+    __syncthreads();
+    for (uint64_t j = i0 + t; j < i1; j += HH_NT) {
+      const uint32_t w = src[j], g = item_of(w);
+      if (g >= hb.nbin) continue;
+      const uint64_t p = bo + atomicAdd(&s_cnt[g], 1u);
+      pw[p] = w;
+      if (pv) pv[p] = sv[bo + j];
     }
     __syncthreads();
   }
@@ -3085,15 +3197,18 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
                                                     const uint32_t* __restrict__ hr_p,
                                                     const uint64_t* __restrict__ bbase,
                                                     const uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
-                                                    const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw,
-                                                    const uint32_t* __restrict__ sv, uint32_t* __restrict__ queue,
+                                                    const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw0,
+                                                    const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ pw,
+                                                    const uint32_t* __restrict__ pv, uint32_t* __restrict__ queue,
                                                     int sortmode, uint64_t cap) {
   constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
   constexpr int LT = 1 << TL;
   constexpr int VT = CUSTOM ? LT : 1;
   static_assert(!CUSTOM || LT >= (int)HH_SCAP, "the sort buffer overlays the vmin / vmax words");
-  __shared__ uint32_t s_k[LT];
-  __shared__ uint32_t s_c[LT];
+  __shared__ uint32_t s_tab[2 * LT];  // keys | counts; or HH_DW direct counters
+  uint32_t* const s_k = s_tab;
+  uint32_t* const s_c = s_tab + LT;
+  static_assert(CUSTOM || 2 * LT >= (int)HH_DW, "direct counters overlay the table");
   __shared__ uint64_t s_vv[VT];  // vmin | vmax (2 x LT u32), or the sort-mode keys (LT u64)
   __shared__ uint8_t s_ex[CUSTOM ? HH_SCAP : 1];
   __shared__ uint32_t s_gu[HH_NW][HP_BSTG], s_gw[HH_NW][HP_BSTG];
@@ -3124,14 +3239,18 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     if (it >= ni) break;
     const HhItem item = items[it];
     const uint32_t gb = item.gb;
-    const uint32_t n = bcnt[gb];
+    // a heavy bucket's item reads its own partitioned wedges, all inside its range
+    const bool part = (item.cnt & HH_PART) != 0;
+    const uint32_t* const sw = part ? pw : sw0;
+    const uint32_t* const sv = part ? pv : sv0;
+    const uint32_t n = part ? item.n : bcnt[gb];
     const uint32_t r = brow[gb];
     const uint32_t u = hr_u[r];
     const uint64_t b = gb - bbase[r];
-    const uint64_t off = boff[gb];
+    const uint64_t off = part ? item.off : boff[gb];
     uint64_t lo;
     const uint64_t width = hh_bucket_range(a, u, hr_shift[r], b, &lo);
-    const bool whole = item.slo == lo && item.shi == lo + width;
+    const bool whole = part || (item.slo == lo && item.shi == lo + width);
     const uint64_t slo = item.slo, shi = item.shi;
     const uint64_t o1 = a.g.off[u + 1];
     const uint64_t du = o1 - a.g.off[u];
@@ -3213,6 +3332,54 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         s_v1[i] = 0;
       }
       __syncthreads();
+      continue;
+    }
+    if (!CUSTOM && (item.cnt & HH_DIRECT)) {
+      // direct counters over sub-ranges of at most HH_DW w (HH_WIDE: of the item's count word)
+      const uint64_t step = (item.cnt & HH_WIDE) ? (item.cnt & HH_CNT) : shi - slo;
+      for (uint64_t xlo = slo; xlo < shi; xlo += step) {
+        const uint64_t xhi = shi - xlo > step ? xlo + step : shi;
+        const uint32_t span = (uint32_t)(xhi - xlo);
+        const bool all = whole && step == shi - slo;
+        for (uint32_t i = t; i < span; i += HH_NT) s_tab[i] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+          uint32_t wq[HP_UN];
+#pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            wq[k] = sw[off + (i < n ? i : 0u)];
+          }
+#pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            if (i < n && (all || ((uint64_t)wq[k] >= xlo && (uint64_t)wq[k] < xhi))) {
+              ++wedges;
+              atomicAdd(&s_tab[(uint64_t)wq[k] - xlo], 1u);
+            }
+          }
+        }
+        __syncthreads();
+        // first-order exclusion: the entries of N(u) in [xlo, xhi) (a count stays: the entry is a candidate of count 0)
+        hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
+          if ((uint64_t)x >= xlo && (uint64_t)x < xhi) atomicOr(&s_tab[(uint64_t)x - xlo], HH_DMARK);
+        });
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < span; i0 += HH_NT) {  // uniform trip count: hp_emit is wave-collective
+          const uint32_t i = i0 + (uint32_t)t;
+          uint32_t c = 0;
+          if (i < span) {
+            c = s_tab[i];
+            s_tab[i] = i < (uint32_t)LT ? HP_EMPTY : 0u;  // the table's empty state again
+          }
+          const bool valid = (c & ~HH_DMARK) != 0;
+          const uint32_t w = (uint32_t)(xlo + i);
+          float sc = 0.0f;
+          if (valid) sc = score_basic(a.metric, (c & HH_DMARK) ? 0u : c, du, (uint64_t)a.g.deg[w]);
+          hp_emit(sg, a, valid, sc, u, w, tau);
+        }
+        __syncthreads();
+      }
       continue;
     }
     const uint32_t dcnt = item.cnt & HH_CNT;

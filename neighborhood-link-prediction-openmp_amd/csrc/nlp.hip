@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -283,6 +283,7 @@ struct nlp_graph {
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
+  uint32_t hh_dw = HH_DW;    // hub pass, counts: direct-counter range width (NLP_HH_DIRECT=0 off, small values test it)
   bool hh_stats = false;     // NLP_HH_STATS=1: per chunk, the hub items' scratch reads on stderr (debug)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
@@ -754,6 +755,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
+  if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
   if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
@@ -1701,6 +1703,7 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   // heavy buckets hold more than `half` wedges each; their groups close past
   // `half` wedges, so a heavy bucket of n wedges gives at most 2 n / half + 2
   // items (single bins beyond a group included)
+  const uint32_t dw = custom ? 0u : g->hh_dw;  // direct counters: counts only
   const uint64_t half = wcap ? wcap : (1ull << (tl - 1));
   const uint64_t hcap = tot / half + 1;
   const uint64_t cap = NB + 4 * (tot / half) + 2 * hcap + 1024;
@@ -1710,20 +1713,27 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   uint64_t* gh;
   TRY(wsget(ws, B_HH_SITEM, cap * sizeof(HhItem) / 8 + 1, (uint64_t**)&items));
   TRY(wsget(ws, B_HH_HEAVY, 1 + hcap * sizeof(HhHeavy) / 8, &hv));
-  TRY(wsget(ws, B_HH_GHIST, gwords / 2 + 2, &gh));
+  TRY(wsget(ws, B_HH_GHIST, gwords + 2, &gh));  // bins, then the item cursors
+  uint32_t* pw;  // the heavy buckets' wedges partitioned by item (and v for AA / RA): bucket offsets as in sw
+  TRY(wsget(ws, B_HH_PART, (custom ? 2 * tot : tot) + 2, &pw));
+  uint32_t* pv = custom ? pw + tot : nullptr;
+  uint32_t* gcur = (uint32_t*)gh + gwords;
   HhHeavy* heavy = (HhHeavy*)(hv + 1);
   unsigned long long* hctr = (unsigned long long*)hv;
   uint32_t* nitems = queue + 1;
   TRY(hipMemsetAsync(queue, 0, 8, st));
   TRY(hipMemsetAsync(hv, 0, 8, st));
   LAUNCH(k_hh_plan, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
-         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, hctr, hcap, (uint32_t*)gh, wcap);
+         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, hctr, hcap, (uint32_t*)gh, wcap, dw);
   hipLaunchKernelGGL(k_hh_hist, dim3((unsigned)std::min<uint64_t>(tot / HH_SEG + hcap, 4096)), dim3(HH_NT), 0, st, a,
                      (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint64_t*)boff,
                      (const uint32_t*)sw, (uint32_t*)gh);
   hipLaunchKernelGGL(k_hh_group, dim3((unsigned)std::min<uint64_t>(hcap, 1024)), dim3(HH_NT), 0, st, a,
-                     (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint32_t*)gh, tl, items,
-                     nitems, cap, wcap);
+                     (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (uint32_t*)gh, gcur,
+                     (const uint64_t*)boff, tl, items, nitems, cap, wcap, dw);
+  hipLaunchKernelGGL(k_hh_part, dim3((unsigned)std::min<uint64_t>(tot / HH_SEG + hcap, 4096)), dim3(HH_NT), 0, st, a,
+                     (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint64_t*)boff,
+                     (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)gh, gcur, pw, pv);
   TRY(hipGetLastError());
   const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
   if (custom)
@@ -1731,13 +1741,13 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue, (int)(wcap != 0), cap);
+                       (const uint32_t*)sv, (const uint32_t*)pw, (const uint32_t*)pv, queue, (int)(wcap != 0), cap);
   else
     hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
                        (const uint32_t*)nitems, (const uint32_t*)brow,
                        (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
                        (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, queue, 0, cap);
+                       (const uint32_t*)sv, (const uint32_t*)pw, (const uint32_t*)pv, queue, 0, cap);
   TRY(hipGetLastError());
   if (g->hh_stats) {  // debug: how often the accumulation items stream their buckets
     TRY(hipStreamSynchronize(st));
@@ -1750,19 +1760,22 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
     std::vector<uint32_t> bn(NB);
     TRY(hipMemcpy(it.data(), items, ni * sizeof(HhItem), hipMemcpyDeviceToHost));
     TRY(hipMemcpy(bn.data(), bcnt, NB * 4, hipMemcpyDeviceToHost));
-    uint64_t rd = 0, big = 0, wide = 0, mx = 0, sortw = 0;
+    uint64_t rd = 0, big = 0, wide = 0, mx = 0, sortw = 0, direct = 0;
     for (const HhItem& x : it) {
-      rd += bn[x.gb];
-      mx = std::max<uint64_t>(mx, bn[x.gb]);
+      const uint64_t xn = (x.cnt & HH_PART) ? x.n : bn[x.gb];
+      rd += xn;
+      direct += (x.cnt & HH_DIRECT) != 0;
+      mx = std::max<uint64_t>(mx, xn);
       big += (x.cnt & HH_BIG) != 0;
       wide += (x.cnt & HH_WIDE) != 0;
-      if (!(x.cnt & HH_BIG) && wcap) sortw += bn[x.gb];
+      if (!(x.cnt & HH_BIG) && wcap) sortw += xn;
     }
     fprintf(stderr, "[hh] rows %llu buckets %llu wedges %llu heavy %llu segs %llu items %u (big %llu wide %llu) "
-            "scratch reads %llu (x%.2f) max bucket %llu sort-mode reads %llu\n",
+            "scratch reads %llu (x%.2f) max bucket %llu sort-mode reads %llu direct items %llu\n",
             (unsigned long long)nh, (unsigned long long)NB, (unsigned long long)tot, hc >> HH_HSH,
             hc & ((1ull << HH_HSH) - 1), ni, (unsigned long long)big, (unsigned long long)wide,
-            (unsigned long long)rd, tot ? (double)rd / tot : 0.0, (unsigned long long)mx, (unsigned long long)sortw);
+            (unsigned long long)rd, tot ? (double)rd / tot : 0.0, (unsigned long long)mx, (unsigned long long)sortw,
+            (unsigned long long)direct);
   }
   *done = true;
   return NLP_OK;

@@ -415,9 +415,10 @@ class _env:
 # (sub-range passes), 5 bin 0 as one 1024-entry launch (no table-size tiers),
 # 6/7 k_hp_part rows sliced over several workgroups (bucket slices, exclusion
 # cursor per slice), 8 the edge-parallel work estimate, 9 a wave per bin-0 row,
-# 10 k_hp_part for every row, 11 hub pass with one w-bucket per row, 12 the
-# same with 128-entry item tables (heavy buckets split into w-range items by
-# their fine histogram), 13 bin-1 rows by the hub pass, 14 the hub pass's AA /
+# 10 k_hp_part for every row, 11 hub pass with one w-bucket per row (direct
+# counters for the counts), 12 the same with 128-entry item tables and no
+# direct counters (heavy buckets split into w-range items by their segment
+# histograms), 13 bin-1 rows by the hub pass, 14 the hub pass's AA /
 # RA items by the ordered re-walk instead of sort mode, 15/16 sort-mode items
 # of at most 16 / 40 wedges (heavy buckets split, single fine ranges beyond
 # flagged HH_BIG), 17 survivor lists from in-edge atomics (unordered: the AA /
@@ -428,7 +429,9 @@ class _env:
 # k_hp_dcls_one), 23 k_hp_dcls_one's output capacity overflowing (the
 # two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
 # above u), 25 the row batches' 4-loads / 3-waves build, 26 the row batches
-# reserving every flush (no emission windows, no padding)
+# reserving every flush (no emission windows, no padding), 27 hub pass with
+# one w-bucket per row and 64-wide direct counters (heavy buckets grouped into
+# direct ranges, single bins beyond by HH_WIDE sub-ranges)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -436,14 +439,15 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="0"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SORT="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"), dict(NLP_HASH_WIN="0")]
+                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"), dict(NLP_HASH_WIN="0"),
+                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
