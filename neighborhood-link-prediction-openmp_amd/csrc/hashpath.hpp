@@ -1404,7 +1404,8 @@ __host__ __device__ constexpr uint64_t hp_tier_w(int t) { return t == 0 ? 128 : 
 template <bool SCATTER>
 __global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ rows, uint64_t nrows,
                                                 const uint64_t* __restrict__ wu, uint64_t ua,
-                                                uint32_t* __restrict__ tcnt, uint32_t* __restrict__ out) {
+                                                uint32_t* __restrict__ tcnt, uint32_t* __restrict__ out,
+                                                uint64_t w0 = hp_tier_w(0), uint64_t w1 = hp_tier_w(1)) {
   __shared__ uint32_t s_n[NWAVE][HP_NTIER];
   __shared__ uint32_t s_base[HP_NTIER];
   const int lane = lane_id(), wv = wave_id();
@@ -1419,7 +1420,7 @@ __global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ row
     if (i < nrows) {
       u = rows[i];
       const uint64_t W = wu[u - ua];
-      t = W <= hp_tier_w(0) ? 0 : W <= hp_tier_w(1) ? 1 : 2;
+      t = W <= w0 ? 0 : W <= w1 ? 1 : 2;
     }
     uint64_t m[HP_NTIER];
 #pragma unroll
@@ -2252,6 +2253,130 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
   hp_finish(sg, a, wedges);
 }
 
+// ---------------------------------------------------------------- bin 1, count metrics: tiered rows
+// k_hp_block holds 110 KB of LDS (a 1024-thread workgroup, an 8192-entry
+// two-array table): one row in flight per CU, and a bin-1 row is a chain of
+// dependent loads (row bounds, survivor entries, N(v), N(u)).  Count metrics
+// with entry degrees take bin 1 here instead: a 256-thread workgroup per row
+// and a one-word table (key << 32 | count word, hp_insert_kd's layout with 13
+// count bits) sized by the row's tier -- W+ <= 1024: 2048 entries, <= 2048:
+// 4096, <= 4096: 8192 -- so five, three or two rows are in flight per CU.
+constexpr int HP_RNT = 256;
+constexpr uint64_t HP_RTIER0 = 1024, HP_RTIER1 = 2048;
+
+template <int LT>
+__global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __restrict__ tl,
+                                                    const uint32_t* __restrict__ tcnt, int tier,
+                                                    const uint64_t* __restrict__ wu, uint64_t ua,
+                                                    uint32_t* __restrict__ queue) {
+  constexpr int NW = HP_RNT / 64;
+  constexpr int TLG = LT == 2048 ? 11 : LT == 4096 ? 12 : 13;
+  static_assert((1 << TLG) == LT, "table sizes 2048, 4096, 8192");
+  __shared__ uint64_t s_t[LT];
+  __shared__ uint64_t s_incl[HP_RNT];
+  __shared__ uint64_t s_start[HP_RNT];
+  __shared__ uint32_t s_iv[HP_RNT];
+  __shared__ uint64_t s_w[NW];
+  __shared__ uint64_t s_tot, s_it;
+  __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ float s_gs[NW][HP_BSTG];
+  const int t = threadIdx.x, wv = wave_id();
+  uint32_t rbase, nrows;  // this tier's rows: a region of the tier list (k_hp_tier)
+  hb_region(tcnt, tier, tier, &rbase, &nrows);
+  const uint32_t* rows = tl + rbase;
+  if (nrows == 0) return;
+  for (int i = t; i < LT; i += HP_RNT) s_t[i] = HP_EMPTY64;
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  __syncthreads();
+  for (;;) {
+    if (t == 0) s_it = atomicAdd(queue, 1u);
+    __syncthreads();
+    const uint64_t ri = s_it;
+    __syncthreads();
+    if (ri >= nrows) break;
+    const uint32_t u = rows[ri];
+    const uint64_t W = wu[u - ua];
+    const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
+    const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
+    const int lg = max(6, log2_ceil(2 * (W < span_w ? W : span_w)));
+    if (lg > TLG) {  // a row beyond its tier (a binning bug): fail the call, never overrun LDS
+      if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+      continue;
+    }
+    const uint32_t T = 1u << lg, mask = T - 1;
+    const int shift = 32 - lg;
+    const uint32_t* fh;
+    uint64_t nf;
+    hp_first_hops(a, u, o0, du, &fh, &nf);
+    // packed survivor entries (the part of N(v) above u, no row-bound gather)
+    const uint64_t* fd = a.sdo && a.soff ? a.sdo + (fh - a.skeys) : nullptr;
+    for (uint64_t base = 0; base < nf; base += HP_RNT) {
+      const uint64_t i = base + t;
+      uint64_t len = 0, st = 0;
+      if (i < nf) {
+        if (fd) {
+          const uint64_t x = fd[i];
+          len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+          st = x & ((1ull << HP_SDO_SH) - 1);
+        } else {
+          const uint32_t v = fh[i], d = a.g.deg[v];
+          if (hp_surv(d, a.H)) {
+            len = d;
+            st = a.g.off[v];
+          }
+        }
+      }
+      const uint64_t incl = block_incl_scan_1024(len, s_w);
+      s_incl[t] = incl;
+      s_start[t] = st;
+      s_iv[t] = 0u;
+      if (t == HP_RNT - 1) s_tot = incl;
+      __syncthreads();
+      hp_wedges<HP_RNT, false, true>(s_tot, (uint32_t)t, (uint32_t)HP_RNT, s_incl, s_start, s_iv, a.g.keys,
+                                     [&](uint32_t w, uint32_t, uint32_t dw) {
+                                       if (w > u) {
+                                         ++wedges;
+                                         h64_insert<13>(s_t, mask, shift, w, dw, &a.ctr[HPC_ERR]);
+                                       }
+                                     }, a.kdeg);
+      __syncthreads();
+    }
+    // first-order exclusion: the entries of N(u) above u (a key <= u has no entry)
+    const uint32_t xu = a.xs ? a.xs[u] : 0u;
+    hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
+              [&](uint32_t x) { h64_mark(s_t, mask, shift, x); });
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < T; i0 += HP_RNT * HP_UN) {  // T >= 64: uniform per wave
+      uint32_t kq[HP_UN], c[HP_UN], dw[HP_UN];
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const uint32_t i = i0 + (uint32_t)q * HP_RNT + (uint32_t)t;
+        kq[q] = HP_EMPTY;
+        c[q] = 0;
+        if (i < T) {
+          const uint64_t x = s_t[i];
+          kq[q] = (uint32_t)(x >> 32);
+          c[q] = (uint32_t)x;
+          if (kq[q] != HP_EMPTY) s_t[i] = HP_EMPTY64;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) dw[q] = kq[q] != HP_EMPTY ? hp_kd_deg<13>(a.g, c[q], kq[q]) : 0u;
+#pragma unroll
+      for (int q = 0; q < HP_UN; ++q) {
+        const bool valid = kq[q] != HP_EMPTY;
+        float sc = 0.0f;
+        if (valid) sc = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & 8191u), du, (uint64_t)dw[q]);
+        hp_emit(sg, a, valid, sc, u, kq[q], tau);
+      }
+    }
+    __syncthreads();
+  }
+  hp_finish(sg, a, wedges);
+}
+
 // ---------------------------------------------------------------- bins 2-3: partitioned rows
 // A row whose wedges overflow an LDS table is cut into P w-buckets of width
 // 2^shift (P <= HP_PMAX).  Pass A counts the row's wedges per bucket (LDS
@@ -3011,22 +3136,29 @@ __global__ __launch_bounds__(HH_NT) void k_hh_hist(HpArgs a, const HhHeavy* __re
 }
 
 // One workgroup per heavy bucket (grid-stride): its bins into LDS, grouped
-// greedily by one thread into the widest consecutive ranges that are one item
-// each (wcap: at most wcap wedges; counts: hh_count_item).  A first walk counts
-// the groups, one atomic reserves their items contiguously, a second walk
-// writes them: item g of the bucket holds its wedges at [boff + pre_g, +cnt_g)
-// of the partitioned scratch.  The bins are overwritten by their item index
-// (HH_NOB: none) and the cursors (HH_BPS words per segment past the bins) set
-// to pre_g for k_hh_part.
+// greedily into the widest consecutive bin ranges that are one item each
+// (wcap: at most wcap wedges; counts: hh_count_item).  The greedy walk is wave
+// 0's, wave-uniform (a bin's count read from a register of 64 by readlane, the
+// walk's state scalar); it records each group's bin range and count in LDS.
+// Then the workgroup reserves the bucket's items contiguously, scans the
+// counts (item g holds its wedges at [boff + pre_g, + cnt_g) of the
+// partitioned scratch), writes the items, the cursors (HH_BPS words per
+// segment past the bins, set to pre_g for k_hh_part) and overwrites each bin
+// by its item.
 __global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __restrict__ heavy,
                                                     const unsigned long long* __restrict__ hctr, uint64_t hcap,
                                                     uint32_t* __restrict__ ghist, uint32_t* __restrict__ gcur,
                                                     const uint64_t* __restrict__ boff, int tl,
                                                     HhItem* __restrict__ items, uint32_t* __restrict__ nitems,
                                                     uint64_t cap, uint32_t wcap, uint32_t dw) {
+  static_assert(HH_NT == NT, "block_excl_scan spans NT threads");
+  constexpr int GPT = HH_FINE / HH_NT;  // groups per thread in the scan
   __shared__ uint32_t s_h[HH_FINE];
-  __shared__ uint32_t s_base;
-  const int t = threadIdx.x;
+  __shared__ uint32_t s_gr[HH_FINE];    // group: first bin | end bin << 16
+  __shared__ uint32_t s_gc[HH_FINE];    // group: wedges
+  __shared__ uint64_t s_scan[NWAVE + 1];
+  __shared__ uint32_t s_ng, s_base;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t pk = *hctr;
   const uint64_t nh = (pk >> HH_HSH) < hcap ? (pk >> HH_HSH) : hcap;
   const uint64_t th = 1ull << (tl - 1);  // distinct w per table
@@ -3034,45 +3166,43 @@ __global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __r
     const HhHeavy hb = heavy[hi];
     uint32_t* gh = ghist + hb.seg0 * HH_BPS;
     uint32_t* gc = gcur + hb.seg0 * HH_BPS;
-    for (uint32_t f = t; f < hb.nbin; f += HH_NT) s_h[f] = gh[f];
+    const uint32_t nbin = hb.nbin;
+    for (uint32_t f = t; f < nbin; f += HH_NT) s_h[f] = gh[f];
     __syncthreads();
-    if (t == 0) {  // a few thousand LDS reads per walk
-      // bins of width 2^fsh from lo cover the bucket, the last ones clipped to its end
-      const uint64_t lo = hb.lo, end = hb.hi;
-      auto rlo = [&](uint64_t f) { return lo + (f << hb.fsh) < end ? lo + (f << hb.fsh) : end; };
+    // bins of width 2^fsh from lo cover the bucket, the last ones clipped to its end
+    const uint64_t lo = hb.lo, end = hb.hi;
+    auto rlo = [&](uint64_t f) { return lo + (f << hb.fsh) < end ? lo + (f << hb.fsh) : end; };
+    auto item_word = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
+      const uint64_t span = rlo(f1) - rlo(f0), dist = cnt < span ? cnt : span;
+      if (wcap) {
+        if (cnt <= wcap) return (uint32_t)dist;
+        if (dist <= th) return (uint32_t)dist | HH_BIG;  // by hash, ordered re-walk
+        return (uint32_t)th | HH_WIDE | HH_BIG;          // by width sub-ranges
+      }
+      const uint32_t c = hh_count_item(cnt, span, th, dw);
+      return c ? c : (dw ? dw | HH_WIDE | HH_DIRECT : (uint32_t)th | HH_WIDE);
+    };
+    if (wv == 0) {
       // a range is fine as one item: sort mode by its wedges, counts by hh_count_item
       auto ok = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
         return cnt == 0 || (wcap ? cnt <= wcap : hh_count_item(cnt, rlo(f1) - rlo(f0), th, dw) != 0);
       };
       uint32_t ng = 0;
-      uint64_t pre = 0;
-      // emit=false: count the groups; true: write item base + ng, its bins' map and its cursor
-      auto walk = [&](bool emit) {
-        auto group = [&](uint64_t f0, uint64_t f1, uint64_t cnt) {
-          if (emit) {
-            const uint64_t slo = rlo(f0), shi = rlo(f1);
-            const uint64_t span = shi - slo, dist = cnt < span ? cnt : span;
-            uint32_t c;
-            if (wcap) {
-              if (cnt <= wcap) c = (uint32_t)dist;
-              else if (dist <= th) c = (uint32_t)dist | HH_BIG;          // by hash, ordered re-walk
-              else c = (uint32_t)th | HH_WIDE | HH_BIG;                  // by width sub-ranges
-            } else {
-              c = hh_count_item(cnt, span, th, dw);
-              if (!c) c = dw ? dw | HH_WIDE | HH_DIRECT : (uint32_t)th | HH_WIDE;
-            }
-            const uint64_t i = (uint64_t)s_base + ng;
-            if (i < cap) items[i] = HhItem{hb.gb, c | HH_PART, slo, shi, boff[hb.gb] + pre, (uint32_t)cnt, 0u};
-            else atomicOr(&a.ctr[HPC_ERR], 4ull);
-            for (uint64_t f = f0; f < f1; ++f) s_h[f] = ng;  // walked already: the bin's count is consumed
-            gc[ng] = (uint32_t)pre;
-          }
-          pre += cnt;
-          ++ng;
-        };
-        uint64_t acc = 0, g0 = 0;
-        for (uint32_t f = 0; f < hb.nbin; ++f) {
-          const uint64_t c = (emit && f < g0) ? 0 : s_h[f];  // (emit: bins before g0 hold item indices now)
+      auto group = [&](uint32_t f0, uint32_t f1, uint64_t cnt) {
+        if (lane == 0) {
+          s_gr[ng] = f0 | f1 << 16;
+          s_gc[ng] = (uint32_t)cnt;
+        }
+        ++ng;
+      };
+      uint64_t acc = 0;
+      uint32_t g0 = 0;
+      for (uint32_t fb = 0; fb < nbin; fb += 64) {
+        const uint32_t cv = fb + lane < nbin ? s_h[fb + lane] : 0u;
+        const uint32_t lim = nbin - fb < 64 ? nbin - fb : 64;
+        for (uint32_t q = 0; q < lim; ++q) {
+          const uint32_t f = fb + q;
+          const uint64_t c = (uint32_t)__builtin_amdgcn_readlane((int)cv, (int)q);
           if (!ok(f, f + 1, c)) {  // a bin beyond a group on its own
             if (acc) group(g0, f, acc);
             group(f, f + 1, c);
@@ -3083,23 +3213,47 @@ __global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __r
             acc = c;
             g0 = f;
           } else {
-            if (!acc && !c) {
-              if (emit) s_h[f] = HH_NOB;  // an empty bin before the group: no wedge maps here
-              g0 = f + 1;
-            }
+            if (!acc && !c) g0 = f + 1;
             acc += c;
           }
         }
-        if (acc) group(g0, hb.nbin, acc);
-      };
-      walk(false);
-      s_base = atomicAdd(nitems, ng);
-      ng = 0;
-      pre = 0;
-      walk(true);
+      }
+      if (acc) group(g0, nbin, acc);
+      if (lane == 0) {
+        s_ng = ng;
+        s_base = atomicAdd(nitems, ng);
+      }
     }
     __syncthreads();
-    for (uint32_t f = t; f < hb.nbin; f += HH_NT) gh[f] = s_h[f];  // bin -> the bucket's item
+    const uint32_t ng = s_ng, base = s_base;
+    // pre_g: exclusive prefix of the group counts (GPT consecutive groups per thread)
+    uint64_t mine = 0;
+    for (int q = 0; q < GPT; ++q) {
+      const uint32_t g = (uint32_t)t * GPT + q;
+      if (g < ng) mine += s_gc[g];
+    }
+    uint64_t pre = block_excl_scan(mine, s_scan, nullptr);
+    const uint64_t bo = boff[hb.gb];
+    for (int q = 0; q < GPT; ++q) {
+      const uint32_t g = (uint32_t)t * GPT + q;
+      if (g >= ng) break;
+      const uint32_t f0 = s_gr[g] & 0xffffu, f1 = s_gr[g] >> 16, cnt = s_gc[g];
+      const uint64_t i = (uint64_t)base + g;
+      if (i < cap) items[i] = HhItem{hb.gb, item_word(f0, f1, cnt) | HH_PART, rlo(f0), rlo(f1), bo + pre, cnt, 0u};
+      else atomicOr(&a.ctr[HPC_ERR], 4ull);
+      gc[g] = (uint32_t)pre;
+      pre += cnt;
+    }
+    // bin -> its group: the last group starting at or before it (a bin before
+    // every group, or between groups, is empty: no wedge maps there)
+    for (uint32_t f = t; f < nbin; f += HH_NT) {
+      uint32_t l = 0, h = ng;
+      while (l < h) {
+        const uint32_t m = (l + h) >> 1;
+        if ((s_gr[m] & 0xffffu) <= f) l = m + 1; else h = m;
+      }
+      gh[f] = l ? l - 1 : HH_NOB;
+    }
     __syncthreads();
   }
 }

@@ -283,6 +283,8 @@ struct nlp_graph {
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
+  int hp_rowb = 1;           // bin 1, count metrics: tiered 256-thread rows (NLP_HASH_ROWB=0: k_hp_block;
+                             // 2: every row in the 8192-entry tier, 3: none in the 2048-entry tier -- tests)
   uint32_t hh_dw = HH_DW;    // hub pass, counts: direct-counter range width (NLP_HH_DIRECT=0 off, small values test it)
   bool hh_stats = false;     // NLP_HH_STATS=1: per chunk, the hub items' scratch reads on stderr (debug)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
@@ -755,6 +757,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
+  if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
@@ -1923,9 +1926,12 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipGetLastError());
   }
   uint32_t* lists[HP_NBINS];
-  uint32_t* tlist;  // bin-0 rows of a chunk by tier, then counters: [0, 6) tiers, [6, 9) work queues of bins 2, 3, 1
-  TRY(wsget(ws, B_HP_TIER, nU + 16, &tlist));
+  // bin-0 rows of a chunk by tier, then counters: [0, 6) tiers, [6, 9) work queues of bins 2, 3, 1,
+  // [10] batches, [11, 14) hub pass, [16, 22) bin-1 tiers, [22, 25) their work queues; then bin-1 rows by tier
+  uint32_t* tlist;
+  TRY(wsget(ws, B_HP_TIER, 2 * nU + 32, &tlist));
   uint32_t* tcnt = tlist + nU;
+  uint32_t* tlist1 = tlist + nU + 32;
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
   for (int b = 0; b < HP_NBINS; ++b) {
     TRY(wsget(ws, lb[b], nU, &lists[b]));
@@ -2123,6 +2129,24 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     if (n1 && g->hp_hub && g->hp_hub_min == 1) {
       nlp_status sh = run_hub(g, a, lists[1] + q0[1], n1, nullptr, 0, wu, ua, custom, scan, tcnt + 11, &b1_done, st);
       if (sh != NLP_OK) return sh;
+    }
+    if (n1 && !b1_done && !custom && a.kdeg && g->hp_rowb) {
+      // count metrics: bin 1 by table tier (k_hp_rowb), 256-thread workgroups
+      TRY(hipMemsetAsync(tcnt + 16, 0, 9 * sizeof(uint32_t), st));
+      const unsigned gt = (unsigned)std::min<uint64_t>((n1 + NT - 1) / NT, 512);
+      const uint64_t rt0 = g->hp_rowb >= 2 ? 0 : HP_RTIER0, rt1 = g->hp_rowb == 2 ? 0 : HP_RTIER1;
+      hipLaunchKernelGGL(k_hp_tier<false>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[1] + q0[1]), n1,
+                         (const uint64_t*)wu, ua, tcnt + 16, tlist1, rt0, rt1);
+      hipLaunchKernelGGL(k_hp_tier<true>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[1] + q0[1]), n1,
+                         (const uint64_t*)wu, ua, tcnt + 16, tlist1, rt0, rt1);
+      TRY(hipGetLastError());
+      // one launch per tier (its rows and count read on the device, no host wait)
+      const unsigned grw = (unsigned)std::min<uint64_t>(n1, 4096);
+      hipLaunchKernelGGL((k_hp_rowb<2048>), dim3(grw), dim3(HP_RNT), 0, st, a, (const uint32_t*)tlist1, (const uint32_t*)(tcnt + 16), 0, wu, ua, tcnt + 22);
+      hipLaunchKernelGGL((k_hp_rowb<4096>), dim3(grw), dim3(HP_RNT), 0, st, a, (const uint32_t*)tlist1, (const uint32_t*)(tcnt + 16), 1, wu, ua, tcnt + 23);
+      hipLaunchKernelGGL((k_hp_rowb<8192>), dim3(grw), dim3(HP_RNT), 0, st, a, (const uint32_t*)tlist1, (const uint32_t*)(tcnt + 16), 2, wu, ua, tcnt + 24);
+      TRY(hipGetLastError());
+      b1_done = true;
     }
     if (n1 && !b1_done) {
       const unsigned gr = (unsigned)std::min<uint64_t>(n1, 2048);
