@@ -2982,19 +2982,24 @@ __global__ __launch_bounds__(HH_NT) void k_hh_enum(HpArgs a, uint64_t nh, const 
 // k_hh_accum sorts by (w, v) in LDS and sums run by run in ascending v; a single
 // bin beyond HH_SCAP wedges is flagged HH_BIG (hash table with the ordered
 // re-walk of hp_ordered_sum).
-struct HhItem {
-  uint32_t gb, cnt;   // bucket, distinct-w bound of the range (| HH_BIG | HH_WIDE | HH_DIRECT | HH_PART)
-  uint64_t slo, shi;  // w-range
-  uint64_t off;       // HH_PART: the item's wedges in the partitioned scratch [off, off + n)
-  uint32_t n, pad;
+struct HhItem {         // 64 bytes: everything k_hh_accum needs, one load
+  uint32_t cnt;         // distinct-w bound of the range | HH_BIG | HH_WIDE | HH_DIRECT | HH_PART | HH_WHOLE
+  uint32_t n;           // its wedges, at sw[off, off + n) (HH_PART: at pw)
+  uint32_t u, du;       // the row and deg u
+  uint64_t slo, shi;    // w-range
+  uint64_t off;
+  uint64_t x0, x1;      // the bucket's exclusion slice of N(u) (absolute entry indices)
+  uint32_t gb, pad;     // bucket (statistics)
 };
+static_assert(sizeof(HhItem) == 64, "one 64-byte item");
 constexpr uint32_t HH_FINE = 4096;
 constexpr uint32_t HH_SCAP = 4096;         // sort-mode wedges per item (32 KB of u64 keys)
 constexpr uint32_t HH_BIG = 0x80000000u;
 constexpr uint32_t HH_WIDE = 0x40000000u;  // the range is accumulated in sub-ranges of cnt w
 constexpr uint32_t HH_DIRECT = 0x20000000u;  // counts (no AA / RA) indexed by w - lo in LDS, no hashing
 constexpr uint32_t HH_PART = 0x10000000u;    // a heavy bucket's item: its own wedges, partitioned by k_hh_part
-constexpr uint32_t HH_CNT = 0x0fffffffu;
+constexpr uint32_t HH_WHOLE = 0x08000000u;   // every wedge at off is inside [slo, shi): no range test
+constexpr uint32_t HH_CNT = 0x07ffffffu;
 constexpr uint32_t HH_DW = 16384;          // direct counters per range (the two words of the 8192-entry table)
 constexpr uint32_t HH_DMARK = 0x80000000u;  // direct counter: w is in N(u)
 constexpr uint64_t HH_SEG = 65536;         // heavy scratch wedges per histogram segment
@@ -3006,6 +3011,8 @@ struct HhHeavy {
   uint32_t nbin, fsh; // bins of width 2^fsh from lo
   uint64_t seg0;      // first segment (its bins at seg0 * HH_BPS)
   uint64_t lo, hi;    // the bucket's w-range
+  uint32_t u, du;     // its row, deg u
+  uint64_t x0, x1;    // its exclusion slice of N(u)
 };
 
 __device__ __forceinline__ uint64_t hh_bucket_range(const HpArgs& a, uint32_t u, uint32_t shift, uint64_t b,
@@ -3039,8 +3046,10 @@ __device__ __forceinline__ uint32_t hh_count_item(uint64_t cnt, uint64_t span, u
 // wedge count (<= wcap) instead of their distinct-w bound.  Heavy buckets go to
 // heavy[] (at most hcap: host bound tot / half + 1) with their bins zeroed.
 __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ brow, const uint32_t* __restrict__ hr_u,
-                          const uint32_t* __restrict__ hr_shift, const uint64_t* __restrict__ bbase,
-                          const uint32_t* __restrict__ bcnt, int tl, HhItem* __restrict__ items,
+                          const uint32_t* __restrict__ hr_shift, const uint32_t* __restrict__ hr_p,
+                          const uint64_t* __restrict__ bbase, const uint64_t* __restrict__ boff,
+                          const uint64_t* __restrict__ xs, const uint32_t* __restrict__ bcnt, int tl,
+                          HhItem* __restrict__ items,
                           uint32_t* __restrict__ nitems, HhHeavy* __restrict__ heavy,
                           unsigned long long* __restrict__ hctr, uint64_t hcap, uint32_t* __restrict__ ghist,
                           uint32_t wcap, uint32_t dw) {
@@ -3048,18 +3057,27 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
   const uint64_t th = 1ull << (tl - 1);
   for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t gb = b0 + threadIdx.x;
-    uint32_t n = 0;
-    uint64_t lo = 0, width = 0;
+    uint32_t n = 0, u = 0, du = 0;
+    uint64_t lo = 0, width = 0, x0 = 0, x1 = 0;
     if (gb < nb) {
       n = bcnt[gb];
       const uint32_t r = brow[gb];
-      width = hh_bucket_range(a, hr_u[r], hr_shift[r], gb - bbase[r], &lo);
+      u = hr_u[r];
+      const uint64_t b = gb - bbase[r];
+      width = hh_bucket_range(a, u, hr_shift[r], b, &lo);
+      if (n) {
+        const uint64_t o1 = a.g.off[u + 1];
+        du = (uint32_t)(o1 - a.g.off[u]);
+        x0 = xs[gb];
+        x1 = b + 1 < hr_p[r] ? xs[gb + 1] : o1;  // N(u) entries in the bucket
+      }
     }
     const uint64_t dist = (uint64_t)n < width ? (uint64_t)n : width;
     const uint32_t ci = wcap ? (n <= wcap ? (uint32_t)dist : 0u) : hh_count_item(n, width, th, dw);
     const bool simple = n > 0 && ci != 0, hv = n > 0 && !simple;
     const uint32_t i = hh_wave_append(simple, nitems);
-    if (simple) items[i] = HhItem{(uint32_t)gb, ci, lo, lo + width, 0ull, 0u, 0u};  // i < nb <= the item capacity
+    if (simple)  // i < nb <= the item capacity
+      items[i] = HhItem{ci | HH_WHOLE, n, u, du, lo, lo + width, boff[gb], x0, x1, (uint32_t)gb, 0u};
     const uint64_t nseg = hv ? (n + HH_SEG - 1) / HH_SEG : 0;
     const uint64_t pk = hv ? (1ull << HH_HSH) | nseg : 0ull;
     const uint64_t inc = wave_incl_scan(pk), wt = __shfl(inc, 63, 64);
@@ -3072,7 +3090,7 @@ __global__ void k_hh_plan(HpArgs a, uint64_t nb, const uint32_t* __restrict__ br
       const uint32_t nbin = (uint32_t)(nseg * HH_BPS < HH_FINE ? nseg * HH_BPS : HH_FINE);
       const uint32_t fsh = (uint32_t)log2_ceil((width + nbin - 1) / nbin);
       if (j < hcap) {
-        heavy[j] = HhHeavy{(uint32_t)gb, n, nbin, fsh, s0, lo, lo + width};
+        heavy[j] = HhHeavy{(uint32_t)gb, n, nbin, fsh, s0, lo, lo + width, u, du, x0, x1};
         uint4* z = (uint4*)(ghist + s0 * HH_BPS);  // 16-byte aligned: HH_BPS words per segment
         for (uint32_t q = 0; q < nbin / 4; ++q) z[q] = make_uint4(0, 0, 0, 0);
       } else {
@@ -3239,7 +3257,9 @@ __global__ __launch_bounds__(HH_NT) void k_hh_group(HpArgs a, const HhHeavy* __r
       if (g >= ng) break;
       const uint32_t f0 = s_gr[g] & 0xffffu, f1 = s_gr[g] >> 16, cnt = s_gc[g];
       const uint64_t i = (uint64_t)base + g;
-      if (i < cap) items[i] = HhItem{hb.gb, item_word(f0, f1, cnt) | HH_PART, rlo(f0), rlo(f1), bo + pre, cnt, 0u};
+      if (i < cap)
+        items[i] = HhItem{item_word(f0, f1, cnt) | HH_PART | HH_WHOLE, cnt, hb.u, hb.du, rlo(f0), rlo(f1), bo + pre,
+                          hb.x0, hb.x1, hb.gb, 0u};
       else atomicOr(&a.ctr[HPC_ERR], 4ull);
       gc[g] = (uint32_t)pre;
       pre += cnt;
@@ -3345,16 +3365,9 @@ constexpr uint32_t HS_DMAX = 4095;
 template <bool CUSTOM>
 __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __restrict__ items,
                                                     const uint32_t* __restrict__ nitems,
-                                                    const uint32_t* __restrict__ brow,
-                                                    const uint32_t* __restrict__ hr_u,
-                                                    const uint32_t* __restrict__ hr_shift,
-                                                    const uint32_t* __restrict__ hr_p,
-                                                    const uint64_t* __restrict__ bbase,
-                                                    const uint32_t* __restrict__ bcnt, const uint64_t* __restrict__ boff,
-                                                    const uint64_t* __restrict__ xs, const uint32_t* __restrict__ sw0,
-                                                    const uint32_t* __restrict__ sv0, const uint32_t* __restrict__ pw,
-                                                    const uint32_t* __restrict__ pv, uint32_t* __restrict__ queue,
-                                                    int sortmode, uint64_t cap) {
+                                                    const uint32_t* __restrict__ sw0, const uint32_t* __restrict__ sv0,
+                                                    const uint32_t* __restrict__ pw, const uint32_t* __restrict__ pv,
+                                                    uint32_t* __restrict__ queue, int sortmode, uint64_t cap) {
   constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
   constexpr int LT = 1 << TL;
   constexpr int VT = CUSTOM ? LT : 1;
@@ -3367,7 +3380,8 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   __shared__ uint8_t s_ex[CUSTOM ? HH_SCAP : 1];
   __shared__ uint32_t s_gu[HH_NW][HP_BSTG], s_gw[HH_NW][HP_BSTG];
   __shared__ float s_gs[HH_NW][HP_BSTG];
-  __shared__ uint64_t s_it;
+  __shared__ uint64_t s_item[8];  // the next item (8 words), loaded while this one runs
+  __shared__ uint32_t s_tk[2];
   __shared__ uint32_t s_n;
   const int t = threadIdx.x, wv = wave_id();
   uint32_t* const s_v0 = (uint32_t*)s_vv;
@@ -3380,35 +3394,31 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   }
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
-  // k_hh_split counts past `cap` when the item array overflows (and raises
+  // k_hh_group counts past `cap` when the item array overflows (and raises
   // HPC_ERR): never read beyond it
   const uint32_t ni = (uint32_t)min((uint64_t)*nitems, cap);
   uint64_t wedges = 0;
+  // Items from the work queue two deep: while item `cur` runs, the next
+  // ticket's item words and the ticket after it are in flight (a workgroup
+  // barrier waits for LDS only, not for these loads), so an item costs no
+  // queue or descriptor round trip of its own.
+  if (t == 0) {
+    s_tk[0] = atomicAdd(queue, 1u);
+    s_tk[1] = atomicAdd(queue, 1u);
+  }
   __syncthreads();
-  for (;;) {
-    if (t == 0) s_it = atomicAdd(queue, 1u);
-    __syncthreads();
-    const uint64_t it = s_it;
-    __syncthreads();
-    if (it >= ni) break;
-    const HhItem item = items[it];
-    const uint32_t gb = item.gb;
-    // a heavy bucket's item reads its own partitioned wedges, all inside its range
+  uint32_t cur = s_tk[0], nx = s_tk[1];
+  if (t < 8 && cur < ni) s_item[t] = ((const uint64_t*)(items + cur))[t];
+  __syncthreads();
+  auto run = [&](const HhItem& item) {
+    // a heavy bucket's item reads its own partitioned wedges
     const bool part = (item.cnt & HH_PART) != 0;
     const uint32_t* const sw = part ? pw : sw0;
     const uint32_t* const sv = part ? pv : sv0;
-    const uint32_t n = part ? item.n : bcnt[gb];
-    const uint32_t r = brow[gb];
-    const uint32_t u = hr_u[r];
-    const uint64_t b = gb - bbase[r];
-    const uint64_t off = part ? item.off : boff[gb];
-    uint64_t lo;
-    const uint64_t width = hh_bucket_range(a, u, hr_shift[r], b, &lo);
-    const bool whole = part || (item.slo == lo && item.shi == lo + width);
+    const uint32_t n = item.n, u = item.u;
+    const uint64_t off = item.off, du = item.du, x0 = item.x0, x1 = item.x1;
+    const bool whole = (item.cnt & HH_WHOLE) != 0;
     const uint64_t slo = item.slo, shi = item.shi;
-    const uint64_t o1 = a.g.off[u + 1];
-    const uint64_t du = o1 - a.g.off[u];
-    const uint64_t x0 = xs[gb], x1 = b + 1 < hr_p[r] ? xs[gb + 1] : o1;  // N(u) entries in the bucket
     if (CUSTOM && sortmode && !(item.cnt & HH_BIG)) {
       uint64_t* const sk = s_vv;
       if (t == 0) s_n = 0;
@@ -3486,7 +3496,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         s_v1[i] = 0;
       }
       __syncthreads();
-      continue;
+      return;
     }
     if (!CUSTOM && (item.cnt & HH_DIRECT)) {
       // direct counters over sub-ranges of at most HH_DW w (HH_WIDE: of the item's count word)
@@ -3534,7 +3544,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         }
         __syncthreads();
       }
-      continue;
+      return;
     }
     const uint32_t dcnt = item.cnt & HH_CNT;
     const int lg = max(6, log2_ceil(2 * (uint64_t)dcnt));
@@ -3572,6 +3582,23 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
       __syncthreads();
     }
+  };
+  while (cur < ni) {
+    HhItem item;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ((uint64_t*)&item)[q] = s_item[q];
+    uint64_t pf = 0;
+    uint32_t tk = 0;
+    if (t < 8 && nx < ni) pf = ((const uint64_t*)(items + nx))[t];  // in flight during this item
+    if (t == 0) tk = atomicAdd(queue, 1u);
+    __syncthreads();  // every thread holds the item before s_item changes
+    run(item);
+    __syncthreads();
+    if (t < 8) s_item[t] = pf;
+    if (t == 0) s_tk[0] = tk;
+    __syncthreads();
+    cur = nx;
+    nx = s_tk[0];
   }
   hp_finish(sg, a, wedges);
 }

@@ -278,6 +278,8 @@ struct nlp_graph {
   bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
+  unsigned occ_esd = 256;    // resident k_es_pass<., DIRECT> workgroups
+  int es_var = 0;            // experiment (NLP_ES_VAR=1): record passes without the LDS reorder
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
@@ -758,6 +760,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
+  if (const char* ev = getenv("NLP_ES_VAR")) g->es_var = atoi(ev);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
@@ -793,6 +796,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
+    TRY(occ((const void*)k_es_pass<false, true>, &g->occ_esd, ES_NT));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1584,7 +1588,16 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
   for (int r = 0; r < P; ++r) {
     EdgeOut* dst = ((P - 1 - r) & 1) ? tmp : out;  // the last pass writes `out`
     const uint64_t ep = ++g->es_epoch;
-    if (r == 0)
+    if (g->es_var == 1) {
+      const unsigned grd = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_esd));
+      if (r == 0)
+        hipLaunchKernelGGL((k_es_pass<true, true>), dim3(grd), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr,
+                           dst, n, vb, 8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+      else
+        hipLaunchKernelGGL((k_es_pass<false, true>), dim3(grd), dim3(ES_NT), 0, st, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (const float*)nullptr, src, dst, n, vb, 8 * run[r],
+                           (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+    } else if (r == 0)
       hipLaunchKernelGGL(k_es_pass<true>, dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst, n, vb,
                          8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
     else
@@ -1727,7 +1740,8 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   TRY(hipMemsetAsync(queue, 0, 8, st));
   TRY(hipMemsetAsync(hv, 0, 8, st));
   LAUNCH(k_hh_plan, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
-         (const uint64_t*)bbase, (const uint32_t*)bcnt, tl, items, nitems, heavy, hctr, hcap, (uint32_t*)gh, wcap, dw);
+         (const uint32_t*)hr_p, (const uint64_t*)bbase, (const uint64_t*)boff, (const uint64_t*)xs,
+         (const uint32_t*)bcnt, tl, items, nitems, heavy, hctr, hcap, (uint32_t*)gh, wcap, dw);
   hipLaunchKernelGGL(k_hh_hist, dim3((unsigned)std::min<uint64_t>(tot / HH_SEG + hcap, 4096)), dim3(HH_NT), 0, st, a,
                      (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint64_t*)boff,
                      (const uint32_t*)sw, (uint32_t*)gh);
@@ -1741,16 +1755,12 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
   if (custom)
     hipLaunchKernelGGL((k_hh_accum<true>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
-                       (const uint32_t*)nitems, (const uint32_t*)brow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, (const uint32_t*)pw, (const uint32_t*)pv, queue, (int)(wcap != 0), cap);
+                       (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw,
+                       (const uint32_t*)pv, queue, (int)(wcap != 0), cap);
   else
     hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
-                       (const uint32_t*)nitems, (const uint32_t*)brow,
-                       (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p, (const uint64_t*)bbase,
-                       (const uint32_t*)bcnt, (const uint64_t*)boff, (const uint64_t*)xs, (const uint32_t*)sw,
-                       (const uint32_t*)sv, (const uint32_t*)pw, (const uint32_t*)pv, queue, 0, cap);
+                       (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw,
+                       (const uint32_t*)pv, queue, 0, cap);
   TRY(hipGetLastError());
   if (g->hh_stats) {  // debug: how often the accumulation items stream their buckets
     TRY(hipStreamSynchronize(st));
@@ -1765,7 +1775,7 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
     TRY(hipMemcpy(bn.data(), bcnt, NB * 4, hipMemcpyDeviceToHost));
     uint64_t rd = 0, big = 0, wide = 0, mx = 0, sortw = 0, direct = 0;
     for (const HhItem& x : it) {
-      const uint64_t xn = (x.cnt & HH_PART) ? x.n : bn[x.gb];
+      const uint64_t xn = x.n;
       rd += xn;
       direct += (x.cnt & HH_DIRECT) != 0;
       mx = std::max<uint64_t>(mx, xn);

@@ -17,7 +17,7 @@ OUT=$REPO/gpurun_out/$TAG
 mkdir -p "$OUT"
 STEPS=${STEPS:-tests,bench}
 BENCH_ARGS=${BENCH_ARGS:-}
-PROF_CMD="python3 $REPO/bench.py --steps 5 --warmup 2 --no-cpu-baseline --sweep = --wp-steps 3 $BENCH_ARGS"
+PROF_CMD="python3 $REPO/bench.py --steps 5 --warmup 2 --no-cpu-baseline --sweep = --wp-steps 3 --work-point ${WP:-16} $BENCH_ARGS"
 C5_CMD="python3 $REPO/tools/range_call.py ${RANGE_ARGS:-}"
 cd "$REPO"
 run() {  # name limit cmd...
