@@ -105,19 +105,15 @@ __device__ __forceinline__ uint64_t es_load(const uint64_t* p) {
 
 // FIRST: the input is the candidate columns (cu, cw, cs); else records `in`.
 // The output is always records (`out`: the caller's edges on the last pass).
-// DIRECT (experiment, NLP_ES_VAR=1): every record stored from registers at
-// its global position (no LDS reorder: scattered 12-byte stores, the tile's
-// runs of one digit meet in L2), 52 KB less LDS per workgroup.
-template <bool FIRST, bool DIRECT = false>
+template <bool FIRST>
 __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                                                    const float* __restrict__ cs, const EdgeOut* __restrict__ in,
                                                    EdgeOut* __restrict__ out, uint64_t n, int vb, int shift,
                                                    const uint32_t* __restrict__ ghist, uint64_t* __restrict__ desc,
                                                    uint32_t* __restrict__ ticket, uint64_t epoch,
                                                    uint32_t* __restrict__ err) {
-  constexpr int LTILE = DIRECT ? 1 : ES_TILE;
-  __shared__ uint32_t s_u[LTILE], s_w[LTILE], s_s[LTILE];
-  __shared__ uint8_t s_d[LTILE];           // each tile position's digit (the write phase does not recompute it)
+  __shared__ uint32_t s_u[ES_TILE], s_w[ES_TILE], s_s[ES_TILE];
+  __shared__ uint8_t s_d[ES_TILE];         // each tile position's digit (the write phase does not recompute it)
   __shared__ uint32_t s_wc[ES_NW][256];   // per wave: running digit counts, then wave prefixes
   __shared__ uint64_t s_gofs[256];        // global position of the tile's first record of each digit
   __shared__ uint32_t s_lofs[256];        // tile position of the first record of each digit
@@ -240,15 +236,6 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
       s_lofs[t] = lof;
     }
     __syncthreads();
-    if constexpr (DIRECT) {
-#pragma unroll
-      for (int i = 0; i < ES_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
-        if (q < tn) out[s_gofs[dg[i]] + s_wc[wv][dg[i]] + rk[i]] = EdgeOut{ru[i], rw[i], __uint_as_float(rs[i])};
-      }
-      __syncthreads();
-      continue;
-    }
     // reorder the tile by digit in LDS
 #pragma unroll
     for (int i = 0; i < ES_IPT; ++i) {

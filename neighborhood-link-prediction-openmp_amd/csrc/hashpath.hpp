@@ -79,6 +79,7 @@ struct HpArgs {
   int xp;                  // experiment (NLP_HB_XP, wrong results): 1 skip k_hp_batch's exclusion, 2 its emission,
                            // 4 its wedge inserts
   uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
+  uint32_t uxf;            // rows whose exclusion slice exceeds uxf x W test the membership table (HP_UX_OFF: never)
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -417,6 +418,18 @@ __device__ __forceinline__ uint32_t pow2_at_least(uint32_t n) {
 // candidate / NaN counts stay in registers until the kernel ends.
 constexpr int HP_STG = 128;
 
+// A row whose exclusion slice (the entries of N(u) above u) exceeds HB_XF
+// times its wedge bound tests its table entries in the per-graph membership
+// table instead (one 64-byte line per entry, kernels.hpp et_has) of marking
+// the slice: a high-degree row with a few low-degree neighbours would read
+// thousands of keys for a handful of entries (C4 JAC H=16: the marks cost
+// ~10 of the row batches' 18 ms).
+constexpr uint64_t HB_XF = 8;
+constexpr uint32_t HP_UX_OFF = 0xffffffffu;
+__device__ __forceinline__ bool hp_use_etab(const HpArgs& a, uint64_t dx, uint64_t W) {
+  return a.g.etab && a.uxf != HP_UX_OFF && dx > (uint64_t)a.uxf * W;
+}
+
 struct HpStage {
   uint32_t* u;
   uint32_t* w;
@@ -607,7 +620,7 @@ __device__ __forceinline__ void hp_stream(const uint32_t* src, uint64_t n, uint3
 // count table (hp_insert_kd<KCB>: deg w in the count word).
 template <bool GLOBAL, bool CUSTOM, int UN = HP_UN, bool ORD = false, int KCB = 0>
 __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t t, uint32_t stride, HpStage& sg,
-                                         const HpArgs& a, uint32_t u, uint64_t du, int64_t tau) {
+                                         const HpArgs& a, uint32_t u, uint64_t du, int64_t tau, bool ux = false) {
   T = __builtin_amdgcn_readfirstlane(T);
   for (uint32_t i0 = 0; i0 < T; i0 += stride * UN) {
     uint32_t w[UN], c[UN], v0[UN], v1[UN], dw[UN];
@@ -619,6 +632,8 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
       c[q] = v0[q] = v1[q] = 0;
       if (ORD) w[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
       else w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
+      // ux: the first-order exclusion by the membership table (no marks were made)
+      if (ux && w[q] != HP_EMPTY && et_has(a.g.etab, a.g.etbits, u, w[q])) c[q] |= HP_EXCL;
     }
     if (ORD) {
 #pragma unroll
@@ -1579,12 +1594,16 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
       wave_sync_lds();
     }
     // first-order exclusion (predict.hxx:306-307): the entries of N(u) above u
+    // marked, or tested in the membership table at the drain (a slice beyond
+    // HB_XF times the row's wedge bound)
     const uint32_t xu = a.xs ? a.xs[u] : 0u;
-    hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)lane, 64u, [&](uint32_t x) {
-      if (x > u) hp_mark<false>(tb, mask, shift, x);
-    });
+    const bool ux = hp_use_etab(a, du - xu, W);
+    if (!ux)
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)lane, 64u, [&](uint32_t x) {
+        if (x > u) hp_mark<false>(tb, mask, shift, x);
+      });
     wave_sync_lds();
-    hp_drain<false, CUSTOM, 8, CUSTOM, KD ? 10 : 0>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau);
+    hp_drain<false, CUSTOM, 8, CUSTOM, KD ? 10 : 0>(tb, T, (uint32_t)lane, 64u, sg, a, u, du, tau, ux);
     wave_sync_lds();
   }
   hp_finish(sg, a, wedges);
@@ -1603,6 +1622,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
 // (slot, x) for x in N(u); the drain decodes the slot back to (u, deg u).
 // Needs S <= 2^(32 - 6) (six slot bits above w).
 constexpr uint64_t HB_ROWCOST = 5;  // budget units per row besides its wedges (bounds the rows per batch)
+
 constexpr int HB_UN = 8;            // loads per lane in flight in the batch loops (a batch is a few round trips)
 
 // The rows of tiers tlo..thi: a contiguous region of the tier list.
@@ -1758,6 +1778,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
   __shared__ uint64_t s_o0[NWAVE][64];
   __shared__ uint32_t s_sp[NWAVE][64];
   __shared__ uint32_t s_np[NWAVE][64];
+  __shared__ uint8_t s_ux[NWAVE][64];     // the row's entries tested in the membership table
   __shared__ uint32_t s_gu[NWAVE][STG], s_gw[NWAVE][STG];
   __shared__ float s_gs[NWAVE][STG];
   constexpr int SK = CUSTOM ? TW / 2 : 1;  // AA / RA: the batch's first hops (slot << wbits | v), sorted
@@ -1786,6 +1807,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
   uint64_t wedges = 0;
   uint64_t abytes = 0;  // algorithmic bytes (wave-uniform): rows, entries, exclusion keys
   uint64_t drained = 0;  // per lane: table entries whose deg w is gathered (count metrics without KD)
+  uint64_t etq = 0;      // per lane: membership-table tests (8 bytes each: the key)
   wave_sync_lds();
   // The next batch's bounds, rows and row data are loaded while this batch
   // works (bounds during the first hops, rows during the exclusion, row data
@@ -1843,7 +1865,9 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
       continue;
     }
     fetch_bounds(bn, &pr0, &pnr);
-    const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(dx);
+    const bool ux = hp_use_etab(a, dx, W);
+    const uint32_t sp = (uint32_t)wave_incl_scan(ns), np = (uint32_t)wave_incl_scan(ux ? 0u : dx);
+    s_ux[wv][lane] = ux ? 1 : 0;
     s_u[wv][lane] = u;
     s_du[wv][lane] = du;
     s_s0[wv][lane] = s0;
@@ -2029,6 +2053,10 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
         const uint32_t uu = s_u[wv][sl];
         const uint64_t du2 = s_du[wv][sl];
+        if (valid && s_ux[wv][sl]) {  // first-order exclusion by the membership table
+          ++etq;
+          if (et_has(a.g.etab, a.g.etbits, uu, w)) c[q] |= HP_EXCL;
+        }
         float s = 0.0f;
         if (valid) {
           if (CUSTOM) s = ho_score(c[q]);
@@ -2056,7 +2084,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     for (int i = 0; i < 4; ++i) atomicAdd(&a.ph[i], (unsigned long long)ph_acc[i]);
   // + per wedge its key (and its degree for KD), per emitted candidate 16 (key, u, w, score)
   const uint64_t wsum = wave_sum(wedges);
-  abytes += (KD ? 8ull : 4ull) * wsum + 16ull * sg.out + 4ull * wave_sum(drained);
+  abytes += (KD ? 8ull : 4ull) * wsum + 16ull * sg.out + 4ull * wave_sum(drained) + 8ull * wave_sum(etq);
   if (lane == 0 && abytes) atomicAdd(&a.ctr[HPC_HOTB], (unsigned long long)abytes);
 }
 
@@ -2240,12 +2268,15 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
         hp_sync<GLOBAL>();
       }
       const uint32_t xu = a.xs ? a.xs[u] : 0u;  // the entries of N(u) above u
-      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
-        if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
-      });
+      // marked, or (LDS table, a slice beyond HB_XF times W) tested in the membership table at the drain
+      const bool ux = !GLOBAL && hp_use_etab(a, du - xu, W);
+      if (!ux)
+        hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_BNT, [&](uint32_t x) {
+          if ((uint64_t)x >= wlo && (uint64_t)x < whi) hp_mark<GLOBAL>(tb, mask, shift, x);
+        });
       hp_sync<GLOBAL>();
       hp_drain<GLOBAL, CUSTOM, HP_UN, ORD, (KD && !GLOBAL && !CUSTOM) ? 13 : 0>(tb, T, (uint32_t)t, (uint32_t)HP_BNT,
-                                                                              sg, a, u, du, tau);
+                                                                              sg, a, u, du, tau, ux);
       hp_sync<GLOBAL>();
       round = 0;
     }
@@ -2343,10 +2374,14 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
                                      }, a.kdeg);
       __syncthreads();
     }
-    // first-order exclusion: the entries of N(u) above u (a key <= u has no entry)
+    // first-order exclusion: the entries of N(u) above u (a key <= u has no
+    // entry) marked, or -- a slice beyond HB_XF times the row's wedge bound --
+    // every entry tested in the membership table at the drain
     const uint32_t xu = a.xs ? a.xs[u] : 0u;
-    hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
-              [&](uint32_t x) { h64_mark(s_t, mask, shift, x); });
+    const bool ux = hp_use_etab(a, du - xu, W);
+    if (!ux)
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
+                [&](uint32_t x) { h64_mark(s_t, mask, shift, x); });
     __syncthreads();
     for (uint32_t i0 = 0; i0 < T; i0 += HP_RNT * HP_UN) {  // T >= 64: uniform per wave
       uint32_t kq[HP_UN], c[HP_UN], dw[HP_UN];
@@ -2363,7 +2398,10 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
         }
       }
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) dw[q] = kq[q] != HP_EMPTY ? hp_kd_deg<13>(a.g, c[q], kq[q]) : 0u;
+      for (int q = 0; q < HP_UN; ++q) {
+        dw[q] = kq[q] != HP_EMPTY ? hp_kd_deg<13>(a.g, c[q], kq[q]) : 0u;
+        if (ux && kq[q] != HP_EMPTY && et_has(a.g.etab, a.g.etbits, u, kq[q])) c[q] |= HP_EXCL;
+      }
 #pragma unroll
       for (int q = 0; q < HP_UN; ++q) {
         const bool valid = kq[q] != HP_EMPTY;

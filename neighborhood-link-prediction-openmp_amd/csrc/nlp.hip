@@ -278,13 +278,13 @@ struct nlp_graph {
   bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
-  unsigned occ_esd = 256;    // resident k_es_pass<., DIRECT> workgroups
-  int es_var = 0;            // experiment (NLP_ES_VAR=1): record passes without the LDS reorder
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
+  uint32_t hp_uxf = HB_XF;   // exclusion by the membership table for slices beyond hp_uxf x W
+                             // (NLP_HASH_UX=off: always marks; =0: always the table)
   int hp_rowb = 1;           // bin 1, count metrics: tiered 256-thread rows (NLP_HASH_ROWB=0: k_hp_block;
                              // 2: every row in the 8192-entry tier, 3: none in the 2048-entry tier -- tests)
   uint32_t hh_dw = HH_DW;    // hub pass, counts: direct-counter range width (NLP_HH_DIRECT=0 off, small values test it)
@@ -760,7 +760,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
-  if (const char* ev = getenv("NLP_ES_VAR")) g->es_var = atoi(ev);
+  if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
@@ -796,7 +796,6 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
-    TRY(occ((const void*)k_es_pass<false, true>, &g->occ_esd, ES_NT));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1588,16 +1587,7 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
   for (int r = 0; r < P; ++r) {
     EdgeOut* dst = ((P - 1 - r) & 1) ? tmp : out;  // the last pass writes `out`
     const uint64_t ep = ++g->es_epoch;
-    if (g->es_var == 1) {
-      const unsigned grd = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_esd));
-      if (r == 0)
-        hipLaunchKernelGGL((k_es_pass<true, true>), dim3(grd), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr,
-                           dst, n, vb, 8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
-      else
-        hipLaunchKernelGGL((k_es_pass<false, true>), dim3(grd), dim3(ES_NT), 0, st, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (const float*)nullptr, src, dst, n, vb, 8 * run[r],
-                           (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
-    } else if (r == 0)
+    if (r == 0)
       hipLaunchKernelGGL(k_es_pass<true>, dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst, n, vb,
                          8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
     else
@@ -2058,6 +2048,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.xs = g->xs;
     a.xp = g->hb_xp;
     a.win = 0;
+    a.uxf = g->hp_uxf;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
     if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];

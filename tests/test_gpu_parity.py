@@ -433,8 +433,9 @@ class _env:
 # one w-bucket per row and 64-wide direct counters (heavy buckets grouped into
 # direct ranges, single bins beyond by HH_WIDE sub-ranges), 28 bin-1 count
 # rows by k_hp_block (not the tiered k_hp_rowb), 29 / 30 every bin-1 row in
-# the 8192- / at least the 4096-entry tier, 31 the final order's record
-# passes storing from registers (no LDS reorder)
+# the 8192- / at least the 4096-entry tier, 31-33 the first-order exclusion
+# of every row by the membership table (row batches and wave rows; bin-1
+# tiers; k_hp_block), 34 every row by marks
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -452,7 +453,9 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"), dict(NLP_HASH_WIN="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
-                 dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"), dict(NLP_ES_VAR="1")]
+                 dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"),
+                 dict(NLP_HASH_UX="0"), dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"),
+                 dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
