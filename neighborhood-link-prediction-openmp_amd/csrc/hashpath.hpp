@@ -1097,6 +1097,130 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill8(GraphView g, const uint8_t
   }
 }
 
+// ---------------------------------------------------------------- survivor lists in three streaming kernels
+// k_hp_dcls_one runs the whole chain of a tile -- classes, look-back, then per
+// survivor its key and off[v] -- with three workgroups per CU (163 VGPRs): a
+// tile waits on five dependent round trips and a lane holds about one survivor
+// per tile (C4 H=16: 4.6e7 survivors among 3.5e9 entries, 7.2 ms).  Here the
+// chain is cut where the parallelism changes:
+//   k_dc_count   a wave per 512-entry wave tile: its survivors counted (one
+//                8-byte class word per lane); the counts are scanned;
+//   k_dc_place   the same tiles again: each survivor's entry e and row r
+//                (row ends of the tile's first 64 rows in LDS, as the fill) at
+//                its position in entry order;
+//   k_dc_gather  a thread per survivor: key v = keys[e], class, rank, off[v] --
+//                independent across survivors, thousands in flight per CU --
+//                the packed entry, and (count << 40 | W+) per row by one
+//                atomic per run of equal rows in a wave.
+__device__ __forceinline__ uint32_t hp_dword(const uint8_t* __restrict__ dcls, uint64_t eb, uint64_t e0, uint64_t e1,
+                                             uint64_t* w) {
+  uint64_t x = 0;
+  if (eb >= e0 && eb + 8 <= e1) x = *(const uint64_t*)(dcls + eb);
+  else
+    for (int q = 0; q < 8; ++q)
+      if (eb + q >= e0 && eb + q < e1) x |= (uint64_t)dcls[eb + q] << (8 * q);
+  *w = x;
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t hp_dsurv8(uint64_t word, uint32_t H) {
+  uint32_t m = 0;  // bit q: byte q is a survivor class
+#pragma unroll
+  for (int q = 0; q < 8; ++q) m |= hp_dsurv((uint32_t)(word >> (8 * q)) & 0xffu, H) ? 1u << q : 0u;
+  return m;
+}
+
+__global__ __launch_bounds__(NT) void k_dc_count(const uint8_t* __restrict__ dcls, uint32_t H, uint64_t e0, uint64_t e1,
+                                                 uint32_t* __restrict__ tcn) {
+  const int lane = lane_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t wt = t0 + (uint64_t)blockIdx.x * NWAVE + wave_id(); wt < t1; wt += (uint64_t)gridDim.x * NWAVE) {
+    uint64_t word;
+    hp_dword(dcls, wt * HP_WTILE + (uint64_t)lane * 8, e0, e1, &word);
+    const uint64_t c = wave_sum((uint64_t)__popc(hp_dsurv8(word, H)));
+    if (lane == 0) tcn[wt - t0] = (uint32_t)c;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_dc_place(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+                                                 uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
+                                                 const uint32_t* __restrict__ tile_row,
+                                                 const uint64_t* __restrict__ tpre, uint64_t* __restrict__ se,
+                                                 uint32_t* __restrict__ sr) {
+  __shared__ uint64_t s_end[NWAVE][64];
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t wt = t0 + (uint64_t)blockIdx.x * NWAVE + wv; wt < t1; wt += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t eb = wt * HP_WTILE + (uint64_t)lane * 8;
+    uint64_t word;
+    hp_dword(dcls, eb, e0, e1, &word);
+    uint32_t m = hp_dsurv8(word, H);
+    const uint64_t tr = tile_row[wt];
+    const uint64_t r0 = tr > ua ? tr - ua : 0;
+    const uint64_t rl = r0 + lane;
+    s_end[wv][lane] = rl < nU ? g.off[ua + rl + 1] : ~0ull;
+    wave_sync_lds();
+    const uint32_t mine = (uint32_t)__popc(m);
+    uint64_t pos = tpre[wt - t0] + wave_incl_scan((uint64_t)mine) - mine;
+    int idx = 0;  // rows of the wave tile ending at or before this lane's first entry
+#pragma unroll
+    for (uint32_t bit = 32; bit > 0; bit >>= 1) idx += s_end[wv][idx + bit - 1] <= eb ? (int)bit : 0;
+    while (m) {
+      const int q = __builtin_ctz(m);
+      m &= m - 1;
+      const uint64_t e = eb + q;
+      while (idx < 64 && s_end[wv][idx] <= e) ++idx;
+      uint64_t r = r0 + (uint64_t)idx;
+      if (idx >= 64) {  // beyond the tile's first 64 rows: search the range's row ends
+        uint64_t lo = r0, hi = nU;
+        while (hi - lo > 1) {
+          const uint64_t md = (lo + hi) >> 1;
+          if (g.off[ua + md] <= e) lo = md; else hi = md;
+        }
+        r = lo;
+      }
+      se[pos] = e;
+      sr[pos] = (uint32_t)r;
+      ++pos;
+    }
+    wave_sync_lds();
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_dc_gather(GraphView g, const uint8_t* __restrict__ dcls,
+                                                  const uint8_t* __restrict__ drank, const uint64_t* __restrict__ se,
+                                                  const uint32_t* __restrict__ sr, uint64_t ns,
+                                                  uint32_t* __restrict__ skeys, uint64_t* __restrict__ sdo,
+                                                  unsigned long long* __restrict__ wu) {
+  const int lane = lane_id();
+  for (uint64_t b = (uint64_t)blockIdx.x * NT; b < ns; b += (uint64_t)gridDim.x * NT) {  // uniform per wave
+    const uint64_t i = b + threadIdx.x;
+    const bool ok = i < ns;
+    uint32_t r = 0xffffffffu;
+    unsigned long long x = 0;
+    if (ok) {
+      const uint64_t e = se[i];
+      r = sr[i];
+      const uint32_t c = dcls[e], l = drank[e];
+      const uint32_t v = g.keys[e];
+      const uint64_t o = g.off[v];
+      const uint32_t n = c - l;  // the part of N(v) above the row
+      skeys[i] = v;
+      sdo[i] = (uint64_t)c << 48 | (uint64_t)n << HP_SDO_SH | (o + l);
+      x = (1ull << 40) | n;
+    }
+    // rows are non-decreasing over consecutive survivors: a segmented sum per run, one atomic at its end
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      const uint32_t ry = __shfl_up(r, d, 64);
+      if (lane >= d && ry == r) x += y;
+    }
+    const uint32_t rn = __shfl_down(r, 1, 64);
+    if (ok && (lane == 63 || rn != r)) atomicAdd(&wu[r], x);
+  }
+}
+
 // ---------------------------------------------------------------- survivor lists in one pass
 // k_hp_dcls_rows8 + scan + k_hp_dcls_fill8 read the range's degree classes
 // twice (C4 H=16: 3.3 + 8.5 ms) and walk each lane's eight entries with a

@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -275,7 +275,8 @@ struct nlp_graph {
                              // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
   int hb_xp = 0;             // experiment (NLP_HB_XP): k_hp_batch phases skipped (wrong results; timing only)
   bool hp_win = true;        // k_hp_batch reserves emission windows (NLP_HASH_WIN=0: one reservation per flush)
-  bool hp_one = true;        // survivor lists in one pass (k_hp_dcls_one; NLP_HASH_ONE=0: count + fill kernels)
+  int hp_one = 2;            // survivor lists: 2 three streaming kernels (k_dc_*), 1 one pass (k_hp_dcls_one),
+                             // 0 count + fill kernels (NLP_HASH_ONE)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
@@ -763,7 +764,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
-  if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = ho[0] != '0';
+  if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = atoi(ho);
   if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
   if (const char* hx = getenv("NLP_HB_XP")) g->hb_xp = atoi(hx);
   if (const char* hw = getenv("NLP_HASH_WIN")) g->hp_win = hw[0] != '0';
@@ -1822,7 +1823,45 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
     bool one_done = false;
-    if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one && g->hp_sdo && g->drank && p.H >= 1 &&
+    if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 2 && g->hp_sdo && g->drank && p.H >= 1 &&
+        p.H <= HP_DCLS_MAX && e1 > e0 && g->nnz < (1ull << HP_SDO_SH)) {
+      // count, place, gather (hashpath.hpp k_dc_*)
+      const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
+      uint32_t *scnt, *tcn;
+      uint64_t* tpre;
+      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
+      TRY(wsget(ws, B_HP_SOFF, nU + 1, &s_soff));
+      TRY(wsget(ws, B_HP_TCNT, nt, &tcn));
+      TRY(wsget(ws, B_HP_TPRE, nt + 1, &tpre));
+      const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
+      hipLaunchKernelGGL(k_dc_count, dim3(gt), dim3(NT), 0, st, (const uint8_t*)g->dcls, p.H, e0, e1, tcn);
+      TRY(hipGetLastError());
+      TRY(wsget(ws, B_SCAN2, scan_scratch_words(nt) + 16, &scan2));
+      TRY(scan_ws<uint32_t>(ws, B_SCAN2, tcn, nt, tpre, tpre + nt, st));
+      TRY(hipMemcpyAsync(&g->host_small[10], tpre + nt, 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      const uint64_t ns = g->host_small[10];
+      uint64_t* se;
+      uint32_t* sr;
+      TRY(wsget(ws, B_HP_SE, std::max<uint64_t>(ns, 1), &se));
+      TRY(wsget(ws, B_HP_SR, std::max<uint64_t>(ns, 1), &sr));
+      TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(ns, 1), &s_skeys));
+      TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(ns, 1), &s_sdo));
+      hipLaunchKernelGGL(k_dc_place, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+                         (const uint32_t*)g->tile_row, (const uint64_t*)tpre, se, sr);
+      if (ns)
+        hipLaunchKernelGGL(k_dc_gather, dim3((unsigned)std::min<uint64_t>((ns + NT - 1) / NT, 65536)), dim3(NT), 0, st,
+                           gv, (const uint8_t*)g->dcls, (const uint8_t*)g->drank, (const uint64_t*)se,
+                           (const uint32_t*)sr, ns, s_skeys, s_sdo, (unsigned long long*)wu);
+      TRY(hipGetLastError());
+      LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
+      TRY(hipGetLastError());
+      TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
+      s_sorted = true;
+      one_done = true;
+    }
+    if (one_done) {
+    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 1 && g->hp_sdo && g->drank && p.H >= 1 &&
         p.H <= HP_DCLS_MAX && e1 > e0 && p_h != ~0ull && g->nnz < (1ull << HP_SDO_SH)) {
       // one pass over the range's classes (hashpath.hpp k_hp_dcls_one); output sized by the
       // degree histogram's P_H (an asymmetric graph's in-degrees may exceed it: overflow -> two passes)

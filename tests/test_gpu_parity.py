@@ -426,8 +426,8 @@ class _env:
 # drain), 19 = 17 with bin-1 rows, 20 row batches gathering deg / off of every
 # first hop (no packed survivor entries), 21 survivor suffixes searched per call
 # (no per-graph rank bytes), 22 survivor counts and fill as two kernels (not
-# k_hp_dcls_one), 23 k_hp_dcls_one's output capacity overflowing (the
-# two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
+# k_dc_count / place / gather), 23 the one-pass build (k_hp_dcls_one) with its
+# output capacity overflowing (the two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
 # above u), 25 the row batches' 4-loads / 3-waves build, 26 the row batches
 # reserving every flush (no emission windows, no padding), 27 hub pass with
 # one w-bucket per row and 64-wide direct counters (heavy buckets grouped into
@@ -435,7 +435,7 @@ class _env:
 # rows by k_hp_block (not the tiered k_hp_rowb), 29 / 30 every bin-1 row in
 # the 8192- / at least the 4096-entry tier, 31-33 the first-order exclusion
 # of every row by the membership table (row batches and wave rows; bin-1
-# tiers; k_hp_block), 34 every row by marks
+# tiers; k_hp_block), 34 every row by marks, 35 the one-pass survivor build
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -450,12 +450,14 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"), dict(NLP_HASH_WIN="0"),
+                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"),
+                 dict(NLP_HASH_WIN="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"),
                  dict(NLP_HASH_UX="0"), dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"),
-                 dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off")]
+                 dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off"),
+                 dict(NLP_HASH_ONE="1")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
