@@ -341,10 +341,11 @@ __device__ __forceinline__ void ho_add_wave(const HpTable& t, bool pend, uint32_
 }
 
 // one workgroup's step (HP_BNT = 1024 threads, every thread calls it)
+template <int TB = 10>  // a workgroup of 2^TB threads
 __device__ __forceinline__ void ho_add_block(const HpTable& t, bool pend, uint32_t h, double c, uint32_t* round) {
   const uint32_t tid = threadIdx.x;
   while (__syncthreads_or(pend)) {
-    const uint32_t tok = (*round << 10) | (1023u - tid);
+    const uint32_t tok = (*round << TB) | ((1u << TB) - 1u - tid);
     if (pend) atomicMax(&t.vmin[h], tok);
     __syncthreads();
     if (pend && *(volatile uint32_t*)&t.vmin[h] == tok) {
@@ -422,9 +423,10 @@ constexpr int HP_STG = 128;
 // times its wedge bound tests its table entries in the per-graph membership
 // table instead (one 64-byte line per entry, kernels.hpp et_has) of marking
 // the slice: a high-degree row with a few low-degree neighbours would read
-// thousands of keys for a handful of entries (C4 JAC H=16: the marks cost
-// ~10 of the row batches' 18 ms).
-constexpr uint64_t HB_XF = 8;
+// thousands of keys for a handful of entries.  C4 JAC H=16, row batches: 18.8
+// ms with marks only, 18.8 / 16.4 / 14.8 / 14.6 / 14.2 ms at factors 8 / 4 / 2 /
+// 1 / 0 (every row by the table); the whole call is fastest at 1.
+constexpr uint64_t HB_XF = 1;
 constexpr uint32_t HP_UX_OFF = 0xffffffffu;
 __device__ __forceinline__ bool hp_use_etab(const HpArgs& a, uint64_t dx, uint64_t W) {
   return a.g.etab && a.uxf != HP_UX_OFF && dx > (uint64_t)a.uxf * W;
@@ -2535,6 +2537,104 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
       }
     }
     __syncthreads();
+  }
+  hp_finish(sg, a, wedges);
+}
+
+// The same tiers for AA / RA (custom bin 1: W+ <= 2048): an ordered table
+// (ho_add_block's owner tokens over 256 threads) of 2048 or 4096 entries,
+// S(u) in ascending v (the degree-class lists are sorted by construction).
+template <int LT>
+__global__ __launch_bounds__(HP_RNT) void k_hp_rowo(HpArgs a, const uint32_t* __restrict__ tl,
+                                                    const uint32_t* __restrict__ tcnt, int tier,
+                                                    const uint64_t* __restrict__ wu, uint64_t ua,
+                                                    uint32_t* __restrict__ queue) {
+  constexpr int NW = HP_RNT / 64;
+  constexpr int TLG = LT == 2048 ? 11 : 12;
+  static_assert((1 << TLG) == LT, "table sizes 2048, 4096");
+  __shared__ uint32_t s_k[LT], s_c[LT], s_o[LT];  // keys, float accumulators, owner tokens
+  __shared__ uint64_t s_incl[HP_RNT];
+  __shared__ uint64_t s_start[HP_RNT];
+  __shared__ uint32_t s_iv[HP_RNT];
+  __shared__ double s_ic[HP_RNT];
+  __shared__ uint64_t s_w[NW];
+  __shared__ uint64_t s_tot, s_it;
+  __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
+  __shared__ float s_gs[NW][HP_BSTG];
+  const int t = threadIdx.x, wv = wave_id();
+  uint32_t rbase, nrows;  // this tier's rows: a region of the tier list (k_hp_tier)
+  hb_region(tcnt, tier, tier, &rbase, &nrows);
+  const uint32_t* rows = tl + rbase;
+  if (nrows == 0) return;
+  const HpTable tb{s_k, s_c, s_o, s_o};
+  for (int i = t; i < LT; i += HP_RNT) {
+    s_k[i] = HP_EMPTY;
+    s_c[i] = 0;
+    s_o[i] = 0;
+  }
+  HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
+  const int64_t tau = *a.tau;
+  uint64_t wedges = 0;
+  __syncthreads();
+  for (;;) {
+    if (t == 0) s_it = atomicAdd(queue, 1u);
+    __syncthreads();
+    const uint64_t ri = s_it;
+    __syncthreads();
+    if (ri >= nrows) break;
+    const uint32_t u = rows[ri];
+    const uint64_t W = wu[u - ua];
+    const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
+    const uint64_t span_w = a.S - 1 - u;
+    const int lg = max(6, log2_ceil(2 * (W < span_w ? W : span_w)));
+    if (lg > TLG) {  // a row beyond its tier (a binning bug): fail the call, never overrun LDS
+      if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+      continue;
+    }
+    const uint32_t T = 1u << lg, mask = T - 1;
+    const int shift = 32 - lg;
+    const uint32_t* fh;
+    uint64_t nf;
+    hp_first_hops(a, u, o0, du, &fh, &nf);
+    const uint64_t* fd = a.sdo + (fh - a.skeys);  // packed survivor entries (host: sdo and sorted lists)
+    uint32_t round = 0;
+    for (uint64_t base = 0; base < nf; base += HP_RNT) {
+      const uint64_t i = base + t;
+      uint64_t len = 0, st = 0;
+      double cv = 0.0;
+      if (i < nf) {
+        const uint64_t x = fd[i];
+        len = (uint32_t)(x >> HP_SDO_SH) & 0xffu;
+        st = x & ((1ull << HP_SDO_SH) - 1);
+        cv = a.g.ctab[x >> 48];
+      }
+      const uint64_t incl = block_incl_scan_1024(len, s_w);
+      s_incl[t] = incl;
+      s_start[t] = st;
+      s_iv[t] = 0u;
+      s_ic[t] = cv;
+      if (t == HP_RNT - 1) s_tot = incl;
+      __syncthreads();
+      // wedges in steps of one per thread, j ascending in the thread index:
+      // the additions of each w in the reference's order of v (predict.hxx:788, 828)
+      hp_wedges<HP_RNT, true>(s_tot, (uint32_t)t, (uint32_t)HP_RNT, s_incl, s_start, s_iv, a.g.keys,
+                              [&](bool ok, uint32_t w, uint32_t ent) {
+                                const bool in = ok && w > u;
+                                if (in) ++wedges;
+                                uint32_t h = 0;
+                                if (in) h = ho_find(tb, mask, shift, w, &a.ctr[HPC_ERR]);
+                                ho_add_block<8>(tb, in, h, s_ic[ent], &round);
+                              });
+      __syncthreads();
+    }
+    const uint32_t xu = a.xs ? a.xs[u] : 0u;
+    const bool ux = hp_use_etab(a, du - xu, W);
+    if (!ux)
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
+                [&](uint32_t x) { hp_mark<false>(tb, mask, shift, x); });
+    __syncthreads();
+    hp_drain<false, true, HP_UN, true, 0>(tb, T, (uint32_t)t, (uint32_t)HP_RNT, sg, a, u, du, tau, ux);
+    __syncthreads();  // (ho_take reset every used entry's owner token)
   }
   hp_finish(sg, a, wedges);
 }

@@ -2170,6 +2170,22 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       nlp_status sh = run_hub(g, a, lists[1] + q0[1], n1, nullptr, 0, wu, ua, custom, scan, tcnt + 11, &b1_done, st);
       if (sh != NLP_OK) return sh;
     }
+    if (n1 && !b1_done && custom && a.sdo && a.ssorted && g->hp_rowb) {
+      // AA / RA: bin 1 (W+ <= 2048) by table tier (k_hp_rowo), ordered tables over 256 threads
+      TRY(hipMemsetAsync(tcnt + 16, 0, 9 * sizeof(uint32_t), st));
+      const unsigned gt = (unsigned)std::min<uint64_t>((n1 + NT - 1) / NT, 512);
+      const uint64_t rt0 = g->hp_rowb >= 2 ? 0 : HP_RTIER0, rt1 = HP_RTIER1;
+      hipLaunchKernelGGL(k_hp_tier<false>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[1] + q0[1]), n1,
+                         (const uint64_t*)wu, ua, tcnt + 16, tlist1, rt0, rt1);
+      hipLaunchKernelGGL(k_hp_tier<true>, dim3(gt), dim3(NT), 0, st, (const uint32_t*)(lists[1] + q0[1]), n1,
+                         (const uint64_t*)wu, ua, tcnt + 16, tlist1, rt0, rt1);
+      TRY(hipGetLastError());
+      const unsigned grw = (unsigned)std::min<uint64_t>(n1, 4096);
+      hipLaunchKernelGGL((k_hp_rowo<2048>), dim3(grw), dim3(HP_RNT), 0, st, a, (const uint32_t*)tlist1, (const uint32_t*)(tcnt + 16), 0, wu, ua, tcnt + 22);
+      hipLaunchKernelGGL((k_hp_rowo<4096>), dim3(grw), dim3(HP_RNT), 0, st, a, (const uint32_t*)tlist1, (const uint32_t*)(tcnt + 16), 1, wu, ua, tcnt + 23);
+      TRY(hipGetLastError());
+      b1_done = true;
+    }
     if (n1 && !b1_done && !custom && a.kdeg && g->hp_rowb) {
       // count metrics: bin 1 by table tier (k_hp_rowb), 256-thread workgroups
       TRY(hipMemsetAsync(tcnt + 16, 0, 9 * sizeof(uint32_t), st));
