@@ -1132,19 +1132,23 @@ __device__ __forceinline__ uint32_t hp_dsurv8(uint64_t word, uint32_t H) {
   return m;
 }
 
+// smask[(wt - t0) * 64 + lane]: bit q = entry wt * 512 + 8 lane + q survives
+// (k_dc_place reads these 64 bytes per wave tile instead of its 512 class bytes)
 __global__ __launch_bounds__(NT) void k_dc_count(const uint8_t* __restrict__ dcls, uint32_t H, uint64_t e0, uint64_t e1,
-                                                 uint32_t* __restrict__ tcn) {
+                                                 uint32_t* __restrict__ tcn, uint8_t* __restrict__ smask) {
   const int lane = lane_id();
   const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
   for (uint64_t wt = t0 + (uint64_t)blockIdx.x * NWAVE + wave_id(); wt < t1; wt += (uint64_t)gridDim.x * NWAVE) {
     uint64_t word;
     hp_dword(dcls, wt * HP_WTILE + (uint64_t)lane * 8, e0, e1, &word);
-    const uint64_t c = wave_sum((uint64_t)__popc(hp_dsurv8(word, H)));
+    const uint32_t m = hp_dsurv8(word, H);
+    smask[(wt - t0) * 64 + lane] = (uint8_t)m;
+    const uint64_t c = wave_sum((uint64_t)__popc(m));
     if (lane == 0) tcn[wt - t0] = (uint32_t)c;
   }
 }
 
-__global__ __launch_bounds__(NT) void k_dc_place(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
+__global__ __launch_bounds__(NT) void k_dc_place(GraphView g, const uint8_t* __restrict__ smask,
                                                  uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
                                                  const uint32_t* __restrict__ tile_row,
                                                  const uint64_t* __restrict__ tpre, uint64_t* __restrict__ se,
@@ -1154,9 +1158,8 @@ __global__ __launch_bounds__(NT) void k_dc_place(GraphView g, const uint8_t* __r
   const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE;
   for (uint64_t wt = t0 + (uint64_t)blockIdx.x * NWAVE + wv; wt < t1; wt += (uint64_t)gridDim.x * NWAVE) {
     const uint64_t eb = wt * HP_WTILE + (uint64_t)lane * 8;
-    uint64_t word;
-    hp_dword(dcls, eb, e0, e1, &word);
-    uint32_t m = hp_dsurv8(word, H);
+    uint32_t m = smask[(wt - t0) * 64 + lane];
+    if (__ballot(m != 0) == 0) continue;  // no survivor in the wave tile: no row ends needed
     const uint64_t tr = tile_row[wt];
     const uint64_t r0 = tr > ua ? tr - ua : 0;
     const uint64_t rl = r0 + lane;

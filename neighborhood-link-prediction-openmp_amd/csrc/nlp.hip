@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR, B_HP_SMASK,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -1834,7 +1834,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(wsget(ws, B_HP_TCNT, nt, &tcn));
       TRY(wsget(ws, B_HP_TPRE, nt + 1, &tpre));
       const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
-      hipLaunchKernelGGL(k_dc_count, dim3(gt), dim3(NT), 0, st, (const uint8_t*)g->dcls, p.H, e0, e1, tcn);
+      uint8_t* smask;
+      TRY(wsget(ws, B_HP_SMASK, nt * 64, &smask));
+      hipLaunchKernelGGL(k_dc_count, dim3(gt), dim3(NT), 0, st, (const uint8_t*)g->dcls, p.H, e0, e1, tcn, smask);
       TRY(hipGetLastError());
       TRY(wsget(ws, B_SCAN2, scan_scratch_words(nt) + 16, &scan2));
       TRY(scan_ws<uint32_t>(ws, B_SCAN2, tcn, nt, tpre, tpre + nt, st));
@@ -1847,7 +1849,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(wsget(ws, B_HP_SR, std::max<uint64_t>(ns, 1), &sr));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(ns, 1), &s_skeys));
       TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(ns, 1), &s_sdo));
-      hipLaunchKernelGGL(k_dc_place, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
+      hipLaunchKernelGGL(k_dc_place, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)smask, ua, nU, e0, e1,
                          (const uint32_t*)g->tile_row, (const uint64_t*)tpre, se, sr);
       if (ns)
         hipLaunchKernelGGL(k_dc_gather, dim3((unsigned)std::min<uint64_t>((ns + NT - 1) / NT, 65536)), dim3(NT), 0, st,

@@ -8,6 +8,7 @@
 #   c5pmc   -- FETCH_SIZE / WRITE_SIZE passes of that range call
 #   sweep   -- tools/sweep.py SWEEP_ARGS
 #   sweepprof -- the same under rocprofv3 --kernel-trace --stats
+#   sweeppmc  -- the same under one --pmc pass of the counters in PMC
 # Output in gpurun_out/$TAG.  Every GPU step has its own time limit and the
 # script stops at the first failure.
 set -u
@@ -49,6 +50,8 @@ for s in ${STEPS//,/ }; do
     sweep) run sweep 900 python3 tools/sweep.py ${SWEEP_ARGS:-} ;;
     sweepprof) (cd /tmp && export TMPDIR=/tmp && run sweepprof 900 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d "$OUT/sweepprof" -o sweep -- python3 $REPO/tools/sweep.py ${SWEEP_ARGS:-}) || exit 1 ;;
+    sweeppmc) (cd /tmp && export TMPDIR=/tmp && run sweeppmc 600 rocprofv3 --kernel-trace --pmc ${PMC:-SQ_WAVE_CYCLES} \
+                 --output-format csv -d "$OUT/sweeppmc" -o pmc -- python3 $REPO/tools/sweep.py ${SWEEP_ARGS:-}) || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
