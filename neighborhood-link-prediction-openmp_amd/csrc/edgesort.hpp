@@ -34,10 +34,8 @@
 namespace nlp {
 
 constexpr int ES_NT = 512;                 // threads per tile
-constexpr int ES_NW = ES_NT / 64;          // 8 waves
 constexpr int ES_IPT = 8;                  // records per thread
 constexpr int ES_WCH = 64 * ES_IPT;        // 512 consecutive records per wave
-constexpr int ES_TILE = ES_NT * ES_IPT;    // 4096 records per tile
 constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
 constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
 constexpr uint32_t ES_SPIN_LIMIT = 1u << 26;
@@ -105,13 +103,15 @@ __device__ __forceinline__ uint64_t es_load(const uint64_t* p) {
 
 // FIRST: the input is the candidate columns (cu, cw, cs); else records `in`.
 // The output is always records (`out`: the caller's edges on the last pass).
-template <bool FIRST>
-__global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+template <bool FIRST, int NTH = ES_NT>  // NTH threads: tiles of NTH x ES_IPT records
+__global__ __launch_bounds__(NTH) void k_es_pass(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                                                    const float* __restrict__ cs, const EdgeOut* __restrict__ in,
                                                    EdgeOut* __restrict__ out, uint64_t n, int vb, int shift,
                                                    const uint32_t* __restrict__ ghist, uint64_t* __restrict__ desc,
                                                    uint32_t* __restrict__ ticket, uint64_t epoch,
                                                    uint32_t* __restrict__ err) {
+  constexpr int ES_NW = NTH / 64, ES_TILE = NTH * ES_IPT;
+  static_assert(NTH >= 256, "threads 0-255 own one digit each");
   __shared__ uint32_t s_u[ES_TILE], s_w[ES_TILE], s_s[ES_TILE];
   __shared__ uint8_t s_d[ES_TILE];         // each tile position's digit (the write phase does not recompute it)
   __shared__ uint32_t s_wc[ES_NW][256];   // per wave: running digit counts, then wave prefixes
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
   const uint64_t ep = epoch << 48;
   while (true) {
     if (t == 0) s_tile = atomicAdd(ticket, 1u);
-    for (int i = t; i < ES_NW * 256; i += ES_NT) (&s_wc[0][0])[i] = 0;
+    for (int i = t; i < ES_NW * 256; i += NTH) (&s_wc[0][0])[i] = 0;
     __syncthreads();
     const uint64_t tile = s_tile;
     if (tile >= ntiles) break;  // uniform: every wave leaves
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass(const uint32_t* __restrict__ 
     }
     __syncthreads();
     // write the digit runs: consecutive tile positions -> consecutive output records
-    for (uint32_t p = (uint32_t)t; p < tn; p += ES_NT) {
+    for (uint32_t p = (uint32_t)t; p < tn; p += NTH) {
       const uint32_t u = s_u[p], w = s_w[p], sb = s_s[p];
       const uint32_t d = s_d[p];
       const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);

@@ -279,6 +279,8 @@ struct nlp_graph {
                              // 0 count + fill kernels (NLP_HASH_ONE)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
+  unsigned occ_es256 = 256;  // the same, 256-thread tiles
+  int es_nt = ES_NT;         // record-pass workgroup size (NLP_ES_NT=256: 2048-record tiles, twice the tiles per CU)
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
@@ -761,6 +763,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
+  if (const char* en = getenv("NLP_ES_NT")) g->es_nt = atoi(en) == 256 ? 256 : ES_NT;
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
@@ -797,6 +800,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
+    TRY(occ((const void*)k_es_pass<false, 256>, &g->occ_es256, 256));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1573,7 +1577,9 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
     LAUNCH(k_es_copy, n, st, cu, cw, cs, n, out);
     return hipGetLastError() == hipSuccess ? NLP_OK : NLP_ERR_DEVICE;
   }
-  const uint64_t ntiles = (n + ES_TILE - 1) / ES_TILE;
+  const int nth = g->es_nt;
+  const uint64_t tile = (uint64_t)nth * ES_IPT;
+  const uint64_t ntiles = (n + tile - 1) / tile;
   uint64_t* desc;
   EdgeOut* tmp = nullptr;
   TRY(wsget(ws, B_ES_DESC, ntiles * 256, &desc));
@@ -1583,12 +1589,19 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
     g->es_desc_bytes = ws.bytes[B_ES_DESC];
     g->es_epoch = 0;
   }
-  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es));
+  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, nth == 256 ? g->occ_es256 : g->occ_es));
   const EdgeOut* src = nullptr;
   for (int r = 0; r < P; ++r) {
     EdgeOut* dst = ((P - 1 - r) & 1) ? tmp : out;  // the last pass writes `out`
     const uint64_t ep = ++g->es_epoch;
-    if (r == 0)
+    if (nth == 256 && r == 0)
+      hipLaunchKernelGGL((k_es_pass<true, 256>), dim3(gr), dim3(256), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst,
+                         n, vb, 8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+    else if (nth == 256)
+      hipLaunchKernelGGL((k_es_pass<false, 256>), dim3(gr), dim3(256), 0, st, (const uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, (const float*)nullptr, src, dst, n, vb, 8 * run[r],
+                         (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
+    else if (r == 0)
       hipLaunchKernelGGL(k_es_pass<true>, dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst, n, vb,
                          8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
     else
