@@ -76,8 +76,6 @@ struct HpArgs {
   const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
   const uint32_t* xs;    // per row: entries of N(u) at or below u (null: none; the exclusion starts after them)
   unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
-  int xp;                  // experiment (NLP_HB_XP, wrong results): 1 skip k_hp_batch's exclusion, 2 its emission,
-                           // 4 its wedge inserts
   uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
   uint32_t uxf;            // rows whose exclusion slice exceeds uxf x W test the membership table (HP_UX_OFF: never)
 };
@@ -2097,7 +2095,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
                                         const uint32_t sl = s_islot[wv][ent];
                                         if (w > s_u[wv][sl]) {
                                           ++wedges;
-                                          if (!(a.xp & 4)) h64_insert<10>(t64, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
+                                          h64_insert<10>(t64, mask, shift, (sl << wbits) | w, dw, &a.ctr[HPC_ERR]);
                                         }
                                       }, a.kdeg);
       } else {
@@ -2118,7 +2116,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     // (marking from N(u) measured faster here than a membership-table line per entry)
     // (prefetching the first block of these keys during the wedge phase measured
     // slower: 46.6 -> 52.7 ms on C3 JAC H=16)
-    const uint32_t NNs = (a.xp & 1) ? 0u : __builtin_amdgcn_readfirstlane(NN);
+    const uint32_t NNs = __builtin_amdgcn_readfirstlane(NN);
     for (uint32_t x0 = 0; x0 < NNs; x0 += 64 * UN) {
       uint32_t key[UN], sl[UN];
       const uint32_t nq = min((uint32_t)UN, (NNs - x0 + 63) / 64);
@@ -2148,7 +2146,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     // drain: every entry scored for its own row (a list of the claimed slots
     // instead of this scan measured slower: the claims cost more in the insert
     // loop than the scan of empty slots)
-    const uint32_t Ts = (a.xp & 8) ? 0u : __builtin_amdgcn_readfirstlane(T);  // xp 8 (with 4): no drain scan
+    const uint32_t Ts = __builtin_amdgcn_readfirstlane(T);
     for (uint32_t i0 = 0; i0 < Ts; i0 += 64 * UN) {
       uint32_t kq[UN], c[UN], v0[UN], v1[UN], dw[UN];
       const uint32_t nq = min((uint32_t)UN, (Ts - i0) / 64);  // T: a power of two >= 64
@@ -2191,7 +2189,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
           if (CUSTOM) s = ho_score(c[q]);
           else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & (KD ? 1023u : HP_CMASK)), du2, (uint64_t)dw[q]);
         }
-        hp_emit(sg, a, valid && !(a.xp & 2), s, uu, w, tau);
+        hp_emit(sg, a, valid, s, uu, w, tau);
       }
     }
     wave_sync_lds();

@@ -271,16 +271,12 @@ struct nlp_graph {
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
-  int hb_var = 0;            // experiment (NLP_HB_VAR): k_hp_batch KD build -- 0: 8 loads per lane, 1: 4, 2: 4 + 3 waves
                              // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
-  int hb_xp = 0;             // experiment (NLP_HB_XP): k_hp_batch phases skipped (wrong results; timing only)
   bool hp_win = true;        // k_hp_batch reserves emission windows (NLP_HASH_WIN=0: one reservation per flush)
   int hp_one = 2;            // survivor lists: 2 three streaming kernels (k_dc_*), 1 one pass (k_hp_dcls_one),
                              // 0 count + fill kernels (NLP_HASH_ONE)
   uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
   unsigned occ_es = 256;     // resident k_es_pass workgroups
-  unsigned occ_es256 = 256;  // the same, 256-thread tiles
-  int es_nt = ES_NT;         // record-pass workgroup size (NLP_ES_NT=256: 2048-record tiles, twice the tiles per CU)
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
@@ -763,13 +759,10 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
-  if (const char* en = getenv("NLP_ES_NT")) g->es_nt = atoi(en) == 256 ? 256 : ES_NT;
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = atoi(ho);
-  if (const char* hv = getenv("NLP_HB_VAR")) g->hb_var = atoi(hv);
-  if (const char* hx = getenv("NLP_HB_XP")) g->hb_xp = atoi(hx);
   if (const char* hw = getenv("NLP_HASH_WIN")) g->hp_win = hw[0] != '0';
   if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
   if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
@@ -800,7 +793,6 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
-    TRY(occ((const void*)k_es_pass<false, 256>, &g->occ_es256, 256));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1577,9 +1569,7 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
     LAUNCH(k_es_copy, n, st, cu, cw, cs, n, out);
     return hipGetLastError() == hipSuccess ? NLP_OK : NLP_ERR_DEVICE;
   }
-  const int nth = g->es_nt;
-  const uint64_t tile = (uint64_t)nth * ES_IPT;
-  const uint64_t ntiles = (n + tile - 1) / tile;
+  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES_IPT - 1) / ((uint64_t)ES_NT * ES_IPT);
   uint64_t* desc;
   EdgeOut* tmp = nullptr;
   TRY(wsget(ws, B_ES_DESC, ntiles * 256, &desc));
@@ -1589,19 +1579,12 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
     g->es_desc_bytes = ws.bytes[B_ES_DESC];
     g->es_epoch = 0;
   }
-  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, nth == 256 ? g->occ_es256 : g->occ_es));
+  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es));
   const EdgeOut* src = nullptr;
   for (int r = 0; r < P; ++r) {
     EdgeOut* dst = ((P - 1 - r) & 1) ? tmp : out;  // the last pass writes `out`
     const uint64_t ep = ++g->es_epoch;
-    if (nth == 256 && r == 0)
-      hipLaunchKernelGGL((k_es_pass<true, 256>), dim3(gr), dim3(256), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst,
-                         n, vb, 8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
-    else if (nth == 256)
-      hipLaunchKernelGGL((k_es_pass<false, 256>), dim3(gr), dim3(256), 0, st, (const uint32_t*)nullptr,
-                         (const uint32_t*)nullptr, (const float*)nullptr, src, dst, n, vb, 8 * run[r],
-                         (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
-    else if (r == 0)
+    if (r == 0)
       hipLaunchKernelGGL(k_es_pass<true>, dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const EdgeOut*)nullptr, dst, n, vb,
                          8 * run[r], (const uint32_t*)(hw + run[r] * 256), desc, tick + r, ep, err);
     else
@@ -2100,7 +2083,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.sdo = s_sdo;
     a.sua = ua;
     a.xs = g->xs;
-    a.xp = g->hb_xp;
     a.win = 0;
     a.uxf = g->hp_uxf;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
@@ -2150,10 +2132,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         }
         TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
         if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 1) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 1>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 2) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 4, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 3) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 8, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg && g->hb_var == 4) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true, 2, 3>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());

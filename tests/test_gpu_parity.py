@@ -409,7 +409,8 @@ class _env:
 
 
 # path 4 (hash accumulation) with every kernel forced: 0 default (bin-0 row
-# batches, hub pass, one-pass survivor lists, record-sort final order), 1
+# batches, tiered bin-1 rows, hub pass, survivor lists by k_dc_*, exclusion of
+# wide rows by the membership table, record-sort final order), 1
 # workgroup/LDS, 2 hub pass for every row, 3 k_hp_part over a tiny scratch
 # (bucket groups and direct accumulation), 4 k_hp_part with one bucket per row
 # (sub-range passes), 5 bin 0 as one 1024-entry launch (no table-size tiers),
@@ -418,24 +419,24 @@ class _env:
 # 10 k_hp_part for every row, 11 hub pass with one w-bucket per row (direct
 # counters for the counts), 12 the same with 128-entry item tables and no
 # direct counters (heavy buckets split into w-range items by their segment
-# histograms), 13 bin-1 rows by the hub pass, 14 the hub pass's AA /
-# RA items by the ordered re-walk instead of sort mode, 15/16 sort-mode items
-# of at most 16 / 40 wedges (heavy buckets split, single fine ranges beyond
-# flagged HH_BIG), 17 survivor lists from in-edge atomics (unordered: the AA /
-# RA row kernels sort them), 18 no entry-degree tables (deg w gathered at the
-# drain), 19 = 17 with bin-1 rows, 20 row batches gathering deg / off of every
-# first hop (no packed survivor entries), 21 survivor suffixes searched per call
-# (no per-graph rank bytes), 22 survivor counts and fill as two kernels (not
-# k_dc_count / place / gather), 23 the one-pass build (k_hp_dcls_one) with its
-# output capacity overflowing (the two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
-# above u), 25 the row batches' 4-loads / 3-waves build, 26 the row batches
-# reserving every flush (no emission windows, no padding), 27 hub pass with
-# one w-bucket per row and 64-wide direct counters (heavy buckets grouped into
-# direct ranges, single bins beyond by HH_WIDE sub-ranges), 28 bin-1 count
-# rows by k_hp_block (not the tiered k_hp_rowb), 29 / 30 every bin-1 row in
-# the 8192- / at least the 4096-entry tier, 31-33 the first-order exclusion
-# of every row by the membership table (row batches and wave rows; bin-1
-# tiers; k_hp_block), 34 every row by marks, 35 the one-pass survivor build
+# histograms), 13 bin-1 rows by the hub pass, 14 the hub pass's AA / RA items
+# by the ordered re-walk instead of sort mode, 15/16 sort-mode items of at
+# most 16 / 40 wedges (heavy buckets split, single bins beyond flagged
+# HH_BIG), 17 survivor lists from in-edge atomics (unordered: the AA / RA row
+# kernels sort them), 18 no entry-degree tables (deg w gathered at the drain),
+# 19 = 17 with bin-1 rows, 20 row batches gathering deg / off of every first
+# hop (no packed survivor entries), 21 survivor suffixes searched per call (no
+# per-graph rank bytes), 22 survivor counts and fill as two kernels, 23 the
+# one-pass build (k_hp_dcls_one) with its output capacity overflowing (the
+# two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
+# above u), 25 the row batches reserving every flush (no emission windows, no
+# padding), 26 hub pass with one w-bucket per row and 64-wide direct counters
+# (heavy buckets grouped into direct ranges, single bins beyond by HH_WIDE
+# sub-ranges), 27 bin-1 rows by k_hp_block (not the tiered k_hp_rowb /
+# k_hp_rowo), 28 / 29 every bin-1 row in the 8192- / at least the 4096-entry
+# tier, 30-32 the first-order exclusion of every row by the membership table
+# (row batches and wave rows; bin-1 tiers; k_hp_block), 33 every row by
+# marks, 34 the one-pass survivor build
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -450,7 +451,7 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"), dict(NLP_HB_VAR="2"),
+                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"),
                  dict(NLP_HASH_WIN="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
