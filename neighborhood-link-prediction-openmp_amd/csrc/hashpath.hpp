@@ -2435,7 +2435,8 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
   __shared__ uint64_t s_start[HP_RNT];
   __shared__ uint32_t s_iv[HP_RNT];
   __shared__ uint64_t s_w[NW];
-  __shared__ uint64_t s_tot, s_it;
+  __shared__ uint64_t s_tot;
+  __shared__ uint32_t s_tk[3];
   __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
   __shared__ float s_gs[NW][HP_BSTG];
   const int t = threadIdx.x, wv = wave_id();
@@ -2447,27 +2448,56 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
+  // Rows from the work queue in a three-stage pipeline: while row `cur` runs,
+  // the next row's data (its W+, bounds, exclusion start, survivor range) and
+  // the row id of the one after are in flight, and a further ticket is drawn
+  // (a workgroup barrier waits for LDS only), so a row pays no queue or row
+  // data round trip of its own.
+  struct RowInfo {
+    uint32_t u;
+    uint64_t W, o0, du, xu, s0, ns;
+  };
+  auto info = [&](bool ok, uint32_t uu) {
+    RowInfo r{0u, 0, 0, 0, 0, 0, 0};
+    if (!ok) return r;
+    r.u = uu;
+    r.W = wu[uu - ua];
+    r.o0 = a.g.off[uu];
+    r.du = a.g.off[uu + 1] - r.o0;
+    r.xu = a.xs ? a.xs[uu] : 0u;
+    r.s0 = a.soff ? a.soff[uu - a.sua] : 0ull;
+    r.ns = a.soff ? a.soff[uu - a.sua + 1] - r.s0 : r.du;
+    return r;
+  };
+  if (t == 0) {
+    s_tk[0] = atomicAdd(queue, 1u);
+    s_tk[1] = atomicAdd(queue, 1u);
+    s_tk[2] = atomicAdd(queue, 1u);
+  }
   __syncthreads();
-  for (;;) {
-    if (t == 0) s_it = atomicAdd(queue, 1u);
-    __syncthreads();
-    const uint64_t ri = s_it;
-    __syncthreads();
-    if (ri >= nrows) break;
-    const uint32_t u = rows[ri];
-    const uint64_t W = wu[u - ua];
-    const uint64_t o0 = a.g.off[u], du = a.g.off[u + 1] - o0;
+  const uint64_t k0 = s_tk[0], k1 = s_tk[1];
+  uint64_t cur = k0, nx = k1, nn = s_tk[2];
+  RowInfo ci = info(k0 < nrows, k0 < nrows ? rows[k0] : 0u);
+  uint32_t nxu = k1 < nrows ? rows[k1] : 0u;
+  __syncthreads();
+  while (cur < nrows) {
+    const RowInfo ni = info(nx < nrows, nxu);  // in flight during this row
+    const uint32_t nnu = nn < nrows ? rows[nn] : 0u;
+    uint32_t tk = 0;
+    if (t == 0) tk = atomicAdd(queue, 1u);
+    const uint32_t u = ci.u;
+    const uint64_t W = ci.W, o0 = ci.o0, du = ci.du;
     const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
     const int lg = max(6, log2_ceil(2 * (W < span_w ? W : span_w)));
+    bool skip = false;
     if (lg > TLG) {  // a row beyond its tier (a binning bug): fail the call, never overrun LDS
       if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
-      continue;
+      skip = true;
     }
-    const uint32_t T = 1u << lg, mask = T - 1;
-    const int shift = 32 - lg;
-    const uint32_t* fh;
-    uint64_t nf;
-    hp_first_hops(a, u, o0, du, &fh, &nf);
+    const uint32_t T = 1u << (skip ? 6 : lg), mask = T - 1;
+    const int shift = 32 - (skip ? 6 : lg);
+    const uint32_t* fh = a.soff ? a.skeys + ci.s0 : a.g.keys + o0;
+    const uint64_t nf = skip ? 0 : ci.ns;
     // packed survivor entries (the part of N(v) above u, no row-bound gather)
     const uint64_t* fd = a.sdo && a.soff ? a.sdo + (fh - a.skeys) : nullptr;
     for (uint64_t base = 0; base < nf; base += HP_RNT) {
@@ -2504,7 +2534,7 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
     // first-order exclusion: the entries of N(u) above u (a key <= u has no
     // entry) marked, or -- a slice beyond HB_XF times the row's wedge bound --
     // every entry tested in the membership table at the drain
-    const uint32_t xu = a.xs ? a.xs[u] : 0u;
+    const uint64_t xu = skip ? du : ci.xu;
     const bool ux = hp_use_etab(a, du - xu, W);
     if (!ux)
       hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
@@ -2538,6 +2568,13 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
       }
     }
     __syncthreads();
+    if (t == 0) s_tk[0] = tk;
+    __syncthreads();
+    cur = nx;
+    nx = nn;
+    nn = s_tk[0];
+    ci = ni;
+    nxu = nnu;
   }
   hp_finish(sg, a, wedges);
 }
