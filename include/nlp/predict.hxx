@@ -48,6 +48,7 @@
 #include <string>
 #include <tuple>
 #include <utility>
+#include <memory>
 #include <vector>
 
 #include "../nlp.h"
@@ -280,22 +281,17 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
   nlp_timing t{};
   uint64_t n = 0;
   const uint64_t me = o.maxEdges == size_t(-1) ? UINT64_MAX : uint64_t(o.maxEdges);
-  std::vector<nlp_edge> buf;
-  if (me == UINT64_MAX) {  // all candidates: predict once (count query), then fetch the kept result
-    check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat, nullptr, &n, &t),
-          "nlp_predict_ex");
-    buf.resize(n);
-    uint64_t got = 0;
-    check(nlp_copy_last(g.get(), buf.data(), n, &got), "nlp_copy_last");
-    n = got;
-  } else {
-    buf.resize(me);
-    check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat,
-                         me ? buf.data() : nullptr, &n, &t),
-          "nlp_predict_ex");
-  }
+  // a count query (the result stays on the device), then exactly the predicted
+  // links fetched: no host buffer of maxEdges records is allocated and cleared
+  // (main.cxx asks for |del|/2 links; a low hub threshold predicts a few)
+  check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat, nullptr, &n, &t),
+        "nlp_predict_ex");
+  std::unique_ptr<nlp_edge[]> buf(new nlp_edge[n ? n : 1]);  // default-initialised: written by the copy
+  uint64_t got = 0;
+  if (n) check(nlp_copy_last(g.get(), buf.get(), n, &got), "nlp_copy_last");
+  n = got;
   std::vector<std::tuple<K, K, W>> a(n);
-  const nlp_edge* b = buf.data();
+  const nlp_edge* b = buf.get();
 #pragma omp parallel for schedule(static)
   for (long long i = 0; i < (long long)n; ++i) a[size_t(i)] = std::tuple<K, K, W>(K(b[i].u), K(b[i].v), W(b[i].score));
   return PredictLinkResult<K, W>(std::move(a), t.total_ms, t.score_ms);
