@@ -632,8 +632,23 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
       c[q] = v0[q] = v1[q] = 0;
       if (ORD) w[q] = i < T ? ho_take(tb, i, &c[q]) : HP_EMPTY;
       else w[q] = i < T ? hp_take<GLOBAL, CUSTOM>(tb, i, &c[q], &v0[q], &v1[q]) : HP_EMPTY;
-      // ux: the first-order exclusion by the membership table (no marks were made)
-      if (ux && w[q] != HP_EMPTY && et_has(a.g.etab, a.g.etbits, u, w[q])) c[q] |= HP_EXCL;
+    }
+    if (ux) {  // the first-order exclusion by the membership table (no marks were made), two probes in flight
+#pragma unroll
+      for (int q0 = 0; q0 < UN; q0 += 2) {
+        uint64_t ek[2];
+        bool ea[2], er[2];
+#pragma unroll
+        for (int z = 0; z < 2; ++z) {
+          const int q = q0 + z;
+          ea[z] = q < UN && (uint32_t)q < nq && w[q] != HP_EMPTY;
+          ek[z] = ea[z] ? ((uint64_t)u << 32 | w[q]) : 0ull;
+        }
+        et_has_n<2>(a.g.etab, a.g.etbits, ek, ea, er);
+#pragma unroll
+        for (int z = 0; z < 2; ++z)
+          if (q0 + z < UN && er[z]) c[q0 + z] |= HP_EXCL;
+      }
     }
     if (ORD) {
 #pragma unroll
@@ -2172,6 +2187,29 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
           dw[q] = KD ? hp_kd_deg<10>(a.g, c[q], w) : a.g.deg[w];
         }
       }
+      // first-order exclusion by the membership table for the entries of
+      // table-tested rows: four first buckets in flight at a time
+#pragma unroll
+      for (int q0 = 0; q0 < UN; q0 += 4) {
+        if ((uint32_t)q0 >= nq) break;
+        uint64_t ek[4];
+        bool ea[4], er[4];
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const int q = q0 + z;
+          const bool valid = q < UN && (uint32_t)q < nq && kq[q] != HP_EMPTY;
+          const uint32_t sl = valid ? kq[q] >> wbits : 0u;
+          ea[z] = valid && s_ux[wv][sl];
+          ek[z] = ea[z] ? ((uint64_t)s_u[wv][sl] << 32 | (kq[q] & wmask)) : 0ull;
+        }
+        et_has_n<4>(a.g.etab, a.g.etbits, ek, ea, er);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          if (q0 + z >= UN) break;
+          etq += ea[z] ? 1 : 0;
+          if (er[z]) c[q0 + z] |= HP_EXCL;
+        }
+      }
 #pragma unroll
       for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
@@ -2180,10 +2218,6 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         const uint32_t sl = valid ? kq[q] >> wbits : 0u, w = kq[q] & wmask;
         const uint32_t uu = s_u[wv][sl];
         const uint64_t du2 = s_du[wv][sl];
-        if (valid && s_ux[wv][sl]) {  // first-order exclusion by the membership table
-          ++etq;
-          if (et_has(a.g.etab, a.g.etbits, uu, w)) c[q] |= HP_EXCL;
-        }
         float s = 0.0f;
         if (valid) {
           if (CUSTOM) s = ho_score(c[q]);
@@ -2555,9 +2589,19 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
         }
       }
 #pragma unroll
-      for (int q = 0; q < HP_UN; ++q) {
-        dw[q] = kq[q] != HP_EMPTY ? hp_kd_deg<13>(a.g, c[q], kq[q]) : 0u;
-        if (ux && kq[q] != HP_EMPTY && et_has(a.g.etab, a.g.etbits, u, kq[q])) c[q] |= HP_EXCL;
+      for (int q = 0; q < HP_UN; ++q) dw[q] = kq[q] != HP_EMPTY ? hp_kd_deg<13>(a.g, c[q], kq[q]) : 0u;
+      if (ux) {  // the membership table, both probes in flight
+        uint64_t ek[HP_UN];
+        bool ea[HP_UN], er[HP_UN];
+#pragma unroll
+        for (int q = 0; q < HP_UN; ++q) {
+          ea[q] = kq[q] != HP_EMPTY;
+          ek[q] = ea[q] ? ((uint64_t)u << 32 | kq[q]) : 0ull;
+        }
+        et_has_n<HP_UN>(a.g.etab, a.g.etbits, ek, ea, er);
+#pragma unroll
+        for (int q = 0; q < HP_UN; ++q)
+          if (er[q]) c[q] |= HP_EXCL;
       }
 #pragma unroll
       for (int q = 0; q < HP_UN; ++q) {

@@ -87,6 +87,51 @@ __device__ __forceinline__ bool et_has(const uint64_t* __restrict__ tab, uint32_
   return false;
 }
 
+// et_has for N keys at once: the first buckets of all N are loaded before any
+// is compared (one round trip for the N instead of N dependent ones); a key
+// whose first bucket is full without it probes on (rare at half load).
+__device__ __forceinline__ bool et_has_from(const uint64_t* __restrict__ tab, uint32_t bits, uint64_t key, uint64_t b) {
+  const uint64_t mask = (1ull << bits) - 1;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const ulonglong2* p = (const ulonglong2*)(tab + b * ET_SLOTS);
+    const ulonglong2 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const uint64_t s[ET_SLOTS] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+    bool hit = false, open = false;
+#pragma unroll
+    for (int i = 0; i < ET_SLOTS; ++i) {
+      hit |= s[i] == key;
+      open |= s[i] == ET_EMPTY;
+    }
+    if (hit) return true;
+    if (open) return false;
+    b = (b + 1) & mask;
+  }
+  return false;
+}
+template <int N>
+__device__ __forceinline__ void et_has_n(const uint64_t* __restrict__ tab, uint32_t bits, const uint64_t (&key)[N],
+                                         const bool (&act)[N], bool (&res)[N]) {
+  ulonglong2 q[N][4];
+  uint64_t b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    b[i] = et_mix(key[i]) >> (64 - bits);
+    const ulonglong2* p = (const ulonglong2*)(tab + (act[i] ? b[i] : 0ull) * ET_SLOTS);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[i][j] = act[i] ? p[j] : make_ulonglong2(ET_EMPTY, ET_EMPTY);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    bool hit = false, open = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hit |= q[i][j].x == key[i] || q[i][j].y == key[i];
+      open |= q[i][j].x == ET_EMPTY || q[i][j].y == ET_EMPTY;
+    }
+    res[i] = act[i] && (hit || (!open && et_has_from(tab, bits, key[i], (b[i] + 1) & ((1ull << bits) - 1))));
+  }
+}
+
 // number of entries <= x in the sorted list a[0..n)
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* __restrict__ a, uint32_t n, uint32_t x) {
   uint32_t lo = 0, hi = n;
