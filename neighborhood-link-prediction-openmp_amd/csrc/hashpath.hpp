@@ -2188,23 +2188,28 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         }
       }
       // first-order exclusion by the membership table for the entries of
-      // table-tested rows: four first buckets in flight at a time
+      // table-tested rows (count tables: two first buckets in flight at a time)
 #pragma unroll
-      for (int q0 = 0; q0 < UN; q0 += 4) {
+      for (int q0 = 0; q0 < UN; q0 += 2) {
         if ((uint32_t)q0 >= nq) break;
-        uint64_t ek[4];
-        bool ea[4], er[4];
+        uint64_t ek[2];
+        bool ea[2], er[2];
 #pragma unroll
-        for (int z = 0; z < 4; ++z) {
+        for (int z = 0; z < 2; ++z) {
           const int q = q0 + z;
           const bool valid = q < UN && (uint32_t)q < nq && kq[q] != HP_EMPTY;
           const uint32_t sl = valid ? kq[q] >> wbits : 0u;
           ea[z] = valid && s_ux[wv][sl];
           ek[z] = ea[z] ? ((uint64_t)s_u[wv][sl] << 32 | (kq[q] & wmask)) : 0ull;
         }
-        et_has_n<4>(a.g.etab, a.g.etbits, ek, ea, er);
+        if (CUSTOM) {
 #pragma unroll
-        for (int z = 0; z < 4; ++z) {
+          for (int z = 0; z < 2; ++z) er[z] = ea[z] && et_has(a.g.etab, a.g.etbits, (uint32_t)(ek[z] >> 32), (uint32_t)ek[z]);
+        } else {
+          et_has_n<2>(a.g.etab, a.g.etbits, ek, ea, er);
+        }
+#pragma unroll
+        for (int z = 0; z < 2; ++z) {
           if (q0 + z >= UN) break;
           etq += ea[z] ? 1 : 0;
           if (er[z]) c[q0 + z] |= HP_EXCL;
