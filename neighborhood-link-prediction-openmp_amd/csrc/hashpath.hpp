@@ -423,8 +423,10 @@ constexpr int HP_STG = 128;
 // the slice: a high-degree row with a few low-degree neighbours would read
 // thousands of keys for a handful of entries.  C4 JAC H=16, row batches: 18.8
 // ms with marks only, 18.8 / 16.4 / 14.8 / 14.6 / 14.2 ms at factors 8 / 4 / 2 /
-// 1 / 0 (every row by the table); the whole call is fastest at 1.
-constexpr uint64_t HB_XF = 1;
+// 1 / 0 (every row by the table); uk-2005's neighbourhoods favour the marks (C3
+// AA H=16: 106 / 100 / 97 ms at 1 / 2 / 4): 2 is within 1 % of the best on
+// both.
+constexpr uint64_t HB_XF = 2;
 constexpr uint32_t HP_UX_OFF = 0xffffffffu;
 __device__ __forceinline__ bool hp_use_etab(const HpArgs& a, uint64_t dx, uint64_t W) {
   return a.g.etab && a.uxf != HP_UX_OFF && dx > (uint64_t)a.uxf * W;
