@@ -26,7 +26,8 @@
 //               never clears the previous pass's descriptors, it ignores
 //               another epoch); the tile is reordered by digit in LDS and
 //               written out in digit runs (consecutive lanes, consecutive
-//               12-byte records: coalesced stores)
+//               12-byte records: coalesced stores; (u, w) staged as one
+//               8-byte word, the digit recomputed at the write)
 #pragma once
 #include "kernels.hpp"
 #include "prims.hpp"
@@ -112,8 +113,8 @@ __global__ __launch_bounds__(NTH) void k_es_pass(const uint32_t* __restrict__ cu
                                                    uint32_t* __restrict__ err) {
   constexpr int ES_NW = NTH / 64, ES_TILE = NTH * ES_IPT;
   static_assert(NTH >= 256, "threads 0-255 own one digit each");
-  __shared__ uint32_t s_u[ES_TILE], s_w[ES_TILE], s_s[ES_TILE];
-  __shared__ uint8_t s_d[ES_TILE];         // each tile position's digit (the write phase does not recompute it)
+  __shared__ uint64_t s_uw[ES_TILE];       // w << 32 | u: one 8-byte LDS write and read per record
+  __shared__ uint32_t s_s[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];   // per wave: running digit counts, then wave prefixes
   __shared__ uint64_t s_gofs[256];        // global position of the tile's first record of each digit
   __shared__ uint32_t s_lofs[256];        // tile position of the first record of each digit
@@ -242,17 +243,16 @@ __global__ __launch_bounds__(NTH) void k_es_pass(const uint32_t* __restrict__ cu
       const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
       if (q < tn) {
         const uint32_t p = s_lofs[dg[i]] + s_wc[wv][dg[i]] + rk[i];
-        s_u[p] = ru[i];
-        s_w[p] = rw[i];
+        s_uw[p] = (uint64_t)rw[i] << 32 | ru[i];
         s_s[p] = rs[i];
-        s_d[p] = (uint8_t)dg[i];
       }
     }
     __syncthreads();
     // write the digit runs: consecutive tile positions -> consecutive output records
     for (uint32_t p = (uint32_t)t; p < tn; p += NTH) {
-      const uint32_t u = s_u[p], w = s_w[p], sb = s_s[p];
-      const uint32_t d = s_d[p];
+      const uint64_t uw = s_uw[p];
+      const uint32_t u = (uint32_t)uw, w = (uint32_t)(uw >> 32), sb = s_s[p];
+      const uint32_t d = es_digit(u, w, __uint_as_float(sb), vb, shift);  // recomputed: cheaper than a byte in LDS
       const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);
       out[pos] = EdgeOut{u, w, __uint_as_float(sb)};
     }
