@@ -2463,18 +2463,18 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_block(HpArgs a, const uint32_t* _
 constexpr int HP_RNT = 256;
 constexpr uint64_t HP_RTIER0 = 1024, HP_RTIER1 = 2048;
 
-template <int LT>
-__global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __restrict__ tl,
+template <int LT, int RNT = HP_RNT>  // RNT threads per row
+__global__ __launch_bounds__(RNT) void k_hp_rowb(HpArgs a, const uint32_t* __restrict__ tl,
                                                     const uint32_t* __restrict__ tcnt, int tier,
                                                     const uint64_t* __restrict__ wu, uint64_t ua,
                                                     uint32_t* __restrict__ queue) {
-  constexpr int NW = HP_RNT / 64;
+  constexpr int NW = RNT / 64;
   constexpr int TLG = LT == 2048 ? 11 : LT == 4096 ? 12 : 13;
   static_assert((1 << TLG) == LT, "table sizes 2048, 4096, 8192");
   __shared__ uint64_t s_t[LT];
-  __shared__ uint64_t s_incl[HP_RNT];
-  __shared__ uint64_t s_start[HP_RNT];
-  __shared__ uint32_t s_iv[HP_RNT];
+  __shared__ uint64_t s_incl[RNT];
+  __shared__ uint64_t s_start[RNT];
+  __shared__ uint32_t s_iv[RNT];
   __shared__ uint64_t s_w[NW];
   __shared__ uint64_t s_tot;
   __shared__ uint32_t s_tk[3];
@@ -2485,7 +2485,7 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
   hb_region(tcnt, tier, tier, &rbase, &nrows);
   const uint32_t* rows = tl + rbase;
   if (nrows == 0) return;
-  for (int i = t; i < LT; i += HP_RNT) s_t[i] = HP_EMPTY64;
+  for (int i = t; i < LT; i += RNT) s_t[i] = HP_EMPTY64;
   HpStage sg{s_gu[wv], s_gw[wv], s_gs[wv], HP_BSTG, 0, 0, 0};
   const int64_t tau = *a.tau;
   uint64_t wedges = 0;
@@ -2541,7 +2541,7 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
     const uint64_t nf = skip ? 0 : ci.ns;
     // packed survivor entries (the part of N(v) above u, no row-bound gather)
     const uint64_t* fd = a.sdo && a.soff ? a.sdo + (fh - a.skeys) : nullptr;
-    for (uint64_t base = 0; base < nf; base += HP_RNT) {
+    for (uint64_t base = 0; base < nf; base += RNT) {
       const uint64_t i = base + t;
       uint64_t len = 0, st = 0;
       if (i < nf) {
@@ -2561,9 +2561,9 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
       s_incl[t] = incl;
       s_start[t] = st;
       s_iv[t] = 0u;
-      if (t == HP_RNT - 1) s_tot = incl;
+      if (t == RNT - 1) s_tot = incl;
       __syncthreads();
-      hp_wedges<HP_RNT, false, true>(s_tot, (uint32_t)t, (uint32_t)HP_RNT, s_incl, s_start, s_iv, a.g.keys,
+      hp_wedges<RNT, false, true>(s_tot, (uint32_t)t, (uint32_t)RNT, s_incl, s_start, s_iv, a.g.keys,
                                      [&](uint32_t w, uint32_t, uint32_t dw) {
                                        if (w > u) {
                                          ++wedges;
@@ -2578,14 +2578,14 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
     const uint64_t xu = skip ? du : ci.xu;
     const bool ux = hp_use_etab(a, du - xu, W);
     if (!ux)
-      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)RNT,
                 [&](uint32_t x) { h64_mark(s_t, mask, shift, x); });
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < T; i0 += HP_RNT * HP_UN) {  // T >= 64: uniform per wave
+    for (uint32_t i0 = 0; i0 < T; i0 += RNT * HP_UN) {  // T >= 64: uniform per wave
       uint32_t kq[HP_UN], c[HP_UN], dw[HP_UN];
 #pragma unroll
       for (int q = 0; q < HP_UN; ++q) {
-        const uint32_t i = i0 + (uint32_t)q * HP_RNT + (uint32_t)t;
+        const uint32_t i = i0 + (uint32_t)q * RNT + (uint32_t)t;
         kq[q] = HP_EMPTY;
         c[q] = 0;
         if (i < T) {
@@ -2633,19 +2633,20 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowb(HpArgs a, const uint32_t* __
 // The same tiers for AA / RA (custom bin 1: W+ <= 2048): an ordered table
 // (ho_add_block's owner tokens over 256 threads) of 2048 or 4096 entries,
 // S(u) in ascending v (the degree-class lists are sorted by construction).
-template <int LT>
-__global__ __launch_bounds__(HP_RNT) void k_hp_rowo(HpArgs a, const uint32_t* __restrict__ tl,
+template <int LT, int RNT = HP_RNT>  // RNT threads per row (a power of two)
+__global__ __launch_bounds__(RNT) void k_hp_rowo(HpArgs a, const uint32_t* __restrict__ tl,
                                                     const uint32_t* __restrict__ tcnt, int tier,
                                                     const uint64_t* __restrict__ wu, uint64_t ua,
                                                     uint32_t* __restrict__ queue) {
-  constexpr int NW = HP_RNT / 64;
+  constexpr int NW = RNT / 64;
+  static_assert(RNT == 128 || RNT == 256, "owner tokens of 7 or 8 thread bits");
   constexpr int TLG = LT == 2048 ? 11 : 12;
   static_assert((1 << TLG) == LT, "table sizes 2048, 4096");
   __shared__ uint32_t s_k[LT], s_c[LT], s_o[LT];  // keys, float accumulators, owner tokens
-  __shared__ uint64_t s_incl[HP_RNT];
-  __shared__ uint64_t s_start[HP_RNT];
-  __shared__ uint32_t s_iv[HP_RNT];
-  __shared__ double s_ic[HP_RNT];
+  __shared__ uint64_t s_incl[RNT];
+  __shared__ uint64_t s_start[RNT];
+  __shared__ uint32_t s_iv[RNT];
+  __shared__ double s_ic[RNT];
   __shared__ uint64_t s_w[NW];
   __shared__ uint64_t s_tot, s_it;
   __shared__ uint32_t s_gu[NW][HP_BSTG], s_gw[NW][HP_BSTG];
@@ -2656,7 +2657,7 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowo(HpArgs a, const uint32_t* __
   const uint32_t* rows = tl + rbase;
   if (nrows == 0) return;
   const HpTable tb{s_k, s_c, s_o, s_o};
-  for (int i = t; i < LT; i += HP_RNT) {
+  for (int i = t; i < LT; i += RNT) {
     s_k[i] = HP_EMPTY;
     s_c[i] = 0;
     s_o[i] = 0;
@@ -2687,7 +2688,7 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowo(HpArgs a, const uint32_t* __
     hp_first_hops(a, u, o0, du, &fh, &nf);
     const uint64_t* fd = a.sdo + (fh - a.skeys);  // packed survivor entries (host: sdo and sorted lists)
     uint32_t round = 0;
-    for (uint64_t base = 0; base < nf; base += HP_RNT) {
+    for (uint64_t base = 0; base < nf; base += RNT) {
       const uint64_t i = base + t;
       uint64_t len = 0, st = 0;
       double cv = 0.0;
@@ -2702,27 +2703,27 @@ __global__ __launch_bounds__(HP_RNT) void k_hp_rowo(HpArgs a, const uint32_t* __
       s_start[t] = st;
       s_iv[t] = 0u;
       s_ic[t] = cv;
-      if (t == HP_RNT - 1) s_tot = incl;
+      if (t == RNT - 1) s_tot = incl;
       __syncthreads();
       // wedges in steps of one per thread, j ascending in the thread index:
       // the additions of each w in the reference's order of v (predict.hxx:788, 828)
-      hp_wedges<HP_RNT, true>(s_tot, (uint32_t)t, (uint32_t)HP_RNT, s_incl, s_start, s_iv, a.g.keys,
+      hp_wedges<RNT, true>(s_tot, (uint32_t)t, (uint32_t)RNT, s_incl, s_start, s_iv, a.g.keys,
                               [&](bool ok, uint32_t w, uint32_t ent) {
                                 const bool in = ok && w > u;
                                 if (in) ++wedges;
                                 uint32_t h = 0;
                                 if (in) h = ho_find(tb, mask, shift, w, &a.ctr[HPC_ERR]);
-                                ho_add_block<8>(tb, in, h, s_ic[ent], &round);
+                                ho_add_block<RNT == 128 ? 7 : 8>(tb, in, h, s_ic[ent], &round);
                               });
       __syncthreads();
     }
     const uint32_t xu = a.xs ? a.xs[u] : 0u;
     const bool ux = hp_use_etab(a, du - xu, W);
     if (!ux)
-      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)HP_RNT,
+      hp_stream(a.g.keys + o0 + xu, du - xu, (uint32_t)t, (uint32_t)RNT,
                 [&](uint32_t x) { hp_mark<false>(tb, mask, shift, x); });
     __syncthreads();
-    hp_drain<false, true, HP_UN, true, 0>(tb, T, (uint32_t)t, (uint32_t)HP_RNT, sg, a, u, du, tau, ux);
+    hp_drain<false, true, HP_UN, true, 0>(tb, T, (uint32_t)t, (uint32_t)RNT, sg, a, u, du, tau, ux);
     __syncthreads();  // (ho_take reset every used entry's owner token)
   }
   hp_finish(sg, a, wedges);
