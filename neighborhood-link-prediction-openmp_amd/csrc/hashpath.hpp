@@ -68,7 +68,8 @@ struct HpArgs {
   // small H: the surviving first hops of every source of the range (S(u) =
   // {v in N(u) : deg v <= H}, multiplicities kept, any order), so a row walks
   // S(u) instead of all of N(u) with a degree gather per entry (null: N(u))
-  const uint64_t* soff;  // [nU + 1], indexed by u - sua
+  const uint64_t* soff;  // [nU + 1], indexed by u - sua: S(u) = skeys[soff[u - sua], + |S(u)|)
+  const uint32_t* scn;   // |S(u)|, indexed by u - sua (null: soff[u - sua + 1] - soff[u - sua])
   const uint32_t* skeys;
   uint64_t sua;
   int ssorted;  // S(u) in N(u)'s (ascending) order: the AA / RA row kernels skip their sort
@@ -95,13 +96,19 @@ __global__ void k_hp_xs(const uint64_t* __restrict__ off, const uint32_t* __rest
 }
 constexpr int HP_SDO_SH = 40;  // offsets < 2^40 (guarded at the list build)
 
+// S(u)'s start in skeys / sdo and its length (the class-ordered short lists
+// leave gaps between rows: lengths from scn)
+__device__ __forceinline__ uint64_t hp_slen(const HpArgs& a, uint32_t u, uint64_t s0) {
+  return a.scn ? (uint64_t)a.scn[u - a.sua] : a.soff[u - a.sua + 1] - s0;
+}
+
 // A row's first-hop list: S(u) when the survivor lists exist, else N(u).
 __device__ __forceinline__ void hp_first_hops(const HpArgs& a, uint32_t u, uint64_t o0, uint64_t du,
                                               const uint32_t** list, uint64_t* n) {
   if (a.soff) {
     const uint64_t s0 = a.soff[u - a.sua];
     *list = a.skeys + s0;
-    *n = a.soff[u - a.sua + 1] - s0;
+    *n = hp_slen(a, u, s0);
   } else {
     *list = a.g.keys + o0;
     *n = du;
@@ -1241,6 +1248,139 @@ __global__ __launch_bounds__(NT) void k_dc_gather(GraphView g, const uint8_t* __
   }
 }
 
+// ---------------------------------------------------------------- class-ordered short lists (per graph)
+// The count metrics do not depend on the order of S(u).  So the graph keeps,
+// per row, its short entries -- v with 1 <= deg v <= HP_DCLS_MAX, packed as
+// the survivor lists are (key v, deg v << 48 | n << 40 | o) -- ordered by
+// deg v: S(u) for any H up to the classes kept is a prefix of the row's list,
+// and a call only measures the prefixes (k_sl_rows: a search of each row's
+// classes, W+(u) from the per-graph prefix of n) instead of compacting the
+// range's classes and gathering off[v] per survivor.  Built once in
+// nlp_graph_create from the degree-class compaction at the classes kept
+// (k_dc_*), then k_sl_sort and k_sl_prefix.
+
+// k_sl_sort: a wave per row, stable by class.  Rows of at most 64 entries rank
+// every lane against every other; longer rows count their classes in an LDS
+// histogram, scan it, and place 64 entries per step ranked by a ballot
+// multisplit on the class (cursor advanced by the last lane of each class).
+__global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo, uint64_t S,
+                                                const uint32_t* __restrict__ ikeys, const uint64_t* __restrict__ isdo,
+                                                uint32_t* __restrict__ okeys, uint64_t* __restrict__ osdo,
+                                                uint8_t* __restrict__ ocls) {
+  __shared__ uint32_t s_h[NWAVE][256];
+  const int lane = lane_id(), wv = wave_id();
+  for (uint64_t u = (uint64_t)blockIdx.x * NWAVE + wv; u < S; u += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t s = lo[u], n = lo[u + 1] - s;
+    if (n == 0) continue;
+    if (n <= 64) {
+      const bool ok = (uint64_t)lane < n;
+      const uint64_t sd = ok ? isdo[s + lane] : 0ull;
+      const uint32_t key = ok ? ikeys[s + lane] : 0u;
+      const uint32_t c = ok ? (uint32_t)(sd >> 48) : 0xffffu;
+      uint32_t rank = 0;
+      for (int j = 0; j < (int)n; ++j) {
+        const uint32_t cj = __shfl(c, j, 64);
+        rank += (cj < c || (cj == c && j < lane)) ? 1u : 0u;
+      }
+      if (ok) {
+        okeys[s + rank] = key;
+        osdo[s + rank] = sd;
+        ocls[s + rank] = (uint8_t)c;
+      }
+      continue;
+    }
+    for (int q = lane; q < 256; q += 64) s_h[wv][q] = 0;
+    wave_sync_lds();
+    for (uint64_t j = lane; j < n; j += 64) atomicAdd(&s_h[wv][(uint32_t)(isdo[s + j] >> 48) & 255u], 1u);
+    wave_sync_lds();
+    {
+      uint32_t h[4], t = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        h[q] = s_h[wv][4 * lane + q];
+        t += h[q];
+      }
+      uint32_t ex = (uint32_t)wave_incl_scan((uint64_t)t) - t;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s_h[wv][4 * lane + q] = ex;
+        ex += h[q];
+      }
+    }
+    wave_sync_lds();
+    for (uint64_t j0 = 0; j0 < n; j0 += 64) {
+      const uint64_t j = j0 + lane;
+      const bool ok = j < n;
+      const uint64_t sd = ok ? isdo[s + j] : 0ull;
+      const uint32_t key = ok ? ikeys[s + j] : 0u;
+      const uint32_t c = (uint32_t)(sd >> 48) & 255u;
+      uint64_t m = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (c >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+      }
+      const uint32_t base = s_h[wv][c];
+      wave_sync_lds();
+      if (ok) {
+        const uint64_t p = s + base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+        okeys[p] = key;
+        osdo[p] = sd;
+        ocls[p] = (uint8_t)c;
+        if ((m >> lane) == 1ull) s_h[wv][c] = base + (uint32_t)__popcll(m);  // the class's last lane
+      }
+      wave_sync_lds();
+    }
+  }
+}
+
+// k_sl_prefix: pn[i] = the inclusive prefix of n over the row's sorted list (a wave per row)
+__global__ __launch_bounds__(NT) void k_sl_prefix(const uint64_t* __restrict__ lo, uint64_t S,
+                                                  const uint64_t* __restrict__ sdo, uint32_t* __restrict__ pn) {
+  const int lane = lane_id(), wv = wave_id();
+  for (uint64_t u = (uint64_t)blockIdx.x * NWAVE + wv; u < S; u += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t s = lo[u], n = lo[u + 1] - s;
+    uint64_t carry = 0;
+    for (uint64_t j0 = 0; j0 < n; j0 += 64) {
+      const uint64_t j = j0 + lane;
+      const uint64_t x = j < n ? (sdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
+      const uint64_t incl = wave_incl_scan(x) + carry;
+      if (j < n) pn[s + j] = (uint32_t)incl;
+      carry = __shfl(incl, 63, 64);
+    }
+  }
+}
+
+// k_sl_rows: a thread per row of the range: |S(u)| = the length of the row's
+// prefix of classes <= H (galloping, then binary search: a few dependent byte
+// probes for most rows, ~2 log2 |list| for a hub), W+(u) = pn at its end.
+// Writes W+(u) and |S(u)| directly (no atomics, no unpack).
+__global__ void k_sl_rows(const uint64_t* __restrict__ lo, const uint8_t* __restrict__ cls,
+                          const uint32_t* __restrict__ pn, uint32_t H, uint64_t ua, uint64_t nU,
+                          uint32_t* __restrict__ cnt, unsigned long long* __restrict__ wu) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nU; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = lo[ua + r], e = lo[ua + r + 1];
+    uint64_t a = s, b = e, step = 1;  // [s, a) <= H; the end of the prefix lies in [a, b]
+    while (a < b) {
+      const uint64_t p = a + step - 1 < b - 1 ? a + step - 1 : b - 1;
+      if (cls[p] <= H) {
+        a = p + 1;
+        step <<= 1;
+      } else {
+        b = p;
+        break;
+      }
+    }
+    while (a < b) {
+      const uint64_t m = (a + b) >> 1;
+      if (cls[m] <= H) a = m + 1; else b = m;
+    }
+    cnt[r] = (uint32_t)(a - s);
+    wu[r] = a > s ? pn[a - 1] : 0u;
+  }
+}
+
 // ---------------------------------------------------------------- survivor lists in one pass
 // k_hp_dcls_rows8 + scan + k_hp_dcls_fill8 read the range's degree classes
 // twice (C4 H=16: 3.3 + 8.5 ms) and walk each lane's eight entries with a
@@ -1971,7 +2111,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
     if ((uint32_t)lane < n) {
       *pW = wu[uu - ua];
       *ps0 = a.soff[uu - a.sua];
-      *pns = (uint32_t)(a.soff[uu - a.sua + 1] - *ps0);
+      *pns = (uint32_t)hp_slen(a, uu, *ps0);
       const uint64_t ob = a.g.off[uu];
       *pdu = (uint32_t)(a.g.off[uu + 1] - ob);
       const uint32_t xu = a.xs ? a.xs[uu] : 0u;
@@ -2507,7 +2647,7 @@ __global__ __launch_bounds__(RNT) void k_hp_rowb(HpArgs a, const uint32_t* __res
     r.du = a.g.off[uu + 1] - r.o0;
     r.xu = a.xs ? a.xs[uu] : 0u;
     r.s0 = a.soff ? a.soff[uu - a.sua] : 0ull;
-    r.ns = a.soff ? a.soff[uu - a.sua + 1] - r.s0 : r.du;
+    r.ns = a.soff ? hp_slen(a, uu, r.s0) : r.du;
     return r;
   };
   if (t == 0) {
@@ -3071,7 +3211,7 @@ __global__ void k_hh_rows(HpArgs a, const uint32_t* __restrict__ l2, uint64_t n2
       if (pd > HH_PMAX) pd = HH_PMAX;
       shift = (uint32_t)log2_ceil((span_w + pd - 1) / pd);
       P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
-      if (a.soff) nf = a.soff[u - a.sua + 1] - a.soff[u - a.sua];
+      if (a.soff) nf = hp_slen(a, u, a.soff[u - a.sua]);
       else nf = a.g.off[u + 1] - a.g.off[u];
       items = nf ? (uint32_t)std::min<uint64_t>((W + HH_WC - 1) / HH_WC, 0x7fffffffull) : 0u;
       if (items == 0) P = 0;  // no first hop or no wedge: no candidate

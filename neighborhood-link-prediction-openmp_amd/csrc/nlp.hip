@@ -253,6 +253,14 @@ struct nlp_graph {
   uint32_t* kdeg = nullptr;                    // deg keys[e] per adjacency entry (path 4's count-metric row kernels)
   uint8_t* drank = nullptr;                    // entries with deg v <= 254: the row's rank in N(v) (survivor suffixes)
   uint32_t* xs = nullptr;                      // per row: entries of N(u) at or below u (the exclusion walks the rest)
+  // class-ordered short lists (hashpath.hpp k_sl_sort): per row its entries v with 1 <= deg v <= 254 by deg v
+  uint64_t* sl_off = nullptr;                  // [S + 1] row offsets
+  uint32_t* sl_keys = nullptr;                 // v
+  uint64_t* sl_sdo = nullptr;                  // deg v << 48 | n << 40 | o (as the survivor lists)
+  uint8_t* sl_cls = nullptr;                   // deg v
+  uint32_t* sl_pn = nullptr;                   // inclusive prefix of n over the row's list (W+(u) of a prefix)
+  uint64_t sl_n = 0;
+  uint32_t sl_cap = 0;                         // classes kept: S(u) for H <= sl_cap
   // evaluation (main.cxx:48-57): sorted directed deletion keys, and the last prediction's device output
   uint64_t* truth = nullptr;
   uint64_t ntruth = 0;
@@ -402,6 +410,8 @@ void destroy_graph(nlp_graph* g) {
   if (g->kdeg) (void)hipFree(g->kdeg);
   if (g->drank) (void)hipFree(g->drank);
   if (g->xs) (void)hipFree(g->xs);
+  for (void* p : {(void*)g->sl_off, (void*)g->sl_keys, (void*)g->sl_sdo, (void*)g->sl_cls, (void*)g->sl_pn})
+    if (p) (void)hipFree(p);
   if (g->truth) (void)hipFree(g->truth);
   g->ws.release();
   if (!g->symmetric) {
@@ -442,6 +452,119 @@ int bits_for(uint64_t maxval) {  // bits needed to represent values <= maxval
   int b = 0;
   while (b < 64 && (maxval >> b)) ++b;
   return b;
+}
+
+// Class-ordered short lists (hashpath.hpp k_sl_sort): the degree-class
+// compaction at H = HP_DCLS_MAX over the whole graph (k_dc_count, scan,
+// k_dc_place, k_dc_gather: the rows' short entries in N(u)'s order, packed,
+// with their rows), the row offsets from the per-row counts, then the stable
+// per-row sort by class.  Skipped -- the calls then compact per call -- when
+// the lists and their build scratch would take more than a quarter of the free
+// HBM; any allocation failure also just skips them.
+template <typename T>
+bool dmalloc(T** out, uint64_t n) {  // device allocation of n items; a failure is cleared and reported as false
+  void* x = nullptr;
+  if (hipMalloc(&x, std::max<uint64_t>(n, 1) * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return false;
+  }
+  *out = (T*)x;
+  return true;
+}
+
+struct DevTemps {  // device scratch freed on scope exit
+  std::vector<void*> p;
+  ~DevTemps() {
+    for (void* x : p) (void)hipFree(x);
+  }
+  template <typename T>
+  bool get(T** out, uint64_t n) {
+    if (!dmalloc(out, n)) return false;
+    p.push_back(*out);
+    return true;
+  }
+};
+
+nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
+  hipStream_t st = g->stream;
+  const uint64_t S = g->span, M = g->nnz;
+  const uint64_t nt = (M + HP_WTILE - 1) / HP_WTILE;
+  DevTemps tmp;
+  uint32_t* tcn;
+  uint64_t *tpre, *scr;
+  uint8_t* smask;
+  if (!tmp.get(&tcn, nt) || !tmp.get(&tpre, nt + 1) || !tmp.get(&smask, nt * 64) ||
+      !tmp.get(&scr, scan_scratch_words(std::max(nt, S)) + 16))
+    return NLP_OK;
+  const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
+  size_t fr = 0, tot = 0;
+  TRY(hipMemGetInfo(&fr, &tot));
+  // the classes kept: up to HP_DCLS_MAX, fewer (128, 64, 32, 16) while the lists and their build would take more
+  // than a quarter of the free HBM (peak 29 B per short entry + 20 B per row; kept 17 B + 8 B)
+  uint64_t L = 0;
+  for (;;) {
+    hipLaunchKernelGGL(k_dc_count, dim3(gt), dim3(NT), 0, st, (const uint8_t*)g->dcls, cap, 0ull, M, tcn, smask);
+    TRY(hipGetLastError());
+    TRY(scan_excl_u64<uint32_t>(tcn, nt, tpre, tpre + nt, scr, st));
+    TRY(hipMemcpyAsync(&L, tpre + nt, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (debug_on()) fprintf(stderr, "nlp: short lists: classes <= %u: %llu entries, %zu bytes free\n", cap,
+                            (unsigned long long)L, fr);
+    if (L == 0) return NLP_OK;
+    if (29 * L + 20 * S <= fr / 4) break;
+    if (cap <= 16) return NLP_OK;
+    cap = cap > 128 ? 128 : cap / 2;
+  }
+  uint64_t* se;
+  uint32_t *sr, *tkeys, *scnt;
+  uint64_t* tsdo;
+  unsigned long long* wu;
+  if (!tmp.get(&se, L) || !tmp.get(&sr, L) || !tmp.get(&tkeys, L) || !tmp.get(&tsdo, L) || !tmp.get(&wu, S) ||
+      !tmp.get(&scnt, S))
+    return NLP_OK;
+  GraphView gv0{};
+  gv0.off = g->off;
+  gv0.keys = g->keys;
+  gv0.deg = g->deg;
+  TRY(hipMemsetAsync(wu, 0, S * 8, st));
+  hipLaunchKernelGGL(k_dc_place, dim3(gt), dim3(NT), 0, st, gv0, (const uint8_t*)smask, 0ull, S, 0ull, M,
+                     (const uint32_t*)g->tile_row, (const uint64_t*)tpre, se, sr);
+  hipLaunchKernelGGL(k_dc_gather, dim3((unsigned)std::min<uint64_t>((L + NT - 1) / NT, 65536)), dim3(NT), 0, st, gv0,
+                     (const uint8_t*)g->dcls, (const uint8_t*)g->drank, (const uint64_t*)se, (const uint32_t*)sr, L,
+                     tkeys, tsdo, wu);
+  TRY(hipGetLastError());
+  LAUNCH(k_hp_unpack, S, st, wu, scnt, S);
+  TRY(hipGetLastError());
+  TRY(hipStreamSynchronize(st));
+  for (void* x : {(void*)se, (void*)sr}) {  // entries and rows are done with: room for the sorted copy
+    (void)hipFree(x);
+    tmp.p.erase(std::find(tmp.p.begin(), tmp.p.end(), x));
+  }
+  nlp_graph& G = *g;
+  if (!dmalloc(&G.sl_off, S + 1) || !dmalloc(&G.sl_keys, L) || !dmalloc(&G.sl_sdo, L) || !dmalloc(&G.sl_cls, L) ||
+      !dmalloc(&G.sl_pn, L)) {
+    for (void* p : {(void*)G.sl_off, (void*)G.sl_keys, (void*)G.sl_sdo, (void*)G.sl_cls, (void*)G.sl_pn})
+      if (p) (void)hipFree(p);
+    G.sl_off = nullptr;
+    G.sl_keys = nullptr;
+    G.sl_sdo = nullptr;
+    G.sl_cls = nullptr;
+    G.sl_pn = nullptr;
+    return NLP_OK;
+  }
+  TRY(scan_excl_u64<uint32_t>(scnt, S, G.sl_off, G.sl_off + S, scr, st));
+  hipLaunchKernelGGL(k_sl_sort, dim3((unsigned)std::min<uint64_t>((S + NWAVE - 1) / NWAVE, 65536)), dim3(NT), 0, st,
+                     (const uint64_t*)G.sl_off, S, (const uint32_t*)tkeys, (const uint64_t*)tsdo, G.sl_keys, G.sl_sdo,
+                     G.sl_cls);
+  TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_sl_prefix, dim3((unsigned)std::min<uint64_t>((S + NWAVE - 1) / NWAVE, 65536)), dim3(NT), 0, st,
+                     (const uint64_t*)G.sl_off, S, (const uint64_t*)G.sl_sdo, G.sl_pn);
+  TRY(hipGetLastError());
+  TRY(hipStreamSynchronize(st));
+  G.sl_n = L;
+  G.sl_cap = cap;
+  return NLP_OK;
 }
 
 // Build everything derived from off/keys (already on the device).
@@ -626,6 +749,15 @@ nlp_status finish_graph(nlp_graph* g) {
     } else {
       (void)hipGetLastError();
       g->dcls = nullptr;
+    }
+  }
+  {  // class-ordered short lists (the count metrics' S(u) as row prefixes; NLP_HASH_SLIST=0: per-call
+     // compaction, =c: classes up to c at most)
+    const char* sl = getenv("NLP_HASH_SLIST");
+    const uint32_t cap = sl ? (uint32_t)std::min<long>(std::max<long>(atol(sl), 0), HP_DCLS_MAX) : HP_DCLS_MAX;
+    if (g->dcls && g->drank && M > 0 && M < (1ull << HP_SDO_SH) && cap > 0) {
+      nlp_status s1 = build_short_lists(g, cap);
+      if (s1 != NLP_OK) return s1;
     }
   }
   // Exact membership table of the entries w > u for the first-order exclusion
@@ -1804,6 +1936,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint32_t* s_skeys = nullptr;
   bool s_sorted = false;       // S(u) in N(u)'s order (degree-class compaction)
   uint64_t* s_sdo = nullptr;   // packed S(u) entries (deg v, off[v]) of the degree-class lists
+  const uint32_t* s_scn = nullptr;  // |S(u)| when S(u) are prefixes of the class-ordered short lists
   uint64_t* scan2 = nullptr;
   {
     TRY(hipMemsetAsync(wu, 0, nU * 8, st));
@@ -1819,7 +1952,24 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
     bool one_done = false;
-    if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 2 && g->hp_sdo && g->drank && p.H >= 1 &&
+    if (g->sl_off && !custom && g->hp_dcls && g->hp_work_surv && g->hp_sdo && p.H >= 1 && p.H <= g->sl_cap) {
+      // count metrics: S(u) = the prefix of u's class-ordered short list (deg v <= H); only the
+      // prefixes' lengths and W+(u) are found (hashpath.hpp k_sl_count)
+      uint32_t* scnt;
+      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
+      hipLaunchKernelGGL(k_sl_rows, dim3(grid_full(nU)), dim3(NT), 0, st, (const uint64_t*)g->sl_off,
+                         (const uint8_t*)g->sl_cls, (const uint32_t*)g->sl_pn, p.H, ua, nU, scnt,
+                         (unsigned long long*)wu);
+      TRY(hipGetLastError());
+      s_soff = g->sl_off + ua;
+      s_scn = scnt;
+      s_skeys = g->sl_keys;
+      s_sdo = g->sl_sdo;
+      s_sorted = false;
+      one_done = true;
+    }
+    if (one_done) {
+    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 2 && g->hp_sdo && g->drank && p.H >= 1 &&
         p.H <= HP_DCLS_MAX && e1 > e0 && g->nnz < (1ull << HP_SDO_SH)) {
       // count, place, gather (hashpath.hpp k_dc_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
@@ -2061,7 +2211,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(&g->host_small[41], pos + r1, 8, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t wchunk = g->host_small[41] - g->host_small[40];
-    HpArgs a;
+    HpArgs a{};
     a.g = gv;
     a.S = S;
     a.H = p.H;
@@ -2077,6 +2227,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.ctr = (unsigned long long*)small;
     a.one_bucket = g->hp_one_bucket;
     a.soff = s_skeys ? s_soff : nullptr;
+    a.scn = s_skeys ? s_scn : nullptr;
     a.skeys = s_skeys;
     a.ssorted = s_sorted ? 1 : 0;
     a.kdeg = g->kdeg;

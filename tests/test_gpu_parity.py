@@ -436,7 +436,10 @@ class _env:
 # k_hp_rowo), 28 / 29 every bin-1 row in the 8192- / at least the 4096-entry
 # tier, 30-32 the first-order exclusion of every row by the membership table
 # (row batches and wave rows; bin-1 tiers; k_hp_block), 33 every row by
-# marks, 34 the one-pass survivor build
+# marks, 34 the one-pass survivor build, 35 the count metrics' survivor lists
+# compacted per call (k_dc_*) instead of taken as prefixes of the per-graph
+# class-ordered short lists (variants 22, 23, 34 also compact per call), 36
+# short lists of the classes up to 3 only (H = 2 from them, H = 4, 16 compacted)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -450,15 +453,15 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
                  dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
-                 dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0"),
-                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5"), dict(NLP_HASH_XS="0"),
+                 dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0", NLP_HASH_SLIST="0"),
+                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5", NLP_HASH_SLIST="0"), dict(NLP_HASH_XS="0"),
                  dict(NLP_HASH_WIN="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"),
                  dict(NLP_HASH_UX="0"), dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off"),
-                 dict(NLP_HASH_ONE="1")]
+                 dict(NLP_HASH_ONE="1", NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
@@ -480,6 +483,23 @@ def test_gpu_hash_path_vs_oracle(gpu, oracle, golden, variant):
                             assert_canonical_equal(eu, ew, es, u, w, s)
                             assert t["wedges"] == info["wedges_gt"]
                             assert t["candidates"] == info["candidates"] and t["nan_candidates"] == info["nan"]
+
+
+def test_gpu_short_list_prefixes_up_to_class_254(gpu, oracle):
+    """The count metrics' S(u) as prefixes of the class-ordered short lists:
+    rows of hundreds of short entries of mixed classes (the sort's histogram
+    path), H at the classes' ends (1, 254) and just beyond them (255: per-call
+    lists), every chunk of a tiny emission buffer, a source range."""
+    off, keys = random_csr(3000, 60, 21)
+    with _env(NLP_HASH="1", NLP_HASH_EMIT="1"):
+        with gpu.Graph(off, keys) as G:
+            for m in (0, 1, 4, 8):
+                for H in (1, 7, 64, 254, 255):
+                    u, w, s, t = G.predict(m, H, 3000)
+                    eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=3000)
+                    assert t["path"] == 4
+                    assert_canonical_equal(eu, ew, es, u, w, s)
+                    assert t["wedges"] == info["wedges_gt"] and t["candidates"] == info["candidates"]
 
 
 def test_gpu_hash_path_all_candidates_and_min_score(gpu, golden, oracle):
