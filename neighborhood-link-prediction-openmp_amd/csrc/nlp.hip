@@ -75,7 +75,7 @@ enum Buf {
   B_HP_WU, B_HP_FLAGS, B_HP_POS, B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3, B_HP_SMALL, B_HP_TIEK0, B_HP_TIEK1,
   B_HP_TIEI0, B_HP_TIEI1, B_EVAL, B_MKEY, B_MBND, B_HP_TIER, B_HP_SCNT, B_HP_SOFF, B_HP_SKEYS,
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
-  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR, B_HP_SMASK,
+  B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR, B_HP_SMASK, B_HP_BPOS,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   NBUF
 };
@@ -1923,9 +1923,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   if (nU == 0 || g->nnz == 0) return NLP_OK;
   { nlp_status s0 = hp_alloc_scratch(g); if (s0 != NLP_OK) return s0; }
   uint64_t *wu, *pos, *small;
-  uint8_t* flags;
   TRY(wsget(ws, B_HP_WU, nU + 1, &wu));
-  TRY(wsget(ws, B_HP_FLAGS, (uint64_t)HP_NBINS * nU, &flags));
   TRY(wsget(ws, B_HP_POS, nU + 1, &pos));
   TRY(wsget(ws, B_HP_SMALL, 64, &small));
   uint64_t* scan;
@@ -1936,6 +1934,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint32_t* s_skeys = nullptr;
   bool s_sorted = false;       // S(u) in N(u)'s order (degree-class compaction)
   uint64_t* s_sdo = nullptr;   // packed S(u) entries (deg v, off[v]) of the degree-class lists
+  const uint64_t b1max = custom ? HP_BT / 4 : HP_B1_MAX;  // the largest W(u) of bin 1
   const uint32_t* s_scn = nullptr;  // |S(u)| when S(u) are prefixes of the class-ordered short lists
   uint64_t* scan2 = nullptr;
   {
@@ -1944,7 +1943,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(&g->host_small[9], g->off + ub, 8, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t e0 = g->host_small[8], e1 = g->host_small[9];
-    const uint64_t b1max = custom ? HP_BT / 4 : HP_B1_MAX;
     // small H: W(u) from the survivors' in-edges (P_H atomics) when that is well below the range's entries
     uint64_t p_h = ~0ull;
     if (p.H >= 1 && p.H <= DCAP && g->vbydeg && !g->deg_hist.empty()) {
@@ -2108,9 +2106,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
                          dim3((unsigned)std::min<uint64_t>((e1 - e0 + NT * HP_WR - 1) / (NT * HP_WR) + 1, 8192)),
                          dim3(NT), 0, st, gv, p.H, ua, nU, e0, e1, (const uint32_t*)g->tile_row,
                          (unsigned long long*)wu);
-    hipLaunchKernelGGL(k_hp_bin, dim3(grid_for(nU)), dim3(NT), 0, st, (const uint64_t*)g->off, ua, nU,
-                       (const uint64_t*)wu, flags, g->hp_minbin, b1max);
-    TRY(hipGetLastError());
   }
   uint32_t* lists[HP_NBINS];
   // bin-0 rows of a chunk by tier, then counters: [0, 6) tiers, [6, 9) work queues of bins 2, 3, 1,
@@ -2120,29 +2115,44 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint32_t* tcnt = tlist + nU;
   uint32_t* tlist1 = tlist + nU + 32;
   const int lb[HP_NBINS] = {B_HP_L0, B_HP_L1, B_HP_L2, B_HP_L3};
-  for (int b = 0; b < HP_NBINS; ++b) {
-    TRY(wsget(ws, lb[b], nU, &lists[b]));
-    TRY(scan_ws<uint8_t>(ws, B_SCAN, flags + (uint64_t)b * nU, nU, pos, small + 24 + b, st));
-    LAUNCH(k_hp_scatter, nU, st, flags + (uint64_t)b * nU, pos, nU, ua, lists[b]);
+  for (int b = 0; b < HP_NBINS; ++b) TRY(wsget(ws, lb[b], nU, &lists[b]));
+  {  // the bins' ascending row lists: count per tile, scan, scatter (hashpath.hpp k_hp_bins)
+    const uint64_t nbt = (nU + HP_BTILE - 1) / HP_BTILE;
+    uint32_t* bcnt;
+    uint64_t* bpos;
+    TRY(wsget(ws, B_HP_FLAGS, (uint64_t)HP_NBINS * nbt, &bcnt));
+    TRY(wsget(ws, B_HP_BPOS, (uint64_t)HP_NBINS * nbt + 1, &bpos));
+    const unsigned gb = (unsigned)std::min<uint64_t>(nbt, 8192);
+    hipLaunchKernelGGL(k_hp_bins<false>, dim3(gb), dim3(NT), 0, st, (const uint64_t*)g->off, ua, nU,
+                       (const uint64_t*)wu, g->hp_minbin, b1max, bcnt, (const uint64_t*)nullptr, lists[0], lists[1],
+                       lists[2], lists[3], small + 24);
+    TRY(hipGetLastError());
+    TRY(wsget(ws, B_SCAN2, scan_scratch_words(HP_NBINS * nbt) + 16, &scan2));
+    TRY(scan_ws<uint32_t>(ws, B_SCAN2, bcnt, HP_NBINS * nbt, bpos, bpos + HP_NBINS * nbt, st));
+    hipLaunchKernelGGL(k_hp_bins<true>, dim3(gb), dim3(NT), 0, st, (const uint64_t*)g->off, ua, nU,
+                       (const uint64_t*)wu, g->hp_minbin, b1max, bcnt, (const uint64_t*)bpos, lists[0], lists[1],
+                       lists[2], lists[3], small + 24);
     TRY(hipGetLastError());
   }
   if (g->hp_stats) {  // diagnostic: rows and wedge bounds per bin, W(u) by power of two
-    std::vector<uint64_t> hw(nU);
-    std::vector<uint8_t> hf((size_t)HP_NBINS * nU);
+    std::vector<uint64_t> hw(nU), nl(HP_NBINS);
     TRY(hipMemcpyAsync(hw.data(), wu, nU * 8, hipMemcpyDeviceToHost, st));
-    TRY(hipMemcpyAsync(hf.data(), flags, (uint64_t)HP_NBINS * nU, hipMemcpyDeviceToHost, st));
+    TRY(hipMemcpyAsync(nl.data(), small + 24, HP_NBINS * 8, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     uint64_t rows[HP_NBINS] = {}, wsum[HP_NBINS] = {}, lr[40] = {}, lw[40] = {};
-    for (uint64_t i = 0; i < nU; ++i)
-      for (int b = 0; b < HP_NBINS; ++b)
-        if (hf[(size_t)b * nU + i]) {
-          ++rows[b];
-          wsum[b] += hw[i];
-          int l = 0;
-          while ((1ull << l) < hw[i] && l < 39) ++l;
-          ++lr[l];
-          lw[l] += hw[i];
-        }
+    for (int b = 0; b < HP_NBINS; ++b) {
+      std::vector<uint32_t> hl(nl[b]);
+      TRY(hipMemcpy(hl.data(), lists[b], nl[b] * 4, hipMemcpyDeviceToHost));
+      for (uint32_t u : hl) {
+        const uint64_t w = hw[u - ua];
+        ++rows[b];
+        wsum[b] += w;
+        int l = 0;
+        while ((1ull << l) < w && l < 39) ++l;
+        ++lr[l];
+        lw[l] += w;
+      }
+    }
     for (int b = 0; b < HP_NBINS; ++b)
       fprintf(stderr, "[hash-stats] bin %d: rows %llu, W %llu\n", b, (unsigned long long)rows[b],
               (unsigned long long)wsum[b]);
