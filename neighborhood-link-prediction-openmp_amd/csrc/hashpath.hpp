@@ -1751,9 +1751,10 @@ constexpr int HP_NTIER = 3;
 __host__ __device__ constexpr uint64_t hp_tier_w(int t) { return t == 0 ? 128 : t == 1 ? 256 : HP_B0_MAX; }
 
 // tcnt: [0, 3) rows per tier (counted by the first pass), [3, 6) cursors.
-// Counts and cursor reservations are aggregated per workgroup in LDS (one
-// global atomic per workgroup and tier: a chip-wide stream of atomics on
-// three words serialises at their L2 channel).
+// A workgroup counts its rows per tier and (SCATTER) reserves its slots with
+// one global atomic per tier, then places its rows from LDS running offsets
+// (round 3 reserved per 256 rows: 6e5 atomics on three words serialised at
+// their L2 channel, 0.9 ms of the C4 H=16 call).
 template <bool SCATTER>
 __global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ rows, uint64_t nrows,
                                                 const uint64_t* __restrict__ wu, uint64_t ua,
@@ -1762,51 +1763,59 @@ __global__ __launch_bounds__(NT) void k_hp_tier(const uint32_t* __restrict__ row
   __shared__ uint32_t s_n[NWAVE][HP_NTIER];
   __shared__ uint32_t s_base[HP_NTIER];
   const int lane = lane_id(), wv = wave_id();
-  uint32_t tb[HP_NTIER] = {0, 0, 0};
-  if (SCATTER)
-    for (int q = 1; q < HP_NTIER; ++q) tb[q] = tb[q - 1] + tcnt[q - 1];
-  uint32_t cnt[HP_NTIER] = {0, 0, 0};  // COUNT pass: this thread's rows per tier (lane 0 holds the wave's)
+  auto tier_of = [&](uint64_t i, uint32_t* pu) -> int {
+    if (i >= nrows) return -1;
+    const uint32_t u = rows[i];
+    *pu = u;
+    const uint64_t W = wu[u - ua];
+    return W <= w0 ? 0 : W <= w1 ? 1 : 2;
+  };
+  uint32_t cnt[HP_NTIER] = {0, 0, 0};  // this wave's rows per tier (lane 0)
   for (uint64_t b0 = (uint64_t)blockIdx.x * NT; b0 < nrows; b0 += (uint64_t)gridDim.x * NT) {
-    const uint64_t i = b0 + threadIdx.x;
     uint32_t u = 0;
-    int t = -1;
-    if (i < nrows) {
-      u = rows[i];
-      const uint64_t W = wu[u - ua];
-      t = W <= w0 ? 0 : W <= w1 ? 1 : 2;
-    }
-    uint64_t m[HP_NTIER];
+    const int t = tier_of(b0 + threadIdx.x, &u);
 #pragma unroll
     for (int q = 0; q < HP_NTIER; ++q) {
-      m[q] = __ballot(t == q);
-      if (!SCATTER) cnt[q] += lane == 0 ? (uint32_t)__popcll(m[q]) : 0u;
+      const uint64_t m = __ballot(t == q);  // every lane votes (a ballot under `lane == 0 ?` would see one lane)
+      cnt[q] += lane == 0 ? (uint32_t)__popcll(m) : 0u;
     }
-    if (!SCATTER) continue;
+  }
+  if (lane == 0)
+    for (int q = 0; q < HP_NTIER; ++q) s_n[wv][q] = cnt[q];
+  __syncthreads();
+  if (threadIdx.x < HP_NTIER) {
+    uint32_t tot = 0;
+    for (int w = 0; w < NWAVE; ++w) tot += s_n[w][threadIdx.x];
+    if (!SCATTER && tot) atomicAdd(&tcnt[threadIdx.x], tot);
+    if (SCATTER) {
+      uint32_t tb = 0;
+      for (int q = 0; q < (int)threadIdx.x; ++q) tb += tcnt[q];
+      s_base[threadIdx.x] = tb + (tot ? atomicAdd(&tcnt[HP_NTIER + threadIdx.x], tot) : 0u);
+    }
+  }
+  if (!SCATTER) return;
+  __syncthreads();
+  for (uint64_t b0 = (uint64_t)blockIdx.x * NT; b0 < nrows; b0 += (uint64_t)gridDim.x * NT) {
+    uint32_t u = 0;
+    const int t = tier_of(b0 + threadIdx.x, &u);
+    uint64_t m[HP_NTIER];
+#pragma unroll
+    for (int q = 0; q < HP_NTIER; ++q) m[q] = __ballot(t == q);
     if (lane == 0)
       for (int q = 0; q < HP_NTIER; ++q) s_n[wv][q] = (uint32_t)__popcll(m[q]);
-    __syncthreads();
-    if (threadIdx.x < HP_NTIER) {
-      uint32_t tot = 0;
-      for (int w = 0; w < NWAVE; ++w) tot += s_n[w][threadIdx.x];
-      s_base[threadIdx.x] = tot ? atomicAdd(&tcnt[HP_NTIER + threadIdx.x], tot) : 0u;
-    }
     __syncthreads();
     if (t >= 0) {
       uint32_t pre = 0;
       for (int w = 0; w < wv; ++w) pre += s_n[w][t];
-      out[tb[t] + s_base[t] + pre + (uint32_t)__popcll(m[t] & ((1ull << lane) - 1))] = u;
+      out[s_base[t] + pre + (uint32_t)__popcll(m[t] & ((1ull << lane) - 1))] = u;
     }
-    __syncthreads();
-  }
-  if (!SCATTER) {
-    if (lane == 0)
-      for (int q = 0; q < HP_NTIER; ++q) s_n[wv][q] = cnt[q];
     __syncthreads();
     if (threadIdx.x < HP_NTIER) {
       uint32_t tot = 0;
       for (int w = 0; w < NWAVE; ++w) tot += s_n[w][threadIdx.x];
-      if (tot) atomicAdd(&tcnt[threadIdx.x], tot);
+      s_base[threadIdx.x] += tot;
     }
+    __syncthreads();
   }
 }
 
