@@ -72,19 +72,34 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist(const uint32_t* __restrict__ 
   for (int i = threadIdx.x; i < ES_MAXP * 256; i += ES_NT) (&h[0][0])[i] = 0;
   __syncthreads();
   const uint64_t lt = (1ull << lane_id()) - 1ull;
-  const uint64_t stride = (uint64_t)gridDim.x * ES_NT;
-  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT; j0 < n; j0 += stride) {  // uniform per wave: ballots below
-    const uint64_t j = j0 + threadIdx.x;
-    const bool ok = j < n;
-    const uint32_t u = ok ? cu[j] : 0u, w = ok ? cw[j] : 0u;
-    const float s = ok ? cs[j] : 0.0f;
-    for (int p = 0; p < npass; ++p) {
-      const uint32_t d = es_digit(u, w, s, vb, 8 * p);
-      if (8 * p + 8 <= 2 * vb) {  // a digit of (u, w): spread over its bins, one LDS atomic per record
-        if (ok) atomicAdd(&h[p][d], 1u);
-      } else {  // a digit of the score key: few bins, so one atomic per group of equal digits (8 ballots)
-        const uint64_t peers = es_peers(d, ok);
-        if (ok && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+  constexpr int UN = 4;  // records per thread per step, loaded together (the digits wait on one round trip)
+  const uint64_t stride = (uint64_t)gridDim.x * ES_NT * UN;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT * UN; j0 < n; j0 += stride) {  // uniform per wave: ballots below
+    uint32_t u[UN], w[UN];
+    float s[UN];
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
+      const bool ok = j < n;
+      u[q] = ok ? cu[j] : 0u;
+      w[q] = ok ? cw[j] : 0u;
+      s[q] = ok ? cs[j] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const bool ok = j0 + (uint64_t)q * ES_NT + threadIdx.x < n;
+      for (int p = 0; p < npass; ++p) {
+        const uint32_t d = es_digit(u[q], w[q], s[q], vb, 8 * p);
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        if (__ballot(ok && d != d0) == 0) {  // one digit in the whole wave (the high digits of u often): one atomic
+          const uint64_t m = __ballot(ok);
+          if (m && lane_id() == 0) atomicAdd(&h[p][d0], (uint32_t)__popcll(m));
+        } else if (8 * p + 8 <= 2 * vb) {  // a digit of (u, w): spread over its bins, one LDS atomic per record
+          if (ok) atomicAdd(&h[p][d], 1u);
+        } else {  // a digit of the score key: few bins, so one atomic per group of equal digits (8 ballots)
+          const uint64_t peers = es_peers(d, ok);
+          if (ok && (peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
+        }
       }
     }
   }

@@ -292,10 +292,16 @@ __global__ __launch_bounds__(NT) void k_sel_hist(const uint32_t* __restrict__ ke
   const int shift = pass == 0 ? 20 : (pass == 1 ? 8 : 0);
   const uint32_t mask = pass == 2 ? 0xffu : 0xfffu;
   const uint32_t prefix = (uint32_t)sel[0];
-  for (uint64_t j = (uint64_t)blockIdx.x * NT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * NT) {
-    uint32_t k = keys[j];
-    bool match = hi_bits == 0 ? true : ((k >> (32 - hi_bits)) == prefix);
-    if (match) atomicAdd(&h[(k >> shift) & mask], 1u);
+  constexpr int UN = 4;  // keys per thread per step, loaded together
+  for (uint64_t j0 = (uint64_t)blockIdx.x * NT * UN + threadIdx.x; j0 < n; j0 += (uint64_t)gridDim.x * NT * UN) {
+    uint32_t k[UN];
+#pragma unroll
+    for (int q = 0; q < UN; ++q) k[q] = j0 + (uint64_t)q * NT < n ? keys[j0 + (uint64_t)q * NT] : 0u;
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const bool match = j0 + (uint64_t)q * NT < n && (hi_bits == 0 || (k[q] >> (32 - hi_bits)) == prefix);
+      if (match) atomicAdd(&h[(k[q] >> shift) & mask], 1u);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < SEL_BINS; i += NT)
