@@ -35,7 +35,7 @@
 namespace nlp {
 
 constexpr int ES_NT = 512;                 // threads per tile
-constexpr int ES_IPT = 8;                  // records per thread
+constexpr int ES_IPT = 10;                 // records per thread
 constexpr int ES_WCH = 64 * ES_IPT;        // 512 consecutive records per wave
 constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
 constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
