@@ -18,8 +18,8 @@
 //   k_es_hist   one read of the records: the 256-bin histogram of every
 //               digit (wave-aggregated LDS counts); a digit whose histogram
 //               has one bin holding every record is a pass not run
-//   k_es_pass   one pass: 4096-record tiles claimed by an ordered ticket; a
-//               wave ranks its 512 consecutive records in 8 ballot-multisplit
+//   k_es_pass   one pass: 5120-record tiles claimed by an ordered ticket; a
+//               wave ranks its 640 consecutive records in 10 ballot-multisplit
 //               substeps; per digit the tile's count is published, the
 //               exclusive prefix over earlier tiles is found by decoupled
 //               look-back (u64 descriptors {epoch, status, count}: a pass
@@ -35,8 +35,9 @@
 namespace nlp {
 
 constexpr int ES_NT = 512;                 // threads per tile
-constexpr int ES_IPT = 10;                 // records per thread
-constexpr int ES_WCH = 64 * ES_IPT;        // 512 consecutive records per wave
+constexpr int ES_IPT = 10;                 // records per thread (tiles of 5120: 71 KB of LDS, two per CU;
+                                           // 3072 measured slower, 4096 too)
+constexpr int ES_WCH = 64 * ES_IPT;        // 640 consecutive records per wave
 constexpr int ES_MAXP = 12;                // digits of a <= 96-bit composite
 constexpr uint64_t ES_AGG = 1ull << 46, ES_PFX = 2ull << 46, ES_VAL = ES_AGG - 1;
 constexpr uint32_t ES_SPIN_LIMIT = 1u << 26;
