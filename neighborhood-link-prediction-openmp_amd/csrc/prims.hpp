@@ -311,17 +311,35 @@ __global__ __launch_bounds__(NT) void k_sel_hist(const uint32_t* __restrict__ ke
 // Single workgroup: walk the histogram from the top digit down.
 __global__ __launch_bounds__(NT) void k_sel_pick(uint32_t* __restrict__ ghist, int pass, uint64_t* __restrict__ sel) {
   __shared__ uint64_t cnt[SEL_BINS];
+  __shared__ uint64_t s_part[NT];  // per thread: the sum of its block of bins (blocks from the top bin down)
   const int bins = pass == 2 ? 256 : SEL_BINS;
+  const int per = bins / NT;       // 16 or 1
   for (int i = threadIdx.x; i < bins; i += NT) cnt[i] = ghist[i];
   __syncthreads();
+  {
+    uint64_t sum = 0;
+    for (int i = 0; i < per; ++i) sum += cnt[bins - 1 - threadIdx.x * per - i];
+    s_part[threadIdx.x] = sum;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    // walk down from the top bin: whole blocks while their sum stays below the
+    // remaining rank, then the block where it is reached bin by bin (bin 0 is
+    // never taken off: the walk stops there)
     uint64_t rem = sel[1], above = sel[2];
-    int d = bins - 1;
-    for (; d > 0; --d) {
+    int b = 0;
+    for (; b < NT - 1; ++b) {
+      if (s_part[b] >= rem) break;
+      rem -= s_part[b];
+      above += s_part[b];
+    }
+    int d = bins - 1 - b * per;
+    for (const int dl = d - per + 1; d > 0 && d >= dl; --d) {
       if (cnt[d] >= rem) break;
       rem -= cnt[d];
       above += cnt[d];
     }
+    if (d < 0) d = 0;
     sel[0] = (sel[0] << (pass == 2 ? 8 : 12)) | (uint64_t)d;
     sel[1] = rem;
     sel[2] = above;
