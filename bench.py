@@ -42,7 +42,7 @@ import nlp_loader  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip-level parameters (spec)
 HOT_KERNELS = {1: "k_sp_bucket", 2: "k_sp_scan<F_Runs>", 3: "k_group_tiles", 4: "k_sp_survivors",
                5: "k_sp_expand", 6: "k_sp_pass", 7: "k_sp_runs", 8: "k_sp_group",
-               9: "k_sp_grouprun", 10: "k_sp_exbucket", 11: "k_hp_batch"}
+               9: "k_sp_grouprun", 10: "k_sp_exbucket", 11: "k_hp_batch", 12: "k_sp_order_rank"}
 CALLS_PER_GRAPH = 99  # main.cxx:67-80,212-220: 9 metrics x 11 hub thresholds per batch graph
 METRIC_NAMES = {"CN": "CommonNeighbors", "JAC": "JaccardCoefficient", "SOR": "SorensenIndex",
                 "SAL": "SaltonCosineSimilarity", "HPI": "HubPromoted", "HDI": "HubDepressed",
@@ -251,7 +251,8 @@ def timed(run, mid, hub, steps, warmup, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    acc = dict(score_ms=0.0, select_ms=0.0, hot_ms=0.0, hot_bytes=0)
+    acc = dict(score_ms=0.0, select_ms=0.0, hot_ms=0.0, hot_bytes=0, call_bytes=0,
+               predict_ms=0.0, select_xchg_ms=0.0, gather_merge_ms=0.0, exchange_ms=0.0)
     last = {}
     cnt = 0
     t0 = time.perf_counter()
@@ -269,6 +270,25 @@ def timed(run, mid, hub, steps, warmup, world):
     for key in acc:
         acc[key] = acc[key] / steps
     return ms, cnt, acc, last
+
+
+def per_rank(acc, world):
+    """N > 1: every rank's mean shard time and exchange time over the timed
+    calls (dist.predict_sharded's stamps), gathered to every rank -- so the
+    line separates shard imbalance (max vs mean predict_ms) from the exchange
+    that replaces the reference's serial merge (predict.hxx:431-460)."""
+    if world == 1:
+        return None
+    v = torch.tensor([acc["predict_ms"], acc["select_xchg_ms"], acc["gather_merge_ms"], acc["exchange_ms"]],
+                     dtype=torch.float64, device="cuda")
+    allv = [torch.zeros_like(v) for _ in range(world)]
+    dist.all_gather(allv, v)
+    rows = [x.cpu().tolist() for x in allv]
+    pm = [r[0] for r in rows]
+    return {"predict_ms": pm, "select_xchg_ms": [r[1] for r in rows], "gather_merge_ms": [r[2] for r in rows],
+            "exchange_ms": [r[3] for r in rows], "predict_ms_max": max(pm), "predict_ms_mean": sum(pm) / world,
+            "imbalance": max(pm) / (sum(pm) / world) if sum(pm) > 0 else None,
+            "exchange_ms_max": max(r[3] for r in rows)}
 
 
 def roofline_of(acc, last, config, world, metric, hub):
@@ -345,6 +365,7 @@ def main():
 
     ms_per_step, cnt, acc, timing = timed(run, mid, hub, args.steps, args.warmup, world)
     value = cnt / (ms_per_step * 1e-3)
+    ranks = per_rank(acc, world)
 
     pipelined_ms = None
     if world == 1 and args.pipelined:  # serving loop: the same calls without a host wait (outside the line's value)
@@ -385,13 +406,26 @@ def main():
                 break
         if wp_h is not None:
             wms, wcnt, wacc, wlast = timed(run, mid, wp_h, args.wp_steps, args.wp_warmup, world)
+            wranks = per_rank(wacc, world)
             balg = b_alg(off, wp_h, wcnt)
+            # F1 of the k-filling call (main.cxx:48-57, 199-206), its links still in `out`
+            wp_p, wp_r, wp_f1 = f1_on_device(G, run.out, wcnt, du, dw) if rank == 0 else (None, None, None)
             wp = {"H": wp_h, "metric": metric, "ms": wms, "predicted": wcnt, "predicted_per_s": wcnt / (wms * 1e-3),
                   "amortized_ms_per_call": wms + amort, "steps": args.wp_steps,
                   "wedges": int(wlast.get("wedges", 0)), "candidates": int(wlast.get("candidates", 0)),
                   "path": wlast.get("path"), "chunks": wlast.get("chunks"),
                   "score_ms": wacc["score_ms"], "select_ms": wacc["select_ms"],
+                  "f1": wp_f1, "precision": wp_p, "recall": wp_r,
+                  # SURVEY 8(d)'s whole-call bytes are the REFERENCE's wedge scan (its 8 M first-hop
+                  # reads included, which this call never makes): call_frac is a cross-implementation
+                  # ratio, not a roofline fraction; call_kernel_bytes is what the call's own kernels
+                  # are specified to move (counted by the library)
                   "call_alg_bytes": balg, "call_frac": balg / (wms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                  "call_frac_kind": "reference's SURVEY 8(d) bytes / our call time / 8 TB/s",
+                  "call_kernel_bytes": int(wacc["call_bytes"]) or None,
+                  "call_kernel_frac": (wacc["call_bytes"] / (wms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                  if wacc["call_bytes"] else None,
+                  "per_rank": wranks,
                   "roofline": roofline_of(wacc, wlast, args.config, world, metric, wp_h) if world == 1 else None,
                   "cpu_baseline": None}
     cnt, _ = run(mid, hub)  # leave the headline call's result in `out` for F1
@@ -435,6 +469,8 @@ def main():
                                  "table, AA/RA tables: built once in nlp_graph_create (graph_create_s; "
                                  "amortized_ms_per_call adds graph_create_s / %d)" % CALLS_PER_GRAPH,
             "roofline": roofline_of(acc, timing, args.config, world, metric, hub) if world == 1 else None,
+            "call_kernel_bytes": int(acc["call_bytes"]) or None,
+            "per_rank": ranks,
             "pipelined_ms_per_step": pipelined_ms,
             "hub_sweep": sweep,
             "work_point": wp,

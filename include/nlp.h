@@ -98,7 +98,11 @@ typedef struct {
                                3 k_group_tiles, 4 k_sp_survivors, 5 k_sp_expand, 6 k_sp_pass,
                                7 k_sp_runs, 8 k_sp_group, 9 k_sp_grouprun, 10 k_sp_exbucket,
                                11 k_hp_batch (path 4: all its launches of the call, times and bytes
-                               summed); 0 none */
+                               summed), 12 k_sp_order_rank; 0 none.  Path 1's fused call reports
+                               the longest of k_sp_exbucket, k_sp_grouprun, k_sp_order_rank */
+  uint64_t call_bytes;      /* algorithmic bytes of ALL the call's kernels by the DESIGN.md §5 model
+                               (paths 1 and 4; 0 when not modelled) -- what this call's own design
+                               must move, beside SURVEY §8(d)'s bytes of the reference's scan */
 } nlp_timing;
 
 typedef struct nlp_graph nlp_graph;

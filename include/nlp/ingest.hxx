@@ -191,16 +191,34 @@ inline MtxPairs readMtxPairs(const std::string& path) {
   if (!f) throw std::runtime_error("nlp::readMtx: cannot open " + path);
   std::vector<char> text;
   {
-    fseek(f, 0, SEEK_END);
-    const long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    text.resize(sz > 0 ? (size_t)sz : 0);
-    if (!text.empty() && fread(text.data(), 1, text.size(), f) != text.size()) {
-      fclose(f);
-      throw std::runtime_error("nlp::readMtx: short read of " + path);
+    // a regular file is read in one piece; a stream that cannot seek (a pipe,
+    // `nlp_main <(zcat g.mtx.gz)`) in chunks until its end, like the
+    // reference's ifstream (mtx.hxx:138)
+    const long sz = fseek(f, 0, SEEK_END) == 0 ? ftell(f) : -1L;
+    if (sz > 0 && fseek(f, 0, SEEK_SET) == 0) {
+      text.resize((size_t)sz);
+      if (fread(text.data(), 1, text.size(), f) != text.size()) {
+        fclose(f);
+        throw std::runtime_error("nlp::readMtx: short read of " + path);
+      }
+    } else {
+      clearerr(f);
+      const size_t chunk = size_t(1) << 24;
+      for (;;) {
+        const size_t at = text.size();
+        text.resize(at + chunk);
+        const size_t got = fread(text.data() + at, 1, chunk, f);
+        text.resize(at + got);
+        if (got < chunk) break;
+      }
+      if (ferror(f)) {
+        fclose(f);
+        throw std::runtime_error("nlp::readMtx: read error on " + path);
+      }
     }
     fclose(f);
   }
+  if (text.empty()) throw std::runtime_error("nlp::readMtx: empty input " + path);
   const char* p = text.data();
   const char* e = p + text.size();
   MtxPairs out;

@@ -50,7 +50,7 @@ class Timing(ctypes.Structure):
                 ("copy_ms", ctypes.c_float), ("wedges", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
                 ("nan_candidates", ctypes.c_uint64), ("path", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
                 ("hot_ms", ctypes.c_float), ("graph_replay", ctypes.c_uint32), ("hot_bytes", ctypes.c_uint64),
-                ("hot_kernel", ctypes.c_uint32)]
+                ("hot_kernel", ctypes.c_uint32), ("call_bytes", ctypes.c_uint64)]
 
     def as_dict(self):
         return dict(zip(_TIMING_FIELDS, _timing_get(self)))

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(NTH) void k_es_pass(const uint32_t* __restrict__ cu
     if (tile >= ntiles) break;  // uniform: every wave leaves
     const uint64_t base = tile * ES_TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - base);
-    // records of this wave: base + wv * 512 + i * 64 + lane (item order = (wave, substep, lane))
+    // records of this wave: base + wv * ES_WCH + i * 64 + lane (item order = (wave, substep, lane))
     uint32_t ru[ES_IPT], rw[ES_IPT], rs[ES_IPT], rk[ES_IPT], dg[ES_IPT];
 #pragma unroll
     for (int i = 0; i < ES_IPT; ++i) {

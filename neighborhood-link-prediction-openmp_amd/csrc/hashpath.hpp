@@ -79,6 +79,7 @@ struct HpArgs {
   unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
   uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
   uint32_t uxf;            // rows whose exclusion slice exceeds uxf x W test the membership table (HP_UX_OFF: never)
+  uint32_t defer;          // k_hp_batch: those tests deferred to k_hp_xprobe (entries emitted with HP_DEFER in w)
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -524,7 +525,7 @@ __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
 // Candidate filter (predict.hxx:309-311: score <= minScore skips, NaN passes)
 // and emission above tau; every active lane of the wave calls it.
 __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid, float s, uint32_t u, uint32_t w,
-                                        int64_t tau) {
+                                        int64_t tau, uint32_t wflag = 0u) {
   const bool cand = valid && !(s <= a.min_score) && !f2_drop(a.g, u, w);
   st.cand += cand ? 1 : 0;
   st.nan += (cand && s != s) ? 1 : 0;
@@ -537,7 +538,7 @@ __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid
   if (out) {
     const uint32_t i = st.n + (uint32_t)__popcll(mo & ((1ull << lane_id()) - 1));
     st.u[i] = u;
-    st.w[i] = w;
+    st.w[i] = w | wflag;
     st.s[i] = s;
   }
   st.n += n;
@@ -556,6 +557,81 @@ __device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t
     if (n) atomicAdd(&a.ctr[HPC_NAN], (unsigned long long)n);
     if (wd) atomicAdd(&a.ctr[HPC_WEDGE], (unsigned long long)wd);
     if (st.pad) atomicAdd(&a.ctr[HPC_PAD], (unsigned long long)st.pad);
+  }
+}
+
+// ---------------------------------------------------------------- deferred exclusion tests
+// k_hp_batch's rows whose exclusion slice is long test their entries in the
+// membership table (one 64-byte line each).  Inside the row batches those
+// tests are a dependent load in a latency-bound loop (C4 JAC H=16: more than
+// half of the kernel).  Before the chunk's candidates are held against a
+// threshold (the host defers only while no tau is in force, so every entry
+// is emitted and counted), the batches emit such entries with their
+// unexcluded score and HP_DEFER set in w (vertex ids < 2^31); k_hp_xprobe
+// then tests all flagged entries of the chunk with IPT lines in flight per
+// thread: a member of N(u) gets the score of count 0 (predict.hxx:306-307,
+// then 309-311: usually 0 <= minScore -> padding; 0/0 = NaN stays a
+// candidate), a non-member loses the flag.  Counts are corrected in
+// xc[0] (candidates removed), xc[1] / xc[2] (NaN removed / added).
+constexpr uint32_t HP_DEFER = 0x80000000u;
+constexpr int HX_IPT = 8;
+__global__ __launch_bounds__(NT) void k_hp_xprobe(GraphView g, int metric, float min_score, uint32_t* __restrict__ ckey,
+                                                  uint32_t* __restrict__ cu, uint32_t* __restrict__ cw,
+                                                  float* __restrict__ cs, uint64_t base, uint64_t cap,
+                                                  const unsigned long long* __restrict__ ctr,
+                                                  unsigned long long* __restrict__ xc) {
+  const uint64_t n = min((uint64_t)ctr[HPC_EMIT], cap);
+  uint64_t drop = 0, nrm = 0, nadd = 0;
+  const uint64_t step = (uint64_t)gridDim.x * NT * HX_IPT;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * NT * HX_IPT; t0 < n; t0 += step) {
+    uint64_t key[HX_IPT];
+    bool act[HX_IPT], res[HX_IPT];
+    uint32_t wq[HX_IPT];
+#pragma unroll
+    for (int q = 0; q < HX_IPT; ++q) {
+      const uint64_t i = t0 + (uint64_t)q * NT + threadIdx.x;
+      wq[q] = i < n ? cw[base + i] : 0u;
+      act[q] = (wq[q] & HP_DEFER) && wq[q] != 0xffffffffu;  // padding: u = w = 0xffffffff
+    }
+#pragma unroll
+    for (int q = 0; q < HX_IPT; ++q) {
+      const uint64_t i = t0 + (uint64_t)q * NT + threadIdx.x;
+      key[q] = act[q] ? ((uint64_t)cu[base + i] << 32 | (wq[q] & ~HP_DEFER)) : 0ull;
+    }
+    et_has_n<HX_IPT>(g.etab, g.etbits, key, act, res);
+#pragma unroll
+    for (int q = 0; q < HX_IPT; ++q) {
+      if (!act[q]) continue;
+      const uint64_t i = base + t0 + (uint64_t)q * NT + threadIdx.x;
+      const uint32_t w = wq[q] & ~HP_DEFER;
+      if (!res[q]) {
+        cw[i] = w;
+        continue;
+      }
+      const uint32_t u = (uint32_t)(key[q] >> 32);
+      const float s0 = cs[i];
+      const float s = (metric == M_AA || metric == M_RA) ? 0.0f
+                                                         : score_basic(metric, 0u, (uint64_t)g.deg[u], (uint64_t)g.deg[w]);
+      nrm += (s0 != s0) ? 1 : 0;
+      if (s <= min_score) {  // no longer a candidate: padding (dropped by the prune)
+        ++drop;
+        ckey[i] = 0u;
+        cu[i] = 0xffffffffu;
+        cw[i] = 0xffffffffu;
+        cs[i] = __uint_as_float(0x7fc00000u);
+      } else {
+        nadd += (s != s) ? 1 : 0;
+        ckey[i] = score_key(s);
+        cw[i] = w;
+        cs[i] = s;
+      }
+    }
+  }
+  const uint64_t d = wave_sum(drop), r = wave_sum(nrm), ad = wave_sum(nadd);
+  if (lane_id() == 0) {
+    if (d) atomicAdd(&xc[0], (unsigned long long)d);
+    if (r) atomicAdd(&xc[1], (unsigned long long)r);
+    if (ad) atomicAdd(&xc[2], (unsigned long long)ad);
   }
 }
 
@@ -2393,10 +2469,12 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         }
       }
       // first-order exclusion by the membership table for the entries of
-      // table-tested rows (count tables: two first buckets in flight at a time)
+      // table-tested rows (count tables: two first buckets in flight at a time);
+      // with a.defer the tests are left to k_hp_xprobe (the entries go out flagged)
 #pragma unroll
       for (int q0 = 0; q0 < UN; q0 += 2) {
         if ((uint32_t)q0 >= nq) break;
+        if (a.defer) break;
         uint64_t ek[2];
         bool ea[2], er[2];
 #pragma unroll
@@ -2433,7 +2511,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
           if (CUSTOM) s = ho_score(c[q]);
           else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & (KD ? 1023u : HP_CMASK)), du2, (uint64_t)dw[q]);
         }
-        hp_emit(sg, a, valid, s, uu, w, tau);
+        hp_emit(sg, a, valid, s, uu, w, tau, (a.defer && valid && s_ux[wv][sl]) ? HP_DEFER : 0u);
       }
     }
     wave_sync_lds();

@@ -288,9 +288,11 @@ struct nlp_graph {
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
+  const void* es_desc_ptr = nullptr;  // and its address (a same-size reallocation restarts them too)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hp_uxf = HB_XF;   // exclusion by the membership table for slices beyond hp_uxf x W
+  bool hp_xdefer = true;      // k_hp_batch's table tests deferred to k_hp_xprobe (NLP_HASH_XDEFER=0: in the kernel)
                              // (NLP_HASH_UX=off: always marks; =0: always the table)
   int hp_rowb = 1;           // bin 1, count metrics: tiered 256-thread rows (NLP_HASH_ROWB=0: k_hp_block;
                              // 2: every row in the 8192-entry tier, 3: none in the 2048-entry tier -- tests)
@@ -892,6 +894,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
+  if (const char* xd = getenv("NLP_HASH_XDEFER")) g->hp_xdefer = xd[0] != '0';
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = atoi(ho);
@@ -990,6 +993,7 @@ struct Cands {
   double hot_ms = 0;       // path 4: device time of the k_hp_batch launches (HIP events around each)
   uint64_t hot_bytes = 0;  // and their algorithmic bytes (counted by the kernel, HPC_HOTB)
   uint32_t hot_launches = 0;
+  uint64_t call_bytes = 0; // DESIGN.md §5 model of the bytes of all the call's kernels (path 4)
 };
 
 // Group the W wedges of one generator pass, score them and append the
@@ -1663,6 +1667,8 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   std::swap(ws.p[B_CU], ws.p[B_TU]); std::swap(ws.bytes[B_CU], ws.bytes[B_TU]);
   std::swap(ws.p[B_CW], ws.p[B_TW]); std::swap(ws.bytes[B_CW], ws.bytes[B_TW]);
   std::swap(ws.p[B_CS], ws.p[B_TS]); std::swap(ws.bytes[B_CS], ws.bytes[B_TS]);
+  // three select histograms (4 B key each), the split (16 B in per candidate, 16 B out per kept)
+  C.call_bytes += 28 * n + 16 * k;
   C.n = k;
   return NLP_OK;
 }
@@ -1674,7 +1680,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
 // (~score_key, u, w) (edgesort.hpp).  Digits that are the same for every
 // record are skipped (one histogram read decides, read back with one sync).
 nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
-                   hipStream_t st) {
+                   hipStream_t st, uint64_t* bytes = nullptr) {
   if (n == 0) return NLP_OK;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
@@ -1697,6 +1703,7 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
     for (int d = 0; d < 256; ++d) mx = std::max(mx, h[(size_t)p * 256 + d]);
     if (mx < n) run[P++] = p;
   }
+  if (bytes) *bytes += 12 * n + 24 * n * (uint64_t)std::max(P, 1);  // histogram read + every pass in and out
   if (P == 0) {
     LAUNCH(k_es_copy, n, st, cu, cw, cs, n, out);
     return hipGetLastError() == hipSuccess ? NLP_OK : NLP_ERR_DEVICE;
@@ -1706,9 +1713,11 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
   EdgeOut* tmp = nullptr;
   TRY(wsget(ws, B_ES_DESC, ntiles * 256, &desc));
   if (P > 1) TRY(wsget(ws, B_ES_TMP, n, &tmp));
-  if (ws.bytes[B_ES_DESC] != g->es_desc_bytes || g->es_epoch + P >= 0xffffull) {
-    TRY(hipMemsetAsync(desc, 0, ws.bytes[B_ES_DESC], st));  // no stale descriptor can carry a live epoch
+  // a new or regrown descriptor buffer (size OR address) starts clear: no stale word can carry a live epoch
+  if (ws.bytes[B_ES_DESC] != g->es_desc_bytes || (const void*)desc != g->es_desc_ptr || g->es_epoch + P >= 0xffffull) {
+    TRY(hipMemsetAsync(desc, 0, ws.bytes[B_ES_DESC], st));
     g->es_desc_bytes = ws.bytes[B_ES_DESC];
+    g->es_desc_ptr = desc;
     g->es_epoch = 0;
   }
   const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es));
@@ -1735,7 +1744,7 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
 nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   if (C.n == 0) return NLP_OK;
   return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
-                 d_out, st);
+                 d_out, st, &C.call_bytes);
 }
 
 // Estimated wedges (w > u) of a call: sum over surviving v of deg(v)^2 / 2,
@@ -2246,10 +2255,13 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.xs = g->xs;
     a.win = 0;
     a.uxf = g->hp_uxf;
+    // membership-table tests of the row batches deferred to k_hp_xprobe while no threshold is in
+    // force (every entry is then emitted, so the probe sees -- and corrects the counts of -- all)
+    a.defer = (!full && g->hp_xdefer && gv.etab && a.uxf != HP_UX_OFF && S <= (1ull << 31)) ? 1u : 0u;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
     if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
-    bool batch_timed = false;
+    bool batch_timed = false, probed = false;
     if (n0 && g->hp_tiers) {
       // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
       TRY(hipMemsetAsync(tcnt, 0, 8 * sizeof(uint32_t), st));
@@ -2298,6 +2310,14 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(hipGetLastError());
         TRY(hipEventRecord(g->ev[6], st));
         batch_timed = true;
+        if (a.defer) {
+          TRY(hipMemsetAsync(small + 60, 0, 24, st));
+          const unsigned gx = (unsigned)std::min<uint64_t>(wchunk / ((uint64_t)NT * HX_IPT) + 1, 8192);
+          hipLaunchKernelGGL(k_hp_xprobe, dim3(gx), dim3(NT), 0, st, gv, p.metric, p.min_score, a.ckey, a.cu, a.cw,
+                             a.cs, a.base, a.cap, (const unsigned long long*)small, (unsigned long long*)(small + 60));
+          TRY(hipGetLastError());
+          probed = true;
+        }
         a.win = 0;  // the other row kernels reserve per flush
         if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_wave<false, HP_WT, HP_STG, true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
@@ -2384,6 +2404,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
     }
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
+    if (probed) TRY(hipMemcpyAsync(&g->host_small[60], small + 60, 24, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
     if (batch_timed) {
@@ -2422,6 +2443,16 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     }
     ++*nchunks;
     retry = false;
+    if (probed) {  // k_hp_xprobe: excluded entries turned into padding, the counts corrected
+      const uint64_t xdrop = g->host_small[60], xnrm = g->host_small[61], xnadd = g->host_small[62];
+      g->host_small[HPC_CAND] -= xdrop;
+      g->host_small[HPC_NAN] = g->host_small[HPC_NAN] + xnadd - xnrm;
+      g->host_small[HPC_PAD] += xdrop;
+      C.call_bytes += 4 * emitted + 72 * xdrop;  // flags read; tested entries: u, w back, a 64-byte line
+    }
+    // row bookkeeping (W+(u), survivor prefix, bins, tiers: ~64 B per row), per wedge its key and
+    // entry degree plus its packed survivor entry at most (16 B of the chunk's bound), 16 B per emission
+    C.call_bytes += 64 * (r1 - r0) + 16 * wchunk + 16 * emitted;
     C.pad += g->host_small[HPC_PAD];
     C.n += emitted;
     C.total += g->host_small[HPC_CAND];
@@ -3568,7 +3599,8 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (result) *result = out;
     if (t) {
       float a = 0, b = 0, hot = 0;
-      if (stamps && ((replayed && g->last_single) || direct_nomark)) {
+      const bool stamped = stamps && ((replayed && g->last_single) || direct_nomark);
+      if (stamped) {
         // the kernels' own stamps -- no event nodes in the graph
         stamp_times(h, &a, &b, &hot);
       } else {
@@ -3592,10 +3624,31 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
         const int s_runs = 4 + (sp.msd ? sp.msd_passes : sp.passes) + (sp.split ? 1 : 0);
         const int hs = g->hot_stage < 0 ? sp_hot_default(sp) : std::min(std::max(g->hot_stage, 1), s_runs);
         t->hot_bytes = sp_stage_bytes(g, sp, hs, h, p.H);
+        t->call_bytes = 0;
+        for (int s2 = 1; s2 <= s_runs; ++s2) t->call_bytes += sp_stage_bytes(g, sp, s2, h, p.H);
+        t->call_bytes += 12 * h[C_C] + 12 * h[C_OUT_N];  // ordering: candidate columns in, links out
         t->hot_kernel = (sp.fused && hs == s_runs - 1) ? 9u
                         : hs == s_runs ? (sp.split ? 7u : sp.msd ? 1u : 2u)
                         : (sp.split && hs == s_runs - 1) ? (sp.msd_passes == 1 && g->group_sort != 1 && !sp.direct ? 1u : 8u)
                         : hs == 1 ? 4u : hs == 2 ? (sp.fused ? 10u : 5u) : hs >= 4 ? 6u : 0u;
+        if (stamped && sp.fused && g->hot_stage < 0) {
+          // the fused call's three stamped spans -- k_sp_exbucket (its entry to grouprun's), k_sp_grouprun,
+          // and the one-launch ordering k_sp_order_rank (grouprun's end to the last tile) -- and the roofline
+          // reports the LONGEST of them, with its own algorithmic bytes
+          const uint64_t* tsv = h + NCTR;
+          const uint64_t first = ~tsv[TS_FIRST], hin = ~tsv[TS_HOT_IN], hout = tsv[TS_HOT_OUT], end = tsv[TS_END];
+          const float exb = hin > first && tsv[TS_FIRST] ? (float)((hin - first) * 1e-5) : 0.0f;
+          const float ord = sp.small && end > hout && hout ? (float)((end - hout) * 1e-5) : 0.0f;
+          if (exb > t->hot_ms && exb >= ord) {
+            t->hot_ms = exb;
+            t->hot_bytes = sp_stage_bytes(g, sp, 2, h, p.H);
+            t->hot_kernel = 10u;
+          } else if (ord > t->hot_ms) {
+            t->hot_ms = ord;
+            t->hot_bytes = 28 * h[C_C] + 12 * h[C_OUT_N];  // keys + candidate columns in, links out
+            t->hot_kernel = 12u;
+          }
+        }
       } else {
         // k_group_tiles: bucket counts, records, flags, runs
         t->hot_bytes = 4 * nU + 8 * h[C_W] + 4 * h[C_W] + 12 * h[C_C];
@@ -3717,6 +3770,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     t->hot_ms = (float)C.hot_ms;
     t->hot_bytes = C.hot_bytes;
     t->hot_kernel = C.hot_launches ? 11u : 0u;
+    t->call_bytes = path == 4 ? C.call_bytes : 0;
     t->graph_replay = 0;
   }
   return NLP_OK;
@@ -4271,7 +4325,17 @@ nlp_status nlp_dcsr_ingest(const uint32_t* src, const uint32_t* dst, uint64_t m,
     return s;
   }
   if (m) {  // distinct pairs and distinct self loops
+    // cnt starts clear (k_in_pairs ORs an out-of-range flag into it; nlp_ingest_device has
+    // already rejected such ids), and every launch is checked
+    if (hipMemset(cnt, 0, 16) != hipSuccess) {
+      dcsr_free(x);
+      return NLP_ERR_DEVICE;
+    }
     LAUNCH(k_in_pairs, m, nullptr, (const uint32_t*)ds, (const uint32_t*)dd, m, n, e, (uint32_t*)cnt);
+    if (hipGetLastError() != hipSuccess) {
+      dcsr_free(x);
+      return NLP_ERR_DEVICE;
+    }
     int shifts[16];
     const int vb = std::max(1, bits_for(n));
     const int np = key_shifts(vb, 32, vb, shifts);
@@ -4287,7 +4351,7 @@ nlp_status nlp_dcsr_ingest(const uint32_t* src, const uint32_t* dst, uint64_t m,
     }
     LAUNCH(k_in_count_distinct, m, nullptr, (const uint64_t*)e, m, (unsigned long long*)cnt);
     uint64_t h[2] = {0, 0};
-    if (hipMemcpy(h, cnt, 16, hipMemcpyDeviceToHost) != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || hipMemcpy(h, cnt, 16, hipMemcpyDeviceToHost) != hipSuccess) {
       dcsr_free(x);
       return NLP_ERR_DEVICE;
     }
@@ -4317,19 +4381,25 @@ nlp_status nlp_dcsr_delete_batch(const nlp_dcsr* x, uint64_t batch, uint32_t* rn
     return NLP_ERR_NOMEM;
   }
   uint64_t nd = 0;
+  // the engine state is restored on every error return, so a retry (e.g. with a larger
+  // deletion buffer) draws the same batch -- the minstd_rand0 replay N2 parity relies on
+  const uint32_t rng0 = *rng_state;
   nlp_status s = nlp_delete_edges_device(x->off, x->keys, x->span, batch, rng_state, y->off, y->keys, &y->nnz, du, dv,
                                          &nd, x->device, nullptr);
   if (s != NLP_OK) {
+    *rng_state = rng0;
     dcsr_free(y);
     return s;
   }
   *ndel = nd;
   if ((del_u || del_v) && nd > del_cap) {
+    *rng_state = rng0;
     dcsr_free(y);
     return NLP_ERR_CAPACITY;
   }
   if (nd && ((del_u && hipMemcpy(del_u, du, nd * 4, hipMemcpyDeviceToHost) != hipSuccess) ||
              (del_v && hipMemcpy(del_v, dv, nd * 4, hipMemcpyDeviceToHost) != hipSuccess))) {
+    *rng_state = rng0;
     dcsr_free(y);
     return NLP_ERR_DEVICE;
   }

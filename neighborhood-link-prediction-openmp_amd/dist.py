@@ -10,12 +10,13 @@ SURVEY.md §8(e).  The reference has a single OpenMP team over source vertices
      its own contiguous source range [u_begin, u_end)  -> nlp_predict_device;
      the ranges balance the per-source wedge estimate (source_weights);
   2. histogram-first selection (select_quota): every rank histograms the top
-     16 bits of its result's score keys, one all_reduce(sum) gives the global
-     histogram and the bin of the k-th key; a second all_reduce of the low 16
-     bits inside that bin gives the k-th key itself.  Every rank then knows how
-     many of its links rank above it; one all_gather of two counts per rank
-     hands out the tie quota in rank (= u) order, the canonical tie rule.  A
-     rank's share of the global top-k is a PREFIX of its canonical list;
+     16 bits of its result's score keys and one all_gather of the 65536-bin
+     histograms (world rows) gives every rank the bin of the k-th key and each
+     rank's count above it; a second all_gather of the low-16-bit histograms
+     inside that bin gives the k-th key itself, each rank's count above it and
+     its ties.  The tie quota is handed out in rank (= u) order, the canonical
+     tie rule, on the device; only the shares (world integers) are read back.
+     A rank's share of the global top-k is a PREFIX of its canonical list;
   3. ONE all_gather of exactly those prefixes (block stride = the largest
      share + 1 header entry): about 12 k bytes in total instead of every
      rank's whole local top-k;
@@ -29,6 +30,8 @@ injectable so that the same orchestration runs under gloo on the CPU in the
 tests (with the oracle standing in for the device kernels there); with the
 gloo backend the collectives run on CPU copies of the small tensors.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -226,14 +229,23 @@ def predict_sharded(local_predict, merge, span, max_edges, group=None, weights=N
     if state.ranges is None:
         state.ranges = shard_ranges(span, world, weights)
     ub, ue = state.ranges[rank]
-    block, n, info = local_predict(ub, ue)
+    t0 = time.perf_counter()
+    block, n, info = local_predict(ub, ue)  # synchronous: the shard's result is complete on return
+    t1 = time.perf_counter()
     if block.shape[0] < min(n, max_edges) + 1:
         raise ValueError("local block must hold the result + 1 header entry")
-    share, shares = select_quota(block[1:], n, max_edges, group)
+    share, shares = select_quota(block[1:], n, max_edges, group)  # ends with a host read of the shares
+    t2 = time.perf_counter()
     write_header(block, share)
     blocks = gather_blocks(block, max(shares) + 1, group)
-    out, k = merge(blocks, max_edges)
-    info = dict(info or {}, shard=(ub, ue), blocks=blocks, stride=max(shares) + 1, shares=shares, local_count=n)
+    out, k = merge(blocks, max_edges)  # synchronous
+    t3 = time.perf_counter()
+    # predict_ms: this rank's shard (score + local top-k + order); the exchange that
+    # replaces the reference's serial merge (predict.hxx:431-460) split into the
+    # histogram selection and the block gather + merge
+    info = dict(info or {}, shard=(ub, ue), blocks=blocks, stride=max(shares) + 1, shares=shares, local_count=n,
+                predict_ms=(t1 - t0) * 1e3, select_xchg_ms=(t2 - t1) * 1e3, gather_merge_ms=(t3 - t2) * 1e3,
+                exchange_ms=(t3 - t1) * 1e3)
     return out, k, info
 
 

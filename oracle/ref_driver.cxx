@@ -175,7 +175,20 @@ static int doPredict(int argc, char** argv, bool write) {
     FILE* f = fopen(argv[9], "wb"); if (!f) die("cannot write out");
     uint64_t n = r.edges.size();
     fwrite(&n, 8, 1, f);
-    for (auto& [u, v, s] : r.edges) { fwrite(&u, 4, 1, f); fwrite(&v, 4, 1, f); fwrite(&s, 4, 1, f); }
+    // packed {u, w, score} records, written in blocks (a full-size top-k is 1e8+ links)
+    vector<uint32_t> buf;
+    const size_t blk = size_t(1) << 22;
+    for (size_t i = 0; i < n; i += blk) {
+      const size_t e = std::min(n, i + blk);
+      buf.resize(3 * (e - i));
+      for (size_t j = i; j < e; ++j) {
+        auto& [u, v, s] = r.edges[j];
+        buf[3 * (j - i)] = u;
+        buf[3 * (j - i) + 1] = v;
+        memcpy(&buf[3 * (j - i) + 2], &s, 4);
+      }
+      if (fwrite(buf.data(), 4, buf.size(), f) != buf.size()) die("short write");
+    }
     fclose(f);
   }
   return 0;

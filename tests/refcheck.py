@@ -1,0 +1,195 @@
+"""Full-size parity against the REFERENCE ITSELF, for the
+k-filling calls of the full-size stand-ins (tests/test_gpu_c3.py, c4.py).
+
+TEST INFRASTRUCTURE: the reference's own predictLinks<Metric>Omp<H> runs as
+oracle/_ref/ref_driver (compiled from /root/reference/inc by oracle/Makefile in
+the build container; the binary travels) on the same CSR, written to /dev/shm.
+The comparison runs on the GPU with torch (sets of 1e8+ links), never through
+the library under test.
+
+The reference's tie order depends on its OpenMP schedule (predict.hxx:287,
+332, 437), so the contract is:
+  1. the same number of links and the same score multiset, bitwise;
+  2. the same set of links strictly above the k-th score;
+  3. every link at the k-th score (ours and the reference's) is in the
+     reference's own tie set -- ALL its candidates at that score, taken from a
+     second reference call with maxEdges = |above| + |ties|;
+  4. F1 (main.cxx:48-57, 199-206) of both lies within the tie bounds: the
+     r = k - |above| boundary links chosen from the tie set T to minimise /
+     maximise the matches with the deletions.
+"""
+import json
+import os
+import subprocess
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+REF_THREADS = int(os.environ.get("NLP_REF_THREADS", os.environ.get("OMP_NUM_THREADS", "16")))
+
+
+def have_ref():
+    return os.path.exists(REF_DRIVER)
+
+
+def write_csr(off, keys):
+    """The CSR as ref_driver reads it ([span, nnz] u64, offsets u64, keys u32),
+    in /dev/shm when present.  Returns (path, TemporaryDirectory)."""
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    tmp = tempfile.TemporaryDirectory(dir=shm)
+    path = os.path.join(tmp.name, "g.csr")
+    with open(path, "wb") as f:
+        np.array([len(off) - 1, len(keys)], np.uint64).tofile(f)
+        np.asarray(off, np.uint64).tofile(f)
+        np.asarray(keys, np.uint32).tofile(f)
+    return path, tmp
+
+
+def ref_predict(csr, metric, H, max_edges, threads=REF_THREADS, timeout=600):
+    """predictLinks<Metric>Omp<H>(G, {1, max_edges}) of the reference on the CSR
+    file: (u, w, score) numpy arrays and its own time (ms)."""
+    fd, out = tempfile.mkstemp(dir=os.path.dirname(csr), suffix=".edges")
+    os.close(fd)
+    try:
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        t0 = time.time()
+        r = subprocess.run([REF_DRIVER, "predict", csr, str(metric), str(H), str(max_edges), "omp", str(threads), "1",
+                            out], capture_output=True, text=True, env=env, timeout=timeout)
+        wall = time.time() - t0
+        assert r.returncode == 0, r.stderr[-500:]
+        t_ms, ts_ms, n = r.stdout.split()
+        raw = np.fromfile(out, dtype=np.uint32)
+    finally:
+        os.unlink(out)
+    n = int(n)
+    assert int(raw[:2].view(np.uint64)[0]) == n
+    rec = raw[2:].reshape(n, 3)
+    return rec[:, 0].copy(), rec[:, 1].copy(), rec[:, 2].copy().view(np.float32), \
+        dict(time_ms=float(t_ms), wall_s=wall, n=n)
+
+
+def _t(x, dev):
+    import torch
+    if isinstance(x, torch.Tensor):
+        return x.to(dev)
+    return torch.as_tensor(np.ascontiguousarray(x)).to(dev)
+
+
+def keys_t(s):
+    """Order-preserving u32 score key (parity.keys_of) as int64, on the device."""
+    import torch
+    s = s.clone()
+    s[s == 0] = 0.0
+    b = s.view(torch.int32).long() & 0xffffffff
+    k = torch.where(b >= 0x80000000, 0xffffffff - b, b | 0x80000000)
+    k[torch.isnan(s)] = 0
+    return k
+
+
+def pk(u, w):
+    return (u.long() << 32) | w.long()
+
+
+def gpu_links(out_t, n):
+    """(u, w, score) device tensors of the first n links of an [N, 3] int32 output tensor."""
+    o = out_t[:n]
+    return o[:, 0].long() & 0xffffffff, o[:, 1].long() & 0xffffffff, o[:, 2].contiguous().view(__import__("torch").float32)
+
+
+def check_contract(gpu, ref_k, ref_ge, k, del_u, del_w, dev="cuda"):
+    """Contract 1-4 of the module docstring.  gpu = device tensors (u, w, s);
+    ref_k, ref_ge = numpy (u, w, s) of the reference's maxEdges = k call and
+    of its call with maxEdges = |above| + |ties|; del_u / del_w = the directed
+    deletions (both directions).  Returns the numbers of the check."""
+    import torch
+    gu, gw, gs = gpu
+    ru, rw, rs = (_t(x, dev) for x in ref_k[:3])
+    eu, ew, es = (_t(x, dev) for x in ref_ge[:3])
+    ru, rw, eu, ew = (x.long() & 0xffffffff for x in (ru, rw, eu, ew))
+    n = gu.numel()
+    assert ru.numel() == n, ("link counts differ", ru.numel(), n)
+    gk, rk, ek = keys_t(gs), keys_t(rs), keys_t(es)
+    assert not torch.isnan(rs).any(), "NaN scores: the reference's order is undefined (SURVEY A.4)"
+    assert torch.equal(torch.sort(gk).values, torch.sort(rk).values), "score multisets differ"
+    kth = int(rk.min())
+    ga = torch.sort(pk(gu, gw)[gk > kth]).values
+    ra = torch.sort(pk(ru, rw)[rk > kth]).values
+    assert torch.equal(ga, ra), "above-boundary sets differ (%d vs %d)" % (ga.numel(), ra.numel())
+    # the reference's whole tie set at the k-th score
+    assert int(ek.min()) >= kth, "the maxEdges = |A| + |T| reference call returned links below the k-th score"
+    ea = torch.sort(pk(eu, ew)[ek > kth]).values
+    assert torch.equal(ea, ra), "the two reference calls disagree above the k-th score"
+    T = torch.sort(pk(eu, ew)[ek == kth]).values
+    assert torch.unique(T).numel() == T.numel()
+    gt = pk(gu, gw)[gk == kth]
+    rt = pk(ru, rw)[rk == kth]
+    assert bool(torch.isin(gt, T).all()), "tie links outside the reference's tie set"
+    assert bool(torch.isin(rt, T).all()), "the reference's own ties outside its tie set"
+    assert torch.unique(pk(gu, gw)).numel() == n, "duplicate links in the output"
+    # F1 (main.cxx:48-57): both directions of every link against the directed deletions
+    D = torch.sort(pk(_t(del_u, dev).long() & 0xffffffff, _t(del_w, dev).long() & 0xffffffff)).values
+
+    def contrib(u, w):  # per link: how many of (u, w), (w, u) are deletions
+        return torch.isin(pk(u, w), D).long() + torch.isin(pk(w, u), D).long()
+
+    def common(u, w):
+        return int(contrib(u, w).sum())
+
+    r = n - ga.numel()
+    ca = common(ga >> 32, ga & 0xffffffff)
+    ct = torch.sort(contrib(T >> 32, T & 0xffffffff)).values
+    lo = ca + int(ct[:r].sum())
+    hi = ca + int(ct[ct.numel() - r:].sum()) if r > 0 else ca
+    cg, cr = common(gu, gw), common(ru, rw)
+    assert lo <= cg <= hi, ("our matches outside the tie bounds", lo, cg, hi)
+    assert lo <= cr <= hi, ("the reference's matches outside the tie bounds", lo, cr, hi)
+    nd = int(D.numel())
+
+    def f1(c):
+        p, rc = c / max(2 * n, 1), c / max(nd, 1)
+        return 0.0 if p + rc == 0 else 2 * p * rc / (p + rc)
+
+    return dict(k=k, n=n, kth_key=kth, above=int(ga.numel()), ties_total=int(T.numel()), ties_taken=r,
+                common_gpu=cg, common_ref=cr, common_lo=lo, common_hi=hi,
+                f1_gpu=f1(cg), f1_ref=f1(cr), f1_lo=f1(lo), f1_hi=f1(hi),
+                precision_gpu=cg / max(2 * n, 1), recall_gpu=cg / max(nd, 1))
+
+
+def run_reference_check(c, csr, metric, H, name):
+    """The whole check for one call on a bigconf.Config: our k-call, the
+    reference's k-call, the count of candidates at or above the k-th score (our
+    top-2k call), the reference's call with that many links, the contract.
+    Writes one JSON line to $NLP_TEST_REPORT_DIR/refcheck.jsonl when set."""
+    import torch
+    out = c.out()
+    n, t = c.G.predict_device(metric, H, c.k, out)
+    gpu = gpu_links(out, n)
+    kth = int(keys_t(gpu[2]).min()) if n else 0
+    # how many candidates score >= the k-th score: our canonical top-m for a
+    # growing m until it reaches below the k-th score (or holds every candidate)
+    m = min(int(t["candidates"]), 2 * c.k)
+    while True:
+        out2 = c.out(m)
+        n2, _ = c.G.predict_device(metric, H, m, out2)
+        k2 = keys_t(gpu_links(out2, n2)[2])
+        n_ge = int((k2 >= kth).sum())
+        if n_ge < n2 or n2 < m or m >= int(t["candidates"]):
+            break
+        m = min(int(t["candidates"]), 2 * m)
+    del out2, k2
+    torch.cuda.empty_cache()
+    ref_k = ref_predict(csr, metric, H, c.k)
+    ref_ge = ref_predict(csr, metric, H, n_ge)
+    res = check_contract(gpu, ref_k, ref_ge, c.k, c.del_u, c.del_w)
+    res.update(config=name, metric=metric, H=H, candidates=int(t["candidates"]), path=t["path"],
+               ref_threads=REF_THREADS, ref_time_ms=ref_k[3]["time_ms"], ref_ge_time_ms=ref_ge[3]["time_ms"],
+               gpu_ms=t["total_ms"])
+    rd = os.environ.get("NLP_TEST_REPORT_DIR")
+    if rd:
+        os.makedirs(rd, exist_ok=True)
+        with open(os.path.join(rd, "refcheck.jsonl"), "a") as f:
+            f.write(json.dumps(res) + "\n")
+    return res

@@ -58,3 +58,24 @@ def test_gpu_c3_jaccard_h16_hash_path(c3, oracle):
 def test_gpu_c3_adamic_adar_h16(c3, oracle):
     n, t = _check(c3, oracle, 7, 16, path=4)
     assert n == c3.k
+
+
+@pytest.fixture(scope="module")
+def c3_csr(c3):
+    import refcheck
+    if not refcheck.have_ref():
+        pytest.skip("oracle/_ref/ref_driver not built (needs the reference headers in the build container)")
+    path, tmp = refcheck.write_csr(c3.off, c3.keys)
+    yield path
+    tmp.cleanup()
+
+
+@pytest.mark.timeout(600)
+def test_gpu_c3_adamic_adar_h16_vs_reference(c3, c3_csr):
+    """BASELINE's "HBM-roofline run" (uk-2005, LHub Adamic-Adar) at H = 16 against the
+    reference ITSELF (predictLinksAdamicAdarCoefficientOmp<16>): the A.1 contract and
+    F1 within the tie bounds."""
+    import refcheck
+    r = refcheck.run_reference_check(c3, c3_csr, 7, 16, "C3-uk-2005")
+    assert r["n"] == c3.k and r["path"] == 4
+    assert r["f1_lo"] <= r["f1_gpu"] <= r["f1_hi"]

@@ -85,3 +85,24 @@ def test_gpu_c4_adamic_adar_h16_hash_path(c4, oracle):
     """Adamic-Adar on path 4 at the same size (ordered accumulation, hub sort mode)."""
     n, t = _check(c4, oracle, 7, 16)
     assert t["path"] == 4 and n == c4.k
+
+
+@pytest.fixture(scope="module")
+def c4_csr(c4):
+    import refcheck
+    if not refcheck.have_ref():
+        pytest.skip("oracle/_ref/ref_driver not built (needs the reference headers in the build container)")
+    path, tmp = refcheck.write_csr(c4.off, c4.keys)
+    yield path
+    tmp.cleanup()
+
+
+@pytest.mark.timeout(600)
+def test_gpu_c4_jaccard_h16_vs_reference(c4, c4_csr):
+    """The work point against the reference ITSELF (predictLinksJaccardCoefficientOmp<16>
+    compiled from /root/reference/inc, on the same CSR): score multiset, above-boundary
+    set, ties inside the reference's tie set, F1 within the tie bounds."""
+    import refcheck
+    r = refcheck.run_reference_check(c4, c4_csr, 1, 16, "C4-sk-2005")
+    assert r["n"] == c4.k and r["path"] == 4
+    assert r["f1_lo"] <= r["f1_gpu"] <= r["f1_hi"]

@@ -104,3 +104,23 @@ int main() {
     subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), str(src), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def test_ingest_reads_a_pipe(ingest_bin, tmp_path):
+    """a stream that cannot seek (a FIFO, as `<(zcat g.mtx.gz)` gives)
+    is read to its end like the reference's ifstream (mtx.hxx:138), not taken
+    for an empty graph."""
+    g = dict(np.load(os.path.join(GOLDEN, "ingest_general.npz"), allow_pickle=False))
+    fifo = str(tmp_path / "in.fifo")
+    os.mkfifo(fifo)
+    import threading
+
+    def feed():
+        with open(fifo, "wb") as f:
+            f.write(g["mtx"].tobytes())
+
+    th = threading.Thread(target=feed)
+    th.start()
+    got = run_ingest(ingest_bin, fifo, int(g["seed"][0]), float(g["d"][0]), str(tmp_path / "out"))
+    th.join()
+    assert_same(got, g)

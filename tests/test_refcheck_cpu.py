@@ -1,0 +1,51 @@
+"""The full-size reference checker (tests/refcheck.py) on the CPU, with the
+reference's own small fixtures: the canonical oracle's top-k stands in for the
+GPU result, the reference's OpenMP top-k is ref_k, and the reference's
+sequential all-candidate list cut at the k-th score is the tie-set call.  Also
+checks that a wrong tie, a changed score and an F1 outside the bounds fail."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import refcheck
+
+torch = pytest.importorskip("torch")
+
+
+def _case(oracle, name, m, H):
+    g = load_golden(name)
+    k = int(g["k"][0])
+    tag = "%d_%d" % (m, H)
+    ru, rw, rs = g["topk_%s_u" % tag], g["topk_%s_w" % tag], g["topk_%s_s" % tag]
+    cu, cw, cs = g["cand_%s_u" % tag], g["cand_%s_w" % tag], g["cand_%s_s" % tag]
+    u, w, s, _ = oracle.predict(g["offsets"], g["keys"], m, H, max_edges=k)
+    kth = refcheck.keys_t(torch.as_tensor(rs)).min()
+    ge = refcheck.keys_t(torch.as_tensor(cs)) >= kth
+    ge = ge.numpy()
+    gpu = (torch.as_tensor(u.astype(np.int64)), torch.as_tensor(w.astype(np.int64)), torch.as_tensor(s))
+    return g, k, gpu, (ru, rw, rs), (cu[ge], cw[ge], cs[ge])
+
+
+@pytest.mark.parametrize("m,H", [(1, 8), (7, 8), (0, 8)])
+def test_refcheck_accepts_the_oracle(oracle, m, H):
+    g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", m, H)
+    r = refcheck.check_contract(gpu, ref_k, ref_ge, k, g["del_u"], g["del_w"], dev="cpu")
+    assert r["n"] == len(ref_k[0]) and r["f1_lo"] <= r["f1_gpu"] <= r["f1_hi"]
+    assert r["ties_total"] >= r["ties_taken"]
+
+
+def test_refcheck_rejects_wrong_results(oracle):
+    g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", 1, 8)
+    u, w, s = gpu
+    # a changed score
+    s2 = s.clone()
+    s2[0] = torch.nextafter(s2[0], torch.tensor(0.0))
+    with pytest.raises(AssertionError):
+        refcheck.check_contract((u, w, s2), ref_k, ref_ge, k, g["del_u"], g["del_w"], dev="cpu")
+    # a boundary link that is not a candidate at that score
+    kk = refcheck.keys_t(s)
+    i = int(torch.nonzero(kk == kk.min())[-1])
+    w2 = w.clone()
+    w2[i] = int(g["offsets"].shape[0])  # no such vertex
+    with pytest.raises(AssertionError):
+        refcheck.check_contract((u, w2, s), ref_k, ref_ge, k, g["del_u"], g["del_w"], dev="cpu")

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session: STEPS (comma list, in order) out of
+# GPU session: STEPS (comma list, in order) out of
 #   tests   -- PYTEST_FILES (default: the dist and ingest GPU tests), one pytest process
 #   bench   -- the default bench line (headline + work point + both CPU baselines)
 #   prof    -- rocprofv3 --kernel-trace --stats of the bench without CPU baselines or sweep
@@ -13,9 +13,10 @@
 # script stops at the first failure.
 set -u
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-TAG=${TAG:-r04}
+TAG=${TAG:-session}
 OUT=$REPO/gpurun_out/$TAG
 mkdir -p "$OUT"
+export NLP_TEST_REPORT_DIR=$OUT
 STEPS=${STEPS:-tests,bench}
 BENCH_ARGS=${BENCH_ARGS:-}
 PROF_CMD="python3 $REPO/bench.py --steps 5 --warmup 2 --no-cpu-baseline --sweep = --wp-steps 3 --work-point ${WP:-16} $BENCH_ARGS"
@@ -31,8 +32,10 @@ run() {  # name limit cmd...
 }
 for s in ${STEPS//,/ }; do
   case $s in
-    tests) run tests ${TESTS_LIMIT:-600} python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_dist.py tests/test_gpu_ingest.py} \
-             ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    tests) run tests ${TESTS_LIMIT:-600} python -u -m pytest \
+             ${PYTEST_FILES:-tests/test_gpu_dist.py tests/test_gpu_ingest.py} ${PYTEST_K:+-k "$PYTEST_K"} -m gpu -x -v \
+             --durations=40 --timeout 600 --timeout-method thread -p no:cacheprovider ;;
+    smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench ${BENCH_LIMIT:-900} python3 bench.py $BENCH_ARGS
            grep '^{' "$OUT/bench.log" > "$OUT/bench.json" ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
