@@ -79,7 +79,6 @@ struct HpArgs {
   unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
   uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
   uint32_t uxf;            // rows whose exclusion slice exceeds uxf x W test the membership table (HP_UX_OFF: never)
-  uint32_t defer;          // k_hp_batch: those tests deferred to k_hp_xprobe (entries emitted with HP_DEFER in w)
 };
 
 // xs[u] = the number of entries of N(u) that are <= u (one binary search per row)
@@ -525,7 +524,7 @@ __device__ __forceinline__ void hp_flush(HpStage& st, const HpArgs& a) {
 // Candidate filter (predict.hxx:309-311: score <= minScore skips, NaN passes)
 // and emission above tau; every active lane of the wave calls it.
 __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid, float s, uint32_t u, uint32_t w,
-                                        int64_t tau, uint32_t wflag = 0u) {
+                                        int64_t tau) {
   const bool cand = valid && !(s <= a.min_score) && !f2_drop(a.g, u, w);
   st.cand += cand ? 1 : 0;
   st.nan += (cand && s != s) ? 1 : 0;
@@ -538,7 +537,7 @@ __device__ __forceinline__ void hp_emit(HpStage& st, const HpArgs& a, bool valid
   if (out) {
     const uint32_t i = st.n + (uint32_t)__popcll(mo & ((1ull << lane_id()) - 1));
     st.u[i] = u;
-    st.w[i] = w | wflag;
+    st.w[i] = w;
     st.s[i] = s;
   }
   st.n += n;
@@ -557,81 +556,6 @@ __device__ __forceinline__ void hp_finish(HpStage& st, const HpArgs& a, uint64_t
     if (n) atomicAdd(&a.ctr[HPC_NAN], (unsigned long long)n);
     if (wd) atomicAdd(&a.ctr[HPC_WEDGE], (unsigned long long)wd);
     if (st.pad) atomicAdd(&a.ctr[HPC_PAD], (unsigned long long)st.pad);
-  }
-}
-
-// ---------------------------------------------------------------- deferred exclusion tests
-// k_hp_batch's rows whose exclusion slice is long test their entries in the
-// membership table (one 64-byte line each).  Inside the row batches those
-// tests are a dependent load in a latency-bound loop (C4 JAC H=16: more than
-// half of the kernel).  Before the chunk's candidates are held against a
-// threshold (the host defers only while no tau is in force, so every entry
-// is emitted and counted), the batches emit such entries with their
-// unexcluded score and HP_DEFER set in w (vertex ids < 2^31); k_hp_xprobe
-// then tests all flagged entries of the chunk with IPT lines in flight per
-// thread: a member of N(u) gets the score of count 0 (predict.hxx:306-307,
-// then 309-311: usually 0 <= minScore -> padding; 0/0 = NaN stays a
-// candidate), a non-member loses the flag.  Counts are corrected in
-// xc[0] (candidates removed), xc[1] / xc[2] (NaN removed / added).
-constexpr uint32_t HP_DEFER = 0x80000000u;
-constexpr int HX_IPT = 8;
-__global__ __launch_bounds__(NT) void k_hp_xprobe(GraphView g, int metric, float min_score, uint32_t* __restrict__ ckey,
-                                                  uint32_t* __restrict__ cu, uint32_t* __restrict__ cw,
-                                                  float* __restrict__ cs, uint64_t base, uint64_t cap,
-                                                  const unsigned long long* __restrict__ ctr,
-                                                  unsigned long long* __restrict__ xc) {
-  const uint64_t n = min((uint64_t)ctr[HPC_EMIT], cap);
-  uint64_t drop = 0, nrm = 0, nadd = 0;
-  const uint64_t step = (uint64_t)gridDim.x * NT * HX_IPT;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * NT * HX_IPT; t0 < n; t0 += step) {
-    uint64_t key[HX_IPT];
-    bool act[HX_IPT], res[HX_IPT];
-    uint32_t wq[HX_IPT];
-#pragma unroll
-    for (int q = 0; q < HX_IPT; ++q) {
-      const uint64_t i = t0 + (uint64_t)q * NT + threadIdx.x;
-      wq[q] = i < n ? cw[base + i] : 0u;
-      act[q] = (wq[q] & HP_DEFER) && wq[q] != 0xffffffffu;  // padding: u = w = 0xffffffff
-    }
-#pragma unroll
-    for (int q = 0; q < HX_IPT; ++q) {
-      const uint64_t i = t0 + (uint64_t)q * NT + threadIdx.x;
-      key[q] = act[q] ? ((uint64_t)cu[base + i] << 32 | (wq[q] & ~HP_DEFER)) : 0ull;
-    }
-    et_has_n<HX_IPT>(g.etab, g.etbits, key, act, res);
-#pragma unroll
-    for (int q = 0; q < HX_IPT; ++q) {
-      if (!act[q]) continue;
-      const uint64_t i = base + t0 + (uint64_t)q * NT + threadIdx.x;
-      const uint32_t w = wq[q] & ~HP_DEFER;
-      if (!res[q]) {
-        cw[i] = w;
-        continue;
-      }
-      const uint32_t u = (uint32_t)(key[q] >> 32);
-      const float s0 = cs[i];
-      const float s = (metric == M_AA || metric == M_RA) ? 0.0f
-                                                         : score_basic(metric, 0u, (uint64_t)g.deg[u], (uint64_t)g.deg[w]);
-      nrm += (s0 != s0) ? 1 : 0;
-      if (s <= min_score) {  // no longer a candidate: padding (dropped by the prune)
-        ++drop;
-        ckey[i] = 0u;
-        cu[i] = 0xffffffffu;
-        cw[i] = 0xffffffffu;
-        cs[i] = __uint_as_float(0x7fc00000u);
-      } else {
-        nadd += (s != s) ? 1 : 0;
-        ckey[i] = score_key(s);
-        cw[i] = w;
-        cs[i] = s;
-      }
-    }
-  }
-  const uint64_t d = wave_sum(drop), r = wave_sum(nrm), ad = wave_sum(nadd);
-  if (lane_id() == 0) {
-    if (d) atomicAdd(&xc[0], (unsigned long long)d);
-    if (r) atomicAdd(&xc[1], (unsigned long long)r);
-    if (ad) atomicAdd(&xc[2], (unsigned long long)ad);
   }
 }
 
@@ -744,12 +668,14 @@ __device__ __forceinline__ void hp_drain(const HpTable& tb, uint32_t T, uint32_t
       continue;
     }
     if (!CUSTOM) {
+      // deg w for the score (Common Neighbours needs none: no gather per entry)
+      const bool need_dw = a.metric != M_CN;
 #pragma unroll
       for (int q = 0; q < UN; ++q) {
         if ((uint32_t)q >= nq) break;
         const uint32_t wq = w[q] != HP_EMPTY ? w[q] : 0u;
         if constexpr (KCB > 0) dw[q] = hp_kd_deg<KCB>(a.g, c[q], wq);
-        else dw[q] = a.g.deg[wq];
+        else dw[q] = need_dw ? a.g.deg[wq] : 0u;
       }
     }
     constexpr uint32_t CM = KCB > 0 ? (1u << KCB) - 1u : HP_CMASK;
@@ -2469,12 +2395,14 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         }
       }
       // first-order exclusion by the membership table for the entries of
-      // table-tested rows (count tables: two first buckets in flight at a time);
-      // with a.defer the tests are left to k_hp_xprobe (the entries go out flagged)
+      // table-tested rows (count tables: two first buckets in flight at a time;
+      // the tests deferred to a separate high-occupancy kernel after the chunk
+      // measured slower: C4 JAC H=16 43.4 -> 48.1 ms, the kernel 13.9 -> 9.7 ms
+      // but the deferred probes ~9 ms -- a random 64-byte line per test, no
+      // longer hidden behind the batches' own latency)
 #pragma unroll
       for (int q0 = 0; q0 < UN; q0 += 2) {
         if ((uint32_t)q0 >= nq) break;
-        if (a.defer) break;
         uint64_t ek[2];
         bool ea[2], er[2];
 #pragma unroll
@@ -2511,7 +2439,7 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
           if (CUSTOM) s = ho_score(c[q]);
           else s = score_basic(a.metric, (c[q] & HP_EXCL) ? 0u : (c[q] & (KD ? 1023u : HP_CMASK)), du2, (uint64_t)dw[q]);
         }
-        hp_emit(sg, a, valid, s, uu, w, tau, (a.defer && valid && s_ux[wv][sl]) ? HP_DEFER : 0u);
+        hp_emit(sg, a, valid, s, uu, w, tau);
       }
     }
     wave_sync_lds();
@@ -3330,6 +3258,9 @@ constexpr uint64_t HH_WC = 16384;   // wedges (every w of the row's flattened li
 constexpr int HH_NT = 256;          // threads of the enumeration and accumulation workgroups
 constexpr int HH_NW = HH_NT / 64;
 constexpr int HH_TL = 13;           // accumulation table: 2^13 LDS entries (2^12 for AA / RA)
+constexpr int HH_XP = 2;            // exclusion keys per thread loaded with an item's first wedges
+constexpr int HH_TLC = 12;          // the count metrics' default table log (k_hh_accum<false, 12>)
+constexpr int HH_AUN = 8;           // an item's wedges per thread loaded together (most items: one round trip)
 
 __device__ __forceinline__ uint32_t hh_row_u(const uint32_t* l2, uint64_t n2, const uint32_t* l3, uint64_t r) {
   return r < n2 ? l2[r] : l3[r - n2];
@@ -3995,20 +3926,21 @@ constexpr uint32_t HS_DMAX = 4095;
 // words of the hash table), sorted, and every run of equal w summed by its
 // first thread in ascending v -- the additions of predict.hxx:788 / 828 in the
 // reference's order; the exclusion marks the run of each x in N(u).
-template <bool CUSTOM>
+// TLC: log2 of the count metrics' table (the LDS it takes sets the workgroups
+// per CU of this latency-bound kernel; k_hh_plan sizes the items for it)
+template <bool CUSTOM, int TLC = HH_TL>
 __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __restrict__ items,
                                                     const uint32_t* __restrict__ nitems,
                                                     const uint32_t* __restrict__ sw0, const uint32_t* __restrict__ sv0,
                                                     const uint32_t* __restrict__ pw, const uint32_t* __restrict__ pv,
                                                     uint32_t* __restrict__ queue, int sortmode, uint64_t cap) {
-  constexpr int TL = CUSTOM ? HH_TL - 1 : HH_TL;
+  constexpr int TL = CUSTOM ? HH_TL - 1 : TLC;
   constexpr int LT = 1 << TL;
   constexpr int VT = CUSTOM ? LT : 1;
   static_assert(!CUSTOM || LT >= (int)HH_SCAP, "the sort buffer overlays the vmin / vmax words");
-  __shared__ uint32_t s_tab[2 * LT];  // keys | counts; or HH_DW direct counters
+  __shared__ uint32_t s_tab[2 * LT];  // keys | counts; or direct counters (ranges of at most 2 LT w: the plan's dw)
   uint32_t* const s_k = s_tab;
   uint32_t* const s_c = s_tab + LT;
-  static_assert(CUSTOM || 2 * LT >= (int)HH_DW, "direct counters overlay the table");
   __shared__ uint64_t s_vv[VT];  // vmin | vmax (2 x LT u32), or the sort-mode keys (LT u64)
   __shared__ uint8_t s_ex[CUSTOM ? HH_SCAP : 1];
   __shared__ uint32_t s_gu[HH_NW][HP_BSTG], s_gw[HH_NW][HP_BSTG];
@@ -4138,17 +4070,21 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         const uint64_t xhi = shi - xlo > step ? xlo + step : shi;
         const uint32_t span = (uint32_t)(xhi - xlo);
         const bool all = whole && step == shi - slo;
+        if (span > 2u * LT) {  // a plan beyond the table (a sizing bug): fail the call, never overrun LDS
+          if (t == 0) atomicOr(&a.ctr[HPC_ERR], 2ull);
+          break;
+        }
         for (uint32_t i = t; i < span; i += HH_NT) s_tab[i] = 0;
         __syncthreads();
-        for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
-          uint32_t wq[HP_UN];
+        for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HH_AUN) {
+          uint32_t wq[HH_AUN];
 #pragma unroll
-          for (int k = 0; k < HP_UN; ++k) {
+          for (int k = 0; k < HH_AUN; ++k) {
             const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
             wq[k] = sw[off + (i < n ? i : 0u)];
           }
 #pragma unroll
-          for (int k = 0; k < HP_UN; ++k) {
+          for (int k = 0; k < HH_AUN; ++k) {
             const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
             if (i < n && (all || ((uint64_t)wq[k] >= xlo && (uint64_t)wq[k] < xhi))) {
               ++wedges;
@@ -4172,7 +4108,8 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
           const bool valid = (c & ~HH_DMARK) != 0;
           const uint32_t w = (uint32_t)(xlo + i);
           float sc = 0.0f;
-          if (valid) sc = score_basic(a.metric, (c & HH_DMARK) ? 0u : c, du, (uint64_t)a.g.deg[w]);
+          if (valid)
+            sc = score_basic(a.metric, (c & HH_DMARK) ? 0u : c, du, a.metric != M_CN ? (uint64_t)a.g.deg[w] : 0ull);
           hp_emit(sg, a, valid, sc, u, w, tau);
         }
         __syncthreads();
@@ -4185,20 +4122,29 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     const int hs = 32 - (lg < TL ? lg : TL);
     // an HH_WIDE item: sub-ranges of dcnt w, each through the table
     const uint64_t step = (item.cnt & HH_WIDE) ? dcnt : shi - slo;
+    // the first HH_XP x HH_NT keys of the exclusion slice are loaded with the
+    // first wedges (one memory round trip fewer per item); the rest streams
+    const uint64_t nx = x1 - x0;
+    uint32_t xk[HH_XP];
+#pragma unroll
+    for (int q = 0; q < HH_XP; ++q) {
+      const uint64_t i = (uint64_t)q * HH_NT + (uint64_t)t;
+      xk[q] = i < nx ? a.g.keys[x0 + i] : 0u;
+    }
     for (uint64_t xlo = slo; xlo < shi; xlo += step) {
       const uint64_t xhi = shi - xlo > step ? xlo + step : shi;
       const bool all = whole && step == shi - slo;
-      for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
-        uint32_t wq[HP_UN], vq[HP_UN];
+      for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HH_AUN) {
+        uint32_t wq[HH_AUN], vq[HH_AUN];
 #pragma unroll
-        for (int k = 0; k < HP_UN; ++k) {
+        for (int k = 0; k < HH_AUN; ++k) {
           const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
           const uint64_t p = off + (i < n ? i : 0u);
           wq[k] = sw[p];
           vq[k] = CUSTOM ? sv[p] : 0u;
         }
 #pragma unroll
-        for (int k = 0; k < HP_UN; ++k) {
+        for (int k = 0; k < HH_AUN; ++k) {
           const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
           if (i < n && (all || ((uint64_t)wq[k] >= xlo && (uint64_t)wq[k] < xhi))) {
             ++wedges;
@@ -4208,9 +4154,17 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       }
       __syncthreads();
       // first-order exclusion: the entries of N(u) in [xlo, xhi)
-      hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
-        if ((uint64_t)x >= xlo && (uint64_t)x < xhi) hp_mark<false>(tb, mask, hs, x);
-      });
+#pragma unroll
+      for (int q = 0; q < HH_XP; ++q) {
+        const uint32_t x = xk[q];
+        if ((uint64_t)q * HH_NT + (uint64_t)t < nx && (uint64_t)x >= xlo && (uint64_t)x < xhi)
+          hp_mark<false>(tb, mask, hs, x);
+      }
+      if (nx > (uint64_t)HH_XP * HH_NT)
+        hp_stream(a.g.keys + x0 + (uint64_t)HH_XP * HH_NT, nx - (uint64_t)HH_XP * HH_NT, (uint32_t)t, (uint32_t)HH_NT,
+                  [&](uint32_t x) {
+                    if ((uint64_t)x >= xlo && (uint64_t)x < xhi) hp_mark<false>(tb, mask, hs, x);
+                  });
       __syncthreads();
       hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
       __syncthreads();

@@ -292,7 +292,6 @@ struct nlp_graph {
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hp_uxf = HB_XF;   // exclusion by the membership table for slices beyond hp_uxf x W
-  bool hp_xdefer = true;      // k_hp_batch's table tests deferred to k_hp_xprobe (NLP_HASH_XDEFER=0: in the kernel)
                              // (NLP_HASH_UX=off: always marks; =0: always the table)
   int hp_rowb = 1;           // bin 1, count metrics: tiered 256-thread rows (NLP_HASH_ROWB=0: k_hp_block;
                              // 2: every row in the 8192-entry tier, 3: none in the 2048-entry tier -- tests)
@@ -894,7 +893,6 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
-  if (const char* xd = getenv("NLP_HASH_XDEFER")) g->hp_xdefer = xd[0] != '0';
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
   if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = atoi(ho);
@@ -1841,13 +1839,16 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                        (const uint64_t*)fbase, (const uint64_t*)fp, bcnt, (const uint64_t*)boff, bcur, sw, sv);
   TRY(hipGetLastError());
   // accumulation items (k_hh_plan, k_hh_group): a bucket, or a w-range of a heavy bucket
-  const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TL);
+  // count metrics: 4096-entry tables by default (C5 range: 47.7 -> 41.9 ms against 8192 entries, two
+  // workgroups per CU more; 2048 entries split too many buckets: 176 ms)
+  const int tl = std::min(custom ? HH_TL - 1 : HH_TL, g->hh_tl ? g->hh_tl : HH_TLC);
   // AA / RA: sort-mode items (at most HH_SCAP wedges each, keys need w, v < 2^26)
   const uint32_t wcap = custom && g->hh_sort && g->span <= (1ull << 26) ? g->hh_scap : 0u;
   // heavy buckets hold more than `half` wedges each; their groups close past
   // `half` wedges, so a heavy bucket of n wedges gives at most 2 n / half + 2
   // items (single bins beyond a group included)
-  const uint32_t dw = custom ? 0u : g->hh_dw;  // direct counters: counts only
+  const uint32_t dw = custom ? 0u : std::min<uint32_t>(g->hh_dw, 2u << tl);  // direct counters: counts only,
+                                                                             // within the table's two words
   const uint64_t half = wcap ? wcap : (1ull << (tl - 1));
   const uint64_t hcap = tot / half + 1;
   const uint64_t cap = NB + 4 * (tot / half) + 2 * hcap + 1024;
@@ -1880,15 +1881,17 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
                      (const HhHeavy*)heavy, (const unsigned long long*)hctr, hcap, (const uint64_t*)boff,
                      (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)gh, gcur, pw, pv);
   TRY(hipGetLastError());
-  const unsigned gr = (unsigned)(4 * (uint64_t)g->hp_gp);
-  if (custom)
-    hipLaunchKernelGGL((k_hh_accum<true>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
-                       (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw,
-                       (const uint32_t*)pv, queue, (int)(wcap != 0), cap);
-  else
-    hipLaunchKernelGGL((k_hh_accum<false>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,
-                       (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw,
-                       (const uint32_t*)pv, queue, 0, cap);
+  // persistent workgroups over the item queue: the table's LDS decides how many fit a CU
+  const unsigned gr = (unsigned)((custom || tl >= 13 ? 4 : 8) * (uint64_t)g->hp_gp);
+#define NLP_HH_ACCUM(CU, TLC)                                                                                 \
+  hipLaunchKernelGGL((k_hh_accum<CU, TLC>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,            \
+                     (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw, \
+                     (const uint32_t*)pv, queue, (int)(wcap != 0), cap)
+  if (custom) NLP_HH_ACCUM(true, HH_TL);
+  else if (tl >= 13) NLP_HH_ACCUM(false, 13);
+  else if (tl == 12) NLP_HH_ACCUM(false, 12);
+  else NLP_HH_ACCUM(false, 11);
+#undef NLP_HH_ACCUM
   TRY(hipGetLastError());
   if (g->hh_stats) {  // debug: how often the accumulation items stream their buckets
     TRY(hipStreamSynchronize(st));
@@ -2255,13 +2258,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.xs = g->xs;
     a.win = 0;
     a.uxf = g->hp_uxf;
-    // membership-table tests of the row batches deferred to k_hp_xprobe while no threshold is in
-    // force (every entry is then emitted, so the probe sees -- and corrects the counts of -- all)
-    a.defer = (!full && g->hp_xdefer && gv.etab && a.uxf != HP_UX_OFF && S <= (1ull << 31)) ? 1u : 0u;
     a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
     if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
-    bool batch_timed = false, probed = false;
+    bool batch_timed = false;
     if (n0 && g->hp_tiers) {
       // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
       TRY(hipMemsetAsync(tcnt, 0, 8 * sizeof(uint32_t), st));
@@ -2310,14 +2310,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         TRY(hipGetLastError());
         TRY(hipEventRecord(g->ev[6], st));
         batch_timed = true;
-        if (a.defer) {
-          TRY(hipMemsetAsync(small + 60, 0, 24, st));
-          const unsigned gx = (unsigned)std::min<uint64_t>(wchunk / ((uint64_t)NT * HX_IPT) + 1, 8192);
-          hipLaunchKernelGGL(k_hp_xprobe, dim3(gx), dim3(NT), 0, st, gv, p.metric, p.min_score, a.ckey, a.cu, a.cw,
-                             a.cs, a.base, a.cap, (const unsigned long long*)small, (unsigned long long*)(small + 60));
-          TRY(hipGetLastError());
-          probed = true;
-        }
         a.win = 0;  // the other row kernels reserve per flush
         if (custom) hipLaunchKernelGGL((k_hp_wave<true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
         else if (a.kdeg) hipLaunchKernelGGL((k_hp_wave<false, HP_WT, HP_STG, true>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
@@ -2404,7 +2396,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
     }
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
-    if (probed) TRY(hipMemcpyAsync(&g->host_small[60], small + 60, 24, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
     if (batch_timed) {
@@ -2443,13 +2434,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     }
     ++*nchunks;
     retry = false;
-    if (probed) {  // k_hp_xprobe: excluded entries turned into padding, the counts corrected
-      const uint64_t xdrop = g->host_small[60], xnrm = g->host_small[61], xnadd = g->host_small[62];
-      g->host_small[HPC_CAND] -= xdrop;
-      g->host_small[HPC_NAN] = g->host_small[HPC_NAN] + xnadd - xnrm;
-      g->host_small[HPC_PAD] += xdrop;
-      C.call_bytes += 4 * emitted + 72 * xdrop;  // flags read; tested entries: u, w back, a 64-byte line
-    }
     // row bookkeeping (W+(u), survivor prefix, bins, tiers: ~64 B per row), per wedge its key and
     // entry degree plus its packed survivor entry at most (16 B of the chunk's bound), 16 B per emission
     C.call_bytes += 64 * (r1 - r0) + 16 * wchunk + 16 * emitted;

@@ -6,6 +6,8 @@
 #   pmc     -- FETCH_SIZE and WRITE_SIZE passes (separate runs) of that same command
 #   c5prof  -- kernel trace + stats of tools/range_call.py (C5 IHub range)
 #   c5pmc   -- FETCH_SIZE / WRITE_SIZE passes of that range call
+#   c5      -- the range call alone (its JSON line in c5.json)
+#   c5sq    -- one --pmc pass of the counters in PMC over the range call
 #   sweep   -- tools/sweep.py SWEEP_ARGS
 #   sweepprof -- the same under rocprofv3 --kernel-trace --stats
 #   sweeppmc  -- the same under one --pmc pass of the counters in PMC
@@ -46,6 +48,10 @@ for s in ${STEPS//,/ }; do
          done ;;
     c5prof) (cd /tmp && export TMPDIR=/tmp && run c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                -d "$OUT/c5prof" -o c5 -- $C5_CMD) || exit 1 ;;
+    c5) run c5 600 $C5_CMD
+        grep '^{' "$OUT/c5.log" > "$OUT/c5.json" ;;
+    c5sq) (cd /tmp && export TMPDIR=/tmp && run c5sq 300 rocprofv3 --kernel-trace --pmc ${PMC:-SQ_WAVE_CYCLES} \
+             --output-format csv -d "$OUT/c5sq" -o pmc -- $C5_CMD) || exit 1 ;;
     c5pmc) for c in FETCH_SIZE WRITE_SIZE; do
              (cd /tmp && export TMPDIR=/tmp && run c5pmc_$c 600 rocprofv3 --kernel-trace --pmc $c --output-format csv \
                 -d "$OUT/c5pmc_$c" -o pmc -- $C5_CMD) || exit 1
