@@ -183,6 +183,13 @@ nlp_status nlp_predict_ex(nlp_graph* g, nlp_metric metric, uint32_t hub_max_degr
  * the handle.  This is the second half of the count query above. */
 nlp_status nlp_copy_last(nlp_graph* g, nlp_edge* out, uint64_t n, uint64_t* copied);
 
+/* Page-locked host memory (hipHostMalloc) for result copies at the full PCIe
+ * rate: the C++ header (include/nlp/predict.hxx) keeps one such staging buffer
+ * per thread and converts the links from it into the reference's
+ * vector<tuple> (PredictLinkResult::edges, predict.hxx:65-102). */
+nlp_status nlp_host_alloc(uint64_t bytes, void** out);
+void nlp_host_free(void* p);
+
 /* Device-resident variant for a source-vertex range [u_begin, u_end) (the
  * multi-GPU shard; pass 0, UINT64_MAX for all).  `d_out` is a DEVICE array of
  * at least max_edges entries; `stream` is a hipStream_t (NULL = the graph's

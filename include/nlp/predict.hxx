@@ -39,6 +39,7 @@
 #pragma once
 #include <algorithm>
 #include <chrono>
+#include <future>
 #include <cstdint>
 #include <cstddef>
 #include <cstdlib>
@@ -143,6 +144,45 @@ inline uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+
+// The row hash r = r * P + v over a row's keys (seed first), evaluated in four
+// independent chains -- entries 4g + j into c_j = c_j P^4 + v, the seed into
+// s = s P^4 -- and recombined as s + c_0 P^3 + c_1 P^2 + c_2 P + c_3, then the
+// remaining < 4 entries one by one: the same value as the sequential loop
+// (polynomial arithmetic mod 2^64), four multiply-adds in flight instead of
+// one dependent chain (the fingerprint was bound by that chain).
+struct RowHash {
+  static constexpr uint64_t P = 0x100000001B3ull, P2 = P * P, P3 = P2 * P, P4 = P2 * P2;
+  uint64_t s, c0 = 0, c1 = 0, c2 = 0, c3 = 0, d = 0;
+  uint32_t q[4];
+  int nq = 0;
+  explicit RowHash(uint64_t seed) : s(seed) {}
+  void add(uint32_t v) {
+    q[nq++] = v;
+    ++d;
+    if (nq == 4) {
+      c0 = c0 * P4 + q[0];
+      c1 = c1 * P4 + q[1];
+      c2 = c2 * P4 + q[2];
+      c3 = c3 * P4 + q[3];
+      s *= P4;
+      nq = 0;
+    }
+  }
+  void add4(const uint32_t* v) {  // four consecutive keys (no partial group pending)
+    c0 = c0 * P4 + v[0];
+    c1 = c1 * P4 + v[1];
+    c2 = c2 * P4 + v[2];
+    c3 = c3 * P4 + v[3];
+    s *= P4;
+    d += 4;
+  }
+  uint64_t value() const {
+    uint64_t r = s + c0 * P3 + c1 * P2 + c2 * P + c3;
+    for (int i = 0; i < nq; ++i) r = r * P + q[i];
+    return r;
+  }
+};
 }  // namespace detail
 
 /** Build the identity-id CSR of any graph concept G (csr.hxx:106-222 layout,
@@ -176,11 +216,21 @@ inline uint64_t graphFingerprint(const G& x, uint64_t* entries) {
   uint64_t h = 0, m = 0;
 #pragma omp parallel for schedule(dynamic, 4096) reduction(+ : h, m)
   for (long long u = 0; u < S; ++u) {
-    uint64_t r = 0x9E3779B97F4A7C15ull * uint64_t(u + 1), d = 0;
-    detail::forRow(x, size_t(u), [&](size_t, uint32_t v) {
-      r = r * 0x100000001B3ull + v;
-      ++d;
-    });
+    detail::RowHash rh(0x9E3779B97F4A7C15ull * uint64_t(u + 1));
+    if constexpr (detail::has_csr_members<G>::value) {
+      const size_t o = size_t(x.offsets[u]), d = size_t(x.degrees[u]);
+      if constexpr (sizeof(x.edgeKeys[0]) == 4) {
+        const uint32_t* k = (const uint32_t*)&x.edgeKeys[0] + o;
+        size_t i = 0;
+        for (; i + 4 <= d; i += 4) rh.add4(k + i);
+        for (; i < d; ++i) rh.add(k[i]);
+      } else {
+        for (size_t i = 0; i < d; ++i) rh.add(uint32_t(x.edgeKeys[o + i]));
+      }
+    } else {
+      detail::forRow(x, size_t(u), [&](size_t, uint32_t v) { rh.add(v); });
+    }
+    const uint64_t r = rh.value(), d = rh.d;
     h += detail::mix64(r ^ (d << 40) ^ uint64_t(u));
     m += d;
   }
@@ -274,6 +324,35 @@ class HipGraph {
   nlp_graph* g_ = nullptr;
 };
 
+namespace detail {
+// One page-locked staging buffer per thread, reused across calls (grown by
+// half again when too small): the device->host copy of a call's links runs at
+// the full PCIe rate instead of through the driver's pageable bounce buffers.
+struct Staging {
+  nlp_edge* p = nullptr;
+  uint64_t cap = 0;
+  std::unique_ptr<nlp_edge[]> heap;  // when page-locked memory is refused
+  ~Staging() { nlp_host_free(p); }
+  nlp_edge* get(uint64_t n) {
+    if (n <= cap) return p ? p : heap.get();
+    nlp_host_free(p);
+    p = nullptr;
+    heap.reset();
+    const uint64_t c = std::max<uint64_t>(n, cap + cap / 2);
+    if (nlp_host_alloc(c * sizeof(nlp_edge), (void**)&p) != NLP_OK) {
+      p = nullptr;
+      heap.reset(new nlp_edge[c]);
+    }
+    cap = c;
+    return p ? p : heap.get();
+  }
+};
+inline Staging& staging() {
+  static thread_local Staging s;
+  return s;
+}
+}  // namespace detail
+
 /** predictLinks<Metric>Omp on a resident graph. */
 template <class K = uint32_t, class W = float>
 inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric metric, uint32_t mindegree1,
@@ -286,12 +365,12 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
   // (main.cxx asks for |del|/2 links; a low hub threshold predicts a few)
   check(nlp_predict_ex(g.get(), metric, mindegree1, maxfactor2, float(o.minScore), me, o.repeat, nullptr, &n, &t),
         "nlp_predict_ex");
-  std::unique_ptr<nlp_edge[]> buf(new nlp_edge[n ? n : 1]);  // default-initialised: written by the copy
+  nlp_edge* buf = detail::staging().get(n ? n : 1);
   uint64_t got = 0;
-  if (n) check(nlp_copy_last(g.get(), buf.get(), n, &got), "nlp_copy_last");
+  if (n) check(nlp_copy_last(g.get(), buf, n, &got), "nlp_copy_last");
   n = got;
   std::vector<std::tuple<K, K, W>> a(n);
-  const nlp_edge* b = buf.get();
+  const nlp_edge* b = buf;
 #pragma omp parallel for schedule(static)
   for (long long i = 0; i < (long long)n; ++i) a[size_t(i)] = std::tuple<K, K, W>(K(b[i].u), K(b[i].v), W(b[i].score));
   return PredictLinkResult<K, W>(std::move(a), t.total_ms, t.score_ms);
@@ -313,9 +392,13 @@ struct GraphCache {
   std::vector<int> devices;
   HipGraph g;
 };
+inline GraphCache& graphCache() {
+  static thread_local GraphCache c;
+  return c;
+}
 template <class G>
 inline const HipGraph& cachedGraph(const G& x) {
-  static thread_local GraphCache c;
+  GraphCache& c = graphCache();
   uint64_t m = 0;
   const uint64_t fp = graphFingerprint(x, &m);
   std::vector<int> devs = defaultDevices();
@@ -340,7 +423,22 @@ inline PredictLinkResult<typename G::key_type, W> predictLinksHipAny(const G& x,
                                                                      uint32_t mindegree1,
                                                                      const PredictLinkOptions<W>& o,
                                                                      uint32_t maxfactor2 = 0) {
-  return predictLinksHip<typename G::key_type, W>(detail::cachedGraph(x), metric, mindegree1, o, maxfactor2);
+  using K = typename G::key_type;
+  detail::GraphCache& c = detail::graphCache();
+  if (c.g.get() && c.addr == (const void*)&x && c.span == size_t(x.span()) && c.devices == defaultDevices()) {
+    // the same object as last time: predict on the resident copy while the
+    // fingerprint confirms, on another thread, that its adjacency is unchanged;
+    // a changed graph discards the result and is uploaded and predicted again
+    auto fut = std::async(std::launch::async, [&x] {
+      uint64_t m = 0;
+      const uint64_t fp = graphFingerprint(x, &m);
+      return std::make_pair(fp, m);
+    });
+    auto r = predictLinksHip<K, W>(c.g, metric, mindegree1, o, maxfactor2);
+    const auto fm = fut.get();
+    if (fm.first == c.fp && fm.second == c.entries) return r;
+  }
+  return predictLinksHip<K, W>(detail::cachedGraph(x), metric, mindegree1, o, maxfactor2);
 }
 
 template <class W>

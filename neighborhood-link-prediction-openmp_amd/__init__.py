@@ -65,7 +65,7 @@ EXPORTS = [
     "nlp_sync", "nlp_select_edges_device",
     "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
     "nlp_metric_name", "nlp_version", "nlp_graph_create_multi", "nlp_device_count", "nlp_graph_parts",
-    "nlp_ingest_device", "nlp_delete_edges_device",
+    "nlp_ingest_device", "nlp_delete_edges_device", "nlp_host_alloc", "nlp_host_free",
 ]
 
 _lib = None

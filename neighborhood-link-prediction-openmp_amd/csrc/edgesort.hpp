@@ -276,6 +276,300 @@ __global__ __launch_bounds__(NTH) void k_es_pass(const uint32_t* __restrict__ cu
   }
 }
 
+// ---------------------------------------------------------------- rank-compressed 8-byte keys
+// A call's top k holds few distinct scores (Jaccard / CN at H = 16 on C4: a
+// few hundred), so the score key is replaced by its dense rank r among the
+// D distinct keys (descending) and the composite
+//
+//     K8 = r << 2vb | u << vb | w          (bits(D - 1) + 2 vb <= 64 bits)
+//
+// is sorted instead of K: passes move 8-byte keys instead of 12-byte records,
+// and K8 has fewer digits than K (C4: 8 instead of 10 passes).  The last pass
+// writes the caller's edges with the score of rank r from a D-entry table.
+// The distinct keys are collected in a global open-addressing set of key + 1
+// (0 = empty; a key of 0xffffffff is a NaN bit pattern and never occurs),
+// filled per workgroup from an LDS set whose lookups are plain reads in the
+// steady state (no atomic once a key is in).  Calls with a NaN or zero score
+// (several bit patterns behind one key), more than ES_DMAX distinct keys or
+// too many bits keep the 12-byte sort.
+constexpr uint32_t ES_DCAP = 16384;  // global set slots (<= ES_DMAX keys: load <= 1/4)
+constexpr uint32_t ES_DMAX = 4096;   // distinct keys at most (12 rank bits)
+constexpr uint32_t ES_LCAP = 4096;   // LDS set slots per workgroup
+constexpr int ES_DLOG = 14;
+constexpr uint64_t ES8_MIN = 1ull << 16;  // smaller calls keep the 12-byte sort (no extra host round trip)
+
+__device__ __forceinline__ uint32_t es_dhash(uint32_t x, int lg) { return (x * 0x9E3779B1u) >> (32 - lg); }
+
+// gcnt[0]: distinct keys in the global set; gcnt[1]: overflow (the caller keeps the 12-byte sort)
+__global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs, uint64_t n, uint32_t* __restrict__ gset,
+                                                    uint32_t* __restrict__ gcnt) {
+  __shared__ uint32_t s_set[ES_LCAP];
+  __shared__ uint32_t s_n, s_over;
+  for (int i = threadIdx.x; i < (int)ES_LCAP; i += ES_NT) s_set[i] = 0;
+  if (threadIdx.x == 0) { s_n = 0; s_over = 0; }
+  __syncthreads();
+  constexpr int LLG = 12;  // log2 ES_LCAP
+  const uint64_t stride = (uint64_t)gridDim.x * ES_NT;
+  for (uint64_t j = (uint64_t)blockIdx.x * ES_NT + threadIdx.x; j < n; j += stride) {
+    const uint32_t x = score_key(cs[j]) + 1u;
+    uint32_t h = es_dhash(x, LLG);
+    for (uint32_t probe = 0; probe < ES_LCAP; ++probe) {
+      const uint32_t cur = s_set[h];  // a plain read: the common case, the key is already in
+      if (cur == x) break;
+      if (cur == 0) {
+        const uint32_t old = atomicCAS(&s_set[h], 0u, x);
+        if (old == 0) {
+          if (atomicAdd(&s_n, 1u) >= ES_LCAP / 2) s_over = 1;
+          break;
+        }
+        if (old == x) break;
+      }
+      h = (h + 1) & (ES_LCAP - 1);
+    }
+    if (s_over) break;  // (racy read is fine: the flag only ever goes up)
+  }
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&gcnt[1], 1u);
+    return;
+  }
+  for (int i = threadIdx.x; i < (int)ES_LCAP; i += ES_NT) {
+    const uint32_t x = s_set[i];
+    if (!x) continue;
+    uint32_t h = es_dhash(x, ES_DLOG);
+    for (uint32_t probe = 0;; ++probe) {
+      if (probe >= ES_DCAP) { atomicOr(&gcnt[1], 1u); break; }
+      const uint32_t cur = __hip_atomic_load(&gset[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == x) break;
+      if (cur == 0) {
+        const uint32_t old = atomicCAS(&gset[h], 0u, x);
+        if (old == 0) {
+          if (atomicAdd(&gcnt[0], 1u) >= ES_DMAX) atomicOr(&gcnt[1], 1u);
+          break;
+        }
+        if (old == x) break;
+      }
+      h = (h + 1) & (ES_DCAP - 1);
+    }
+  }
+}
+
+// the rank of a record's score key (it is in the set)
+__device__ __forceinline__ uint64_t es_rank(const uint32_t* __restrict__ gset, const uint16_t* __restrict__ srank,
+                                            float s) {
+  const uint32_t x = score_key(s) + 1u;
+  uint32_t h = es_dhash(x, ES_DLOG);
+  for (uint32_t probe = 0; probe < ES_DCAP; ++probe) {
+    if (gset[h] == x) return srank[h];
+    h = (h + 1) & (ES_DCAP - 1);
+  }
+  return 0;  // unreachable: every key was inserted
+}
+
+__device__ __forceinline__ uint64_t es_k8(const uint32_t* __restrict__ gset, const uint16_t* __restrict__ srank,
+                                          uint32_t u, uint32_t w, float s, int vb) {
+  return es_rank(gset, srank, s) << (2 * vb) | (uint64_t)u << vb | w;
+}
+
+// ghist[p * 256 + d]: records whose digit p of K8 is d
+__global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+                                                    const float* __restrict__ cs, uint64_t n, int vb,
+                                                    const uint32_t* __restrict__ gset,
+                                                    const uint16_t* __restrict__ srank, uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t h[8][256];
+  for (int i = threadIdx.x; i < 8 * 256; i += ES_NT) (&h[0][0])[i] = 0;
+  __syncthreads();
+  constexpr int UN = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * ES_NT * UN;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT * UN; j0 < n; j0 += stride) {  // uniform per wave: ballots below
+    uint32_t u[UN], w[UN];
+    float s[UN];
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
+      const bool ok = j < n;
+      u[q] = ok ? cu[j] : 0u;
+      w[q] = ok ? cw[j] : 0u;
+      s[q] = ok ? cs[j] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const bool ok = j0 + (uint64_t)q * ES_NT + threadIdx.x < n;
+      const uint64_t k = ok ? es_k8(gset, srank, u[q], w[q], s[q], vb) : 0ull;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const uint32_t d = (uint32_t)(k >> (8 * p)) & 0xffu;
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        if (__ballot(ok && d != d0) == 0) {  // one digit in the whole wave: one atomic
+          const uint64_t m = __ballot(ok);
+          if (m && lane_id() == 0) atomicAdd(&h[p][d0], (uint32_t)__popcll(m));
+        } else if (ok) {
+          atomicAdd(&h[p][d], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 8 * 256; i += ES_NT) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&ghist[i], c);
+  }
+}
+
+// One pass over 8-byte keys.  FIRST: the input is the candidate columns (K8
+// built from them); LAST: the output is the caller's edges (the score of rank
+// r from rscore).  Same tiling, look-back and write-out as k_es_pass.
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
+                                                    const float* __restrict__ cs, const uint32_t* __restrict__ gset,
+                                                    const uint16_t* __restrict__ srank,
+                                                    const float* __restrict__ rscore, const uint64_t* __restrict__ in,
+                                                    uint64_t* __restrict__ out, EdgeOut* __restrict__ eout, uint64_t n,
+                                                    int vb, int shift, const uint32_t* __restrict__ ghist,
+                                                    uint64_t* __restrict__ desc, uint32_t* __restrict__ ticket,
+                                                    uint64_t epoch, uint32_t* __restrict__ err) {
+  constexpr int NTH = ES_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES_IPT;
+  __shared__ uint64_t s_k[ES_TILE];
+  __shared__ uint32_t s_wc[ES_NW][256];
+  __shared__ uint64_t s_gofs[256];
+  __shared__ uint32_t s_lofs[256];
+  __shared__ uint32_t s_scan[8];
+  __shared__ uint32_t s_tile;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t ntiles = (n + ES_TILE - 1) / ES_TILE;
+  const uint64_t ep = epoch << 48;
+  const uint64_t vmask = (1ull << vb) - 1ull;
+  while (true) {
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+    for (int i = t; i < ES_NW * 256; i += NTH) (&s_wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    if (tile >= ntiles) break;  // uniform: every wave leaves
+    const uint64_t base = tile * ES_TILE;
+    const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - base);
+    uint64_t rk8[ES_IPT];
+    uint32_t rk[ES_IPT], dg[ES_IPT];
+    if (FIRST) {
+      uint32_t ru[ES_IPT], rw[ES_IPT];
+      float rs[ES_IPT];
+#pragma unroll
+      for (int i = 0; i < ES_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+        const bool ok = q < tn;
+        const uint64_t j = base + q;
+        ru[i] = ok ? cu[j] : 0u;
+        rw[i] = ok ? cw[j] : 0u;
+        rs[i] = ok ? cs[j] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < ES_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+        rk8[i] = q < tn ? es_k8(gset, srank, ru[i], rw[i], rs[i], vb) : 0ull;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ES_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+        rk8[i] = q < tn ? in[base + q] : 0ull;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ES_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      const bool ok = q < tn;
+      dg[i] = (uint32_t)(rk8[i] >> shift) & 0xffu;
+      const uint64_t peers = es_peers(dg[i], ok);
+      const uint64_t below = peers & ((1ull << lane) - 1ull);
+      rk[i] = ok ? s_wc[wv][dg[i]] + (uint32_t)__popcll(below) : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      if (ok && below == 0) s_wc[wv][dg[i]] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    }
+    __syncthreads();
+    uint32_t cnt = 0, gh = 0;
+    if (t < 256) {
+#pragma unroll
+      for (int w = 0; w < ES_NW; ++w) {
+        const uint32_t c = s_wc[w][t];
+        s_wc[w][t] = cnt;
+        cnt += c;
+      }
+      gh = ghist[t];
+      es_publish(desc + tile * 256 + t, ep | (tile == 0 ? ES_PFX : ES_AGG) | (uint64_t)cnt);
+    }
+    uint32_t lof = 0, gb = 0;
+    {
+      uint32_t a = cnt, b = gh;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ya = __shfl_up(a, o, 64), yb = __shfl_up(b, o, 64);
+        if (lane >= o) { a += ya; b += yb; }
+      }
+      if (lane == 63 && wv < 4) { s_scan[wv] = a; s_scan[4 + wv] = b; }
+      __syncthreads();
+      uint32_t pa = 0, pb = 0;
+      for (int w = 0; w < wv && w < 4; ++w) { pa += s_scan[w]; pb += s_scan[4 + w]; }
+      lof = pa + a - cnt;
+      gb = pb + b - gh;
+    }
+    if (t < 256) {
+      uint64_t excl = 0;
+      if (tile > 0) {
+        int64_t j = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        bool fin = false;
+        while (!fin) {
+          uint64_t x[ES_LBW];
+#pragma unroll
+          for (int r = 0; r < ES_LBW; ++r)
+            x[r] = j - r >= 0 ? es_load(desc + (uint64_t)(j - r) * 256 + t) : (ep | ES_PFX);
+          int used = 0;
+          bool blocked = false;
+#pragma unroll
+          for (int r = 0; r < ES_LBW; ++r) {
+            if (fin || blocked) continue;
+            const uint64_t st = (x[r] >> 48) == epoch ? (x[r] >> 46) & 3ull : 0ull;
+            if (st == 0) {
+              blocked = true;
+              continue;
+            }
+            excl += x[r] & ES_VAL;
+            ++used;
+            fin = st == 2;
+          }
+          j -= used;
+          if (!fin && used == 0) {
+            if (++spins > ES_SPIN_LIMIT) { atomicOr(err, 1u); break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        es_publish(desc + tile * 256 + t, ep | ES_PFX | (excl + cnt));
+      }
+      s_gofs[t] = (uint64_t)gb + excl;
+      s_lofs[t] = lof;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ES_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      if (q < tn) s_k[s_lofs[dg[i]] + s_wc[wv][dg[i]] + rk[i]] = rk8[i];
+    }
+    __syncthreads();
+    for (uint32_t p = (uint32_t)t; p < tn; p += NTH) {
+      const uint64_t k = s_k[p];
+      const uint32_t d = (uint32_t)(k >> shift) & 0xffu;
+      const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);
+      if (LAST) eout[pos] = EdgeOut{(uint32_t)((k >> vb) & vmask), (uint32_t)(k & vmask), rscore[k >> (2 * vb)]};
+      else out[pos] = k;
+    }
+    __syncthreads();
+  }
+}
+
 // n <= 1 or every digit constant: the candidate columns as records, in place order
 __global__ void k_es_copy(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                           const float* __restrict__ cs, uint64_t n, EdgeOut* __restrict__ out) {

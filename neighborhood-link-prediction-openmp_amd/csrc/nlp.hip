@@ -77,6 +77,7 @@ enum Buf {
   B_HP_TCNT, B_HP_TPRE, B_HP_SDO, B_TSHIST, B_HH_SCAN,
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR, B_HP_SMASK, B_HP_BPOS,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
+  B_ES_SET, B_ES_K0, B_ES_K1,            // edgesort.hpp 8-byte keys: distinct-key set + ranks + scores, key buffers
   NBUF
 };
 
@@ -289,6 +290,9 @@ struct nlp_graph {
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   const void* es_desc_ptr = nullptr;  // and its address (a same-size reallocation restarts them too)
+  unsigned occ_es8 = 256;    // resident workgroups of k_es_pass8
+  int es_k8 = 1;             // the final order over rank-compressed 8-byte keys when it qualifies: 1 from
+                             // ES8_MIN links on, 2 always (tests), 0 never (NLP_ES8)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hp_uxf = HB_XF;   // exclusion by the membership table for slices beyond hp_uxf x W
@@ -892,6 +896,7 @@ nlp_status finish_graph(nlp_graph* g) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
+  if (const char* e8 = getenv("NLP_ES8")) g->es_k8 = std::min(2, std::max(0, atoi(e8)));
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
@@ -926,6 +931,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
+    TRY(occ((const void*)k_es_pass8<false, false>, &g->occ_es8, ES_NT));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1564,7 +1570,7 @@ nlp_status hp_alloc_scratch(nlp_graph* g) {
   size_t fr = 0, tot = 0;
   TRY(hipMemGetInfo(&fr, &tot));
   g->hp_gp = 256;
-  uint64_t scap = g->hp_scap_force ? g->hp_scap_force : (1ull << 21);
+  uint64_t scap = g->hp_scap_force ? g->hp_scap_force : (1ull << 22);  // 8 GB when a sixteenth of HBM is free
   while (scap > 4096 && (uint64_t)g->hp_gp * scap * 8 > fr / 16) scap >>= 1;
   g->hp_scap = scap;
   TRY(hipMalloc(&g->hp_scratch, (uint64_t)g->hp_gp * scap * 8));
@@ -1677,9 +1683,127 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
 // `out` as records: one stable LSD sort of the records by
 // (~score_key, u, w) (edgesort.hpp).  Digits that are the same for every
 // record are skipped (one histogram read decides, read back with one sync).
+// The look-back descriptors of the record passes: cleared when the buffer is
+// new or regrown (size OR address) or the epochs run out, so no stale word can
+// carry a live epoch.
+nlp_status es_descs(nlp_graph* g, uint64_t ntiles, int P, uint64_t** desc, hipStream_t st) {
+  Workspace& ws = g->ws;
+  TRY(wsget(ws, B_ES_DESC, ntiles * 256, desc));
+  if (ws.bytes[B_ES_DESC] != g->es_desc_bytes || (const void*)*desc != g->es_desc_ptr || g->es_epoch + P >= 0xffffull) {
+    TRY(hipMemsetAsync(*desc, 0, ws.bytes[B_ES_DESC], st));
+    g->es_desc_bytes = ws.bytes[B_ES_DESC];
+    g->es_desc_ptr = *desc;
+    g->es_epoch = 0;
+  }
+  return NLP_OK;
+}
+
+// es_sort over rank-compressed 8-byte keys (edgesort.hpp k_es_dkeys, k_es_hist8,
+// k_es_pass8).  *done = false when the call does not qualify (too many distinct
+// score keys, a NaN or zero score, too many key bits): nothing was written.
+nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
+                    hipStream_t st, uint64_t* bytes, bool* done) {
+  *done = false;
+  Workspace& ws = g->ws;
+  const int vb = std::max(1, bits_for(g->span - 1));
+  if (2 * vb > 63) return NLP_OK;
+  // [ES_DCAP] set, [4] counts, then the slot ranks (u16) and the rank scores (f32)
+  uint32_t* dset;
+  const uint64_t words = ES_DCAP + 4 + ES_DCAP / 2 + ES_DMAX;
+  TRY(wsget(ws, B_ES_SET, words, &dset));
+  uint32_t* dcnt = dset + ES_DCAP;
+  uint16_t* srank = (uint16_t*)(dcnt + 4);
+  float* rscore = (float*)(dcnt + 4 + ES_DCAP / 2);
+  TRY(hipMemsetAsync(dset, 0, (ES_DCAP + 4) * 4, st));
+  hipLaunchKernelGGL(k_es_dkeys, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
+                     cs, n, dset, dcnt);
+  TRY(hipGetLastError());
+  std::vector<uint32_t> hs(ES_DCAP + 4);
+  TRY(hipMemcpyAsync(hs.data(), dset, (ES_DCAP + 4) * 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint32_t D = hs[ES_DCAP], over = hs[ES_DCAP + 1];
+  if (over || D == 0 || D > ES_DMAX) return NLP_OK;
+  std::vector<uint32_t> keys;
+  keys.reserve(D);
+  for (uint32_t i = 0; i < ES_DCAP; ++i)
+    if (hs[i]) keys.push_back(hs[i] - 1u);
+  if (keys.size() != D) return NLP_OK;
+  for (uint32_t k : keys)
+    if (k == 0u || k == 0x80000000u) return NLP_OK;  // NaN / zero: several bit patterns behind one key
+  const int rb = D > 1 ? bits_for(D - 1) : 0;
+  if (rb + 2 * vb > 64) return NLP_OK;
+  std::sort(keys.begin(), keys.end(), std::greater<uint32_t>());  // rank 0 = the highest score
+  std::vector<uint16_t> hr(ES_DCAP, 0);
+  std::vector<float> hsc(D);
+  for (uint32_t r = 0; r < D; ++r) {
+    const uint32_t k = keys[r];
+    const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;  // score_key's inverse
+    memcpy(&hsc[r], &b, 4);
+  }
+  for (uint32_t i = 0; i < ES_DCAP; ++i)
+    if (hs[i]) hr[i] = (uint16_t)(std::lower_bound(keys.begin(), keys.end(), hs[i] - 1u, std::greater<uint32_t>()) -
+                                  keys.begin());
+  TRY(hipMemcpyAsync(srank, hr.data(), ES_DCAP * 2, hipMemcpyHostToDevice, st));
+  TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
+  // every digit's histogram, one read; constant digits are passes not run
+  uint32_t* hw;
+  TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
+  uint32_t* tick = hw + ES_MAXP * 256;
+  uint32_t* err = tick + ES_MAXP;
+  TRY(hipMemsetAsync(hw, 0, ((uint64_t)ES_MAXP * 256 + ES_MAXP + 4) * 4, st));
+  hipLaunchKernelGGL(k_es_hist8, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
+                     cu, cw, cs, n, vb, (const uint32_t*)dset, (const uint16_t*)srank, hw);
+  TRY(hipGetLastError());
+  std::vector<uint32_t> h(8 * 256);
+  TRY(hipMemcpyAsync(h.data(), hw, h.size() * 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  int run[8], P = 0;
+  for (int p = 0; p < 8; ++p) {
+    uint32_t mx = 0;
+    for (int d = 0; d < 256; ++d) mx = std::max(mx, h[(size_t)p * 256 + d]);
+    if (mx < n) run[P++] = p;
+  }
+  if (P == 0) run[P++] = 0;  // one record (or every key equal): one pass places it
+  if (bytes) *bytes += 4 * n + 12 * n + (P == 1 ? 24 * n : 20 * n + 16 * n * (uint64_t)(P - 2) + 20 * n);
+  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES_IPT - 1) / ((uint64_t)ES_NT * ES_IPT);
+  uint64_t* desc;
+  { nlp_status s = es_descs(g, ntiles, P, &desc, st); if (s != NLP_OK) return s; }
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  if (P > 1) TRY(wsget(ws, B_ES_K0, n, &k0));
+  if (P > 2) TRY(wsget(ws, B_ES_K1, n, &k1));
+  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es8));
+  const uint64_t* src = nullptr;
+  for (int r = 0; r < P; ++r) {
+    uint64_t* dst = (r & 1) ? k1 : k0;
+    const uint64_t ep = ++g->es_epoch;
+    const uint32_t* gh = hw + run[r] * 256;
+#define NLP_ES8(F, L)                                                                                               \
+  hipLaunchKernelGGL((k_es_pass8<F, L>), dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const uint32_t*)dset,            \
+                     (const uint16_t*)srank, (const float*)rscore, src, dst, out, n, vb, 8 * run[r], gh, desc,        \
+                     tick + r, ep, err)
+    if (P == 1) NLP_ES8(true, true);
+    else if (r == 0) NLP_ES8(true, false);
+    else if (r == P - 1) NLP_ES8(false, true);
+    else NLP_ES8(false, false);
+#undef NLP_ES8
+    TRY(hipGetLastError());
+    src = dst;
+  }
+  uint32_t herr = 0;
+  TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  *done = true;
+  return herr ? NLP_ERR_DEVICE : NLP_OK;  // a look-back gave up (never expected)
+}
+
 nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
                    hipStream_t st, uint64_t* bytes = nullptr) {
   if (n == 0) return NLP_OK;
+  if ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2) {
+    bool done = false;
+    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done);
+    if (s != NLP_OK || done) return s;
+  }
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
   const int npass = (32 + 2 * vb + 7) / 8;
@@ -1709,15 +1833,8 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
   const uint64_t ntiles = (n + (uint64_t)ES_NT * ES_IPT - 1) / ((uint64_t)ES_NT * ES_IPT);
   uint64_t* desc;
   EdgeOut* tmp = nullptr;
-  TRY(wsget(ws, B_ES_DESC, ntiles * 256, &desc));
+  { nlp_status s = es_descs(g, ntiles, P, &desc, st); if (s != NLP_OK) return s; }
   if (P > 1) TRY(wsget(ws, B_ES_TMP, n, &tmp));
-  // a new or regrown descriptor buffer (size OR address) starts clear: no stale word can carry a live epoch
-  if (ws.bytes[B_ES_DESC] != g->es_desc_bytes || (const void*)desc != g->es_desc_ptr || g->es_epoch + P >= 0xffffull) {
-    TRY(hipMemsetAsync(desc, 0, ws.bytes[B_ES_DESC], st));
-    g->es_desc_bytes = ws.bytes[B_ES_DESC];
-    g->es_desc_ptr = desc;
-    g->es_epoch = 0;
-  }
   const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es));
   const EdgeOut* src = nullptr;
   for (int r = 0; r < P; ++r) {
@@ -2192,7 +2309,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
   bool full = false;  // k candidates held: tau is in force
   bool retry = false; // the chunk is a retry after an emission overflow
-  uint64_t target = E;
+  // the hub pass's scratch in wedges (run_hub: w, and v for AA / RA)
+  const uint64_t hub_cap = std::max<uint64_t>(1, ((uint64_t)g->hp_gp * g->hp_scap * 2) / (custom ? 2 : 1));
+  uint64_t target = std::min<uint64_t>(E, hub_cap);
   // Prune the held candidates: with at least k real ones (padding excluded) to
   // the canonical top k, and tau = the k-th key from then on; with fewer, only
   // the padding goes (it ranks below every real candidate: key 0, u and w
@@ -2449,11 +2568,16 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       nlp_status s = prune_held();
       if (s != NLP_OK) return s;
     }
-    // next chunk: aim at half of the free buffer at the last emission rate
+    // next chunk: aim at half of the free buffer at the last emission rate, and
+    // at most the hub pass's scratch in wedges: a chunk beyond it would run its
+    // hub rows through k_hp_part (with a threshold in force the emission rate
+    // is tiny and the emission bound alone grew IHub chunks to 3e11 wedges:
+    // the C5 shard 0 ran at 5.8e9 instead of 2.4e10 wedges/s)
     const uint64_t free_slots = capC - C.n;
     const double want = 0.5 * (double)free_slots / std::max(rate, 1e-9);
     target = (uint64_t)std::min(want, 1e18);
     if (!full && target > free_slots) target = free_slots;  // no threshold yet: emissions <= W(u)
+    target = std::min<uint64_t>(target, hub_cap);
     if (target == 0) target = 1;
   }
   // held candidates are unordered: the caller orders them (hp_final_order)
@@ -4805,6 +4929,20 @@ nlp_status nlp_copy_last(nlp_graph* g, nlp_edge* out, uint64_t n, uint64_t* copi
   TRY(hipStreamSynchronize(g->last_stream));
   *copied = m;
   return NLP_OK;
+}
+
+nlp_status nlp_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return NLP_ERR_INVALID;
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return NLP_ERR_NOMEM;
+  }
+  return NLP_OK;
+}
+
+void nlp_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 nlp_status nlp_set_truth(nlp_graph* g, const uint32_t* u, const uint32_t* v, uint64_t n) {

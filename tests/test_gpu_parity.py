@@ -439,7 +439,9 @@ class _env:
 # marks, 34 the one-pass survivor build, 35 the count metrics' survivor lists
 # compacted per call (k_dc_*) instead of taken as prefixes of the per-graph
 # class-ordered short lists (variants 22, 23, 34 also compact per call), 36
-# short lists of the classes up to 3 only (H = 2 from them, H = 4, 16 compacted)
+# short lists of the classes up to 3 only (H = 2 from them, H = 4, 16 compacted),
+# 37 / 38 the final order over rank-compressed 8-byte keys on every call
+# (k_es_pass8; by default only from ES8_MIN links on)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
@@ -461,7 +463,8 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"),
                  dict(NLP_HASH_UX="0"), dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"),
                  dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off"),
-                 dict(NLP_HASH_ONE="1", NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3")]
+                 dict(NLP_HASH_ONE="1", NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3"),
+                 dict(NLP_ES8="2"), dict(NLP_ES8="2", NLP_HASH_MINBIN="2")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
