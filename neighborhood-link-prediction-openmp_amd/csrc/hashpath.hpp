@@ -1124,11 +1124,10 @@ __global__ __launch_bounds__(NT) void k_hp_dcls_fill8(GraphView g, const uint8_t
 }
 
 // ---------------------------------------------------------------- survivor lists in three streaming kernels
-// k_hp_dcls_one runs the whole chain of a tile -- classes, look-back, then per
-// survivor its key and off[v] -- with three workgroups per CU (163 VGPRs): a
-// tile waits on five dependent round trips and a lane holds about one survivor
-// per tile (C4 H=16: 4.6e7 survivors among 3.5e9 entries, 7.2 ms).  Here the
-// chain is cut where the parallelism changes:
+// A one-pass build (classes, look-back, then per survivor its key and off[v],
+// three workgroups per CU at 163 VGPRs) waited on five dependent round trips
+// per tile (C4 H=16: 4.6e7 survivors among 3.5e9 entries, 7.2 ms; removed in
+// round 5).  Here the chain is cut where the parallelism changes:
 //   k_dc_count   a wave per 512-entry wave tile: its survivors counted (one
 //                8-byte class word per lane); the counts are scanned;
 //   k_dc_place   the same tiles again: each survivor's entry e and row r
@@ -1380,214 +1379,6 @@ __global__ void k_sl_rows(const uint64_t* __restrict__ lo, const uint8_t* __rest
     }
     cnt[r] = (uint32_t)(a - s);
     wu[r] = a > s ? pn[a - 1] : 0u;
-  }
-}
-
-// ---------------------------------------------------------------- survivor lists in one pass
-// k_hp_dcls_rows8 + scan + k_hp_dcls_fill8 read the range's degree classes
-// twice (C4 H=16: 3.3 + 8.5 ms) and walk each lane's eight entries with a
-// dependent gather chain per entry.  Here one pass does both: tiles of
-// HD_TILE entries (every wave takes HD_SUB consecutive 512-entry wave tiles,
-// one 8-byte class word per lane each, kept in registers); the tile's output
-// offset comes from decoupled look-back on one u64 descriptor per tile
-// (ordered tile tickets; wave 0 reads 64 predecessors per round trip); the
-// loads that only depend on the tile (its rows' ends, the rank words of words
-// holding a survivor) are issued together before the look-back; then each lane
-// takes its survivors HD_R at a time -- row from the LDS row ends, key, rank,
-// then off[v] -- so a wave pays two dependent round trips per round instead
-// of two per entry.  Survivors are written in entry order (S(u) stays sorted)
-// with their packed entries; per row (count << 40 | W+) goes through LDS
-// accumulators of the wave tile's first 64 rows (global atomics beyond them),
-// unpacked and scanned into soff afterwards (the lists are the entry-order
-// compaction, so the rows' counts give their starts).  Output capacity `cap`
-// (from the degree histogram); more survivors raise err bit 1 (the caller
-// falls back to the two-kernel build).
-constexpr int HD_SUB = 8;                                          // wave tiles per wave per tile
-constexpr uint64_t HD_TILE = (uint64_t)NWAVE * HD_SUB * HP_WTILE;  // 16384 entries
-constexpr uint64_t HD_AGG = 1ull << 62, HD_PFX = 2ull << 62, HD_VAL = HD_AGG - 1;
-constexpr int HD_R = 4;                                            // survivors per lane per round
-
-__global__ __launch_bounds__(NT) void k_hp_dcls_one(GraphView g, const uint8_t* __restrict__ dcls, uint32_t H,
-                                                    uint64_t ua, uint64_t nU, uint64_t e0, uint64_t e1,
-                                                    const uint32_t* __restrict__ tile_row, uint32_t* __restrict__ skeys,
-                                                    uint64_t* __restrict__ sdo, uint64_t cap,
-                                                    unsigned long long* __restrict__ wu,
-                                                    const uint8_t* __restrict__ drank, uint64_t* __restrict__ desc,
-                                                    uint32_t* __restrict__ ticket, uint32_t* __restrict__ err) {
-  __shared__ unsigned long long s_acc[NWAVE][HD_SUB][64];
-  __shared__ uint64_t s_end[NWAVE][HD_SUB][64];
-  __shared__ uint32_t s_wt[NWAVE][HD_SUB];
-  __shared__ uint64_t s_base;
-  __shared__ uint32_t s_tile;
-  const int lane = lane_id(), wv = wave_id();
-  const uint64_t T0 = e0 / HD_TILE, ntiles = (e1 + HD_TILE - 1) / HD_TILE - T0;
-  for (int sb = 0; sb < HD_SUB; ++sb) s_acc[wv][sb][lane] = 0;
-  while (true) {
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint64_t ti = s_tile;
-    if (ti >= ntiles) break;
-    const uint64_t wt0 = (T0 + ti) * (NWAVE * HD_SUB) + (uint64_t)wv * HD_SUB;  // this wave's first wave tile
-    // the rows of the wave tiles (lane sb < HD_SUB loads one) and the class words
-    const uint32_t trl = lane < HD_SUB && (wt0 + lane) * HP_WTILE < e1 ? tile_row[wt0 + lane] : 0u;
-    uint64_t word[HD_SUB], rkw[HD_SUB];
-    uint32_t mine[HD_SUB], excl[HD_SUB];
-    uint64_t smask = 0;  // survivor bits of this lane: bit 8 sb + q
-#pragma unroll
-    for (int sb = 0; sb < HD_SUB; ++sb) {
-      const uint64_t eb = (wt0 + sb) * HP_WTILE + (uint64_t)lane * 8;
-      uint64_t w = 0;
-      if (eb >= e0 && eb + 8 <= e1) w = *(const uint64_t*)(dcls + eb);
-      else
-        for (int q = 0; q < 8; ++q)
-          if (eb + q >= e0 && eb + q < e1) w |= (uint64_t)dcls[eb + q] << (8 * q);
-      word[sb] = w;
-    }
-#pragma unroll
-    for (int sb = 0; sb < HD_SUB; ++sb) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const bool sv = hp_dsurv((uint32_t)(word[sb] >> (8 * q)) & 0xffu, H);  // out of range: class 0
-        c += sv ? 1u : 0u;
-        smask |= sv ? 1ull << (8 * sb + q) : 0ull;
-      }
-      mine[sb] = c;
-      const uint64_t inc = wave_incl_scan((uint64_t)c);
-      excl[sb] = (uint32_t)inc - c;
-      if (lane == 63) s_wt[wv][sb] = (uint32_t)inc;
-      // rank bytes only for words holding a survivor
-      const uint64_t eb = (wt0 + sb) * HP_WTILE + (uint64_t)lane * 8;
-      uint64_t r = 0;
-      if (c) {
-        if (eb >= e0 && eb + 8 <= e1) r = *(const uint64_t*)(drank + eb);
-        else
-          for (int q = 0; q < 8; ++q)
-            if (eb + q >= e0 && eb + q < e1) r |= (uint64_t)drank[eb + q] << (8 * q);
-      }
-      rkw[sb] = r;
-    }
-    // row ends of every wave tile's first 64 rows
-#pragma unroll
-    for (int sb = 0; sb < HD_SUB; ++sb) {
-      const uint64_t tr = __shfl(trl, sb, 64);
-      const uint64_t rl = (tr > ua ? tr - ua : 0) + lane;
-      s_end[wv][sb][lane] = rl < nU ? g.off[ua + rl + 1] : ~0ull;
-    }
-    __syncthreads();
-    // the tile's offset: wave 0 publishes the count and looks back, 64 predecessors a round
-    if (wv == 0) {
-      uint64_t cnt = 0;
-      for (int i = 0; i < NWAVE * HD_SUB; ++i) cnt += (&s_wt[0][0])[i];
-      uint64_t ex = 0;
-      if (ti == 0) {
-        if (lane == 0) __hip_atomic_store(&desc[ti], HD_PFX | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        if (lane == 0) __hip_atomic_store(&desc[ti], HD_AGG | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int64_t j = (int64_t)ti - 1;
-        uint32_t spins = 0;
-        while (true) {
-          const uint64_t x = j - lane >= 0
-                                 ? __hip_atomic_load(&desc[j - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                 : HD_PFX;  // before tile 0: a zero prefix
-          const uint64_t st = x >> 62;
-          const uint64_t stop = __ballot(st != 1);  // the nearest lane that is not a plain count
-          const int k = stop ? __builtin_ctzll(stop) : 64;
-          const bool pfx = k < 64 && __shfl(st, k, 64) == 2;
-          const uint64_t take = lane < k || (pfx && lane == k) ? (x & HD_VAL) : 0ull;
-          ex += wave_sum(take);
-          if (pfx) break;
-          j -= k;
-          if (k == 0) {
-            if (++spins > (1u << 26)) {
-              if (lane == 0) atomicOr(err, 2u);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        if (lane == 0) __hip_atomic_store(&desc[ti], HD_PFX | (ex + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane == 0) s_base = ex;
-    }
-    __syncthreads();
-    // positions: the tile base + the wave tiles before + the lane's prefix in its wave tile
-    uint64_t spre[HD_SUB];
-    {
-      uint64_t run = s_base;
-      for (int i = 0; i < wv * HD_SUB; ++i) run += (&s_wt[0][0])[i];
-#pragma unroll
-      for (int sb = 0; sb < HD_SUB; ++sb) {
-        spre[sb] = run + excl[sb];
-        run += s_wt[wv][sb];
-      }
-    }
-    // the lane's survivors, HD_R per round: row (LDS), key and rank, then off[v]
-    while (__ballot(smask != 0)) {
-      uint32_t v[HD_R], n[HD_R], c[HD_R], sbq[HD_R], idx[HD_R];
-      uint64_t e[HD_R], pos[HD_R];
-      bool ok[HD_R];
-#pragma unroll
-      for (int i = 0; i < HD_R; ++i) {
-        ok[i] = smask != 0;
-        const int bit = ok[i] ? __builtin_ctzll(smask) : 0;
-        smask &= ok[i] ? smask - 1 : ~0ull;
-        const int sb = bit >> 3, q = bit & 7;
-        sbq[i] = (uint32_t)sb;
-        uint64_t wsb = 0, rsb = 0, psb = 0;
-#pragma unroll
-        for (int z = 0; z < HD_SUB; ++z)
-          if (z == sb) { wsb = word[z]; rsb = rkw[z]; psb = spre[z]; }
-        c[i] = (uint32_t)(wsb >> (8 * q)) & 0xffu;
-        n[i] = c[i] - ((uint32_t)(rsb >> (8 * q)) & 0xffu);
-        // rank among the lane's survivors of this word: the survivor classes below q
-        uint32_t below = 0;
-#pragma unroll
-        for (int z = 0; z < 8; ++z) below += (z < q && hp_dsurv((uint32_t)(wsb >> (8 * z)) & 0xffu, H)) ? 1u : 0u;
-        pos[i] = psb + below;
-        e[i] = (wt0 + sb) * HP_WTILE + (uint64_t)lane * 8 + q;
-        int x = 0;  // local row: the number of row ends <= e among the wave tile's first 64 rows (64: beyond them)
-#pragma unroll
-        for (uint32_t bb = 32; bb > 0; bb >>= 1) x += s_end[wv][sb][x + bb - 1] <= e[i] ? (int)bb : 0;
-        if (s_end[wv][sb][63] <= e[i]) x = 64;
-        idx[i] = (uint32_t)x;
-        v[i] = ok[i] ? g.keys[e[i]] : 0u;
-      }
-#pragma unroll
-      for (int i = 0; i < HD_R; ++i) {
-        if (!ok[i]) continue;
-        const uint64_t o = g.off[v[i]];
-        const uint32_t l = c[i] - n[i];
-        if (pos[i] < cap) {
-          skeys[pos[i]] = v[i];
-          sdo[pos[i]] = (uint64_t)c[i] << 48 | (uint64_t)n[i] << HP_SDO_SH | (o + l);
-        } else {
-          atomicOr(err, 1u);
-        }
-        const unsigned long long add = (1ull << 40) | n[i];
-        if (idx[i] < 64) {
-          atomicAdd(&s_acc[wv][sbq[i]][idx[i]], add);
-        } else {  // more than 64 rows in this wave tile: search the offsets
-          uint64_t a0 = 0, b0 = nU;
-          while (b0 - a0 > 1) {
-            const uint64_t md = (a0 + b0) >> 1;
-            if (g.off[ua + md] <= e[i]) a0 = md; else b0 = md;
-          }
-          atomicAdd(&wu[a0], add);
-        }
-      }
-    }
-    wave_sync_lds();
-#pragma unroll
-    for (int sb = 0; sb < HD_SUB; ++sb) {
-      const uint64_t tr = __shfl(trl, sb, 64);
-      const unsigned long long x = s_acc[wv][sb][lane];
-      if (x) {
-        atomicAdd(&wu[(tr > ua ? tr - ua : 0) + lane], x);
-        s_acc[wv][sb][lane] = 0;
-      }
-    }
-    wave_sync_lds();
   }
 }
 

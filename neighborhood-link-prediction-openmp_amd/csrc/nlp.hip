@@ -282,9 +282,8 @@ struct nlp_graph {
   bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
                              // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
   bool hp_win = true;        // k_hp_batch reserves emission windows (NLP_HASH_WIN=0: one reservation per flush)
-  int hp_one = 2;            // survivor lists: 2 three streaming kernels (k_dc_*), 1 one pass (k_hp_dcls_one),
-                             // 0 count + fill kernels (NLP_HASH_ONE)
-  uint64_t hp_one_cap = 0;   // test hook (NLP_HASH_ONE_CAP): cap of the one-pass output
+  // survivor lists: three streaming kernels (k_dc_*; a one-pass build with a decoupled look-back measured
+  // slower, 7.2 vs 5.9 ms on C4 H=16, and was removed in round 5)
   unsigned occ_es = 256;     // resident k_es_pass workgroups
   unsigned occ_hb = 512;     // resident k_hp_batch workgroups (count-metric build)
   uint64_t es_epoch = 0;     // look-back descriptor epoch of the last edgesort pass
@@ -300,7 +299,6 @@ struct nlp_graph {
   int hp_rowb = 1;           // bin 1, count metrics: tiered 256-thread rows (NLP_HASH_ROWB=0: k_hp_block;
                              // 2: every row in the 8192-entry tier, 3: none in the 2048-entry tier -- tests)
   uint32_t hh_dw = HH_DW;    // hub pass, counts: direct-counter range width (NLP_HH_DIRECT=0 off, small values test it)
-  bool hh_stats = false;     // NLP_HH_STATS=1: per chunk, the hub items' scratch reads on stderr (debug)
   uint32_t hh_scap = HH_SCAP;  // sort-mode wedges per item (NLP_HASH_HUB_SCAP: small values test the splits and HH_BIG)
   uint64_t hh_bw = HH_BW;   // hub pass: W(u) per w-bucket (NLP_HASH_HUB_BW; large values test the sub-range passes)
   int hp_hub_min = 2;        // lowest bin the hub pass takes (NLP_HASH_HUB_MIN=1: bin 1 too)
@@ -308,7 +306,6 @@ struct nlp_graph {
   bool hp_batch = true;      // path 4: bin-0 tiers 0 / 1 in row batches (k_hp_batch; NLP_HASH_BATCH=0: a wave per row)
   // (u64, u32) sorts of paths 2 / 4 by onesweep passes (NLP_OS_SORT=1); the default hist / scan / scatter
   // passes measured faster at these sizes (C4 JAC H=16 ordering: 22 vs 77 ms; C3 AA H=16 path 2: 122 vs 418 ms)
-  bool hp_stats = false;     // NLP_HASH_STATS=1: per-bin rows / W(u) histogram to stderr (diagnostic)
   bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   bool hp_dcls = true;       // survivor lists by filtering N(u) with the degree classes (NLP_HASH_DCLS=0: in-edge atomics)
   uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
@@ -339,9 +336,9 @@ nlp_status from_hip(hipError_t e) {
   return NLP_ERR_DEVICE;
 }
 
-// NLP_DEBUG=1 reports the failing runtime call on stderr
+// debug_on() (build-time) reports the failing runtime call on stderr
 inline bool debug_on() {
-  static const bool on = getenv("NLP_DEBUG") != nullptr;
+  constexpr bool on = false;  // a build-time switch: the failing runtime call on stderr
   return on;
 }
 #define TRY(x)                                                                                     \
@@ -844,20 +841,12 @@ nlp_status finish_graph(nlp_graph* g) {
     unsigned long long v = strtoull(ev, nullptr, 10);
     if (v > 0) g->wedge_budget = v;
   }
-  if (const char* hs = getenv("NLP_HOT_STAGE")) g->hot_stage = atoi(hs);
   if (const char* de = getenv("NLP_DIRECT")) g->direct_emit = de[0] != '0';
-  if (const char* fr = getenv("NLP_FUSE_RUNS")) g->fuse_runs = fr[0] != '0';
   if (const char* dl = getenv("NLP_DIRECT_LAUNCH")) {
     g->direct_launch = dl[0] == '1';
     g->sync_direct = dl[0] != '0';
     if (g->direct_launch) g->use_graphs = false;
   }
-  if (const char* ag = getenv("NLP_ASYNC_GRAPH")) {
-    g->async_direct = ag[0] != '1';
-  }
-  if (const char* gt = getenv("NLP_GR_NT")) g->gr_nt = atoi(gt) == 512 ? 512 : GR_NT;
-  if (const char* es = getenv("NLP_EXB_SPT")) g->exb_spt = std::max(1, std::min(4, atoi(es)));
-  if (const char* o11 = getenv("NLP_ORD11")) g->ord11 = o11[0] == '1';
   if (const char* cp = getenv("NLP_COUNTED")) {  // 0: off, 2: whatever the estimate (tests the F_CPASS redo)
     g->counted = cp[0] != '0';
     g->counted_force = cp[0] == '2';
@@ -866,49 +855,33 @@ nlp_status finish_graph(nlp_graph* g) {
     g->small_order = so[0] != '0';
     g->small_force = so[0] == '2';
   }
-  if (const char* dt = getenv("NLP_DX_TARGET")) g->dx_target = std::max(1.0, atof(dt));
   if (const char* dbs = getenv("NLP_DX_BITS")) g->dx_bits = std::max(0, atoi(dbs));
-  if (const char* fg = getenv("NLP_FUSE_GATHER")) g->fuse_gather = fg[0] == '1';
-  if (const char* xi = getenv("NLP_EX_IPT")) g->ex_ipt = atoi(xi) >= 4 ? 4 : (atoi(xi) >= 2 ? 2 : 1);
-  if (const char* gs = getenv("NLP_GRAPH_SEGMENTS")) g->graph_single = gs[0] != '1';
   if (const char* sp = getenv("NLP_STAMP")) {
     g->stamp_path = sp;
     TRY(hipMalloc(&g->d_stamp, 8 * 65536 * 8));
     TRY(hipMemset(g->d_stamp, 0, 8 * 65536 * 8));
   }
   if (const char* nd = getenv("NLP_NO_DINDEX")) g->use_dindex = nd[0] != '1';
-  if (const char* nr = getenv("NLP_NO_RINDEX")) g->use_rindex = nr[0] != '1';
   if (const char* hm = getenv("NLP_HASH")) g->hash_mode = hm[0] == '1' ? 1 : (hm[0] == '0' ? -1 : 0);
   if (const char* hw = getenv("NLP_HASH_MIN_WEDGES")) g->hp_min_wedges = strtoull(hw, nullptr, 10);
   if (const char* he = getenv("NLP_HASH_EMIT")) g->hp_emit = strtoull(he, nullptr, 10);
   if (const char* hb = getenv("NLP_HASH_MINBIN")) g->hp_minbin = std::min(3, std::max(0, atoi(hb)));
   if (const char* hc = getenv("NLP_HASH_SCAP")) g->hp_scap_force = std::max<uint64_t>(64, strtoull(hc, nullptr, 10));
-  if (const char* h1 = getenv("NLP_HASH_ONE_BUCKET")) g->hp_one_bucket = h1[0] == '1';
-  if (const char* ht = getenv("NLP_HASH_TIERS")) g->hp_tiers = ht[0] != '0';
-  if (const char* hw = getenv("NLP_HASH_WORK_SURV")) g->hp_work_surv = hw[0] != '0';
   if (const char* hd = getenv("NLP_HASH_DCLS")) g->hp_dcls = hd[0] != '0';
-  if (const char* hq = getenv("NLP_HASH_STATS")) g->hp_stats = hq[0] == '1';
   if (const char* hb = getenv("NLP_HASH_BATCH")) g->hp_batch = hb[0] != '0';
   if (const char* hh = getenv("NLP_HASH_HUB")) g->hp_hub = hh[0] != '0';
   if (const char* hm = getenv("NLP_HASH_HUB_MIN")) g->hp_hub_min = std::max(1, std::min(2, atoi(hm)));
   if (const char* hw = getenv("NLP_HASH_HUB_BW")) g->hh_bw = std::max<uint64_t>(64, strtoull(hw, nullptr, 10));
   if (const char* ht = getenv("NLP_HASH_HUB_TL")) g->hh_tl = std::max(7, std::min(HH_TL, atoi(ht)));
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
-  if (const char* hs = getenv("NLP_HH_STATS")) g->hh_stats = hs[0] == '1';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* e8 = getenv("NLP_ES8")) g->es_k8 = std::min(2, std::max(0, atoi(e8)));
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
-  if (const char* ho = getenv("NLP_HASH_ONE")) g->hp_one = atoi(ho);
-  if (const char* hw = getenv("NLP_HASH_WIN")) g->hp_win = hw[0] != '0';
-  if (const char* hc = getenv("NLP_HASH_ONE_CAP")) g->hp_one_cap = strtoull(hc, nullptr, 10);
-  if (const char* hs = getenv("NLP_HASH_SDO")) g->hp_sdo = hs[0] != '0';
   if (const char* hc = getenv("NLP_HASH_HUB_SCAP"))
     g->hh_scap = (uint32_t)std::max<long>(16, std::min<long>(HH_SCAP, atol(hc)));
-  if (const char* hs = getenv("NLP_HASH_SLICES")) g->hp_slices = (uint32_t)std::min(4096, std::max(0, atoi(hs)));
   if (const char* bf = getenv("NLP_BUCKET_FUSED")) g->split_bucket = bf[0] != '1';
-  if (const char* gs = getenv("NLP_GROUP_SORT")) g->group_sort = atoi(gs);
   if (const char* mp = getenv("NLP_MSD_PASSES")) g->msd_force = std::min(2, std::max(0, atoi(mp)));
   if (const char* gr = getenv("NLP_GROUPING")) {
     g->sort_grouping = strcmp(gr, "bucket") != 0;
@@ -972,7 +945,6 @@ nlp_status new_graph(int device, nlp_graph** out) {
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
-  if (const char* em = getenv("NLP_END_MODE")) g->end_mode = std::min(2, std::max(0, atoi(em)));
   *out = g;
   return NLP_OK;
 }
@@ -2010,34 +1982,6 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   else NLP_HH_ACCUM(false, 11);
 #undef NLP_HH_ACCUM
   TRY(hipGetLastError());
-  if (g->hh_stats) {  // debug: how often the accumulation items stream their buckets
-    TRY(hipStreamSynchronize(st));
-    uint32_t ni = 0;
-    unsigned long long hc = 0;
-    TRY(hipMemcpy(&ni, nitems, 4, hipMemcpyDeviceToHost));
-    TRY(hipMemcpy(&hc, hctr, 8, hipMemcpyDeviceToHost));
-    ni = (uint32_t)std::min<uint64_t>(ni, cap);
-    std::vector<HhItem> it(ni);
-    std::vector<uint32_t> bn(NB);
-    TRY(hipMemcpy(it.data(), items, ni * sizeof(HhItem), hipMemcpyDeviceToHost));
-    TRY(hipMemcpy(bn.data(), bcnt, NB * 4, hipMemcpyDeviceToHost));
-    uint64_t rd = 0, big = 0, wide = 0, mx = 0, sortw = 0, direct = 0;
-    for (const HhItem& x : it) {
-      const uint64_t xn = x.n;
-      rd += xn;
-      direct += (x.cnt & HH_DIRECT) != 0;
-      mx = std::max<uint64_t>(mx, xn);
-      big += (x.cnt & HH_BIG) != 0;
-      wide += (x.cnt & HH_WIDE) != 0;
-      if (!(x.cnt & HH_BIG) && wcap) sortw += xn;
-    }
-    fprintf(stderr, "[hh] rows %llu buckets %llu wedges %llu heavy %llu segs %llu items %u (big %llu wide %llu) "
-            "scratch reads %llu (x%.2f) max bucket %llu sort-mode reads %llu direct items %llu\n",
-            (unsigned long long)nh, (unsigned long long)NB, (unsigned long long)tot, hc >> HH_HSH,
-            hc & ((1ull << HH_HSH) - 1), ni, (unsigned long long)big, (unsigned long long)wide,
-            (unsigned long long)rd, tot ? (double)rd / tot : 0.0, (unsigned long long)mx, (unsigned long long)sortw,
-            (unsigned long long)direct);
-  }
   *done = true;
   return NLP_OK;
 }
@@ -2096,7 +2040,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       one_done = true;
     }
     if (one_done) {
-    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 2 && g->hp_sdo && g->drank && p.H >= 1 &&
+    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_sdo && g->drank && p.H >= 1 &&
         p.H <= HP_DCLS_MAX && e1 > e0 && g->nnz < (1ull << HP_SDO_SH)) {
       // count, place, gather (hashpath.hpp k_dc_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
@@ -2134,44 +2078,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
       s_sorted = true;
       one_done = true;
-    }
-    if (one_done) {
-    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_one == 1 && g->hp_sdo && g->drank && p.H >= 1 &&
-        p.H <= HP_DCLS_MAX && e1 > e0 && p_h != ~0ull && g->nnz < (1ull << HP_SDO_SH)) {
-      // one pass over the range's classes (hashpath.hpp k_hp_dcls_one); output sized by the
-      // degree histogram's P_H (an asymmetric graph's in-degrees may exceed it: overflow -> two passes)
-      uint64_t cap = std::min<uint64_t>(e1 - e0, p_h + p_h / 8 + 4096);
-      if (g->hp_one_cap) cap = std::min<uint64_t>(cap, g->hp_one_cap);  // test hook: force the overflow fallback
-      const uint64_t ntl = (e1 + HD_TILE - 1) / HD_TILE - e0 / HD_TILE;
-      uint32_t* scnt;
-      uint64_t* hd;  // [0] ticket + error, [1, 1 + ntl) descriptors
-      TRY(wsget(ws, B_HP_SCNT, nU, &scnt));
-      TRY(wsget(ws, B_HP_SOFF, nU + 1, &s_soff));
-      TRY(wsget(ws, B_HP_SKEYS, cap, &s_skeys));
-      TRY(wsget(ws, B_HP_SDO, cap, &s_sdo));
-      TRY(wsget(ws, B_HP_TPRE, ntl + 1, &hd));
-      TRY(hipMemsetAsync(hd, 0, (ntl + 1) * 8, st));
-      const unsigned gt = (unsigned)std::min<uint64_t>(ntl, 2048);
-      hipLaunchKernelGGL(k_hp_dcls_one, dim3(gt), dim3(NT), 0, st, gv, (const uint8_t*)g->dcls, p.H, ua, nU, e0, e1,
-                         (const uint32_t*)g->tile_row, s_skeys, s_sdo, cap, (unsigned long long*)wu,
-                         (const uint8_t*)g->drank, hd + 1, (uint32_t*)hd, (uint32_t*)hd + 1);
-      TRY(hipGetLastError());
-      LAUNCH(k_hp_unpack, nU, st, (unsigned long long*)wu, scnt, nU);
-      TRY(hipGetLastError());
-      TRY(scan_ws<uint32_t>(ws, B_SCAN, scnt, nU, s_soff, s_soff + nU, st));
-      TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
-      TRY(hipMemcpyAsync(&g->host_small[11], hd, 8, hipMemcpyDeviceToHost, st));
-      TRY(hipStreamSynchronize(st));
-      const uint32_t herr = (uint32_t)(g->host_small[11] >> 32);
-      if (herr & 2u) return NLP_ERR_DEVICE;  // a look-back gave up (never expected)
-      if (herr & 1u) {                      // more survivors than the histogram bound: the two-kernel build
-        TRY(hipMemsetAsync(wu, 0, nU * 8, st));
-        s_skeys = nullptr;
-        s_sdo = nullptr;
-      } else {
-        s_sorted = true;
-        one_done = true;
-      }
     }
     if (one_done) {
     } else if (g->dcls && g->hp_dcls && g->hp_work_surv && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
@@ -2263,33 +2169,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
                        lists[2], lists[3], small + 24);
     TRY(hipGetLastError());
   }
-  if (g->hp_stats) {  // diagnostic: rows and wedge bounds per bin, W(u) by power of two
-    std::vector<uint64_t> hw(nU), nl(HP_NBINS);
-    TRY(hipMemcpyAsync(hw.data(), wu, nU * 8, hipMemcpyDeviceToHost, st));
-    TRY(hipMemcpyAsync(nl.data(), small + 24, HP_NBINS * 8, hipMemcpyDeviceToHost, st));
-    TRY(hipStreamSynchronize(st));
-    uint64_t rows[HP_NBINS] = {}, wsum[HP_NBINS] = {}, lr[40] = {}, lw[40] = {};
-    for (int b = 0; b < HP_NBINS; ++b) {
-      std::vector<uint32_t> hl(nl[b]);
-      TRY(hipMemcpy(hl.data(), lists[b], nl[b] * 4, hipMemcpyDeviceToHost));
-      for (uint32_t u : hl) {
-        const uint64_t w = hw[u - ua];
-        ++rows[b];
-        wsum[b] += w;
-        int l = 0;
-        while ((1ull << l) < w && l < 39) ++l;
-        ++lr[l];
-        lw[l] += w;
-      }
-    }
-    for (int b = 0; b < HP_NBINS; ++b)
-      fprintf(stderr, "[hash-stats] bin %d: rows %llu, W %llu\n", b, (unsigned long long)rows[b],
-              (unsigned long long)wsum[b]);
-    for (int l = 0; l < 40; ++l)
-      if (lr[l])
-        fprintf(stderr, "[hash-stats] W <= 2^%d: rows %llu, W %llu\n", l, (unsigned long long)lr[l],
-                (unsigned long long)lw[l]);
-  }
   // row prefix of W(u) (wu[nU] = total)
   TRY(scan_ws<uint64_t>(ws, B_SCAN, wu, nU, pos, small + 16, st));
   TRY(hipMemcpyAsync(pos + nU, small + 16, 8, hipMemcpyDeviceToDevice, st));
@@ -2377,8 +2256,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.xs = g->xs;
     a.win = 0;
     a.uxf = g->hp_uxf;
-    a.ph = g->hp_stats ? (unsigned long long*)(small + 56) : nullptr;  // small[56, 60): k_hp_batch phase ticks
-    if (g->hp_stats) TRY(hipMemsetAsync(small + 56, 0, 32, st));
+    a.ph = nullptr;  // k_hp_batch phase ticks (a diagnostic hook: small[56, 60) when set)
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0 && g->hp_tiers) {
@@ -2524,18 +2402,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       C.hot_bytes += g->host_small[HPC_HOTB];
       ++C.hot_launches;
     }
-    if (g->hp_stats && batch_timed) {
-      uint64_t ph[4];
-      TRY(hipMemcpy(ph, small + 56, 32, hipMemcpyDeviceToHost));
-      const double tot = (double)(ph[0] + ph[1] + ph[2] + ph[3]) + 1e-9;
-      fprintf(stderr, "[hash-stats] k_hp_batch wave time: setup %.1f%% wedges %.1f%% exclusion %.1f%% drain %.1f%% "
-              "(%.3g wave-s)\n", 100 * ph[0] / tot, 100 * ph[1] / tot, 100 * ph[2] / tot, 100 * ph[3] / tot, tot * 1e-8);
-    }
-    if (g->hp_stats)
-      fprintf(stderr, "[hash-stats] chunk rows [%llu, %llu) bins %llu %llu %llu %llu W %llu emitted %llu cand %llu tau %lld\n",
-              (unsigned long long)r0, (unsigned long long)r1, (unsigned long long)n0, (unsigned long long)n1,
-              (unsigned long long)(q1[2] - q0[2]), (unsigned long long)(q1[3] - q0[3]), (unsigned long long)wchunk,
-              (unsigned long long)emitted, (unsigned long long)g->host_small[HPC_CAND], (long long)tau);
     if (g->host_small[HPC_ERR]) return NLP_ERR_DEVICE;
     if (emitted > a.cap) {
       // overflow: nothing of this chunk is kept; prune what is held and retry a smaller chunk
@@ -3467,7 +3333,7 @@ nlp_status run_graph(nlp_graph* g, const Params& p, EdgeOut* out, hipStream_t st
 // Run the fast path; *handled = false when the caller must use the general
 // flow (wedges beyond the budget, or -- bucket grouping -- a bucket beyond the
 // LDS cap).
-// NLP_HOSTPROF=1: host-side phase times of the fast path, averaged and printed
+// hprof (build-time): host-side phase times of the fast path, averaged and printed
 // every 100 calls (diagnostics of the per-call overhead outside the kernels).
 struct HostProf {
   double prep = 0, launch = 0, wait = 0, post = 0;
@@ -3505,7 +3371,7 @@ void stamp_times(const uint64_t* h, float* score, float* select, float* hot) {
 // the call's flags reach g->d_sticky, its counters and stamps host_ctr.
 nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result, bool* handled, bool async = false) {
-  static const bool hprof = getenv("NLP_HOSTPROF") != nullptr;
+  constexpr bool hprof = false;  // host-side phase times of the fast path (a build-time diagnostic)
   static HostProf hp;
   double t0 = hprof ? now_us() : 0, t1 = 0, t2 = 0, t3 = 0;
   *handled = false;
@@ -3549,10 +3415,10 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (hprof) t1 = now_us();
     const bool stamps = sorted && sp.split && g->hot_stage < 0;
     // Stamp-timed graphs end without an event node and the host polls the
-    // stream (NLP_STREAM_WAIT=0: an end event instead).  Equal for one
+    // stream (an end event instead measured equal).  Equal for one
     // synchronous call; back-to-back calls (nlp_predict_device_async) run
     // 0.117 -> 0.111 ms each on C2, the event node costing GPU time per graph.
-    static const bool stream_wait = !(getenv("NLP_STREAM_WAIT") && getenv("NLP_STREAM_WAIT")[0] == '0');
+    constexpr bool stream_wait = true;
     const bool gseq = stream_wait && sorted;
     // asynchronous stamp-timed calls are launched kernel by kernel (below): the
     // host's ~40 us of launches hide behind the previous call's kernels, and
@@ -3595,70 +3461,6 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
               "flags %llx replayed %d\n", attempt, (unsigned long long)p.ua, (unsigned long long)p.ub, (int)msd,
               sorted ? sp.msd_passes : 0, sorted ? (int)sp.split : 0, (unsigned long long)g->capW,
               (unsigned long long)h[C_W], (unsigned long long)h[C_C], (unsigned long long)h[C_FLAGS], (int)replayed);
-    if (sorted && sp.msd && getenv("NLP_CHECK_SORT")) {  // diagnostics: records sorted after grouping?
-      const uint64_t n = h[C_WSORT];
-      const int P = sp.msd_passes;
-      std::vector<uint64_t> rk(n);
-      TRY(hipMemcpy(rk.data(), (P & 1) ? sp.rk1 : sp.rk0, n * 8, hipMemcpyDeviceToHost));
-      uint64_t bad = 0, first = ~0ull;
-      for (uint64_t i = 1; i < n; ++i)
-        if (rk[i] < rk[i - 1]) {
-          if (!bad) first = i;
-          ++bad;
-        }
-      fprintf(stderr, "nlp: sort check n %llu shift %d wbits %d: %llu inversions", (unsigned long long)n,
-              sp.msd_shift, sp.wbits, (unsigned long long)bad);
-      if (bad) {
-        fprintf(stderr, " first at %llu: %llx > %llx (fine %llx %llx)\n  around:", (unsigned long long)first,
-                (unsigned long long)rk[first - 1], (unsigned long long)rk[first],
-                (unsigned long long)(rk[first - 1] >> sp.msd_shift), (unsigned long long)(rk[first] >> sp.msd_shift));
-        for (uint64_t i = first > 6 ? first - 6 : 0; i < std::min(n, first + 6); ++i)
-          fprintf(stderr, " %llx", (unsigned long long)(rk[i] >> sp.msd_shift));
-        // device digit histograms (sum of the copies) vs the records' own
-        std::vector<uint32_t> hd(HCOPIES * HSTRIDE);
-        TRY(hipMemcpy(hd.data(), sp.arena + SP_HREC, hd.size() * 4, hipMemcpyDeviceToHost));
-        for (int dg = 0; dg < P; ++dg) {
-          std::vector<uint64_t> hh(256, 0);
-          for (uint64_t i = 0; i < n; ++i) ++hh[(rk[i] >> (sp.msd_shift + 8 * dg)) & 255];
-          int mism = 0;
-          for (int b = 0; b < 256; ++b) {
-            uint64_t s = 0;
-            for (int c = 0; c < HCOPIES; ++c) s += hd[c * HSTRIDE + dg * 256 + b];
-            if (s != hh[b]) {
-              if (mism < 4) fprintf(stderr, "\n  digit %d bin %d: device %llu records %llu", dg, b,
-                                    (unsigned long long)s, (unsigned long long)hh[b]);
-              ++mism;
-            }
-          }
-          fprintf(stderr, "\n  digit %d: %d bins differ", dg, mism);
-        }
-        // run-length encoding of the top digit in the final records
-        fprintf(stderr, "\n  top-digit runs:");
-        {
-          const int tsh = sp.msd_shift + 8 * (P - 1);
-          uint64_t i = 0;
-          while (i < n) {
-            uint64_t j = i;
-            while (j < n && ((rk[j] >> tsh) & 255) == ((rk[i] >> tsh) & 255)) ++j;
-            if (j - i < 4 || ((rk[i] >> tsh) & 255) >= 0x30) fprintf(stderr, " %llx@%llu+%llu", (unsigned long long)((rk[i] >> tsh) & 255),
-                                      (unsigned long long)i, (unsigned long long)(j - i));
-            i = j;
-          }
-        }
-        if (P == 2) {  // pass-0 output (rk1) must be sorted by digit 0
-          std::vector<uint64_t> r1(n);
-          TRY(hipMemcpy(r1.data(), sp.rk1, n * 8, hipMemcpyDeviceToHost));
-          uint64_t b0 = 0;
-          for (uint64_t i = 1; i < n; ++i)
-            if (((r1[i] >> sp.msd_shift) & 255) < ((r1[i - 1] >> sp.msd_shift) & 255)) ++b0;
-          fprintf(stderr, "\n  pass-0 output digit-0 inversions: %llu", (unsigned long long)b0);
-        }
-        // the k_sp_group ranges containing the inversion
-        fprintf(stderr, "\n  GR_T tile of the inversion: %llu (offset %llu)", (unsigned long long)(first / GR_T),
-                (unsigned long long)(first % GR_T));
-      }
-      fprintf(stderr, "\n");
-    }
     if (h[C_FLAGS] >> 32) {  // look-back timeout
       if (debug_on())
         fprintf(stderr, "nlp: look-back timeout, flags %llx W %llu C %llu msd %d passes %d\n",
@@ -3768,7 +3570,7 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
       hp.launch += t2 - t1;
       hp.wait += t3 - t2;
       hp.post += now_us() - t3;
-      static const int every = std::max(1, atoi(getenv("NLP_HOSTPROF")));
+      constexpr int every = 1000;
       if (++hp.n == every) {
         fprintf(stderr, "nlp host us/call: prepare %.1f launch %.1f wait %.1f post %.1f (replayed %d)\n",
                 hp.prep / every, hp.launch / every, hp.wait / every, hp.post / every, (int)replayed);

@@ -408,62 +408,36 @@ class _env:
                 os.environ[k] = v
 
 
-# path 4 (hash accumulation) with every kernel forced: 0 default (bin-0 row
-# batches, tiered bin-1 rows, hub pass, survivor lists by k_dc_*, exclusion of
-# wide rows by the membership table, record-sort final order), 1
-# workgroup/LDS, 2 hub pass for every row, 3 k_hp_part over a tiny scratch
-# (bucket groups and direct accumulation), 4 k_hp_part with one bucket per row
-# (sub-range passes), 5 bin 0 as one 1024-entry launch (no table-size tiers),
-# 6/7 k_hp_part rows sliced over several workgroups (bucket slices, exclusion
-# cursor per slice), 8 the edge-parallel work estimate, 9 a wave per bin-0 row,
-# 10 k_hp_part for every row, 11 hub pass with one w-bucket per row (direct
-# counters for the counts), 12 the same with 128-entry item tables and no
-# direct counters (heavy buckets split into w-range items by their segment
-# histograms), 13 bin-1 rows by the hub pass, 14 the hub pass's AA / RA items
-# by the ordered re-walk instead of sort mode, 15/16 sort-mode items of at
-# most 16 / 40 wedges (heavy buckets split, single bins beyond flagged
-# HH_BIG), 17 survivor lists from in-edge atomics (unordered: the AA / RA row
-# kernels sort them), 18 no entry-degree tables (deg w gathered at the drain),
-# 19 = 17 with bin-1 rows, 20 row batches gathering deg / off of every first
-# hop (no packed survivor entries), 21 survivor suffixes searched per call (no
-# per-graph rank bytes), 22 survivor counts and fill as two kernels, 23 the
-# one-pass build (k_hp_dcls_one) with its output capacity overflowing (the
-# two-kernel fallback), 24 the exclusion walking all of N(u) (no per-row start
-# above u), 25 the row batches reserving every flush (no emission windows, no
-# padding), 26 hub pass with one w-bucket per row and 64-wide direct counters
-# (heavy buckets grouped into direct ranges, single bins beyond by HH_WIDE
-# sub-ranges), 27 bin-1 rows by k_hp_block (not the tiered k_hp_rowb /
-# k_hp_rowo), 28 / 29 every bin-1 row in the 8192- / at least the 4096-entry
-# tier, 30-32 the first-order exclusion of every row by the membership table
-# (row batches and wave rows; bin-1 tiers; k_hp_block), 33 every row by
-# marks, 34 the one-pass survivor build, 35 the count metrics' survivor lists
-# compacted per call (k_dc_*) instead of taken as prefixes of the per-graph
-# class-ordered short lists (variants 22, 23, 34 also compact per call), 36
-# short lists of the classes up to 3 only (H = 2 from them, H = 4, 16 compacted),
-# 37 / 38 the final order over rank-compressed 8-byte keys on every call
-# (k_es_pass8; by default only from ES8_MIN links on)
+# Path-4 variants against the oracle (round 5: cut to the defaults plus the
+# fallbacks that trigger on real inputs): 0 the defaults (on `edge`: the
+# round-4 emission-window hang case), 1-3 rows forced into bins 1 / 2 / 3 (bin
+# 3 with a tiny k_hp_part scratch and no hub pass), 4 no row batches (graphs
+# with ids beyond 2^26), 5 bins 2-3 by k_hp_part (a chunk beyond the hub
+# scratch), 6 hub pass with 128-entry item tables and no direct counters
+# (heavy buckets split by their segment histograms), 7 bin-1 rows by the hub
+# pass, 8 AA / RA hub items by the ordered re-walk, 9 / 10 sort-mode items of
+# at most 16 / 40 wedges (heavy buckets split, single bins beyond flagged
+# HH_BIG), 11-14 the per-graph tables a full HBM leaves out (degree classes,
+# entry degrees, rank bytes, exclusion starts), 15 one w-bucket rows with
+# 64-wide direct counters (HH_WIDE sub-ranges), 16 bin-1 rows by k_hp_block,
+# 17 every bin-1 row in the 8192-entry tier, 18 every row's exclusion by the
+# membership table, 19 every row's by marks (no table), 20 the count metrics'
+# survivor lists compacted per call (k_dc_*, the AA / RA route), 21 short lists
+# of the classes up to 3 only, 22 / 23 the final order over rank-compressed
+# 8-byte keys on every call (by default from ES8_MIN links on)
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_ONE_BUCKET="1", NLP_HASH_HUB="0"), dict(NLP_HASH_TIERS="0"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_SLICES="7", NLP_HASH_HUB="0"),
-                 dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_SLICES="3", NLP_HASH_HUB="0"),
-                 dict(NLP_HASH_WORK_SURV="0"), dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
-                 dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000"),
+                 dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="0"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_HUB_MIN="1"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SORT="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="16", NLP_HASH_HUB_TL="7"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_SCAP="40", NLP_HASH_HUB_BW="1000000"),
-                 dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DCLS="0", NLP_HASH_MINBIN="1"),
-                 dict(NLP_HASH_SDO="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_ONE="0", NLP_HASH_SLIST="0"),
-                 dict(NLP_HASH_ONE="1", NLP_HASH_ONE_CAP="5", NLP_HASH_SLIST="0"), dict(NLP_HASH_XS="0"),
-                 dict(NLP_HASH_WIN="0"),
+                 dict(NLP_HASH_DCLS="0"), dict(NLP_HASH_KDEG="0"), dict(NLP_HASH_DRANK="0"), dict(NLP_HASH_XS="0"),
                  dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB_BW="1000000", NLP_HASH_HUB_TL="7", NLP_HH_DIRECT="64"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
-                 dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="3"),
-                 dict(NLP_HASH_UX="0"), dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"),
-                 dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_UX="off"),
-                 dict(NLP_HASH_ONE="1", NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3"),
+                 dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"), dict(NLP_HASH_UX="off"),
+                 dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3"),
                  dict(NLP_ES8="2"), dict(NLP_ES8="2", NLP_HASH_MINBIN="2")]
 
 
@@ -530,8 +504,7 @@ def test_gpu_hash_path_all_candidates_and_min_score(gpu, golden, oracle):
 def test_gpu_hash_path_star_hub(gpu, oracle):
     """A hub source whose row holds > 10^4 distinct second hops (bins 2 and 3)."""
     off, keys = star_csr(20000)
-    for v in (dict(), dict(NLP_HASH_SCAP="5000"), dict(NLP_HASH_ONE_BUCKET="1"), dict(NLP_HASH_SLICES="1"),
-              dict(NLP_HASH_SLICES="13", NLP_HASH_SCAP="5000")):
+    for v in (dict(), dict(NLP_HASH_SCAP="5000"), dict(NLP_HASH_HUB="0"), dict(NLP_HASH_HUB="0", NLP_HASH_SCAP="5000")):
         with _env(NLP_HASH="1", **v):
             with gpu.Graph(off, keys) as G:
                 for m, H, k in ((0, 0, 500), (7, 0, 30000), (1, 2, 10 ** 6), (8, 4, 100)):
@@ -774,18 +747,15 @@ def test_gpu_exclusion_without_edge_table(gpu, oracle):
                 assert_canonical_equal(eu, ew, es, u2, w2, s2)
 
 
-@pytest.mark.parametrize("env", [dict(NLP_FUSE_GATHER="1"), dict(NLP_EX_IPT="2"), dict(NLP_EX_IPT="4"), dict(NLP_DIRECT="0"),
-                                 dict(NLP_MSD_PASSES="2"), dict(NLP_FUSE_RUNS="0"), dict(NLP_DX_BITS="1"),
-                                 dict(NLP_DX_BITS="2"), dict(NLP_DX_BITS="3"), dict(NLP_DX_BITS="12"),
-                                 dict(NLP_ORD11="1"), dict(NLP_GR_NT="512"), dict(NLP_COUNTED="0"),
+@pytest.mark.parametrize("env", [dict(NLP_DIRECT="0"), dict(NLP_MSD_PASSES="2"), dict(NLP_DX_BITS="1"),
+                                 dict(NLP_DX_BITS="3"), dict(NLP_DX_BITS="12"), dict(NLP_COUNTED="0"),
                                  dict(NLP_EDGE_FILTER="2"), dict(NLP_SV_PACK="0")])
 def test_gpu_sort_path_variants_equal(gpu, oracle, env):
-    """Sort-path build variants (fused output gather, several survivors per
-    expansion thread, two MSD passes + group sort, separate grouping and
+    """Sort-path variants (two MSD passes + group sort, separate grouping and
     scoring, direct buckets so wide that k_sp_grouprun sorts 2 or 4 keys per
-    thread or falls back on too-big ranges, three 11-bit ordering passes,
-    look-back ordering passes instead of the counted k_sp_cpass) give the
-    default's results."""
+    thread or falls back on too-big ranges, look-back ordering passes instead
+    of the counted k_sp_cpass, the edge filter in front of the membership
+    table, unpacked survivor rows) give the default's results."""
     off, keys = random_csr(9000, 14, 21)
     k = 2500
     with gpu.Graph(off, keys) as G:
@@ -821,12 +791,12 @@ def test_gpu_counted_passes_tiles_and_redo(gpu, oracle, n, avg, H, env):
             assert_canonical_equal(eu, ew, es, u, w, s)
 
 
-@pytest.mark.parametrize("env", [{}, dict(NLP_ASYNC_GRAPH="1")])
+@pytest.mark.parametrize("env", [{}])
 def test_gpu_async_batch_equals_sync(gpu, oracle, env):
     """nlp_predict_device_async / nlp_sync: a call with no synchronous
     predecessor runs synchronously; after a synchronous call with the same
-    arguments the calls are only enqueued (kernel by kernel, or as replayed
-    graphs with NLP_ASYNC_GRAPH=1); a batch mixing both ends with the last
+    arguments the calls are only enqueued (kernel by kernel); a batch mixing
+    both ends with the last
     call's count and output; nlp_sync with nothing pending is refused."""
     import torch
     off, keys = random_csr(20000, 12, 31)

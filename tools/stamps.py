@@ -1,6 +1,6 @@
 """Summarise NLP_STAMP phase stamps (s_memrealtime, 100 MHz) of the last call.
 
-    NLP_STAMP=gpurun_out/st.bin NLP_HOT_STAGE=5 python bench.py ...
+    NLP_STAMP=gpurun_out/st.bin python bench.py ...
     python tools/stamps.py gpurun_out/st.bin [nphases]
 """
 import sys
