@@ -588,3 +588,35 @@ int nlpo_predict_par(const uint64_t *off, const uint32_t *keys, uint64_t span,
   stats[7] = dxor;
   return 0;
 }
+
+/* Wedges (u, v, w) with w > u of the sources [ua, ub): the count of the
+ * reference's wedge loop (predict.hxx:284-304 -> 153-160: every v of N(u)
+ * with deg v <= H, or all for H = 0, every w of N(v) with w > u), found per
+ * (u, v) entry by one binary search of the sorted list N(v) instead of a walk
+ * -- O(entries log deg) for ranges whose walk would take minutes (the C5
+ * shards' property test).  OpenMP over sources when built with it. */
+uint64_t nlpo_wedges_gt(const uint64_t *off, const uint32_t *keys, uint64_t span, uint32_t hub, uint64_t ua,
+                        uint64_t ub, int threads) {
+  uint64_t total = 0;
+  if (ub > span) ub = span;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
+#endif
+  for (long long uu = (long long)ua; uu < (long long)ub; ++uu) {
+    const uint64_t u = (uint64_t)uu;
+    for (uint64_t i = off[u]; i < off[u + 1]; ++i) {
+      const uint32_t v = keys[i];
+      if (v >= span) continue;
+      const uint64_t lo0 = off[v], hi0 = off[v + 1];
+      if (hub && hi0 - lo0 > hub) continue;        /* predict.hxx:298-301 */
+      uint64_t lo = lo0, hi = hi0;                 /* first entry of N(v) above u */
+      while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        if (keys[m] <= u) lo = m + 1; else hi = m;
+      }
+      total += hi0 - lo;
+    }
+  }
+  return total;
+}

@@ -50,6 +50,9 @@ def lib():
         L.nlpo_edge_hash.restype = ctypes.c_uint64
         L.nlpo_score_key.argtypes = [ctypes.c_float]
         L.nlpo_score_key.restype = ctypes.c_uint32
+        L.nlpo_wedges_gt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]
+        L.nlpo_wedges_gt.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -207,3 +210,12 @@ def ref_predict(csr_path, metric, hub, max_edges=-1, mode="seq", threads=1, repe
     t, ts, n = r.stdout.split()
     u, w, s = read_edges(out)
     return u, w, s, dict(time_ms=float(t), scoring_ms=float(ts))
+
+
+def wedges_gt(offsets, keys, hub, u_begin, u_end, threads=0):
+    """Wedges (u, v, w), w > u, of the sources [u_begin, u_end) (nlpo_wedges_gt:
+    one binary search of N(v) per (u, v) entry, predict.hxx:284-304)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    keys = np.ascontiguousarray(keys, dtype=np.uint32)
+    return int(lib().nlpo_wedges_gt(offsets.ctypes.data, keys.ctypes.data, len(offsets) - 1, hub, u_begin, u_end,
+                                    threads))

@@ -106,3 +106,55 @@ def test_gpu_c5_ihub_shards_merge_to_the_range_result(c5):
     km = c5.G.merge_blocks_device(blocks, k, merged)
     assert km == n
     assert torch.equal(merged[:n], whole[:n])
+
+
+@pytest.mark.timeout(600)
+def test_gpu_c5_heaviest_shard_leading_wedges(c5, oracle):
+    """The leading 1 % of the wedges of shard 0 of the 8 wedge-balanced shards
+    of the whole call (dist.shard_ranges over dist.source_weights: the lowest
+    ids, whose sources see the most w > u) -- ~5e10 wedges, far beyond what the
+    oracle can score, so size-independent properties: the canonical order, every
+    link in the range, the wedge counter equal to the exact count of w > u
+    wedges (oracle.wedges_gt: one binary search of N(v) per (u, v) entry,
+    predict.hxx:284-304), and the range split at its middle weight, the halves
+    predicted and merged by nlp_merge_blocks_device, equal to the whole."""
+    import torch
+    import nlp_loader
+    dmod = nlp_loader.load_sub("dist")
+    span = len(c5.off) - 1
+    w = dmod.source_weights(c5.off_t, c5.keys_t, 0)
+    ranges = dmod.shard_ranges(span, 8, w)
+    ua, ub = ranges[0]
+    cw = torch.cumsum(torch.as_tensor(w, dtype=torch.float64).cpu()[ua:ub], 0)
+    ub1 = ua + int(torch.searchsorted(cw, 0.01 * float(cw[-1]))) + 1
+    mid = ua + int(torch.searchsorted(cw, 0.005 * float(cw[-1]))) + 1
+    k = c5.k
+    whole = c5.out()
+    n, t = c5.G.predict_device(0, 0, k, whole, ua, ub1)
+    u, ww, s = c5.nlp.edges_from_tensor(whole, n)
+    assert t["path"] == 4 and n > 0
+    assert_canonical_order(u, ww, s)
+    assert np.all((u >= ua) & (u < ub1))
+    exact = oracle.wedges_gt(c5.off, c5.keys, 0, ua, ub1, threads=ORACLE_THREADS)
+    assert t["wedges"] == exact, (t["wedges"], exact)
+    assert t["wedges"] >= 0.005 * 3.9e13 / 8  # about 1 % of a shard of the whole call's ~3.9e13
+    parts = []
+    for a, b in ((ua, mid), (mid, ub1)):
+        blk = c5.out(k + 1)
+        m, tm = c5.G.predict_device(0, 0, k, blk[1:], a, b)
+        h = np.array([m & 0xFFFFFFFF, m >> 32, 0x4E4C5042], np.uint32).view(np.int32)
+        blk[0] = torch.from_numpy(h).cuda()
+        parts.append((blk, m, tm["wedges"]))
+    assert parts[0][2] + parts[1][2] == t["wedges"]
+    stride = max(m for _, m, _ in parts) + 1
+    blocks = torch.stack([b[:stride] for b, _, _ in parts])
+    merged = c5.out()
+    km = c5.G.merge_blocks_device(blocks, k, merged)
+    assert km == n
+    assert torch.equal(merged[:n], whole[:n])
+    d = os.environ.get("NLP_TEST_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "c5_shard0_leading.json"), "w") as f:
+            json.dump(dict(shard0=[ua, ub], leading=[ua, ub1], wedges=t["wedges"], exact_wedges=exact,
+                           candidates=t["candidates"], predicted=n, chunks=t["chunks"]), f)
