@@ -2186,6 +2186,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   TRY(hipMemcpyAsync(small + 8, &g->host_small[8], 8, hipMemcpyHostToDevice, st));
   uint64_t r0 = 0, q0[HP_NBINS] = {0, 0, 0, 0};
   double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
+  double real_rate = 1.0;  // the same without window padding: sizes the next chunk's emission windows
   bool full = false;  // k candidates held: tau is in force
   bool retry = false; // the chunk is a retry after an emission overflow
   // the hub pass's scratch in wedges (run_hub: w, and v for AA / RA)
@@ -2294,7 +2295,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
           // small for a window of HP_STG per wave, or the retry of an overflowed
           // chunk, reserves per flush
           const unsigned grb = std::min<unsigned>(gr, g->occ_hb);
-          const uint64_t per = wchunk / ((uint64_t)grb * NWAVE * 8 + 1);
+          // from the last chunk's REAL emissions: with a threshold in force a chunk emits a few percent
+          // of its wedges, and windows sized by the wedge bound padded ~1.3e7 slots per chunk of the
+          // C5 IHub shards (every chunk then filled the buffer and forced a prune)
+          const uint64_t per = (uint64_t)(real_rate * (double)wchunk) / ((uint64_t)grb * NWAVE * 8 + 1);
           if (per >= (uint64_t)HP_STG) {
             a.win = (uint32_t)std::min<uint64_t>(HP_WIN, per);
             gb = grb;
@@ -2428,6 +2432,8 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     C.nan += g->host_small[HPC_NAN];
     C.wedges += g->host_small[HPC_WEDGE];
     rate = (double)emitted / (double)std::max<uint64_t>(wchunk, 1);
+    real_rate = (double)(emitted - std::min<uint64_t>(emitted, g->host_small[HPC_PAD])) /
+                (double)std::max<uint64_t>(wchunk, 1);
     r0 = r1;
     for (int b = 0; b < HP_NBINS; ++b) q0[b] = q1[b];
     if ((C.n > k && C.n > k + E / 2) || (r0 >= nU && (C.n > k || C.pad))) {
