@@ -3066,24 +3066,45 @@ __global__ void k_hh_rows(HpArgs a, const uint32_t* __restrict__ l2, uint64_t n2
     const uint32_t u = hh_row_u(l2, n2, l3, r);
     const uint64_t W = wu[u - ua];
     const uint64_t span_w = a.S - 1 - u;  // candidate w in (u, S)
-    uint32_t P = 0, shift = 0, items = 0;
     uint64_t nf = 0;
-    if (span_w > 0) {
-      uint64_t pd = (W + bw - 1) / bw;
+    if (span_w > 0 && W > 0) {
+      if (a.soff) nf = hp_slen(a, u, a.soff[u - a.sua]);
+      else nf = a.g.off[u + 1] - a.g.off[u];
+    }
+    hr_u[r] = u;
+    hr_nf[r] = nf;
+    (void)hr_shift;
+    (void)hr_p;
+    (void)hr_items;
+    (void)bw;
+  }
+}
+
+// After k_hh_fpre: per hub row its wedges above u, Wr = the last inclusive
+// prefix of its first hops' above-u lengths, give the w-buckets (about bw
+// wedges each, at most HH_PMAX) and the enumeration items (HH_WC wedges each)
+// -- sized by the wedges the row really enumerates, not by W(u) (every w).
+__global__ void k_hh_items(HpArgs a, uint64_t nh, const uint32_t* __restrict__ hr_u, const uint64_t* __restrict__ hr_nf,
+                           const uint64_t* __restrict__ fbase, const uint64_t* __restrict__ fp,
+                           uint32_t* __restrict__ hr_shift, uint32_t* __restrict__ hr_p, uint32_t* __restrict__ hr_items,
+                           uint64_t bw) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t u = hr_u[r];
+    const uint64_t nf = hr_nf[r];
+    const uint64_t Wr = nf ? fp[fbase[r] + nf - 1] : 0ull;
+    const uint64_t span_w = a.S - 1 - u;
+    uint32_t P = 0, shift = 0, items = 0;
+    if (Wr > 0 && span_w > 0) {
+      uint64_t pd = (Wr + bw - 1) / bw;
       if (pd < 1) pd = 1;
       if (pd > HH_PMAX) pd = HH_PMAX;
       shift = (uint32_t)log2_ceil((span_w + pd - 1) / pd);
       P = (uint32_t)((span_w + (1ull << shift) - 1) >> shift);
-      if (a.soff) nf = hp_slen(a, u, a.soff[u - a.sua]);
-      else nf = a.g.off[u + 1] - a.g.off[u];
-      items = nf ? (uint32_t)std::min<uint64_t>((W + HH_WC - 1) / HH_WC, 0x7fffffffull) : 0u;
-      if (items == 0) P = 0;  // no first hop or no wedge: no candidate
+      items = (uint32_t)std::min<uint64_t>((Wr + HH_WC - 1) / HH_WC, 0x7fffffffull);
     }
-    hr_u[r] = u;
     hr_shift[r] = shift;
     hr_p[r] = P;
     hr_items[r] = items;
-    hr_nf[r] = items ? nf : 0;
   }
 }
 
@@ -3128,8 +3149,14 @@ __device__ __forceinline__ HhHops hh_hops(const HpArgs& a, uint32_t u) {
   h.fd = a.sdo && a.soff ? a.sdo + (h.fh - a.skeys) : nullptr;
   return h;
 }
-__device__ __forceinline__ void hh_hop(const HpArgs& a, const HhHops& h, uint64_t i, uint32_t* v, uint64_t* st,
-                                       uint64_t* len) {
+// First hop i of row u: v, and the part of N(v) above u, [st, st + len) --
+// only w > u are candidates (predict.hxx:221), and N(v) is sorted, so the
+// entries at or below u are a prefix: one binary search per first hop (none
+// when N(v) starts above u) instead of enumerating wedges that are dropped.
+// (The late rows of an IHub call see mostly w < u: the C5 shards of the
+// highest ids enumerated three times their wedges before round 5.)
+__device__ __forceinline__ void hh_hop(const HpArgs& a, const HhHops& h, uint32_t u, uint64_t i, uint32_t* v,
+                                       uint64_t* st, uint64_t* len) {
   *v = h.fh[i];
   if (h.fd) {
     const uint64_t x = h.fd[i];
@@ -3137,8 +3164,21 @@ __device__ __forceinline__ void hh_hop(const HpArgs& a, const HhHops& h, uint64_
     *st = x & ((1ull << HP_SDO_SH) - 1);
   } else {
     const uint32_t d = a.g.deg[*v];
-    *len = hp_surv(d, a.H) ? d : 0;
-    *st = *len ? a.g.off[*v] : 0;
+    uint64_t lo = 0, hi = 0;
+    if (hp_surv(d, a.H)) {
+      lo = a.g.off[*v];
+      hi = lo + d;
+      if (a.g.keys[lo] <= u) {  // first entry above u
+        uint64_t l = lo + 1, r = hi;
+        while (l < r) {
+          const uint64_t m = (l + r) >> 1;
+          if (a.g.keys[m] <= u) l = m + 1; else r = m;
+        }
+        lo = l;
+      }
+    }
+    *st = lo;
+    *len = hi - lo;
   }
 }
 
@@ -3158,7 +3198,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_fpre(HpArgs a, uint64_t nh, const 
       const uint64_t i = b0 + t;
       uint32_t v;
       uint64_t st, len = 0;
-      if (i < nf) hh_hop(a, h, i, &v, &st, &len);
+      if (i < nf) hh_hop(a, h, hr_u[r], i, &v, &st, &len);
       const uint64_t incl = block_incl_scan_1024(len, s_w);
       if (i < nf) fp[fbase[r] + i] = carry + incl;
       if (t == HH_NT - 1) s_tot = incl;
@@ -3189,7 +3229,7 @@ __device__ __forceinline__ void hh_enum_range(const HpArgs& a, uint32_t u, uint3
       const uint64_t lo = s0 > j0 ? s0 : j0, hi = e < j1 ? e : j1;
       if (hi > lo) {
         uint64_t full;
-        hh_hop(a, h, i, &v, &st, &full);
+        hh_hop(a, h, u, i, &v, &st, &full);
         st += lo - s0;
         len = hi - lo;
       }

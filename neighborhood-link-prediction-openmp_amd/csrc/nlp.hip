@@ -1851,7 +1851,7 @@ double hp_estimate(const nlp_graph* g, const Params& p) {
 // k_hp_part instead; nothing was emitted).
 nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n2, const uint32_t* l3, uint64_t n3,
                    const uint64_t* wu, uint64_t ua, bool custom, uint64_t* scan, uint32_t* queue, bool* done,
-                   hipStream_t st) {
+                   hipStream_t st, uint64_t* hub_wedges = nullptr) {
   Workspace& ws = g->ws;
   *done = false;
   const uint64_t nh = n2 + n3;
@@ -1863,14 +1863,29 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   uint64_t *bbase = pre, *ibase = pre + nh + 1, *hr_nf = pre + 2 * (nh + 1), *fbase = pre + 3 * (nh + 1);
   LAUNCH(k_hh_rows, nh, st, a, l2, n2, l3, n3, wu, ua, hr_u, hr_shift, hr_p, hr_items, hr_nf, g->hh_bw);
   TRY(hipGetLastError());
-  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_p, nh, bbase, bbase + nh, st));
-  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_items, nh, ibase, ibase + nh, st));
+  // first hops -> the prefix of their lists' parts above u (k_hh_fpre), then the
+  // buckets and items of every row from the wedges it really enumerates (k_hh_items)
   TRY(scan_ws<uint64_t>(ws, B_SCAN, hr_nf, nh, fbase, fbase + nh, st));
-  TRY(hipMemcpyAsync(&g->host_small[48], bbase + nh, 8, hipMemcpyDeviceToHost, st));
-  TRY(hipMemcpyAsync(&g->host_small[49], ibase + nh, 8, hipMemcpyDeviceToHost, st));
   TRY(hipMemcpyAsync(&g->host_small[51], fbase + nh, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
-  const uint64_t NB = g->host_small[48], NI = g->host_small[49], NF = g->host_small[51];
+  const uint64_t NF = g->host_small[51];
+  if (NF == 0) {
+    *done = true;
+    return NLP_OK;
+  }
+  uint64_t* fp;
+  TRY(wsget(ws, B_HH_FP, std::max<uint64_t>(NF, 1), &fp));
+  hipLaunchKernelGGL(k_hh_fpre, dim3((unsigned)std::min<uint64_t>(nh, 4096)), dim3(HH_NT), 0, st, a, nh,
+                     (const uint32_t*)hr_u, (const uint64_t*)hr_nf, (const uint64_t*)fbase, fp);
+  LAUNCH(k_hh_items, nh, st, a, nh, (const uint32_t*)hr_u, (const uint64_t*)hr_nf, (const uint64_t*)fbase,
+         (const uint64_t*)fp, hr_shift, hr_p, hr_items, g->hh_bw);
+  TRY(hipGetLastError());
+  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_p, nh, bbase, bbase + nh, st));
+  TRY(scan_ws<uint32_t>(ws, B_SCAN, hr_items, nh, ibase, ibase + nh, st));
+  TRY(hipMemcpyAsync(&g->host_small[48], bbase + nh, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(&g->host_small[49], ibase + nh, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  const uint64_t NB = g->host_small[48], NI = g->host_small[49];
   if (NB == 0 || NI == 0) {
     *done = true;
     return NLP_OK;
@@ -1878,20 +1893,17 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   if (NI > 0x7fffffffull) return NLP_OK;
   uint32_t* maps;  // brow [NB]
   uint32_t* bc;    // bcnt [NB], bcur [NB]
-  uint64_t *boff, *xs, *fp;
+  uint64_t *boff, *xs;
   TRY(wsget(ws, B_HH_MAPS, NB, &maps));
   TRY(wsget(ws, B_HH_BCNT, 2 * NB, &bc));
   TRY(wsget(ws, B_HH_BOFF, NB + 1, &boff));
   TRY(wsget(ws, B_HH_XS, NB, &xs));
-  TRY(wsget(ws, B_HH_FP, std::max<uint64_t>(NF, 1), &fp));
   uint32_t *brow = maps, *bcnt = bc, *bcur = bc + NB;
   TRY(hipMemsetAsync(bc, 0, 2 * NB * 4, st));
   LAUNCH(k_hh_maps, nh, st, a, nh, (const uint32_t*)hr_u, (const uint32_t*)hr_shift, (const uint32_t*)hr_p,
          (const uint64_t*)bbase, (const uint32_t*)hr_items, (const uint64_t*)ibase, brow, (uint32_t*)nullptr);
   LAUNCH(k_hh_xstart, NB, st, a, NB, (const uint32_t*)brow, (const uint32_t*)hr_u, (const uint32_t*)hr_shift,
          (const uint64_t*)bbase, xs);
-  hipLaunchKernelGGL(k_hh_fpre, dim3((unsigned)std::min<uint64_t>(nh, 4096)), dim3(HH_NT), 0, st, a, nh,
-                     (const uint32_t*)hr_u, (const uint64_t*)hr_nf, (const uint64_t*)fbase, fp);
   TRY(hipGetLastError());
   if (custom)
     hipLaunchKernelGGL((k_hh_enum<false, true>), dim3((unsigned)NI), dim3(HH_NT), 0, st, a, nh, (const uint32_t*)hr_u,
@@ -1912,6 +1924,7 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   TRY(hipMemcpyAsync(&g->host_small[50], boff + NB, 8, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
   const uint64_t tot = g->host_small[50];
+  if (hub_wedges) *hub_wedges += tot;
   TRY(hipMemsetAsync(bcur, 0, NB * 4, st));
   const uint64_t words = (uint64_t)g->hp_gp * g->hp_scap * 2;  // u32 words of the k_hp_part scratch
   const uint64_t capw = custom ? words / 2 : words;
@@ -2187,6 +2200,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t r0 = 0, q0[HP_NBINS] = {0, 0, 0, 0};
   double rate = 1.0;  // emitted candidates per unit of W(u), from the last chunk
   double real_rate = 1.0;  // the same without window padding: sizes the next chunk's emission windows
+  double hub_ratio = 1.0;  // hub wedges above u per unit of W(u), from the last chunk with hub rows
   bool full = false;  // k candidates held: tau is in force
   bool retry = false; // the chunk is a retry after an emission overflow
   // the hub pass's scratch in wedges (run_hub: w, and v for AA / RA)
@@ -2380,9 +2394,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipGetLastError());
     }
     bool hub_done = false;
+    uint64_t hub_w = 0;  // the chunk's hub wedges above u (run_hub's count pass)
     if (g->hp_hub && (q1[2] - q0[2]) + (q1[3] - q0[3]) > 0) {
       nlp_status sh = run_hub(g, a, lists[2] + q0[2], q1[2] - q0[2], lists[3] + q0[3], q1[3] - q0[3], wu, ua, custom,
-                              scan, tcnt + 11, &hub_done, st);  // tcnt[11, 14): queue, item and heavy counts
+                              scan, tcnt + 11, &hub_done, st, &hub_w);  // tcnt[11, 14): queue, item and heavy counts
       if (sh != NLP_OK) return sh;
     }
     for (int b = 2; b < HP_NBINS && !hub_done; ++b) {  // rows beyond an LDS table: w-bucket partitioning
@@ -2434,6 +2449,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     rate = (double)emitted / (double)std::max<uint64_t>(wchunk, 1);
     real_rate = (double)(emitted - std::min<uint64_t>(emitted, g->host_small[HPC_PAD])) /
                 (double)std::max<uint64_t>(wchunk, 1);
+    // the hub rows' real wedges (above u) per unit of the chunk's bound W(u) (every w): the next
+    // chunk's bound may be that much larger for the same hub scratch (IHub rows of high ids
+    // enumerate a small part of their lists)
+    if (hub_w > 0 && wchunk > 0) hub_ratio = std::min(1.0, (double)hub_w / (double)wchunk);
     r0 = r1;
     for (int b = 0; b < HP_NBINS; ++b) q0[b] = q1[b];
     if ((C.n > k && C.n > k + E / 2) || (r0 >= nU && (C.n > k || C.pad))) {
@@ -2449,7 +2468,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     const double want = 0.5 * (double)free_slots / std::max(rate, 1e-9);
     target = (uint64_t)std::min(want, 1e18);
     if (!full && target > free_slots) target = free_slots;  // no threshold yet: emissions <= W(u)
-    target = std::min<uint64_t>(target, hub_cap);
+    target = std::min<uint64_t>(target, (uint64_t)std::min(1e18, 0.8 * (double)hub_cap / std::max(hub_ratio, 0.02)));
     if (target == 0) target = 1;
   }
   // held candidates are unordered: the caller orders them (hp_final_order)
