@@ -40,6 +40,9 @@
 #include <algorithm>
 #include <chrono>
 #include <future>
+#ifdef __linux__
+#include <sys/mman.h>
+#endif
 #include <cstdint>
 #include <cstddef>
 #include <cstdlib>
@@ -369,7 +372,19 @@ inline PredictLinkResult<K, W> predictLinksHip(const HipGraph& g, nlp_metric met
   uint64_t got = 0;
   if (n) check(nlp_copy_last(g.get(), buf, n, &got), "nlp_copy_last");
   n = got;
-  std::vector<std::tuple<K, K, W>> a(n);
+  std::vector<std::tuple<K, K, W>> a;
+  a.reserve(n);
+#ifdef __linux__
+  // a result of 1e8+ links is a fresh multi-GB mapping: ask for huge pages before
+  // the value-initialisation touches it (4-KiB page faults dominated the copy of
+  // a C4 H=16 result; a no-op where transparent huge pages are off)
+  if (n * sizeof(std::tuple<K, K, W>) >= (size_t(64) << 20)) {
+    const uintptr_t p0 = (uintptr_t)a.data(), p1 = p0 + n * sizeof(std::tuple<K, K, W>);
+    const uintptr_t a0 = (p0 + (size_t(2) << 20) - 1) & ~((uintptr_t(2) << 20) - 1), a1 = p1 & ~((uintptr_t(2) << 20) - 1);
+    if (a1 > a0) (void)madvise((void*)a0, a1 - a0, MADV_HUGEPAGE);
+  }
+#endif
+  a.resize(n);
   const nlp_edge* b = buf;
 #pragma omp parallel for schedule(static)
   for (long long i = 0; i < (long long)n; ++i) a[size_t(i)] = std::tuple<K, K, W>(K(b[i].u), K(b[i].v), W(b[i].score));

@@ -371,11 +371,14 @@ __device__ __forceinline__ uint64_t es_k8(const uint32_t* __restrict__ gset, con
   return es_rank(gset, srank, s) << (2 * vb) | (uint64_t)u << vb | w;
 }
 
-// ghist[p * 256 + d]: records whose digit p of K8 is d
+// ghist[p * 256 + d]: records whose digit p of K8 is d; and every record's K8
+// written to `keys` (the passes then read 8-byte keys only: the rank lookup
+// is paid once)
 __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                                                     const float* __restrict__ cs, uint64_t n, int vb,
                                                     const uint32_t* __restrict__ gset,
-                                                    const uint16_t* __restrict__ srank, uint32_t* __restrict__ ghist) {
+                                                    const uint16_t* __restrict__ srank, uint32_t* __restrict__ ghist,
+                                                    uint64_t* __restrict__ keys) {
   __shared__ uint32_t h[8][256];
   for (int i = threadIdx.x; i < 8 * 256; i += ES_NT) (&h[0][0])[i] = 0;
   __syncthreads();
@@ -394,8 +397,10 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
     }
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
-      const bool ok = j0 + (uint64_t)q * ES_NT + threadIdx.x < n;
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
+      const bool ok = j < n;
       const uint64_t k = ok ? es_k8(gset, srank, u[q], w[q], s[q], vb) : 0ull;
+      if (ok) keys[j] = k;
 #pragma unroll
       for (int p = 0; p < 8; ++p) {
         const uint32_t d = (uint32_t)(k >> (8 * p)) & 0xffu;
@@ -419,6 +424,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
 // One pass over 8-byte keys.  FIRST: the input is the candidate columns (K8
 // built from them); LAST: the output is the caller's edges (the score of rank
 // r from rscore).  Same tiling, look-back and write-out as k_es_pass.
+constexpr int ES8_IPT = 16;  // keys per thread: 8192-key tiles (64 KB of keys in LDS, two workgroups per CU)
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                                                     const float* __restrict__ cs, const uint32_t* __restrict__ gset,
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__
                                                     int vb, int shift, const uint32_t* __restrict__ ghist,
                                                     uint64_t* __restrict__ desc, uint32_t* __restrict__ ticket,
                                                     uint64_t epoch, uint32_t* __restrict__ err) {
-  constexpr int NTH = ES_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES_IPT;
+  constexpr int NTH = ES_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
   __shared__ uint64_t s_k[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];
   __shared__ uint64_t s_gofs[256];
@@ -447,14 +453,14 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__
     if (tile >= ntiles) break;  // uniform: every wave leaves
     const uint64_t base = tile * ES_TILE;
     const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - base);
-    uint64_t rk8[ES_IPT];
-    uint32_t rk[ES_IPT], dg[ES_IPT];
+    uint64_t rk8[ES8_IPT];
+    uint32_t rk[ES8_IPT], dg[ES8_IPT];
     if (FIRST) {
-      uint32_t ru[ES_IPT], rw[ES_IPT];
-      float rs[ES_IPT];
+      uint32_t ru[ES8_IPT], rw[ES8_IPT];
+      float rs[ES8_IPT];
 #pragma unroll
-      for (int i = 0; i < ES_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      for (int i = 0; i < ES8_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
         const bool ok = q < tn;
         const uint64_t j = base + q;
         ru[i] = ok ? cu[j] : 0u;
@@ -462,20 +468,20 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__
         rs[i] = ok ? cs[j] : 0.0f;
       }
 #pragma unroll
-      for (int i = 0; i < ES_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      for (int i = 0; i < ES8_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
         rk8[i] = q < tn ? es_k8(gset, srank, ru[i], rw[i], rs[i], vb) : 0ull;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < ES_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+      for (int i = 0; i < ES8_IPT; ++i) {
+        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
         rk8[i] = q < tn ? in[base + q] : 0ull;
       }
     }
 #pragma unroll
-    for (int i = 0; i < ES_IPT; ++i) {
-      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+    for (int i = 0; i < ES8_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
       const bool ok = q < tn;
       dg[i] = (uint32_t)(rk8[i] >> shift) & 0xffu;
       const uint64_t peers = es_peers(dg[i], ok);
@@ -554,8 +560,8 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < ES_IPT; ++i) {
-      const uint32_t q = (uint32_t)(wv * ES_WCH + i * 64 + lane);
+    for (int i = 0; i < ES8_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
       if (q < tn) s_k[s_lofs[dg[i]] + s_wc[wv][dg[i]] + rk[i]] = rk8[i];
     }
     __syncthreads();

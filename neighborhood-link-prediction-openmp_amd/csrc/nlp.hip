@@ -1723,8 +1723,10 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   uint32_t* tick = hw + ES_MAXP * 256;
   uint32_t* err = tick + ES_MAXP;
   TRY(hipMemsetAsync(hw, 0, ((uint64_t)ES_MAXP * 256 + ES_MAXP + 4) * 4, st));
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  TRY(wsget(ws, B_ES_K0, n, &k0));
   hipLaunchKernelGGL(k_es_hist8, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
-                     cu, cw, cs, n, vb, (const uint32_t*)dset, (const uint16_t*)srank, hw);
+                     cu, cw, cs, n, vb, (const uint32_t*)dset, (const uint16_t*)srank, hw, k0);
   TRY(hipGetLastError());
   std::vector<uint32_t> h(8 * 256);
   TRY(hipMemcpyAsync(h.data(), hw, h.size() * 4, hipMemcpyDeviceToHost, st));
@@ -1736,26 +1738,23 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
     if (mx < n) run[P++] = p;
   }
   if (P == 0) run[P++] = 0;  // one record (or every key equal): one pass places it
-  if (bytes) *bytes += 4 * n + 12 * n + (P == 1 ? 24 * n : 20 * n + 16 * n * (uint64_t)(P - 2) + 20 * n);
-  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES_IPT - 1) / ((uint64_t)ES_NT * ES_IPT);
+  // scores (4 B), then columns in and keys out (20 B), then every pass 16 B (the last 8 in, 12 out)
+  if (bytes) *bytes += 4 * n + 20 * n + 16 * n * (uint64_t)(P - 1) + 20 * n;
+  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES8_IPT - 1) / ((uint64_t)ES_NT * ES8_IPT);
   uint64_t* desc;
   { nlp_status s = es_descs(g, ntiles, P, &desc, st); if (s != NLP_OK) return s; }
-  uint64_t *k0 = nullptr, *k1 = nullptr;
-  if (P > 1) TRY(wsget(ws, B_ES_K0, n, &k0));
-  if (P > 2) TRY(wsget(ws, B_ES_K1, n, &k1));
+  if (P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
   const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es8));
-  const uint64_t* src = nullptr;
+  const uint64_t* src = k0;  // k_es_hist8 wrote every key
   for (int r = 0; r < P; ++r) {
-    uint64_t* dst = (r & 1) ? k1 : k0;
+    uint64_t* dst = (r & 1) ? k0 : k1;
     const uint64_t ep = ++g->es_epoch;
     const uint32_t* gh = hw + run[r] * 256;
 #define NLP_ES8(F, L)                                                                                               \
   hipLaunchKernelGGL((k_es_pass8<F, L>), dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const uint32_t*)dset,            \
                      (const uint16_t*)srank, (const float*)rscore, src, dst, out, n, vb, 8 * run[r], gh, desc,        \
                      tick + r, ep, err)
-    if (P == 1) NLP_ES8(true, true);
-    else if (r == 0) NLP_ES8(true, false);
-    else if (r == P - 1) NLP_ES8(false, true);
+    if (r == P - 1) NLP_ES8(false, true);
     else NLP_ES8(false, false);
 #undef NLP_ES8
     TRY(hipGetLastError());
