@@ -354,149 +354,204 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
   }
 }
 
-// the rank of a record's score key (it is in the set)
-__device__ __forceinline__ uint64_t es_rank(const uint32_t* __restrict__ gset, const uint16_t* __restrict__ srank,
-                                            float s) {
-  const uint32_t x = score_key(s) + 1u;
-  uint32_t h = es_dhash(x, ES_DLOG);
-  for (uint32_t probe = 0; probe < ES_DCAP; ++probe) {
-    if (gset[h] == x) return srank[h];
-    h = (h + 1) & (ES_DCAP - 1);
-  }
-  return 0;  // unreachable: every key was inserted
-}
 
-__device__ __forceinline__ uint64_t es_k8(const uint32_t* __restrict__ gset, const uint16_t* __restrict__ srank,
-                                          uint32_t u, uint32_t w, float s, int vb) {
-  return es_rank(gset, srank, s) << (2 * vb) | (uint64_t)u << vb | w;
-}
+// The 8-byte passes split the keys into G ranges of tpw tiles (range g =
+// tiles [g tpw, (g + 1) tpw)), one workgroup per range, so that a pass needs no
+// look-back: a range's output offsets for digit d are the digit's global
+// offset plus the range counts of d in every earlier range, known before the
+// pass starts (k_es_off8).  The counts of pass r come from one read of its
+// input keys (k_es_cnt8); those of the first pass from k_es_hist8, which reads
+// every key anyway.  (Measured on the C4 order: the decoupled look-back of
+// k_es_pass took 0.6 of 1.28 ms per pass -- a chain of cross-XCD round trips;
+// a pass without it 0.68 ms.)
 
-// ghist[p * 256 + d]: records whose digit p of K8 is d; and every record's K8
-// written to `keys` (the passes then read 8-byte keys only: the rank lookup
-// is paid once)
+constexpr int ES8_IPT = 16;  // keys per thread: 8192-key tiles (64 KB of keys in LDS, two workgroups per CU)
+
+// Every record's K8 written to `keys` (the passes then read 8-byte keys only:
+// the rank lookup is paid once), and the first pass's counts: cnt[d * G + g]
+// = the records of range g whose low byte is d, ghist[d] their sum over the
+// ranges.  The score -> rank map is rebuilt per workgroup as an LDS hash of
+// the D <= ES_DMAX rank scores (rscore[r], rank order): a lookup is an LDS
+// probe, not a chain of dependent global loads.  Grid: G.
+constexpr int ES8_HLG = 13;  // LDS hash slots: 2 x ES_DMAX
 __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
                                                     const float* __restrict__ cs, uint64_t n, int vb,
-                                                    const uint32_t* __restrict__ gset,
-                                                    const uint16_t* __restrict__ srank, uint32_t* __restrict__ ghist,
-                                                    uint64_t* __restrict__ keys) {
-  __shared__ uint32_t h[8][256];
-  for (int i = threadIdx.x; i < 8 * 256; i += ES_NT) (&h[0][0])[i] = 0;
+                                                    const float* __restrict__ rscore, uint32_t D,
+                                                    uint32_t* __restrict__ ghist, uint64_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ cnt, uint32_t tpw, uint32_t G) {
+  __shared__ uint32_t h[ES_NT / 64][256];
+  __shared__ uint32_t s_hk[1 << ES8_HLG];  // score key + 1 (0: empty)
+  __shared__ uint16_t s_hr[1 << ES8_HLG];  // its rank
+  const int t = threadIdx.x, wv = wave_id();
+  for (int i = t; i < ES_NT / 64 * 256; i += ES_NT) (&h[0][0])[i] = 0;
+  for (int i = t; i < (1 << ES8_HLG); i += ES_NT) s_hk[i] = 0;
   __syncthreads();
+  for (uint32_t r = t; r < D; r += ES_NT) {
+    const uint32_t x = score_key(rscore[r]) + 1u;
+    uint32_t hh = es_dhash(x, ES8_HLG);
+    while (atomicCAS(&s_hk[hh], 0u, x) != 0u) hh = (hh + 1) & ((1u << ES8_HLG) - 1);  // keys distinct, load <= 1/2
+    s_hr[hh] = (uint16_t)r;
+  }
+  __syncthreads();
+  auto k8 = [&](uint32_t u, uint32_t w, float sc) {
+    const uint32_t x = score_key(sc) + 1u;
+    uint32_t hh = es_dhash(x, ES8_HLG);
+    while (s_hk[hh] != x) hh = (hh + 1) & ((1u << ES8_HLG) - 1);  // present: every score key has a rank
+    return (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)u << vb | w;
+  };
   constexpr int UN = 4;
-  const uint64_t stride = (uint64_t)gridDim.x * ES_NT * UN;
-  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT * UN; j0 < n; j0 += stride) {  // uniform per wave: ballots below
+  const uint64_t tile = (uint64_t)ES_NT * ES8_IPT;
+  const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
+  for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * UN) {
     uint32_t u[UN], w[UN];
     float s[UN];
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
-      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
-      const bool ok = j < n;
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
+      const bool ok = j < hi;
       u[q] = ok ? cu[j] : 0u;
       w[q] = ok ? cw[j] : 0u;
       s[q] = ok ? cs[j] : 0.0f;
     }
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
-      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
-      const bool ok = j < n;
-      const uint64_t k = ok ? es_k8(gset, srank, u[q], w[q], s[q], vb) : 0ull;
-      if (ok) keys[j] = k;
-#pragma unroll
-      for (int p = 0; p < 8; ++p) {
-        const uint32_t d = (uint32_t)(k >> (8 * p)) & 0xffu;
-        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-        if (__ballot(ok && d != d0) == 0) {  // one digit in the whole wave: one atomic
-          const uint64_t m = __ballot(ok);
-          if (m && lane_id() == 0) atomicAdd(&h[p][d0], (uint32_t)__popcll(m));
-        } else if (ok) {
-          atomicAdd(&h[p][d], 1u);
-        }
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
+      if (j < hi) {
+        const uint64_t k = k8(u[q], w[q], s[q]);
+        keys[j] = k;
+        atomicAdd(&h[wv][(uint32_t)k & 0xffu], 1u);
       }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 8 * 256; i += ES_NT) {
-    const uint32_t c = (&h[0][0])[i];
-    if (c) atomicAdd(&ghist[i], c);
+  if (t < 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < ES_NT / 64; ++w) c += h[w][t];
+    cnt[(uint64_t)t * G + blockIdx.x] = c;
+    if (c) atomicAdd(&ghist[t], c);
   }
 }
 
-// One pass over 8-byte keys.  FIRST: the input is the candidate columns (K8
-// built from them); LAST: the output is the caller's edges (the score of rank
-// r from rscore).  Same tiling, look-back and write-out as k_es_pass.
-constexpr int ES8_IPT = 16;  // keys per thread: 8192-key tiles (64 KB of keys in LDS, two workgroups per CU)
-template <bool FIRST, bool LAST>
-__global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cw,
-                                                    const float* __restrict__ cs, const uint32_t* __restrict__ gset,
-                                                    const uint16_t* __restrict__ srank,
-                                                    const float* __restrict__ rscore, const uint64_t* __restrict__ in,
-                                                    uint64_t* __restrict__ out, EdgeOut* __restrict__ eout, uint64_t n,
-                                                    int vb, int shift, const uint32_t* __restrict__ ghist,
-                                                    uint64_t* __restrict__ desc, uint32_t* __restrict__ ticket,
-                                                    uint64_t epoch, uint32_t* __restrict__ err) {
+// cnt[d * G + g]: the keys of range g whose digit (bits shift..) is d, ghist[d]
+// their sum over the ranges; ES8_CUN loads in flight per thread
+constexpr int ES8_CUN = 8;
+__global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ keys, uint64_t n, int shift,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ ghist,
+                                                   uint32_t tpw, uint32_t G) {
+  __shared__ uint32_t h[ES_NT / 64][256];
+  const int t = threadIdx.x, wv = wave_id();
+  for (int i = t; i < ES_NT / 64 * 256; i += ES_NT) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t tile = (uint64_t)ES_NT * ES8_IPT;
+  const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
+  for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * ES8_CUN) {
+    uint64_t k[ES8_CUN];
+#pragma unroll
+    for (int q = 0; q < ES8_CUN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
+      k[q] = j < hi ? keys[j] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < ES8_CUN; ++q)
+      if (j0 + (uint64_t)q * ES_NT + t < hi) atomicAdd(&h[wv][(uint32_t)(k[q] >> shift) & 0xffu], 1u);
+  }
+  __syncthreads();
+  if (t < 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < ES_NT / 64; ++w) c += h[w][t];
+    cnt[(uint64_t)t * G + blockIdx.x] = c;
+    if (c) atomicAdd(&ghist[t], c);
+  }
+}
+
+// off[d * G + g] = (records of digits below d) + (records of digit d in ranges
+// below g): grid 256 (one digit each), 1024 threads, G <= 1024
+constexpr int ES8_GMAX = 1024;
+__global__ __launch_bounds__(ES8_GMAX) void k_es_off8(const uint32_t* __restrict__ cnt,
+                                                      const uint32_t* __restrict__ ghist, uint32_t G,
+                                                      uint32_t* __restrict__ off) {
+  __shared__ uint32_t s_w[ES8_GMAX / 64];
+  __shared__ uint32_t s_base;
+  const uint32_t d = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  if (t < 64) {  // the digit's global offset: ghist[0 .. d)
+    uint32_t b = 0;
+    for (uint32_t e = t; e < d; e += 64) b += ghist[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if (t == 0) s_base = b;
+  }
+  const uint32_t c = t < G ? cnt[(uint64_t)d * G + t] : 0u;
+  uint32_t a = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(a, o, 64);
+    if ((int)lane >= o) a += y;
+  }
+  if (lane == 63) s_w[wv] = a;
+  __syncthreads();
+  uint32_t pre = s_base;
+  for (uint32_t w = 0; w < wv; ++w) pre += s_w[w];
+  if (t < G) off[(uint64_t)d * G + t] = pre + a - c;
+}
+
+// One pass over 8-byte keys (k_es_hist8 wrote them), one workgroup per range:
+// its tiles in order, each ranked in LDS (in-wave match over the digit's bits,
+// per-wave counters, a column scan), gathered in digit order and written to
+// the range's running offsets -- the output positions of a stable LSD pass.
+// LAST: the output is the caller's edges
+// (the score of rank r from rscore).  No workgroup waits on another.
+template <bool LAST>
+__global__ __launch_bounds__(ES_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
+    const float* __restrict__ rscore, const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
+    EdgeOut* __restrict__ eout, uint64_t n, int vb, int shift, const uint32_t* __restrict__ off, uint32_t tpw,
+    uint32_t G) {
   constexpr int NTH = ES_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
   __shared__ uint64_t s_k[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];
-  __shared__ uint64_t s_gofs[256];
-  __shared__ uint32_t s_lofs[256];
-  __shared__ uint32_t s_scan[8];
-  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_run[256];   // the range's next output position per digit
+  __shared__ uint32_t s_lofs[256];  // the tile's first LDS slot per digit
+  __shared__ uint32_t s_scan[4];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   const uint64_t ntiles = (n + ES_TILE - 1) / ES_TILE;
-  const uint64_t ep = epoch << 48;
+  const uint64_t tb = min(ntiles, (uint64_t)blockIdx.x * tpw), te = min(ntiles, tb + tpw);
   const uint64_t vmask = (1ull << vb) - 1ull;
-  while (true) {
-    if (t == 0) s_tile = atomicAdd(ticket, 1u);
+  if (t < 256) s_run[t] = off[(uint64_t)t * G + blockIdx.x];
+  uint64_t rk8[ES8_IPT];
+  auto load = [&](uint64_t tl) {
+    const uint64_t bs = tl * ES_TILE;
+    const uint32_t m = tl < te ? (uint32_t)min((uint64_t)ES_TILE, n - bs) : 0u;
+#pragma unroll
+    for (int i = 0; i < ES8_IPT; ++i) {
+      const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
+      rk8[i] = q < m ? in[bs + q] : 0ull;
+    }
+  };
+  load(tb);
+  for (uint64_t tile = tb; tile < te; ++tile) {
     for (int i = t; i < ES_NW * 256; i += NTH) (&s_wc[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t tile = s_tile;
-    if (tile >= ntiles) break;  // uniform: every wave leaves
-    const uint64_t base = tile * ES_TILE;
-    const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - base);
-    uint64_t rk8[ES8_IPT];
-    uint32_t rk[ES8_IPT], dg[ES8_IPT];
-    if (FIRST) {
-      uint32_t ru[ES8_IPT], rw[ES8_IPT];
-      float rs[ES8_IPT];
-#pragma unroll
-      for (int i = 0; i < ES8_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
-        const bool ok = q < tn;
-        const uint64_t j = base + q;
-        ru[i] = ok ? cu[j] : 0u;
-        rw[i] = ok ? cw[j] : 0u;
-        rs[i] = ok ? cs[j] : 0.0f;
-      }
-#pragma unroll
-      for (int i = 0; i < ES8_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
-        rk8[i] = q < tn ? es_k8(gset, srank, ru[i], rw[i], rs[i], vb) : 0ull;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < ES8_IPT; ++i) {
-        const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
-        rk8[i] = q < tn ? in[base + q] : 0ull;
-      }
-    }
+    const uint32_t tn = (uint32_t)min((uint64_t)ES_TILE, n - tile * ES_TILE);
+    uint32_t rd[ES8_IPT];  // in-wave rank << 8 | digit
 #pragma unroll
     for (int i = 0; i < ES8_IPT; ++i) {
       const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
       const bool ok = q < tn;
-      dg[i] = (uint32_t)(rk8[i] >> shift) & 0xffu;
-      const uint64_t peers = es_peers(dg[i], ok);
+      const uint32_t dg = (uint32_t)(rk8[i] >> shift) & 0xffu;
+      const uint64_t peers = es_peers(dg, ok);
       const uint64_t below = peers & ((1ull << lane) - 1ull);
-      rk[i] = ok ? s_wc[wv][dg[i]] + (uint32_t)__popcll(below) : 0u;
+      rd[i] = (ok ? s_wc[wv][dg] + (uint32_t)__popcll(below) : 0u) << 8 | dg;
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-      if (ok && below == 0) s_wc[wv][dg[i]] += (uint32_t)__popcll(peers);
+      if (ok && below == 0) s_wc[wv][dg] += (uint32_t)__popcll(peers);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     }
     __syncthreads();
-    uint32_t cnt = 0, gh = 0;
+    uint32_t cnt = 0;
     if (t < 256) {
 #pragma unroll
       for (int w = 0; w < ES_NW; ++w) {
@@ -504,75 +559,42 @@ __global__ __launch_bounds__(ES_NT) void k_es_pass8(const uint32_t* __restrict__
         s_wc[w][t] = cnt;
         cnt += c;
       }
-      gh = ghist[t];
-      es_publish(desc + tile * 256 + t, ep | (tile == 0 ? ES_PFX : ES_AGG) | (uint64_t)cnt);
     }
-    uint32_t lof = 0, gb = 0;
-    {
-      uint32_t a = cnt, b = gh;
+    {  // exclusive scan of the tile's digit counts (waves 0-3)
+      uint32_t a = cnt;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t ya = __shfl_up(a, o, 64), yb = __shfl_up(b, o, 64);
-        if (lane >= o) { a += ya; b += yb; }
+        const uint32_t y = __shfl_up(a, o, 64);
+        if (lane >= o) a += y;
       }
-      if (lane == 63 && wv < 4) { s_scan[wv] = a; s_scan[4 + wv] = b; }
+      if (lane == 63 && wv < 4) s_scan[wv] = a;
       __syncthreads();
-      uint32_t pa = 0, pb = 0;
-      for (int w = 0; w < wv && w < 4; ++w) { pa += s_scan[w]; pb += s_scan[4 + w]; }
-      lof = pa + a - cnt;
-      gb = pb + b - gh;
-    }
-    if (t < 256) {
-      uint64_t excl = 0;
-      if (tile > 0) {
-        int64_t j = (int64_t)tile - 1;
-        uint32_t spins = 0;
-        bool fin = false;
-        while (!fin) {
-          uint64_t x[ES_LBW];
-#pragma unroll
-          for (int r = 0; r < ES_LBW; ++r)
-            x[r] = j - r >= 0 ? es_load(desc + (uint64_t)(j - r) * 256 + t) : (ep | ES_PFX);
-          int used = 0;
-          bool blocked = false;
-#pragma unroll
-          for (int r = 0; r < ES_LBW; ++r) {
-            if (fin || blocked) continue;
-            const uint64_t st = (x[r] >> 48) == epoch ? (x[r] >> 46) & 3ull : 0ull;
-            if (st == 0) {
-              blocked = true;
-              continue;
-            }
-            excl += x[r] & ES_VAL;
-            ++used;
-            fin = st == 2;
-          }
-          j -= used;
-          if (!fin && used == 0) {
-            if (++spins > ES_SPIN_LIMIT) { atomicOr(err, 1u); break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        es_publish(desc + tile * 256 + t, ep | ES_PFX | (excl + cnt));
-      }
-      s_gofs[t] = (uint64_t)gb + excl;
-      s_lofs[t] = lof;
+      uint32_t pa = 0;
+      for (int w = 0; w < wv && w < 4; ++w) pa += s_scan[w];
+      if (t < 256) s_lofs[t] = pa + a - cnt;
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ES8_IPT; ++i) {
       const uint32_t q = (uint32_t)(wv * WCH + i * 64 + lane);
-      if (q < tn) s_k[s_lofs[dg[i]] + s_wc[wv][dg[i]] + rk[i]] = rk8[i];
+      const uint32_t dg = rd[i] & 0xffu;
+      if (q < tn) s_k[s_lofs[dg] + s_wc[wv][dg] + (rd[i] >> 8)] = rk8[i];
     }
     __syncthreads();
+    load(tile + 1);  // the next tile's keys, in flight through the write-out
+#pragma unroll 4
     for (uint32_t p = (uint32_t)t; p < tn; p += NTH) {
       const uint64_t k = s_k[p];
       const uint32_t d = (uint32_t)(k >> shift) & 0xffu;
-      const uint64_t pos = s_gofs[d] + (p - s_lofs[d]);
-      if (LAST) eout[pos] = EdgeOut{(uint32_t)((k >> vb) & vmask), (uint32_t)(k & vmask), rscore[k >> (2 * vb)]};
-      else out[pos] = k;
+      const uint64_t pos = (uint64_t)s_run[d] + (p - s_lofs[d]);
+      if (LAST) {
+        eout[pos] = EdgeOut{(uint32_t)((k >> vb) & vmask), (uint32_t)(k & vmask), rscore[k >> (2 * vb)]};
+      } else {
+        out[pos] = k;
+      }
     }
     __syncthreads();
+    if (t < 256) s_run[t] += cnt;
   }
 }
 

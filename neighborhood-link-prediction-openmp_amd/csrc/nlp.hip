@@ -78,6 +78,7 @@ enum Buf {
   B_HB_W, B_HB_PRE, B_HB_START, B_HH_ROWS, B_HH_PRE, B_HH_MAPS, B_HH_BCNT, B_HH_BOFF, B_HH_XS, B_HH_SPRE, B_HH_SITEM, B_HH_FP, B_HH_HEAVY, B_HH_GHIST, B_HH_PART, B_HP_SE, B_HP_SR, B_HP_SMASK, B_HP_BPOS,
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   B_ES_SET, B_ES_K0, B_ES_K1,            // edgesort.hpp 8-byte keys: distinct-key set + ranks + scores, key buffers
+  B_ES_CNT,                              // 8-byte keys: per-range digit counts + offsets
   NBUF
 };
 
@@ -904,7 +905,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
-    TRY(occ((const void*)k_es_pass8<false, false>, &g->occ_es8, ES_NT));
+    TRY(occ((const void*)k_es_pass8<false>, &g->occ_es8, ES_NT));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1679,13 +1680,12 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
   if (2 * vb > 63) return NLP_OK;
-  // [ES_DCAP] set, [4] counts, then the slot ranks (u16) and the rank scores (f32)
+  // [ES_DCAP] set, [4] counts, then the rank scores (f32)
   uint32_t* dset;
-  const uint64_t words = ES_DCAP + 4 + ES_DCAP / 2 + ES_DMAX;
+  const uint64_t words = ES_DCAP + 4 + ES_DMAX;
   TRY(wsget(ws, B_ES_SET, words, &dset));
   uint32_t* dcnt = dset + ES_DCAP;
-  uint16_t* srank = (uint16_t*)(dcnt + 4);
-  float* rscore = (float*)(dcnt + 4 + ES_DCAP / 2);
+  float* rscore = (float*)(dcnt + 4);
   TRY(hipMemsetAsync(dset, 0, (ES_DCAP + 4) * 4, st));
   hipLaunchKernelGGL(k_es_dkeys, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
                      cs, n, dset, dcnt);
@@ -1703,68 +1703,59 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   for (uint32_t k : keys)
     if (k == 0u || k == 0x80000000u) return NLP_OK;  // NaN / zero: several bit patterns behind one key
   const int rb = D > 1 ? bits_for(D - 1) : 0;
-  if (rb + 2 * vb > 64) return NLP_OK;
+  if (rb + 2 * vb > 64 || n >= (1ull << 32)) return NLP_OK;  // 32-bit range offsets
   std::sort(keys.begin(), keys.end(), std::greater<uint32_t>());  // rank 0 = the highest score
-  std::vector<uint16_t> hr(ES_DCAP, 0);
   std::vector<float> hsc(D);
   for (uint32_t r = 0; r < D; ++r) {
     const uint32_t k = keys[r];
     const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;  // score_key's inverse
     memcpy(&hsc[r], &b, 4);
   }
-  for (uint32_t i = 0; i < ES_DCAP; ++i)
-    if (hs[i]) hr[i] = (uint16_t)(std::lower_bound(keys.begin(), keys.end(), hs[i] - 1u, std::greater<uint32_t>()) -
-                                  keys.begin());
-  TRY(hipMemcpyAsync(srank, hr.data(), ES_DCAP * 2, hipMemcpyHostToDevice, st));
   TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
-  // every digit's histogram, one read; constant digits are passes not run
-  uint32_t* hw;
+  // the keys (and the first pass's range counts) in one read; P passes cover
+  // the rb + 2 vb key bits (every higher digit is zero)
+  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES8_IPT - 1) / ((uint64_t)ES_NT * ES8_IPT);
+  uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)g->occ_es8, (uint64_t)ES8_GMAX}));
+  const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
+  G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
+  const int P = std::max(1, (rb + 2 * vb + 7) / 8);
+  uint32_t* hw;  // [P][256] digit totals
   TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
-  uint32_t* tick = hw + ES_MAXP * 256;
-  uint32_t* err = tick + ES_MAXP;
-  TRY(hipMemsetAsync(hw, 0, ((uint64_t)ES_MAXP * 256 + ES_MAXP + 4) * 4, st));
+  TRY(hipMemsetAsync(hw, 0, (uint64_t)P * 256 * 4, st));
+  uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
+  TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+  uint32_t* offs = cnt + (uint64_t)256 * G;
   uint64_t *k0 = nullptr, *k1 = nullptr;
   TRY(wsget(ws, B_ES_K0, n, &k0));
-  hipLaunchKernelGGL(k_es_hist8, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
-                     cu, cw, cs, n, vb, (const uint32_t*)dset, (const uint16_t*)srank, hw, k0);
-  TRY(hipGetLastError());
-  std::vector<uint32_t> h(8 * 256);
-  TRY(hipMemcpyAsync(h.data(), hw, h.size() * 4, hipMemcpyDeviceToHost, st));
-  TRY(hipStreamSynchronize(st));
-  int run[8], P = 0;
-  for (int p = 0; p < 8; ++p) {
-    uint32_t mx = 0;
-    for (int d = 0; d < 256; ++d) mx = std::max(mx, h[(size_t)p * 256 + d]);
-    if (mx < n) run[P++] = p;
-  }
-  if (P == 0) run[P++] = 0;  // one record (or every key equal): one pass places it
-  // scores (4 B), then columns in and keys out (20 B), then every pass 16 B (the last 8 in, 12 out)
-  if (bytes) *bytes += 4 * n + 20 * n + 16 * n * (uint64_t)(P - 1) + 20 * n;
-  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES8_IPT - 1) / ((uint64_t)ES_NT * ES8_IPT);
-  uint64_t* desc;
-  { nlp_status s = es_descs(g, ntiles, P, &desc, st); if (s != NLP_OK) return s; }
   if (P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
-  const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntiles, g->occ_es8));
+  hipLaunchKernelGGL(k_es_hist8, dim3(G), dim3(ES_NT), 0, st, cu, cw, cs, n, vb, (const float*)rscore, D, hw, k0,
+                     cnt, tpw, G);
+  TRY(hipGetLastError());
+  // scores (4 B), columns in and keys out (20 B), every later pass's count
+  // read (8 B), every pass but the last 8 in and out, the last 8 in, 12 out
+  if (bytes) *bytes += 4 * n + 20 * n + 24 * n * (uint64_t)(P - 1) + 20 * n;
   const uint64_t* src = k0;  // k_es_hist8 wrote every key
   for (int r = 0; r < P; ++r) {
     uint64_t* dst = (r & 1) ? k0 : k1;
-    const uint64_t ep = ++g->es_epoch;
-    const uint32_t* gh = hw + run[r] * 256;
-#define NLP_ES8(F, L)                                                                                               \
-  hipLaunchKernelGGL((k_es_pass8<F, L>), dim3(gr), dim3(ES_NT), 0, st, cu, cw, cs, (const uint32_t*)dset,            \
-                     (const uint16_t*)srank, (const float*)rscore, src, dst, out, n, vb, 8 * run[r], gh, desc,        \
-                     tick + r, ep, err)
-    if (r == P - 1) NLP_ES8(false, true);
-    else NLP_ES8(false, false);
-#undef NLP_ES8
+    if (r > 0) {  // this pass's range counts: one read of its input
+      hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, 8 * r, cnt, hw + r * 256, tpw, G);
+      TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_es_off8, dim3(256), dim3(ES8_GMAX), 0, st, (const uint32_t*)cnt,
+                       (const uint32_t*)(hw + r * 256), G, offs);
+    TRY(hipGetLastError());
+    const bool last = r == P - 1;
+    if (last)
+      hipLaunchKernelGGL(k_es_pass8<true>, dim3(G), dim3(ES_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
+                         8 * r, (const uint32_t*)offs, tpw, G);
+    else
+      hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
+                         8 * r, (const uint32_t*)offs, tpw, G);
     TRY(hipGetLastError());
     src = dst;
   }
-  uint32_t herr = 0;
-  TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-  TRY(hipStreamSynchronize(st));
   *done = true;
-  return herr ? NLP_ERR_DEVICE : NLP_OK;  // a look-back gave up (never expected)
+  return NLP_OK;
 }
 
 nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
