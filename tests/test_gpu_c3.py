@@ -1,9 +1,10 @@
 """BASELINE configs[2] / SURVEY §8(d) C3: the uk-2005-shaped stand-in
 (n = 39.5 M, M = 1.7e9) -- the "HBM-roofline run".  LHub Adamic-Adar (the
-config's metric) and Jaccard at H = 4 (path 1) and H = 16 (Jaccard on path 4,
-the hash accumulation, Adamic-Adar too: ordered accumulation in the row
-kernels, sort-mode items in the hub pass -- k = 8.7e7 of 9.6e8 candidates),
-exact against the parallel oracle, order included."""
+config's metric) and Jaccard at H = 4 (path 1), Adamic-Adar at H = 16 (path 4:
+ordered accumulation in the row kernels, sort-mode items in the hub pass --
+k = 8.7e7 of 9.6e8 candidates), exact against the parallel oracle, order
+included, and against the reference itself.  (Jaccard at H = 16 on path 4 is
+the C4 tests' call.)"""
 import numpy as np
 import pytest
 
@@ -46,12 +47,6 @@ def test_gpu_c3_adamic_adar_h4(c3, oracle):
 @pytest.mark.timeout(300)
 def test_gpu_c3_jaccard_h4(c3, oracle):
     _check(c3, oracle, 1, 4, path=1)
-
-
-@pytest.mark.timeout(300)
-def test_gpu_c3_jaccard_h16_hash_path(c3, oracle):
-    n, t = _check(c3, oracle, 1, 16, path=4)
-    assert n == c3.k and t["chunks"] >= 1
 
 
 @pytest.mark.timeout(300)

@@ -8,6 +8,7 @@ import os
 import numpy as np
 import pytest
 
+from bigconf import ORACLE_THREADS
 from parity import (assert_canonical_equal, assert_canonical_order, assert_same_candidates,
                     assert_topk_matches_reference, f1_score)
 
@@ -272,6 +273,9 @@ def test_gpu_oversized_bucket_falls_back(gpu, oracle, grouping):
         del os.environ["NLP_GROUPING"]
 
 
+_GROUPING_DEFAULT = {}
+
+
 @pytest.mark.parametrize("other", ["bucket", "lsd", "fused"])
 def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
     """The sync-free groupings (wedge records: MSD buckets / full LSD sort;
@@ -279,8 +283,10 @@ def test_gpu_sort_grouping_equals_bucket_grouping(gpu, oracle, other):
     (sort groupings only)."""
     off, keys = random_csr(8000, 14, 7)
     k = 3000
-    with gpu.Graph(off, keys) as Gs:
-        res = {(m, H): Gs.predict(m, H, k) for m in range(9) for H in (0, 1, 2, 4, 16)}
+    if "res" not in _GROUPING_DEFAULT:  # the default grouping's results, shared by the parametrisations
+        with gpu.Graph(off, keys) as Gs:
+            _GROUPING_DEFAULT["res"] = {(m, H): Gs.predict(m, H, k) for m in range(9) for H in (0, 1, 2, 4, 16)}
+    res = _GROUPING_DEFAULT["res"]
     env = ("NLP_BUCKET_FUSED", "1") if other == "fused" else ("NLP_GROUPING", other)
     try:
         os.environ[env[0]] = env[1]
@@ -555,7 +561,7 @@ def test_gpu_full_size_c2_large_hub_threshold(gpu, oracle, nlp):
     keys = keys_t.cpu().numpy().view(np.uint32)
     k = info["k"]
     out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
-    ref = {m: oracle.predict(off, keys, m, 16, max_edges=k) for m in (1, 7)}
+    ref = {m: oracle.predict_par(off, keys, m, 16, max_edges=k, threads=ORACLE_THREADS) for m in (1, 7)}
     for env, cases in ((dict(), ((1, 4), (7, 4))), (dict(NLP_HASH_AA="0"), ((7, 1),))):
         with _env(**env):
             with gpu.Graph.from_device(off_t, keys_t) as G:
@@ -847,7 +853,7 @@ def test_gpu_survivor_scan_after_other_survivor_set(gpu, oracle):
     with gpu.Graph(off, keys) as G:
         for m, H in ((7, 4), (1, 0), (7, 8), (1, 2048), (0, 0), (8, 3), (1, 0)):
             u, w, s, t = G.predict(m, H, k)
-            eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k)
+            eu, ew, es, info = oracle.predict_par(off, keys, m, H, max_edges=k, threads=ORACLE_THREADS)
             assert_canonical_equal(eu, ew, es, u, w, s)
             assert t["wedges"] == info["wedges_gt"]
 
