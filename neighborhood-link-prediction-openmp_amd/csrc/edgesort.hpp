@@ -365,7 +365,9 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
 // k_es_pass took 0.6 of 1.28 ms per pass -- a chain of cross-XCD round trips;
 // a pass without it 0.68 ms.)
 
-constexpr int ES8_IPT = 16;  // keys per thread: 8192-key tiles (64 KB of keys in LDS, two workgroups per CU)
+constexpr int ES8_IPT = 16;  // keys per thread of k_es_pass8
+constexpr int ES8_NT = 256;  // its threads: 4096-key tiles (32 KB of keys in LDS, four workgroups per CU)
+constexpr uint64_t ES8_TILE = (uint64_t)ES8_NT * ES8_IPT;
 
 // Every record's K8 written to `keys` (the passes then read 8-byte keys only:
 // the rank lookup is paid once), and the first pass's counts: cnt[d * G + g]
@@ -400,7 +402,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
     return (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)u << vb | w;
   };
   constexpr int UN = 4;
-  const uint64_t tile = (uint64_t)ES_NT * ES8_IPT;
+  const uint64_t tile = ES8_TILE;
   const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
   for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * UN) {
     uint32_t u[UN], w[UN];
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ 
   const int t = threadIdx.x, wv = wave_id();
   for (int i = t; i < ES_NT / 64 * 256; i += ES_NT) (&h[0][0])[i] = 0;
   __syncthreads();
-  const uint64_t tile = (uint64_t)ES_NT * ES8_IPT;
+  const uint64_t tile = ES8_TILE;
   const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
   for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * ES8_CUN) {
     uint64_t k[ES8_CUN];
@@ -503,11 +505,11 @@ __global__ __launch_bounds__(ES8_GMAX) void k_es_off8(const uint32_t* __restrict
 // LAST: the output is the caller's edges
 // (the score of rank r from rscore).  No workgroup waits on another.
 template <bool LAST>
-__global__ __launch_bounds__(ES_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
+__global__ __launch_bounds__(ES8_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
     const float* __restrict__ rscore, const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
     EdgeOut* __restrict__ eout, uint64_t n, int vb, int shift, const uint32_t* __restrict__ off, uint32_t tpw,
     uint32_t G) {
-  constexpr int NTH = ES_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
+  constexpr int NTH = ES8_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
   __shared__ uint64_t s_k[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];
   __shared__ uint32_t s_run[256];   // the range's next output position per digit

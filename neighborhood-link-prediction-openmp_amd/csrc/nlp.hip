@@ -905,7 +905,7 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(occ((const void*)k_sp_expand<true>, &g->occ_exp));
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
-    TRY(occ((const void*)k_es_pass8<false>, &g->occ_es8, ES_NT));
+    TRY(occ((const void*)k_es_pass8<false>, &g->occ_es8, ES8_NT));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1714,7 +1714,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
   // the keys (and the first pass's range counts) in one read; P passes cover
   // the rb + 2 vb key bits (every higher digit is zero)
-  const uint64_t ntiles = (n + (uint64_t)ES_NT * ES8_IPT - 1) / ((uint64_t)ES_NT * ES8_IPT);
+  const uint64_t ntiles = (n + ES8_TILE - 1) / ES8_TILE;
   uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)g->occ_es8, (uint64_t)ES8_GMAX}));
   const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
   G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
@@ -1746,10 +1746,10 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
     TRY(hipGetLastError());
     const bool last = r == P - 1;
     if (last)
-      hipLaunchKernelGGL(k_es_pass8<true>, dim3(G), dim3(ES_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
+      hipLaunchKernelGGL(k_es_pass8<true>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
                          8 * r, (const uint32_t*)offs, tpw, G);
     else
-      hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
+      hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
                          8 * r, (const uint32_t*)offs, tpw, G);
     TRY(hipGetLastError());
     src = dst;
