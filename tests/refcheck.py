@@ -17,6 +17,10 @@ The reference's tie order depends on its OpenMP schedule (predict.hxx:287,
   4. F1 (main.cxx:48-57, 199-206) of both lies within the tie bounds: the
      r = k - |above| boundary links chosen from the tie set T to minimise /
      maximise the matches with the deletions.
+and, for OUR output only (the canonical contract of this library, which the
+parallel oracle restates): the r boundary links are the r smallest (u, w) of
+the reference's tie set, and the list is in canonical order (score key desc,
+u asc, w asc) -- together with 1-2, the output is the oracle's bit for bit.
 """
 import json
 import os
@@ -129,6 +133,11 @@ def check_contract(gpu, ref_k, ref_ge, k, del_u, del_w, dev="cuda"):
     assert bool(torch.isin(gt, T).all()), "tie links outside the reference's tie set"
     assert bool(torch.isin(rt, T).all()), "the reference's own ties outside its tie set"
     assert torch.unique(pk(gu, gw)).numel() == n, "duplicate links in the output"
+    # canonical: the boundary links are the smallest (u, w) of T, the list in canonical order
+    assert torch.equal(torch.sort(gt).values, T[:gt.numel()]), "boundary links are not the first ties in (u, w) order"
+    if n > 1:
+        dk, dp = gk[1:] - gk[:-1], pk(gu, gw)[1:] - pk(gu, gw)[:-1]
+        assert bool(((dk < 0) | ((dk == 0) & (dp > 0))).all()), "output not in canonical order"
     # F1 (main.cxx:48-57): both directions of every link against the directed deletions
     D = torch.sort(pk(_t(del_u, dev).long() & 0xffffffff, _t(del_w, dev).long() & 0xffffffff)).values
 
@@ -184,7 +193,7 @@ def run_reference_check(c, csr, metric, H, name):
     ref_k = ref_predict(csr, metric, H, c.k)
     ref_ge = ref_predict(csr, metric, H, n_ge)
     res = check_contract(gpu, ref_k, ref_ge, c.k, c.del_u, c.del_w)
-    res.update(config=name, metric=metric, H=H, candidates=int(t["candidates"]), path=t["path"],
+    res.update(config=name, metric=metric, H=H, candidates=int(t["candidates"]), wedges=int(t["wedges"]), path=t["path"],
                ref_threads=REF_THREADS, ref_time_ms=ref_k[3]["time_ms"], ref_ge_time_ms=ref_ge[3]["time_ms"],
                gpu_ms=t["total_ms"])
     rd = os.environ.get("NLP_TEST_REPORT_DIR")

@@ -848,8 +848,8 @@ def test_gpu_survivor_scan_after_other_survivor_set(gpu, oracle):
     H > 1024).  A graph of > 32768 vertices (several survivor tiles), an
     Adamic-Adar call (ordered survivor scan, other survivor set) first, then
     count-metric calls without the index on the same handle, each exact."""
-    off, keys = random_csr(100000, 6, 11)
-    k = 20000
+    off, keys = random_csr(40000, 6, 11)
+    k = 8000
     with gpu.Graph(off, keys) as G:
         for m, H in ((7, 4), (1, 0), (7, 8), (1, 2048), (0, 0), (8, 3), (1, 0)):
             u, w, s, t = G.predict(m, H, k)
