@@ -301,8 +301,11 @@ constexpr uint64_t ES8_MIN = 1ull << 16;  // smaller calls keep the 12-byte sort
 __device__ __forceinline__ uint32_t es_dhash(uint32_t x, int lg) { return (x * 0x9E3779B1u) >> (32 - lg); }
 
 // gcnt[0]: distinct keys in the global set; gcnt[1]: overflow (the caller keeps the 12-byte sort)
+// ckey != nullptr: the keys are read from ckey and only those >= kmin count
+// (the final order of the kept candidates straight from the unpruned buffer)
 __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs, uint64_t n, uint32_t* __restrict__ gset,
-                                                    uint32_t* __restrict__ gcnt) {
+                                                    uint32_t* __restrict__ gcnt, const uint32_t* __restrict__ ckey,
+                                                    uint32_t kmin) {
   __shared__ uint32_t s_set[ES_LCAP];
   __shared__ uint32_t s_n, s_over;
   for (int i = threadIdx.x; i < (int)ES_LCAP; i += ES_NT) s_set[i] = 0;
@@ -311,7 +314,9 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
   constexpr int LLG = 12;  // log2 ES_LCAP
   const uint64_t stride = (uint64_t)gridDim.x * ES_NT;
   for (uint64_t j = (uint64_t)blockIdx.x * ES_NT + threadIdx.x; j < n; j += stride) {
-    const uint32_t x = score_key(cs[j]) + 1u;
+    const uint32_t key = ckey ? ckey[j] : score_key(cs[j]);
+    if (ckey && key < kmin) continue;
+    const uint32_t x = key + 1u;
     uint32_t h = es_dhash(x, LLG);
     for (uint32_t probe = 0; probe < ES_LCAP; ++probe) {
       const uint32_t cur = s_set[h];  // a plain read: the common case, the key is already in
@@ -435,6 +440,65 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
   }
 }
 
+// The kept candidates (key >= kmin) of an unpruned buffer as K8 keys,
+// compacted in any order (the sort orders them): one reservation per
+// workgroup and 4096 candidates.  The score -> rank map as in k_es_hist8.
+__global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cu,
+                                                    const uint32_t* __restrict__ cw, uint64_t n, uint32_t kmin, int vb,
+                                                    const float* __restrict__ rscore, uint32_t D,
+                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ count) {
+  __shared__ uint32_t s_hk[1 << ES8_HLG];
+  __shared__ uint16_t s_hr[1 << ES8_HLG];
+  __shared__ uint32_t s_wn[ES_NT / 64];
+  __shared__ unsigned long long s_base;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  for (int i = t; i < (1 << ES8_HLG); i += ES_NT) s_hk[i] = 0;
+  __syncthreads();
+  for (uint32_t r = t; r < D; r += ES_NT) {
+    const uint32_t x = score_key(rscore[r]) + 1u;
+    uint32_t hh = es_dhash(x, ES8_HLG);
+    while (atomicCAS(&s_hk[hh], 0u, x) != 0u) hh = (hh + 1) & ((1u << ES8_HLG) - 1);
+    s_hr[hh] = (uint16_t)r;
+  }
+  __syncthreads();
+  constexpr int UN = 8;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT * UN; j0 < n; j0 += (uint64_t)gridDim.x * ES_NT * UN) {
+    uint32_t x[UN];
+    bool kp[UN];
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
+      x[q] = j < n ? ckey[j] : 0u;
+      kp[q] = j < n && x[q] >= kmin;
+      c += (uint32_t)__popcll(__ballot(kp[q]));
+    }
+    if (lane == 0) s_wn[wv] = c;
+    __syncthreads();
+    if (t == 0) {
+      uint32_t tot = 0;
+      for (int w = 0; w < ES_NT / 64; ++w) tot += s_wn[w];
+      s_base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    uint64_t pos = s_base;
+    for (int w = 0; w < wv; ++w) pos += s_wn[w];
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t m = __ballot(kp[q]);
+      if (kp[q]) {
+        const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
+        uint32_t hh = es_dhash(x[q] + 1u, ES8_HLG);
+        while (s_hk[hh] != x[q] + 1u) hh = (hh + 1) & ((1u << ES8_HLG) - 1);  // present: every kept key has a rank
+        keys[pos + (uint64_t)__popcll(m & lt)] = (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)cu[j] << vb | cw[j];
+      }
+      pos += (uint64_t)__popcll(m);
+    }
+    __syncthreads();  // s_wn / s_base are rewritten by the next block
+  }
+}
+
 // cnt[d * G + g]: the keys of range g whose digit (bits shift..) is d, ghist[d]
 // their sum over the ranges; ES8_CUN loads in flight per thread
 constexpr int ES8_CUN = 8;
@@ -502,13 +566,13 @@ __global__ __launch_bounds__(ES8_GMAX) void k_es_off8(const uint32_t* __restrict
 // its tiles in order, each ranked in LDS (in-wave match over the digit's bits,
 // per-wave counters, a column scan), gathered in digit order and written to
 // the range's running offsets -- the output positions of a stable LSD pass.
-// LAST: the output is the caller's edges
-// (the score of rank r from rscore).  No workgroup waits on another.
+// LAST: the output is the caller's edges (the score of rank r from rscore),
+// the first nout of them.  No workgroup waits on another.
 template <bool LAST>
 __global__ __launch_bounds__(ES8_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
     const float* __restrict__ rscore, const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
     EdgeOut* __restrict__ eout, uint64_t n, int vb, int shift, const uint32_t* __restrict__ off, uint32_t tpw,
-    uint32_t G) {
+    uint32_t G, uint64_t nout) {
   constexpr int NTH = ES8_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
   __shared__ uint64_t s_k[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];
@@ -590,7 +654,8 @@ __global__ __launch_bounds__(ES8_NT) __attribute__((amdgpu_waves_per_eu(4))) voi
       const uint32_t d = (uint32_t)(k >> shift) & 0xffu;
       const uint64_t pos = (uint64_t)s_run[d] + (p - s_lofs[d]);
       if (LAST) {
-        eout[pos] = EdgeOut{(uint32_t)((k >> vb) & vmask), (uint32_t)(k & vmask), rscore[k >> (2 * vb)]};
+        if (pos < nout)  // the first nout in canonical order (the rest: ties beyond the quota)
+          eout[pos] = EdgeOut{(uint32_t)((k >> vb) & vmask), (uint32_t)(k & vmask), rscore[k >> (2 * vb)]};
       } else {
         out[pos] = k;
       }

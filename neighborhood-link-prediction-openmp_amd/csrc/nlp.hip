@@ -971,6 +971,10 @@ struct Cands {
   uint64_t hot_bytes = 0;  // and their algorithmic bytes (counted by the kernel, HPC_HOTB)
   uint32_t hot_launches = 0;
   uint64_t call_bytes = 0; // DESIGN.md §5 model of the bytes of all the call's kernels (path 4)
+  // path 4, final prune folded into the order: the n held are unpruned, the
+  // order keeps the keys >= kmin and writes the first `keep` (0: pruned)
+  uint64_t keep = 0, cap = 0;
+  uint32_t kmin = 0;
 };
 
 // Group the W wedges of one generator pass, score them and append the
@@ -1553,7 +1557,13 @@ nlp_status hp_alloc_scratch(nlp_graph* g) {
 // Prune the (unordered) candidate buffer to the canonical top k:
 // radix-select the k-th key, keep every key above it and the first ties in
 // (u, w) order.  Returns the k-th key in *kth.
-nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* kth, hipStream_t st) {
+// fuse (the call's last prune): when the keys at or above the k-th are few
+// beyond k (the tie set small) and the 8-byte order may take them, nothing is
+// split -- C.keep / C.kmin hand the unpruned buffer to hp_final_order, which
+// sorts the keys >= kmin and writes the first k (the canonical tie rule is the
+// sort order).
+nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* kth, hipStream_t st,
+                    bool fuse = false) {
   Workspace& ws = g->ws;
   const uint64_t n = C.n;
   uint32_t *ckey = (uint32_t*)ws.p[B_CKEY], *cu = (uint32_t*)ws.p[B_CU], *cw = (uint32_t*)ws.p[B_CW];
@@ -1577,6 +1587,19 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
     LAUNCH(k_sel_hist, n, st, ckey, small + 32, pass, sel, selhist);
     hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(NT), 0, st, selhist, pass, sel);
     TRY(hipGetLastError());
+  }
+  if (fuse && g->es_k8 == 1 && n >= ES8_MIN && n < (1ull << 32)) {
+    TRY(hipMemcpyAsync(&h[16], sel, 40, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    const uint64_t above = h[18], key = h[19], ties = h[20];
+    if (key > 0 && above < k && above + ties >= k && above + ties <= k + std::max<uint64_t>(k / 16, 1ull << 16)) {
+      *kth = (uint32_t)key;
+      C.keep = k;
+      C.kmin = (uint32_t)key;
+      C.cap = cap;
+      C.call_bytes += 12 * n;  // three select histograms
+      return NLP_OK;
+    }
   }
   uint32_t *nk, *nu, *nw, *ti0, *ti1;
   float* ns;
@@ -1674,8 +1697,13 @@ nlp_status es_descs(nlp_graph* g, uint64_t ntiles, int P, uint64_t** desc, hipSt
 // es_sort over rank-compressed 8-byte keys (edgesort.hpp k_es_dkeys, k_es_hist8,
 // k_es_pass8).  *done = false when the call does not qualify (too many distinct
 // score keys, a NaN or zero score, too many key bits): nothing was written.
+// ckey != nullptr: the input is an UNPRUNED buffer of n candidates whose score
+// keys are ckey; only those >= kmin are sorted, and the first nout of them (in
+// canonical order) are written -- the prune's split and tie selection folded
+// into the sort (the canonical tie rule is the sort order itself).
 nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
-                    hipStream_t st, uint64_t* bytes, bool* done) {
+                    hipStream_t st, uint64_t* bytes, bool* done, const uint32_t* ckey = nullptr, uint32_t kmin = 0,
+                    uint64_t nout = UINT64_MAX) {
   *done = false;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
@@ -1688,7 +1716,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   float* rscore = (float*)(dcnt + 4);
   TRY(hipMemsetAsync(dset, 0, (ES_DCAP + 4) * 4, st));
   hipLaunchKernelGGL(k_es_dkeys, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
-                     cs, n, dset, dcnt);
+                     cs, n, dset, dcnt, ckey, kmin);
   TRY(hipGetLastError());
   std::vector<uint32_t> hs(ES_DCAP + 4);
   TRY(hipMemcpyAsync(hs.data(), dset, (ES_DCAP + 4) * 4, hipMemcpyDeviceToHost, st));
@@ -1704,6 +1732,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
     if (k == 0u || k == 0x80000000u) return NLP_OK;  // NaN / zero: several bit patterns behind one key
   const int rb = D > 1 ? bits_for(D - 1) : 0;
   if (rb + 2 * vb > 64 || n >= (1ull << 32)) return NLP_OK;  // 32-bit range offsets
+  const uint64_t n_in = n;
   std::sort(keys.begin(), keys.end(), std::greater<uint32_t>());  // rank 0 = the highest score
   std::vector<float> hsc(D);
   for (uint32_t r = 0; r < D; ++r) {
@@ -1712,6 +1741,19 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
     memcpy(&hsc[r], &b, 4);
   }
   TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  if (ckey) {  // the kept candidates' keys, compacted: the sort's n is their count
+    TRY(wsget(ws, B_ES_K0, n, &k0));
+    unsigned long long* kc = (unsigned long long*)(dcnt + 2);  // zeroed with the set
+    hipLaunchKernelGGL(k_es_keep8, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)),
+                       dim3(ES_NT), 0, st, ckey, cu, cw, n, kmin, vb, (const float*)rscore, D, k0, kc);
+    TRY(hipGetLastError());
+    unsigned long long kept = 0;
+    TRY(hipMemcpyAsync(&kept, kc, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (kept < std::min<uint64_t>(nout, n) || kept > n) return NLP_ERR_DEVICE;
+    n = kept;
+  }
   // the keys (and the first pass's range counts) in one read; P passes cover
   // the rb + 2 vb key bits (every higher digit is zero)
   const uint64_t ntiles = (n + ES8_TILE - 1) / ES8_TILE;
@@ -1725,15 +1767,22 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
   TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
   uint32_t* offs = cnt + (uint64_t)256 * G;
-  uint64_t *k0 = nullptr, *k1 = nullptr;
-  TRY(wsget(ws, B_ES_K0, n, &k0));
+  if (!ckey) TRY(wsget(ws, B_ES_K0, n, &k0));
   if (P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
-  hipLaunchKernelGGL(k_es_hist8, dim3(G), dim3(ES_NT), 0, st, cu, cw, cs, n, vb, (const float*)rscore, D, hw, k0,
-                     cnt, tpw, G);
+  if (ckey) {
+    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, (const uint64_t*)k0, n, 0, cnt, hw, tpw, G);
+  } else {
+    hipLaunchKernelGGL(k_es_hist8, dim3(G), dim3(ES_NT), 0, st, cu, cw, cs, n, vb, (const float*)rscore, D, hw, k0,
+                       cnt, tpw, G);
+  }
   TRY(hipGetLastError());
   // scores (4 B), columns in and keys out (20 B), every later pass's count
-  // read (8 B), every pass but the last 8 in and out, the last 8 in, 12 out
-  if (bytes) *bytes += 4 * n + 20 * n + 24 * n * (uint64_t)(P - 1) + 20 * n;
+  // read (8 B), every pass but the last 8 in and out, the last 8 in, 12 out;
+  // filtered: keys of every candidate (8 B), the kept ones' columns (8 B) and
+  // keys out (8 B), the first pass's count read (8 B)
+  const uint64_t nw = std::min<uint64_t>(nout, n);
+  if (bytes)
+    *bytes += (ckey ? 8 * n_in + 24 * n : 24 * n) + 24 * n * (uint64_t)(P - 1) + 8 * n + 12 * nw;
   const uint64_t* src = k0;  // k_es_hist8 wrote every key
   for (int r = 0; r < P; ++r) {
     uint64_t* dst = (r & 1) ? k0 : k1;
@@ -1747,10 +1796,10 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
     const bool last = r == P - 1;
     if (last)
       hipLaunchKernelGGL(k_es_pass8<true>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
-                         8 * r, (const uint32_t*)offs, tpw, G);
+                         8 * r, (const uint32_t*)offs, tpw, G, nw);
     else
       hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
-                         8 * r, (const uint32_t*)offs, tpw, G);
+                         8 * r, (const uint32_t*)offs, tpw, G, nw);
     TRY(hipGetLastError());
     src = dst;
   }
@@ -1820,6 +1869,22 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
 
 nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   if (C.n == 0) return NLP_OK;
+  if (C.keep) {  // the last prune folded into the 8-byte order
+    bool done = false;
+    Workspace& ws = g->ws;
+    nlp_status s = es_sort8(g, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], C.n,
+                            d_out, st, &C.call_bytes, &done, (const uint32_t*)ws.p[B_CKEY], C.kmin, C.keep);
+    if (s != NLP_OK) return s;
+    const uint64_t keep = C.keep;
+    C.keep = 0;
+    if (done) {
+      C.n = keep;
+      return NLP_OK;
+    }
+    uint32_t kth = 0;  // the keys do not qualify (too many distinct scores, ...): prune, then order
+    s = hp_prune(g, C, keep, C.cap, &kth, st);
+    if (s != NLP_OK) return s;
+  }
   return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
                  d_out, st, &C.call_bytes);
 }
@@ -2200,12 +2265,12 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   // the canonical top k, and tau = the k-th key from then on; with fewer, only
   // the padding goes (it ranks below every real candidate: key 0, u and w
   // 0xffffffff), and no threshold is set.
-  auto prune_held = [&]() -> nlp_status {
+  auto prune_held = [&](bool last) -> nlp_status {
     const uint64_t real = C.n - C.pad;
     uint32_t kth = 0;
     if (real >= k) {
       if (C.n > k) {
-        nlp_status s = hp_prune(g, C, k, capC, &kth, st);
+        nlp_status s = hp_prune(g, C, k, capC, &kth, st, last);
         if (s != NLP_OK) return s;
       }
       C.pad = 0;
@@ -2419,7 +2484,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       rate = std::max(rate, (double)emitted / (double)std::max<uint64_t>(wchunk, 1));
       target = std::max<uint64_t>(1, wchunk / 4);
       if (C.n > k || C.pad) {
-        nlp_status s = prune_held();
+        nlp_status s = prune_held(false);
         if (s != NLP_OK) return s;
       } else if (r1 == r0 + 1) {
         return NLP_ERR_DEVICE;  // one row cannot exceed E >= S free slots
@@ -2446,7 +2511,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     r0 = r1;
     for (int b = 0; b < HP_NBINS; ++b) q0[b] = q1[b];
     if ((C.n > k && C.n > k + E / 2) || (r0 >= nU && (C.n > k || C.pad))) {
-      nlp_status s = prune_held();
+      nlp_status s = prune_held(r0 >= nU);
       if (s != NLP_OK) return s;
     }
     // next chunk: aim at half of the free buffer at the last emission rate, and
@@ -3671,9 +3736,10 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (s != NLP_OK) return s;
   }
   uint64_t total = C.total, nan = C.nan;
-  nlp_status s = prune_to(g, C, p.max_edges, st);
+  // path 4 may leave its last prune to the order (C.keep: hp_final_order)
+  nlp_status s = C.keep ? NLP_OK : prune_to(g, C, p.max_edges, st);
   if (s != NLP_OK) return s;
-  if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.n, 1), &d_out));
+  if (!d_out) TRY(wsget(g->ws, B_EDGES, std::max<uint64_t>(C.keep ? C.keep : C.n, 1), &d_out));
   s = path == 4 ? hp_final_order(g, C, d_out, st) : order_v1(g, C, d_out, st);
   if (s != NLP_OK) return s;
   TRY(hipEventRecord(g->ev[2], st));

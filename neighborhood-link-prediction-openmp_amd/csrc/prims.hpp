@@ -279,7 +279,8 @@ inline hipError_t sort_pairs_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint3
 // ---------------------------------------------------------------- radix select (k-th largest u32)
 // State in device memory: sel[0] = prefix (high bits fixed so far), sel[1] = remaining
 // rank (1-based among keys matching the prefix), sel[2] = count strictly above
-// the final key, sel[3] = the final key.  Digits: 12, 12, 8 bits from the top.
+// the final key, sel[3] = the final key, sel[4] = the keys equal to it.
+// Digits: 12, 12, 8 bits from the top.
 constexpr int SEL_BINS = 4096;
 
 __global__ __launch_bounds__(NT) void k_sel_hist(const uint32_t* __restrict__ keys, const uint64_t* __restrict__ d_n,
@@ -343,7 +344,10 @@ __global__ __launch_bounds__(NT) void k_sel_pick(uint32_t* __restrict__ ghist, i
     sel[0] = (sel[0] << (pass == 2 ? 8 : 12)) | (uint64_t)d;
     sel[1] = rem;
     sel[2] = above;
-    if (pass == 2) sel[3] = sel[0] & 0xffffffffull;
+    if (pass == 2) {
+      sel[3] = sel[0] & 0xffffffffull;
+      sel[4] = cnt[d];
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < SEL_BINS; i += NT) ghist[i] = 0;  // ready for next pass

@@ -520,6 +520,26 @@ def test_gpu_hash_path_star_hub(gpu, oracle):
                     assert_canonical_equal(eu, ew, es, u, w, s)
 
 
+def test_gpu_final_prune_folded_into_order(gpu, oracle):
+    """The call's last prune folded into the 8-byte order (hp_prune fuse: the
+    keys >= the k-th sorted straight from the unpruned buffer, the first k
+    written -- the canonical tie rule is the sort order): Jaccard with few
+    ties takes it, Adamic-Adar (too many distinct scores for 8-byte keys) and
+    Common Neighbours (a tie set far beyond k) fall back to the split; every
+    result exact against the oracle, one and several chunks."""
+    off, keys = random_csr(20000, 16, 41)
+    for env in (dict(), dict(NLP_HASH_EMIT="300000")):
+        with _env(NLP_HASH="1", **env):
+            with gpu.Graph(off, keys) as G:
+                for m in (1, 7, 0, 3):
+                    for H in (0, 16):
+                        for k in (70000, 250000):
+                            u, w, s, t = G.predict(m, H, k)
+                            assert t["path"] == 4
+                            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                            assert_canonical_equal(eu, ew, es, u, w, s)
+
+
 def test_gpu_hash_routing_and_shards(gpu, oracle):
     """Automatic routing by the wedge estimate, and per-shard path-4 results
     merged on the device equal the single-range result."""
