@@ -228,9 +228,8 @@ class Runner:
         self.states = {}
 
     def __call__(self, mid, hub):
-        if self.world == 1:
-            cnt, t = self.G.predict_device(mid, hub, self.k, self.out, stream=self.stream)
-            return cnt, dict(t)
+        if self.world == 1:  # (the timing dict is the call's own: no copy)
+            return self.G.predict_device(mid, hub, self.k, self.out, stream=self.stream)
         if hub not in self.states:  # shard bounds balanced by the per-source wedge estimate, per H
             st = self.dmod.Exchange()
             st.weights = self.dmod.source_weights(self.off, self.keys, hub)
@@ -255,11 +254,11 @@ def timed(run, mid, hub, steps, warmup, world):
                predict_ms=0.0, select_xchg_ms=0.0, gather_merge_ms=0.0, exchange_ms=0.0)
     last = {}
     cnt = 0
+    lasts = []  # the calls' timing fields, summed after the timed region
     t0 = time.perf_counter()
     for _ in range(steps):
         cnt, last = run(mid, hub)
-        for key in acc:
-            acc[key] += last.get(key, 0)
+        lasts.append(last)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -267,6 +266,9 @@ def timed(run, mid, hub, steps, warmup, world):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = float(el.item()) / steps * 1e3
+    for one in lasts:
+        for key in acc:
+            acc[key] += one.get(key, 0)
     for key in acc:
         acc[key] = acc[key] / steps
     return ms, cnt, acc, last
@@ -358,7 +360,7 @@ def main():
     ginfo = G.info()
     span = ginfo["span"]
     k = info["k"]
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.current_stream().cuda_stream  # the raw hipStream_t: no lookup per call
     mid = nlp.METRICS.index(metric)
     run = Runner(nlp, dmod, G, off, keys, span, k, world, stream)
     amort = create_s * 1e3 / CALLS_PER_GRAPH
