@@ -231,7 +231,7 @@ struct nlp_graph {
   double last_ok_w = 0;                        // wedge estimate of the last successful sort-path call
   bool last_ok_msd = true;                     //   and its grouping (MSD bucket passes or full LSD sort)
   int last_ok_passes = 1;
-  bool use_graphs = true;                      // NLP_NO_GRAPH=1 disables hipGraph replay
+  bool use_graphs = true;                      // hipGraph replay (off with NLP_DIRECT_LAUNCH=1)
   bool graph_single = true;                    // NLP_GRAPH_SEGMENTS=1: four graph segments with host events
   uint64_t ws_gen = 0;                         // bumped whenever a workspace buffer moves
   struct Cached {
@@ -836,7 +836,6 @@ nlp_status finish_graph(nlp_graph* g) {
   uint64_t b = (uint64_t)(fr / 8 / 44);
   g->wedge_budget = std::max<uint64_t>(1u << 20, std::min<uint64_t>(b, 1ull << 30));
   if (const char* fr = getenv("NLP_FORCE_RADIX")) g->force_radix = fr[0] == '1';
-  if (const char* ng = getenv("NLP_NO_GRAPH")) g->use_graphs = ng[0] != '1';
   // test hook: NLP_WEDGE_BUDGET forces path-2 chunking on small graphs
   if (const char* ev = getenv("NLP_WEDGE_BUDGET")) {
     unsigned long long v = strtoull(ev, nullptr, 10);

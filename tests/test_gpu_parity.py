@@ -361,16 +361,12 @@ def test_gpu_graph_replay_equals_direct_launch(gpu, oracle):
                 assert t["graph_replay"] == 1
             seen[(m, H, k)] = True
             assert t["hot_ms"] > 0 and t["hot_bytes"] > 0
-    try:
-        os.environ["NLP_NO_GRAPH"] = "1"
-        with gpu.Graph(off, keys) as G:
-            for m, H, k in runs[:3]:
-                u, w, s, t = G.predict(m, H, k)
-                assert t["graph_replay"] == 0
-                eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
-                assert_canonical_equal(eu, ew, es, u, w, s)
-    finally:
-        del os.environ["NLP_NO_GRAPH"]
+    with _env(NLP_DIRECT_LAUNCH="1"), gpu.Graph(off, keys) as G:  # no graphs at all
+        for m, H, k in runs[:3]:
+            u, w, s, t = G.predict(m, H, k)
+            assert t["graph_replay"] == 0
+            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+            assert_canonical_equal(eu, ew, es, u, w, s)
 
 
 def test_gpu_degree_index_equals_survivor_scan(gpu, oracle):
