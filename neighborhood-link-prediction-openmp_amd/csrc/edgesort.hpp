@@ -505,9 +505,12 @@ constexpr int ES8_CUN = 8;
 __global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ keys, uint64_t n, int shift,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ ghist,
                                                    uint32_t tpw, uint32_t G) {
-  __shared__ uint32_t h[ES_NT / 64][256];
-  const int t = threadIdx.x, wv = wave_id();
-  for (int i = t; i < ES_NT / 64 * 256; i += ES_NT) (&h[0][0])[i] = 0;
+  // four copies per wave (lane & 3), rows padded to 257 words: lanes with the
+  // same digit -- the score-rank digits are skewed -- spread over copies and banks
+  constexpr int CP = 4, RW = 257;
+  __shared__ uint32_t h[ES_NT / 64][CP][RW];
+  const int t = threadIdx.x, wv = wave_id(), cp = lane_id() & (CP - 1);
+  for (int i = t; i < ES_NT / 64 * CP * RW; i += ES_NT) (&h[0][0][0])[i] = 0;
   __syncthreads();
   const uint64_t tile = ES8_TILE;
   const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
@@ -520,13 +523,15 @@ __global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ 
     }
 #pragma unroll
     for (int q = 0; q < ES8_CUN; ++q)
-      if (j0 + (uint64_t)q * ES_NT + t < hi) atomicAdd(&h[wv][(uint32_t)(k[q] >> shift) & 0xffu], 1u);
+      if (j0 + (uint64_t)q * ES_NT + t < hi) atomicAdd(&h[wv][cp][(uint32_t)(k[q] >> shift) & 0xffu], 1u);
   }
   __syncthreads();
   if (t < 256) {
     uint32_t c = 0;
 #pragma unroll
-    for (int w = 0; w < ES_NT / 64; ++w) c += h[w][t];
+    for (int w = 0; w < ES_NT / 64; ++w)
+#pragma unroll
+      for (int z = 0; z < CP; ++z) c += h[w][z][t];
     cnt[(uint64_t)t * G + blockIdx.x] = c;
     if (c) atomicAdd(&ghist[t], c);
   }
