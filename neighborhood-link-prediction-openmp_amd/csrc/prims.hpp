@@ -301,7 +301,14 @@ __global__ __launch_bounds__(NT) void k_sel_hist(const uint32_t* __restrict__ ke
 #pragma unroll
     for (int q = 0; q < UN; ++q) {
       const bool match = j0 + (uint64_t)q * NT < n && (hi_bits == 0 || (k[q] >> (32 - hi_bits)) == prefix);
-      if (match) atomicAdd(&h[(k[q] >> shift) & mask], 1u);
+      // the lanes sharing lane 0's bin (score keys are skewed: one bin often
+      // holds most of a wave) add once; the others one by one
+      const uint32_t b = match ? (k[q] >> shift) & mask : 0xffffffffu;
+      const uint32_t lead = __builtin_amdgcn_readfirstlane(b);
+      const uint64_t same = __ballot(b == lead && lead != 0xffffffffu);
+      if (same && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)same) - 1))
+        atomicAdd(&h[lead], (uint32_t)__popcll(same));
+      if (match && !((same >> (threadIdx.x & 63)) & 1ull)) atomicAdd(&h[b], 1u);
     }
   }
   __syncthreads();
