@@ -341,6 +341,10 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
   for (int i = threadIdx.x; i < (int)ES_LCAP; i += ES_NT) {
     const uint32_t x = s_set[i];
     if (!x) continue;
+    // once the set has overflowed (more than ES_DMAX keys: the caller keeps the
+    // 12-byte sort) nothing more is inserted -- a global set filling up far
+    // beyond ES_DMAX made its probe chains long (C4 AA H=32: 66 ms)
+    if (__hip_atomic_load(&gcnt[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     uint32_t h = es_dhash(x, ES_DLOG);
     for (uint32_t probe = 0;; ++probe) {
       if (probe >= ES_DCAP) { atomicOr(&gcnt[1], 1u); break; }
