@@ -103,7 +103,15 @@ typedef struct {
   uint64_t call_bytes;      /* algorithmic bytes of ALL the call's kernels by the DESIGN.md §5 model
                                (paths 1 and 4; 0 when not modelled) -- what this call's own design
                                must move, beside SURVEY §8(d)'s bytes of the reference's scan */
+  uint32_t order_route;     /* path 4: how the final order ran -- NLP_ORDER_FOLD8 (the last prune folded
+                               into the 8-byte order), NLP_ORDER_FOLD_REFUSED (folded, the keys refused
+                               the 8-byte order: pruned, then the 12-byte sort), NLP_ORDER_SORT8 / _SORT12
+                               (pruned, then the 8-byte / 12-byte sort); 0 for the other paths */
 } nlp_timing;
+#define NLP_ORDER_FOLD8 1
+#define NLP_ORDER_FOLD_REFUSED 2
+#define NLP_ORDER_SORT8 3
+#define NLP_ORDER_SORT12 4
 
 typedef struct nlp_graph nlp_graph;
 
@@ -152,6 +160,25 @@ void nlp_graph_destroy(nlp_graph* g);
 /* Graph properties: span (S), nnz (M), maximum degree, symmetric flag. */
 nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uint32_t* max_degree,
                           int* symmetric);
+
+/* Where the graph build went (no reference counterpart: the reference builds
+ * nothing per graph beyond its DiGraph, and main.cxx times only the predict
+ * calls, main.cxx:50 / predict.hxx:420-430).  *n receives the number of build
+ * phases of the create call that made `g` (for a multi-device handle: its
+ * first replica's); the first min(*n, cap) are written in build order as
+ * (names[i], ms[i]): host wall time with the device stream drained at every
+ * phase boundary, so the phases sum to the create call's time.  *alloc_ms
+ * (may be NULL) is the part of that time spent inside hipMalloc.  Names:
+ * upload, degrees, transpose, degree_class_index, row_index, entry_classes,
+ * short_lists, membership_table, edge_filter, tables_and_setup. */
+nlp_status nlp_graph_build_phases(const nlp_graph* g, uint32_t cap, uint32_t* n, const char** names, double* ms,
+                                  double* alloc_ms);
+
+/* Measurement hook (no reference counterpart): the sort path's stage whose
+ * launch nlp_timing.hot_ms times with HIP events recorded around it on the
+ * call's stream (stage 2 = k_sp_exbucket of the fused call); -1 (the default)
+ * restores the kernels' own low-overhead stamps.  Results are unchanged. */
+nlp_status nlp_set_hot_stage(nlp_graph* g, int stage);
 
 /* predictLinks<Metric>Omp<hub_max_degree>(G, {repeat, max_edges, min_score}).
  * `out` is a caller-owned HOST array of at least min(max_edges, number of

@@ -39,7 +39,10 @@
 #pragma once
 #include <algorithm>
 #include <chrono>
-#include <future>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #ifdef __linux__
 #include <sys/mman.h>
 #endif
@@ -412,10 +415,12 @@ inline GraphCache& graphCache() {
   return c;
 }
 template <class G>
-inline const HipGraph& cachedGraph(const G& x) {
+inline const HipGraph& cachedGraph(const G& x, const std::pair<uint64_t, uint64_t>* known = nullptr) {
   GraphCache& c = graphCache();
   uint64_t m = 0;
-  const uint64_t fp = graphFingerprint(x, &m);
+  // `known`: the fingerprint the caller already computed for x (not hashed twice)
+  const uint64_t fp = known ? known->first : graphFingerprint(x, &m);
+  if (known) m = known->second;
   std::vector<int> devs = defaultDevices();
   if (!c.g.get() || devs != c.devices || c.addr != (const void*)&x || c.span != size_t(x.span()) ||
       c.entries != m || c.fp != fp) {
@@ -431,6 +436,63 @@ inline const HipGraph& cachedGraph(const G& x) {
   }
   return c.g;
 }
+
+// One persistent worker per calling thread for the fingerprint that runs
+// beside a prediction: the same thread every call, so its OpenMP team is
+// built once (a fresh std::async thread per call built a new team each time).
+class FingerprintWorker {
+ public:
+  FingerprintWorker() : th_([this] { loop(); }) {}
+  ~FingerprintWorker() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void start(std::function<void()> job) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      job_ = std::move(job);
+      done_ = false;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> l(mu_);
+    cv_.wait(l, [this] { return done_; });
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> j;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [this] { return stop_ || bool(job_); });
+        if (stop_) return;
+        j = std::move(job_);
+        job_ = nullptr;
+      }
+      j();
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        done_ = true;
+      }
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  bool done_ = true, stop_ = false;
+  std::thread th_;
+};
+inline FingerprintWorker& fingerprintWorker() {
+  static thread_local FingerprintWorker w;
+  return w;
+}
 }  // namespace detail
 
 template <class G, class W>
@@ -444,14 +506,23 @@ inline PredictLinkResult<typename G::key_type, W> predictLinksHipAny(const G& x,
     // the same object as last time: predict on the resident copy while the
     // fingerprint confirms, on another thread, that its adjacency is unchanged;
     // a changed graph discards the result and is uploaded and predicted again
-    auto fut = std::async(std::launch::async, [&x] {
+    std::pair<uint64_t, uint64_t> fm;
+    detail::FingerprintWorker& fw = detail::fingerprintWorker();
+    fw.start([&x, &fm] {
       uint64_t m = 0;
       const uint64_t fp = graphFingerprint(x, &m);
-      return std::make_pair(fp, m);
+      fm = std::make_pair(fp, m);
     });
-    auto r = predictLinksHip<K, W>(c.g, metric, mindegree1, o, maxfactor2);
-    const auto fm = fut.get();
+    PredictLinkResult<K, W> r;
+    try {
+      r = predictLinksHip<K, W>(c.g, metric, mindegree1, o, maxfactor2);
+    } catch (...) {
+      fw.wait();  // the worker reads x: never leave it running
+      throw;
+    }
+    fw.wait();
     if (fm.first == c.fp && fm.second == c.entries) return r;
+    return predictLinksHip<K, W>(detail::cachedGraph(x, &fm), metric, mindegree1, o, maxfactor2);
   }
   return predictLinksHip<K, W>(detail::cachedGraph(x), metric, mindegree1, o, maxfactor2);
 }

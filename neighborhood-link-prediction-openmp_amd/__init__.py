@@ -50,7 +50,7 @@ class Timing(ctypes.Structure):
                 ("copy_ms", ctypes.c_float), ("wedges", ctypes.c_uint64), ("candidates", ctypes.c_uint64),
                 ("nan_candidates", ctypes.c_uint64), ("path", ctypes.c_uint32), ("chunks", ctypes.c_uint32),
                 ("hot_ms", ctypes.c_float), ("graph_replay", ctypes.c_uint32), ("hot_bytes", ctypes.c_uint64),
-                ("hot_kernel", ctypes.c_uint32), ("call_bytes", ctypes.c_uint64)]
+                ("hot_kernel", ctypes.c_uint32), ("call_bytes", ctypes.c_uint64), ("order_route", ctypes.c_uint32)]
 
     def as_dict(self):
         return dict(zip(_TIMING_FIELDS, _timing_get(self)))
@@ -65,7 +65,8 @@ EXPORTS = [
     "nlp_sync", "nlp_select_edges_device",
     "nlp_merge_blocks_device", "nlp_set_truth", "nlp_count_common_device", "nlp_last_common", "nlp_status_string",
     "nlp_metric_name", "nlp_version", "nlp_graph_create_multi", "nlp_device_count", "nlp_graph_parts",
-    "nlp_ingest_device", "nlp_delete_edges_device", "nlp_host_alloc", "nlp_host_free",
+    "nlp_ingest_device", "nlp_delete_edges_device", "nlp_host_alloc", "nlp_host_free", "nlp_graph_build_phases",
+    "nlp_set_hot_stage",
 ]
 
 _lib = None
@@ -97,6 +98,10 @@ def lib(build_if_missing=True):
     L.nlp_graph_destroy.argtypes = [vp]
     L.nlp_graph_destroy.restype = None
     L.nlp_graph_info.argtypes = [vp, P(u64), P(u64), P(u32), P(i32)]
+    L.nlp_graph_build_phases.argtypes = [vp, u32, P(u32), vp, vp, P(ctypes.c_double)]
+    L.nlp_graph_build_phases.restype = i32
+    L.nlp_set_hot_stage.argtypes = [vp, i32]
+    L.nlp_set_hot_stage.restype = i32
     L.nlp_predict.argtypes = [vp, i32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
     L.nlp_predict_ex.argtypes = [vp, i32, u32, u32, f32, u64, i32, vp, P(u64), P(Timing)]
     L.nlp_copy_last.argtypes = [vp, vp, u64, P(u64)]
@@ -257,6 +262,25 @@ class Graph:
         _check(lib().nlp_graph_info(self._h, ctypes.byref(s), ctypes.byref(m), ctypes.byref(d), ctypes.byref(y)),
                "nlp_graph_info")
         return dict(span=s.value, nnz=m.value, max_degree=d.value, symmetric=bool(y.value))
+
+    def set_hot_stage(self, stage):
+        """nlp_set_hot_stage: time sort-path stage `stage` with HIP events (-1: the kernels' stamps)."""
+        _check(lib().nlp_set_hot_stage(self._h, int(stage)), "nlp_set_hot_stage")
+
+    def build_phases(self):
+        """Where the create call's time went (nlp_graph_build_phases): an
+        ordered {phase: ms} dict (host wall time, the stream drained at each
+        phase boundary) plus 'hipMalloc_ms', the part spent inside hipMalloc."""
+        L = lib()
+        n = ctypes.c_uint32()
+        names = (ctypes.c_char_p * 32)()
+        ms = (ctypes.c_double * 32)()
+        alloc = ctypes.c_double()
+        _check(L.nlp_graph_build_phases(self._h, 32, ctypes.byref(n), names, ms, ctypes.byref(alloc)),
+               "nlp_graph_build_phases")
+        out = {names[i].decode(): ms[i] for i in range(min(n.value, 32))}
+        out["hipMalloc_ms"] = alloc.value
+        return out
 
     def predict(self, metric, hub, max_edges=None, min_score=0.0, repeat=1, maxfactor2=0):
         """Host-output predict: returns (u, v, score) numpy arrays and the timing dict.

@@ -58,43 +58,6 @@ struct GraphView {
   uint32_t etbits;        // log2 of its bucket count
 };
 
-// One wave per row u: count (pass 0) or insert (pass 1) the entries w > u.
-template <bool INSERT>
-__global__ __launch_bounds__(256) void k_etab_build(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
-                                                    uint64_t S, uint64_t* __restrict__ tab, uint32_t bits,
-                                                    unsigned long long* __restrict__ count) {
-  const uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  uint64_t c = 0;
-  if (u < S) {
-    const uint64_t a = off[u], e = off[u + 1];
-    const uint64_t mask = (1ull << bits) - 1;
-    for (uint64_t i = a + lane; i < e; i += 64) {
-      const uint32_t w = keys[i];
-      if (w <= u) continue;
-      ++c;
-      if (!INSERT) continue;
-      const uint64_t key = (u << 32) | w;
-      uint64_t b = et_mix(key) >> (64 - bits);
-      bool done = false;
-      for (uint64_t probe = 0; probe <= mask && !done; ++probe) {
-        for (int s = 0; s < ET_SLOTS && !done; ++s) {
-          unsigned long long* q = (unsigned long long*)&tab[b * ET_SLOTS + s];
-          unsigned long long cur = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (cur == ET_EMPTY) cur = atomicCAS(q, ET_EMPTY, key);
-          done = cur == ET_EMPTY || cur == key;
-        }
-        b = (b + 1) & mask;
-      }
-    }
-  }
-  if (!INSERT) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if (lane == 0 && c) atomicAdd(count, (unsigned long long)c);
-  }
-}
-
 // The reference's MAXFACTOR2 filter on second-hop keys (predict.hxx:221,295):
 // ft(w) = w > u && deg(u) <= F deg(u) && deg(w) <= F deg(u), size_t products.
 // Its first clause holds for F >= 1; the second is a per-(u, w) predicate, so a

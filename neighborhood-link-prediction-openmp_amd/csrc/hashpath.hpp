@@ -64,7 +64,6 @@ struct HpArgs {
   uint64_t cap;       // free slots from base on
   const int64_t* tau; // emit only key > *tau
   unsigned long long* ctr;
-  int one_bucket;     // test hook (k_hp_part): one w-bucket per row
   // small H: the surviving first hops of every source of the range (S(u) =
   // {v in N(u) : deg v <= H}, multiplicities kept, any order), so a row walks
   // S(u) instead of all of N(u) with a degree gather per entry (null: N(u))
@@ -931,6 +930,91 @@ __global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __r
         if (g.keys[o + md] <= u) l = md + 1; else h = md;
       }
       out[e] = (uint8_t)l;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- membership table build (per graph)
+// The table's size bound: the entries w > u, sum over rows of deg u - xs[u]
+// (xs = the entries at or below u, k_hp_xs) -- a streaming read of two S-word
+// arrays instead of a pass over the adjacency with a wave per row.
+__global__ void k_etab_upper(const uint32_t* __restrict__ deg, const uint32_t* __restrict__ xs, uint64_t S,
+                             unsigned long long* __restrict__ count) {
+  uint64_t c = 0;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < S; u += (uint64_t)gridDim.x * blockDim.x)
+    c += deg[u] - xs[u];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane_id() == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
+// Insert one key: the bucket line is read whole (8 slots, one round trip),
+// then its first empty slot is claimed by one CAS; a lost race re-reads the
+// same bucket.  Slots only go from empty to full and a writer claims only the
+// first empty slot it saw, so a bucket never has a hole and a key never lands
+// twice -- et_has's rule (absent once a bucket with an empty slot lacks it)
+// holds.
+__device__ __forceinline__ void et_insert(uint64_t* __restrict__ tab, uint32_t bits, uint64_t key) {
+  const uint64_t mask = (1ull << bits) - 1;
+  uint64_t b = et_mix(key) >> (64 - bits);
+  for (uint64_t probe = 0; probe <= mask;) {
+    unsigned long long* q = (unsigned long long*)(tab + b * ET_SLOTS);
+    uint64_t s[ET_SLOTS];
+#pragma unroll
+    for (int j = 0; j < ET_SLOTS; ++j) s[j] = __hip_atomic_load(q + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int first = -1;
+    bool hit = false;
+#pragma unroll
+    for (int j = ET_SLOTS - 1; j >= 0; --j) {
+      hit |= s[j] == key;
+      if (s[j] == ET_EMPTY) first = j;
+    }
+    if (hit) return;
+    if (first < 0) {
+      b = (b + 1) & mask;
+      ++probe;
+      continue;
+    }
+    const unsigned long long cur = atomicCAS(q + first, ET_EMPTY, (unsigned long long)key);
+    if (cur == ET_EMPTY || cur == key) return;
+  }
+}
+
+// The entries w > u inserted edge-parallel: a wave takes HP_WTILE consecutive
+// adjacency entries (coalesced keys, every lane busy whatever the degrees),
+// finding each entry's row from the tile's first row like k_hp_drank.
+__global__ __launch_bounds__(NT) void k_etab_insert(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                                                    uint64_t S, uint64_t M, const uint32_t* __restrict__ tile_row,
+                                                    uint64_t* __restrict__ tab, uint32_t bits) {
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t nt = (M + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t tile = (uint64_t)blockIdx.x * NWAVE + wv; tile < nt; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t r0 = tile_row[tile];
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < S ? off[rl + 1] : ~0ull;
+    const uint64_t last_end = __shfl(rend, 63, 64);
+#pragma unroll 1
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      const uint32_t w = e < M ? keys[e] : 0u;
+      int lo = 0, hi = 64;
+      while (lo < hi) {
+        const int md = (lo + hi) >> 1;
+        const uint64_t x = __shfl(rend, md, 64);
+        if (x <= e) lo = md + 1; else hi = md;
+      }
+      if (e >= M) continue;
+      uint64_t r = r0 + lo;
+      if (e >= last_end) {
+        uint64_t a = r0, b = S;
+        while (b - a > 1) {
+          const uint64_t md = (a + b) >> 1;
+          if (off[md] <= e) a = md; else b = md;
+        }
+        r = a;
+      }
+      if (w > r) et_insert(tab, bits, (r << 32) | w);
     }
   }
 }
@@ -2882,7 +2966,6 @@ __global__ __launch_bounds__(HP_BNT) void k_hp_part(HpArgs a, const uint32_t* __
     uint64_t pd = (W + HP_PART_W - 1) / HP_PART_W;
     const uint64_t pspan = (span_w + (LT / 2) - 1) / (LT / 2);
     if (pd > pspan) pd = pspan;
-    if (a.one_bucket) pd = 1;  // test hook: one bucket per row (sub-range passes)
     if (pd < 1) pd = 1;
     if (pd > HP_PMAX) pd = HP_PMAX;
     const int shift = log2_ceil((span_w + pd - 1) / pd);

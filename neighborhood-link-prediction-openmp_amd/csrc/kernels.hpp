@@ -50,7 +50,7 @@ __device__ __forceinline__ float score_basic(int m, uint32_t c, uint64_t du, uin
 // The first-order exclusion (predict.hxx:306-307) asks, for a candidate (u, w)
 // with w > u, whether w is in N(u).  A search of the sorted list costs
 // log(deg) dependent loads; this table answers with one 64-byte line.  Built
-// once per graph (k_etab_build): open addressing over buckets of 8 u64 keys
+// once per graph (hashpath.hpp k_etab_insert): open addressing over buckets of 8 u64 keys
 // (u << 32 | w), one bucket = one cache line, linear probing by bucket, at most
 // half full.  Only entries with w > u are stored (a candidate always has
 // w > u); duplicate entries (the reference's multiset rows) are stored once.
@@ -209,11 +209,6 @@ __global__ void k_check_keys(const uint64_t* __restrict__ off, const uint32_t* _
   }
 }
 
-__global__ void k_count_cols(const uint32_t* __restrict__ keys, uint64_t nnz, uint32_t* __restrict__ tdeg) {
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x)
-    atomicAdd(&tdeg[keys[e]], 1u);
-}
-
 // (v << 32 | u) for every edge u -> v; row u found by binary search on offsets
 __global__ void k_transpose_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
                                  uint64_t nnz, uint64_t* __restrict__ out) {
@@ -223,9 +218,23 @@ __global__ void k_transpose_keys(const uint64_t* __restrict__ off, const uint32_
   }
 }
 
-__global__ void k_low32(const uint64_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ out) {
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x)
-    out[e] = (uint32_t)in[e];
+// I(v) from the (v << 32 | u) keys sorted by v (u ascending inside a v, the
+// keys having been generated in CSR order and sorted stably): tkeys = the u
+// halves, toff[x] = the first position whose v >= x (S + 1 entries; item M
+// closes the columns above the last v) -- one streaming pass instead of an
+// atomic column count plus a scan
+__global__ void k_toff_split(const uint64_t* __restrict__ sorted, uint64_t M, uint64_t S, uint64_t* __restrict__ toff,
+                             uint32_t* __restrict__ tkeys) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= M; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t v = S;
+    if (i < M) {
+      const uint64_t x = sorted[i];
+      v = x >> 32;
+      tkeys[i] = (uint32_t)x;
+    }
+    const uint64_t vp = i ? (sorted[i - 1] >> 32) + 1 : 0;  // the first column not opened before i
+    for (uint64_t c = vp; c <= v; ++c) toff[c] = i;
+  }
 }
 
 __global__ void k_diff_u64(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint64_t n, uint32_t* __restrict__ flag) {

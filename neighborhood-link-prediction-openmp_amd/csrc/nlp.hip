@@ -82,6 +82,18 @@ enum Buf {
   NBUF
 };
 
+// Graph build timing (nlp_graph_build_phases): while a build runs, the time
+// spent inside hipMalloc accumulates here (null: not timed).
+thread_local double* t_alloc_ms = nullptr;
+template <typename T>
+hipError_t hmalloc(T** p, size_t bytes) {
+  if (!t_alloc_ms) return hipMalloc((void**)p, bytes);
+  const auto t0 = std::chrono::steady_clock::now();
+  const hipError_t e = hipMalloc((void**)p, bytes);
+  *t_alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return e;
+}
+
 struct Workspace {
   void* p[NBUF] = {};
   size_t bytes[NBUF] = {};
@@ -96,7 +108,7 @@ struct Workspace {
       }
       size_t nb = std::max(need, bytes[id] + bytes[id] / 2);
       nb = (nb + 255) & ~(size_t)255;
-      hipError_t e = hipMalloc(&p[id], nb);
+      hipError_t e = hmalloc(&p[id], nb);
       if (e != hipSuccess) { p[id] = nullptr; return e; }
       bytes[id] = nb;
     }
@@ -148,7 +160,7 @@ struct nlp_graph {
   double* ctab_ra = nullptr;  // 1.0 / (double)d                        (predict.hxx:828)
   uint32_t* efilt = nullptr;  // edge filter of the first-order exclusion (k_sp_runs; only without etab)
   uint32_t efbits = 0;
-  uint64_t* etab = nullptr;   // exact membership table of the entries w > u (group.hpp k_etab_build)
+  uint64_t* etab = nullptr;   // exact membership table of the entries w > u (hashpath.hpp k_etab_insert)
   uint32_t etbits = 0;
   uint64_t* host_small = nullptr;  // pinned counters
   uint64_t* host_ctr = nullptr;    // host-mapped counters written by the last kernel (sort path)
@@ -274,15 +286,11 @@ struct nlp_graph {
   uint64_t hp_min_wedges = 1ull << 26;         // NLP_HASH_MIN_WEDGES: estimated wedges above which path 4 runs
   int hash_mode = 0;                           // NLP_HASH: 0 auto, 1 always, -1 never
   // test hooks: NLP_HASH_EMIT (emission slots per chunk), NLP_HASH_MINBIN (smallest bin), NLP_HASH_SCAP
-  // (scratch words per workgroup), NLP_HASH_ONE_BUCKET (one w-bucket per partitioned row)
+  // (scratch words per workgroup)
   uint64_t hp_emit = 0;
-  int hp_minbin = 0, hp_one_bucket = 0;
-  int hp_tiers = 1;        // bin 0 split by table-size tier (NLP_HASH_TIERS=0: one 1024-entry launch)
+  int hp_minbin = 0;
   bool sv_pack_on = true;   // NLP_SV_PACK=0: survivors' rows loaded unpacked (parity of the packed loads)
   int hh_tl = 0;             // hub pass: table log for the item plan (NLP_HASH_HUB_TL, 7..13; small values test the splits)
-  bool hp_sdo = true;        // degree-class lists also packed (deg v, off[v]) for the row batches (NLP_HASH_SDO=0)
-                             // per SIMD, 3: 8 + 3 waves, 4: 2 + 3 waves
-  bool hp_win = true;        // k_hp_batch reserves emission windows (NLP_HASH_WIN=0: one reservation per flush)
   // survivor lists: three streaming kernels (k_dc_*; a one-pass build with a decoupled look-back measured
   // slower, 7.2 vs 5.9 ms on C4 H=16, and was removed in round 5)
   unsigned occ_es = 256;     // resident k_es_pass workgroups
@@ -307,9 +315,7 @@ struct nlp_graph {
   bool hp_batch = true;      // path 4: bin-0 tiers 0 / 1 in row batches (k_hp_batch; NLP_HASH_BATCH=0: a wave per row)
   // (u64, u32) sorts of paths 2 / 4 by onesweep passes (NLP_OS_SORT=1); the default hist / scan / scatter
   // passes measured faster at these sizes (C4 JAC H=16 ordering: 22 vs 77 ms; C3 AA H=16 path 2: 122 vs 418 ms)
-  bool hp_work_surv = true;  // small H: W(u) from the survivors' in-edges (NLP_HASH_WORK_SURV=0: edge pass)
   bool hp_dcls = true;       // survivor lists by filtering N(u) with the degree classes (NLP_HASH_DCLS=0: in-edge atomics)
-  uint32_t hp_slices = 0;  // k_hp_part slices per row (0: hp_gp / rows, at most 256; NLP_HASH_SLICES forces)
   uint64_t hp_scap_force = 0;
   std::vector<uint64_t> deg_hist;              // vertices per degree 0..DCAP, for wedge estimates
   uint64_t big_deg2 = 0;                       // sum of deg^2 over vertices of degree > DCAP
@@ -326,6 +332,9 @@ struct nlp_graph {
   uint64_t gather_cap = 0;
   EdgeOut* group_out = nullptr;                // on members[0]: the merged result of a host-output call
   uint64_t group_out_cap = 0;
+  // phases of the build (nlp_graph_build_phases): name and host wall ms, the stream drained at each boundary
+  std::vector<std::pair<const char*, double>> build_phases;
+  double build_alloc_ms = 0;                   // of the build, the time inside hipMalloc
 };
 
 namespace {
@@ -464,10 +473,32 @@ int bits_for(uint64_t maxval) {  // bits needed to represent values <= maxval
 // per-row sort by class.  Skipped -- the calls then compact per call -- when
 // the lists and their build scratch would take more than a quarter of the free
 // HBM; any allocation failure also just skips them.
+// Wall time of the build's phases (nlp_graph_build_phases): mark() drains the
+// graph's stream and closes a phase; hipMalloc time is summed on the side.
+struct BuildClock {
+  nlp_graph* g;
+  std::chrono::steady_clock::time_point t;
+  double alloc = 0;
+  double* prev;
+  explicit BuildClock(nlp_graph* gr) : g(gr), t(std::chrono::steady_clock::now()), prev(t_alloc_ms) {
+    g->build_phases.clear();
+    t_alloc_ms = &alloc;
+  }
+  ~BuildClock() { t_alloc_ms = prev; }  // (g may be gone: an error path destroys it first)
+  hipError_t mark(const char* name) {
+    const hipError_t e = hipStreamSynchronize(g->stream);
+    const auto n = std::chrono::steady_clock::now();
+    g->build_phases.emplace_back(name, std::chrono::duration<double, std::milli>(n - t).count());
+    g->build_alloc_ms = alloc;
+    t = n;
+    return e;
+  }
+};
+
 template <typename T>
 bool dmalloc(T** out, uint64_t n) {  // device allocation of n items; a failure is cleared and reported as false
   void* x = nullptr;
-  if (hipMalloc(&x, std::max<uint64_t>(n, 1) * sizeof(T)) != hipSuccess) {
+  if (hmalloc(&x, std::max<uint64_t>(n, 1) * sizeof(T)) != hipSuccess) {
     (void)hipGetLastError();
     *out = nullptr;
     return false;
@@ -571,13 +602,13 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
 }
 
 // Build everything derived from off/keys (already on the device).
-nlp_status finish_graph(nlp_graph* g) {
+nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   hipStream_t st = g->stream;
   const uint64_t S = g->span, M = g->nnz;
   uint32_t* flags;  // [0] bad, [1] maxdeg, [2] asym
   TRY(wsget(g->ws, B_CNT, 8, &flags));
   TRY(hipMemsetAsync(flags, 0, 32, st));
-  TRY(hipMalloc(&g->deg, std::max<uint64_t>(S, 1) * 4));
+  TRY(hmalloc(&g->deg, std::max<uint64_t>(S, 1) * 4));
   LAUNCH(k_degrees, S, st, g->off, S, g->deg, flags + 1, flags);
   TRY(hipGetLastError());
   if (M) {
@@ -595,6 +626,7 @@ nlp_status finish_graph(nlp_graph* g) {
   TRY(hipMemcpy(&ends[0], g->off, 8, hipMemcpyDeviceToHost));
   TRY(hipMemcpy(&ends[1], g->off + S, 8, hipMemcpyDeviceToHost));
   if (ends[0] != 0 || ends[1] != M) return NLP_ERR_INVALID;
+  TRY(clk.mark("degrees"));
 
   // Transposed adjacency I(v): stable radix sort of (v << 32 | u).
   g->symmetric = true;
@@ -602,32 +634,28 @@ nlp_status finish_graph(nlp_graph* g) {
   g->tkeys = g->keys;
   if (M) {
     uint64_t *k0, *k1, *scan, *hoff;
-    uint32_t *tdeg, *hist;
+    uint32_t* hist;
     TRY(wsget(g->ws, B_WKEY0, M, &k0));
     TRY(wsget(g->ws, B_WKEY1, M, &k1));
     uint64_t nb = rs_blocks(M);
     TRY(wsget(g->ws, B_HIST, RS_BINS * nb, &hist));
     TRY(wsget(g->ws, B_HOFF, RS_BINS * nb, &hoff));
-    TRY(wsget(g->ws, B_SCAN, scan_scratch_words(std::max<uint64_t>(RS_BINS * nb, S + 1)) + 16, &scan));
-    TRY(wsget(g->ws, B_C32, S + 1, &tdeg));
+    TRY(wsget(g->ws, B_SCAN, scan_scratch_words(RS_BINS * nb) + 16, &scan));
     uint64_t* toff;
     uint32_t* tkeys;
-    TRY(hipMalloc(&toff, (S + 1) * 8));
-    TRY(hipMalloc(&tkeys, M * 4));
-    TRY(hipMemsetAsync(tdeg, 0, (S + 1) * 4, st));
-    LAUNCH(k_count_cols, M, st, g->keys, M, tdeg);
-    TRY(hipGetLastError());
-    TRY(scan_excl_u64<uint32_t>(tdeg, S + 1, toff, nullptr, scan, st));
+    TRY(hmalloc(&toff, (S + 1) * 8));
+    TRY(hmalloc(&tkeys, M * 4));
     LAUNCH(k_transpose_keys, M, st, g->off, g->keys, S, M, k0);
     TRY(hipGetLastError());
+    // the keys come in CSR order (u ascending), so a stable sort on the v bytes
+    // alone leaves every I(v) sorted by u: half the passes of a full key sort
     int vb = bits_for(S - 1);
-    int shifts[8], np = 0;
-    for (int b = 0; b < vb; b += 8) shifts[np++] = b;            // u bytes (low word)
+    int shifts[4], np = 0;
     for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;       // v bytes (high word)
     SortScratch sc{hist, hoff, scan, nb};
     int which = 0;
     TRY(sort_pairs_u64(k0, nullptr, k1, nullptr, M, shifts, np, sc, &which, st));
-    LAUNCH(k_low32, M, st, which ? k1 : k0, M, tkeys);
+    LAUNCH(k_toff_split, M + 1, st, (const uint64_t*)(which ? k1 : k0), M, S, toff, tkeys);
     TRY(hipGetLastError());
     LAUNCH(k_diff_u64, S + 1, st, toff, g->off, S + 1, flags + 2);
     LAUNCH(k_diff_u32, M, st, tkeys, g->keys, M, flags + 2);
@@ -645,6 +673,7 @@ nlp_status finish_graph(nlp_graph* g) {
       TRY(hipFree(tkeys));
     }
   }
+  TRY(clk.mark("transpose"));
   // Degree-class index: survivors of any H <= DCAP without a pass over deg[].
   {
     uint32_t* hist;
@@ -669,7 +698,7 @@ nlp_status finish_graph(nlp_graph* g) {
     g->dstart.assign(DCAP + 2, 0);
     for (uint32_t d = 1; d <= DCAP; ++d) g->dstart[d + 1] = g->dstart[d] + hh[d];
     const uint64_t nv = g->dstart[DCAP + 1];
-    TRY(hipMalloc(&g->vbydeg, std::max<uint64_t>(nv, 1) * 4));
+    TRY(hmalloc(&g->vbydeg, std::max<uint64_t>(nv, 1) * 4));
     unsigned long long* cur;
     TRY(wsget(g->ws, B_SCAN, DCAP + 2, &cur));
     TRY(hipMemcpyAsync(cur, g->dstart.data(), (DCAP + 2) * 8, hipMemcpyHostToDevice, st));
@@ -678,10 +707,10 @@ nlp_status finish_graph(nlp_graph* g) {
     TRY(hipGetLastError());
     if (const char* sp = getenv("NLP_SV_PACK")) g->sv_pack_on = sp[0] != '0';
     if (nv > 0 && g->nnz < (1ull << SV_PACK_SHIFT) && g->sv_pack_on) {
-      TRY(hipMalloc(&g->sv_pack, nv * 8));
+      TRY(hmalloc(&g->sv_pack, nv * 8));
       uint32_t* flag = nullptr;
       if (!g->symmetric) {
-        TRY(hipMalloc(&g->sv_pack_in, nv * 8));
+        TRY(hmalloc(&g->sv_pack_in, nv * 8));
         TRY(wsget(g->ws, B_HP_SMALL, 8, &flag));
         TRY(hipMemsetAsync(flag, 0, 4, st));
       }
@@ -702,11 +731,12 @@ nlp_status finish_graph(nlp_graph* g) {
     }
     TRY(hipStreamSynchronize(st));
   }
+  TRY(clk.mark("degree_class_index"));
   // per row the entries of N(u) at or below u: the first-order exclusion only
   // marks x > u (predict.hxx:306-307 zeroes all of N(u), but only w > u are
   // candidates), so path 4's row kernels walk N(u) from there
   if (S > 0 && !(getenv("NLP_HASH_XS") && getenv("NLP_HASH_XS")[0] == '0')) {
-    if (hipMalloc(&g->xs, S * 4) == hipSuccess) {
+    if (hmalloc(&g->xs, S * 4) == hipSuccess) {
       LAUNCH(k_hp_xs, S, st, (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->xs);
       TRY(hipGetLastError());
     } else {
@@ -715,18 +745,19 @@ nlp_status finish_graph(nlp_graph* g) {
     }
   }
   // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
-  TRY(hipMalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
+  TRY(hmalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
   TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
   LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
   TRY(hipGetLastError());
+  TRY(clk.mark("row_index"));
   // degree class of every adjacency entry: path 4 filters N(u) by it (coalesced
   // bytes instead of a degree gather per entry) to build the survivor lists S(u)
   const char* hdc = getenv("NLP_HASH_DCLS");
   if (M > 0 && !(hdc && hdc[0] == '0') && g->maxdeg < (1u << 24)) {
-    if (hipMalloc(&g->dcls, M) == hipSuccess) {
+    if (hmalloc(&g->dcls, M) == hipSuccess) {
       // and the entry degrees (the count-metric row kernels carry deg w in their tables)
       const char* hkd = getenv("NLP_HASH_KDEG");
-      if (!(hkd && hkd[0] == '0') && hipMalloc(&g->kdeg, M * 4) != hipSuccess) {
+      if (!(hkd && hkd[0] == '0') && hmalloc(&g->kdeg, M * 4) != hipSuccess) {
         (void)hipGetLastError();
         g->kdeg = nullptr;
       }
@@ -735,7 +766,7 @@ nlp_status finish_graph(nlp_graph* g) {
       // and the rank of every short-list entry's row in the list (k_hp_drank)
       const char* hdr = getenv("NLP_HASH_DRANK");
       if (!(hdr && hdr[0] == '0')) {
-        if (hipMalloc(&g->drank, M) == hipSuccess) {
+        if (hmalloc(&g->drank, M) == hipSuccess) {
           GraphView gv0{};
           gv0.off = g->off;
           gv0.keys = g->keys;
@@ -754,6 +785,7 @@ nlp_status finish_graph(nlp_graph* g) {
       g->dcls = nullptr;
     }
   }
+  TRY(clk.mark("entry_classes"));
   {  // class-ordered short lists (the count metrics' S(u) as row prefixes; NLP_HASH_SLIST=0: per-call
      // compaction, =c: classes up to c at most)
     const char* sl = getenv("NLP_HASH_SLIST");
@@ -763,6 +795,7 @@ nlp_status finish_graph(nlp_graph* g) {
       if (s1 != NLP_OK) return s1;
     }
   }
+  TRY(clk.mark("short_lists"));
   // Exact membership table of the entries w > u for the first-order exclusion
   // (kernels.hpp et_has): one 64-byte bucket read per candidate instead of a
   // search of N(u).  At most half full; skipped (NLP_ETAB=0, or when it would
@@ -773,8 +806,11 @@ nlp_status finish_graph(nlp_graph* g) {
       unsigned long long* cnt;
       TRY(wsget(g->ws, B_HP_SMALL, 8, &cnt));
       TRY(hipMemsetAsync(cnt, 0, 8, st));
-      hipLaunchKernelGGL(k_etab_build<false>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, (const uint64_t*)g->off,
-                         (const uint32_t*)g->keys, S, (uint64_t*)nullptr, 1u, cnt);
+      if (g->xs) {  // the entries w > u: sum of deg u - xs[u]
+        LAUNCH(k_etab_upper, S, st, (const uint32_t*)g->deg, (const uint32_t*)g->xs, S, cnt);
+      } else {  // an upper bound: every entry
+        TRY(hipMemcpyAsync(cnt, &M, 8, hipMemcpyHostToDevice, st));
+      }
       TRY(hipGetLastError());
       uint64_t upper = 0;
       TRY(hipMemcpyAsync(&upper, cnt, 8, hipMemcpyDeviceToHost, st));
@@ -785,16 +821,17 @@ nlp_status finish_graph(nlp_graph* g) {
       size_t fr = 0, tot = 0;
       TRY(hipMemGetInfo(&fr, &tot));
       if (upper > 0 && bytes < fr / 4) {
-        TRY(hipMalloc(&g->etab, bytes));
+        TRY(hmalloc(&g->etab, bytes));
         TRY(hipMemsetAsync(g->etab, 0xff, bytes, st));
-        hipLaunchKernelGGL(k_etab_build<true>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st,
-                           (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->etab, bits,
-                           (unsigned long long*)nullptr);
+        const unsigned gi = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 65536);
+        hipLaunchKernelGGL(k_etab_insert, dim3(gi), dim3(NT), 0, st, (const uint64_t*)g->off,
+                           (const uint32_t*)g->keys, S, M, (const uint32_t*)g->tile_row, g->etab, bits);
         TRY(hipGetLastError());
         g->etbits = bits;
       }
     }
   }
+  TRY(clk.mark("membership_table"));
   // Edge filter for the first-order exclusion of the scoring kernel when there
   // is no table: one bit per (u, w) hash slot, 16 slots per adjacency entry
   // (~6 % of non-edges hit a set bit and are searched; every edge is).
@@ -808,7 +845,7 @@ nlp_status finish_graph(nlp_graph* g) {
       size_t fr = 0, tot = 0;
       TRY(hipMemGetInfo(&fr, &tot));
       if ((1ull << bits) / 8 < fr / 16) {
-        TRY(hipMalloc(&g->efilt, (1ull << bits) / 8));
+        TRY(hmalloc(&g->efilt, (1ull << bits) / 8));
         TRY(hipMemsetAsync(g->efilt, 0, (1ull << bits) / 8, st));
         hipLaunchKernelGGL(k_edge_filter, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, st, (const uint64_t*)g->off,
                            (const uint32_t*)g->keys, S, g->efilt, bits);
@@ -817,6 +854,7 @@ nlp_status finish_graph(nlp_graph* g) {
       }
     }
   }
+  TRY(clk.mark("edge_filter"));
   // AA / RA contribution tables, computed on the host with the same libm the
   // reference uses (glibc log), indexed by degree.
   std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
@@ -824,8 +862,8 @@ nlp_status finish_graph(nlp_graph* g) {
     aa[d] = 1.0 / log((double)d);
     ra[d] = 1.0 / (double)d;
   }
-  TRY(hipMalloc(&g->ctab_aa, aa.size() * 8));
-  TRY(hipMalloc(&g->ctab_ra, ra.size() * 8));
+  TRY(hmalloc(&g->ctab_aa, aa.size() * 8));
+  TRY(hmalloc(&g->ctab_ra, ra.size() * 8));
   TRY(hipMemcpyAsync(g->ctab_aa, aa.data(), aa.size() * 8, hipMemcpyHostToDevice, st));
   TRY(hipMemcpyAsync(g->ctab_ra, ra.data(), ra.size() * 8, hipMemcpyHostToDevice, st));
   TRY(hipStreamSynchronize(st));
@@ -914,6 +952,7 @@ nlp_status finish_graph(nlp_graph* g) {
     g->occ_run = std::min(a, b);
   }
   g->ws.release();  // drop build scratch; predict grows its own
+  TRY(clk.mark("tables_and_setup"));
   return NLP_OK;
 }
 
@@ -974,6 +1013,7 @@ struct Cands {
   // order keeps the keys >= kmin and writes the first `keep` (0: pruned)
   uint64_t keep = 0, cap = 0;
   uint32_t kmin = 0;
+  uint32_t route = 0;  // path 4: how the final order ran (nlp_timing.order_route)
 };
 
 // Group the W wedges of one generator pass, score them and append the
@@ -1806,14 +1846,21 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   return NLP_OK;
 }
 
+// try8 = false: the caller already knows the keys refuse the 8-byte order.
+// *route (may be null): NLP_ORDER_SORT8 or NLP_ORDER_SORT12, the sort that ran.
 nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
-                   hipStream_t st, uint64_t* bytes = nullptr) {
+                   hipStream_t st, uint64_t* bytes = nullptr, bool try8 = true, uint32_t* route = nullptr) {
   if (n == 0) return NLP_OK;
-  if ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2) {
+  if (try8 && ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2)) {
     bool done = false;
     nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done);
-    if (s != NLP_OK || done) return s;
+    if (s != NLP_OK) return s;
+    if (done) {
+      if (route) *route = NLP_ORDER_SORT8;
+      return NLP_OK;
+    }
   }
+  if (route) *route = NLP_ORDER_SORT12;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
   const int npass = (32 + 2 * vb + 7) / 8;
@@ -1878,14 +1925,21 @@ nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st
     C.keep = 0;
     if (done) {
       C.n = keep;
+      C.route = NLP_ORDER_FOLD8;
       return NLP_OK;
     }
-    uint32_t kth = 0;  // the keys do not qualify (too many distinct scores, ...): prune, then order
+    // the keys do not qualify (too many distinct scores, ...): prune, then the
+    // 12-byte order (the kept keys are a subset of the refused ones)
+    uint32_t kth = 0;
     s = hp_prune(g, C, keep, C.cap, &kth, st);
     if (s != NLP_OK) return s;
+    s = es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
+                d_out, st, &C.call_bytes, false);
+    C.route = NLP_ORDER_FOLD_REFUSED;
+    return s;
   }
   return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
-                 d_out, st, &C.call_bytes);
+                 d_out, st, &C.call_bytes, true, &C.route);
 }
 
 // Estimated wedges (w > u) of a call: sum over surviving v of deg(v)^2 / 2,
@@ -2090,7 +2144,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       for (uint32_t d = 1; d <= p.H; ++d) p_h += (uint64_t)d * g->deg_hist[d];
     }
     bool one_done = false;
-    if (g->sl_off && !custom && g->hp_dcls && g->hp_work_surv && g->hp_sdo && p.H >= 1 && p.H <= g->sl_cap) {
+    if (g->sl_off && !custom && g->hp_dcls && p.H >= 1 && p.H <= g->sl_cap) {
       // count metrics: S(u) = the prefix of u's class-ordered short list (deg v <= H); only the
       // prefixes' lengths and W+(u) are found (hashpath.hpp k_sl_count)
       uint32_t* scnt;
@@ -2107,7 +2161,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       one_done = true;
     }
     if (one_done) {
-    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && g->hp_sdo && g->drank && p.H >= 1 &&
+    } else if (g->dcls && g->hp_dcls && g->drank && p.H >= 1 &&
         p.H <= HP_DCLS_MAX && e1 > e0 && g->nnz < (1ull << HP_SDO_SH)) {
       // count, place, gather (hashpath.hpp k_dc_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
@@ -2147,7 +2201,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       one_done = true;
     }
     if (one_done) {
-    } else if (g->dcls && g->hp_dcls && g->hp_work_surv && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
+    } else if (g->dcls && g->hp_dcls && p.H >= 1 && p.H <= HP_DCLS_MAX && e1 > e0) {
       // the survivor lists S(u) as the compaction of the range's entries by
       // degree class (sorted, no atomics; hashpath.hpp k_hp_dcls_*)
       const uint64_t t0 = e0 / HP_WTILE, t1 = (e1 + HP_WTILE - 1) / HP_WTILE, nt = t1 - t0;
@@ -2169,7 +2223,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       TRY(hipMemcpyAsync(&g->host_small[10], s_soff + nU, 8, hipMemcpyDeviceToHost, st));
       TRY(hipStreamSynchronize(st));
       TRY(wsget(ws, B_HP_SKEYS, std::max<uint64_t>(g->host_small[10], 1), &s_skeys));
-      if (g->hp_sdo && g->nnz < (1ull << HP_SDO_SH)) {
+      if (g->nnz < (1ull << HP_SDO_SH)) {
         TRY(wsget(ws, B_HP_SDO, std::max<uint64_t>(g->host_small[10], 1), &s_sdo));
         TRY(hipMemsetAsync(wu, 0, nU * 8, st));  // W+(u), accumulated by the fill
       }
@@ -2183,7 +2237,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
                            (unsigned long long*)wu, (const uint8_t*)g->drank);
       TRY(hipGetLastError());
       s_sorted = true;
-    } else if (p_h != ~0ull && 4 * p_h < e1 - e0 && g->hp_work_surv) {
+    } else if (p_h != ~0ull && 4 * p_h < e1 - e0) {
       // the survivor lists S(u) of the range, and W(u) with them: the row kernels walk S(u), not N(u)
       const uint64_t ns = g->dstart[p.H + 1];
       uint32_t* scnt;
@@ -2269,7 +2323,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     uint32_t kth = 0;
     if (real >= k) {
       if (C.n > k) {
-        nlp_status s = hp_prune(g, C, k, capC, &kth, st, last);
+        // the last prune may fold into the 8-byte order; not for AA / RA, whose
+        // top-k scores are nearly all distinct (the order would refuse them)
+        nlp_status s = hp_prune(g, C, k, capC, &kth, st, last && !custom);
         if (s != NLP_OK) return s;
       }
       C.pad = 0;
@@ -2314,7 +2370,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.cap = capC - C.n;
     a.tau = (const int64_t*)(small + 8);
     a.ctr = (unsigned long long*)small;
-    a.one_bucket = g->hp_one_bucket;
     a.soff = s_skeys ? s_soff : nullptr;
     a.scn = s_skeys ? s_scn : nullptr;
     a.skeys = s_skeys;
@@ -2328,7 +2383,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.ph = nullptr;  // k_hp_batch phase ticks (a diagnostic hook: small[56, 60) when set)
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
-    if (n0 && g->hp_tiers) {
+    if (n0) {
       // bin 0 by table-size tier (hashpath.hpp:k_hp_tier): counts, scatter, one launch per tier
       TRY(hipMemsetAsync(tcnt, 0, 8 * sizeof(uint32_t), st));
       const unsigned gt = (unsigned)std::min<uint64_t>((n0 + NT - 1) / NT, 512);
@@ -2356,7 +2411,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         LAUNCH(k_hp_batch_starts, n0, st, (const uint64_t*)bpre, tc, 0, 1, bwid, bst, nbat);
         TRY(hipGetLastError());
         unsigned gb = gr;  // row batches
-        if (g->hp_win && !retry) {
+        if (!retry) {
           // persistent waves (one resident round) reserving emission windows: about an
           // eighth of a wave's share of the chunk's wedge bound per window, so the
           // padding stays below an eighth of the chunk's emission bound; a chunk too
@@ -2392,11 +2447,6 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
         hipLaunchKernelGGL((k_hp_wave<false, 512, 256>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 1);
         hipLaunchKernelGGL((k_hp_wave<false>), dim3(gr), dim3(NT), 0, st, a, tl, n0, wu, ua, tc, 2);
       }
-      TRY(hipGetLastError());
-    } else if (n0) {
-      const unsigned gr = (unsigned)std::min<uint64_t>((n0 + NWAVE - 1) / NWAVE, 8192);
-      if (custom) hipLaunchKernelGGL(k_hp_wave<true>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
-      else hipLaunchKernelGGL(k_hp_wave<false>, dim3(gr), dim3(NT), 0, st, a, lists[0] + q0[0], n0, wu, ua);
       TRY(hipGetLastError());
     }
     TRY(hipMemsetAsync(tcnt + 6, 0, 3 * sizeof(uint32_t), st));  // work queues of bins 2, 3 and 1
@@ -2458,8 +2508,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
       const uint64_t nb = q1[b] - q0[b];
       if (!nb) continue;
       // fewer rows than workgroups: slice each row's w-buckets over several workgroups
-      const uint32_t nsl = g->hp_slices ? g->hp_slices
-                                        : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g->hp_gp / nb, 256));
+      const uint32_t nsl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g->hp_gp / nb, 256));
       const unsigned gr = (unsigned)std::min<uint64_t>(nb * nsl, g->hp_gp);
       if (custom) hipLaunchKernelGGL(k_hp_part<true>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl, tcnt + 4 + b);
       else hipLaunchKernelGGL(k_hp_part<false>, dim3(gr), dim3(HP_BNT), 0, st, a, lists[b] + q0[b], nb, wu, ua, g->hp_scratch, g->hp_scap, nsl, tcnt + 4 + b);
@@ -3679,6 +3728,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   // kernels' ordered accumulation and the hub pass's sort-mode items
   // (NLP_HASH_AA=0 keeps them on the sort paths, as before round 3)
   const bool custom = p.metric == M_AA || p.metric == M_RA;
+  if (t) memset(t, 0, sizeof(*t));  // every path fills its own fields
   // a synchronous call may change what an asynchronous replay would rebuild
   // (capacities, the grouping memo, the range index): only the call that ends
   // eligible below may be replayed
@@ -3761,6 +3811,7 @@ nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     t->hot_bytes = C.hot_bytes;
     t->hot_kernel = C.hot_launches ? 11u : 0u;
     t->call_bytes = path == 4 ? C.call_bytes : 0;
+    t->order_route = path == 4 ? C.route : 0u;
     t->graph_replay = 0;
   }
   return NLP_OK;
@@ -4436,9 +4487,10 @@ nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint6
   nlp_graph* g;
   nlp_status s = new_graph(device, &g);
   if (s != NLP_OK) return s;
+  BuildClock clk(g);
   g->span = span;
   g->nnz = M;
-  if (hipMalloc(&g->off, (span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(M, 1) * 4) != hipSuccess) {
+  if (hmalloc(&g->off, (span + 1) * 8) != hipSuccess || hmalloc(&g->keys, std::max<uint64_t>(M, 1) * 4) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_NOMEM;
   }
@@ -4447,7 +4499,11 @@ nlp_status nlp_graph_create(const uint64_t* offsets, const uint32_t* keys, uint6
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
-  s = finish_graph(g);
+  if (clk.mark("upload") != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g, clk);
   if (s != NLP_OK) { destroy_graph(g); return s; }
   *out = g;
   return NLP_OK;
@@ -4465,10 +4521,11 @@ nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_
   nlp_graph* g;
   nlp_status s = new_graph(device, &g);
   if (s != NLP_OK) return s;
+  BuildClock clk(g);
   g->span = span;
   g->nnz = nnz;
   hipStream_t ust = (hipStream_t)stream;
-  if (hipMalloc(&g->off, (span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(nnz, 1) * 4) != hipSuccess) {
+  if (hmalloc(&g->off, (span + 1) * 8) != hipSuccess || hmalloc(&g->keys, std::max<uint64_t>(nnz, 1) * 4) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_NOMEM;
   }
@@ -4482,7 +4539,11 @@ nlp_status nlp_graph_create_device(const uint64_t* d_offsets, const uint32_t* d_
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
-  s = finish_graph(g);
+  if (clk.mark("upload") != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g, clk);
   if (s != NLP_OK) { destroy_graph(g); return s; }
   *out = g;
   return NLP_OK;
@@ -4497,9 +4558,10 @@ static nlp_status graph_create_peer(const nlp_graph* src, int device, nlp_graph*
   nlp_graph* g;
   nlp_status s = new_graph(device, &g);
   if (s != NLP_OK) return s;
+  BuildClock clk(g);
   g->span = src->span;
   g->nnz = src->nnz;
-  if (hipMalloc(&g->off, (g->span + 1) * 8) != hipSuccess || hipMalloc(&g->keys, std::max<uint64_t>(g->nnz, 1) * 4) != hipSuccess) {
+  if (hmalloc(&g->off, (g->span + 1) * 8) != hipSuccess || hmalloc(&g->keys, std::max<uint64_t>(g->nnz, 1) * 4) != hipSuccess) {
     destroy_graph(g);
     return NLP_ERR_NOMEM;
   }
@@ -4510,7 +4572,11 @@ static nlp_status graph_create_peer(const nlp_graph* src, int device, nlp_graph*
     destroy_graph(g);
     return NLP_ERR_DEVICE;
   }
-  s = finish_graph(g);
+  if (clk.mark("upload") != hipSuccess) {
+    destroy_graph(g);
+    return NLP_ERR_DEVICE;
+  }
+  s = finish_graph(g, clk);
   if (s != NLP_OK) { destroy_graph(g); return s; }
   *out = g;
   return NLP_OK;
@@ -4603,6 +4669,33 @@ nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uin
   if (nnz) *nnz = g->nnz;
   if (max_degree) *max_degree = g->maxdeg;
   if (symmetric) *symmetric = g->symmetric ? 1 : 0;
+  return NLP_OK;
+}
+
+nlp_status nlp_set_hot_stage(nlp_graph* g, int stage) {
+  if (!g || g->is_group || g->async_pending) return NLP_ERR_INVALID;
+  if (hipSetDevice(g->device) != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess) return NLP_ERR_DEVICE;
+  if (stage != g->hot_stage) {  // captured graphs carry the old event placement
+    for (auto& c : g->graphs)
+      for (auto& x : c.exec)
+        if (x) (void)hipGraphExecDestroy(x);
+    g->graphs.clear();
+    g->async_ok = false;
+  }
+  g->hot_stage = stage < 0 ? -1 : stage;
+  return NLP_OK;
+}
+
+nlp_status nlp_graph_build_phases(const nlp_graph* g, uint32_t cap, uint32_t* n, const char** names, double* ms,
+                                  double* alloc_ms) {
+  if (!g || !n) return NLP_ERR_INVALID;
+  const nlp_graph* m = g->is_group ? g->members[0] : g;
+  *n = (uint32_t)m->build_phases.size();
+  for (uint32_t i = 0; i < *n && i < cap; ++i) {
+    if (names) names[i] = m->build_phases[i].first;
+    if (ms) ms[i] = m->build_phases[i].second;
+  }
+  if (alloc_ms) *alloc_ms = m->build_alloc_ms;
   return NLP_OK;
 }
 

@@ -308,13 +308,38 @@ __global__ __launch_bounds__(NT) void k_deg_class_hist(const uint32_t* __restric
     if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-// cursor[d] starts at the first slot of class d (relative to class 1).
+// cursor[d] starts at the first slot of class d (relative to class 1).  A
+// workgroup ranks a tile of DC_IPT x NT vertices per class in LDS and reserves
+// each class's run with ONE global atomic (a power-law degree sequence puts
+// most vertices in a few low classes: an atomic per vertex serialised on
+// those few cursors).  Order inside a class stays arbitrary.
+constexpr int DC_IPT = 16;
 __global__ __launch_bounds__(NT) void k_deg_class_scatter(const uint32_t* __restrict__ deg, uint64_t S,
                                                           unsigned long long* __restrict__ cursor,
                                                           uint32_t* __restrict__ vbydeg) {
-  for (uint64_t v = (uint64_t)blockIdx.x * NT + threadIdx.x; v < S; v += (uint64_t)gridDim.x * NT) {
-    const uint32_t d = deg[v];
-    if (d >= 1 && d <= DCAP) vbydeg[atomicAdd(&cursor[d], 1ull)] = (uint32_t)v;
+  __shared__ uint32_t cnt[DCAP + 1];
+  __shared__ unsigned long long base[DCAP + 1];
+  constexpr uint64_t TILE = (uint64_t)NT * DC_IPT;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < S; t0 += (uint64_t)gridDim.x * TILE) {
+    for (uint32_t i = threadIdx.x; i <= DCAP; i += NT) cnt[i] = 0;
+    __syncthreads();
+    uint32_t d[DC_IPT], r[DC_IPT];
+#pragma unroll
+    for (int q = 0; q < DC_IPT; ++q) {
+      const uint64_t v = t0 + (uint64_t)q * NT + threadIdx.x;
+      d[q] = v < S ? deg[v] : 0u;
+      if (d[q] >= 1 && d[q] <= DCAP) r[q] = atomicAdd(&cnt[d[q]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i <= DCAP; i += NT)
+      if (cnt[i]) base[i] = atomicAdd(&cursor[i], (unsigned long long)cnt[i]);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < DC_IPT; ++q) {
+      const uint64_t v = t0 + (uint64_t)q * NT + threadIdx.x;
+      if (d[q] >= 1 && d[q] <= DCAP) vbydeg[base[d[q]] + r[q]] = (uint32_t)v;
+    }
+    __syncthreads();
   }
 }
 

@@ -173,10 +173,22 @@ int main(int argc, char** argv) {
           cur = nx;
         }
         if (du.empty()) continue;  // main.cxx:209
+        const auto tc0 = std::chrono::steady_clock::now();
         if (host) nlp::check(nlp_graph_create(y.off.data(), y.keys.empty() ? nullptr : y.keys.data(), y.span(), device, &gh),
                              "nlp_graph_create");
         else nlp::check(nlp_graph_create_dcsr(cur, &gh), "nlp_graph_create_dcsr");
         nlp::HipGraph hg(gh);
+        {  // the per-graph build the 99 calls share (not a main.cxx line: process.js skips it)
+          const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
+          const char* names[32];
+          double pms[32], alloc = 0;
+          uint32_t np = 0;
+          nlp::check(nlp_graph_build_phases(gh, 32, &np, names, pms, &alloc), "nlp_graph_build_phases");
+          printf("graph build: %.1f ms (hipMalloc %.1f ms;", ms, alloc);
+          for (uint32_t i = 0; i < np && i < 32; ++i) printf(" %s %.1f", names[i], pms[i]);
+          printf(")\n");
+          fflush(stdout);
+        }
         nlp::check(nlp_set_truth(hg.get(), du.data(), dv.data(), du.size()), "nlp_set_truth");
         struct Del { size_t n; size_t size() const { return n; } } del{du.size()};
         const size_t k = del.size() / 2;  // insertions0.size() / 2 (main.cxx:50)

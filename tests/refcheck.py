@@ -13,7 +13,10 @@ The reference's tie order depends on its OpenMP schedule (predict.hxx:287,
   2. the same set of links strictly above the k-th score;
   3. every link at the k-th score (ours and the reference's) is in the
      reference's own tie set -- ALL its candidates at that score, taken from a
-     second reference call with maxEdges = |above| + |ties|;
+     second reference call with maxEdges = |above| + |ties| + 1 (our count of
+     links at or above the k-th score, plus one): that call must come back
+     with a link below the k-th score (or with fewer links than asked, every
+     candidate), which proves the tie set complete whatever our count was;
   4. F1 (main.cxx:48-57, 199-206) of both lies within the tie bounds: the
      r = k - |above| boundary links chosen from the tie set T to minimise /
      maximise the matches with the deletions.
@@ -103,11 +106,13 @@ def gpu_links(out_t, n):
     return o[:, 0].long() & 0xffffffff, o[:, 1].long() & 0xffffffff, o[:, 2].contiguous().view(__import__("torch").float32)
 
 
-def check_contract(gpu, ref_k, ref_ge, k, del_u, del_w, dev="cuda"):
+def check_contract(gpu, ref_k, ref_ge, k, del_u, del_w, dev="cuda", asked=None):
     """Contract 1-4 of the module docstring.  gpu = device tensors (u, w, s);
     ref_k, ref_ge = numpy (u, w, s) of the reference's maxEdges = k call and
-    of its call with maxEdges = |above| + |ties|; del_u / del_w = the directed
-    deletions (both directions).  Returns the numbers of the check."""
+    of its tie-set call, which asked for `asked` links (None: ref_ge is the
+    exact set at or above the k-th score, as the CPU fixtures cut it); del_u /
+    del_w = the directed deletions (both directions).  Returns the numbers of
+    the check."""
     import torch
     gu, gw, gs = gpu
     ru, rw, rs = (_t(x, dev) for x in ref_k[:3])
@@ -123,7 +128,13 @@ def check_contract(gpu, ref_k, ref_ge, k, del_u, del_w, dev="cuda"):
     ra = torch.sort(pk(ru, rw)[rk > kth]).values
     assert torch.equal(ga, ra), "above-boundary sets differ (%d vs %d)" % (ga.numel(), ra.numel())
     # the reference's whole tie set at the k-th score
-    assert int(ek.min()) >= kth, "the maxEdges = |A| + |T| reference call returned links below the k-th score"
+    if asked is not None:
+        # asked = our count at or above the k-th score + 1: a complete set leaves room for one link below it
+        assert ek.numel() < asked or int(ek.min()) < kth, \
+            "the reference has more links at or above the k-th score than our output: a candidate was lost"
+        keep = ek >= kth
+        eu, ew, es, ek = eu[keep], ew[keep], es[keep], ek[keep]
+    assert int(ek.min()) >= kth, "the tie-set call returned links below the k-th score"
     ea = torch.sort(pk(eu, ew)[ek > kth]).values
     assert torch.equal(ea, ra), "the two reference calls disagree above the k-th score"
     T = torch.sort(pk(eu, ew)[ek == kth]).values
@@ -191,8 +202,8 @@ def run_reference_check(c, csr, metric, H, name):
     del out2, k2
     torch.cuda.empty_cache()
     ref_k = ref_predict(csr, metric, H, c.k)
-    ref_ge = ref_predict(csr, metric, H, n_ge)
-    res = check_contract(gpu, ref_k, ref_ge, c.k, c.del_u, c.del_w)
+    ref_ge = ref_predict(csr, metric, H, n_ge + 1)
+    res = check_contract(gpu, ref_k, ref_ge, c.k, c.del_u, c.del_w, asked=n_ge + 1)
     res.update(config=name, metric=metric, H=H, candidates=int(t["candidates"]), wedges=int(t["wedges"]), path=t["path"],
                ref_threads=REF_THREADS, ref_time_ms=ref_k[3]["time_ms"], ref_ge_time_ms=ref_ge[3]["time_ms"],
                gpu_ms=t["total_ms"])

@@ -34,6 +34,26 @@ def test_refcheck_accepts_the_oracle(oracle, m, H):
     assert r["ties_total"] >= r["ties_taken"]
 
 
+@pytest.mark.parametrize("m,H", [(1, 8), (7, 8)])
+def test_refcheck_tie_set_call_with_one_more(oracle, m, H):
+    """The full-size form: the tie-set call asks for |at or above| + 1 links and
+    gets one below the k-th score -- accepted; asked for exactly |at or above|
+    (as if our output had lost a candidate, so our count is one short), every
+    link it returns is at or above the k-th score -- rejected."""
+    g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", m, H)
+    tag = "%d_%d" % (m, H)
+    cu, cw, cs = g["cand_%s_u" % tag], g["cand_%s_w" % tag], g["cand_%s_s" % tag]
+    kth = refcheck.keys_t(torch.as_tensor(ref_k[2])).min()
+    below = (refcheck.keys_t(torch.as_tensor(cs)) < kth).numpy()
+    j = int(np.nonzero(below)[0][0])
+    plus = tuple(np.concatenate([a, b[j:j + 1]]) for a, b in zip(ref_ge, (cu, cw, cs)))
+    r = refcheck.check_contract(gpu, ref_k, plus, k, g["del_u"], g["del_w"], dev="cpu", asked=len(plus[0]))
+    assert r["ties_total"] >= r["ties_taken"]
+    short = tuple(a[:-1] for a in ref_ge)  # one tie fewer: our count would have been one short
+    with pytest.raises(AssertionError):
+        refcheck.check_contract(gpu, ref_k, short, k, g["del_u"], g["del_w"], dev="cpu", asked=len(short[0]))
+
+
 def test_refcheck_rejects_wrong_results(oracle):
     g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", 1, 8)
     u, w, s = gpu
