@@ -74,6 +74,27 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+HBM_CLEAR_GBS = 25.0  # the driver clears freed HBM at ~33 GB/s (tools/probe/alloc_probe2.hip, r06): 25 to be safe
+
+
+def release_cached(what):
+    """Hand torch's cached blocks back to the driver and wait until it has
+    cleared them.  The driver wipes freed HBM asynchronously (~33 GB/s on the
+    box, tools/probe/alloc_probe2.hip); a hipMalloc that needs more than the
+    never-used memory WAITS for that wipe (measured: 4.8 s after freeing 160 GB;
+    2.4 s inside the round-6 graph build's membership table).  The wait belongs
+    to whoever freed the memory, not to the graph build that follows, so the
+    settle is timed with the freeing step (graph generation).  Returns the GB
+    released."""
+    before = torch.cuda.memory_reserved()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    gb = (before - torch.cuda.memory_reserved()) / 1e9
+    time.sleep(gb / HBM_CLEAR_GBS)
+    log("bench: %s: %.1f GB of torch's cache released, %.1f s for the driver to clear it" % (what, gb, gb / HBM_CLEAR_GBS))
+    return gb
+
+
 def f1_on_device(G, out, n, du, dw):
     """main.cxx:48-57,199-206: P = |ins1 ∩ del0| / |ins1|, R = ... / |del0|, with
     |ins1 ∩ del0| counted by the library's evaluation kernel (nlp_set_truth,
@@ -391,8 +412,7 @@ def main():
     spec = (n, m, alpha, seed, d, metric, hub)  # strong scaling: the same graph on every rank
     t0 = time.time()
     off, keys, du, dw, info = gg.make_workload(spec, "cuda")
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()  # hand the generator's cached blocks back: libnlp allocates with hipMalloc
+    released_gb = release_cached("graph generation")  # libnlp allocates with hipMalloc
     gen_s = time.time() - t0
     t0 = time.time()
     G = nlp.Graph.from_device(off, keys)
@@ -525,6 +545,7 @@ def main():
             "wedges": int(timing.get("wedges", 0)), "candidates": int(timing.get("candidates", 0)),
             "path": timing.get("path"),
             "graph_gen_s": gen_s,
+            "graph_gen_released_gb": released_gb,
             "graph_create_s": create_s,
             "graph_create_phases_ms": phases,
             # graph_create amortised over main.cxx's 99 calls per batch graph (value's time)
@@ -561,6 +582,12 @@ def main():
                 except Exception as e:
                     wp["cpu_baseline"] = {"error": repr(e)}
             if csr is not None and not args.no_dropin:
+                # the drop-in builds its own copy of the graph in another process: hand this
+                # one's HBM back first and let the driver clear it (see release_cached)
+                free0 = torch.cuda.mem_get_info()[0]
+                G.close()
+                freed = max(0, torch.cuda.mem_get_info()[0] - free0) / 1e9
+                time.sleep(freed / HBM_CLEAR_GBS)
                 line["dropin"] = dropin_bench(csr, k, [hub] + ([wp["H"]] if wp is not None else []))
             if tmpd is not None:
                 tmpd.cleanup()

@@ -169,7 +169,7 @@ nlp_status nlp_graph_info(const nlp_graph* g, uint64_t* span, uint64_t* nnz, uin
  * (names[i], ms[i]): host wall time with the device stream drained at every
  * phase boundary, so the phases sum to the create call's time.  *alloc_ms
  * (may be NULL) is the part of that time spent inside hipMalloc.  Names:
- * upload, degrees, transpose, degree_class_index, row_index, entry_classes,
+ * upload, degrees, row_index, transpose, degree_class_index, entry_classes,
  * short_lists, membership_table, edge_filter, tables_and_setup. */
 nlp_status nlp_graph_build_phases(const nlp_graph* g, uint32_t cap, uint32_t* n, const char** names, double* ms,
                                   double* alloc_ms);

@@ -887,7 +887,9 @@ __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __res
 // tpre: exclusive prefix of the tile counts (tile - t0 indexed)
 // Per graph: for every entry e = (u -> v) with deg v <= 254, the number of
 // entries of N(v) at or below u (its rank there; u8) -- the survivor lists'
-// fill reads it instead of searching N(v) on every call.
+// fill reads it instead of searching N(v) on every call.  (Searching a lane's
+// eight entries together, one branchless step of all of them at a time,
+// measured slower: 240 -> 375 ms for the entry-class phase on C4.)
 __global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __restrict__ dcls, uint64_t S,
                                                  uint64_t M, const uint32_t* __restrict__ tile_row,
                                                  uint8_t* __restrict__ out) {
@@ -930,6 +932,46 @@ __global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __r
         if (g.keys[o + md] <= u) l = md + 1; else h = md;
       }
       out[e] = (uint8_t)l;
+    }
+  }
+}
+
+// (v << 32 | u) for every entry u -> v, in CSR order (the transposed build's
+// sort input): edge-parallel over HP_WTILE-entry tiles, each entry's row from
+// its tile's first row (tile_row) by a search of 64 row ends held in lanes
+// (a binary search of all offsets per entry cost ~85 ms on C4).
+__global__ __launch_bounds__(NT) void k_transpose_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
+                                                       uint64_t S, uint64_t M, const uint32_t* __restrict__ tile_row,
+                                                       uint64_t* __restrict__ out) {
+  const int lane = lane_id(), wv = wave_id();
+  const uint64_t nt = (M + HP_WTILE - 1) / HP_WTILE;
+  for (uint64_t tile = (uint64_t)blockIdx.x * NWAVE + wv; tile < nt; tile += (uint64_t)gridDim.x * NWAVE) {
+    const uint64_t base = tile * HP_WTILE;
+    const uint64_t r0 = tile_row[tile];
+    const uint64_t rl = r0 + lane;
+    const uint64_t rend = rl < S ? off[rl + 1] : ~0ull;
+    const uint64_t last_end = __shfl(rend, 63, 64);
+#pragma unroll 1
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      const uint32_t w = e < M ? keys[e] : 0u;
+      int lo = 0, hi = 64;
+      while (lo < hi) {
+        const int md = (lo + hi) >> 1;
+        const uint64_t x = __shfl(rend, md, 64);
+        if (x <= e) lo = md + 1; else hi = md;
+      }
+      if (e >= M) continue;
+      uint64_t r = r0 + lo;
+      if (e >= last_end) {
+        uint64_t a = r0, b = S;
+        while (b - a > 1) {
+          const uint64_t md = (a + b) >> 1;
+          if (off[md] <= e) a = md; else b = md;
+        }
+        r = a;
+      }
+      out[e] = ((uint64_t)w << 32) | r;
     }
   }
 }

@@ -195,27 +195,35 @@ __global__ void k_degrees(const uint64_t* __restrict__ off, uint64_t span, uint3
   }
 }
 
-// keys must be < span and sorted ascending inside each row
-__global__ void k_check_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
-                             uint64_t nnz, uint32_t* __restrict__ bad) {
+// keys must be < span and sorted ascending inside each row.  A descent
+// keys[e + 1] < keys[e] is legal only where e + 1 starts a row, so the
+// descents over all entries (desc[0], counted here) must equal the descents at
+// the starts of non-empty rows (desc[1], k_row_descents): two streaming counts
+// instead of a search of the offsets at every descent.
+__global__ void k_check_keys(const uint32_t* __restrict__ keys, uint64_t span, uint64_t nnz, uint32_t* __restrict__ bad,
+                             unsigned long long* __restrict__ desc) {
+  uint64_t c = 0;
   for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t k = keys[e];
+    const uint32_t k = keys[e];
     if (k >= span) atomicOr(bad, 4u);
-    if (e + 1 < nnz && keys[e + 1] < k) {
-      // a descent is only legal at a row boundary
-      uint64_t u = lbs_find(off, span + 1, e);
-      if (off[u + 1] != e + 1) atomicOr(bad, 8u);
-    }
+    if (e + 1 < nnz && keys[e + 1] < k) ++c;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&desc[0], (unsigned long long)c);
 }
 
-// (v << 32 | u) for every edge u -> v; row u found by binary search on offsets
-__global__ void k_transpose_keys(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
-                                 uint64_t nnz, uint64_t* __restrict__ out) {
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t u = lbs_find(off, span + 1, e);
-    out[e] = ((uint64_t)keys[e] << 32) | u;
+__global__ void k_row_descents(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys, uint64_t span,
+                               uint64_t nnz, unsigned long long* __restrict__ desc) {
+  uint64_t c = 0;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < span; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = off[u];
+    // one non-empty row starts at a position (offsets not yet validated: reads stay below nnz)
+    if (a > 0 && a < nnz && off[u + 1] > a && keys[a] < keys[a - 1]) ++c;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&desc[1], (unsigned long long)c);
 }
 
 // I(v) from the (v << 32 | u) keys sorted by v (u ascending inside a v, the

@@ -84,13 +84,17 @@ enum Buf {
 
 // Graph build timing (nlp_graph_build_phases): while a build runs, the time
 // spent inside hipMalloc accumulates here (null: not timed).
+// NLP_BUILD_TRACE=1: every such allocation (bytes, ms) on stderr (diagnostic).
 thread_local double* t_alloc_ms = nullptr;
 template <typename T>
 hipError_t hmalloc(T** p, size_t bytes) {
   if (!t_alloc_ms) return hipMalloc((void**)p, bytes);
   const auto t0 = std::chrono::steady_clock::now();
   const hipError_t e = hipMalloc((void**)p, bytes);
-  *t_alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *t_alloc_ms += ms;
+  static const bool trace = getenv("NLP_BUILD_TRACE") && getenv("NLP_BUILD_TRACE")[0] == '1';
+  if (trace) fprintf(stderr, "nlp build: hipMalloc %.3f GB %.1f ms\n", bytes / 1e9, ms);
   return e;
 }
 
@@ -611,15 +615,19 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   TRY(hmalloc(&g->deg, std::max<uint64_t>(S, 1) * 4));
   LAUNCH(k_degrees, S, st, g->off, S, g->deg, flags + 1, flags);
   TRY(hipGetLastError());
+  unsigned long long* desc = (unsigned long long*)(flags + 4);  // [0] all descents, [1] at row starts
   if (M) {
-    LAUNCH(k_check_keys, M, st, g->off, g->keys, S, M, flags);
+    LAUNCH(k_check_keys, M, st, g->keys, S, M, flags, desc);
+    LAUNCH(k_row_descents, S, st, g->off, g->keys, S, M, desc);
     TRY(hipGetLastError());
   }
-  TRY(hipMemcpyAsync(g->host_small, flags, 8, hipMemcpyDeviceToHost, st));
+  TRY(hipMemcpyAsync(g->host_small, flags, 32, hipMemcpyDeviceToHost, st));
   TRY(hipStreamSynchronize(st));
-  uint32_t hf[2];
-  memcpy(hf, g->host_small, 8);
-  if (hf[0]) return NLP_ERR_INVALID;
+  uint32_t hf[8];
+  memcpy(hf, g->host_small, 32);
+  uint64_t hd[2];
+  memcpy(hd, hf + 4, 16);
+  if (hf[0] || hd[0] != hd[1]) return NLP_ERR_INVALID;
   g->maxdeg = hf[1];
   // the offsets must also start at 0 and end at nnz
   uint64_t ends[2];
@@ -627,6 +635,24 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   TRY(hipMemcpy(&ends[1], g->off + S, 8, hipMemcpyDeviceToHost));
   if (ends[0] != 0 || ends[1] != M) return NLP_ERR_INVALID;
   TRY(clk.mark("degrees"));
+  // per row the entries of N(u) at or below u: the first-order exclusion only
+  // marks x > u (predict.hxx:306-307 zeroes all of N(u), but only w > u are
+  // candidates), so path 4's row kernels walk N(u) from there
+  if (S > 0 && !(getenv("NLP_HASH_XS") && getenv("NLP_HASH_XS")[0] == '0')) {
+    if (hmalloc(&g->xs, S * 4) == hipSuccess) {
+      LAUNCH(k_hp_xs, S, st, (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->xs);
+      TRY(hipGetLastError());
+    } else {
+      (void)hipGetLastError();
+      g->xs = nullptr;
+    }
+  }
+  // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
+  TRY(hmalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
+  TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
+  LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
+  TRY(hipGetLastError());
+  TRY(clk.mark("row_index"));
 
   // Transposed adjacency I(v): stable radix sort of (v << 32 | u).
   g->symmetric = true;
@@ -645,7 +671,9 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     uint32_t* tkeys;
     TRY(hmalloc(&toff, (S + 1) * 8));
     TRY(hmalloc(&tkeys, M * 4));
-    LAUNCH(k_transpose_keys, M, st, g->off, g->keys, S, M, k0);
+    const unsigned gk = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 65536);
+    hipLaunchKernelGGL(k_transpose_keys, dim3(gk), dim3(NT), 0, st, (const uint64_t*)g->off, (const uint32_t*)g->keys,
+                       S, M, (const uint32_t*)g->tile_row, k0);
     TRY(hipGetLastError());
     // the keys come in CSR order (u ascending), so a stable sort on the v bytes
     // alone leaves every I(v) sorted by u: half the passes of a full key sort
@@ -673,6 +701,9 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
       TRY(hipFree(tkeys));
     }
   }
+  // the sort's scratch (2 x 8 B per entry) goes back now: the build's later
+  // arrays (the membership table above all) reuse its pages
+  g->ws.release();
   TRY(clk.mark("transpose"));
   // Degree-class index: survivors of any H <= DCAP without a pass over deg[].
   {
@@ -732,24 +763,6 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     TRY(hipStreamSynchronize(st));
   }
   TRY(clk.mark("degree_class_index"));
-  // per row the entries of N(u) at or below u: the first-order exclusion only
-  // marks x > u (predict.hxx:306-307 zeroes all of N(u), but only w > u are
-  // candidates), so path 4's row kernels walk N(u) from there
-  if (S > 0 && !(getenv("NLP_HASH_XS") && getenv("NLP_HASH_XS")[0] == '0')) {
-    if (hmalloc(&g->xs, S * 4) == hipSuccess) {
-      LAUNCH(k_hp_xs, S, st, (const uint64_t*)g->off, (const uint32_t*)g->keys, S, g->xs);
-      TRY(hipGetLastError());
-    } else {
-      (void)hipGetLastError();
-      g->xs = nullptr;
-    }
-  }
-  // row of every HP_WTILE-entry adjacency tile (path 4's edge-parallel work estimate)
-  TRY(hmalloc(&g->tile_row, (M / HP_WTILE + 2) * 4));
-  TRY(hipMemsetAsync(g->tile_row, 0, (M / HP_WTILE + 2) * 4, st));
-  LAUNCH(k_hp_tile_rows, S, st, (const uint64_t*)g->off, S, g->tile_row);
-  TRY(hipGetLastError());
-  TRY(clk.mark("row_index"));
   // degree class of every adjacency entry: path 4 filters N(u) by it (coalesced
   // bytes instead of a degree gather per entry) to build the survivor lists S(u)
   const char* hdc = getenv("NLP_HASH_DCLS");

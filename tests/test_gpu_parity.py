@@ -199,6 +199,11 @@ def test_gpu_invalid_inputs(gpu):
         gpu.Graph(np.array([0, 2, 3], np.uint64), np.array([1, 0, 0], np.uint32))  # unsorted row
     with pytest.raises(gpu.NlpError):
         gpu.Graph(np.array([0, 2, 1], np.uint64), np.array([1, 0], np.uint32))  # offsets decrease
+    # descents at row starts are legal, one inside a row is not (the build counts both kinds)
+    with gpu.Graph(np.array([0, 2, 4, 5], np.uint64), np.array([1, 2, 0, 2, 1], np.uint32)) as G:
+        assert G.info()["nnz"] == 5
+    with pytest.raises(gpu.NlpError):
+        gpu.Graph(np.array([0, 2, 4, 5], np.uint64), np.array([1, 2, 2, 0, 1], np.uint32))
 
 
 def test_gpu_reference_api_names(gpu, golden):

@@ -1,0 +1,43 @@
+"""Graph build timing on a full-size config (diagnostic): generate the config's
+stand-in on the device as bench.py does, hand torch's cached blocks back, build
+the graph handle, print the create wall time and nlp_graph_build_phases.
+NLP_BUILD_TRACE=1 adds every build allocation on stderr.
+
+    python tools/create_probe.py [--config C4-sk-2005] [--repeat 2]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import nlp_loader  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C4-sk-2005")
+    ap.add_argument("--repeat", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    nlp = nlp_loader.load()
+    gg = nlp_loader.load_sub("graphgen")
+    t0 = time.time()
+    off, keys, du, dw, info = gg.make_workload(args.config, "cuda")
+    from bench import release_cached, HBM_CLEAR_GBS
+    release_cached("graph generation")
+    print(json.dumps({"config": args.config, "gen_s": time.time() - t0, "M": int(keys.numel())}), flush=True)
+    for r in range(args.repeat):
+        t0 = time.time()
+        G = nlp.Graph.from_device(off, keys)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        print(json.dumps({"create_s": dt, "phases_ms": G.build_phases()}), flush=True)
+        free0 = torch.cuda.mem_get_info()[0]
+        G.close()
+        time.sleep(max(0, torch.cuda.mem_get_info()[0] - free0) / 1e9 / HBM_CLEAR_GBS)  # the driver's clear
+
+
+if __name__ == "__main__":
+    main()
