@@ -205,6 +205,7 @@ def run_reference_check(c, csr, metric, H, name):
     ref_ge = ref_predict(csr, metric, H, n_ge + 1)
     res = check_contract(gpu, ref_k, ref_ge, c.k, c.del_u, c.del_w, asked=n_ge + 1)
     res.update(config=name, metric=metric, H=H, candidates=int(t["candidates"]), wedges=int(t["wedges"]), path=t["path"],
+               chunks=int(t["chunks"]), order_route=int(t.get("order_route", 0)),
                ref_threads=REF_THREADS, ref_time_ms=ref_k[3]["time_ms"], ref_ge_time_ms=ref_ge[3]["time_ms"],
                gpu_ms=t["total_ms"])
     rd = os.environ.get("NLP_TEST_REPORT_DIR")

@@ -525,10 +525,12 @@ def test_gpu_final_prune_folded_into_order(gpu, oracle):
     """The call's last prune folded into the 8-byte order (hp_prune fuse: the
     keys >= the k-th sorted straight from the unpruned buffer, the first k
     written -- the canonical tie rule is the sort order): Jaccard with few
-    ties takes it, Adamic-Adar (too many distinct scores for 8-byte keys) and
-    Common Neighbours (a tie set far beyond k) fall back to the split; every
-    result exact against the oracle, one and several chunks."""
+    ties takes it (nlp_timing.order_route = NLP_ORDER_FOLD8), Adamic-Adar is
+    never offered the fold (nearly every score distinct: pruned, then
+    ordered), Common Neighbours (a tie set far beyond k) falls back to the
+    split; every result exact against the oracle, one and several chunks."""
     off, keys = random_csr(20000, 16, 41)
+    routes = {}
     for env in (dict(), dict(NLP_HASH_EMIT="300000")):
         with _env(NLP_HASH="1", **env):
             with gpu.Graph(off, keys) as G:
@@ -537,8 +539,12 @@ def test_gpu_final_prune_folded_into_order(gpu, oracle):
                         for k in (70000, 250000):
                             u, w, s, t = G.predict(m, H, k)
                             assert t["path"] == 4
+                            routes.setdefault(m, set()).add(t["order_route"])
                             eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
                             assert_canonical_equal(eu, ew, es, u, w, s)
+    assert 1 in routes[1], routes                 # Jaccard: the fold
+    assert not routes[7] & {1, 2}, routes         # Adamic-Adar: never folded
+    assert all(r in (1, 2, 3, 4) for rs in routes.values() for r in rs), routes
 
 
 def test_gpu_hash_routing_and_shards(gpu, oracle):

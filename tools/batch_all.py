@@ -73,7 +73,8 @@ def main():
             dst.to(torch.int32).cpu().numpy().tofile(f)
         del src, dst
         torch.cuda.empty_cache()
-        mw = os.path.join(tmp.name, "mtxwrite")
+        bindir = tempfile.mkdtemp()  # /dev/shm may be mounted noexec
+        mw = os.path.join(bindir, "mtxwrite")
         subprocess.run(["gcc", "-O2", "-o", mw, os.path.join(ROOT, "tools", "mtxwrite.c")], check=True)
         mtx = os.path.join(tmp.name, "g.mtx")
         subprocess.run([mw, pb, str(n), mtx], check=True)
@@ -119,7 +120,18 @@ def main():
                 np.array([len(o) - 1, keys.numel()], np.uint64).tofile(f)
                 o.tofile(f)
                 keys.cpu().numpy().view(np.uint32).tofile(f)
-            del off, keys, du, dw
+            # maxEdges capped at the candidate count (from our own call): above it the
+            # reference's OpenMP merge reads past its per-thread lists
+            nlp = nlp_loader.load()
+            G = nlp.Graph.from_device(off, keys)
+            outb = torch.empty((max(k, 1), 3), dtype=torch.int32, device="cuda")
+            ncand = {}
+            for mi in range(len(METRICS)):
+                for h in (int(x) for x in args.hubs.split(",")):
+                    _, t = G.predict_device(mi, h, k, outb)
+                    ncand[(mi, h)] = int(t["candidates"])
+            G.close()
+            del off, keys, du, dw, outb
             torch.cuda.empty_cache()
             threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
             ref = []
@@ -130,7 +142,8 @@ def main():
                     if left <= 5:
                         break
                     try:
-                        rr = subprocess.run([drv, "time", csr, str(mi), str(h), str(k), str(threads), "1"],
+                        me = max(1, min(k, ncand[(mi, h)]))
+                        rr = subprocess.run([drv, "time", csr, str(mi), str(h), str(me), str(threads), "1"],
                                             capture_output=True, text=True, timeout=left,
                                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)))
                     except subprocess.TimeoutExpired:
