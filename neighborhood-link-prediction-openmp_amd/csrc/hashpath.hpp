@@ -54,6 +54,7 @@ struct HpArgs {
   GraphView g;
   uint64_t S;
   uint32_t H;
+  uint32_t ctn;       // entries of g.ctab (max degree + 1): the AA / RA contribution table
   int metric;
   float min_score;
   uint32_t* ckey;     // candidate columns (score key, u, w, score)
@@ -1890,6 +1891,7 @@ __global__ __launch_bounds__(NT) void k_hp_wave(HpArgs a, const uint32_t* __rest
 constexpr uint64_t HB_ROWCOST = 5;  // budget units per row besides its wedges (bounds the rows per batch)
 
 constexpr int HB_UN = 8;            // loads per lane in flight in the batch loops (a batch is a few round trips)
+constexpr int HB_EP = 4;            // membership-table probes in flight per lane in the batch drain
 
 // The rows of tiers tlo..thi: a contiguous region of the tier list.
 __device__ __forceinline__ void hb_region(const uint32_t* tcnt, int tlo, int thi, uint32_t* base, uint32_t* cnt) {
@@ -2317,13 +2319,15 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
       // measured slower: C4 JAC H=16 43.4 -> 48.1 ms, the kernel 13.9 -> 9.7 ms
       // but the deferred probes ~9 ms -- a random 64-byte line per test, no
       // longer hidden behind the batches' own latency)
+      // (count tables: HB_EP first buckets in flight at a time)
+      constexpr int EP = CUSTOM ? 2 : HB_EP;
 #pragma unroll
-      for (int q0 = 0; q0 < UN; q0 += 2) {
+      for (int q0 = 0; q0 < UN; q0 += EP) {
         if ((uint32_t)q0 >= nq) break;
-        uint64_t ek[2];
-        bool ea[2], er[2];
+        uint64_t ek[EP];
+        bool ea[EP], er[EP];
 #pragma unroll
-        for (int z = 0; z < 2; ++z) {
+        for (int z = 0; z < EP; ++z) {
           const int q = q0 + z;
           const bool valid = q < UN && (uint32_t)q < nq && kq[q] != HP_EMPTY;
           const uint32_t sl = valid ? kq[q] >> wbits : 0u;
@@ -2332,12 +2336,12 @@ __global__ __launch_bounds__(NT, MW) void k_hp_batch(HpArgs a, const uint32_t* _
         }
         if (CUSTOM) {
 #pragma unroll
-          for (int z = 0; z < 2; ++z) er[z] = ea[z] && et_has(a.g.etab, a.g.etbits, (uint32_t)(ek[z] >> 32), (uint32_t)ek[z]);
+          for (int z = 0; z < EP; ++z) er[z] = ea[z] && et_has(a.g.etab, a.g.etbits, (uint32_t)(ek[z] >> 32), (uint32_t)ek[z]);
         } else {
-          et_has_n<2>(a.g.etab, a.g.etbits, ek, ea, er);
+          et_has_n<EP>(a.g.etab, a.g.etbits, ek, ea, er);
         }
 #pragma unroll
-        for (int z = 0; z < 2; ++z) {
+        for (int z = 0; z < EP; ++z) {
           if (q0 + z >= UN) break;
           etq += ea[z] ? 1 : 0;
           if (er[z]) c[q0 + z] |= HP_EXCL;
@@ -3876,6 +3880,7 @@ __device__ __forceinline__ void block_bitonic_u64(uint64_t* s, uint32_t n) {
 // Sort-mode keys: (w - slo) << 38 | v << 12 | min(deg v, 4095) (w - slo, v < 2^26)
 constexpr int HS_WSH = 38;
 constexpr uint32_t HS_DMAX = 4095;
+constexpr int HS_CT = 256;  // contributions cached in LDS by k_hh_accum's sort mode
 
 // sortmode (AA / RA, items of at most HH_SCAP wedges unless flagged HH_BIG): an
 // item's wedges are loaded as (w, v, deg v) keys into LDS (over the vmin / vmax
@@ -3904,7 +3909,14 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   __shared__ uint64_t s_item[8];  // the next item (8 words), loaded while this one runs
   __shared__ uint32_t s_tk[2];
   __shared__ uint32_t s_n;
+  // AA / RA sort mode: the contributions c(d) of the degrees below HS_CT in
+  // LDS -- every first hop of an LHub call up to H = 255 -- so a run's sum
+  // waits on no global load (one dependent L2 round trip per run start was
+  // the sort mode's critical path)
+  __shared__ double s_ct[CUSTOM ? HS_CT : 1];
   const int t = threadIdx.x, wv = wave_id();
+  if (CUSTOM)
+    for (int i = t; i < HS_CT; i += HH_NT) s_ct[i] = (uint32_t)i < a.ctn ? a.g.ctab[i] : 0.0;
   uint32_t* const s_v0 = (uint32_t*)s_vv;
   uint32_t* const s_v1 = (uint32_t*)s_vv + (CUSTOM ? LT : 0);
   const HpTable tb{s_k, s_c, s_v0, s_v1};
@@ -4004,7 +4016,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
           for (uint32_t j = i; j < m && (sk[j] >> HS_WSH) == wl; ++j) {
             uint32_t d = (uint32_t)(sk[j] & 0xfffu);
             if (d == HS_DMAX) d = a.g.deg[(uint32_t)(sk[j] >> 12) & 0x3ffffffu];
-            acc = (float)((double)acc + a.g.ctab[d]);
+            acc = (float)((double)acc + (d < (uint32_t)HS_CT ? s_ct[d] : a.g.ctab[d]));
           }
           s = s_ex[i] ? 0.0f : acc;
           w = (uint32_t)(slo + wl);

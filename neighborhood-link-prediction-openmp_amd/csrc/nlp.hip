@@ -2371,6 +2371,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     const uint64_t wchunk = g->host_small[41] - g->host_small[40];
     HpArgs a{};
     a.g = gv;
+    a.ctn = g->maxdeg + 1;
     a.S = S;
     a.H = p.H;
     a.metric = p.metric;

@@ -54,6 +54,23 @@ def test_refcheck_tie_set_call_with_one_more(oracle, m, H):
         refcheck.check_contract(gpu, ref_k, short, k, g["del_u"], g["del_w"], dev="cpu", asked=len(short[0]))
 
 
+def test_refcheck_single_reference_call(oracle):
+    """The one-call form (the tie-set call alone stands for the reference's
+    top-k): accepted for the oracle's result, a changed score rejected."""
+    g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", 1, 8)
+    cu, cw, cs = g["cand_1_8_u"], g["cand_1_8_w"], g["cand_1_8_s"]
+    kth = refcheck.keys_t(torch.as_tensor(ref_k[2])).min()
+    j = int(np.nonzero((refcheck.keys_t(torch.as_tensor(cs)) < kth).numpy())[0][0])
+    plus = tuple(np.concatenate([a, b[j:j + 1]]) for a, b in zip(ref_ge, (cu, cw, cs)))
+    r = refcheck.check_contract(gpu, None, plus, k, g["del_u"], g["del_w"], dev="cpu", asked=len(plus[0]))
+    assert r["common_ref"] is None and r["f1_lo"] <= r["f1_gpu"] <= r["f1_hi"]
+    u, w, s = gpu
+    s2 = s.clone()
+    s2[0] = torch.nextafter(s2[0], torch.tensor(0.0))
+    with pytest.raises(AssertionError):
+        refcheck.check_contract((u, w, s2), None, plus, k, g["del_u"], g["del_w"], dev="cpu", asked=len(plus[0]))
+
+
 def test_refcheck_rejects_wrong_results(oracle):
     g, k, gpu, ref_k, ref_ge = _case(oracle, "g3k", 1, 8)
     u, w, s = gpu
