@@ -48,7 +48,9 @@ constexpr int HP_NBINS = 4;
 // per-chunk counters (u64)
 // HPC_HOTB: algorithmic bytes of the chunk's k_hp_batch launch, counted by the kernel;
 // HPC_PAD: padding entries written into the unused tails of emission windows (hp_flush)
-enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_HOTB = 5, HPC_PAD = 6, HPC_NCTR = 8 };
+// HPC_BIGW: wedges of the hub pass's HH_BIG items (AA / RA hash tables with the ordered re-walk; diagnostic)
+enum { HPC_EMIT = 0, HPC_CAND = 1, HPC_NAN = 2, HPC_WEDGE = 3, HPC_ERR = 4, HPC_HOTB = 5, HPC_PAD = 6, HPC_BIGW = 7,
+       HPC_NCTR = 8 };
 
 struct HpArgs {
   GraphView g;
@@ -3943,6 +3945,15 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   uint32_t cur = s_tk[0], nx = s_tk[1];
   if (t < 8 && cur < ni) s_item[t] = ((const uint64_t*)(items + cur))[t];
   __syncthreads();
+  // diagnostic (NLP_TRACE_HUB=1): the sort mode's phase times, thread 0's clock between barriers
+  uint64_t ph_t = 0, ph_acc[4] = {0, 0, 0, 0};
+  auto hh_mark = [&](int i) {
+    if (a.ph && t == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (i >= 0) ph_acc[i] += now - ph_t;
+      ph_t = now;
+    }
+  };
   auto run = [&](const HhItem& item) {
     // a heavy bucket's item reads its own partitioned wedges
     const bool part = (item.cnt & HH_PART) != 0;
@@ -3952,10 +3963,12 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     const uint64_t off = item.off, du = item.du, x0 = item.x0, x1 = item.x1;
     const bool whole = (item.cnt & HH_WHOLE) != 0;
     const uint64_t slo = item.slo, shi = item.shi;
+    if (CUSTOM && (item.cnt & HH_BIG) && t == 0) atomicAdd(&a.ctr[HPC_BIGW], (unsigned long long)n);
     if (CUSTOM && sortmode && !(item.cnt & HH_BIG)) {
       uint64_t* const sk = s_vv;
       if (t == 0) s_n = 0;
       __syncthreads();
+      hh_mark(-1);
       for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
         uint32_t wq[HP_UN], vq[HP_UN], dq[HP_UN];
         bool in[HP_UN];
@@ -3986,12 +3999,14 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         }
       }
       __syncthreads();
+      hh_mark(0);  // wedges loaded and appended
       const uint32_t m = s_n < HH_SCAP ? s_n : HH_SCAP;
       const uint32_t m2 = pow2_at_least(m);
       for (uint32_t i = m + t; i < m2; i += HH_NT) sk[i] = ~0ull;
       for (uint32_t i = t; i < m2; i += HH_NT) s_ex[i] = 0;
       __syncthreads();
       block_bitonic_u64<HH_NT>(sk, m2);
+      hh_mark(1);  // sorted
       // first-order exclusion: the run of every x in N(u) within [slo, shi)
       hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
         if ((uint64_t)x >= slo && (uint64_t)x < shi) {
@@ -4005,6 +4020,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         }
       });
       __syncthreads();
+      hh_mark(2);  // exclusion marked
       for (uint32_t i0 = 0; i0 < m2; i0 += HH_NT) {
         const uint32_t i = i0 + (uint32_t)t;
         const bool start = i < m && (i == 0 || (sk[i] >> HS_WSH) != (sk[i - 1] >> HS_WSH));
@@ -4024,6 +4040,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
         hp_emit(sg, a, start, s, u, w, tau);
       }
       __syncthreads();
+      hh_mark(3);  // runs summed, scored, emitted
       for (int i = t; i < LT; i += HH_NT) {  // the hash-table words under the buffer
         s_v0[i] = HP_EMPTY;
         s_v1[i] = 0;
@@ -4155,6 +4172,8 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     cur = nx;
     nx = s_tk[0];
   }
+  if (a.ph && t == 0)
+    for (int i = 0; i < 4; ++i) atomicAdd(&a.ph[i], (unsigned long long)ph_acc[i]);
   hp_finish(sg, a, wedges);
 }
 

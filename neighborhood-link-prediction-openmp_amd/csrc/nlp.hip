@@ -2106,8 +2106,11 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
   TRY(hipGetLastError());
   // persistent workgroups over the item queue: the table's LDS decides how many fit a CU
   const unsigned gr = (unsigned)((custom || tl >= 13 ? 4 : 8) * (uint64_t)g->hp_gp);
+  HpArgs ah = a;  // NLP_TRACE_HUB=1: the sort mode's phase ticks into the chunk counters' small[56, 60)
+  static const bool trace_hub = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
+  ah.ph = trace_hub ? a.ctr + 56 : nullptr;
 #define NLP_HH_ACCUM(CU, TLC)                                                                                 \
-  hipLaunchKernelGGL((k_hh_accum<CU, TLC>), dim3(gr), dim3(HH_NT), 0, st, a, (const HhItem*)items,            \
+  hipLaunchKernelGGL((k_hh_accum<CU, TLC>), dim3(gr), dim3(HH_NT), 0, st, ah, (const HhItem*)items,           \
                      (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw, \
                      (const uint32_t*)pv, queue, (int)(wcap != 0), cap)
   if (custom) NLP_HH_ACCUM(true, HH_TL);
@@ -2394,7 +2397,10 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     a.xs = g->xs;
     a.win = 0;
     a.uxf = g->hp_uxf;
-    a.ph = nullptr;  // k_hp_batch phase ticks (a diagnostic hook: small[56, 60) when set)
+    // phase ticks (k_hp_batch, k_hh_accum's sort mode; diagnostic: small[56, 60) with NLP_TRACE_HUB=1)
+    static const bool trace_hub = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
+    a.ph = nullptr;  // run_hub points its copy at small[56, 60) when tracing
+    if (trace_hub) TRY(hipMemsetAsync(small + 56, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0) {
@@ -2531,6 +2537,18 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
+    {
+      static const bool trace = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
+      if (trace) {
+        uint64_t ph[4] = {0, 0, 0, 0};
+        TRY(hipMemcpy(ph, small + 56, 32, hipMemcpyDeviceToHost));
+        fprintf(stderr, "nlp hub: chunk %u rows %llu wedges %llu hub wedges %llu of which in HH_BIG items %llu; "
+                "phase ticks (10 ns, summed over workgroups / waves) %llu %llu %llu %llu\n",
+                *nchunks, (unsigned long long)(r1 - r0), (unsigned long long)g->host_small[HPC_WEDGE],
+                (unsigned long long)hub_w, (unsigned long long)g->host_small[HPC_BIGW], (unsigned long long)ph[0],
+                (unsigned long long)ph[1], (unsigned long long)ph[2], (unsigned long long)ph[3]);
+      }
+    }
     if (batch_timed) {
       float ms = 0;
       TRY(hipEventElapsedTime(&ms, g->ev[5], g->ev[6]));
@@ -3734,7 +3752,32 @@ nlp_status predict_fast(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
   return NLP_OK;
 }
 
+nlp_status predict_once(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
+                        hipStream_t st, EdgeOut** result);
+
+// A call that runs out of HBM is retried once with the per-call workspace
+// released first: the buffers only grow (a long-lived handle keeps what its
+// largest earlier call needed -- a C4 AA H = 32 call then left too little for
+// the next Jaccard H = 32 call).
 nlp_status predict_impl(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
+                        hipStream_t st, EdgeOut** result) {
+  nlp_status s = predict_once(g, p, d_out, out_count, t, st, result);
+  if (s != NLP_ERR_NOMEM) return s;
+  (void)hipGetLastError();
+  if (hipStreamSynchronize(st) != hipSuccess) return NLP_ERR_DEVICE;
+  g->ws.release();
+  g->ord_clean = nullptr;     // state keyed by workspace addresses: a new buffer may reuse one
+  g->es_desc_bytes = 0;
+  g->es_desc_ptr = nullptr;
+  g->async_ok = false;
+  if (g->hp_scratch) {
+    (void)hipFree(g->hp_scratch);
+    g->hp_scratch = nullptr;
+  }
+  return predict_once(g, p, d_out, out_count, t, st, result);
+}
+
+nlp_status predict_once(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t* out_count, nlp_timing* t,
                         hipStream_t st, EdgeOut** result) {
   // path 3 (hash accumulation) once the wedge count is large: bounded memory,
   // no wedge materialisation (NLP_HASH=1 forces it, NLP_HASH=0 disables it).

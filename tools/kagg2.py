@@ -6,8 +6,9 @@ import glob
 import os
 import sys
 
-GRAPH = ("k_in_", "k_del_", "k_degrees", "k_check_keys", "k_count_cols", "k_transpose_keys", "k_etab_build", "k_edge_filter",
-         "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_hp_xs", "k_diff_", "k_low32", "k_sum_deg2", "k_hp_dcls(", "k_hp_drank", "k_etab_build")
+GRAPH = ("k_in_", "k_del_", "k_degrees", "k_check_keys", "k_row_descents", "k_transpose_keys", "k_toff_split",
+         "k_etab_upper", "k_etab_insert", "k_edge_filter", "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_hp_xs",
+         "k_diff_", "k_sum_deg2", "k_hp_dcls(", "k_hp_drank")
 path = sys.argv[1]
 if os.path.isdir(path):
     path = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)[0]
@@ -16,7 +17,7 @@ r = sorted((x for x in csv.DictReader(open(path)) if "nlp::" in x["Kernel_Name"]
            key=lambda x: int(x["Start_Timestamp"]))
 # the graph build's radix sort (k_rs_*) precedes the first predict kernel; the build's last kernels (the
 # membership table, the short lists' sort and prefix, which follow its own degree-class compaction) end it
-last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_build", "k_sl_sort", "k_sl_prefix", "k_hp_drank"))),
+last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_insert", "k_sl_sort", "k_sl_prefix", "k_hp_drank"))),
            default=-1)
 first = next(i for i, x in enumerate(r) if i > last and not any(g in x["Kernel_Name"] for g in GRAPH + ("k_rs_", "k_scan")))
 r = r[first:]
