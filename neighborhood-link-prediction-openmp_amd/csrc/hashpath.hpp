@@ -3884,7 +3884,8 @@ constexpr int HS_WSH = 38;
 constexpr uint32_t HS_DMAX = 4095;
 constexpr int HS_CT = 256;  // contributions cached in LDS by k_hh_accum's sort mode
 
-// sortmode (AA / RA, items of at most HH_SCAP wedges unless flagged HH_BIG): an
+// sortmode (AA / RA; nonzero: the plan's wedges per item, at most HH_SCAP, unless
+// flagged HH_BIG -- those are cut into passes of at most that many): an
 // item's wedges are loaded as (w, v, deg v) keys into LDS (over the vmin / vmax
 // words of the hash table), sorted, and every run of equal w summed by its
 // first thread in ascending v -- the additions of predict.hxx:788 / 828 in the
@@ -3911,6 +3912,9 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   __shared__ uint64_t s_item[8];  // the next item (8 words), loaded while this one runs
   __shared__ uint32_t s_tk[2];
   __shared__ uint32_t s_n;
+  __shared__ uint32_t s_sp, s_rng[3];  // HH_BIG items: the range stack's size and the range being done,
+  __shared__ uint32_t s_cur, s_grp[3];  // the next bin and the group cut from it
+  __shared__ uint32_t s_w;              // the one w whose v-ranges are being added (thread 0: oacc)
   // AA / RA sort mode: the contributions c(d) of the degrees below HS_CT in
   // LDS -- every first hop of an LHub call up to H = 255 -- so a run's sum
   // waits on no global load (one dependent L2 round trip per run start was
@@ -3933,6 +3937,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   // HPC_ERR): never read beyond it
   const uint32_t ni = (uint32_t)min((uint64_t)*nitems, cap);
   uint64_t wedges = 0;
+  float oacc = 0.0f;  // HH_BIG items, thread 0: the running sum of the one w (mode 2 - 4 below)
   // Items from the work queue two deep: while item `cur` runs, the next
   // ticket's item words and the ticket after it are in flight (a workgroup
   // barrier waits for LDS only, not for these loads), so an item costs no
@@ -3946,11 +3951,12 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
   if (t < 8 && cur < ni) s_item[t] = ((const uint64_t*)(items + cur))[t];
   __syncthreads();
   // diagnostic (NLP_TRACE_HUB=1): the sort mode's phase times, thread 0's clock between barriers
-  uint64_t ph_t = 0, ph_acc[4] = {0, 0, 0, 0};
+  uint64_t ph_t = 0, ph_acc[5] = {0, 0, 0, 0, 0}, ph_max = 0;
   auto hh_mark = [&](int i) {
     if (a.ph && t == 0) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (i >= 0) ph_acc[i] += now - ph_t;
+      if (i == 4 && now - ph_t > ph_max) ph_max = now - ph_t;
       ph_t = now;
     }
   };
@@ -3964,88 +3970,351 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     const bool whole = (item.cnt & HH_WHOLE) != 0;
     const uint64_t slo = item.slo, shi = item.shi;
     if (CUSTOM && (item.cnt & HH_BIG) && t == 0) atomicAdd(&a.ctr[HPC_BIGW], (unsigned long long)n);
-    if (CUSTOM && sortmode && !(item.cnt & HH_BIG)) {
-      uint64_t* const sk = s_vv;
-      if (t == 0) s_n = 0;
-      __syncthreads();
-      hh_mark(-1);
-      for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
-        uint32_t wq[HP_UN], vq[HP_UN], dq[HP_UN];
-        bool in[HP_UN];
-#pragma unroll
-        for (int k = 0; k < HP_UN; ++k) {
-          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
-          const uint64_t p = off + (i < n ? i : 0u);
-          wq[k] = sw[p];
-          vq[k] = sv[p];
-        }
-#pragma unroll
-        for (int k = 0; k < HP_UN; ++k) {
-          const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
-          in[k] = i < n && (whole || ((uint64_t)wq[k] >= slo && (uint64_t)wq[k] < shi));
-          dq[k] = in[k] ? a.g.deg[vq[k]] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < HP_UN; ++k) {
-          const uint32_t pos = hh_wave_append(in[k], &s_n);  // one LDS atomic per wave
-          if (in[k]) {
-            ++wedges;
-            if (pos < HH_SCAP)
-              sk[pos] = ((uint64_t)wq[k] - slo) << HS_WSH | (uint64_t)vq[k] << 12 |
-                        (dq[k] < HS_DMAX ? dq[k] : HS_DMAX);
-            else
-              atomicOr(&a.ctr[HPC_ERR], 8ull);
+    // AA / RA sort mode: the wedges of [xlo, xhi) (at most HH_SCAP of them) as
+    // (w, v, deg v) keys into LDS, sorted, every run of equal w summed by its
+    // first thread in ascending v -- the reference's order of additions
+    uint64_t* const sk = s_vv;
+    auto sort_pass = [&](const uint64_t xlo, const uint64_t xhi, const bool all) {
+        if (t == 0) s_n = 0;
+        __syncthreads();
+        hh_mark(-1);
+        for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+          uint32_t wq[HP_UN], vq[HP_UN], dq[HP_UN];
+          bool in[HP_UN];
+  #pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            const uint64_t p = off + (i < n ? i : 0u);
+            wq[k] = sw[p];
+            vq[k] = sv[p];
+          }
+  #pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            in[k] = i < n && (all || ((uint64_t)wq[k] >= xlo && (uint64_t)wq[k] < xhi));
+            dq[k] = in[k] ? a.g.deg[vq[k]] : 0u;
+          }
+  #pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t pos = hh_wave_append(in[k], &s_n);  // one LDS atomic per wave
+            if (in[k]) {
+              ++wedges;
+              if (pos < HH_SCAP)
+                sk[pos] = ((uint64_t)wq[k] - xlo) << HS_WSH | (uint64_t)vq[k] << 12 |
+                          (dq[k] < HS_DMAX ? dq[k] : HS_DMAX);
+              else
+                atomicOr(&a.ctr[HPC_ERR], 8ull);
+            }
           }
         }
-      }
-      __syncthreads();
-      hh_mark(0);  // wedges loaded and appended
-      const uint32_t m = s_n < HH_SCAP ? s_n : HH_SCAP;
-      const uint32_t m2 = pow2_at_least(m);
-      for (uint32_t i = m + t; i < m2; i += HH_NT) sk[i] = ~0ull;
-      for (uint32_t i = t; i < m2; i += HH_NT) s_ex[i] = 0;
-      __syncthreads();
-      block_bitonic_u64<HH_NT>(sk, m2);
-      hh_mark(1);  // sorted
-      // first-order exclusion: the run of every x in N(u) within [slo, shi)
-      hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
-        if ((uint64_t)x >= slo && (uint64_t)x < shi) {
-          const uint64_t xl = (uint64_t)x - slo;
-          uint32_t l = 0, h = m;
-          while (l < h) {
-            const uint32_t md = (l + h) >> 1;
-            if ((sk[md] >> HS_WSH) < xl) l = md + 1; else h = md;
+        __syncthreads();
+        hh_mark(0);  // wedges loaded and appended
+        const uint32_t m = s_n < HH_SCAP ? s_n : HH_SCAP;
+        const uint32_t m2 = pow2_at_least(m);
+        for (uint32_t i = m + t; i < m2; i += HH_NT) sk[i] = ~0ull;
+        for (uint32_t i = t; i < m2; i += HH_NT) s_ex[i] = 0;
+        __syncthreads();
+        block_bitonic_u64<HH_NT>(sk, m2);
+        hh_mark(1);  // sorted
+        // first-order exclusion: the run of every x in N(u) within [xlo, xhi)
+        hp_stream(a.g.keys + x0, x1 - x0, (uint32_t)t, (uint32_t)HH_NT, [&](uint32_t x) {
+          if ((uint64_t)x >= xlo && (uint64_t)x < xhi) {
+            const uint64_t xl = (uint64_t)x - xlo;
+            uint32_t l = 0, h = m;
+            while (l < h) {
+              const uint32_t md = (l + h) >> 1;
+              if ((sk[md] >> HS_WSH) < xl) l = md + 1; else h = md;
+            }
+            if (l < m && (sk[l] >> HS_WSH) == xl) s_ex[l] = 1;
           }
-          if (l < m && (sk[l] >> HS_WSH) == xl) s_ex[l] = 1;
-        }
-      });
-      __syncthreads();
-      hh_mark(2);  // exclusion marked
-      for (uint32_t i0 = 0; i0 < m2; i0 += HH_NT) {
-        const uint32_t i = i0 + (uint32_t)t;
-        const bool start = i < m && (i == 0 || (sk[i] >> HS_WSH) != (sk[i - 1] >> HS_WSH));
-        float s = 0.0f;
-        uint32_t w = 0;
-        if (start) {
-          const uint64_t wl = sk[i] >> HS_WSH;
-          float acc = 0.0f;
-          for (uint32_t j = i; j < m && (sk[j] >> HS_WSH) == wl; ++j) {
-            uint32_t d = (uint32_t)(sk[j] & 0xfffu);
-            if (d == HS_DMAX) d = a.g.deg[(uint32_t)(sk[j] >> 12) & 0x3ffffffu];
-            acc = (float)((double)acc + (d < (uint32_t)HS_CT ? s_ct[d] : a.g.ctab[d]));
+        });
+        __syncthreads();
+        hh_mark(2);  // exclusion marked
+        for (uint32_t i0 = 0; i0 < m2; i0 += HH_NT) {
+          const uint32_t i = i0 + (uint32_t)t;
+          const bool start = i < m && (i == 0 || (sk[i] >> HS_WSH) != (sk[i - 1] >> HS_WSH));
+          float s = 0.0f;
+          uint32_t w = 0;
+          if (start) {
+            const uint64_t wl = sk[i] >> HS_WSH;
+            float acc = 0.0f;
+            for (uint32_t j = i; j < m && (sk[j] >> HS_WSH) == wl; ++j) {
+              uint32_t d = (uint32_t)(sk[j] & 0xfffu);
+              if (d == HS_DMAX) d = a.g.deg[(uint32_t)(sk[j] >> 12) & 0x3ffffffu];
+              acc = (float)((double)acc + (d < (uint32_t)HS_CT ? s_ct[d] : a.g.ctab[d]));
+            }
+            s = s_ex[i] ? 0.0f : acc;
+            w = (uint32_t)(xlo + wl);
           }
-          s = s_ex[i] ? 0.0f : acc;
-          w = (uint32_t)(slo + wl);
+          hp_emit(sg, a, start, s, u, w, tau);
         }
-        hp_emit(sg, a, start, s, u, w, tau);
-      }
-      __syncthreads();
-      hh_mark(3);  // runs summed, scored, emitted
-      for (int i = t; i < LT; i += HH_NT) {  // the hash-table words under the buffer
+        __syncthreads();
+    };
+    auto reset_vv = [&]() {  // the hash-table words under the sort buffer
+      for (int i = t; i < LT; i += HH_NT) {
         s_v0[i] = HP_EMPTY;
         s_v1[i] = 0;
       }
       __syncthreads();
+    };
+    if (CUSTOM && sortmode && !(item.cnt & HH_BIG)) {
+      hh_mark(-1);
+      sort_pass(slo, shi, whole);
+      hh_mark(3);  // runs summed, scored, emitted
+      reset_vv();
+      return;
+    }
+    if (CUSTOM && sortmode) {
+      // an HH_BIG item (more than HH_SCAP wedges in one bin of the plan): cut
+      // into w-ranges of at most `sortmode` wedges by histograms of its wedges
+      // (ranges refined until they fit), each a sort pass; a single w with
+      // more contributions than that is added over v-ranges in ascending v
+      // (the reference's order: N(u) is sorted).  Round 5 took these items through the hash table
+      // and re-walked N(u) x I(w) per entry with three or more contributions,
+      // one thread each: one such item of C4 AA H = 32 took 840 ms.
+      hh_mark(-1);
+      uint32_t* const hist = s_k;   // LT bin counts
+      // ranges to do: (lo, hi, mode) triples; mode 0 a w-range to cut, 2 one w,
+      // 3 a v-range of that w, 4 that w's score
+      uint32_t* const stk = s_c;
+      constexpr uint32_t SCAP = LT / 3;
+      if (t == 0) {
+        stk[0] = (uint32_t)slo;
+        stk[1] = (uint32_t)min(shi, (uint64_t)0xffffffffull);
+        stk[2] = 0;
+        s_sp = 1;
+      }
+      for (;;) {
+        __syncthreads();
+        if (s_sp == 0) break;
+        if (t == 0) {
+          const uint32_t q = --s_sp;
+          s_rng[0] = stk[3 * q];
+          s_rng[1] = stk[3 * q + 1];
+          s_rng[2] = stk[3 * q + 2];
+        }
+        __syncthreads();
+        const uint64_t lo = s_rng[0], hi = s_rng[1];
+        const uint32_t mode = s_rng[2];
+        if (mode == 2) {  // one w: its contributions over v-ranges (mode 3), then its score (mode 4)
+          if (t == 0) {
+            s_w = (uint32_t)lo;
+            oacc = 0.0f;
+            if (s_sp + 2 <= SCAP) {
+              stk[3 * s_sp] = (uint32_t)lo;
+              stk[3 * s_sp + 1] = (uint32_t)hi;
+              stk[3 * s_sp + 2] = 4;
+              stk[3 * s_sp + 3] = 0;
+              stk[3 * s_sp + 4] = 1u << 26;  // sort mode: v < 2^26
+              stk[3 * s_sp + 5] = 3;
+              s_sp += 2;
+            } else {
+              atomicOr(&a.ctr[HPC_ERR], 16ull);
+            }
+          }
+          continue;
+        }
+        if (mode == 4) {  // w's first-order exclusion (w in the item's slice of N(u): score 0) and emission
+          bool ex = false;
+          if (t == 0) {
+            uint64_t l = x0, h = x1;
+            while (l < h) {
+              const uint64_t md = (l + h) >> 1;
+              if ((uint64_t)a.g.keys[md] < lo) l = md + 1; else h = md;
+            }
+            ex = l < x1 && (uint64_t)a.g.keys[l] == lo;
+          }
+          hp_emit(sg, a, t == 0, ex ? 0.0f : oacc, u, (uint32_t)lo, tau);
+          continue;
+        }
+        if (mode == 3) {
+          // the one w's wedges with v in [lo, hi) in ascending v: a histogram of
+          // their v over at most LT bins, groups of at most `sortmode` wedges
+          // sorted and added by thread 0 in order; a bin beyond that is one v
+          // (its equal contributions added in place) or refined: it and the rest
+          // of the range go back onto the stack, the bin on top
+          const uint32_t wv = s_w;
+          int bsh = 0;
+          while (((hi - lo + (1ull << bsh) - 1) >> bsh) > (uint64_t)LT) ++bsh;
+          const uint32_t nb = (uint32_t)((hi - lo + (1ull << bsh) - 1) >> bsh);
+          for (uint32_t i = t; i < nb; i += HH_NT) hist[i] = 0;
+          __syncthreads();
+          for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+            uint32_t wq[HP_UN], vq[HP_UN];
+#pragma unroll
+            for (int k = 0; k < HP_UN; ++k) {
+              const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+              const uint64_t p = off + (i < n ? i : 0u);
+              wq[k] = sw[p];
+              vq[k] = sv[p];
+            }
+#pragma unroll
+            for (int k = 0; k < HP_UN; ++k) {
+              const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+              if (i < n && wq[k] == wv && (uint64_t)vq[k] >= lo && (uint64_t)vq[k] < hi)
+                atomicAdd(&hist[((uint64_t)vq[k] - lo) >> bsh], 1u);
+            }
+          }
+          if (t == 0) s_cur = 0;
+          for (;;) {
+            __syncthreads();
+            if (t == 0) {
+              uint32_t c = s_cur;
+              uint64_t acc = 0, g0 = lo + ((uint64_t)c << bsh);
+              while (c < nb) {
+                const uint32_t cnt = hist[c];
+                const uint64_t b0 = lo + ((uint64_t)c << bsh), b1 = min(hi, b0 + (1ull << bsh));
+                if (cnt > (uint32_t)sortmode) {
+                  if (acc) break;
+                  if (b1 - b0 == 1) {
+                    const uint32_t d = a.g.deg[(uint32_t)b0];
+                    const double cc = d < (uint32_t)HS_CT ? s_ct[d] : a.g.ctab[d];
+                    for (uint32_t q = 0; q < cnt; ++q) oacc = (float)((double)oacc + cc);
+                    wedges += cnt;
+                    ++c;
+                    g0 = b1;
+                    continue;
+                  }
+                  if (s_sp + 2 <= SCAP) {
+                    uint32_t q = s_sp;
+                    if (b1 < hi) {
+                      stk[3 * q] = (uint32_t)b1;
+                      stk[3 * q + 1] = (uint32_t)hi;
+                      stk[3 * q + 2] = 3;
+                      ++q;
+                    }
+                    stk[3 * q] = (uint32_t)b0;
+                    stk[3 * q + 1] = (uint32_t)b1;
+                    stk[3 * q + 2] = 3;
+                    s_sp = q + 1;
+                  } else {
+                    atomicOr(&a.ctr[HPC_ERR], 16ull);
+                  }
+                  c = nb;
+                  break;
+                }
+                if (acc + cnt > (uint64_t)sortmode) break;
+                acc += cnt;
+                ++c;
+              }
+              s_cur = c;
+              s_grp[0] = (uint32_t)g0;
+              s_grp[1] = (uint32_t)(c < nb ? lo + ((uint64_t)c << bsh) : hi);
+              s_grp[2] = acc ? 1u : 0u;
+            }
+            __syncthreads();
+            if (!s_grp[2]) break;
+            const uint32_t v0 = s_grp[0], v1 = s_grp[1];
+            if (t == 0) s_n = 0;
+            __syncthreads();
+            for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+              uint32_t wq[HP_UN], vq[HP_UN];
+              bool in[HP_UN];
+#pragma unroll
+              for (int k = 0; k < HP_UN; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+                const uint64_t p = off + (i < n ? i : 0u);
+                wq[k] = sw[p];
+                vq[k] = sv[p];
+              }
+#pragma unroll
+              for (int k = 0; k < HP_UN; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+                in[k] = i < n && wq[k] == wv && vq[k] >= v0 && vq[k] < v1;
+                const uint32_t pos = hh_wave_append(in[k], &s_n);
+                if (in[k]) {
+                  ++wedges;
+                  const uint32_t d = a.g.deg[vq[k]];
+                  if (pos < HH_SCAP)
+                    sk[pos] = (uint64_t)vq[k] << 12 | (d < HS_DMAX ? d : HS_DMAX);
+                  else
+                    atomicOr(&a.ctr[HPC_ERR], 8ull);
+                }
+              }
+            }
+            __syncthreads();
+            const uint32_t m = s_n < HH_SCAP ? s_n : HH_SCAP;
+            const uint32_t m2 = pow2_at_least(m);
+            for (uint32_t i = m + t; i < m2; i += HH_NT) sk[i] = ~0ull;
+            __syncthreads();
+            block_bitonic_u64<HH_NT>(sk, m2);
+            if (t == 0)
+              for (uint32_t j = 0; j < m; ++j) {
+                uint32_t d = (uint32_t)(sk[j] & 0xfffu);
+                if (d == HS_DMAX) d = a.g.deg[(uint32_t)(sk[j] >> 12)];
+                oacc = (float)((double)oacc + (d < (uint32_t)HS_CT ? s_ct[d] : a.g.ctab[d]));
+              }
+          }
+          continue;
+        }
+        // mode 0: histogram [lo, hi) over at most LT bins, then group the bins
+        int bsh = 0;
+        while (((hi - lo + (1ull << bsh) - 1) >> bsh) > (uint64_t)LT) ++bsh;
+        const uint32_t nb = (uint32_t)((hi - lo + (1ull << bsh) - 1) >> bsh);
+        for (uint32_t i = t; i < nb; i += HH_NT) hist[i] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < n; i0 += HH_NT * HP_UN) {
+          uint32_t wq[HP_UN];
+#pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            wq[k] = sw[off + (i < n ? i : 0u)];
+          }
+#pragma unroll
+          for (int k = 0; k < HP_UN; ++k) {
+            const uint32_t i = i0 + (uint32_t)k * HH_NT + (uint32_t)t;
+            if (i < n && (uint64_t)wq[k] >= lo && (uint64_t)wq[k] < hi) atomicAdd(&hist[((uint64_t)wq[k] - lo) >> bsh], 1u);
+          }
+        }
+        __syncthreads();
+        // greedy groups of consecutive bins of at most `sortmode` (the plan's
+        // capacity, HH_SCAP unless NLP_HASH_HUB_SCAP) wedges, each sorted
+        // as soon as thread 0 has cut it (serial: rare items); a bin beyond that
+        // goes onto the stack (refined, or one w)
+        if (t == 0) s_cur = 0;
+        for (;;) {
+          __syncthreads();
+          if (t == 0) {
+            uint32_t c = s_cur;
+            uint64_t acc = 0, g0 = lo + ((uint64_t)c << bsh);
+            while (c < nb) {
+              const uint32_t cnt = hist[c];
+              const uint64_t b0 = lo + ((uint64_t)c << bsh), b1 = min(hi, b0 + (1ull << bsh));
+              if (cnt > (uint32_t)sortmode) {
+                if (acc) break;
+                if (s_sp < SCAP) {
+                  stk[3 * s_sp] = (uint32_t)b0;
+                  stk[3 * s_sp + 1] = (uint32_t)b1;
+                  stk[3 * s_sp + 2] = b1 - b0 == 1 ? 2u : 0u;
+                  ++s_sp;
+                } else {
+                  atomicOr(&a.ctr[HPC_ERR], 16ull);  // more pending ranges than the stack holds: fail the call
+                }
+                ++c;
+                g0 = b1;
+                continue;
+              }
+              if (acc + cnt > (uint64_t)sortmode) break;
+              acc += cnt;
+              ++c;
+            }
+            s_cur = c;
+            s_grp[0] = (uint32_t)g0;
+            s_grp[1] = (uint32_t)(c < nb ? lo + ((uint64_t)c << bsh) : hi);
+            s_grp[2] = acc ? 1u : 0u;
+          }
+          __syncthreads();
+          if (!s_grp[2]) break;
+          sort_pass(s_grp[0], s_grp[1], false);
+        }
+      }
+      __syncthreads();
+      for (int i = t; i < LT; i += HH_NT) {  // the hash table under the histogram and the stack
+        s_k[i] = HP_EMPTY;
+        s_c[i] = 0;
+      }
+      hh_mark(4);
+      reset_vv();
       return;
     }
     if (!CUSTOM && (item.cnt & HH_DIRECT)) {
@@ -4102,6 +4371,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       return;
     }
     const uint32_t dcnt = item.cnt & HH_CNT;
+    hh_mark(-1);
     const int lg = max(6, log2_ceil(2 * (uint64_t)dcnt));
     const uint32_t T = 1u << (lg < TL ? lg : TL), mask = T - 1;
     const int hs = 32 - (lg < TL ? lg : TL);
@@ -4154,6 +4424,7 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
       hp_drain<false, CUSTOM, 8>(tb, T, (uint32_t)t, (uint32_t)HH_NT, sg, a, u, du, tau);
       __syncthreads();
     }
+    hh_mark(4);  // a hash-table item (AA / RA: HH_BIG, with the ordered re-walk)
   };
   while (cur < ni) {
     HhItem item;
@@ -4172,8 +4443,10 @@ __global__ __launch_bounds__(HH_NT) void k_hh_accum(HpArgs a, const HhItem* __re
     cur = nx;
     nx = s_tk[0];
   }
-  if (a.ph && t == 0)
-    for (int i = 0; i < 4; ++i) atomicAdd(&a.ph[i], (unsigned long long)ph_acc[i]);
+  if (a.ph && t == 0) {
+    for (int i = 0; i < 5; ++i) atomicAdd(&a.ph[i], (unsigned long long)ph_acc[i]);
+    atomicMax(&a.ph[5], (unsigned long long)ph_max);  // the longest hash-table item
+  }
   hp_finish(sg, a, wedges);
 }
 

@@ -2112,7 +2112,7 @@ nlp_status run_hub(nlp_graph* g, const HpArgs& a, const uint32_t* l2, uint64_t n
 #define NLP_HH_ACCUM(CU, TLC)                                                                                 \
   hipLaunchKernelGGL((k_hh_accum<CU, TLC>), dim3(gr), dim3(HH_NT), 0, st, ah, (const HhItem*)items,           \
                      (const uint32_t*)nitems, (const uint32_t*)sw, (const uint32_t*)sv, (const uint32_t*)pw, \
-                     (const uint32_t*)pv, queue, (int)(wcap != 0), cap)
+                     (const uint32_t*)pv, queue, (int)wcap, cap)
   if (custom) NLP_HH_ACCUM(true, HH_TL);
   else if (tl >= 13) NLP_HH_ACCUM(false, 13);
   else if (tl == 12) NLP_HH_ACCUM(false, 12);
@@ -2400,7 +2400,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     // phase ticks (k_hp_batch, k_hh_accum's sort mode; diagnostic: small[56, 60) with NLP_TRACE_HUB=1)
     static const bool trace_hub = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
     a.ph = nullptr;  // run_hub points its copy at small[56, 60) when tracing
-    if (trace_hub) TRY(hipMemsetAsync(small + 56, 0, 32, st));
+    if (trace_hub) TRY(hipMemsetAsync(small + 56, 0, 48, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0) {
@@ -2540,13 +2540,15 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     {
       static const bool trace = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
       if (trace) {
-        uint64_t ph[4] = {0, 0, 0, 0};
-        TRY(hipMemcpy(ph, small + 56, 32, hipMemcpyDeviceToHost));
+        uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+        TRY(hipMemcpy(ph, small + 56, 48, hipMemcpyDeviceToHost));
         fprintf(stderr, "nlp hub: chunk %u rows %llu wedges %llu hub wedges %llu of which in HH_BIG items %llu; "
-                "phase ticks (10 ns, summed over workgroups / waves) %llu %llu %llu %llu\n",
+                "ticks (10 ns, summed over workgroups): sort mode load %llu sort %llu exclusion %llu runs %llu; "
+                "hash items %llu, the longest %llu\n",
                 *nchunks, (unsigned long long)(r1 - r0), (unsigned long long)g->host_small[HPC_WEDGE],
                 (unsigned long long)hub_w, (unsigned long long)g->host_small[HPC_BIGW], (unsigned long long)ph[0],
-                (unsigned long long)ph[1], (unsigned long long)ph[2], (unsigned long long)ph[3]);
+                (unsigned long long)ph[1], (unsigned long long)ph[2], (unsigned long long)ph[3],
+                (unsigned long long)ph[4], (unsigned long long)ph[5]);
       }
     }
     if (batch_timed) {
