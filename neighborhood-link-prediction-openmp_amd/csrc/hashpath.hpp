@@ -999,9 +999,9 @@ __global__ void k_etab_upper(const uint32_t* __restrict__ deg, const uint32_t* _
 // first empty slot it saw, so a bucket never has a hole and a key never lands
 // twice -- et_has's rule (absent once a bucket with an empty slot lacks it)
 // holds.
-__device__ __forceinline__ void et_insert(uint64_t* __restrict__ tab, uint32_t bits, uint64_t key) {
+// (from bucket b on: the probe of a key whose home bucket was found full)
+__device__ __forceinline__ void et_insert_at(uint64_t* __restrict__ tab, uint32_t bits, uint64_t key, uint64_t b) {
   const uint64_t mask = (1ull << bits) - 1;
-  uint64_t b = et_mix(key) >> (64 - bits);
   for (uint64_t probe = 0; probe <= mask;) {
     unsigned long long* q = (unsigned long long*)(tab + b * ET_SLOTS);
     uint64_t s[ET_SLOTS];
@@ -1025,9 +1025,65 @@ __device__ __forceinline__ void et_insert(uint64_t* __restrict__ tab, uint32_t b
   }
 }
 
+// N keys at once, two round trips for all of them instead of two each: their
+// home buckets are read together with plain loads (a hint: a stale line only
+// lacks keys, never shows a slot full that is empty), then each claims the
+// first empty slot it saw by CAS, the N CASes issued together.  A CAS that
+// finds another key moves to the next slot (the CAS's answer is the truth, so
+// no re-read); a bucket seen full probes on from the next bucket (et_insert_at).
+// A writer claims slot j only after finding slots below j full and stops at
+// its own key, so buckets keep no holes and no key lands twice.
+template <int N>
+__device__ __forceinline__ void et_insert_n(uint64_t* __restrict__ tab, uint32_t bits, const uint64_t (&key)[N],
+                                            const bool (&act)[N]) {
+  const uint64_t mask = (1ull << bits) - 1;
+  ulonglong2 q[N][4];
+  uint64_t b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    b[i] = et_mix(key[i]) >> (64 - bits);
+    const ulonglong2* p = (const ulonglong2*)(tab + (act[i] ? b[i] : 0ull) * ET_SLOTS);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[i][j] = act[i] ? p[j] : make_ulonglong2(0, 0);
+  }
+  int pos[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t sl[ET_SLOTS] = {q[i][0].x, q[i][0].y, q[i][1].x, q[i][1].y,
+                                   q[i][2].x, q[i][2].y, q[i][3].x, q[i][3].y};
+    int first = ET_SLOTS;
+    bool hit = false;
+#pragma unroll
+    for (int j = ET_SLOTS - 1; j >= 0; --j) {
+      hit |= sl[j] == key[i];
+      if (sl[j] == ET_EMPTY) first = j;
+    }
+    pos[i] = !act[i] || hit ? -1 : first;  // ET_SLOTS: the bucket is full
+  }
+  unsigned long long cur[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    cur[i] = pos[i] >= 0 && pos[i] < ET_SLOTS
+                 ? atomicCAS((unsigned long long*)(tab + b[i] * ET_SLOTS + pos[i]), ET_EMPTY,
+                             (unsigned long long)key[i])
+                 : ET_EMPTY;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (pos[i] < 0) continue;
+    int j = pos[i];
+    if (j < ET_SLOTS) {
+      unsigned long long c = cur[i];
+      while (c != ET_EMPTY && c != key[i] && ++j < ET_SLOTS)
+        c = atomicCAS((unsigned long long*)(tab + b[i] * ET_SLOTS + j), ET_EMPTY, (unsigned long long)key[i]);
+    }
+    if (j >= ET_SLOTS) et_insert_at(tab, bits, key[i], (b[i] + 1) & mask);
+  }
+}
+
 // The entries w > u inserted edge-parallel: a wave takes HP_WTILE consecutive
 // adjacency entries (coalesced keys, every lane busy whatever the degrees),
-// finding each entry's row from the tile's first row like k_hp_drank.
+// finding each entry's row from the tile's first row like k_hp_drank; a
+// lane's HP_WR keys go in together (et_insert_n).
 __global__ __launch_bounds__(NT) void k_etab_insert(const uint64_t* __restrict__ off, const uint32_t* __restrict__ keys,
                                                     uint64_t S, uint64_t M, const uint32_t* __restrict__ tile_row,
                                                     uint64_t* __restrict__ tab, uint32_t bits) {
@@ -1039,7 +1095,9 @@ __global__ __launch_bounds__(NT) void k_etab_insert(const uint64_t* __restrict__
     const uint64_t rl = r0 + lane;
     const uint64_t rend = rl < S ? off[rl + 1] : ~0ull;
     const uint64_t last_end = __shfl(rend, 63, 64);
-#pragma unroll 1
+    uint64_t key[HP_WR];
+    bool act[HP_WR];
+#pragma unroll
     for (int i = 0; i < HP_WR; ++i) {
       const uint64_t e = base + (uint64_t)i * 64 + lane;
       const uint32_t w = e < M ? keys[e] : 0u;
@@ -1049,9 +1107,8 @@ __global__ __launch_bounds__(NT) void k_etab_insert(const uint64_t* __restrict__
         const uint64_t x = __shfl(rend, md, 64);
         if (x <= e) lo = md + 1; else hi = md;
       }
-      if (e >= M) continue;
       uint64_t r = r0 + lo;
-      if (e >= last_end) {
+      if (e < M && e >= last_end) {
         uint64_t a = r0, b = S;
         while (b - a > 1) {
           const uint64_t md = (a + b) >> 1;
@@ -1059,8 +1116,10 @@ __global__ __launch_bounds__(NT) void k_etab_insert(const uint64_t* __restrict__
         }
         r = a;
       }
-      if (w > r) et_insert(tab, bits, (r << 32) | w);
+      act[i] = e < M && w > r;
+      key[i] = (r << 32) | w;
     }
+    et_insert_n<HP_WR>(tab, bits, key, act);
   }
 }
 
