@@ -799,16 +799,6 @@ __global__ __launch_bounds__(NT) void k_hp_work_edges(GraphView g, uint32_t H, u
 // into W's 40 bits: W <= 254 deg u).
 constexpr uint32_t HP_DCLS_MAX = 254;
 
-// (and, when kd is given, the entry degrees themselves: kd[e] = deg keys[e])
-__global__ void k_hp_dcls(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ deg, uint64_t M,
-                          uint8_t* __restrict__ out, uint32_t* __restrict__ kd) {
-  for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t d = deg[keys[e]];
-    out[e] = (uint8_t)(d < 255u ? d : 255u);
-    if (kd) kd[e] = d;
-  }
-}
-
 __device__ __forceinline__ bool hp_dsurv(uint32_t c, uint32_t H) { return c >= 1 && c <= H; }
 
 // The same per-row (count, W) and tile counts with eight consecutive entries
@@ -887,35 +877,69 @@ __global__ void k_hp_unpack(unsigned long long* __restrict__ wu, uint32_t* __res
   }
 }
 
-// tpre: exclusive prefix of the tile counts (tile - t0 indexed)
-// Per graph: for every entry e = (u -> v) with deg v <= 254, the number of
-// entries of N(v) at or below u (its rank there; u8) -- the survivor lists'
-// fill reads it instead of searching N(v) on every call.  (Searching a lane's
-// eight entries together, one branchless step of all of them at a time,
-// measured slower: 240 -> 375 ms for the entry-class phase on C4.)
-__global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __restrict__ dcls, uint64_t S,
-                                                 uint64_t M, const uint32_t* __restrict__ tile_row,
-                                                 uint8_t* __restrict__ out) {
+// Per graph, one pass over the adjacency entries e = (u -> v): the degree class
+// of v (dcls[e] = min(deg v, 255): path 4 filters N(u) by it, coalesced bytes
+// instead of a degree gather), deg v itself (kd, when given: the count-metric
+// row kernels carry it) and, for deg v <= 254, the entries of N(v) at or below
+// u (drank, when given: its rank there -- the survivor lists' fill reads it
+// instead of searching N(v) on every call).  deg v comes from off[v], off[v + 1]
+// (one line, which the search of N(v) needs anyway), a lane's HP_WR gathers in
+// flight together.  Edge-parallel over HP_WTILE-entry tiles, each entry's row
+// from its tile's first row by a search of 64 row ends held in lanes.  C4:
+// 200 ms, against 68 + 178 ms for round 5's degree-gather and binary-search
+// passes; an 8-way split search (7 pivot loads a round) measured slower here
+// (312 ms fused, 374 ms in two passes): the lists are at most 254 entries, so
+// the binary search's later probes hit lines already fetched.
+__global__ __launch_bounds__(NT) void k_hp_entry_classes(const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ keys, uint64_t S, uint64_t M,
+                                                         const uint32_t* __restrict__ tile_row,
+                                                         uint8_t* __restrict__ dcls, uint32_t* __restrict__ kd,
+                                                         uint8_t* __restrict__ drank) {
   const int lane = lane_id(), wv = wave_id();
   const uint64_t nt = (M + HP_WTILE - 1) / HP_WTILE;
   for (uint64_t tile = (uint64_t)blockIdx.x * NWAVE + wv; tile < nt; tile += (uint64_t)gridDim.x * NWAVE) {
     const uint64_t base = tile * HP_WTILE;
     const uint64_t r0 = tile_row[tile];
     const uint64_t rl = r0 + lane;
-    const uint64_t rend = rl < S ? g.off[rl + 1] : ~0ull;
+    const uint64_t rend = rl < S ? off[rl + 1] : ~0ull;
     const uint64_t last_end = __shfl(rend, 63, 64);
+    // the lane's HP_WR entries: keys (coalesced), then their row bounds all in flight together
+    uint32_t v[HP_WR];
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      v[i] = e < M ? keys[e] : 0u;
+    }
+    uint64_t o[HP_WR], o1[HP_WR];
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      o[i] = off[v[i]];
+      o1[i] = off[v[i] + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < HP_WR; ++i) {
+      const uint64_t e = base + (uint64_t)i * 64 + lane;
+      const uint64_t d64 = o1[i] - o[i];
+      const uint32_t d = d64 > 0xffffffffull ? 0xffffffffu : (uint32_t)d64;
+      if (e < M) {
+        dcls[e] = (uint8_t)(d < 255u ? d : 255u);
+        if (kd) kd[e] = d;
+      }
+    }
+    if (!drank) continue;
 #pragma unroll 1
     for (int i = 0; i < HP_WR; ++i) {
       const uint64_t e = base + (uint64_t)i * 64 + lane;
-      const uint32_t c = e < M ? (uint32_t)dcls[e] : 0u;
       int lo = 0, hi = 64;
       while (lo < hi) {
         const int md = (lo + hi) >> 1;
         const uint64_t x = __shfl(rend, md, 64);
         if (x <= e) lo = md + 1; else hi = md;
       }
-      if (c == 0 || c > HP_DCLS_MAX) {
-        if (e < M) out[e] = 0;
+      if (e >= M) continue;
+      const uint64_t d = o1[i] - o[i];
+      if (d == 0 || d > HP_DCLS_MAX) {
+        drank[e] = 0;
         continue;
       }
       uint64_t r = r0 + lo;
@@ -923,18 +947,11 @@ __global__ __launch_bounds__(NT) void k_hp_drank(GraphView g, const uint8_t* __r
         uint64_t a = r0, b = S;
         while (b - a > 1) {
           const uint64_t md = (a + b) >> 1;
-          if (g.off[md] <= e) a = md; else b = md;
+          if (off[md] <= e) a = md; else b = md;
         }
         r = a;
       }
-      const uint32_t u = (uint32_t)r, v = g.keys[e];
-      const uint64_t o = g.off[v];
-      uint32_t l = 0, h = c;
-      while (l < h) {
-        const uint32_t md = (l + h) >> 1;
-        if (g.keys[o + md] <= u) l = md + 1; else h = md;
-      }
-      out[e] = (uint8_t)l;
+      drank[e] = (uint8_t)upper_bound_u32(keys + o[i], (uint32_t)d, (uint32_t)r);
     }
   }
 }

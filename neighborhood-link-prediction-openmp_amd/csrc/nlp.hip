@@ -763,36 +763,28 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     TRY(hipStreamSynchronize(st));
   }
   TRY(clk.mark("degree_class_index"));
-  // degree class of every adjacency entry: path 4 filters N(u) by it (coalesced
-  // bytes instead of a degree gather per entry) to build the survivor lists S(u)
+  // degree class of every adjacency entry (path 4 filters N(u) by it: coalesced
+  // bytes instead of a degree gather per entry, to build the survivor lists
+  // S(u)), the entry degrees (the count-metric row kernels carry deg w in their
+  // tables) and the rank of every short-list entry's row in the list: one pass,
+  // k_hp_entry_classes
   const char* hdc = getenv("NLP_HASH_DCLS");
   if (M > 0 && !(hdc && hdc[0] == '0') && g->maxdeg < (1u << 24)) {
     if (hmalloc(&g->dcls, M) == hipSuccess) {
-      // and the entry degrees (the count-metric row kernels carry deg w in their tables)
       const char* hkd = getenv("NLP_HASH_KDEG");
       if (!(hkd && hkd[0] == '0') && hmalloc(&g->kdeg, M * 4) != hipSuccess) {
         (void)hipGetLastError();
         g->kdeg = nullptr;
       }
-      LAUNCH(k_hp_dcls, M, st, (const uint32_t*)g->keys, (const uint32_t*)g->deg, M, g->dcls, g->kdeg);
-      TRY(hipGetLastError());
-      // and the rank of every short-list entry's row in the list (k_hp_drank)
       const char* hdr = getenv("NLP_HASH_DRANK");
-      if (!(hdr && hdr[0] == '0')) {
-        if (hmalloc(&g->drank, M) == hipSuccess) {
-          GraphView gv0{};
-          gv0.off = g->off;
-          gv0.keys = g->keys;
-          gv0.deg = g->deg;
-          const unsigned gd = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 16384);
-          hipLaunchKernelGGL(k_hp_drank, dim3(gd), dim3(NT), 0, st, gv0, (const uint8_t*)g->dcls, S, M,
-                             (const uint32_t*)g->tile_row, g->drank);
-          TRY(hipGetLastError());
-        } else {
-          (void)hipGetLastError();
-          g->drank = nullptr;
-        }
+      if (!(hdr && hdr[0] == '0') && hmalloc(&g->drank, M) != hipSuccess) {
+        (void)hipGetLastError();
+        g->drank = nullptr;
       }
+      const unsigned gd = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 65536);
+      hipLaunchKernelGGL(k_hp_entry_classes, dim3(gd), dim3(NT), 0, st, (const uint64_t*)g->off,
+                         (const uint32_t*)g->keys, S, M, (const uint32_t*)g->tile_row, g->dcls, g->kdeg, g->drank);
+      TRY(hipGetLastError());
     } else {
       (void)hipGetLastError();
       g->dcls = nullptr;

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C4-sk-2005")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--envs", default="", help="';'-separated NAME=VALUE[,NAME=VALUE] sets, one create each (A/B runs)")
     args = ap.parse_args()
     import torch
     nlp = nlp_loader.load()
@@ -28,12 +29,16 @@ def main():
     from bench import release_cached, HBM_CLEAR_GBS
     release_cached("graph generation")
     print(json.dumps({"config": args.config, "gen_s": time.time() - t0, "M": int(keys.numel())}), flush=True)
-    for r in range(args.repeat):
+    sets = [x for x in args.envs.split(";") if x] or [""] * args.repeat
+    for es in sets:
+        for kv in (x for x in es.split(",") if x):
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
         t0 = time.time()
         G = nlp.Graph.from_device(off, keys)
         torch.cuda.synchronize()
         dt = time.time() - t0
-        print(json.dumps({"create_s": dt, "phases_ms": G.build_phases()}), flush=True)
+        print(json.dumps({"env": es, "create_s": dt, "phases_ms": G.build_phases()}), flush=True)
         free0 = torch.cuda.mem_get_info()[0]
         G.close()
         time.sleep(max(0, torch.cuda.mem_get_info()[0] - free0) / 1e9 / HBM_CLEAR_GBS)  # the driver's clear

@@ -8,7 +8,7 @@ import sys
 
 GRAPH = ("k_in_", "k_del_", "k_degrees", "k_check_keys", "k_row_descents", "k_transpose_keys", "k_toff_split",
          "k_etab_upper", "k_etab_insert", "k_edge_filter", "k_deg_class", "k_sv_pack", "k_hp_tile_rows", "k_hp_xs",
-         "k_diff_", "k_sum_deg2", "k_hp_dcls(", "k_hp_drank")
+         "k_diff_", "k_sum_deg2", "k_hp_entry_classes")
 path = sys.argv[1]
 if os.path.isdir(path):
     path = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)[0]
@@ -17,7 +17,7 @@ r = sorted((x for x in csv.DictReader(open(path)) if "nlp::" in x["Kernel_Name"]
            key=lambda x: int(x["Start_Timestamp"]))
 # the graph build's radix sort (k_rs_*) precedes the first predict kernel; the build's last kernels (the
 # membership table, the short lists' sort and prefix, which follow its own degree-class compaction) end it
-last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_insert", "k_sl_sort", "k_sl_prefix", "k_hp_drank"))),
+last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_insert", "k_sl_sort", "k_sl_prefix", "k_hp_entry_classes"))),
            default=-1)
 first = next(i for i, x in enumerate(r) if i > last and not any(g in x["Kernel_Name"] for g in GRAPH + ("k_rs_", "k_scan")))
 r = r[first:]
