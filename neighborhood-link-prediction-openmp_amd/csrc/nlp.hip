@@ -605,6 +605,50 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
   return NLP_OK;
 }
 
+// A stable LSD sort of n 8-byte keys on the 8-bit digits at `shifts` with
+// the order's range-local passes (edgesort.hpp k_es_cnt8 / k_es_off8 /
+// k_es_pass8: a workgroup per range of consecutive tiles, digit runs written
+// to the range's running offsets): the graph build's transposed sort.
+// *which = 1: the result is in k1.  *done = false (nothing sorted) when n needs
+// more than the passes' 32-bit offsets.
+nlp_status lsd8_keys(nlp_graph* g, uint64_t* k0, uint64_t* k1, uint64_t n, const int* shifts, int np, int* which,
+                     hipStream_t st, bool* done) {
+  *done = false;
+  *which = 0;
+  if (n == 0 || n >= (1ull << 32) || np > ES_MAXP) return NLP_OK;
+  Workspace& ws = g->ws;
+  int nb = 0;
+  TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_es_pass8<false>, ES8_NT, 0));
+  int dev = 0, cus = 0;
+  TRY(hipGetDevice(&dev));
+  TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const uint64_t ntiles = (n + ES8_TILE - 1) / ES8_TILE;
+  uint32_t G = (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>({ntiles, (uint64_t)cus * (uint64_t)std::max(nb, 1), (uint64_t)ES8_GMAX}));
+  const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
+  G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
+  uint32_t* hw;  // [np][256] digit totals
+  TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
+  TRY(hipMemsetAsync(hw, 0, (uint64_t)np * 256 * 4, st));
+  uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
+  TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+  uint32_t* offs = cnt + (uint64_t)256 * G;
+  const uint64_t* src = k0;
+  for (int r = 0; r < np; ++r) {
+    uint64_t* dst = (r & 1) ? k0 : k1;
+    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, shifts[r], cnt, hw + r * 256, tpw, G);
+    hipLaunchKernelGGL(k_es_off8, dim3(256), dim3(ES8_GMAX), 0, st, (const uint32_t*)cnt,
+                       (const uint32_t*)(hw + r * 256), G, offs);
+    hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES8_NT), 0, st, (const float*)nullptr, src, dst,
+                       (EdgeOut*)nullptr, n, 0, shifts[r], (const uint32_t*)offs, tpw, G, (uint64_t)0);
+    TRY(hipGetLastError());
+    src = dst;
+  }
+  *which = np & 1;
+  *done = true;
+  return NLP_OK;
+}
+
 // Build everything derived from off/keys (already on the device).
 nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   hipStream_t st = g->stream;
@@ -663,10 +707,6 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     uint32_t* hist;
     TRY(wsget(g->ws, B_WKEY0, M, &k0));
     TRY(wsget(g->ws, B_WKEY1, M, &k1));
-    uint64_t nb = rs_blocks(M);
-    TRY(wsget(g->ws, B_HIST, RS_BINS * nb, &hist));
-    TRY(wsget(g->ws, B_HOFF, RS_BINS * nb, &hoff));
-    TRY(wsget(g->ws, B_SCAN, scan_scratch_words(RS_BINS * nb) + 16, &scan));
     uint64_t* toff;
     uint32_t* tkeys;
     TRY(hmalloc(&toff, (S + 1) * 8));
@@ -680,9 +720,21 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     int vb = bits_for(S - 1);
     int shifts[4], np = 0;
     for (int b = 0; b < vb; b += 8) shifts[np++] = 32 + b;       // v bytes (high word)
-    SortScratch sc{hist, hoff, scan, nb};
     int which = 0;
-    TRY(sort_pairs_u64(k0, nullptr, k1, nullptr, M, shifts, np, sc, &which, st));
+    bool sorted = false;
+    const char* tl = getenv("NLP_TRANSPOSE_LSD8");
+    if (!(tl && tl[0] == '0')) {
+      nlp_status s8 = lsd8_keys(g, k0, k1, M, shifts, np, &which, st, &sorted);
+      if (s8 != NLP_OK) return s8;
+    }
+    if (!sorted) {  // beyond 2^32 entries: the general sort
+      uint64_t nb = rs_blocks(M);
+      TRY(wsget(g->ws, B_HIST, RS_BINS * nb, &hist));
+      TRY(wsget(g->ws, B_HOFF, RS_BINS * nb, &hoff));
+      TRY(wsget(g->ws, B_SCAN, scan_scratch_words(RS_BINS * nb) + 16, &scan));
+      SortScratch sc{hist, hoff, scan, nb};
+      TRY(sort_pairs_u64(k0, nullptr, k1, nullptr, M, shifts, np, sc, &which, st));
+    }
     LAUNCH(k_toff_split, M + 1, st, (const uint64_t*)(which ? k1 : k0), M, S, toff, tkeys);
     TRY(hipGetLastError());
     LAUNCH(k_diff_u64, S + 1, st, toff, g->off, S + 1, flags + 2);
