@@ -1463,17 +1463,21 @@ __global__ __launch_bounds__(NT) void k_dc_gather(GraphView g, const uint8_t* __
 // classes, W+(u) from the per-graph prefix of n) instead of compacting the
 // range's classes and gathering off[v] per survivor.  Built once in
 // nlp_graph_create from the degree-class compaction at the classes kept
-// (k_dc_*), then k_sl_sort and k_sl_prefix.
+// (k_dc_*), then k_sl_sort (which also writes the prefix of n).
 
-// k_sl_sort: a wave per row, stable by class.  Rows of at most 64 entries rank
-// every lane against every other; longer rows count their classes in an LDS
-// histogram, scan it, and place 64 entries per step ranked by a ballot
-// multisplit on the class (cursor advanced by the last lane of each class).
+// k_sl_sort: a wave per row, stable by class, and pn[i] = the inclusive prefix
+// of n over the row's sorted list.  Rows of at most 64 entries rank every lane
+// against every other (the prefix: a wave scan of n in sorted order through
+// LDS); longer rows count their classes in an LDS histogram, scan it, and
+// place 64 entries per step ranked by a ballot multisplit on the class (cursor
+// advanced by the last lane of each class), then scan the row just written
+// (cache-warm; round 5 ran the prefix as a separate pass: 31 ms on C4).
 __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo, uint64_t S,
                                                 const uint32_t* __restrict__ ikeys, const uint64_t* __restrict__ isdo,
                                                 uint32_t* __restrict__ okeys, uint64_t* __restrict__ osdo,
-                                                uint8_t* __restrict__ ocls) {
+                                                uint8_t* __restrict__ ocls, uint32_t* __restrict__ pn) {
   __shared__ uint32_t s_h[NWAVE][256];
+  __shared__ uint32_t s_n[NWAVE][64];
   const int lane = lane_id(), wv = wave_id();
   for (uint64_t u = (uint64_t)blockIdx.x * NWAVE + wv; u < S; u += (uint64_t)gridDim.x * NWAVE) {
     const uint64_t s = lo[u], n = lo[u + 1] - s;
@@ -1492,7 +1496,12 @@ __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo,
         okeys[s + rank] = key;
         osdo[s + rank] = sd;
         ocls[s + rank] = (uint8_t)c;
+        s_n[wv][rank] = (uint32_t)(sd >> HP_SDO_SH) & 0xffu;
       }
+      wave_sync_lds();
+      const uint64_t incl = wave_incl_scan(ok ? (uint64_t)s_n[wv][lane] : 0ull);
+      if (ok) pn[s + lane] = (uint32_t)incl;
+      wave_sync_lds();
       continue;
     }
     for (int q = lane; q < 256; q += 64) s_h[wv][q] = 0;
@@ -1538,19 +1547,13 @@ __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo,
       }
       wave_sync_lds();
     }
-  }
-}
-
-// k_sl_prefix: pn[i] = the inclusive prefix of n over the row's sorted list (a wave per row)
-__global__ __launch_bounds__(NT) void k_sl_prefix(const uint64_t* __restrict__ lo, uint64_t S,
-                                                  const uint64_t* __restrict__ sdo, uint32_t* __restrict__ pn) {
-  const int lane = lane_id(), wv = wave_id();
-  for (uint64_t u = (uint64_t)blockIdx.x * NWAVE + wv; u < S; u += (uint64_t)gridDim.x * NWAVE) {
-    const uint64_t s = lo[u], n = lo[u + 1] - s;
+    // the row's prefix of n, read back from the list just written by this wave
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     uint64_t carry = 0;
     for (uint64_t j0 = 0; j0 < n; j0 += 64) {
       const uint64_t j = j0 + lane;
-      const uint64_t x = j < n ? (sdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
+      const uint64_t x = j < n ? (osdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
       const uint64_t incl = wave_incl_scan(x) + carry;
       if (j < n) pn[s + j] = (uint32_t)incl;
       carry = __shfl(incl, 63, 64);

@@ -594,10 +594,7 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
   TRY(scan_excl_u64<uint32_t>(scnt, S, G.sl_off, G.sl_off + S, scr, st));
   hipLaunchKernelGGL(k_sl_sort, dim3((unsigned)std::min<uint64_t>((S + NWAVE - 1) / NWAVE, 65536)), dim3(NT), 0, st,
                      (const uint64_t*)G.sl_off, S, (const uint32_t*)tkeys, (const uint64_t*)tsdo, G.sl_keys, G.sl_sdo,
-                     G.sl_cls);
-  TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_sl_prefix, dim3((unsigned)std::min<uint64_t>((S + NWAVE - 1) / NWAVE, 65536)), dim3(NT), 0, st,
-                     (const uint64_t*)G.sl_off, S, (const uint64_t*)G.sl_sdo, G.sl_pn);
+                     G.sl_cls, G.sl_pn);
   TRY(hipGetLastError());
   TRY(hipStreamSynchronize(st));
   G.sl_n = L;

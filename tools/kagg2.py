@@ -17,7 +17,7 @@ r = sorted((x for x in csv.DictReader(open(path)) if "nlp::" in x["Kernel_Name"]
            key=lambda x: int(x["Start_Timestamp"]))
 # the graph build's radix sort (k_rs_*) precedes the first predict kernel; the build's last kernels (the
 # membership table, the short lists' sort and prefix, which follow its own degree-class compaction) end it
-last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_insert", "k_sl_sort", "k_sl_prefix", "k_hp_entry_classes"))),
+last = max((i for i, x in enumerate(r) if any(g in x["Kernel_Name"] for g in ("k_etab_insert", "k_sl_sort", "k_hp_entry_classes"))),
            default=-1)
 first = next(i for i, x in enumerate(r) if i > last and not any(g in x["Kernel_Name"] for g in GRAPH + ("k_rs_", "k_scan")))
 r = r[first:]
