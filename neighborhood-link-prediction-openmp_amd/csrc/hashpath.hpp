@@ -1471,17 +1471,26 @@ __global__ __launch_bounds__(NT) void k_dc_gather(GraphView g, const uint8_t* __
 // LDS); longer rows count their classes in an LDS histogram, scan it, and
 // place 64 entries per step ranked by a ballot multisplit on the class (cursor
 // advanced by the last lane of each class), then scan the row just written
-// (cache-warm; round 5 ran the prefix as a separate pass: 31 ms on C4).
+// (cache-warm; round 5 ran the prefix as a separate pass: 31 ms on C4), each
+// of those loops with several steps' loads in flight.  Rows of long_min
+// entries or more are listed for k_sl_sort_long instead (one wave would walk
+// a hub's ~1e6 entries alone).
 __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo, uint64_t S,
                                                 const uint32_t* __restrict__ ikeys, const uint64_t* __restrict__ isdo,
                                                 uint32_t* __restrict__ okeys, uint64_t* __restrict__ osdo,
-                                                uint8_t* __restrict__ ocls, uint32_t* __restrict__ pn) {
+                                                uint8_t* __restrict__ ocls, uint32_t* __restrict__ pn,
+                                                uint64_t long_min, uint32_t* __restrict__ longrows,
+                                                uint32_t* __restrict__ nlong) {
   __shared__ uint32_t s_h[NWAVE][256];
   __shared__ uint32_t s_n[NWAVE][64];
   const int lane = lane_id(), wv = wave_id();
   for (uint64_t u = (uint64_t)blockIdx.x * NWAVE + wv; u < S; u += (uint64_t)gridDim.x * NWAVE) {
     const uint64_t s = lo[u], n = lo[u + 1] - s;
     if (n == 0) continue;
+    if (n >= long_min) {  // a hub's list: a workgroup of its own (k_sl_sort_long)
+      if (lane == 0) longrows[atomicAdd(nlong, 1u)] = (uint32_t)u;
+      continue;
+    }
     if (n <= 64) {
       const bool ok = (uint64_t)lane < n;
       const uint64_t sd = ok ? isdo[s + lane] : 0ull;
@@ -1504,9 +1513,22 @@ __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo,
       wave_sync_lds();
       continue;
     }
+    // a long row (a hub's short list can hold ~1e6 entries, and one wave owns
+    // it): every loop below issues SL_U steps of loads before using them
+    constexpr int SL_U = 8;
     for (int q = lane; q < 256; q += 64) s_h[wv][q] = 0;
     wave_sync_lds();
-    for (uint64_t j = lane; j < n; j += 64) atomicAdd(&s_h[wv][(uint32_t)(isdo[s + j] >> 48) & 255u], 1u);
+    for (uint64_t j0 = 0; j0 < n; j0 += 64 * SL_U) {
+      uint32_t cq[SL_U];
+#pragma unroll
+      for (int q = 0; q < SL_U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        cq[q] = j < n ? (uint32_t)(isdo[s + j] >> 48) & 255u : 256u;
+      }
+#pragma unroll
+      for (int q = 0; q < SL_U; ++q)
+        if (cq[q] < 256u) atomicAdd(&s_h[wv][cq[q]], 1u);
+    }
     wave_sync_lds();
     {
       uint32_t h[4], t = 0;
@@ -1523,41 +1545,190 @@ __global__ __launch_bounds__(NT) void k_sl_sort(const uint64_t* __restrict__ lo,
       }
     }
     wave_sync_lds();
-    for (uint64_t j0 = 0; j0 < n; j0 += 64) {
-      const uint64_t j = j0 + lane;
-      const bool ok = j < n;
-      const uint64_t sd = ok ? isdo[s + j] : 0ull;
-      const uint32_t key = ok ? ikeys[s + j] : 0u;
-      const uint32_t c = (uint32_t)(sd >> 48) & 255u;
-      uint64_t m = __ballot(ok);
+    constexpr int SL_P = 4;
+    for (uint64_t j00 = 0; j00 < n; j00 += 64 * SL_P) {
+      uint64_t sdq[SL_P];
+      uint32_t kq[SL_P];
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const bool bit = (c >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
+      for (int q = 0; q < SL_P; ++q) {
+        const uint64_t j = j00 + (uint64_t)q * 64 + lane;
+        sdq[q] = j < n ? isdo[s + j] : 0ull;
+        kq[q] = j < n ? ikeys[s + j] : 0u;
       }
-      const uint32_t base = s_h[wv][c];
-      wave_sync_lds();
-      if (ok) {
-        const uint64_t p = s + base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
-        okeys[p] = key;
-        osdo[p] = sd;
-        ocls[p] = (uint8_t)c;
-        if ((m >> lane) == 1ull) s_h[wv][c] = base + (uint32_t)__popcll(m);  // the class's last lane
+#pragma unroll
+      for (int q = 0; q < SL_P; ++q) {
+        const uint64_t j = j00 + (uint64_t)q * 64 + lane;
+        if (j00 + (uint64_t)q * 64 >= n) break;  // wave-uniform
+        const bool ok = j < n;
+        const uint64_t sd = sdq[q];
+        const uint32_t c = (uint32_t)(sd >> 48) & 255u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const bool bit = (c >> b) & 1u;
+          const uint64_t bb = __ballot(bit);
+          m &= bit ? bb : ~bb;
+        }
+        const uint32_t base = s_h[wv][c];
+        wave_sync_lds();
+        if (ok) {
+          const uint64_t p = s + base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+          okeys[p] = kq[q];
+          osdo[p] = sd;
+          ocls[p] = (uint8_t)c;
+          if ((m >> lane) == 1ull) s_h[wv][c] = base + (uint32_t)__popcll(m);  // the class's last lane
+        }
+        wave_sync_lds();
       }
-      wave_sync_lds();
     }
     // the row's prefix of n, read back from the list just written by this wave
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
     uint64_t carry = 0;
-    for (uint64_t j0 = 0; j0 < n; j0 += 64) {
-      const uint64_t j = j0 + lane;
-      const uint64_t x = j < n ? (osdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
-      const uint64_t incl = wave_incl_scan(x) + carry;
-      if (j < n) pn[s + j] = (uint32_t)incl;
-      carry = __shfl(incl, 63, 64);
+    for (uint64_t j0 = 0; j0 < n; j0 += 64 * SL_U) {
+      uint64_t xq[SL_U];
+#pragma unroll
+      for (int q = 0; q < SL_U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        xq[q] = j < n ? (osdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < SL_U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        const uint64_t incl = wave_incl_scan(xq[q]) + carry;
+        if (j < n) pn[s + j] = (uint32_t)incl;
+        carry = __shfl(incl, 63, 64);
+      }
     }
+  }
+}
+
+// k_sl_sort_long: the listed long rows, a workgroup of SLL_NW waves each,
+// every wave a contiguous chunk of the row: per-wave class histograms, per
+// class the waves' exclusive offsets after the classes' starts (stable: chunk
+// order is row order), every chunk placed by the same ballot multisplit, then
+// the prefix of n as chunk sums, their exclusive scan, and a scan per chunk.
+constexpr int SLL_NW = 16, SLL_NT = 64 * SLL_NW;
+constexpr uint64_t SL_LONG = 4096;  // short entries from which a row is k_sl_sort_long's
+__global__ __launch_bounds__(SLL_NT) void k_sl_sort_long(const uint64_t* __restrict__ lo,
+                                                         const uint32_t* __restrict__ rows, uint32_t nrows,
+                                                         const uint32_t* __restrict__ ikeys,
+                                                         const uint64_t* __restrict__ isdo,
+                                                         uint32_t* __restrict__ okeys, uint64_t* __restrict__ osdo,
+                                                         uint8_t* __restrict__ ocls, uint32_t* __restrict__ pn) {
+  __shared__ uint32_t s_h[SLL_NW][256];
+  __shared__ uint32_t s_tot[256];
+  __shared__ uint64_t s_w4[4];
+  __shared__ uint64_t s_sum[SLL_NW];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  constexpr int U = 8, P = 4;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t u = rows[r];
+    const uint64_t s = lo[u], n = lo[u + 1] - s;
+    const uint64_t chunk = ((n + SLL_NW - 1) / SLL_NW + 63) / 64 * 64;
+    const uint64_t c0 = min(n, (uint64_t)wv * chunk), c1 = min(n, c0 + chunk);
+    for (int q = lane; q < 256; q += 64) s_h[wv][q] = 0;
+    wave_sync_lds();
+    for (uint64_t j0 = c0; j0 < c1; j0 += 64 * U) {
+      uint32_t cq[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        cq[q] = j < c1 ? (uint32_t)(isdo[s + j] >> 48) & 255u : 256u;
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        if (cq[q] < 256u) atomicAdd(&s_h[wv][cq[q]], 1u);
+    }
+    __syncthreads();
+    uint32_t run = 0;
+    if (t < 256) {
+      for (int w = 0; w < SLL_NW; ++w) {
+        const uint32_t c = s_h[w][t];
+        s_h[w][t] = run;
+        run += c;
+      }
+    }
+    uint64_t incl = 0;
+    if (t < 256) {  // waves 0-3: the classes' starts
+      incl = wave_incl_scan((uint64_t)run);
+      if (lane == 63) s_w4[wv] = incl;
+    }
+    __syncthreads();
+    if (t < 256) {
+      uint64_t pre = 0;
+      for (int w = 0; w < wv; ++w) pre += s_w4[w];
+      const uint32_t cs = (uint32_t)(pre + incl - run);
+      for (int w = 0; w < SLL_NW; ++w) s_h[w][t] += cs;
+    }
+    __syncthreads();
+    for (uint64_t j00 = c0; j00 < c1; j00 += 64 * P) {
+      uint64_t sdq[P];
+      uint32_t kq[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const uint64_t j = j00 + (uint64_t)q * 64 + lane;
+        sdq[q] = j < c1 ? isdo[s + j] : 0ull;
+        kq[q] = j < c1 ? ikeys[s + j] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        if (j00 + (uint64_t)q * 64 >= c1) break;  // wave-uniform
+        const uint64_t j = j00 + (uint64_t)q * 64 + lane;
+        const bool ok = j < c1;
+        const uint32_t c = (uint32_t)(sdq[q] >> 48) & 255u;
+        uint64_t m = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const bool bit = (c >> b) & 1u;
+          const uint64_t bb = __ballot(bit);
+          m &= bit ? bb : ~bb;
+        }
+        const uint32_t base = s_h[wv][c];
+        wave_sync_lds();
+        if (ok) {
+          const uint64_t p = s + base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+          okeys[p] = kq[q];
+          osdo[p] = sdq[q];
+          ocls[p] = (uint8_t)c;
+          if ((m >> lane) == 1ull) s_h[wv][c] = base + (uint32_t)__popcll(m);
+        }
+        wave_sync_lds();
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // the prefix of n over the sorted row: chunk sums, their exclusive scan, a scan per chunk
+    uint64_t sum = 0;
+    for (uint64_t j0 = c0; j0 < c1; j0 += 64 * U) {
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        sum += j < c1 ? (osdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
+      }
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) s_sum[wv] = sum;
+    __syncthreads();
+    uint64_t carry = 0;
+    for (int w = 0; w < wv; ++w) carry += s_sum[w];
+    for (uint64_t j0 = c0; j0 < c1; j0 += 64 * U) {
+      uint64_t xq[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        xq[q] = j < c1 ? (osdo[s + j] >> HP_SDO_SH) & 0xffull : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const uint64_t j = j0 + (uint64_t)q * 64 + lane;
+        const uint64_t in = wave_incl_scan(xq[q]) + carry;
+        if (j < c1) pn[s + j] = (uint32_t)in;
+        carry = __shfl(in, 63, 64);
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -592,9 +592,23 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
     return NLP_OK;
   }
   TRY(scan_excl_u64<uint32_t>(scnt, S, G.sl_off, G.sl_off + S, scr, st));
+  // rows of SL_LONG short entries or more (hubs) are sorted by a workgroup each
+  uint32_t *lrows = nullptr, *nlong = nullptr;
+  const bool lr_ok = tmp.get(&lrows, L / SL_LONG + 1) && tmp.get(&nlong, 1);
+  if (lr_ok) TRY(hipMemsetAsync(nlong, 0, 4, st));
   hipLaunchKernelGGL(k_sl_sort, dim3((unsigned)std::min<uint64_t>((S + NWAVE - 1) / NWAVE, 65536)), dim3(NT), 0, st,
                      (const uint64_t*)G.sl_off, S, (const uint32_t*)tkeys, (const uint64_t*)tsdo, G.sl_keys, G.sl_sdo,
-                     G.sl_cls, G.sl_pn);
+                     G.sl_cls, G.sl_pn, lr_ok ? (uint64_t)SL_LONG : ~0ull, lrows, nlong);
+  TRY(hipGetLastError());
+  uint32_t nl = 0;
+  if (lr_ok) {
+    TRY(hipMemcpyAsync(&nl, nlong, 4, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+  }
+  if (nl)
+    hipLaunchKernelGGL(k_sl_sort_long, dim3(std::min<uint32_t>(nl, 65535u)), dim3(SLL_NT), 0, st,
+                       (const uint64_t*)G.sl_off, (const uint32_t*)lrows, nl, (const uint32_t*)tkeys,
+                       (const uint64_t*)tsdo, G.sl_keys, G.sl_sdo, G.sl_cls, G.sl_pn);
   TRY(hipGetLastError());
   TRY(hipStreamSynchronize(st));
   G.sl_n = L;

@@ -589,6 +589,37 @@ def test_gpu_hash_path_star_hub(gpu, oracle):
                     assert_canonical_equal(eu, ew, es, u, w, s)
 
 
+def test_gpu_short_lists_of_hub_rows(gpu, oracle):
+    """Hub rows whose class-ordered short lists are long (>= 4096 entries: a
+    workgroup per row, k_sl_sort_long) with mixed classes, beside short rows:
+    the count metrics' prefixes S(u) for several H against the oracle."""
+    L = 9000
+    leaves = np.arange(L)
+    src, dst = [], []
+    for hub in (0, 1):
+        src.append(np.full(L, hub)); dst.append(2 + leaves)
+    for j in range(1, 30):
+        sel = leaves[(leaves % 30) >= j]
+        src.append(2 + sel); dst.append(2 + (sel + j) % L)
+    a = np.concatenate(src).astype(np.int64)
+    b = np.concatenate(dst).astype(np.int64)
+    pairs = np.unique(np.stack([np.minimum(a, b), np.maximum(a, b)], 1), axis=0)
+    pairs = pairs[pairs[:, 0] != pairs[:, 1]]
+    off, keys = _csr_from_pairs(np.concatenate([pairs[:, 0], pairs[:, 1]]),
+                                np.concatenate([pairs[:, 1], pairs[:, 0]]), L + 2)
+    deg = np.diff(off).astype(np.int64)
+    assert deg[0] == L and deg[1] == L and len(np.unique(np.minimum(deg[keys[off[0]:off[1]]], 255))) > 10
+    with _env(NLP_HASH="1"):
+        with gpu.Graph(off, keys) as G:
+            for m in (0, 1, 4, 6):
+                for H in (4, 16, 64):
+                    u, w, sc, t = G.predict(m, H, 20000)
+                    eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=20000)
+                    assert t["path"] == 4
+                    assert_canonical_equal(eu, ew, es, u, w, sc)
+                    assert t["wedges"] == info["wedges_gt"]
+
+
 def test_gpu_final_prune_folded_into_order(gpu, oracle):
     """The call's last prune folded into the 8-byte order (hp_prune fuse: the
     keys >= the k-th sorted straight from the unpruned buffer, the first k

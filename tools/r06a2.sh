@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out/r06a2
+timeout -k 10 400 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_gpu_parity.py > gpurun_out/r06a2/tests.log 2>&1 &&
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r06a2/prof -o create -- python3 -u $GRAFT_REPO_ROOT/tools/create_probe.py --repeat 1 > $GRAFT_REPO_ROOT/gpurun_out/r06a2/probe.log 2>&1
