@@ -202,6 +202,25 @@ __global__ void k_degrees(const uint64_t* __restrict__ off, uint64_t span, uint3
   if ((threadIdx.x & 63) == 0 && mx) atomicMax(maxdeg, mx);
 }
 
+// The AA / RA tables' sparse part: bit d of `present` for every degree d >=
+// d0 that some vertex has (the host computes those entries only, glibc's log
+// being the reference's), and the scatter of the computed entries.
+__global__ void k_deg_present(const uint32_t* __restrict__ deg, uint64_t span, uint32_t d0,
+                              unsigned long long* __restrict__ present) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < span; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = deg[u];
+    if (d >= d0) atomicOr(&present[d >> 6], 1ull << (d & 63));
+  }
+}
+__global__ void k_ctab_scatter(const uint32_t* __restrict__ ds, const double* __restrict__ va,
+                               const double* __restrict__ vr, uint64_t n, double* __restrict__ aa,
+                               double* __restrict__ ra) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    aa[ds[i]] = va[i];
+    ra[ds[i]] = vr[i];
+  }
+}
+
 // keys must be < span and sorted ascending inside each row.  A descent
 // keys[e + 1] < keys[e] is legal only where e + 1 starts a row, so the
 // descents over all entries (desc[0], counted here) must equal the descents at

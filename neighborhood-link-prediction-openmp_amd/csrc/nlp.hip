@@ -924,17 +924,57 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   }
   TRY(clk.mark("edge_filter"));
   // AA / RA contribution tables, computed on the host with the same libm the
-  // reference uses (glibc log), indexed by degree.
-  std::vector<double> aa(g->maxdeg + 1), ra(g->maxdeg + 1);
-  for (uint64_t d = 0; d <= g->maxdeg; ++d) {
-    aa[d] = 1.0 / log((double)d);
-    ra[d] = 1.0 / (double)d;
+  // reference uses (glibc log), indexed by degree: every degree below CT_DENSE,
+  // above it only the degrees some vertex has (C4: maxdeg ~5.7e6, a few
+  // thousand distinct degrees above 65536), scattered on the device
+  {
+    constexpr uint64_t CT_DENSE = 65536;
+    const uint64_t nd = (uint64_t)g->maxdeg + 1, dense = std::min(nd, CT_DENSE);
+    TRY(hmalloc(&g->ctab_aa, nd * 8));
+    TRY(hmalloc(&g->ctab_ra, nd * 8));
+    std::vector<double> aa(dense), ra(dense);
+    for (uint64_t d = 0; d < dense; ++d) {
+      aa[d] = 1.0 / log((double)d);
+      ra[d] = 1.0 / (double)d;
+    }
+    TRY(hipMemcpyAsync(g->ctab_aa, aa.data(), dense * 8, hipMemcpyHostToDevice, st));
+    TRY(hipMemcpyAsync(g->ctab_ra, ra.data(), dense * 8, hipMemcpyHostToDevice, st));
+    if (nd > dense) {
+      const uint64_t words = (nd + 63) / 64;
+      unsigned long long* pres;
+      TRY(wsget(g->ws, B_C32, words * 2, (uint32_t**)&pres));
+      TRY(hipMemsetAsync(pres, 0, words * 8, st));
+      LAUNCH(k_deg_present, S, st, (const uint32_t*)g->deg, S, (uint32_t)dense, pres);
+      TRY(hipGetLastError());
+      std::vector<unsigned long long> hp(words);
+      TRY(hipMemcpyAsync(hp.data(), pres, words * 8, hipMemcpyDeviceToHost, st));
+      TRY(hipStreamSynchronize(st));
+      std::vector<uint32_t> ds;
+      std::vector<double> va, vr;
+      for (uint64_t w = dense / 64; w < words; ++w)
+        for (unsigned long long x = hp[w]; x; x &= x - 1) {
+          const uint64_t d = w * 64 + (uint64_t)__builtin_ctzll(x);
+          if (d < dense || d >= nd) continue;
+          ds.push_back((uint32_t)d);
+          va.push_back(1.0 / log((double)d));
+          vr.push_back(1.0 / (double)d);
+        }
+      if (!ds.empty()) {
+        uint32_t* dd;
+        double *da, *dr;
+        TRY(wsget(g->ws, B_HIST, ds.size(), &dd));
+        TRY(wsget(g->ws, B_HOFF, ds.size(), (uint64_t**)&da));
+        TRY(wsget(g->ws, B_SCAN, ds.size(), (uint64_t**)&dr));
+        TRY(hipMemcpyAsync(dd, ds.data(), ds.size() * 4, hipMemcpyHostToDevice, st));
+        TRY(hipMemcpyAsync(da, va.data(), va.size() * 8, hipMemcpyHostToDevice, st));
+        TRY(hipMemcpyAsync(dr, vr.data(), vr.size() * 8, hipMemcpyHostToDevice, st));
+        LAUNCH(k_ctab_scatter, ds.size(), st, (const uint32_t*)dd, (const double*)da, (const double*)dr,
+               (uint64_t)ds.size(), g->ctab_aa, g->ctab_ra);
+        TRY(hipGetLastError());
+      }
+    }
+    TRY(hipStreamSynchronize(st));
   }
-  TRY(hmalloc(&g->ctab_aa, aa.size() * 8));
-  TRY(hmalloc(&g->ctab_ra, ra.size() * 8));
-  TRY(hipMemcpyAsync(g->ctab_aa, aa.data(), aa.size() * 8, hipMemcpyHostToDevice, st));
-  TRY(hipMemcpyAsync(g->ctab_ra, ra.data(), ra.size() * 8, hipMemcpyHostToDevice, st));
-  TRY(hipStreamSynchronize(st));
   // Wedge budget per chunk of path 2 / limit of path 1: ~1/8 of free HBM at
   // ~44 B per wedge of working set.
   size_t fr = 0, tot = 0;

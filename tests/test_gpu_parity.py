@@ -620,6 +620,31 @@ def test_gpu_short_lists_of_hub_rows(gpu, oracle):
                     assert t["wedges"] == info["wedges_gt"]
 
 
+def test_gpu_aa_ra_tables_beyond_the_dense_degrees(gpu, oracle):
+    """Adamic-Adar / Resource-Allocation through an intermediate of degree
+    70,001 (> 65,536: its contribution computed for the degrees present only,
+    nlp.hip finish_graph): IHub over a source range of leaves, every wedge via
+    the hub, against the oracle on the same range."""
+    import torch
+    L = 70000
+    leaves = np.arange(2, 2 + L, dtype=np.int64)
+    a = np.concatenate([np.ones(L, np.int64), leaves[:-1]])
+    b = np.concatenate([leaves, leaves[1:]])
+    off, keys = _csr_from_pairs(np.concatenate([a, b]), np.concatenate([b, a]), L + 2)
+    assert np.diff(off)[1] == L
+    k = 3000
+    out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
+    with gpu.Graph(off, keys) as G:
+        for m in (7, 8):
+            for H in (0, 100000):
+                n, t = G.predict_device(m, H, k, out, 2, 12)
+                u, w, sc = gpu.edges_from_tensor(out, n)
+                eu, ew, es, info = oracle.predict(off, keys, m, H, max_edges=k, u_begin=2, u_end=12)
+                assert n > 0
+                assert_canonical_equal(eu, ew, es, u, w, sc)
+                assert t["wedges"] == info["wedges_gt"]
+
+
 def test_gpu_final_prune_folded_into_order(gpu, oracle):
     """The call's last prune folded into the 8-byte order (hp_prune fuse: the
     keys >= the k-th sorted straight from the unpruned buffer, the first k
