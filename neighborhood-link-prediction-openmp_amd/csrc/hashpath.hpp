@@ -78,7 +78,7 @@ struct HpArgs {
   const uint32_t* kdeg;  // deg keys[e] per adjacency entry (null: none; KD row kernels)
   const uint64_t* sdo;   // S(u) entries packed deg v << 48 | n << HP_SDO_SH | o, [o, o + n) = N(v) above u (null: none)
   const uint32_t* xs;    // per row: entries of N(u) at or below u (null: none; the exclusion starts after them)
-  unsigned long long* ph;  // diagnostic (NLP_HASH_STATS=1): k_hp_batch wave time per phase, 100 MHz ticks (null: off)
+  unsigned long long* ph;  // diagnostic (NLP_TRACE_BATCH=1 / NLP_TRACE_HUB=1): phase ticks, 100 MHz (null: off)
   uint32_t win;            // k_hp_batch's emission window in slots (0: a reservation per flush; padding in HPC_PAD)
   uint32_t uxf;            // rows whose exclusion slice exceeds uxf x W test the membership table (HP_UX_OFF: never)
 };

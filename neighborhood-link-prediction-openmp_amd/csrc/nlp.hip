@@ -1719,7 +1719,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
   uint64_t *sel, *small;
   TRY(wsget(ws, B_SELHIST, SEL_BINS, &selhist));
   TRY(wsget(ws, B_SEL, 8, &sel));
-  TRY(wsget(ws, B_HP_SMALL, 64, &small));
+  TRY(wsget(ws, B_HP_SMALL, 72, &small));  // [64, 68): NLP_TRACE_BATCH phase ticks
   uint64_t* h = g->host_small;
   h[8] = n;
   h[9] = 0;  // sel: prefix, rank, above, key
@@ -2230,7 +2230,7 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
   uint64_t *wu, *pos, *small;
   TRY(wsget(ws, B_HP_WU, nU + 1, &wu));
   TRY(wsget(ws, B_HP_POS, nU + 1, &pos));
-  TRY(wsget(ws, B_HP_SMALL, 64, &small));
+  TRY(wsget(ws, B_HP_SMALL, 72, &small));  // [64, 68): NLP_TRACE_BATCH phase ticks
   uint64_t* scan;
   TRY(wsget(ws, B_SCAN, scan_scratch_words(nU + 1) + 16, &scan));
   // small: [0,8) chunk counters, [8] tau, [16,24) bounds, [24,28) list sizes, [32..] prune scratch
@@ -2496,6 +2496,9 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     static const bool trace_hub = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
     a.ph = nullptr;  // run_hub points its copy at small[56, 60) when tracing
     if (trace_hub) TRY(hipMemsetAsync(small + 56, 0, 48, st));
+    // NLP_TRACE_BATCH=1 (diagnostic): k_hp_batch's wave time per phase into small[64, 68)
+    static const bool trace_batch = getenv("NLP_TRACE_BATCH") && getenv("NLP_TRACE_BATCH")[0] == '1';
+    if (trace_batch) TRY(hipMemsetAsync(small + 64, 0, 32, st));
     const uint64_t n0 = q1[0] - q0[0], n1 = q1[1] - q0[1];
     bool batch_timed = false;
     if (n0) {
@@ -2543,9 +2546,11 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
           }
         }
         TRY(hipEventRecord(g->ev[5], st));  // the dominant kernel of path 4, timed on its own stream
-        if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
-        else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gb), dim3(NT), 0, st, a, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        HpArgs ab = a;
+        ab.ph = trace_batch ? (unsigned long long*)(small + 64) : nullptr;
+        if (custom) hipLaunchKernelGGL((k_hp_batch<true, 1024, 128>), dim3(gb), dim3(NT), 0, st, ab, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else if (a.kdeg) hipLaunchKernelGGL((k_hp_batch<false, 1024, 128, true>), dim3(gb), dim3(NT), 0, st, ab, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
+        else hipLaunchKernelGGL((k_hp_batch<false, 1024, 128>), dim3(gb), dim3(NT), 0, st, ab, tl, tc, 0, 1, (const uint32_t*)bst, (const uint32_t*)nbat, (const uint64_t*)wu, ua, wbits);
         TRY(hipGetLastError());
         TRY(hipEventRecord(g->ev[6], st));
         batch_timed = true;
@@ -2632,6 +2637,15 @@ nlp_status run_path3(nlp_graph* g, const Params& p, Cands& C, uint32_t* nchunks,
     TRY(hipMemcpyAsync(g->host_small, small, 8 * HPC_NCTR, hipMemcpyDeviceToHost, st));
     TRY(hipStreamSynchronize(st));
     const uint64_t emitted = g->host_small[HPC_EMIT];
+    if (trace_batch) {
+      uint64_t pb[4] = {0, 0, 0, 0};
+      TRY(hipMemcpy(pb, small + 64, 32, hipMemcpyDeviceToHost));
+      const double tot = (double)(pb[0] + pb[1] + pb[2] + pb[3]) + 1e-9;
+      fprintf(stderr, "nlp batch: chunk %u wave ticks (10 ns) setup %llu (%.1f%%) wedges %llu (%.1f%%) exclusion %llu "
+              "(%.1f%%) drain %llu (%.1f%%)\n", *nchunks, (unsigned long long)pb[0], 100.0 * pb[0] / tot,
+              (unsigned long long)pb[1], 100.0 * pb[1] / tot, (unsigned long long)pb[2], 100.0 * pb[2] / tot,
+              (unsigned long long)pb[3], 100.0 * pb[3] / tot);
+    }
     {
       static const bool trace = getenv("NLP_TRACE_HUB") && getenv("NLP_TRACE_HUB")[0] == '1';
       if (trace) {
