@@ -22,8 +22,10 @@ The reference times its whole first-hop scan in every call (predict.hxx:224-230,
 per-graph build of nlp_graph_create (degrees, degree-class index, transposed
 CSR when asymmetric, short lists, edge-membership table, AA/RA tables), so its
 time is spread over main.cxx's 99 calls per batch graph (main.cxx:67-80).
-`graph_create_phases_ms` says where the build went; `resident_call_value` is
-the rate of the resident call alone (not credited).  NLP_DIST_BACKEND=gloo runs
+`graph_create_phases_ms` says where the build went, `roofline_build` bounds
+its largest kernel (k_hp_entry_classes: algorithmic and PMC bytes over its
+phase time); `resident_call_value` is the rate of the resident call alone (not
+credited).  NLP_DIST_BACKEND=gloo runs
 the N > 1 path with ranks sharing one GPU (tests).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--sweep H,H,...]
@@ -255,6 +257,36 @@ def pmc_traffic(config, world, metric, hub, kernel):
             return {"bytes_per_launch": kr["traffic_bytes"], "source": rec.get("source"), "kernel": kernel,
                     "launches_per_call": kr.get("launches_per_call")}
     return None
+
+
+def build_roofline(phases, M, config, world):
+    """The amortized value's largest build kernel, k_hp_entry_classes (one
+    pass over the M adjacency entries: the phase `entry_classes` is its launch,
+    timed by the build with the stream drained at both ends).  Algorithmic
+    bytes per entry, a lower bound: the key (4), v's row bounds off[v],
+    off[v + 1] (16), the class, degree and rank written (1 + 4 + 1); the rank
+    search's probes of N(v) are not counted.  `traffic` from the PMC record of
+    the same config whose build included that kernel."""
+    ms = (phases or {}).get("entry_classes")
+    if not ms or not M:
+        return None
+    alg = 26 * M
+    traffic = src = None
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            for rec in json.load(f).get("records", []):
+                kr = rec.get("kernels", {}).get("k_hp_entry_classes")
+                if kr and rec.get("config") == config and rec.get("n_gpus") == world:
+                    traffic, src = kr["traffic_bytes"], rec.get("source")
+                    break
+    except (OSError, ValueError):
+        pass
+    achieved = alg / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "k_hp_entry_classes", "kernel_ms": ms, "algorithmic_bytes": alg,
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_frac": (traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "traffic_source": src}
 
 
 class Runner:
@@ -548,6 +580,7 @@ def main():
             "graph_gen_released_gb": released_gb,
             "graph_create_s": create_s,
             "graph_create_phases_ms": phases,
+            "roofline_build": build_roofline(phases, ginfo["nnz"], args.config, world) if world == 1 else None,
             # graph_create amortised over main.cxx's 99 calls per batch graph (value's time)
             "amortized_ms_per_call": amortized_ms,
             "resident_call_value": resident_value,

@@ -31,3 +31,16 @@ def test_roofline_pairs_bytes_and_time_of_one_kernel():
     assert r["kernel"] == b.HOT_KERNELS[ids[0]]  # the longer one, not the last call's
     assert r["algorithmic_bytes"] == 200000 and abs(r["kernel_ms"] - 0.020) < 1e-12
     assert abs(r["achieved"] - 200000 / 0.020e-3 / 1e9) < 1e-6
+
+
+def test_build_roofline_names_the_entry_pass():
+    """roofline_build: the amortized value's largest build kernel, its phase
+    time and 26 algorithmic bytes per entry; traffic from the committed PMC
+    record of the config (C4 holds one), none for an unknown config."""
+    b = _bench()
+    r = b.build_roofline({"entry_classes": 200.0, "transpose": 100.0}, 10 ** 9, "C4-sk-2005", 1)
+    assert r["kernel"] == "k_hp_entry_classes" and r["algorithmic_bytes"] == 26 * 10 ** 9
+    assert abs(r["achieved"] - 26e9 / 0.2 / 1e9) < 1e-9 and abs(r["frac"] - r["achieved"] / b.HBM_PEAK_GBS) < 1e-12
+    assert r["traffic"] and r["traffic_frac"] > r["frac"]
+    assert b.build_roofline({"entry_classes": 200.0}, 10 ** 9, "none", 1)["traffic"] is None
+    assert b.build_roofline({}, 10 ** 9, "C4-sk-2005", 1) is None
