@@ -106,12 +106,15 @@ typedef struct {
   uint32_t order_route;     /* path 4: how the final order ran -- NLP_ORDER_FOLD8 (the last prune folded
                                into the 8-byte order), NLP_ORDER_FOLD_REFUSED (folded, the keys refused
                                the 8-byte order: pruned, then the 12-byte sort), NLP_ORDER_SORT8 / _SORT12
-                               (pruned, then the 8-byte / 12-byte sort); 0 for the other paths */
+                               (pruned, then the 8-byte / 12-byte sort); 0 for the other paths; with
+                               NLP_ORDER_RUNS added when the 8-byte order took its two-level form (LSD
+                               passes over (rank, u), then every run of equal (rank, u) put in w order) */
 } nlp_timing;
 #define NLP_ORDER_FOLD8 1
 #define NLP_ORDER_FOLD_REFUSED 2
 #define NLP_ORDER_SORT8 3
 #define NLP_ORDER_SORT12 4
+#define NLP_ORDER_RUNS 16
 
 typedef struct nlp_graph nlp_graph;
 

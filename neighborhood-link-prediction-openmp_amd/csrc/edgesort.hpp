@@ -376,12 +376,13 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
 
 constexpr int ES8_IPT = 16;  // keys per thread of k_es_pass8
 constexpr int ES8_NT = 256;  // its threads: 4096-key tiles (32 KB of keys in LDS, four workgroups per CU)
-constexpr uint64_t ES8_TILE = (uint64_t)ES8_NT * ES8_IPT;
+constexpr int ES8_NTW = 512; // the wide form: 8192-key tiles (64 KB, two workgroups per CU), twice the
+                             // keys per digit run and tile -- fewer partial lines at the runs' ends
 
 // Every record's K8 written to `keys` (the passes then read 8-byte keys only:
 // the rank lookup is paid once), and the first pass's counts: cnt[d * G + g]
-// = the records of range g whose low byte is d, ghist[d] their sum over the
-// ranges.  The score -> rank map is rebuilt per workgroup as an LDS hash of
+// = the records of range g whose digit at bit shift0 is d, ghist[d] their sum
+// over the ranges.  The score -> rank map is rebuilt per workgroup as an LDS hash of
 // the D <= ES_DMAX rank scores (rscore[r], rank order): a lookup is an LDS
 // probe, not a chain of dependent global loads.  Grid: G.
 constexpr int ES8_HLG = 13;  // LDS hash slots: 2 x ES_DMAX
@@ -389,7 +390,8 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
                                                     const float* __restrict__ cs, uint64_t n, int vb,
                                                     const float* __restrict__ rscore, uint32_t D,
                                                     uint32_t* __restrict__ ghist, uint64_t* __restrict__ keys,
-                                                    uint32_t* __restrict__ cnt, uint32_t tpw, uint32_t G) {
+                                                    uint32_t* __restrict__ cnt, uint32_t tpw, uint32_t G,
+                                                    int shift0, uint64_t tile) {
   __shared__ uint32_t h[ES_NT / 64][256];
   __shared__ uint32_t s_hk[1 << ES8_HLG];  // score key + 1 (0: empty)
   __shared__ uint16_t s_hr[1 << ES8_HLG];  // its rank
@@ -411,7 +413,6 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
     return (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)u << vb | w;
   };
   constexpr int UN = 4;
-  const uint64_t tile = ES8_TILE;
   const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
   for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * UN) {
     uint32_t u[UN], w[UN];
@@ -430,7 +431,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
       if (j < hi) {
         const uint64_t k = k8(u[q], w[q], s[q]);
         keys[j] = k;
-        atomicAdd(&h[wv][(uint32_t)k & 0xffu], 1u);
+        atomicAdd(&h[wv][(uint32_t)(k >> shift0) & 0xffu], 1u);
       }
     }
   }
@@ -447,15 +448,24 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
 // The kept candidates (key >= kmin) of an unpruned buffer as K8 keys,
 // compacted in any order (the sort orders them): one reservation per
 // workgroup and 4096 candidates.  The score -> rank map as in k_es_hist8.
+// cnt != nullptr: the first pass's range counts as well (k_es_cnt8's cnt and
+// ghist at bit shift0, ranges of tpw tiles of `tile` keys -- the kept count
+// known beforehand sizes them): a reservation spans two ranges at most,
+// counted in LDS and added once per reservation.
 __global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cu,
                                                     const uint32_t* __restrict__ cw, uint64_t n, uint32_t kmin, int vb,
                                                     const float* __restrict__ rscore, uint32_t D,
-                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ count) {
+                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ count,
+                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ ghist,
+                                                    uint32_t tpw, uint32_t G, int shift0, uint64_t tile) {
   __shared__ uint32_t s_hk[1 << ES8_HLG];
   __shared__ uint16_t s_hr[1 << ES8_HLG];
   __shared__ uint32_t s_wn[ES_NT / 64];
+  __shared__ uint32_t s_h[2][256];  // the reservation's counts: its first range, the next
   __shared__ unsigned long long s_base;
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const uint64_t rsz = (uint64_t)tpw * tile;
+  for (int i = t; i < 512; i += ES_NT) (&s_h[0][0])[i] = 0;
   for (int i = t; i < (1 << ES8_HLG); i += ES_NT) s_hk[i] = 0;
   __syncthreads();
   for (uint32_t r = t; r < D; r += ES_NT) {
@@ -495,11 +505,28 @@ __global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__
         const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
         uint32_t hh = es_dhash(x[q] + 1u, ES8_HLG);
         while (s_hk[hh] != x[q] + 1u) hh = (hh + 1) & ((1u << ES8_HLG) - 1);  // present: every kept key has a rank
-        keys[pos + (uint64_t)__popcll(m & lt)] = (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)cu[j] << vb | cw[j];
+        const uint64_t at = pos + (uint64_t)__popcll(m & lt);
+        const uint64_t k = (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)cu[j] << vb | cw[j];
+        keys[at] = k;
+        if (cnt) atomicAdd(&s_h[at / rsz - s_base / rsz][(uint32_t)(k >> shift0) & 0xffu], 1u);
       }
       pos += (uint64_t)__popcll(m);
     }
     __syncthreads();  // s_wn / s_base are rewritten by the next block
+    if (cnt) {
+      const uint64_t g0 = s_base / rsz;
+      for (int i = t; i < 512; i += ES_NT) {
+        const uint32_t c = (&s_h[0][0])[i];
+        if (c) {
+          const uint32_t d = (uint32_t)i & 0xffu;
+          const uint64_t g = g0 + (uint64_t)(i >> 8);
+          if (g < G) atomicAdd(&cnt[(uint64_t)d * G + g], c);
+          atomicAdd(&ghist[d], c);
+          (&s_h[0][0])[i] = 0;
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -508,7 +535,7 @@ __global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__
 constexpr int ES8_CUN = 8;
 __global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ keys, uint64_t n, int shift,
                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ ghist,
-                                                   uint32_t tpw, uint32_t G) {
+                                                   uint32_t tpw, uint32_t G, uint64_t tile) {
   // four copies per wave (lane & 3), rows padded to 257 words: lanes with the
   // same digit -- the score-rank digits are skewed -- spread over copies and banks
   constexpr int CP = 4, RW = 257;
@@ -516,7 +543,6 @@ __global__ __launch_bounds__(ES_NT) void k_es_cnt8(const uint64_t* __restrict__ 
   const int t = threadIdx.x, wv = wave_id(), cp = lane_id() & (CP - 1);
   for (int i = t; i < ES_NT / 64 * CP * RW; i += ES_NT) (&h[0][0][0])[i] = 0;
   __syncthreads();
-  const uint64_t tile = ES8_TILE;
   const uint64_t lo = min(n, (uint64_t)blockIdx.x * tpw * tile), hi = min(n, lo + (uint64_t)tpw * tile);
   for (uint64_t j0 = lo; j0 < hi; j0 += (uint64_t)ES_NT * ES8_CUN) {
     uint64_t k[ES8_CUN];
@@ -577,12 +603,13 @@ __global__ __launch_bounds__(ES8_GMAX) void k_es_off8(const uint32_t* __restrict
 // the range's running offsets -- the output positions of a stable LSD pass.
 // LAST: the output is the caller's edges (the score of rank r from rscore),
 // the first nout of them.  No workgroup waits on another.
-template <bool LAST>
-__global__ __launch_bounds__(ES8_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
+template <bool LAST, int NTH = ES8_NT>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_es_pass8(
     const float* __restrict__ rscore, const uint64_t* __restrict__ in, uint64_t* __restrict__ out,
     EdgeOut* __restrict__ eout, uint64_t n, int vb, int shift, const uint32_t* __restrict__ off, uint32_t tpw,
     uint32_t G, uint64_t nout) {
-  constexpr int NTH = ES8_NT, ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
+  static_assert(NTH >= 256 && NTH % 64 == 0, "threads 0-255 own one digit each");
+  constexpr int ES_NW = NTH / 64, ES_TILE = NTH * ES8_IPT, WCH = 64 * ES8_IPT;
   __shared__ uint64_t s_k[ES_TILE];
   __shared__ uint32_t s_wc[ES_NW][256];
   __shared__ uint32_t s_run[256];   // the range's next output position per digit
@@ -671,6 +698,153 @@ __global__ __launch_bounds__(ES8_NT) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
     __syncthreads();
     if (t < 256) s_run[t] += cnt;
+  }
+}
+
+// ---------------------------------------------------------------- the two-level order
+// K8 = rank << 2vb | u << vb | w.  The LSD passes of the two-level order run
+// over the (rank, u) bits only -- ceil((rb + vb) / 8) passes instead of
+// ceil((rb + 2 vb) / 8): C4 JAC H=16, 5 instead of 8 -- which leaves every run
+// of equal (rank, u) contiguous and in the canonical run order, its w in any
+// order.  The runs are then put in w order where they lie (w is unique within
+// a run: a candidate (u, w) is one link):
+//   k_es_runs  tiles of ER_TILE keys plus an rs-key window beyond; a run that
+//              starts in the tile and is at most rs long: each key's place is
+//              its run's start plus the keys of the run with a smaller w
+//              (counted in LDS), the edge written there; a longer run's first
+//              key appends the run to the long list
+//   k_es_long  a workgroup per long run: its length found by a scan, at most
+//              lcap keys sorted in LDS (bitonic over w); a run beyond lcap goes
+//              to the very-long list (start, length)
+//   very long  (host) the runs gathered as (run index << vb | w), one
+//              lsd8_keys sort of them, scattered back (k_es_vgather / k_es_vscatter)
+constexpr int ER_IPT = 8;
+constexpr uint32_t ER_TILE = (uint32_t)ES_NT * ER_IPT;  // 4096 keys per tile
+constexpr uint32_t ER_RSMAX = 64;                        // the window beyond the tile (rs <= ER_RSMAX)
+constexpr int EL_NT = 512;
+constexpr uint32_t EL_CAPMAX = 8192;                     // keys of a long run sorted in LDS (lcap <= EL_CAPMAX)
+
+__device__ __forceinline__ EdgeOut er_edge(const float* __restrict__ rscore, uint64_t hi, uint32_t w, int vb) {
+  return EdgeOut{(uint32_t)(hi & ((1ull << vb) - 1ull)), w, rscore[hi >> vb]};
+}
+
+__global__ __launch_bounds__(ES_NT) void k_es_runs(const float* __restrict__ rscore, const uint64_t* __restrict__ keys,
+                                                   uint64_t n, int vb, EdgeOut* __restrict__ eout, uint64_t nout,
+                                                   uint32_t rs, uint64_t* __restrict__ lst, uint64_t lcap,
+                                                   unsigned long long* __restrict__ lcnt) {
+  __shared__ uint64_t s_k[ER_TILE + ER_RSMAX + 1];
+  const uint32_t t = threadIdx.x;
+  const uint64_t vmask = (1ull << vb) - 1ull;
+  for (uint64_t a = (uint64_t)blockIdx.x * ER_TILE; a < n; a += (uint64_t)gridDim.x * ER_TILE) {
+    const uint64_t wb = a ? a - 1 : 0;  // the window: the key before the tile, the tile, rs keys beyond
+    const uint32_t off = a ? 1u : 0u;
+    const uint32_t wn = (uint32_t)min(n - wb, (uint64_t)(off + ER_TILE + rs));
+    const bool cut = wb + wn == n;      // the window reaches the last key
+    __syncthreads();                    // the previous tile's reads are done
+    for (uint32_t i = t; i < wn; i += ES_NT) s_k[i] = keys[wb + i];
+    __syncthreads();
+    const uint32_t tn = (uint32_t)min(n - a, (uint64_t)ER_TILE);
+    // every key of a run that starts in the tile, the window's keys beyond it included
+#pragma unroll 2
+    for (uint32_t x = off + t; x < wn; x += ES_NT) {
+      const uint64_t k = s_k[x], hi = k >> vb;
+      uint32_t s = x;
+      while (s > off && x - s < rs && (s_k[s - 1] >> vb) == hi) --s;
+      if (s > 0 && (s_k[s - 1] >> vb) == hi) continue;  // longer than rs behind x, or begun before the tile
+      if (s >= off + tn) continue;                      // begun after the tile: the next tile's
+      uint32_t e = x + 1;
+      while (e < wn && e - s <= rs && (s_k[e] >> vb) == hi) ++e;
+      const bool ended = e < wn ? (s_k[e] >> vb) != hi : cut;
+      if (ended && e - s <= rs) {
+        const uint32_t w = (uint32_t)(k & vmask);
+        uint32_t r = 0;
+        for (uint32_t j = s; j < e; ++j) r += (uint32_t)(s_k[j] & vmask) < w ? 1u : 0u;
+        const uint64_t pos = wb + s + r;
+        if (pos < nout) eout[pos] = er_edge(rscore, hi, w, vb);
+      } else if (x == s) {
+        const unsigned long long i = atomicAdd(lcnt, 1ull);
+        if (i < lcap) lst[i] = wb + s;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(EL_NT) void k_es_long(const float* __restrict__ rscore, const uint64_t* __restrict__ keys,
+                                                   uint64_t n, int vb, EdgeOut* __restrict__ eout, uint64_t nout,
+                                                   uint32_t lcap, const uint64_t* __restrict__ lst, uint64_t lmax,
+                                                   const unsigned long long* __restrict__ lcnt,
+                                                   uint64_t* __restrict__ vlst, uint64_t vcap,
+                                                   unsigned long long* __restrict__ vcnt) {
+  __shared__ uint32_t s_w[EL_CAPMAX];
+  __shared__ unsigned long long s_len;
+  const uint32_t t = threadIdx.x;
+  const uint64_t vmask = (1ull << vb) - 1ull;
+  const uint64_t nl = min((uint64_t)*lcnt, lmax);
+  for (uint64_t r = blockIdx.x; r < nl; r += gridDim.x) {
+    const uint64_t p = lst[r];
+    const uint64_t hi = keys[p] >> vb;
+    if (t == 0) s_len = ~0ull;
+    __syncthreads();
+    uint64_t L = 0;
+    for (uint64_t c0 = 0;; c0 += lcap) {  // the first key past p of another run (or n), lcap + 1 keys a round
+      for (uint32_t j = t; j <= lcap; j += EL_NT) {
+        const uint64_t q = p + c0 + j;
+        if (q >= n || (keys[q] >> vb) != hi) atomicMin(&s_len, (unsigned long long)(c0 + j));
+        else if (c0 == 0 && j < lcap) s_w[j] = (uint32_t)(keys[q] & vmask);
+      }
+      __syncthreads();
+      L = s_len;
+      __syncthreads();  // every thread read s_len before the next round's atomics
+      if (L != ~0ull) break;
+    }
+    if (L <= lcap) {
+      const uint32_t n2 = L <= 2 ? 2u : 1u << (32 - __builtin_clz((uint32_t)L - 1u));
+      for (uint32_t j = (uint32_t)L + t; j < n2; j += EL_NT) s_w[j] = 0xffffffffu;
+      __syncthreads();
+      for (uint32_t kk = 2; kk <= n2; kk <<= 1)
+        for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+          for (uint32_t i = t; i < n2 / 2; i += EL_NT) {
+            const uint32_t lo = ((i & ~(jj - 1)) << 1) | (i & (jj - 1)), hb = lo + jj;
+            const uint32_t x = s_w[lo], y = s_w[hb];
+            if ((x > y) == ((lo & kk) == 0)) {
+              s_w[lo] = y;
+              s_w[hb] = x;
+            }
+          }
+          __syncthreads();
+        }
+      for (uint32_t j = t; j < L; j += EL_NT)
+        if (p + j < nout) eout[p + j] = er_edge(rscore, hi, s_w[j], vb);
+    } else if (t == 0) {
+      const unsigned long long i = atomicAdd(vcnt, 1ull);
+      if (i < vcap) {
+        vlst[2 * i] = p;
+        vlst[2 * i + 1] = L;
+      }
+    }
+    __syncthreads();  // s_w and s_len are rewritten by the next run
+  }
+}
+
+// the very long runs: vt[3 r] = start, [3 r + 1] length, [3 r + 2] offset in
+// the gathered array; a workgroup per run
+__global__ void k_es_vgather(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vt, uint64_t nv, int vb,
+                             uint64_t* __restrict__ x) {
+  const uint64_t vmask = (1ull << vb) - 1ull;
+  for (uint64_t r = blockIdx.x; r < nv; r += gridDim.x) {
+    const uint64_t p = vt[3 * r], L = vt[3 * r + 1], o = vt[3 * r + 2];
+    for (uint64_t j = threadIdx.x; j < L; j += blockDim.x) x[o + j] = r << vb | (keys[p + j] & vmask);
+  }
+}
+
+__global__ void k_es_vscatter(const float* __restrict__ rscore, const uint64_t* __restrict__ x,
+                              const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vt, uint64_t nv, int vb,
+                              EdgeOut* __restrict__ eout, uint64_t nout) {
+  const uint64_t vmask = (1ull << vb) - 1ull;
+  for (uint64_t r = blockIdx.x; r < nv; r += gridDim.x) {
+    const uint64_t p = vt[3 * r], L = vt[3 * r + 1], o = vt[3 * r + 2], hi = keys[p] >> vb;
+    for (uint64_t j = threadIdx.x; j < L; j += blockDim.x)
+      if (p + j < nout) eout[p + j] = er_edge(rscore, hi, (uint32_t)(x[o + j] & vmask), vb);
   }
 }
 

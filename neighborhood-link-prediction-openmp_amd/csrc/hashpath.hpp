@@ -1617,7 +1617,6 @@ __global__ __launch_bounds__(SLL_NT) void k_sl_sort_long(const uint64_t* __restr
                                                          uint32_t* __restrict__ okeys, uint64_t* __restrict__ osdo,
                                                          uint8_t* __restrict__ ocls, uint32_t* __restrict__ pn) {
   __shared__ uint32_t s_h[SLL_NW][256];
-  __shared__ uint32_t s_tot[256];
   __shared__ uint64_t s_w4[4];
   __shared__ uint64_t s_sum[SLL_NW];
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();

@@ -79,6 +79,7 @@ enum Buf {
   B_ES_HIST, B_ES_DESC, B_ES_TMP,        // edgesort.hpp: histograms + tickets, look-back descriptors, records
   B_ES_SET, B_ES_K0, B_ES_K1,            // edgesort.hpp 8-byte keys: distinct-key set + ranks + scores, key buffers
   B_ES_CNT,                              // 8-byte keys: per-range digit counts + offsets
+  B_ES_RUNS,                             // two-level order: counters, long-run and very-long-run lists
   NBUF
 };
 
@@ -303,8 +304,15 @@ struct nlp_graph {
   size_t es_desc_bytes = 0;  // descriptor buffer the epochs refer to (a new buffer restarts them)
   const void* es_desc_ptr = nullptr;  // and its address (a same-size reallocation restarts them too)
   unsigned occ_es8 = 256;    // resident workgroups of k_es_pass8
+  unsigned occ_es8w = 256;   // and of its wide form (ES8_NTW threads)
+  int es8_nt = ES8_NT;       // the 8-byte passes' workgroup: ES8_NT or ES8_NTW threads (NLP_ES8_NT)
   int es_k8 = 1;             // the final order over rank-compressed 8-byte keys when it qualifies: 1 from
                              // ES8_MIN links on, 2 always (tests), 0 never (NLP_ES8)
+  int es_runs = 1;           // the 8-byte order's two-level form (passes over (rank, u), runs put in w order):
+                             // 1 when it saves two passes or more, 2 whenever the 8-byte order runs, 0 never
+                             // (NLP_ES_RUNS)
+  uint32_t es_rs = ER_RSMAX;   // runs up to this long ranked by k_es_runs (NLP_ES_RS: small values test the rest)
+  uint32_t es_lcap = EL_CAPMAX;  // long runs up to this long sorted in LDS by k_es_long (NLP_ES_LCAP)
   bool hp_aa = true;         // AA / RA route to path 4 like the count metrics (NLP_HASH_AA=0: sort paths only)
   bool hh_sort = true;       // hub pass, AA / RA: sort-mode items instead of the ordered re-walk (NLP_HASH_HUB_SORT=0)
   uint32_t hp_uxf = HB_XF;   // exclusion by the membership table for slices beyond hp_uxf x W
@@ -616,6 +624,29 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
   return NLP_OK;
 }
 
+// The 8-byte passes' launch shape: threads per workgroup, keys per tile,
+// resident workgroups (NLP_ES8_NT=512: the wide form).
+struct Es8Shape {
+  int nt;
+  uint64_t tile;
+  unsigned occ;
+};
+Es8Shape es8_shape(const nlp_graph* g) {
+  return g->es8_nt == ES8_NTW ? Es8Shape{ES8_NTW, (uint64_t)ES8_NTW * ES8_IPT, g->occ_es8w}
+                              : Es8Shape{ES8_NT, (uint64_t)ES8_NT * ES8_IPT, g->occ_es8};
+}
+void es8_pass(const Es8Shape& sh8, bool last, uint32_t G, hipStream_t st, const float* rscore, const uint64_t* src,
+              uint64_t* dst, EdgeOut* out, uint64_t n, int vb, int shift, const uint32_t* offs, uint32_t tpw,
+              uint64_t nout) {
+  if (sh8.nt == ES8_NTW) {
+    if (last) hipLaunchKernelGGL((k_es_pass8<true, ES8_NTW>), dim3(G), dim3(ES8_NTW), 0, st, rscore, src, dst, out, n, vb, shift, offs, tpw, G, nout);
+    else hipLaunchKernelGGL((k_es_pass8<false, ES8_NTW>), dim3(G), dim3(ES8_NTW), 0, st, rscore, src, dst, out, n, vb, shift, offs, tpw, G, nout);
+  } else {
+    if (last) hipLaunchKernelGGL((k_es_pass8<true>), dim3(G), dim3(ES8_NT), 0, st, rscore, src, dst, out, n, vb, shift, offs, tpw, G, nout);
+    else hipLaunchKernelGGL((k_es_pass8<false>), dim3(G), dim3(ES8_NT), 0, st, rscore, src, dst, out, n, vb, shift, offs, tpw, G, nout);
+  }
+}
+
 // A stable LSD sort of n 8-byte keys on the 8-bit digits at `shifts` with
 // the order's range-local passes (edgesort.hpp k_es_cnt8 / k_es_off8 /
 // k_es_pass8: a workgroup per range of consecutive tiles, digit runs written
@@ -628,14 +659,9 @@ nlp_status lsd8_keys(nlp_graph* g, uint64_t* k0, uint64_t* k1, uint64_t n, const
   *which = 0;
   if (n == 0 || n >= (1ull << 32) || np > ES_MAXP) return NLP_OK;
   Workspace& ws = g->ws;
-  int nb = 0;
-  TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_es_pass8<false>, ES8_NT, 0));
-  int dev = 0, cus = 0;
-  TRY(hipGetDevice(&dev));
-  TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const uint64_t ntiles = (n + ES8_TILE - 1) / ES8_TILE;
-  uint32_t G = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({ntiles, (uint64_t)cus * (uint64_t)std::max(nb, 1), (uint64_t)ES8_GMAX}));
+  const Es8Shape sh8 = es8_shape(g);
+  const uint64_t ntiles = (n + sh8.tile - 1) / sh8.tile;
+  uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)sh8.occ, (uint64_t)ES8_GMAX}));
   const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
   G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
   uint32_t* hw;  // [np][256] digit totals
@@ -647,11 +673,11 @@ nlp_status lsd8_keys(nlp_graph* g, uint64_t* k0, uint64_t* k1, uint64_t n, const
   const uint64_t* src = k0;
   for (int r = 0; r < np; ++r) {
     uint64_t* dst = (r & 1) ? k0 : k1;
-    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, shifts[r], cnt, hw + r * 256, tpw, G);
+    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, shifts[r], cnt, hw + r * 256, tpw, G,
+                       sh8.tile);
     hipLaunchKernelGGL(k_es_off8, dim3(256), dim3(ES8_GMAX), 0, st, (const uint32_t*)cnt,
                        (const uint32_t*)(hw + r * 256), G, offs);
-    hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES8_NT), 0, st, (const float*)nullptr, src, dst,
-                       (EdgeOut*)nullptr, n, 0, shifts[r], (const uint32_t*)offs, tpw, G, (uint64_t)0);
+    es8_pass(sh8, false, G, st, nullptr, src, dst, nullptr, n, 0, shifts[r], offs, tpw, 0);
     TRY(hipGetLastError());
     src = dst;
   }
@@ -1022,6 +1048,10 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* e8 = getenv("NLP_ES8")) g->es_k8 = std::min(2, std::max(0, atoi(e8)));
+  if (const char* en = getenv("NLP_ES8_NT")) g->es8_nt = atoi(en) == ES8_NTW ? ES8_NTW : ES8_NT;
+  if (const char* er = getenv("NLP_ES_RUNS")) g->es_runs = std::min(2, std::max(0, atoi(er)));
+  if (const char* rs = getenv("NLP_ES_RS")) g->es_rs = (uint32_t)std::min<long>(ER_RSMAX, std::max(1l, atol(rs)));
+  if (const char* lc = getenv("NLP_ES_LCAP")) g->es_lcap = (uint32_t)std::min<long>(EL_CAPMAX, std::max(2l, atol(lc)));
   if (const char* ux = getenv("NLP_HASH_UX")) g->hp_uxf = strcmp(ux, "off") == 0 ? HP_UX_OFF : (uint32_t)atoi(ux);
   if (const char* hd = getenv("NLP_HH_DIRECT")) g->hh_dw = (uint32_t)std::max<long>(0, std::min<long>(HH_DW, atol(hd)));
   if (const char* ha = getenv("NLP_HASH_AA")) g->hp_aa = ha[0] != '0';
@@ -1051,6 +1081,7 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
     TRY(occ((const void*)k_sp_pass<uint64_t, OS2_IPT>, &g->occ_p64, OS_NT));
     TRY(occ((const void*)k_es_pass<false>, &g->occ_es, ES_NT));
     TRY(occ((const void*)k_es_pass8<false>, &g->occ_es8, ES8_NT));
+    TRY(occ((const void*)k_es_pass8<false, ES8_NTW>, &g->occ_es8w, ES8_NTW));
     TRY(occ((const void*)k_hp_batch<false, 1024, 128, true>, &g->occ_hb));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT>, &g->occ_p32, OS_NT));
     TRY(occ((const void*)k_sp_pass<uint32_t, OS2_IPT, false, false, GAP_NONE, 11>, &g->occ_p11, OS_NT));
@@ -1120,6 +1151,7 @@ struct Cands {
   // path 4, final prune folded into the order: the n held are unpruned, the
   // order keeps the keys >= kmin and writes the first `keep` (0: pruned)
   uint64_t keep = 0, cap = 0;
+  uint64_t kcnt = 0;  // the unpruned buffer's candidates >= kmin (the prune's select: above + ties)
   uint32_t kmin = 0;
   uint32_t route = 0;  // path 4: how the final order ran (nlp_timing.order_route)
 };
@@ -1743,6 +1775,7 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
       *kth = (uint32_t)key;
       C.keep = k;
       C.kmin = (uint32_t)key;
+      C.kcnt = above + ties;
       C.cap = cap;
       C.call_bytes += 12 * n;  // three select histograms
       return NLP_OK;
@@ -1841,6 +1874,69 @@ nlp_status es_descs(nlp_graph* g, uint64_t ntiles, int P, uint64_t** desc, hipSt
   return NLP_OK;
 }
 
+// The two-level order's run pass (edgesort.hpp k_es_runs, k_es_long; the very
+// long runs by k_es_vgather, lsd8_keys and k_es_vscatter): `keys` (n K8 keys)
+// sorted by (rank, u), every run of equal (rank, u) put in w order and the
+// first nout written to `out` as edges.  `spare` (n keys) is free scratch.
+nlp_status es_runs_order(nlp_graph* g, const float* rscore, const uint64_t* keys, uint64_t* spare, uint64_t n, int vb,
+                         EdgeOut* out, uint64_t nout, hipStream_t st) {
+  Workspace& ws = g->ws;
+  const uint32_t rs = std::min<uint32_t>(std::max<uint32_t>(g->es_rs, 1), ER_RSMAX);
+  const uint32_t lcap = std::min<uint32_t>(std::max<uint32_t>(g->es_lcap, 2), EL_CAPMAX);
+  // a long run is longer than rs, a very long one than lcap: the lists' bounds
+  const uint64_t lmax = n / (rs + 1) + 1, vmax = n / (lcap + 1) + 1;
+  uint64_t* rb;  // [0] long runs, [1] very long runs, the long list, (start, length) pairs, the run table
+  TRY(wsget(ws, B_ES_RUNS, 2 + lmax + 5 * vmax, &rb));
+  uint64_t *lst = rb + 2, *vl = lst + lmax, *vt = vl + 2 * vmax;
+  TRY(hipMemsetAsync(rb, 0, 16, st));
+  const uint64_t ntl = (n + ER_TILE - 1) / ER_TILE;
+  hipLaunchKernelGGL(k_es_runs, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ntl, 2048))), dim3(ES_NT), 0,
+                     st, rscore, keys, n, vb, out, nout, rs, lst, lmax, (unsigned long long*)rb);
+  hipLaunchKernelGGL(k_es_long, dim3(512), dim3(EL_NT), 0, st, rscore, keys, n, vb, out, nout, lcap,
+                     (const uint64_t*)lst, lmax, (const unsigned long long*)rb, vl, vmax, (unsigned long long*)(rb + 1));
+  TRY(hipGetLastError());
+  uint64_t hc[2] = {0, 0};
+  TRY(hipMemcpyAsync(hc, rb, 16, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  if (hc[0] > lmax || hc[1] > vmax) return NLP_ERR_DEVICE;  // the lists' bounds are exact: never expected
+  static const bool trace = getenv("NLP_TRACE_RUNS") && getenv("NLP_TRACE_RUNS")[0] == '1';
+  if (trace)
+    fprintf(stderr, "nlp runs: %llu keys, %llu runs beyond %u keys, %llu beyond %u\n", (unsigned long long)n,
+            (unsigned long long)hc[0], rs, (unsigned long long)hc[1], lcap);
+  if (hc[1] == 0) return NLP_OK;
+  const uint64_t nv = hc[1];
+  std::vector<uint64_t> pr(2 * nv), tab(3 * nv);
+  TRY(hipMemcpyAsync(pr.data(), vl, 16 * nv, hipMemcpyDeviceToHost, st));
+  TRY(hipStreamSynchronize(st));
+  uint64_t tot = 0;
+  for (uint64_t r = 0; r < nv; ++r) {
+    tab[3 * r] = pr[2 * r];
+    tab[3 * r + 1] = pr[2 * r + 1];
+    tab[3 * r + 2] = tot;
+    tot += pr[2 * r + 1];
+  }
+  if (tot > n) return NLP_ERR_DEVICE;
+  TRY(hipMemcpyAsync(vt, tab.data(), 24 * nv, hipMemcpyHostToDevice, st));
+  uint64_t* x1;
+  TRY(wsget(ws, B_ES_TMP, tot, &x1));
+  const unsigned gv = (unsigned)std::min<uint64_t>(nv, 4096);
+  hipLaunchKernelGGL(k_es_vgather, dim3(gv), dim3(256), 0, st, keys, (const uint64_t*)vt, nv, vb, spare);
+  TRY(hipGetLastError());
+  // (run index, w): the runs keep their places and lengths, each in w order
+  const int nb = vb + (nv > 1 ? bits_for(nv - 1) : 0);
+  int shifts[ES_MAXP], np = 0;
+  for (int b = 0; b < nb && np < ES_MAXP; b += 8) shifts[np++] = b;
+  int which = 0;
+  bool sorted = false;
+  { nlp_status s = lsd8_keys(g, spare, x1, tot, shifts, np, &which, st, &sorted); if (s != NLP_OK) return s; }
+  if (!sorted) return NLP_ERR_INVALID;
+  hipLaunchKernelGGL(k_es_vscatter, dim3(gv), dim3(256), 0, st, rscore, (const uint64_t*)(which ? x1 : spare), keys,
+                     (const uint64_t*)vt, nv, vb, out, nout);
+  TRY(hipGetLastError());
+  TRY(hipStreamSynchronize(st));  // `tab` is read by the copy above
+  return NLP_OK;
+}
+
 // es_sort over rank-compressed 8-byte keys (edgesort.hpp k_es_dkeys, k_es_hist8,
 // k_es_pass8).  *done = false when the call does not qualify (too many distinct
 // score keys, a NaN or zero score, too many key bits): nothing was written.
@@ -1850,7 +1946,7 @@ nlp_status es_descs(nlp_graph* g, uint64_t ntiles, int P, uint64_t** desc, hipSt
 // into the sort (the canonical tie rule is the sort order itself).
 nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
                     hipStream_t st, uint64_t* bytes, bool* done, const uint32_t* ckey = nullptr, uint32_t kmin = 0,
-                    uint64_t nout = UINT64_MAX) {
+                    uint64_t nout = UINT64_MAX, bool* runs = nullptr, uint64_t kcnt = 0) {
   *done = false;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
@@ -1889,66 +1985,99 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   }
   TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
   uint64_t *k0 = nullptr, *k1 = nullptr;
-  if (ckey) {  // the kept candidates' keys, compacted: the sort's n is their count
-    TRY(wsget(ws, B_ES_K0, n, &k0));
-    unsigned long long* kc = (unsigned long long*)(dcnt + 2);  // zeroed with the set
-    hipLaunchKernelGGL(k_es_keep8, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)),
-                       dim3(ES_NT), 0, st, ckey, cu, cw, n, kmin, vb, (const float*)rscore, D, k0, kc);
-    TRY(hipGetLastError());
-    unsigned long long kept = 0;
-    TRY(hipMemcpyAsync(&kept, kc, 8, hipMemcpyDeviceToHost, st));
-    TRY(hipStreamSynchronize(st));
-    if (kept < std::min<uint64_t>(nout, n) || kept > n) return NLP_ERR_DEVICE;
-    n = kept;
-  }
-  // the keys (and the first pass's range counts) in one read; P passes cover
-  // the rb + 2 vb key bits (every higher digit is zero)
-  const uint64_t ntiles = (n + ES8_TILE - 1) / ES8_TILE;
-  uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)g->occ_es8, (uint64_t)ES8_GMAX}));
-  const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
-  G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
-  const int P = std::max(1, (rb + 2 * vb + 7) / 8);
+  // the sort's key count: the kept candidates' when the buffer is unpruned
+  // (known beforehand from the prune's select when kcnt is given)
+  const uint64_t ns = ckey ? (kcnt ? kcnt : 0) : n;
+  // the two-level form (edgesort.hpp k_es_runs): passes over the (rank, u)
+  // bits only, then the runs of equal (rank, u) put in w order in place -- the
+  // run pass stands in for the last pass (both read the keys and write the
+  // edges), so it pays from two passes saved
+  const int Pf = std::max(1, (rb + 2 * vb + 7) / 8), Ph = std::max(1, (rb + vb + 7) / 8);
+  const bool two = g->es_runs == 2 || (g->es_runs == 1 && Ph + 2 <= Pf);
+  const int P = two ? Ph : Pf, sh0 = two ? vb : 0;
+  // ranges of tpw tiles, one workgroup each
+  const Es8Shape sh8 = es8_shape(g);
+  uint32_t G = 1, tpw = 1;
+  auto ranges = [&](uint64_t nn) {
+    const uint64_t ntiles = (nn + sh8.tile - 1) / sh8.tile;
+    G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)sh8.occ, (uint64_t)ES8_GMAX}));
+    tpw = (uint32_t)std::max<uint64_t>(1, (ntiles + G - 1) / G);
+    G = (uint32_t)std::max<uint64_t>(1, (ntiles + tpw - 1) / tpw);  // every range non-empty
+  };
   uint32_t* hw;  // [P][256] digit totals
   TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
   TRY(hipMemsetAsync(hw, 0, (uint64_t)P * 256 * 4, st));
   uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
-  TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+  bool counted = false;  // the first pass's counts made with the keys
+  if (ckey) {  // the kept candidates' keys, compacted: the sort's n is their count
+    TRY(wsget(ws, B_ES_K0, n, &k0));
+    unsigned long long* kc = (unsigned long long*)(dcnt + 2);  // zeroed with the set
+    if (ns) {
+      ranges(ns);
+      TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+      TRY(hipMemsetAsync(cnt, 0, (uint64_t)256 * G * 4, st));
+      counted = true;
+    }
+    hipLaunchKernelGGL(k_es_keep8, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)),
+                       dim3(ES_NT), 0, st, ckey, cu, cw, n, kmin, vb, (const float*)rscore, D, k0, kc,
+                       counted ? cnt : (uint32_t*)nullptr, hw, tpw, G, sh0, sh8.tile);
+    TRY(hipGetLastError());
+    unsigned long long kept = 0;
+    TRY(hipMemcpyAsync(&kept, kc, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (kept < std::min<uint64_t>(nout, n) || kept > n || (ns && kept != ns)) return NLP_ERR_DEVICE;
+    n = kept;
+  }
+  if (!counted) {
+    ranges(n);
+    TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+  }
   uint32_t* offs = cnt + (uint64_t)256 * G;
+  {
+    static const bool trace = getenv("NLP_TRACE_RUNS") && getenv("NLP_TRACE_RUNS")[0] == '1';
+    if (trace)
+      fprintf(stderr, "nlp order: %llu keys, %u scores (%d rank bits), %d id bits, %d passes (%d without runs), "
+              "%d-thread passes, first counts %s\n", (unsigned long long)n, D, rb, vb, P, Pf, sh8.nt,
+              counted ? "with the kept keys" : "by a read");
+  }
   if (!ckey) TRY(wsget(ws, B_ES_K0, n, &k0));
-  if (P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
-  if (ckey) {
-    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, (const uint64_t*)k0, n, 0, cnt, hw, tpw, G);
-  } else {
+  if (two || P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
+  if (ckey && !counted) {
+    hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, (const uint64_t*)k0, n, sh0, cnt, hw, tpw, G,
+                       sh8.tile);
+  } else if (!ckey) {
     hipLaunchKernelGGL(k_es_hist8, dim3(G), dim3(ES_NT), 0, st, cu, cw, cs, n, vb, (const float*)rscore, D, hw, k0,
-                       cnt, tpw, G);
+                       cnt, tpw, G, sh0, sh8.tile);
   }
   TRY(hipGetLastError());
   // scores (4 B), columns in and keys out (20 B), every later pass's count
   // read (8 B), every pass but the last 8 in and out, the last 8 in, 12 out;
   // filtered: keys of every candidate (8 B), the kept ones' columns (8 B) and
-  // keys out (8 B), the first pass's count read (8 B)
+  // keys out (8 B), the first pass's count read (8 B); two-level: P passes
+  // of keys, the run pass 8 in, 12 out
   const uint64_t nw = std::min<uint64_t>(nout, n);
   if (bytes)
-    *bytes += (ckey ? 8 * n_in + 24 * n : 24 * n) + 24 * n * (uint64_t)(P - 1) + 8 * n + 12 * nw;
+    *bytes += (ckey ? 8 * n_in + (counted ? 16 : 24) * n : 24 * n) + 24 * n * (uint64_t)(two ? P : P - 1) + 8 * n +
+              12 * nw;
   const uint64_t* src = k0;  // k_es_hist8 wrote every key
   for (int r = 0; r < P; ++r) {
     uint64_t* dst = (r & 1) ? k0 : k1;
+    const int sh = sh0 + 8 * r;
     if (r > 0) {  // this pass's range counts: one read of its input
-      hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, 8 * r, cnt, hw + r * 256, tpw, G);
+      hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, src, n, sh, cnt, hw + r * 256, tpw, G, sh8.tile);
       TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_es_off8, dim3(256), dim3(ES8_GMAX), 0, st, (const uint32_t*)cnt,
                        (const uint32_t*)(hw + r * 256), G, offs);
     TRY(hipGetLastError());
-    const bool last = r == P - 1;
-    if (last)
-      hipLaunchKernelGGL(k_es_pass8<true>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
-                         8 * r, (const uint32_t*)offs, tpw, G, nw);
-    else
-      hipLaunchKernelGGL(k_es_pass8<false>, dim3(G), dim3(ES8_NT), 0, st, (const float*)rscore, src, dst, out, n, vb,
-                         8 * r, (const uint32_t*)offs, tpw, G, nw);
+    es8_pass(sh8, r == P - 1 && !two, G, st, (const float*)rscore, src, dst, out, n, vb, sh, offs, tpw, nw);
     TRY(hipGetLastError());
     src = dst;
+  }
+  if (two) {
+    nlp_status s = es_runs_order(g, (const float*)rscore, src, src == k0 ? k1 : k0, n, vb, out, nw, st);
+    if (s != NLP_OK) return s;
+    if (runs) *runs = true;
   }
   *done = true;
   return NLP_OK;
@@ -1960,11 +2089,11 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
                    hipStream_t st, uint64_t* bytes = nullptr, bool try8 = true, uint32_t* route = nullptr) {
   if (n == 0) return NLP_OK;
   if (try8 && ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2)) {
-    bool done = false;
-    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done);
+    bool done = false, runs = false;
+    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done, nullptr, 0, UINT64_MAX, &runs);
     if (s != NLP_OK) return s;
     if (done) {
-      if (route) *route = NLP_ORDER_SORT8;
+      if (route) *route = NLP_ORDER_SORT8 | (runs ? NLP_ORDER_RUNS : 0u);
       return NLP_OK;
     }
   }
@@ -2024,16 +2153,17 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
 nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st) {
   if (C.n == 0) return NLP_OK;
   if (C.keep) {  // the last prune folded into the 8-byte order
-    bool done = false;
+    bool done = false, runs = false;
     Workspace& ws = g->ws;
     nlp_status s = es_sort8(g, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], C.n,
-                            d_out, st, &C.call_bytes, &done, (const uint32_t*)ws.p[B_CKEY], C.kmin, C.keep);
+                            d_out, st, &C.call_bytes, &done, (const uint32_t*)ws.p[B_CKEY], C.kmin, C.keep, &runs,
+                            C.kcnt);
     if (s != NLP_OK) return s;
     const uint64_t keep = C.keep;
     C.keep = 0;
     if (done) {
       C.n = keep;
-      C.route = NLP_ORDER_FOLD8;
+      C.route = NLP_ORDER_FOLD8 | (runs ? NLP_ORDER_RUNS : 0u);
       return NLP_OK;
     }
     // the keys do not qualify (too many distinct scores, ...): prune, then the

@@ -499,7 +499,9 @@ class _env:
 # membership table, 19 every row's by marks (no table), 20 the count metrics'
 # survivor lists compacted per call (k_dc_*, the AA / RA route), 21 short lists
 # of the classes up to 3 only, 22 / 23 the final order over rank-compressed
-# 8-byte keys on every call (by default from ES8_MIN links on)
+# 8-byte keys on every call (by default from ES8_MIN links on), 24 its
+# two-level form on every call with runs beyond 2 keys by k_es_long and beyond
+# 8 by the very-long sort
 HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="3", NLP_HASH_SCAP="300", NLP_HASH_HUB="0"),
                  dict(NLP_HASH_BATCH="0"), dict(NLP_HASH_MINBIN="2", NLP_HASH_HUB="0"),
@@ -513,7 +515,8 @@ HASH_VARIANTS = [dict(), dict(NLP_HASH_MINBIN="1"), dict(NLP_HASH_MINBIN="2"),
                  dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="0"), dict(NLP_HASH_MINBIN="1", NLP_HASH_ROWB="2"),
                  dict(NLP_HASH_UX="0", NLP_HASH_MINBIN="1"), dict(NLP_HASH_UX="off"),
                  dict(NLP_HASH_SLIST="0"), dict(NLP_HASH_SLIST="3"),
-                 dict(NLP_ES8="2"), dict(NLP_ES8="2", NLP_HASH_MINBIN="2")]
+                 dict(NLP_ES8="2"), dict(NLP_ES8="2", NLP_HASH_MINBIN="2"),
+                 dict(NLP_ES8="2", NLP_ES_RUNS="2", NLP_ES_RS="2", NLP_ES_LCAP="8")]
 
 
 @pytest.mark.parametrize("variant", range(len(HASH_VARIANTS)))
@@ -663,12 +666,39 @@ def test_gpu_final_prune_folded_into_order(gpu, oracle):
                         for k in (70000, 250000):
                             u, w, s, t = G.predict(m, H, k)
                             assert t["path"] == 4
-                            routes.setdefault(m, set()).add(t["order_route"])
+                            routes.setdefault(m, set()).add(t["order_route"] & 15)  # 16: the two-level form
                             eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
                             assert_canonical_equal(eu, ew, es, u, w, s)
     assert 1 in routes[1], routes                 # Jaccard: the fold
     assert not routes[7] & {1, 2}, routes         # Adamic-Adar: never folded
     assert all(r in (1, 2, 3, 4) for rs in routes.values() for r in rs), routes
+
+
+def test_gpu_two_level_order(gpu, oracle):
+    """The 8-byte order's two-level form (edgesort.hpp k_es_runs): LSD passes
+    over (rank, u) only, then every run of equal (rank, u) put in w order in
+    place -- runs ranked in their tile (up to NLP_ES_RS keys, across tile
+    boundaries), sorted by a workgroup (k_es_long, up to NLP_ES_LCAP) and by
+    the very-long gather + sort; Common Neighbours has long runs (few distinct
+    counts), Jaccard short ones; several tiles of keys, the fold's first k of
+    an unpruned buffer; exact against the oracle, route flagged."""
+    off, keys = random_csr(20000, 16, 41)
+    ran = 0
+    for env in (dict(), dict(NLP_ES_RS="1", NLP_ES_LCAP="2"), dict(NLP_ES_RS="3", NLP_ES_LCAP="16"),
+                dict(NLP_ES_LCAP="64", NLP_HASH_EMIT="300000")):
+        with _env(NLP_HASH="1", NLP_ES_RUNS="2", **env):
+            with gpu.Graph(off, keys) as G:
+                for m in (1, 0, 7, 2):
+                    for H in (0, 16):
+                        for k in (70000, 250000):
+                            u, w, s, t = G.predict(m, H, k)
+                            assert t["path"] == 4
+                            if t["order_route"] & 15 in (1, 3):  # the 8-byte order ran
+                                assert t["order_route"] & 16, t["order_route"]
+                                ran += 1
+                            eu, ew, es, _ = oracle.predict(off, keys, m, H, max_edges=k)
+                            assert_canonical_equal(eu, ew, es, u, w, s)
+    assert ran >= 16, ran
 
 
 def test_gpu_hash_routing_and_shards(gpu, oracle):

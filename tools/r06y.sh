@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r06y
+timeout -k 10 400 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_gpu_parity.py -k "two_level or folded_into_order or hash_path_vs_oracle and (22 or 23 or 24)" > gpurun_out/r06y/tests.log 2>&1 &&
+NLP_ES8_NT=512 timeout -k 10 300 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_gpu_parity.py -k "two_level or folded_into_order" > gpurun_out/r06y/tests_wide.log 2>&1 &&
+NLP_TRACE_RUNS=1 timeout -k 10 400 python3 -u tools/sweep.py --config C4-sk-2005 --metrics JAC,CN,AA --hubs 16 --cpu-hubs '' --reps 3 --envs 'NLP_ES_RUNS=0;NLP_ES_RUNS=1;NLP_ES_RUNS=0,NLP_ES8_NT=512;NLP_ES_RUNS=1,NLP_ES8_NT=512' > gpurun_out/r06y/sweep.log 2>&1 &&
+timeout -k 10 300 python3 -u tools/create_probe.py --repeat 1 --envs 'NLP_ES8_NT=256;NLP_ES8_NT=512' > gpurun_out/r06y/probe.log 2>&1

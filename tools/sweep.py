@@ -83,6 +83,13 @@ def main():
         G.close()
 
 
+def _checksum(out, cnt):
+    """Position-weighted sum of the links (u, w, score bits): equal outputs give equal sums."""
+    x = out[:cnt].to(torch.int64)
+    pos = torch.arange(1, cnt + 1, device=out.device, dtype=torch.int64)
+    return int(((x[:, 0] * 1000003 + x[:, 1]) * 1000033 + x[:, 2]).mul(pos).sum().item())
+
+
 def run_sweep(args, nlp, G, out, k, span, nnz, b_alg, csr, cpu_hubs, cpu_metrics, drv, cores, envspec):
     for metric in args.metrics.split(","):
         mid = nlp.METRICS.index(metric)
@@ -97,7 +104,8 @@ def run_sweep(args, nlp, G, out, k, span, nnz, b_alg, csr, cpu_hubs, cpu_metrics
                     "chunks": t["chunks"], "wedges": t["wedges"], "candidates": t["candidates"],
                     "hot_kernel": t.get("hot_kernel"), "hot_ms": t.get("hot_ms"), "hot_bytes": t.get("hot_bytes"),
                     "gpu_predicted_per_s": cnt / (wall / 1e3), "gpu_wedges_per_s": t["wedges"] / (wall / 1e3),
-                    "n": span - 1, "M": nnz}
+                    "n": span - 1, "M": nnz, "order_route": t.get("order_route"),
+                    "checksum": _checksum(out, cnt)}
             ba = b_alg(H, cnt)
             line.update(call_alg_bytes=ba, call_effective_gbs=ba / (wall / 1e3) / 1e9)
             if csr and H in cpu_hubs and metric in cpu_metrics and os.path.exists(drv):
