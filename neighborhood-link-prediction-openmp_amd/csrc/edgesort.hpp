@@ -776,28 +776,40 @@ __global__ __launch_bounds__(EL_NT) void k_es_long(const float* __restrict__ rsc
                                                    uint64_t* __restrict__ vlst, uint64_t vcap,
                                                    unsigned long long* __restrict__ vcnt) {
   __shared__ uint32_t s_w[EL_CAPMAX];
-  __shared__ unsigned long long s_len;
+  __shared__ uint32_t s_first;
   const uint32_t t = threadIdx.x;
   const uint64_t vmask = (1ull << vb) - 1ull;
   const uint64_t nl = min((uint64_t)*lcnt, lmax);
   for (uint64_t r = blockIdx.x; r < nl; r += gridDim.x) {
     const uint64_t p = lst[r];
     const uint64_t hi = keys[p] >> vb;
-    if (t == 0) s_len = ~0ull;
-    __syncthreads();
+    // the run's length by a search of EL_NT probes a round: galloping (the
+    // probes lo + (t + 1) step, step x EL_NT while every probe is in the run),
+    // then narrowing (step / EL_NT) -- a few rounds whatever the length
+    uint64_t lo = 0, step = 1;  // key p + lo is in the run
     uint64_t L = 0;
-    for (uint64_t c0 = 0;; c0 += lcap) {  // the first key past p of another run (or n), lcap + 1 keys a round
-      for (uint32_t j = t; j <= lcap; j += EL_NT) {
-        const uint64_t q = p + c0 + j;
-        if (q >= n || (keys[q] >> vb) != hi) atomicMin(&s_len, (unsigned long long)(c0 + j));
-        else if (c0 == 0 && j < lcap) s_w[j] = (uint32_t)(keys[q] & vmask);
-      }
+    while (true) {
+      if (t == 0) s_first = EL_NT;
       __syncthreads();
-      L = s_len;
-      __syncthreads();  // every thread read s_len before the next round's atomics
-      if (L != ~0ull) break;
+      const uint64_t q = p + lo + (uint64_t)(t + 1) * step;
+      if (q >= n || (keys[q] >> vb) != hi) atomicMin(&s_first, t);
+      __syncthreads();
+      const uint32_t f = s_first;
+      __syncthreads();  // every thread read s_first before the next round resets it
+      if (f == EL_NT) {  // every probe in the run (only while galloping)
+        lo += (uint64_t)EL_NT * step;
+        step *= EL_NT;
+        continue;
+      }
+      lo += (uint64_t)f * step;  // in the run; the end within (lo, lo + step]
+      if (step == 1) {
+        L = lo + 1;
+        break;
+      }
+      step = (step + EL_NT - 1) / EL_NT;  // the probes still reach lo + step
     }
     if (L <= lcap) {
+      for (uint32_t j = t; j < L; j += EL_NT) s_w[j] = (uint32_t)(keys[p + j] & vmask);
       const uint32_t n2 = L <= 2 ? 2u : 1u << (32 - __builtin_clz((uint32_t)L - 1u));
       for (uint32_t j = (uint32_t)L + t; j < n2; j += EL_NT) s_w[j] = 0xffffffffu;
       __syncthreads();

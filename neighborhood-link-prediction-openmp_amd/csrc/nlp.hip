@@ -305,7 +305,8 @@ struct nlp_graph {
   const void* es_desc_ptr = nullptr;  // and its address (a same-size reallocation restarts them too)
   unsigned occ_es8 = 256;    // resident workgroups of k_es_pass8
   unsigned occ_es8w = 256;   // and of its wide form (ES8_NTW threads)
-  int es8_nt = ES8_NT;       // the 8-byte passes' workgroup: ES8_NT or ES8_NTW threads (NLP_ES8_NT)
+  int es8_nt = ES8_NTW;      // the 8-byte passes' workgroup: ES8_NTW (8192-key tiles) or ES8_NT threads
+                             // (NLP_ES8_NT=256; C4 H=16 orders: 0.3-0.6 ms faster wide)
   int es_k8 = 1;             // the final order over rank-compressed 8-byte keys when it qualifies: 1 from
                              // ES8_MIN links on, 2 always (tests), 0 never (NLP_ES8)
   int es_runs = 1;           // the 8-byte order's two-level form (passes over (rank, u), runs put in w order):
@@ -1048,7 +1049,7 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   if (const char* hs = getenv("NLP_HASH_HUB_SORT")) g->hh_sort = hs[0] != '0';
   if (const char* hr = getenv("NLP_HASH_ROWB")) g->hp_rowb = atoi(hr);
   if (const char* e8 = getenv("NLP_ES8")) g->es_k8 = std::min(2, std::max(0, atoi(e8)));
-  if (const char* en = getenv("NLP_ES8_NT")) g->es8_nt = atoi(en) == ES8_NTW ? ES8_NTW : ES8_NT;
+  if (const char* en = getenv("NLP_ES8_NT")) g->es8_nt = atoi(en) == ES8_NT ? ES8_NT : ES8_NTW;
   if (const char* er = getenv("NLP_ES_RUNS")) g->es_runs = std::min(2, std::max(0, atoi(er)));
   if (const char* rs = getenv("NLP_ES_RS")) g->es_rs = (uint32_t)std::min<long>(ER_RSMAX, std::max(1l, atol(rs)));
   if (const char* lc = getenv("NLP_ES_LCAP")) g->es_lcap = (uint32_t)std::min<long>(EL_CAPMAX, std::max(2l, atol(lc)));
@@ -1154,6 +1155,7 @@ struct Cands {
   uint64_t kcnt = 0;  // the unpruned buffer's candidates >= kmin (the prune's select: above + ties)
   uint32_t kmin = 0;
   uint32_t route = 0;  // path 4: how the final order ran (nlp_timing.order_route)
+  int metric = -1;     // the call's (the final order's two-level form is chosen by it)
 };
 
 // Group the W wedges of one generator pass, score them and append the
@@ -1874,6 +1876,15 @@ nlp_status es_descs(nlp_graph* g, uint64_t ntiles, int P, uint64_t** desc, hipSt
   return NLP_OK;
 }
 
+// The metrics whose score moves with deg w for a fixed (u, common count):
+// Jaccard, Sorensen, Salton, Leicht-Holme-Newman.  Their runs of equal (rank,
+// u) are short (C4 JAC H=16: none beyond 64 keys), so the two-level form
+// pays; CN / AA / RA (the score of a u shared by every w with the same common
+// neighbours) and HPI / HDI (c / deg u for every w on one side of deg u) have
+// long runs (C4 H=16: CN 287,505 beyond 64 keys and 215 beyond 8192, AA
+// 114,093 and 66): the whole sort there (11 ms against 60 / 31 ms).
+bool es_runs_metric(int m) { return m == M_JAC || m == M_SOR || m == M_SAL || m == M_LHN; }
+
 // The two-level order's run pass (edgesort.hpp k_es_runs, k_es_long; the very
 // long runs by k_es_vgather, lsd8_keys and k_es_vscatter): `keys` (n K8 keys)
 // sorted by (rank, u), every run of equal (rank, u) put in w order and the
@@ -1946,7 +1957,7 @@ nlp_status es_runs_order(nlp_graph* g, const float* rscore, const uint64_t* keys
 // into the sort (the canonical tie rule is the sort order itself).
 nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
                     hipStream_t st, uint64_t* bytes, bool* done, const uint32_t* ckey = nullptr, uint32_t kmin = 0,
-                    uint64_t nout = UINT64_MAX, bool* runs = nullptr, uint64_t kcnt = 0) {
+                    uint64_t nout = UINT64_MAX, bool* runs = nullptr, uint64_t kcnt = 0, bool runs_ok = false) {
   *done = false;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
@@ -1993,7 +2004,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   // run pass stands in for the last pass (both read the keys and write the
   // edges), so it pays from two passes saved
   const int Pf = std::max(1, (rb + 2 * vb + 7) / 8), Ph = std::max(1, (rb + vb + 7) / 8);
-  const bool two = g->es_runs == 2 || (g->es_runs == 1 && Ph + 2 <= Pf);
+  const bool two = g->es_runs == 2 || (g->es_runs == 1 && runs_ok && Ph + 2 <= Pf);
   const int P = two ? Ph : Pf, sh0 = two ? vb : 0;
   // ranges of tpw tiles, one workgroup each
   const Es8Shape sh8 = es8_shape(g);
@@ -2086,11 +2097,13 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
 // try8 = false: the caller already knows the keys refuse the 8-byte order.
 // *route (may be null): NLP_ORDER_SORT8 or NLP_ORDER_SORT12, the sort that ran.
 nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
-                   hipStream_t st, uint64_t* bytes = nullptr, bool try8 = true, uint32_t* route = nullptr) {
+                   hipStream_t st, uint64_t* bytes = nullptr, bool try8 = true, uint32_t* route = nullptr,
+                   int metric = -1) {
   if (n == 0) return NLP_OK;
   if (try8 && ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2)) {
     bool done = false, runs = false;
-    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done, nullptr, 0, UINT64_MAX, &runs);
+    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done, nullptr, 0, UINT64_MAX, &runs, 0,
+                            es_runs_metric(metric));
     if (s != NLP_OK) return s;
     if (done) {
       if (route) *route = NLP_ORDER_SORT8 | (runs ? NLP_ORDER_RUNS : 0u);
@@ -2157,7 +2170,7 @@ nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st
     Workspace& ws = g->ws;
     nlp_status s = es_sort8(g, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], C.n,
                             d_out, st, &C.call_bytes, &done, (const uint32_t*)ws.p[B_CKEY], C.kmin, C.keep, &runs,
-                            C.kcnt);
+                            C.kcnt, es_runs_metric(C.metric));
     if (s != NLP_OK) return s;
     const uint64_t keep = C.keep;
     C.keep = 0;
@@ -2177,7 +2190,7 @@ nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st
     return s;
   }
   return es_sort(g, (const uint32_t*)g->ws.p[B_CU], (const uint32_t*)g->ws.p[B_CW], (const float*)g->ws.p[B_CS], C.n,
-                 d_out, st, &C.call_bytes, true, &C.route);
+                 d_out, st, &C.call_bytes, true, &C.route, C.metric);
 }
 
 // Estimated wedges (w > u) of a call: sum over surviving v of deg(v)^2 / 2,
@@ -4040,6 +4053,7 @@ nlp_status predict_once(nlp_graph* g, const Params& p, EdgeOut* d_out, uint64_t*
     if (s != NLP_OK || handled) return s;
   }
   Cands C;
+  C.metric = p.metric;
   uint32_t path = 0, chunks = 0;
   bool have_nan = false;
   TRY(hipEventRecord(g->ev[0], st));

@@ -685,7 +685,7 @@ def test_gpu_two_level_order(gpu, oracle):
     off, keys = random_csr(20000, 16, 41)
     ran = 0
     for env in (dict(), dict(NLP_ES_RS="1", NLP_ES_LCAP="2"), dict(NLP_ES_RS="3", NLP_ES_LCAP="16"),
-                dict(NLP_ES_LCAP="64", NLP_HASH_EMIT="300000")):
+                dict(NLP_ES_LCAP="64", NLP_HASH_EMIT="300000"), dict(NLP_ES8_NT="256")):
         with _env(NLP_HASH="1", NLP_ES_RUNS="2", **env):
             with gpu.Graph(off, keys) as G:
                 for m in (1, 0, 7, 2):
