@@ -43,22 +43,40 @@ def _worker(rank, world, port, cases, q, backend="gloo", graph="small"):
         from test_gpu_parity import random_csr
         nlp = nlp_loader.load()
         dmod = nlp_loader.load_sub("dist")
-        off, keys = random_csr(*GRAPHS[graph])
         res = []
-        with nlp.Graph(off, keys, device=0) as G:
+        if graph in GRAPHS:
+            off, keys = random_csr(*GRAPHS[graph])
+            G = nlp.Graph(off, keys, device=0)
             off_t = torch.from_numpy(off.astype(np.int64))
             keys_t = torch.from_numpy(keys.view(np.int32))
+        else:  # a bench config's stand-in, generated on the device (identical on every rank)
+            off_t, keys_t = _standin(graph)
+            G = nlp.Graph.from_device(off_t, keys_t)
+        span = off_t.numel() - 1
+        with G:
             for metric, hub, k in cases:
                 block = torch.empty((k + 1, 3), dtype=torch.int32, device="cuda")
                 out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
                 st = dmod.Exchange()
                 w = dmod.source_weights(off_t, keys_t, hub)
                 edges, n, info = dmod.predict_sharded(dmod.hip_local_predict(G, metric, hub, k, block),
-                                                      dmod.hip_merge(G, out), len(off) - 1, k, state=st, weights=w)
+                                                      dmod.hip_merge(G, out), span, k, state=st, weights=w)
                 res.append((edges[:n].cpu().numpy().copy(), info["shares"]))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
+
+
+def _standin(name):
+    """The CONFIGS entry's stand-in graph on cuda:0 (graphgen: Chung-Lu pairs,
+    the reference's ingest and deletion batch on the device)."""
+    import torch
+    import nlp_loader
+    gg = nlp_loader.load_sub("graphgen")
+    off, keys, _, _, _ = gg.make_workload(gg.CONFIGS[name], "cuda")
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return off, keys
 
 
 def _run_chain(nlp, world, cases, backend="gloo", graph="small"):
@@ -67,9 +85,16 @@ def _run_chain(nlp, world, cases, backend="gloo", graph="small"):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from test_gpu_parity import random_csr
-    off, keys = random_csr(*GRAPHS[graph])
+    if graph in GRAPHS:
+        off, keys = random_csr(*GRAPHS[graph])
+        G = nlp.Graph(off, keys)
+    else:
+        sys.path.insert(0, ROOT)
+        off_t, keys_t = _standin(graph)
+        G = nlp.Graph.from_device(off_t, keys_t)
+        del off_t, keys_t
     want = []
-    with nlp.Graph(off, keys) as G:
+    with G:
         for metric, hub, k in cases:
             out = torch.empty((k, 3), dtype=torch.int32, device="cuda")
             n, _ = G.predict_device(metric, hub, k, out)
@@ -80,7 +105,7 @@ def _run_chain(nlp, world, cases, backend="gloo", graph="small"):
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q, backend, graph)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=240) for _ in range(world)]
+    got = [q.get(timeout=400) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -108,3 +133,12 @@ def test_gpu_sharded_chain_nccl_world1(nlp):
     histogram all_gathers, the quota and the block exchange never leave the
     device except for the shares (one rank: RCCL refuses two ranks on one GPU)."""
     _run_chain(nlp, 1, [(1, 4, 2000), (1, 16, 400_000)], backend="nccl", graph="1M")
+
+
+@pytest.mark.timeout(500)
+def test_gpu_sharded_chain_c2_standin(nlp):
+    """The exchange at a bench config's size: the C2 (soc-LiveJournal1) stand-in,
+    4.8 M vertices, 1.4e8 entries, generated by every rank on the device; 2
+    ranks, Jaccard and Adamic-Adar at H = 16 with k beyond one rank's share,
+    every rank's merged list equal to the single-process call bit for bit."""
+    _run_chain(nlp, 2, [(1, 16, 3_000_000), (7, 16, 1_000_000), (0, 4, 200_000)], graph="C2-soc-LiveJournal1")
