@@ -448,24 +448,15 @@ __global__ __launch_bounds__(ES_NT) void k_es_hist8(const uint32_t* __restrict__
 // The kept candidates (key >= kmin) of an unpruned buffer as K8 keys,
 // compacted in any order (the sort orders them): one reservation per
 // workgroup and 4096 candidates.  The score -> rank map as in k_es_hist8.
-// cnt != nullptr: the first pass's range counts as well (k_es_cnt8's cnt and
-// ghist at bit shift0, ranges of tpw tiles of `tile` keys -- the kept count
-// known beforehand sizes them): a reservation spans two ranges at most,
-// counted in LDS and added once per reservation.
 __global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__ ckey, const uint32_t* __restrict__ cu,
                                                     const uint32_t* __restrict__ cw, uint64_t n, uint32_t kmin, int vb,
                                                     const float* __restrict__ rscore, uint32_t D,
-                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ count,
-                                                    uint32_t* __restrict__ cnt, uint32_t* __restrict__ ghist,
-                                                    uint32_t tpw, uint32_t G, int shift0, uint64_t tile) {
+                                                    uint64_t* __restrict__ keys, unsigned long long* __restrict__ count) {
   __shared__ uint32_t s_hk[1 << ES8_HLG];
   __shared__ uint16_t s_hr[1 << ES8_HLG];
   __shared__ uint32_t s_wn[ES_NT / 64];
-  __shared__ uint32_t s_h[2][256];  // the reservation's counts: its first range, the next
   __shared__ unsigned long long s_base;
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const uint64_t rsz = (uint64_t)tpw * tile;
-  for (int i = t; i < 512; i += ES_NT) (&s_h[0][0])[i] = 0;
   for (int i = t; i < (1 << ES8_HLG); i += ES_NT) s_hk[i] = 0;
   __syncthreads();
   for (uint32_t r = t; r < D; r += ES_NT) {
@@ -505,28 +496,11 @@ __global__ __launch_bounds__(ES_NT) void k_es_keep8(const uint32_t* __restrict__
         const uint64_t j = j0 + (uint64_t)q * ES_NT + t;
         uint32_t hh = es_dhash(x[q] + 1u, ES8_HLG);
         while (s_hk[hh] != x[q] + 1u) hh = (hh + 1) & ((1u << ES8_HLG) - 1);  // present: every kept key has a rank
-        const uint64_t at = pos + (uint64_t)__popcll(m & lt);
-        const uint64_t k = (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)cu[j] << vb | cw[j];
-        keys[at] = k;
-        if (cnt) atomicAdd(&s_h[at / rsz - s_base / rsz][(uint32_t)(k >> shift0) & 0xffu], 1u);
+        keys[pos + (uint64_t)__popcll(m & lt)] = (uint64_t)s_hr[hh] << (2 * vb) | (uint64_t)cu[j] << vb | cw[j];
       }
       pos += (uint64_t)__popcll(m);
     }
     __syncthreads();  // s_wn / s_base are rewritten by the next block
-    if (cnt) {
-      const uint64_t g0 = s_base / rsz;
-      for (int i = t; i < 512; i += ES_NT) {
-        const uint32_t c = (&s_h[0][0])[i];
-        if (c) {
-          const uint32_t d = (uint32_t)i & 0xffu;
-          const uint64_t g = g0 + (uint64_t)(i >> 8);
-          if (g < G) atomicAdd(&cnt[(uint64_t)d * G + g], c);
-          atomicAdd(&ghist[d], c);
-          (&s_h[0][0])[i] = 0;
-        }
-      }
-      __syncthreads();
-    }
   }
 }
 
@@ -732,17 +706,42 @@ __global__ __launch_bounds__(ES_NT) void k_es_runs(const float* __restrict__ rsc
                                                    uint64_t n, int vb, EdgeOut* __restrict__ eout, uint64_t nout,
                                                    uint32_t rs, uint64_t* __restrict__ lst, uint64_t lcap,
                                                    unsigned long long* __restrict__ lcnt) {
+  constexpr int NQ = (ER_TILE + ER_RSMAX + 1 + ES_NT - 1) / ES_NT;  // window keys per thread
   __shared__ uint64_t s_k[ER_TILE + ER_RSMAX + 1];
   const uint32_t t = threadIdx.x;
   const uint64_t vmask = (1ull << vb) - 1ull;
+  // the window of the tile at a: the key before it, the tile, rs keys beyond
+  auto window = [&](uint64_t a, uint64_t* wb, uint32_t* off, uint32_t* wn) {
+    *wb = a ? a - 1 : 0;
+    *off = a ? 1u : 0u;
+    *wn = (uint32_t)min(n - *wb, (uint64_t)(*off + ER_TILE + rs));
+  };
+  uint64_t pre[NQ];  // the next window's keys, in flight while a tile is worked
+  auto load = [&](uint64_t a) {
+    if (a >= n) return;
+    uint64_t wb;
+    uint32_t off, wn;
+    window(a, &wb, &off, &wn);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t i = (uint32_t)q * ES_NT + t;
+      pre[q] = i < wn ? keys[wb + i] : 0ull;
+    }
+  };
+  load((uint64_t)blockIdx.x * ER_TILE);
   for (uint64_t a = (uint64_t)blockIdx.x * ER_TILE; a < n; a += (uint64_t)gridDim.x * ER_TILE) {
-    const uint64_t wb = a ? a - 1 : 0;  // the window: the key before the tile, the tile, rs keys beyond
-    const uint32_t off = a ? 1u : 0u;
-    const uint32_t wn = (uint32_t)min(n - wb, (uint64_t)(off + ER_TILE + rs));
+    uint64_t wb;
+    uint32_t off, wn;
+    window(a, &wb, &off, &wn);
     const bool cut = wb + wn == n;      // the window reaches the last key
     __syncthreads();                    // the previous tile's reads are done
-    for (uint32_t i = t; i < wn; i += ES_NT) s_k[i] = keys[wb + i];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const uint32_t i = (uint32_t)q * ES_NT + t;
+      if (i < wn) s_k[i] = pre[q];
+    }
     __syncthreads();
+    load(a + (uint64_t)gridDim.x * ER_TILE);
     const uint32_t tn = (uint32_t)min(n - a, (uint64_t)ER_TILE);
     // every key of a run that starts in the tile, the window's keys beyond it included
 #pragma unroll 2

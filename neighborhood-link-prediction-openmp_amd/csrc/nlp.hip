@@ -166,6 +166,10 @@ struct nlp_graph {
   uint32_t* efilt = nullptr;  // edge filter of the first-order exclusion (k_sp_runs; only without etab)
   uint32_t efbits = 0;
   uint64_t* etab = nullptr;   // exact membership table of the entries w > u (hashpath.hpp k_etab_insert)
+  // the transposed sort's scratch, kept after the sort: the later build arrays (entry classes, degrees
+  // and ranks, the membership table) are carved from it (gmalloc) instead of freed and re-allocated
+  char* slab = nullptr;
+  uint64_t slab_bytes = 0, slab_used = 0;
   uint32_t etbits = 0;
   uint64_t* host_small = nullptr;  // pinned counters
   uint64_t* host_ctr = nullptr;    // host-mapped counters written by the last kernel (sort path)
@@ -407,6 +411,28 @@ hipError_t read_small(nlp_graph* g, const uint64_t* d, int n, hipStream_t st) {
   return hipStreamSynchronize(st);
 }
 
+// A per-graph build array carved from the slab (the transposed sort's kept
+// scratch) when it fits, else its own allocation.  The driver wipes freed HBM
+// asynchronously and an allocation that needs those pages waits for the wipe:
+// the round-6 bench box where a box before us had freed its memory waited
+// 3.4 s in the membership table's hipMalloc after the sort's scratch was
+// freed (0.6 s builds elsewhere).  Carving takes no free and no allocation.
+template <typename T>
+hipError_t gmalloc(nlp_graph* g, T** p, size_t bytes) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  if (g->slab && g->slab_used + bytes <= g->slab_bytes) {
+    *p = (T*)(g->slab + g->slab_used);
+    g->slab_used += bytes;
+    return hipSuccess;
+  }
+  return hmalloc(p, bytes);
+}
+void gfree(nlp_graph* g, void* p) {
+  if (!p) return;
+  if (g->slab && (char*)p >= g->slab && (char*)p < g->slab + g->slab_bytes) return;  // the slab's: freed with it
+  (void)hipFree(p);
+}
+
 void destroy_graph(nlp_graph* g) {
   if (!g) return;
   if (g->is_group) {
@@ -431,9 +457,9 @@ void destroy_graph(nlp_graph* g) {
   if (g->d_stamp) (void)hipFree(g->d_stamp);
   if (g->hp_scratch) (void)hipFree(g->hp_scratch);
   if (g->tile_row) (void)hipFree(g->tile_row);
-  if (g->dcls) (void)hipFree(g->dcls);
-  if (g->kdeg) (void)hipFree(g->kdeg);
-  if (g->drank) (void)hipFree(g->drank);
+  gfree(g, g->dcls);
+  gfree(g, g->kdeg);
+  gfree(g, g->drank);
   if (g->xs) (void)hipFree(g->xs);
   for (void* p : {(void*)g->sl_off, (void*)g->sl_keys, (void*)g->sl_sdo, (void*)g->sl_cls, (void*)g->sl_pn})
     if (p) (void)hipFree(p);
@@ -452,7 +478,8 @@ void destroy_graph(nlp_graph* g) {
   if (g->ctab_aa) (void)hipFree(g->ctab_aa);
   if (g->ctab_ra) (void)hipFree(g->ctab_ra);
   if (g->efilt) (void)hipFree(g->efilt);
-  if (g->etab) (void)hipFree(g->etab);
+  gfree(g, g->etab);
+  if (g->slab) (void)hipFree(g->slab);
   if (g->rx_vbydeg) (void)hipFree(g->rx_vbydeg);
   if (g->rx_cnt) (void)hipFree(g->rx_cnt);
   for (int i = 0; i < 8; ++i)
@@ -547,6 +574,7 @@ nlp_status build_short_lists(nlp_graph* g, uint32_t cap) {
   const unsigned gt = (unsigned)std::min<uint64_t>((nt + NWAVE - 1) / NWAVE, 16384);
   size_t fr = 0, tot = 0;
   TRY(hipMemGetInfo(&fr, &tot));
+  fr += g->slab ? g->slab_bytes - g->slab_used : 0;  // the slab's rest: free HBM before the slab was kept
   // the classes kept: up to HP_DCLS_MAX, fewer (128, 64, 32, 16) while the lists and their build would take more
   // than a quarter of the free HBM (peak 29 B per short entry + 20 B per row; kept 17 B + 8 B)
   uint64_t L = 0;
@@ -743,8 +771,11 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   if (M) {
     uint64_t *k0, *k1, *scan, *hoff;
     uint32_t* hist;
-    TRY(wsget(g->ws, B_WKEY0, M, &k0));
-    TRY(wsget(g->ws, B_WKEY1, M, &k1));
+    TRY(hmalloc(&g->slab, 2 * M * 8));  // the sort's two key buffers, kept for the later arrays
+    g->slab_bytes = 2 * M * 8;
+    g->slab_used = 0;
+    k0 = (uint64_t*)g->slab;
+    k1 = k0 + M;
     uint64_t* toff;
     uint32_t* tkeys;
     TRY(hmalloc(&toff, (S + 1) * 8));
@@ -791,8 +822,8 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
       TRY(hipFree(tkeys));
     }
   }
-  // the sort's scratch (2 x 8 B per entry) goes back now: the build's later
-  // arrays (the membership table above all) reuse its pages
+  // the sort's other scratch goes back; its key buffers (2 x 8 B per entry)
+  // stay as the slab the later arrays are carved from (gmalloc)
   g->ws.release();
   TRY(clk.mark("transpose"));
   // Degree-class index: survivors of any H <= DCAP without a pass over deg[].
@@ -860,14 +891,14 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
   // k_hp_entry_classes
   const char* hdc = getenv("NLP_HASH_DCLS");
   if (M > 0 && !(hdc && hdc[0] == '0') && g->maxdeg < (1u << 24)) {
-    if (hmalloc(&g->dcls, M) == hipSuccess) {
+    if (gmalloc(g, &g->dcls, M) == hipSuccess) {
       const char* hkd = getenv("NLP_HASH_KDEG");
-      if (!(hkd && hkd[0] == '0') && hmalloc(&g->kdeg, M * 4) != hipSuccess) {
+      if (!(hkd && hkd[0] == '0') && gmalloc(g, &g->kdeg, M * 4) != hipSuccess) {
         (void)hipGetLastError();
         g->kdeg = nullptr;
       }
       const char* hdr = getenv("NLP_HASH_DRANK");
-      if (!(hdr && hdr[0] == '0') && hmalloc(&g->drank, M) != hipSuccess) {
+      if (!(hdr && hdr[0] == '0') && gmalloc(g, &g->drank, M) != hipSuccess) {
         (void)hipGetLastError();
         g->drank = nullptr;
       }
@@ -915,8 +946,9 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
       const uint64_t bytes = (1ull << bits) * ET_SLOTS * 8;
       size_t fr = 0, tot = 0;
       TRY(hipMemGetInfo(&fr, &tot));
-      if (upper > 0 && bytes < fr / 4) {
-        TRY(hmalloc(&g->etab, bytes));
+      const bool in_slab = g->slab && g->slab_used + bytes <= g->slab_bytes;
+      if (upper > 0 && (in_slab || bytes < fr / 4)) {
+        TRY(gmalloc(g, &g->etab, bytes));
         TRY(hipMemsetAsync(g->etab, 0xff, bytes, st));
         const unsigned gi = (unsigned)std::min<uint64_t>((M / HP_WTILE + NWAVE) / NWAVE + 1, 65536);
         hipLaunchKernelGGL(k_etab_insert, dim3(gi), dim3(NT), 0, st, (const uint64_t*)g->off,
@@ -925,6 +957,11 @@ nlp_status finish_graph(nlp_graph* g, BuildClock& clk) {
         g->etbits = bits;
       }
     }
+  }
+  if (g->slab && g->slab_used == 0) {  // nothing carved (no entry classes, no table): the slab goes back
+    TRY(hipFree(g->slab));
+    g->slab = nullptr;
+    g->slab_bytes = 0;
   }
   TRY(clk.mark("membership_table"));
   // Edge filter for the first-order exclusion of the scoring kernel when there
@@ -1152,7 +1189,6 @@ struct Cands {
   // path 4, final prune folded into the order: the n held are unpruned, the
   // order keeps the keys >= kmin and writes the first `keep` (0: pruned)
   uint64_t keep = 0, cap = 0;
-  uint64_t kcnt = 0;  // the unpruned buffer's candidates >= kmin (the prune's select: above + ties)
   uint32_t kmin = 0;
   uint32_t route = 0;  // path 4: how the final order ran (nlp_timing.order_route)
   int metric = -1;     // the call's (the final order's two-level form is chosen by it)
@@ -1777,7 +1813,6 @@ nlp_status hp_prune(nlp_graph* g, Cands& C, uint64_t k, uint64_t cap, uint32_t* 
       *kth = (uint32_t)key;
       C.keep = k;
       C.kmin = (uint32_t)key;
-      C.kcnt = above + ties;
       C.cap = cap;
       C.call_bytes += 12 * n;  // three select histograms
       return NLP_OK;
@@ -1957,7 +1992,7 @@ nlp_status es_runs_order(nlp_graph* g, const float* rscore, const uint64_t* keys
 // into the sort (the canonical tie rule is the sort order itself).
 nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const float* cs, uint64_t n, EdgeOut* out,
                     hipStream_t st, uint64_t* bytes, bool* done, const uint32_t* ckey = nullptr, uint32_t kmin = 0,
-                    uint64_t nout = UINT64_MAX, bool* runs = nullptr, uint64_t kcnt = 0, bool runs_ok = false) {
+                    uint64_t nout = UINT64_MAX, bool* runs = nullptr, bool runs_ok = false) {
   *done = false;
   Workspace& ws = g->ws;
   const int vb = std::max(1, bits_for(g->span - 1));
@@ -1996,9 +2031,25 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   }
   TRY(hipMemcpyAsync(rscore, hsc.data(), D * 4, hipMemcpyHostToDevice, st));
   uint64_t *k0 = nullptr, *k1 = nullptr;
-  // the sort's key count: the kept candidates' when the buffer is unpruned
-  // (known beforehand from the prune's select when kcnt is given)
-  const uint64_t ns = ckey ? (kcnt ? kcnt : 0) : n;
+  if (ckey) {  // the kept candidates' keys, compacted: the sort's n is their count
+    TRY(wsget(ws, B_ES_K0, n, &k0));
+    unsigned long long* kc = (unsigned long long*)(dcnt + 2);  // zeroed with the set
+    hipLaunchKernelGGL(k_es_keep8, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)),
+                       dim3(ES_NT), 0, st, ckey, cu, cw, n, kmin, vb, (const float*)rscore, D, k0, kc);
+    TRY(hipGetLastError());
+    unsigned long long kept = 0;
+    TRY(hipMemcpyAsync(&kept, kc, 8, hipMemcpyDeviceToHost, st));
+    TRY(hipStreamSynchronize(st));
+    if (kept < std::min<uint64_t>(nout, n) || kept > n) return NLP_ERR_DEVICE;
+    n = kept;
+  }
+  // the keys (and the first pass's range counts) in one read; ranges of tpw
+  // tiles, one workgroup each
+  const Es8Shape sh8 = es8_shape(g);
+  const uint64_t ntiles = (n + sh8.tile - 1) / sh8.tile;
+  uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)sh8.occ, (uint64_t)ES8_GMAX}));
+  const uint32_t tpw = (uint32_t)((ntiles + G - 1) / G);
+  G = (uint32_t)((ntiles + tpw - 1) / tpw);  // every range non-empty
   // the two-level form (edgesort.hpp k_es_runs): passes over the (rank, u)
   // bits only, then the runs of equal (rank, u) put in w order in place -- the
   // run pass stands in for the last pass (both read the keys and write the
@@ -2006,57 +2057,24 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   const int Pf = std::max(1, (rb + 2 * vb + 7) / 8), Ph = std::max(1, (rb + vb + 7) / 8);
   const bool two = g->es_runs == 2 || (g->es_runs == 1 && runs_ok && Ph + 2 <= Pf);
   const int P = two ? Ph : Pf, sh0 = two ? vb : 0;
-  // ranges of tpw tiles, one workgroup each
-  const Es8Shape sh8 = es8_shape(g);
-  uint32_t G = 1, tpw = 1;
-  auto ranges = [&](uint64_t nn) {
-    const uint64_t ntiles = (nn + sh8.tile - 1) / sh8.tile;
-    G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({ntiles, (uint64_t)sh8.occ, (uint64_t)ES8_GMAX}));
-    tpw = (uint32_t)std::max<uint64_t>(1, (ntiles + G - 1) / G);
-    G = (uint32_t)std::max<uint64_t>(1, (ntiles + tpw - 1) / tpw);  // every range non-empty
-  };
-  uint32_t* hw;  // [P][256] digit totals
-  TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
-  TRY(hipMemsetAsync(hw, 0, (uint64_t)P * 256 * 4, st));
-  uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
-  bool counted = false;  // the first pass's counts made with the keys
-  if (ckey) {  // the kept candidates' keys, compacted: the sort's n is their count
-    TRY(wsget(ws, B_ES_K0, n, &k0));
-    unsigned long long* kc = (unsigned long long*)(dcnt + 2);  // zeroed with the set
-    if (ns) {
-      ranges(ns);
-      TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
-      TRY(hipMemsetAsync(cnt, 0, (uint64_t)256 * G * 4, st));
-      counted = true;
-    }
-    hipLaunchKernelGGL(k_es_keep8, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)),
-                       dim3(ES_NT), 0, st, ckey, cu, cw, n, kmin, vb, (const float*)rscore, D, k0, kc,
-                       counted ? cnt : (uint32_t*)nullptr, hw, tpw, G, sh0, sh8.tile);
-    TRY(hipGetLastError());
-    unsigned long long kept = 0;
-    TRY(hipMemcpyAsync(&kept, kc, 8, hipMemcpyDeviceToHost, st));
-    TRY(hipStreamSynchronize(st));
-    if (kept < std::min<uint64_t>(nout, n) || kept > n || (ns && kept != ns)) return NLP_ERR_DEVICE;
-    n = kept;
-  }
-  if (!counted) {
-    ranges(n);
-    TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
-  }
-  uint32_t* offs = cnt + (uint64_t)256 * G;
   {
     static const bool trace = getenv("NLP_TRACE_RUNS") && getenv("NLP_TRACE_RUNS")[0] == '1';
     if (trace)
       fprintf(stderr, "nlp order: %llu keys, %u scores (%d rank bits), %d id bits, %d passes (%d without runs), "
-              "%d-thread passes, first counts %s\n", (unsigned long long)n, D, rb, vb, P, Pf, sh8.nt,
-              counted ? "with the kept keys" : "by a read");
+              "%d-thread passes\n", (unsigned long long)n, D, rb, vb, P, Pf, sh8.nt);
   }
+  uint32_t* hw;  // [P][256] digit totals
+  TRY(wsget(ws, B_ES_HIST, (uint64_t)ES_MAXP * 256 + ES_MAXP + 4, &hw));
+  TRY(hipMemsetAsync(hw, 0, (uint64_t)P * 256 * 4, st));
+  uint32_t* cnt;  // [256][G] range counts, then [256][G] offsets
+  TRY(wsget(ws, B_ES_CNT, (uint64_t)2 * 256 * G, &cnt));
+  uint32_t* offs = cnt + (uint64_t)256 * G;
   if (!ckey) TRY(wsget(ws, B_ES_K0, n, &k0));
   if (two || P > 1) TRY(wsget(ws, B_ES_K1, n, &k1));
-  if (ckey && !counted) {
+  if (ckey) {
     hipLaunchKernelGGL(k_es_cnt8, dim3(G), dim3(ES_NT), 0, st, (const uint64_t*)k0, n, sh0, cnt, hw, tpw, G,
                        sh8.tile);
-  } else if (!ckey) {
+  } else {
     hipLaunchKernelGGL(k_es_hist8, dim3(G), dim3(ES_NT), 0, st, cu, cw, cs, n, vb, (const float*)rscore, D, hw, k0,
                        cnt, tpw, G, sh0, sh8.tile);
   }
@@ -2068,8 +2086,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   // of keys, the run pass 8 in, 12 out
   const uint64_t nw = std::min<uint64_t>(nout, n);
   if (bytes)
-    *bytes += (ckey ? 8 * n_in + (counted ? 16 : 24) * n : 24 * n) + 24 * n * (uint64_t)(two ? P : P - 1) + 8 * n +
-              12 * nw;
+    *bytes += (ckey ? 8 * n_in + 24 * n : 24 * n) + 24 * n * (uint64_t)(two ? P : P - 1) + 8 * n + 12 * nw;
   const uint64_t* src = k0;  // k_es_hist8 wrote every key
   for (int r = 0; r < P; ++r) {
     uint64_t* dst = (r & 1) ? k0 : k1;
@@ -2102,7 +2119,7 @@ nlp_status es_sort(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const f
   if (n == 0) return NLP_OK;
   if (try8 && ((n >= ES8_MIN && g->es_k8 == 1) || g->es_k8 == 2)) {
     bool done = false, runs = false;
-    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done, nullptr, 0, UINT64_MAX, &runs, 0,
+    nlp_status s = es_sort8(g, cu, cw, cs, n, out, st, bytes, &done, nullptr, 0, UINT64_MAX, &runs,
                             es_runs_metric(metric));
     if (s != NLP_OK) return s;
     if (done) {
@@ -2170,7 +2187,7 @@ nlp_status hp_final_order(nlp_graph* g, Cands& C, EdgeOut* d_out, hipStream_t st
     Workspace& ws = g->ws;
     nlp_status s = es_sort8(g, (const uint32_t*)ws.p[B_CU], (const uint32_t*)ws.p[B_CW], (const float*)ws.p[B_CS], C.n,
                             d_out, st, &C.call_bytes, &done, (const uint32_t*)ws.p[B_CKEY], C.kmin, C.keep, &runs,
-                            C.kcnt, es_runs_metric(C.metric));
+                            es_runs_metric(C.metric));
     if (s != NLP_OK) return s;
     const uint64_t keep = C.keep;
     C.keep = 0;
