@@ -312,24 +312,34 @@ __global__ __launch_bounds__(ES_NT) void k_es_dkeys(const float* __restrict__ cs
   if (threadIdx.x == 0) { s_n = 0; s_over = 0; }
   __syncthreads();
   constexpr int LLG = 12;  // log2 ES_LCAP
-  const uint64_t stride = (uint64_t)gridDim.x * ES_NT;
-  for (uint64_t j = (uint64_t)blockIdx.x * ES_NT + threadIdx.x; j < n; j += stride) {
-    const uint32_t key = ckey ? ckey[j] : score_key(cs[j]);
-    if (ckey && key < kmin) continue;
-    const uint32_t x = key + 1u;
-    uint32_t h = es_dhash(x, LLG);
-    for (uint32_t probe = 0; probe < ES_LCAP; ++probe) {
-      const uint32_t cur = s_set[h];  // a plain read: the common case, the key is already in
-      if (cur == x) break;
-      if (cur == 0) {
-        const uint32_t old = atomicCAS(&s_set[h], 0u, x);
-        if (old == 0) {
-          if (atomicAdd(&s_n, 1u) >= ES_LCAP / 2) s_over = 1;
-          break;
+  constexpr int UN = 8;    // keys per thread loaded together (one round trip, then the LDS probes)
+  const uint64_t stride = (uint64_t)gridDim.x * ES_NT * UN;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * ES_NT * UN; j0 < n; j0 += stride) {
+    uint32_t kq[UN];
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
+      kq[q] = j < n ? (ckey ? ckey[j] : score_key(cs[j])) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < UN; ++q) {
+      const uint64_t j = j0 + (uint64_t)q * ES_NT + threadIdx.x;
+      if (j >= n || (ckey && kq[q] < kmin)) continue;
+      const uint32_t x = kq[q] + 1u;
+      uint32_t h = es_dhash(x, LLG);
+      for (uint32_t probe = 0; probe < ES_LCAP; ++probe) {
+        const uint32_t cur = s_set[h];  // a plain read: the common case, the key is already in
+        if (cur == x) break;
+        if (cur == 0) {
+          const uint32_t old = atomicCAS(&s_set[h], 0u, x);
+          if (old == 0) {
+            if (atomicAdd(&s_n, 1u) >= ES_LCAP / 2) s_over = 1;
+            break;
+          }
+          if (old == x) break;
         }
-        if (old == x) break;
+        h = (h + 1) & (ES_LCAP - 1);
       }
-      h = (h + 1) & (ES_LCAP - 1);
     }
     if (s_over) break;  // (racy read is fine: the flag only ever goes up)
   }

@@ -2004,7 +2004,7 @@ nlp_status es_sort8(nlp_graph* g, const uint32_t* cu, const uint32_t* cw, const 
   uint32_t* dcnt = dset + ES_DCAP;
   float* rscore = (float*)(dcnt + 4);
   TRY(hipMemsetAsync(dset, 0, (ES_DCAP + 4) * 4, st));
-  hipLaunchKernelGGL(k_es_dkeys, dim3((unsigned)std::min<uint64_t>((n + ES_NT - 1) / ES_NT, 2048)), dim3(ES_NT), 0, st,
+  hipLaunchKernelGGL(k_es_dkeys, dim3((unsigned)std::min<uint64_t>((n + ES_NT * 8 - 1) / (ES_NT * 8), 2048)), dim3(ES_NT), 0, st,
                      cs, n, dset, dcnt, ckey, kmin);
   TRY(hipGetLastError());
   std::vector<uint32_t> hs(ES_DCAP + 4);
